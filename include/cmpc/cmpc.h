@@ -1,0 +1,173 @@
+/*
+ * cmpc.h — C ABI of the MI355X-native batched centroidal-MPC QP engine.
+ *
+ * This is the drop-in boundary. It replaces, for the CentroidalMPC hot path:
+ *   - CentroidalMPC::UpdateMPC            (reference CentroidalMPC.cpp:278-370 / CentroidalMPC.h:32)
+ *       → cmpc_solve_batch (B = 1 is one UpdateMPC call)
+ *   - HpipmInterface::Impl::solve          (reference ocs2_sqp/hpipm_catkin/src/HpipmInterface.cpp:166-301)
+ *       → cmpc_ocp_solve_batch (condensed OCP-QP, x0 eliminated as :177-208)
+ *   - hpipm_interface::Settings            (reference hpipm_catkin/include/hpipm_catkin/HpipmInterfaceSettings.h:44-57)
+ *       → cmpc_settings
+ *   - d_ocp_qp_ipm_get_status codes        (reference HpipmInterface.h:79-85, HpipmInterface.cpp:462-473)
+ *       → enum cmpc_qp_status
+ *
+ * Conventions (mirroring HPIPM's C API, HpipmInterface.cpp:104-128, :282-284):
+ *   - plain pointers + sizes, no C++ types, no exceptions across the ABI;
+ *   - API functions return an int error code (CMPC_OK = 0, negative on error); per-QP solver outcome is an
+ *     int status array with HPIPM's codes;
+ *   - batch entry points take DEVICE pointers and an opaque hipStream_t (void*), and are asynchronous on it;
+ *     the *_host variants take host pointers and synchronise;
+ *   - batch input layouts are QP-major (one contiguous record per QP): one wavefront/workgroup serves one QP and
+ *     reads its record coalesced.
+ *
+ * Per-QP record layouts (N = horizon, L = n_legs = 4):
+ *   x0      [13]              = [c(3), v(3), L(3), Theta(3), g_z]        (c,v,L as CentroidalMPC.cpp:284-286)
+ *   xref    [(N+1)][13]       node k = 0..N                              (des_state, CentroidalMPC.cpp:297-299, extended)
+ *   foot    [(N+1)][L][3]     desired foot position p^des_{i,k}          (des_inputs, CentroidalMPC.cpp:316-317)
+ *   contact [N][L]  (uint8)   e_{i,k} in {0,1}                           (mpc_table, CentroidalMPC.cpp:315-335)
+ *   u       [N][L][3]         world-frame contact forces (0 for swing legs)
+ *   x       [(N+1)][13]       optional state rollout of the solution
+ */
+#ifndef CMPC_CMPC_H_
+#define CMPC_CMPC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMPC_NX 13
+#define CMPC_MAX_LEGS 4
+#define CMPC_NU (3 * CMPC_MAX_LEGS)
+#define CMPC_NUM_WEIGHTS ((CMPC_MAX_LEGS + 1) * 9) /* 45, CentoidMPCTest.cpp:18 */
+
+/* API return codes */
+enum cmpc_error {
+  CMPC_OK = 0,
+  CMPC_ERR_ARG = -1,      /* bad argument (null pointer, size out of range) */
+  CMPC_ERR_HIP = -2,      /* HIP runtime error */
+  CMPC_ERR_SIZE = -3,     /* batch larger than the context's max_batch, or horizon mismatch */
+  CMPC_ERR_NO_DEVICE = -4 /* no usable gfx950 device */
+};
+
+/* Per-QP solver status. 0..4 keep HPIPM's hpipm_status order (HpipmInterface.h:79-85). */
+enum cmpc_qp_status {
+  CMPC_SUCCESS = 0,          /* QP solved */
+  CMPC_MAX_ITER = 1,         /* maximum number of iterations reached */
+  CMPC_MIN_STEP = 2,         /* minimum step length reached */
+  CMPC_NAN_SOL = 3,          /* NaN in computations / non-finite solution (HpipmInterface.cpp:290-295) */
+  CMPC_INCONS_EQ = 4,        /* inconsistent equality constraints (kept for ABI parity; never produced) */
+  CMPC_INVALID_CONTACT = 5,  /* a horizon step has no stance leg: reference throws "mpc table invalid"
+                                (CentroidalMPC.cpp:328-330) */
+  CMPC_TOO_LARGE = 6         /* condensed size exceeds what this build's kernels support */
+};
+
+enum cmpc_precision { CMPC_F64 = 0, CMPC_F32 = 1 };
+
+/* Interior-point settings. Field-for-field mirror of hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57),
+ * defaults identical (cmpc_settings_default). hpipm_mode / warm_start / ric_alg are accepted for ABI parity. */
+typedef struct cmpc_settings {
+  int hpipm_mode;   /* 0 = SPEED (default) */
+  int iter_max;     /* 30 */
+  double alpha_min; /* 1e-12 */
+  double mu0;       /* 10 */
+  double tol_stat;  /* 1e-6 */
+  double tol_eq;    /* 1e-8 */
+  double tol_ineq;  /* 1e-8 */
+  double tol_comp;  /* 1e-8 */
+  double reg_prim;  /* 1e-12 */
+  int warm_start;   /* 0 */
+  int pred_corr;    /* 1 */
+  int ric_alg;      /* 0 */
+} cmpc_settings;
+
+/* Centroidal model (CentroidalMPC ctor args, CentroidalMPC.h:26-27, plus SRBD extensions of SURVEY App. A). */
+typedef struct cmpc_model {
+  int N;                              /* predict_horizon */
+  int n_legs;                         /* num_legs (must be 4 in this build) */
+  double mass;                        /* kg */
+  double dt;                          /* time_step */
+  double inertia[9];                  /* body inertia I_b, row-major (build extension, A.2) */
+  double mu[CMPC_MAX_LEGS];           /* friction coefficient per leg */
+  double weights[CMPC_NUM_WEIGHTS];   /* CentroidalMPC weight vector, same indexing as CentroidalMPC.cpp:203-231 */
+  double force_ub[5];                 /* pyramid row upper bounds; default {5000,5000,5000,5000, m*9.81*n_legs}
+                                         (CentroidalMPC.cpp:182-183) */
+  double theta_weights[3];            /* Q weight on roll/pitch/yaw (build extension, default 0) */
+} cmpc_model;
+
+void cmpc_settings_default(cmpc_settings* s);
+/* CentoidMPCTest.cpp:12-33 parameters (m = 8, dt = 0.01, mu = 0.8, the 45 weights) at horizon N. */
+void cmpc_model_default(cmpc_model* m, int N);
+
+typedef struct cmpc_ctx cmpc_ctx;
+
+/* Device workspace bytes a context needs for max_batch QPs (HPIPM-style *_memsize). */
+size_t cmpc_memsize(const cmpc_model* model, int precision, int max_batch);
+/* Create a context on the current HIP device. dev_mem: caller-owned device buffer of cmpc_memsize bytes, or NULL
+ * to let the context allocate (and free) it. */
+int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int precision, int max_batch, void* dev_mem,
+                cmpc_ctx** out);
+int cmpc_destroy(cmpc_ctx* ctx);
+int cmpc_set_settings(cmpc_ctx* ctx, const cmpc_settings* settings);
+int cmpc_set_model(cmpc_ctx* ctx, const cmpc_model* model); /* horizon N must not change */
+int cmpc_get_model(const cmpc_ctx* ctx, cmpc_model* out);
+/* Leading dimension (padded max condensed size) of the context's H workspace. */
+int cmpc_ctx_ld(const cmpc_ctx* ctx);
+
+/* Full hot path: SRBD linearisation -> condensing (H, g) -> friction/force-bound stacking -> batched IPM ->
+ * scatter to [N][L][3] (zeros for swing legs) and optional rollout. Device pointers, async on stream.
+ * d_x may be NULL. d_iters may be NULL. */
+int cmpc_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                     const uint8_t* d_contact, double* d_u, double* d_x, int* d_status, int* d_iters, void* stream);
+/* Same, host pointers; synchronous. */
+int cmpc_solve_batch_host(cmpc_ctx* ctx, int B, const double* x0, const double* xref, const double* foot,
+                          const uint8_t* contact, double* u, double* x, int* status, int* iters);
+
+/* Stage 1 alone (test/inspection hook): condensed QP in the context precision, widened to double.
+ *   d_H [B][ld][ld] (padded rows/cols carry an identity), d_g [B][ld], d_n [B] (condensed size, 0 if invalid),
+ *   d_status [B] (CMPC_SUCCESS, or CMPC_INVALID_CONTACT / CMPC_TOO_LARGE). */
+int cmpc_condense_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                        const uint8_t* d_contact, double* d_H, double* d_g, int* d_n, int* d_status, void* stream);
+
+/* Generic batched dense friction-pyramid QP (stage 2 alone):
+ *   min 1/2 u'Hu + g'u  s.t.  lo_j <= F(mu_a) u_{3a..3a+2} <= hi_j   (F as CentroidalMPC.cpp:186-190)
+ * per QP q: n[q] (multiple of 3, <= ld), H [ld][ld] row-major (symmetric), g [ld], tri_mu [ld/3],
+ * tri_lo/tri_hi [ld/3][5]. Outputs u [ld] (entries >= n are 0), status, iters. Inputs are double; solved in the
+ * context precision. ld must equal cmpc_ctx_ld(ctx). */
+int cmpc_qp_solve_batch(cmpc_ctx* ctx, int B, const double* d_H, const double* d_g, const int* d_n,
+                        const double* d_tri_mu, const double* d_tri_lo, const double* d_tri_hi, double* d_u,
+                        int* d_status, int* d_iters, void* stream);
+
+/* Counter-based synthetic input generator (Philox4x32-10 keyed by seed, counter = global QP id), identical
+ * bit-for-bit to oracle_generate(). gait: 0 = trot (configs 2-4), 1 = mixed trot/bound/pronk (config 5).
+ * QP ids run qp_offset .. qp_offset+B-1, so sharding across GPUs leaves every QP's inputs unchanged. */
+int cmpc_generate_batch(const cmpc_model* model, uint64_t seed, int64_t qp_offset, int B, int gait, double* d_x0,
+                        double* d_xref, double* d_foot, uint8_t* d_contact, void* stream);
+
+/* Generic OCP-QP (HpipmInterface::solve semantics, HpipmInterface.cpp:166-301), batched, no inequality rows:
+ *   min sum_k [1/2 x'Q_k x + u'S_k x + 1/2 u'R_k u + q_k'x + r_k'u] + 1/2 x_N'Q_N x_N + q_N'x_N
+ *   s.t. x_{k+1} = A_k x_k + B_k u_k + b_k,  x_0 given.
+ * Constant nx, per-stage nu_k (nu_N = 0). Matrices COLUMN-major (Eigen default, so ocs2 .data() passes through).
+ * Per-QP packed record (offsets computed by cmpc_ocp_record_size):
+ *   A_k (nx*nx), B_k (nx*nu_k), b_k (nx)                       k = 0..N-1
+ *   Q_k (nx*nx), S_k (nu_k*nx), R_k (nu_k*nu_k), q_k (nx), r_k (nu_k)   k = 0..N (S,R,r empty at N)
+ * Outputs x [(N+1)][nx] (x[0] = x0) and u [sum nu_k]. Solved by condensing + dense Cholesky on the device. */
+size_t cmpc_ocp_record_size(int N, int nx, const int* nu);
+int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
+                              double* u, int* status);
+
+/* Human-readable names. */
+const char* cmpc_status_string(int status);
+const char* cmpc_error_string(int err);
+/* Device properties used by the bench roofline (peak fp64 FLOP/s from the datasheet unless measured). */
+int cmpc_device_info(int* num_cu, int* clock_khz, char* arch_name, int arch_len);
+/* Version string of the build. */
+const char* cmpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CMPC_CMPC_H_ */

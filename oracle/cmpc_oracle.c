@@ -1,0 +1,1002 @@
+/*
+ * cmpc_oracle.c — CPU fp64 restatement of the reference hot path. TEST INFRASTRUCTURE ONLY (see cmpc_oracle.h).
+ *
+ * What each function follows in the reference (paths relative to /root/reference):
+ *   oracle_consts_init   weights indexing CentroidalMPC.cpp:203-231 (force weights w[9+3L+3i+c], rate w[9+6L+3i+c]),
+ *                        CoM-z weight (w2/2)e^{-k}+w2/2 squared by sumsqr (:203-206, :210), force_ub :182-183.
+ *   oracle_srbd_dynamics forward-Euler centroidal map CentroidalMPC.cpp:85-92 (gravity :70-73), bilinear lever arm
+ *                        linearised at r = p^des - c^ref; Theta/g_z rows are the 13-state extension.
+ *   oracle_condense*     multiple shooting of CentroidalMPC.cpp:159-176 eliminated into Aqp/Bqp (App. A.3);
+ *                        f^des_z = m*9.81/n_stance with the "mpc table invalid" check CentroidalMPC.cpp:326-335;
+ *                        friction pyramid rows CentroidalMPC.cpp:179-201 (swing legs eliminated, App. A.4).
+ *   oracle_qp_ipm        primal-dual Mehrotra predictor-corrector with HPIPM's stopping rule and settings
+ *                        (HpipmInterfaceSettings.h:44-57; d_ocp_qp_ipm_solve is [external] HPIPM@255ffdf).
+ *   oracle_ocp_*         HpipmInterface::Impl::solve x0 elimination HpipmInterface.cpp:177-208; Riccati recursion of
+ *                        testHpipmInterface.cpp:280-304.
+ */
+#include "cmpc_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NX CMPC_NX
+#define NU CMPC_NU
+#define GRAV 9.81
+#define GAIT_HALF_PERIOD 5
+#define THR0 1.0
+#define TAU 0.995
+
+static inline double dmin(double a, double b) { return a < b ? a : b; }
+static inline double dmax(double a, double b) { return a > b ? a : b; }
+
+/* ------------------------------------------------------------------------------------------------ model */
+
+void oracle_consts_init(const cmpc_model* m, oracle_consts* c) {
+  memset(c, 0, sizeof(*c));
+  const int L = m->n_legs;
+  const double* w = m->weights;
+  c->N = m->N;
+  c->L = L;
+  c->mass = m->mass;
+  c->dt = m->dt;
+  for (int i = 0; i < L; ++i) {
+    c->mu[i] = m->mu[i];
+    for (int d = 0; d < 3; ++d) {
+      c->Wf[3 * i + d] = w[9 + 3 * L + 3 * i + d];
+      c->Wr[3 * i + d] = w[9 + 6 * L + 3 * i + d];
+    }
+  }
+  for (int k = 0; k <= m->N && k < 64; ++k) {
+    const double wz = (w[2] / 2.0) * exp(-(double)k) + w[2] / 2.0;
+    double* q = c->qdiag[k];
+    q[0] = 2.0 * w[0];
+    q[1] = 2.0 * w[1];
+    q[2] = 2.0 * (wz * wz);
+    for (int j = 3; j < 9; ++j) q[j] = 2.0 * w[j];
+    for (int j = 0; j < 3; ++j) q[9 + j] = 2.0 * m->theta_weights[j];
+    q[12] = 0.0;
+  }
+  for (int j = 0; j < 5; ++j) c->force_ub[j] = m->force_ub[j];
+  /* inverse of the body inertia (adjugate / determinant) */
+  const double* I = m->inertia;
+  const double a00 = I[4] * I[8] - I[5] * I[7], a01 = I[2] * I[7] - I[1] * I[8], a02 = I[1] * I[5] - I[2] * I[4];
+  const double a10 = I[5] * I[6] - I[3] * I[8], a11 = I[0] * I[8] - I[2] * I[6], a12 = I[2] * I[3] - I[0] * I[5];
+  const double a20 = I[3] * I[7] - I[4] * I[6], a21 = I[1] * I[6] - I[0] * I[7], a22 = I[0] * I[4] - I[1] * I[3];
+  const double det = I[0] * a00 + I[1] * a10 + I[2] * a20;
+  const double id = 1.0 / det;
+  double* R = c->inv_inertia;
+  R[0] = a00 * id; R[1] = a01 * id; R[2] = a02 * id;
+  R[3] = a10 * id; R[4] = a11 * id; R[5] = a12 * id;
+  R[6] = a20 * id; R[7] = a21 * id; R[8] = a22 * id;
+}
+
+void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                          double* A, double* B) {
+  const int N = c->N, L = c->L;
+  const double dt = c->dt;
+  for (int k = 0; k < N; ++k) {
+    double* Ak = A + (size_t)k * NX * NX;
+    double* Bk = B + (size_t)k * NX * NU;
+    memset(Ak, 0, sizeof(double) * NX * NX);
+    memset(Bk, 0, sizeof(double) * NX * NU);
+    for (int i = 0; i < NX; ++i) Ak[i * NX + i] = 1.0;
+    /* c+ = c + dt v */
+    for (int d = 0; d < 3; ++d) Ak[d * NX + 3 + d] = dt;
+    /* v_z+ = v_z + dt g_z */
+    Ak[5 * NX + 12] = dt;
+    /* Theta+ = Theta + dt * I_b^{-1} R_z(psi)^T L */
+    const double psi = xref[k * NX + 11];
+    const double cp = cos(psi), sp = sin(psi);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double s = 0.0;
+        for (int e = 0; e < 3; ++e) s += c->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
+        Ak[(9 + a) * NX + 6 + b] = dt * s;
+      }
+    /* inputs: v+ += dt/m f_i, L+ += dt [r_ik]x f_i for stance legs */
+    for (int i = 0; i < L; ++i) {
+      if (!contact[k * L + i]) continue;
+      const double* p = foot + ((size_t)k * L + i) * 3;
+      const double rx = p[0] - xref[k * NX + 0], ry = p[1] - xref[k * NX + 1], rz = p[2] - xref[k * NX + 2];
+      const double S[9] = {0.0, -rz, ry, rz, 0.0, -rx, -ry, rx, 0.0};
+      for (int d = 0; d < 3; ++d) Bk[(3 + d) * NU + 3 * i + d] = dt / c->mass;
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) Bk[(6 + a) * NU + 3 * i + b] = dt * S[a * 3 + b];
+    }
+  }
+}
+
+static int fdes_and_check(const oracle_consts* c, const uint8_t* contact, double* fdes_z /* [N][L] */) {
+  const int N = c->N, L = c->L;
+  for (int k = 0; k < N; ++k) {
+    int ns = 0;
+    for (int i = 0; i < L; ++i) ns += contact[k * L + i] ? 1 : 0;
+    if (ns <= 0) return CMPC_INVALID_CONTACT;
+    for (int i = 0; i < L; ++i) fdes_z[k * L + i] = contact[k * L + i] ? c->mass * GRAV / (double)ns : 0.0;
+  }
+  return CMPC_SUCCESS;
+}
+
+int oracle_condense_full(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, double* H, double* g) {
+  const int N = c->N, L = c->L, n = NU * N;
+  double* fdes = (double*)malloc(sizeof(double) * N * L);
+  const int st = fdes_and_check(c, contact, fdes);
+  if (st != CMPC_SUCCESS) {
+    free(fdes);
+    return st;
+  }
+  double* A = (double*)malloc(sizeof(double) * N * NX * NX);
+  double* B = (double*)malloc(sizeof(double) * N * NX * NU);
+  oracle_srbd_dynamics(c, xref, foot, contact, A, B);
+  double* G = (double*)calloc((size_t)NX * n, sizeof(double));  /* block row of Bqp for x_k: 13 x 12N */
+  double* G2 = (double*)malloc(sizeof(double) * NX * n);
+  double xh[NX], xh2[NX], e[NX];
+  memcpy(xh, x0, sizeof(xh));
+  memset(H, 0, sizeof(double) * n * n);
+  memset(g, 0, sizeof(double) * n);
+  for (int k = 0; k < N; ++k) {
+    const double* Ak = A + (size_t)k * NX * NX;
+    const double* Bk = B + (size_t)k * NX * NU;
+    /* G <- A_k G + [B_k at columns of step k]; xh <- A_k xh (free response, Aqp x0) */
+    for (int r = 0; r < NX; ++r) {
+      for (int j = 0; j < n; ++j) {
+        double s = 0.0;
+        for (int t = 0; t < NX; ++t) s += Ak[r * NX + t] * G[t * n + j];
+        G2[r * n + j] = s;
+      }
+      for (int j = 0; j < NU; ++j) G2[r * n + NU * k + j] += Bk[r * NU + j];
+      double s = 0.0;
+      for (int t = 0; t < NX; ++t) s += Ak[r * NX + t] * xh[t];
+      xh2[r] = s;
+    }
+    memcpy(G, G2, sizeof(double) * NX * n);
+    memcpy(xh, xh2, sizeof(xh));
+    /* node k+1 cost: H += G' Q G, g += G' Q (xh - xref) */
+    const double* q = c->qdiag[k + 1];
+    for (int r = 0; r < NX; ++r) e[r] = q[r] * (xh[r] - xref[(k + 1) * NX + r]);
+    for (int a = 0; a < n; ++a) {
+      double ga = 0.0;
+      for (int r = 0; r < NX; ++r) ga += G[r * n + a] * e[r];
+      g[a] += ga;
+      for (int b = 0; b <= a; ++b) {
+        double s = 0.0;
+        for (int r = 0; r < NX; ++r) s += G[r * n + a] * q[r] * G[r * n + b];
+        H[a * n + b] += s;
+      }
+    }
+  }
+  for (int a = 0; a < n; ++a)
+    for (int b = a + 1; b < n; ++b) H[a * n + b] = H[b * n + a];
+  /* R-bar: force tracking + force-rate (block tridiagonal), r-bar = -2 W_f f^des */
+  for (int k = 0; k < N; ++k)
+    for (int j = 0; j < NU; ++j) {
+      const int idx = NU * k + j;
+      const int nb = (k > 0) + (k < N - 1);
+      H[idx * n + idx] += 2.0 * c->Wf[j] + 2.0 * c->Wr[j] * (double)nb;
+      if (k < N - 1) {
+        H[idx * n + idx + NU] += -2.0 * c->Wr[j];
+        H[(idx + NU) * n + idx] += -2.0 * c->Wr[j];
+      }
+      if (j % 3 == 2) g[idx] += -2.0 * c->Wf[j] * fdes[k * L + j / 3];
+    }
+  free(fdes);
+  free(A);
+  free(B);
+  free(G);
+  free(G2);
+  return CMPC_SUCCESS;
+}
+
+int oracle_condense(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                    const uint8_t* contact, int ld, int* n_out, double* H, double* g, double* tri_mu, double* tri_lo,
+                    double* tri_hi, int* tri_map) {
+  const int N = c->N, L = c->L, nf = NU * N;
+  *n_out = 0;
+  int idx[NU * 64];
+  int nt = 0;
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < L; ++i)
+      if (contact[k * L + i]) {
+        if (tri_map) tri_map[nt] = k * L + i;
+        idx[nt++] = NU * k + 3 * i;
+      }
+  const int n = 3 * nt;
+  {
+    int ns_ok = 1;
+    for (int k = 0; k < N; ++k) {
+      int ns = 0;
+      for (int i = 0; i < L; ++i) ns += contact[k * L + i] ? 1 : 0;
+      if (ns == 0) ns_ok = 0;
+    }
+    if (!ns_ok) return CMPC_INVALID_CONTACT;
+  }
+  if (n > ld) return CMPC_TOO_LARGE;
+  double* Hf = (double*)malloc(sizeof(double) * nf * nf);
+  double* gf = (double*)malloc(sizeof(double) * nf);
+  const int st = oracle_condense_full(c, x0, xref, foot, contact, Hf, gf);
+  if (st != CMPC_SUCCESS) {
+    free(Hf);
+    free(gf);
+    return st;
+  }
+  for (int a = 0; a < ld; ++a) {
+    for (int b = 0; b < ld; ++b) {
+      double v;
+      if (a < n && b < n)
+        v = Hf[(idx[a / 3] + a % 3) * nf + idx[b / 3] + b % 3];
+      else
+        v = (a == b) ? 1.0 : 0.0;
+      H[(size_t)a * ld + b] = v;
+    }
+    g[a] = a < n ? gf[idx[a / 3] + a % 3] : 0.0;
+  }
+  for (int t = 0; t < ld / 3; ++t) {
+    const int leg = t < nt ? (tri_map ? tri_map[t] % L : 0) : 0;
+    if (tri_mu) tri_mu[t] = t < nt ? c->mu[leg] : 0.0;
+    for (int r = 0; r < 5; ++r) {
+      if (tri_lo) tri_lo[t * 5 + r] = 0.0;
+      if (tri_hi) tri_hi[t * 5 + r] = c->force_ub[r];
+    }
+  }
+  if (tri_mu && !tri_map) {
+    /* recompute leg of each triple when no map was requested */
+    int t = 0;
+    for (int k = 0; k < N; ++k)
+      for (int i = 0; i < L; ++i)
+        if (contact[k * L + i]) tri_mu[t++] = c->mu[i];
+  }
+  *n_out = n;
+  free(Hf);
+  free(gf);
+  return CMPC_SUCCESS;
+}
+
+/* ------------------------------------------------------------------------------------------------ dense LA */
+
+int oracle_cholesky(int n, double* A, int lda) {
+  for (int k = 0; k < n; ++k) {
+    double d = A[k * lda + k];
+    for (int j = 0; j < k; ++j) d -= A[k * lda + j] * A[k * lda + j];
+    if (!(d > 0.0)) return -1;
+    const double l = sqrt(d);
+    A[k * lda + k] = l;
+    for (int i = k + 1; i < n; ++i) {
+      double s = A[i * lda + k];
+      for (int j = 0; j < k; ++j) s -= A[i * lda + j] * A[k * lda + j];
+      A[i * lda + k] = s / l;
+    }
+  }
+  return 0;
+}
+
+void oracle_chol_solve(int n, const double* Lm, int lda, double* b) {
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int j = 0; j < i; ++j) s -= Lm[i * lda + j] * b[j];
+    b[i] = s / Lm[i * lda + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int j = i + 1; j < n; ++j) s -= Lm[j * lda + i] * b[j];
+    b[i] = s / Lm[i * lda + i];
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ IPM */
+
+/* friction pyramid F(mu) rows (CentroidalMPC.cpp:186-190) applied to one force triple */
+static inline void pyr_apply(double mu, const double* f, double* c5) {
+  c5[0] = -f[0] + mu * f[2];
+  c5[1] = f[0] + mu * f[2];
+  c5[2] = -f[1] + mu * f[2];
+  c5[3] = f[1] + mu * f[2];
+  c5[4] = f[2];
+}
+static inline void pyr_applyT(double mu, const double* w, double* f) {
+  f[0] = -w[0] + w[1];
+  f[1] = -w[2] + w[3];
+  f[2] = mu * (w[0] + w[1] + w[2] + w[3]) + w[4];
+}
+
+typedef struct ipm_ws {
+  double *K, *rg, *rhs, *du, *cu, *cdu, *tl, *tu, *ll, *lu, *rl, *ru, *dtl, *dtu, *dll, *dlu, *rml, *rmu, *w;
+} ipm_ws;
+
+static void ipm_dir(int n, int ld, int nt, const double* tri_mu, ipm_ws* W) {
+  const int m = 5 * nt;
+  (void)ld;
+  for (int j = 0; j < m; ++j)
+    W->w[j] = (W->rml[j] + W->ll[j] * W->rl[j]) / W->tl[j] - (W->rmu[j] + W->lu[j] * W->ru[j]) / W->tu[j];
+  for (int i = 0; i < n; ++i) W->rhs[i] = -W->rg[i];
+  for (int t = 0; t < nt; ++t) {
+    double f[3];
+    pyr_applyT(tri_mu[t], W->w + 5 * t, f);
+    for (int d = 0; d < 3; ++d) W->rhs[3 * t + d] -= f[d];
+  }
+  memcpy(W->du, W->rhs, sizeof(double) * n);
+  oracle_chol_solve(n, W->K, n, W->du);
+  for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], W->du + 3 * t, W->cdu + 5 * t);
+  for (int j = 0; j < m; ++j) {
+    W->dtl[j] = W->cdu[j] + W->rl[j];
+    W->dtu[j] = W->ru[j] - W->cdu[j];
+    W->dll[j] = -(W->rml[j] + W->ll[j] * W->dtl[j]) / W->tl[j];
+    W->dlu[j] = -(W->rmu[j] + W->lu[j] * W->dtu[j]) / W->tu[j];
+  }
+}
+
+static double ipm_maxstep(int m, const ipm_ws* W) {
+  double a = 1e300;
+  for (int j = 0; j < m; ++j) {
+    if (W->dtl[j] < 0.0) a = dmin(a, -W->tl[j] / W->dtl[j]);
+    if (W->dtu[j] < 0.0) a = dmin(a, -W->tu[j] / W->dtu[j]);
+    if (W->dll[j] < 0.0) a = dmin(a, -W->ll[j] / W->dll[j]);
+    if (W->dlu[j] < 0.0) a = dmin(a, -W->lu[j] / W->dlu[j]);
+  }
+  return a;
+}
+
+int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
+                  const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters,
+                  double* res) {
+  const int nt = n / 3, m = 5 * nt;
+  ipm_ws W;
+  double* buf = (double*)calloc((size_t)n * n + 4 * (size_t)n + 15 * (size_t)(m + 1), sizeof(double));
+  double* p = buf;
+  W.K = p; p += (size_t)n * n;
+  W.rg = p; p += n;
+  W.rhs = p; p += n;
+  W.du = p; p += n;
+  double* hu = p; p += n;
+  double** mv[] = {&W.cu, &W.cdu, &W.tl, &W.tu, &W.ll, &W.lu, &W.rl, &W.ru, &W.dtl, &W.dtu, &W.dll, &W.dlu,
+                   &W.rml, &W.rmu, &W.w};
+  for (int i = 0; i < 15; ++i) {
+    *mv[i] = p;
+    p += m + 1;
+  }
+  for (int i = 0; i < n; ++i) u[i] = 0.0;
+  /* cold start (warm_start = 0): u = 0, slacks clipped at THR0, lam = mu0 / t */
+  for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], u + 3 * t, W.cu + 5 * t);
+  for (int j = 0; j < m; ++j) {
+    W.tl[j] = dmax(W.cu[j] - tri_lo[j], THR0);
+    W.tu[j] = dmax(tri_hi[j] - W.cu[j], THR0);
+    W.ll[j] = s->mu0 / W.tl[j];
+    W.lu[j] = s->mu0 / W.tu[j];
+  }
+  int status = CMPC_MAX_ITER, it = 0;
+  double rs = 0, ri = 0, rc = 0;
+  for (it = 0;; ++it) {
+    /* residuals */
+    for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], u + 3 * t, W.cu + 5 * t);
+    for (int i = 0; i < n; ++i) {
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc += H[(size_t)i * ld + j] * u[j];
+      hu[i] = acc;
+    }
+    for (int j = 0; j < m; ++j) W.w[j] = W.ll[j] - W.lu[j];
+    for (int t = 0; t < nt; ++t) {
+      double f[3];
+      pyr_applyT(tri_mu[t], W.w + 5 * t, f);
+      for (int d = 0; d < 3; ++d) W.rg[3 * t + d] = hu[3 * t + d] + g[3 * t + d] - f[d];
+    }
+    double musum = 0.0;
+    rs = 0.0;
+    ri = 0.0;
+    rc = 0.0;
+    for (int i = 0; i < n; ++i) rs = dmax(rs, fabs(W.rg[i]));
+    for (int j = 0; j < m; ++j) {
+      W.rl[j] = W.cu[j] - tri_lo[j] - W.tl[j];
+      W.ru[j] = tri_hi[j] - W.cu[j] - W.tu[j];
+      ri = dmax(ri, dmax(fabs(W.rl[j]), fabs(W.ru[j])));
+      const double cl = W.tl[j] * W.ll[j], cu = W.tu[j] * W.lu[j];
+      rc = dmax(rc, dmax(cl, cu));
+      musum += cl + cu;
+    }
+    const double mu = m > 0 ? musum / (2.0 * m) : 0.0;
+    if (!isfinite(rs) || !isfinite(ri) || !isfinite(rc)) {
+      status = CMPC_NAN_SOL;
+      break;
+    }
+    if (rs <= s->tol_stat && ri <= s->tol_ineq && rc <= s->tol_comp) {
+      status = CMPC_SUCCESS;
+      break;
+    }
+    if (it >= s->iter_max) {
+      status = CMPC_MAX_ITER;
+      break;
+    }
+    /* Newton matrix K = H + C' diag(lam/t) C + reg I */
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) W.K[i * n + j] = H[(size_t)i * ld + j];
+    for (int t = 0; t < nt; ++t) {
+      const double* ll = W.ll + 5 * t;
+      const double* lu = W.lu + 5 * t;
+      const double* tl = W.tl + 5 * t;
+      const double* tu = W.tu + 5 * t;
+      double sg[5];
+      for (int r = 0; r < 5; ++r) sg[r] = ll[r] / tl[r] + lu[r] / tu[r];
+      const double mu_t = tri_mu[t];
+      const int b = 3 * t;
+      W.K[b * n + b] += sg[0] + sg[1];
+      W.K[(b + 1) * n + b + 1] += sg[2] + sg[3];
+      W.K[(b + 2) * n + b + 2] += mu_t * mu_t * (sg[0] + sg[1] + sg[2] + sg[3]) + sg[4];
+      const double xz = mu_t * (-sg[0] + sg[1]), yz = mu_t * (-sg[2] + sg[3]);
+      W.K[b * n + b + 2] += xz;
+      W.K[(b + 2) * n + b] += xz;
+      W.K[(b + 1) * n + b + 2] += yz;
+      W.K[(b + 2) * n + b + 1] += yz;
+    }
+    for (int i = 0; i < n; ++i) W.K[i * n + i] += s->reg_prim;
+    if (oracle_cholesky(n, W.K, n) != 0) {
+      status = CMPC_NAN_SOL;
+      break;
+    }
+    /* predictor (affine scaling) */
+    for (int j = 0; j < m; ++j) {
+      W.rml[j] = W.tl[j] * W.ll[j];
+      W.rmu[j] = W.tu[j] * W.lu[j];
+    }
+    ipm_dir(n, ld, nt, tri_mu, &W);
+    double alpha = dmin(1.0, ipm_maxstep(m, &W));
+    if (m > 0) {
+      double maff = 0.0;
+      for (int j = 0; j < m; ++j)
+        maff += (W.tl[j] + alpha * W.dtl[j]) * (W.ll[j] + alpha * W.dll[j]) +
+                (W.tu[j] + alpha * W.dtu[j]) * (W.lu[j] + alpha * W.dlu[j]);
+      maff /= 2.0 * m;
+      const double ratio = maff / mu;
+      const double sigma = ratio * ratio * ratio;
+      /* corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu */
+      for (int j = 0; j < m; ++j) {
+        W.rml[j] = W.tl[j] * W.ll[j] + W.dtl[j] * W.dll[j] - sigma * mu;
+        W.rmu[j] = W.tu[j] * W.lu[j] + W.dtu[j] * W.dlu[j] - sigma * mu;
+      }
+      ipm_dir(n, ld, nt, tri_mu, &W);
+      alpha = dmin(1.0, TAU * ipm_maxstep(m, &W));
+    }
+    if (alpha < s->alpha_min) {
+      status = CMPC_MIN_STEP;
+      break;
+    }
+    for (int i = 0; i < n; ++i) u[i] += alpha * W.du[i];
+    for (int j = 0; j < m; ++j) {
+      W.tl[j] += alpha * W.dtl[j];
+      W.tu[j] += alpha * W.dtu[j];
+      W.ll[j] += alpha * W.dll[j];
+      W.lu[j] += alpha * W.dlu[j];
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    if (!isfinite(u[i])) status = CMPC_NAN_SOL;
+  if (lam_lo) memcpy(lam_lo, W.ll, sizeof(double) * m);
+  if (lam_hi) memcpy(lam_hi, W.lu, sizeof(double) * m);
+  if (iters) *iters = it;
+  if (res) {
+    res[0] = rs;
+    res[1] = 0.0;
+    res[2] = ri;
+    res[3] = rc;
+  }
+  free(buf);
+  return status;
+}
+
+void oracle_qp_kkt(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
+                   const double* tri_hi, const double* u, const double* lam_lo, const double* lam_hi, double* out) {
+  const int nt = n / 3;
+  double st = 0.0, pf = 0.0, cp = 0.0, dn = 0.0;
+  for (int t = 0; t < nt; ++t) {
+    double w[5], f[3], c5[5];
+    for (int r = 0; r < 5; ++r) w[r] = lam_lo[5 * t + r] - lam_hi[5 * t + r];
+    pyr_applyT(tri_mu[t], w, f);
+    pyr_apply(tri_mu[t], u + 3 * t, c5);
+    for (int d = 0; d < 3; ++d) {
+      const int i = 3 * t + d;
+      double acc = g[i] - f[d];
+      for (int j = 0; j < n; ++j) acc += H[(size_t)i * ld + j] * u[j];
+      st = dmax(st, fabs(acc));
+    }
+    for (int r = 0; r < 5; ++r) {
+      const int j = 5 * t + r;
+      pf = dmax(pf, dmax(tri_lo[j] - c5[r], c5[r] - tri_hi[j]));
+      cp = dmax(cp, dmax(fabs(lam_lo[j] * (c5[r] - tri_lo[j])), fabs(lam_hi[j] * (tri_hi[j] - c5[r]))));
+      dn = dmax(dn, dmax(-lam_lo[j], -lam_hi[j]));
+    }
+  }
+  out[0] = st;
+  out[1] = pf;
+  out[2] = cp;
+  out[3] = dn;
+}
+
+/* ------------------------------------------------------------------------------------------------ full path */
+
+int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                     const double* foot, const uint8_t* contact, double* u, double* x, int* iters) {
+  const int N = c->N, L = c->L, ld = NU * N;
+  double* H = (double*)malloc(sizeof(double) * ld * ld);
+  double* g = (double*)malloc(sizeof(double) * ld);
+  double* mu = (double*)malloc(sizeof(double) * ld);
+  double* lo = (double*)malloc(sizeof(double) * 5 * ld);
+  double* hi = (double*)malloc(sizeof(double) * 5 * ld);
+  double* uc = (double*)malloc(sizeof(double) * ld);
+  int* map = (int*)malloc(sizeof(int) * ld);
+  int n = 0, it = 0;
+  memset(u, 0, sizeof(double) * N * NU);
+  int st = oracle_condense(c, x0, xref, foot, contact, ld, &n, H, g, mu, lo, hi, map);
+  if (st == CMPC_SUCCESS) {
+    st = oracle_qp_ipm(n, ld, H, g, mu, lo, hi, s, uc, NULL, NULL, &it, NULL);
+    for (int t = 0; t < n / 3; ++t)
+      for (int d = 0; d < 3; ++d) u[map[t] * 3 + d] = uc[3 * t + d];
+  }
+  if (x) {
+    /* rollout x_{k+1} = A_k x_k + B_k u_k */
+    double* A = (double*)malloc(sizeof(double) * N * NX * NX);
+    double* B = (double*)malloc(sizeof(double) * N * NX * NU);
+    oracle_srbd_dynamics(c, xref, foot, contact, A, B);
+    memcpy(x, x0, sizeof(double) * NX);
+    for (int k = 0; k < N; ++k)
+      for (int r = 0; r < NX; ++r) {
+        double acc = 0.0;
+        for (int t = 0; t < NX; ++t) acc += A[(size_t)k * NX * NX + r * NX + t] * x[k * NX + t];
+        for (int j = 0; j < NU; ++j) acc += B[(size_t)k * NX * NU + r * NU + j] * u[k * NU + j];
+        x[(k + 1) * NX + r] = acc;
+      }
+    free(A);
+    free(B);
+  }
+  if (iters) *iters = it;
+  free(H);
+  free(g);
+  free(mu);
+  free(lo);
+  free(hi);
+  free(uc);
+  free(map);
+  return st;
+}
+
+typedef struct batch_job {
+  const oracle_consts* c;
+  const cmpc_settings* s;
+  int B, tid, nthreads;
+  const double *x0, *xref, *foot;
+  const uint8_t* contact;
+  double *u, *x;
+  int *status, *iters;
+} batch_job;
+
+static void* batch_worker(void* arg) {
+  batch_job* j = (batch_job*)arg;
+  const int N = j->c->N, L = j->c->L;
+  for (int q = j->tid; q < j->B; q += j->nthreads) {
+    int it = 0;
+    const int st = oracle_solve_one(j->c, j->s, j->x0 + (size_t)q * NX, j->xref + (size_t)q * (N + 1) * NX,
+                                    j->foot + (size_t)q * (N + 1) * L * 3, j->contact + (size_t)q * N * L,
+                                    j->u + (size_t)q * N * NU, j->x ? j->x + (size_t)q * (N + 1) * NX : NULL, &it);
+    if (j->status) j->status[q] = st;
+    if (j->iters) j->iters[q] = it;
+  }
+  return NULL;
+}
+
+int oracle_solve_batch(const cmpc_model* m, const cmpc_settings* s, int B, const double* x0, const double* xref,
+                       const double* foot, const uint8_t* contact, double* u, double* x, int* status, int* iters,
+                       int nthreads) {
+  oracle_consts c;
+  oracle_consts_init(m, &c);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  batch_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; ++t) {
+    batch_job jb = {&c, s, B, t, nthreads, x0, xref, foot, contact, u, x, status, iters};
+    jobs[t] = jb;
+  }
+  if (nthreads == 1) {
+    batch_worker(&jobs[0]);
+    return 0;
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------------ generator */
+
+static inline void mulhilo32(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {
+  const uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  *lo = (uint32_t)p;
+}
+
+void oracle_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo32(0xD2511F53u, c0, &hi0, &lo0);
+    mulhilo32(0xCD9E8D57u, c2, &hi1, &lo1);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+/* uniform draw idx of QP gid in [0,1): 53-bit mantissa, exact on any IEEE host/device */
+static double gen_uniform(uint64_t seed, uint64_t gid, int idx) {
+  const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  const uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)(idx >> 1), 0x43504D43u /* "CMPC" */};
+  uint32_t o[4];
+  oracle_philox4x32_10(ctr, key, o);
+  const uint64_t v = (idx & 1) ? ((uint64_t)o[3] << 32 | o[2]) : ((uint64_t)o[1] << 32 | o[0]);
+  return (double)(v >> 11) * 0x1.0p-53;
+}
+
+static inline double urange(double a, double b, double u) { return fma(b - a, u, a); }
+
+/* nominal feet of CentoidMPCTest.cpp:43-46 (lf, rf, rh, lh) */
+static const double kNomFoot[4][2] = {{0.35, 0.052}, {0.35, -0.054}, {-0.37, -0.053}, {-0.36, 0.054}};
+
+void oracle_generate(const cmpc_model* m, uint64_t seed, int64_t qp_offset, int B, int gait, double* x0,
+                     double* xref, double* foot, uint8_t* contact) {
+  const int N = m->N, L = m->n_legs;
+  const double PI = 3.14159265358979323846;
+  for (int q = 0; q < B; ++q) {
+    const uint64_t gid = (uint64_t)(qp_offset + q);
+    double U[24];
+    for (int i = 0; i < 24; ++i) U[i] = gen_uniform(seed, gid, i);
+    double* X0 = x0 + (size_t)q * NX;
+    X0[0] = urange(-0.2, 0.2, U[0]);
+    X0[1] = urange(-0.2, 0.2, U[1]);
+    X0[2] = urange(0.12, 0.20, U[2]);
+    X0[3] = urange(-1.0, 1.0, U[3]);
+    X0[4] = urange(-1.0, 1.0, U[4]);
+    X0[5] = urange(-0.2, 0.2, U[5]);
+    for (int d = 0; d < 3; ++d) X0[6 + d] = urange(-0.1, 0.1, U[6 + d]);
+    X0[9] = urange(-0.1, 0.1, U[9]);
+    X0[10] = urange(-0.1, 0.1, U[10]);
+    X0[11] = urange(-PI, PI, U[11]);
+    X0[12] = -GRAV;
+    const double vdx = urange(-1.0, 1.0, U[12]), vdy = urange(-1.0, 1.0, U[13]);
+    double* XR = xref + (size_t)q * (N + 1) * NX;
+    double* FT = foot + (size_t)q * (N + 1) * L * 3;
+    for (int k = 0; k <= N; ++k) {
+      double* xr = XR + k * NX;
+      const double tk = (double)k * m->dt;
+      xr[0] = fma(tk, vdx, X0[0]);
+      xr[1] = fma(tk, vdy, X0[1]);
+      xr[2] = 0.15;
+      xr[3] = vdx;
+      xr[4] = vdy;
+      xr[5] = 0.0;
+      for (int d = 6; d < 11; ++d) xr[d] = 0.0;
+      xr[11] = X0[11];
+      xr[12] = -GRAV;
+      for (int i = 0; i < L; ++i) {
+        double* p = FT + ((size_t)k * L + i) * 3;
+        p[0] = (xr[0] + kNomFoot[i & 3][0]) + urange(-0.03, 0.03, U[14 + 2 * (i & 3)]);
+        p[1] = (xr[1] + kNomFoot[i & 3][1]) + urange(-0.03, 0.03, U[15 + 2 * (i & 3)]);
+        p[2] = 0.0;
+      }
+    }
+    const int h = GAIT_HALF_PERIOD;
+    const int phase = (int)(U[22] * (double)(2 * h));
+    int gsel = 0;
+    if (gait == 1) gsel = (int)(U[23] * 3.0);
+    uint8_t* C = contact + (size_t)q * N * L;
+    for (int k = 0; k < N; ++k) {
+      const int first = ((k + phase) % (2 * h)) < h;
+      for (int i = 0; i < L; ++i) {
+        int e;
+        if (gsel == 0) /* trot: {lf, rh} / {rf, lh} (CentoidMPCTest.cpp:68-73) */
+          e = first ? (i == 0 || i == 2) : (i == 1 || i == 3);
+        else if (gsel == 1) /* bound: front {0,1} / hind {2,3} */
+          e = first ? (i < 2) : (i >= 2);
+        else /* pronk, stance phase: all legs */
+          e = 1;
+        C[k * L + i] = (uint8_t)e;
+      }
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ generic OCP */
+
+static void ocp_offsets(int N, int nx, const int* nu, size_t* offA, size_t* offB, size_t* offb, size_t* offQ,
+                        size_t* offS, size_t* offR, size_t* offq, size_t* offr, size_t* total) {
+  size_t o = 0;
+  for (int k = 0; k < N; ++k) {
+    offA[k] = o; o += (size_t)nx * nx;
+    offB[k] = o; o += (size_t)nx * nu[k];
+    offb[k] = o; o += (size_t)nx;
+  }
+  for (int k = 0; k <= N; ++k) {
+    const int m = k < N ? nu[k] : 0;
+    offQ[k] = o; o += (size_t)nx * nx;
+    offS[k] = o; o += (size_t)m * nx;
+    offR[k] = o; o += (size_t)m * m;
+    offq[k] = o; o += (size_t)nx;
+    offr[k] = o; o += (size_t)m;
+  }
+  *total = o;
+}
+
+size_t oracle_ocp_record_size(int N, int nx, const int* nu) {
+  size_t o = 0;
+  for (int k = 0; k < N; ++k) o += (size_t)nx * nx + (size_t)nx * nu[k] + nx;
+  for (int k = 0; k <= N; ++k) {
+    const int m = k < N ? nu[k] : 0;
+    o += (size_t)nx * nx + (size_t)m * nx + (size_t)m * m + nx + m;
+  }
+  return o;
+}
+
+#define CM(M, ld, r, c) ((M)[(size_t)(c) * (ld) + (r)]) /* column-major access */
+
+int oracle_ocp_condense(int N, int nx, const int* nu, const double* x0, const double* rec, double* H, double* g) {
+  size_t offA[N], offB[N], offb[N], offQ[N + 1], offS[N + 1], offR[N + 1], offq[N + 1], offr[N + 1], tot;
+  ocp_offsets(N, nx, nu, offA, offB, offb, offQ, offS, offR, offq, offr, &tot);
+  int cu[N + 1];
+  int nU = 0;
+  for (int k = 0; k < N; ++k) {
+    cu[k] = nU;
+    nU += nu[k];
+  }
+  cu[N] = nU;
+  memset(H, 0, sizeof(double) * nU * nU);
+  memset(g, 0, sizeof(double) * nU);
+  double* G = (double*)calloc((size_t)nx * (nU + 1), sizeof(double)); /* row-major nx x nU */
+  double* G2 = (double*)malloc(sizeof(double) * nx * (nU + 1));
+  double* xb = (double*)malloc(sizeof(double) * nx);
+  double* xb2 = (double*)malloc(sizeof(double) * nx);
+  double* tmp = (double*)malloc(sizeof(double) * nx);
+  memcpy(xb, x0, sizeof(double) * nx);
+  /* k = 0: only the linear term r0 + S0 x0 (HpipmInterface.cpp:205-208) and R0 */
+  for (int k = 0; k <= N; ++k) {
+    const int m = k < N ? nu[k] : 0;
+    const double* Q = rec + offQ[k];
+    const double* S = rec + offS[k];
+    const double* R = rec + offR[k];
+    const double* q = rec + offq[k];
+    const double* r = rec + offr[k];
+    if (k >= 1) {
+      /* H += G' Q G; g += G' (Q xb + q) */
+      for (int i = 0; i < nx; ++i) {
+        double s = q[i];
+        for (int j = 0; j < nx; ++j) s += CM(Q, nx, i, j) * xb[j];
+        tmp[i] = s;
+      }
+      for (int a = 0; a < cu[k]; ++a) {
+        double s = 0.0;
+        for (int i = 0; i < nx; ++i) s += G[i * nU + a] * tmp[i];
+        g[a] += s;
+        for (int b = 0; b < cu[k]; ++b) {
+          double h = 0.0;
+          for (int i = 0; i < nx; ++i) {
+            double qg = 0.0;
+            for (int j = 0; j < nx; ++j) qg += CM(Q, nx, i, j) * G[j * nU + b];
+            h += G[i * nU + a] * qg;
+          }
+          H[a * nU + b] += h;
+        }
+      }
+    }
+    if (m > 0) {
+      /* g_k += S xb + r ; H_kk += R ; cross terms E'S G + G'S'E */
+      for (int a = 0; a < m; ++a) {
+        double s = r[a];
+        for (int j = 0; j < nx; ++j) s += CM(S, m, a, j) * xb[j];
+        g[cu[k] + a] += s;
+        for (int b = 0; b < m; ++b) H[(cu[k] + a) * nU + cu[k] + b] += CM(R, m, a, b);
+        if (k >= 1)
+          for (int b = 0; b < cu[k]; ++b) {
+            double sg = 0.0;
+            for (int j = 0; j < nx; ++j) sg += CM(S, m, a, j) * G[j * nU + b];
+            H[(cu[k] + a) * nU + b] += sg;
+            H[b * nU + cu[k] + a] += sg;
+          }
+      }
+    }
+    if (k < N) {
+      /* propagate: G <- A G + [B at columns of k]; xb <- A xb + b */
+      const double* A = rec + offA[k];
+      const double* Bm = rec + offB[k];
+      const double* b = rec + offb[k];
+      for (int i = 0; i < nx; ++i) {
+        for (int a = 0; a < nU; ++a) {
+          double s = 0.0;
+          for (int j = 0; j < nx; ++j) s += CM(A, nx, i, j) * G[j * nU + a];
+          G2[i * nU + a] = s;
+        }
+        for (int a = 0; a < m; ++a) G2[i * nU + cu[k] + a] += CM(Bm, nx, i, a);
+        double s = b[i];
+        for (int j = 0; j < nx; ++j) s += CM(A, nx, i, j) * xb[j];
+        xb2[i] = s;
+      }
+      memcpy(G, G2, sizeof(double) * nx * nU);
+      memcpy(xb, xb2, sizeof(double) * nx);
+    }
+  }
+  free(G);
+  free(G2);
+  free(xb);
+  free(xb2);
+  free(tmp);
+  return nU;
+}
+
+int oracle_ocp_solve(int N, int nx, const int* nu, const double* x0, const double* rec, double* x, double* u) {
+  int nU = 0;
+  for (int k = 0; k < N; ++k) nU += nu[k];
+  double* H = (double*)malloc(sizeof(double) * (nU * nU + 1));
+  double* g = (double*)malloc(sizeof(double) * (nU + 1));
+  oracle_ocp_condense(N, nx, nu, x0, rec, H, g);
+  int st = CMPC_SUCCESS;
+  if (nU > 0) {
+    if (oracle_cholesky(nU, H, nU) != 0) st = CMPC_NAN_SOL;
+    for (int i = 0; i < nU; ++i) u[i] = -g[i];
+    if (st == CMPC_SUCCESS) oracle_chol_solve(nU, H, nU, u);
+  }
+  size_t offA[N], offB[N], offb[N], offQ[N + 1], offS[N + 1], offR[N + 1], offq[N + 1], offr[N + 1], tot;
+  ocp_offsets(N, nx, nu, offA, offB, offb, offQ, offS, offR, offq, offr, &tot);
+  memcpy(x, x0, sizeof(double) * nx);
+  int cu = 0;
+  for (int k = 0; k < N; ++k) {
+    const double* A = rec + offA[k];
+    const double* Bm = rec + offB[k];
+    const double* b = rec + offb[k];
+    for (int i = 0; i < nx; ++i) {
+      double s = b[i];
+      for (int j = 0; j < nx; ++j) s += CM(A, nx, i, j) * x[k * nx + j];
+      for (int a = 0; a < nu[k]; ++a) s += CM(Bm, nx, i, a) * u[cu + a];
+      x[(k + 1) * nx + i] = s;
+    }
+    cu += nu[k];
+  }
+  for (int i = 0; i < (N + 1) * nx; ++i)
+    if (!isfinite(x[i])) st = CMPC_NAN_SOL;
+  for (int i = 0; i < nU; ++i)
+    if (!isfinite(u[i])) st = CMPC_NAN_SOL;
+  free(H);
+  free(g);
+  return st;
+}
+
+/* general inverse via Cholesky of an SPD matrix (n <= 64): out = M^{-1} */
+static int spd_inverse(int n, const double* M, double* out) {
+  double* Lm = (double*)malloc(sizeof(double) * (n * n + 1));
+  memcpy(Lm, M, sizeof(double) * n * n);
+  if (oracle_cholesky(n, Lm, n) != 0) {
+    free(Lm);
+    return -1;
+  }
+  double* e = (double*)malloc(sizeof(double) * (n + 1));
+  for (int j = 0; j < n; ++j) {
+    for (int i = 0; i < n; ++i) e[i] = (i == j) ? 1.0 : 0.0;
+    oracle_chol_solve(n, Lm, n, e);
+    for (int i = 0; i < n; ++i) out[i * n + j] = e[i];
+  }
+  free(e);
+  free(Lm);
+  return 0;
+}
+
+int oracle_ocp_riccati(int N, int nx, const int* nu, const double* rec, double* Sm, double* sv, double* K,
+                       double* kff) {
+  size_t offA[N], offB[N], offb[N], offQ[N + 1], offS[N + 1], offR[N + 1], offq[N + 1], offr[N + 1], tot;
+  ocp_offsets(N, nx, nu, offA, offB, offb, offQ, offS, offR, offq, offr, &tot);
+  size_t offK[N + 1];
+  int offk[N + 1];
+  size_t ok = 0;
+  int okk = 0;
+  for (int k = 0; k < N; ++k) {
+    offK[k] = ok;
+    ok += (size_t)nu[k] * nx;
+    offk[k] = okk;
+    okk += nu[k];
+  }
+  /* terminal */
+  for (int i = 0; i < nx; ++i) {
+    for (int j = 0; j < nx; ++j) Sm[(size_t)N * nx * nx + i * nx + j] = CM(rec + offQ[N], nx, i, j);
+    sv[(size_t)N * nx + i] = rec[offq[N] + i];
+  }
+  double* SmA = (double*)malloc(sizeof(double) * nx * nx);
+  double* Smb = (double*)malloc(sizeof(double) * nx);
+  double* P = (double*)malloc(sizeof(double) * 64 * nx);
+  double* Rt = (double*)malloc(sizeof(double) * 64 * 64);
+  double* iR = (double*)malloc(sizeof(double) * 64 * 64);
+  double* rr = (double*)malloc(sizeof(double) * 64);
+  double* SmB = (double*)malloc(sizeof(double) * nx * 64);
+  int st = 0;
+  for (int k = N - 1; k >= 0; --k) {
+    const int m = nu[k];
+    const double* A = rec + offA[k];
+    const double* Bm = rec + offB[k];
+    const double* b = rec + offb[k];
+    const double* Q = rec + offQ[k];
+    const double* S = rec + offS[k];
+    const double* R = rec + offR[k];
+    const double* q = rec + offq[k];
+    const double* r = rec + offr[k];
+    const double* Sn = Sm + (size_t)(k + 1) * nx * nx;
+    const double* sn = sv + (size_t)(k + 1) * nx;
+    for (int i = 0; i < nx; ++i) {
+      for (int j = 0; j < nx; ++j) {
+        double s = 0.0;
+        for (int t = 0; t < nx; ++t) s += Sn[i * nx + t] * CM(A, nx, t, j);
+        SmA[i * nx + j] = s;
+      }
+      for (int a = 0; a < m; ++a) {
+        double s = 0.0;
+        for (int t = 0; t < nx; ++t) s += Sn[i * nx + t] * CM(Bm, nx, t, a);
+        SmB[i * 64 + a] = s;
+      }
+      double s = 0.0;
+      for (int t = 0; t < nx; ++t) s += Sn[i * nx + t] * b[t];
+      Smb[i] = s;
+    }
+    /* P = S + B' Sm A (m x nx); Rt = R + B' Sm B; rr = r + B' sv + B' Sm b */
+    for (int a = 0; a < m; ++a) {
+      for (int j = 0; j < nx; ++j) {
+        double s = CM(S, m, a, j);
+        for (int t = 0; t < nx; ++t) s += CM(Bm, nx, t, a) * SmA[t * nx + j];
+        P[a * nx + j] = s;
+      }
+      for (int c = 0; c < m; ++c) {
+        double s = CM(R, m, a, c);
+        for (int t = 0; t < nx; ++t) s += CM(Bm, nx, t, a) * SmB[t * 64 + c];
+        Rt[a * m + c] = s;
+      }
+      double s = r[a];
+      for (int t = 0; t < nx; ++t) s += CM(Bm, nx, t, a) * (sn[t] + Smb[t]);
+      rr[a] = s;
+    }
+    if (m > 0 && spd_inverse(m, Rt, iR) != 0) st = -1;
+    double* Sk = Sm + (size_t)k * nx * nx;
+    double* sk = sv + (size_t)k * nx;
+    for (int i = 0; i < nx; ++i) {
+      for (int j = 0; j < nx; ++j) {
+        double s = CM(Q, nx, i, j);
+        for (int t = 0; t < nx; ++t) s += CM(A, nx, t, i) * SmA[t * nx + j];
+        for (int a = 0; a < m; ++a)
+          for (int c = 0; c < m; ++c) s -= P[a * nx + i] * iR[a * m + c] * P[c * nx + j];
+        Sk[i * nx + j] = s;
+      }
+      double s = q[i];
+      for (int t = 0; t < nx; ++t) s += CM(A, nx, t, i) * (sn[t] + Smb[t]);
+      for (int a = 0; a < m; ++a)
+        for (int c = 0; c < m; ++c) s -= P[a * nx + i] * iR[a * m + c] * rr[c];
+      sk[i] = s;
+    }
+    for (int a = 0; a < m; ++a) {
+      for (int j = 0; j < nx; ++j) {
+        double s = 0.0;
+        for (int c = 0; c < m; ++c) s -= iR[a * m + c] * P[c * nx + j];
+        K[offK[k] + (size_t)a * nx + j] = s;
+      }
+      double s = 0.0;
+      for (int c = 0; c < m; ++c) s -= iR[a * m + c] * rr[c];
+      kff[offk[k] + a] = s;
+    }
+  }
+  free(SmA);
+  free(Smb);
+  free(P);
+  free(Rt);
+  free(iR);
+  free(rr);
+  free(SmB);
+  return st;
+}

@@ -1,0 +1,100 @@
+/*
+ * cmpc_oracle.h — CPU fp64 restatement of the reference's CentroidalMPC / HpipmInterface hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Nothing in the product (cheeta-mpc_amd/) links, loads or calls this code; only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, and only as the checker / the CPU
+ * baseline. Parity status: the reference's solver (CasADi/IPOPT, HPIPM@255ffdf/BLASFEO@ae6e2d1) is absent from the
+ * image and cannot be built offline; this restatement is pinned by the reference's own
+ * known-answer constructions (testHpipmInterface.cpp:112-152 knownSolution, :208-256 noInputs, :258-340
+ * retrieveRiccati), by KKT certificates and by numpy golden vectors (tests/golden/). Parity against the HPIPM
+ * binary itself is unpinned.
+ */
+#ifndef CMPC_ORACLE_H_
+#define CMPC_ORACLE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cmpc/cmpc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Model constants derived once per model (weights re-indexed, Q diag per node, inverse inertia). */
+typedef struct oracle_consts {
+  int N, L;
+  double mass, dt;
+  double inv_inertia[9];
+  double mu[CMPC_MAX_LEGS];
+  double Wf[CMPC_NU]; /* force tracking weight per (leg, comp) */
+  double Wr[CMPC_NU]; /* force-rate weight per (leg, comp) */
+  double qdiag[64][CMPC_NX]; /* 2*diag(Q_k), k = 0..N (k = 0 unused) */
+  double force_ub[5];
+} oracle_consts;
+
+void oracle_consts_init(const cmpc_model* m, oracle_consts* c);
+
+/* SRBD linearisation (SURVEY App. A.2 from CentroidalMPC.cpp:41-100): A [N][13][13], B [N][13][12] row-major. */
+void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                          double* A, double* B);
+
+/* Full condensing over all 12N inputs (no elimination): Hfull [12N][12N], gfull [12N]. Returns 0 or
+ * CMPC_INVALID_CONTACT. */
+int oracle_condense_full(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, double* Hfull, double* gfull);
+
+/* Condensed QP restricted to stance forces (swing legs eliminated):
+ *   *n = 3 * (#stance (k,i)); H [ld][ld] with identity padding; g [ld];
+ *   tri_mu [ld/3], tri_lo/tri_hi [ld/3][5]; tri_map [ld/3] = k*L + i of each active triple.
+ * Returns CMPC_SUCCESS, CMPC_INVALID_CONTACT or CMPC_TOO_LARGE. */
+int oracle_condense(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                    const uint8_t* contact, int ld, int* n, double* H, double* g, double* tri_mu, double* tri_lo,
+                    double* tri_hi, int* tri_map);
+
+/* Dense friction-pyramid QP, Mehrotra predictor-corrector IPM (the algorithm the HIP kernels run).
+ * H [ld][ld], n <= ld, n % 3 == 0. u [n] out; lam_lo/lam_hi [5n/3] out (may be NULL).
+ * res[4] out (may be NULL): max |r_stat|, 0 (no equalities), max |r_ineq|, max comp. Returns status. */
+int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
+                  const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters,
+                  double* res);
+
+/* Whole hot path for one QP: u [N][L][3] (zeros for swing), x [(N+1)][13] (may be NULL). */
+int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                     const double* foot, const uint8_t* contact, double* u, double* x, int* iters);
+
+/* Batch over QP-major records with nthreads pthreads (nthreads <= 1: serial). */
+int oracle_solve_batch(const cmpc_model* m, const cmpc_settings* s, int B, const double* x0, const double* xref,
+                       const double* foot, const uint8_t* contact, double* u, double* x, int* status, int* iters,
+                       int nthreads);
+
+/* KKT certificate of a QP solution: returns max of stationarity / primal infeasibility / |complementarity| /
+ * dual negativity, each in out[0..3]. */
+void oracle_qp_kkt(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
+                   const double* tri_hi, const double* u, const double* lam_lo, const double* lam_hi, double* out);
+
+/* Synthetic inputs (bit-identical to the device generator cmpc_generate_batch). */
+void oracle_generate(const cmpc_model* m, uint64_t seed, int64_t qp_offset, int B, int gait, double* x0,
+                     double* xref, double* foot, uint8_t* contact);
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* ---- Generic OCP-QP (HpipmInterface semantics), record layout as cmpc_ocp_record_size ---- */
+size_t oracle_ocp_record_size(int N, int nx, const int* nu);
+/* Condense: H [nU][nU], g [nU] with nU = sum nu_k (row-major), after x0 elimination (HpipmInterface.cpp:177-208). */
+int oracle_ocp_condense(int N, int nx, const int* nu, const double* x0, const double* rec, double* H, double* g);
+/* Solve by condensing + Cholesky; x [(N+1)][nx], u [nU]. Returns status. */
+int oracle_ocp_solve(int N, int nx, const int* nu, const double* x0, const double* rec, double* x, double* u);
+/* Discrete Riccati recursion (testHpipmInterface.cpp:280-304): Sm [(N+1)][nx][nx], sv [(N+1)][nx],
+ * K [N][nu_k x nx] (row-major, packed by stage), kff [sum nu_k]. */
+int oracle_ocp_riccati(int N, int nx, const int* nu, const double* rec, double* Sm, double* sv, double* K,
+                       double* kff);
+
+/* Small dense helpers exported for tests. */
+int oracle_cholesky(int n, double* A, int lda);                       /* in place, lower; 0 ok, -1 not PD */
+void oracle_chol_solve(int n, const double* L, int lda, double* b);   /* solves (L L^T) x = b in place */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CMPC_ORACLE_H_ */

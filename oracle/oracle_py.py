@@ -1,0 +1,261 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) plus the shared model/settings structs.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+product (cheeta-mpc_amd/). See oracle/cmpc_oracle.h for what the oracle restates and how it is pinned.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NX, NU, NL = 13, 12, 4
+
+# CentoidMPCTest.cpp:19-33 weight vector (ordering as the code reads it, CentroidalMPC.cpp:203-231)
+TEST_WEIGHTS = [1, 1, 100, 0.5, 0.5, 0, 2, 2, 8,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1]
+STATUS = {0: "SUCCESS", 1: "MAX_ITER", 2: "MIN_STEP", 3: "NAN_SOL", 4: "INCONS_EQ", 5: "INVALID_CONTACT",
+          6: "TOO_LARGE"}
+
+
+class Model(C.Structure):
+    _fields_ = [("N", C.c_int), ("n_legs", C.c_int), ("mass", C.c_double), ("dt", C.c_double),
+                ("inertia", C.c_double * 9), ("mu", C.c_double * 4), ("weights", C.c_double * 45),
+                ("force_ub", C.c_double * 5), ("theta_weights", C.c_double * 3)]
+
+
+class Settings(C.Structure):
+    _fields_ = [("hpipm_mode", C.c_int), ("iter_max", C.c_int), ("alpha_min", C.c_double), ("mu0", C.c_double),
+                ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double),
+                ("tol_comp", C.c_double), ("reg_prim", C.c_double), ("warm_start", C.c_int),
+                ("pred_corr", C.c_int), ("ric_alg", C.c_int)]
+
+
+def default_model(N=10):
+    """CentoidMPCTest.cpp:12-33 (m=8, dt=0.01, mu=0.8, 45 weights); inertia diag(0.07,0.26,0.28)."""
+    m = Model()
+    m.N = N
+    m.n_legs = NL
+    m.mass = 8.0
+    m.dt = 0.01
+    for i, v in enumerate([0.07, 0, 0, 0, 0.26, 0, 0, 0, 0.28]):
+        m.inertia[i] = v
+    for i in range(4):
+        m.mu[i] = 0.8
+    for i, v in enumerate(TEST_WEIGHTS):
+        m.weights[i] = float(v)
+    for i in range(4):
+        m.force_ub[i] = 5000.0
+    m.force_ub[4] = 8.0 * 9.81 * NL
+    return m
+
+
+def default_settings(**kw):
+    """hpipm_interface::Settings defaults (HpipmInterfaceSettings.h:44-57)."""
+    s = Settings(hpipm_mode=0, iter_max=30, alpha_min=1e-12, mu0=10.0, tol_stat=1e-6, tol_eq=1e-8, tol_ineq=1e-8,
+                 tol_comp=1e-8, reg_prim=1e-12, warm_start=0, pred_corr=1, ric_alg=0)
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def tight_settings():
+    return default_settings(tol_stat=1e-10, tol_ineq=1e-10, tol_comp=1e-11, iter_max=50)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        L = C.CDLL(path)
+        P = C.POINTER
+        d, i, u8 = P(C.c_double), P(C.c_int), P(C.c_uint8)
+        L.oracle_solve_batch.argtypes = [P(Model), P(Settings), C.c_int, d, d, d, u8, d, d, i, i, C.c_int]
+        L.oracle_generate.argtypes = [P(Model), C.c_uint64, C.c_int64, C.c_int, C.c_int, d, d, d, u8]
+        L.oracle_qp_ipm.argtypes = [C.c_int, C.c_int, d, d, d, d, d, P(Settings), d, d, d, i, d]
+        L.oracle_qp_kkt.argtypes = [C.c_int, C.c_int, d, d, d, d, d, d, d, d, d]
+        L.oracle_ocp_record_size.restype = C.c_size_t
+        L.oracle_ocp_record_size.argtypes = [C.c_int, C.c_int, i]
+        L.oracle_ocp_condense.argtypes = [C.c_int, C.c_int, i, d, d, d, d]
+        L.oracle_ocp_solve.argtypes = [C.c_int, C.c_int, i, d, d, d, d]
+        L.oracle_ocp_riccati.argtypes = [C.c_int, C.c_int, i, d, d, d, d, d]
+        L.oracle_cholesky.argtypes = [C.c_int, d, C.c_int]
+        L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
+        _lib = L
+    return _lib
+
+
+class _Consts(C.Structure):
+    _fields_ = [("N", C.c_int), ("L", C.c_int), ("mass", C.c_double), ("dt", C.c_double),
+                ("inv_inertia", C.c_double * 9), ("mu", C.c_double * 4), ("Wf", C.c_double * 12),
+                ("Wr", C.c_double * 12), ("qdiag", (C.c_double * 13) * 64), ("force_ub", C.c_double * 5)]
+
+
+def _p(a, t=C.c_double):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def consts(model):
+    L = lib()
+    c = _Consts()
+    L.oracle_consts_init(C.byref(model), C.byref(c))
+    return c
+
+
+def generate(model, seed, B, gait=0, offset=0):
+    N = model.N
+    x0 = np.zeros((B, NX))
+    xref = np.zeros((B, N + 1, NX))
+    foot = np.zeros((B, N + 1, NL, 3))
+    contact = np.zeros((B, N, NL), dtype=np.uint8)
+    lib().oracle_generate(C.byref(model), seed, offset, B, gait, _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8))
+    return x0, xref, foot, contact
+
+
+def solve_batch(model, settings, x0, xref, foot, contact, nthreads=1, want_x=True):
+    B = x0.shape[0]
+    N = model.N
+    x0, xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    u = np.zeros((B, N, NL, 3))
+    x = np.zeros((B, N + 1, NX)) if want_x else None
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    lib().oracle_solve_batch(C.byref(model), C.byref(settings), B, _p(x0), _p(xref), _p(foot),
+                             _p(contact, C.c_uint8), _p(u), _p(x) if want_x else None, _p(st, C.c_int),
+                             _p(it, C.c_int), nthreads)
+    return u, x, st, it
+
+
+def condense(model, x0, xref, foot, contact, ld=None):
+    """Condensed QP of one problem: (n, H[ld,ld], g[ld], mu[ld/3], lo[ld/3,5], hi[ld/3,5], map, status)."""
+    N = model.N
+    ld = ld or NU * N
+    c = consts(model)
+    H = np.zeros((ld, ld))
+    g = np.zeros(ld)
+    mu = np.zeros(ld // 3)
+    lo = np.zeros((ld // 3, 5))
+    hi = np.zeros((ld // 3, 5))
+    mp = np.zeros(ld // 3, dtype=np.int32)
+    n = C.c_int(0)
+    x0, xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    st = lib().oracle_condense(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), ld, C.byref(n),
+                               _p(H), _p(g), _p(mu), _p(lo), _p(hi), _p(mp, C.c_int))
+    return n.value, H, g, mu, lo, hi, mp, st
+
+
+def condense_full(model, x0, xref, foot, contact):
+    N = model.N
+    c = consts(model)
+    n = NU * N
+    H = np.zeros((n, n))
+    g = np.zeros(n)
+    x0, xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    st = lib().oracle_condense_full(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(H), _p(g))
+    return H, g, st
+
+
+def srbd_dynamics(model, xref, foot, contact):
+    N = model.N
+    c = consts(model)
+    A = np.zeros((N, NX, NX))
+    B = np.zeros((N, NX, NU))
+    xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    lib().oracle_srbd_dynamics(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(A), _p(B))
+    return A, B
+
+
+def qp_ipm(n, H, g, mu, lo, hi, settings):
+    ld = H.shape[0]
+    H, g, mu, lo, hi = (np.ascontiguousarray(a, dtype=np.float64) for a in (H, g, mu, lo, hi))
+    u = np.zeros(max(n, 1))
+    m = max(5 * (n // 3), 1)
+    ll = np.zeros(m)
+    lu = np.zeros(m)
+    it = C.c_int(0)
+    res = np.zeros(4)
+    st = lib().oracle_qp_ipm(n, ld, _p(H), _p(g), _p(mu), _p(lo), _p(hi), C.byref(settings), _p(u), _p(ll), _p(lu),
+                             C.byref(it), _p(res))
+    return u[:n], ll[:5 * (n // 3)], lu[:5 * (n // 3)], st, it.value, res
+
+
+def qp_kkt(n, H, g, mu, lo, hi, u, ll, lu):
+    ld = H.shape[0]
+    out = np.zeros(4)
+    H, g, mu, lo, hi, u, ll, lu = (np.ascontiguousarray(a, dtype=np.float64) for a in (H, g, mu, lo, hi, u, ll, lu))
+    lib().oracle_qp_kkt(n, ld, _p(H), _p(g), _p(mu), _p(lo), _p(hi), _p(u), _p(ll), _p(lu), _p(out))
+    return out
+
+
+# ---- generic OCP-QP (HpipmInterface semantics) -------------------------------------------------------------
+
+def ocp_pack(N, nx, nu, A, B, b, Q, S, R, q, r):
+    """Pack per-stage lists into the column-major record of cmpc_ocp_record_size."""
+    parts = []
+    for k in range(N):
+        parts += [np.asarray(A[k]).reshape(nx, nx).flatten(order="F"),
+                  np.asarray(B[k]).reshape(nx, nu[k]).flatten(order="F"), np.asarray(b[k]).reshape(nx)]
+    for k in range(N + 1):
+        m = nu[k] if k < N else 0
+        parts += [np.asarray(Q[k]).reshape(nx, nx).flatten(order="F"),
+                  np.asarray(S[k]).reshape(m, nx).flatten(order="F") if m else np.zeros(0),
+                  np.asarray(R[k]).reshape(m, m).flatten(order="F") if m else np.zeros(0),
+                  np.asarray(q[k]).reshape(nx), np.asarray(r[k]).reshape(m) if m else np.zeros(0)]
+    return np.concatenate(parts).astype(np.float64)
+
+
+def ocp_solve(N, nx, nu, x0, rec):
+    nua = np.asarray(nu, dtype=np.int32)
+    nU = int(nua.sum())
+    x = np.zeros((N + 1) * nx)
+    u = np.zeros(max(nU, 1))
+    st = lib().oracle_ocp_solve(N, nx, _p(nua, C.c_int), _p(np.ascontiguousarray(x0, dtype=np.float64)), _p(rec),
+                                _p(x), _p(u))
+    return x.reshape(N + 1, nx), u[:nU], st
+
+
+def ocp_condense(N, nx, nu, x0, rec):
+    nua = np.asarray(nu, dtype=np.int32)
+    nU = int(nua.sum())
+    H = np.zeros((max(nU, 1), max(nU, 1)))
+    g = np.zeros(max(nU, 1))
+    lib().oracle_ocp_condense(N, nx, _p(nua, C.c_int), _p(np.ascontiguousarray(x0, dtype=np.float64)), _p(rec),
+                              _p(H), _p(g))
+    return H[:nU, :nU], g[:nU]
+
+
+def ocp_riccati(N, nx, nu, rec):
+    nua = np.asarray(nu, dtype=np.int32)
+    Sm = np.zeros((N + 1, nx, nx))
+    sv = np.zeros((N + 1, nx))
+    K = np.zeros(max(int(sum(nu[k] * nx for k in range(N))), 1))
+    kff = np.zeros(max(int(nua[:N].sum()), 1))
+    st = lib().oracle_ocp_riccati(N, nx, _p(nua, C.c_int), _p(rec), _p(Sm), _p(sv), _p(K), _p(kff))
+    Ks, ks, o, ok = [], [], 0, 0
+    for k in range(N):
+        Ks.append(K[o:o + nu[k] * nx].reshape(nu[k], nx))
+        ks.append(kff[ok:ok + nu[k]])
+        o += nu[k] * nx
+        ok += nu[k]
+    return Sm, sv, Ks, ks, st
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().oracle_philox4x32_10(c, k, o)
+    return list(o)
