@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X batched centroidal-MPC QP engine.
+
+Metric (BASELINE.json): centroidal QPs/sec (N=10, 13-state/12-input) at batch=4096, max|du| vs the fp64 reference.
+One "step" = one cmpc_solve_batch over a batch of synthetic QPs already resident in HBM: SRBD linearisation +
+condensing + pyramid stacking + batched IPM + scatter/rollout (the whole hot path, nothing skipped).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N      (one process per GPU)
+
+Multi-GPU: the QP batch shards with no data-path collective (weak scaling, B per GPU, QP ids offset by rank so every
+QP's inputs are the same whatever the sharding); gloo is used only for the start/stop barriers and the max-over-ranks
+time. Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cheeta-mpc_amd", "python"))
+
+FP64_PEAK = 78.6e12   # MI355X fp64 vector/matrix, datasheet
+FP32_PEAK = 157.3e12  # MI355X fp32 vector (MI355X_MICROARCH.md chip table)
+SEED = 20221125
+
+
+def ipm_flops(n, iters):
+    """Algorithmic FLOPs of the IPM stage for one QP: per Newton iteration one Cholesky (n^3/3) and
+    two solves with the factor (2 x 2n^2); per residual evaluation one H u product (2n^2)."""
+    n = n.astype(np.float64)
+    it = iters.astype(np.float64)
+    return it * (n ** 3 / 3.0 + 4.0 * n ** 2) + (it + 1.0) * 2.0 * n ** 2
+
+
+def cpu_baseline(model_n, x0, xref, foot, contact, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as op  # test infrastructure: the CPU restatement, timed as the baseline
+    mo = op.default_model(model_n)
+    s = op.default_settings()
+    t0 = time.perf_counter()
+    u, _, st, _ = op.solve_batch(mo, s, x0, xref, foot, contact, nthreads=threads, want_x=False)
+    dt = time.perf_counter() - t0
+    return u, st, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="QPs per GPU per step")
+    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--gait", type=int, default=0, help="0 trot (configs 2-4), 1 mixed trot/bound/pronk (config 5)")
+    ap.add_argument("--cpu-sample", type=int, default=2048, help="QPs in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import cheeta_mpc as cm
+    cm.hip().hipSetDevice(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        import torch
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        dist = (tdist, torch)
+
+    def barrier():
+        if dist:
+            dist[0].barrier()
+
+    def max_over_ranks(v):
+        if not dist:
+            return v
+        t = dist[1].tensor([v], dtype=dist[1].float64)
+        dist[0].all_reduce(t, op=dist[0].ReduceOp.MAX)
+        return float(t.item())
+
+    B, N = args.batch, args.horizon
+    prec = cm.F64 if args.precision == "f64" else cm.F32
+    model = cm.default_model(N)
+    if prec == cm.F64:
+        settings = cm.default_settings()
+    else:
+        settings = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-4, tol_comp=1e-4)
+    eng = cm.Engine(model, settings, precision=prec, max_batch=B)
+    x0, xref, foot, contact = cm.generate_device(model, SEED, B, gait=args.gait, offset=rank * B)
+    u = cm.DeviceArray((B, N, 4, 3), np.float64)
+    st = cm.DeviceArray((B,), np.int32)
+    it = cm.DeviceArray((B,), np.int32)
+    H = cm.hip()
+    import ctypes as C
+    stream = C.c_void_p()
+    H.hipStreamCreate(C.byref(stream))
+
+    for _ in range(args.warmup):
+        eng.solve_device(B, x0, xref, foot, contact, u, None, st, it, stream)
+    H.hipStreamSynchronize(stream)
+
+    cm.lib().cmpc_profile_begin(eng.ctx, args.steps)
+    barrier()
+    H.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.solve_device(B, x0, xref, foot, contact, u, None, st, it, stream)
+    H.hipStreamSynchronize(stream)
+    H.hipDeviceSynchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = max_over_ranks(t1 - t0)
+    ms = [C.c_double(0), C.c_double(0), C.c_double(0)]
+    ncalls = C.c_int(0)
+    cm.lib().cmpc_profile_end(eng.ctx, *[C.byref(m) for m in ms], C.byref(ncalls))
+    ms_cond, ms_ipm, ms_exp = (m.value / max(ncalls.value, 1) for m in ms)
+
+    status = st.host()
+    iters = it.host()
+    ct = contact.host()
+    nvar = 3 * ct.reshape(B, -1).sum(axis=1)
+    ok = status == 0
+    flops_launch = float(ipm_flops(nvar[ok], iters[ok]).sum())
+    peak = FP64_PEAK if prec == cm.F64 else FP32_PEAK
+    achieved = flops_launch / (ms_ipm * 1e-3) if ms_ipm > 0 else 0.0
+
+    value = world * B * args.steps / elapsed
+    result = {
+        "metric": "centroidal QPs/sec (N=10, 13-state/12-input) at batch=4096; max|du| vs HPIPM",
+        "value": value,
+        "unit": "QPs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64" if prec == cm.F64 else "f32",
+        "data": "synthetic (Philox4x32-10 counter-based generator, seed 20221125, CentoidMPCTest params)",
+        "config": {"workload": f"batch {B} QPs/GPU, N={N}, 13-state/12-input SRBD, "
+                               f"{'4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk'}, "
+                               f"{'fp64' if prec == cm.F64 else 'fp32'}, full hot path per step",
+                   "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
+        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "k_ipm_reg (IPM stage)",
+                     "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
+        "stages_ms": {"condense": ms_cond, "ipm": ms_ipm, "expand": ms_exp},
+        "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,
+                   "mean_n": float(nvar.mean())},
+    }
+
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        S = min(args.cpu_sample, B)
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        hx0, hxr, hft = x0.host()[:S], xref.host()[:S], foot.host()[:S]
+        uc, stc, dtc = cpu_baseline(N, hx0, hxr, hft, ct[:S], threads)
+        ug = u.host()[:S]
+        scale = np.maximum(1.0, np.abs(uc).reshape(S, -1).max(axis=1))
+        rel = (np.abs(ug - uc).reshape(S, -1).max(axis=1) / scale)
+        both = (stc == 0) & (status[:S] == 0)
+        result["cpu_baseline"] = {"value": S / dtc, "unit": "QPs/s", "cores": threads, "kind": "port",
+                                  "sample": f"first {S} QPs of the same batch, oracle/cmpc_oracle.c fp64, "
+                                            f"{threads} pthreads, {dtc:.2f} s"}
+        result["max_rel_du_vs_cpu_fp64"] = float(rel[both].max()) if both.any() else None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist[0].destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

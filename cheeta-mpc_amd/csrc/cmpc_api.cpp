@@ -1,0 +1,634 @@
+// cmpc_api.cpp — implementation of the C ABI (include/cmpc/cmpc.h): contexts, device workspace, launches.
+//
+// Ownership follows HPIPM's memsize/create pattern as wrapped by HpipmInterface (HpipmInterface.cpp:46-83, :104-128):
+// the context owns (or borrows) one device slab sized by cmpc_memsize and re-uses it for every batch up to
+// max_batch; no allocation happens on the solve path (graph-capturable). Settings map 1:1 onto
+// hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57). No exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "cmpc/cmpc.h"
+#include "cmpc_device.hpp"
+#include "cmpc_kernels.hpp"
+
+using namespace cmpc;
+
+struct cmpc_ctx {
+  cmpc_model model;
+  cmpc_settings settings;
+  int precision;
+  int max_batch;
+  int ld;
+  int device;
+  DevModel* d_model;
+  char* ws;
+  bool own_ws;
+  size_t ws_bytes;
+  // typed views into ws
+  void* H;
+  void* g;
+  void* tri_mu;
+  void* tri_lo;
+  void* tri_hi;
+  void* u;
+  int* tri_map;
+  int* nvar;
+  int* status;
+  int* iters;
+  // host-API staging (grown on demand, outside the async path)
+  char* stage;
+  size_t stage_bytes;
+  // stage profiling (cmpc_profile_begin/end)
+  std::vector<hipEvent_t> prof_ev;
+  int prof_max;
+  int prof_calls;
+  bool profiling;
+};
+
+namespace {
+
+#define HIP_OK(expr)                      \
+  do {                                    \
+    if ((expr) != hipSuccess) return CMPC_ERR_HIP; \
+  } while (0)
+
+int ld_for(const cmpc_model& m) {
+  const int nf = CMPC_NU * m.N;
+  return nf <= 64 ? 64 : 128;
+}
+
+struct Layout {
+  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, total;
+};
+
+Layout layout(int ld, int precision, int B) {
+  const size_t es = precision == CMPC_F64 ? 8 : 4;
+  const size_t nt = (size_t)(ld / 3);
+  Layout L;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += (bytes + 255) & ~(size_t)255;
+    return at;
+  };
+  L.H = take((size_t)B * ld * ld * es);
+  L.g = take((size_t)B * ld * es);
+  L.mu = take((size_t)B * nt * es);
+  L.lo = take((size_t)B * nt * 5 * es);
+  L.hi = take((size_t)B * nt * 5 * es);
+  L.u = take((size_t)B * ld * es);
+  L.map = take((size_t)B * nt * sizeof(int));
+  L.nvar = take((size_t)B * sizeof(int));
+  L.status = take((size_t)B * sizeof(int));
+  L.iters = take((size_t)B * sizeof(int));
+  L.total = o;
+  return L;
+}
+
+// Model constants (host derivation of SURVEY App. A; weights indexed as CentroidalMPC.cpp:203-231).
+void derive_model(const cmpc_model& m, DevModel& d) {
+  std::memset(&d, 0, sizeof(d));
+  const int L = m.n_legs;
+  const double* w = m.weights;
+  d.N = m.N;
+  d.L = L;
+  d.mass = m.mass;
+  d.dt = m.dt;
+  d.dt_over_m = m.dt / m.mass;
+  for (int i = 0; i < L; ++i) {
+    d.mu[i] = m.mu[i];
+    for (int c = 0; c < 3; ++c) {
+      d.Wf[3 * i + c] = w[9 + 3 * L + 3 * i + c];
+      d.Wr[3 * i + c] = w[9 + 6 * L + 3 * i + c];
+    }
+  }
+  for (int k = 0; k <= m.N && k <= MAXN; ++k) {
+    const double wz = (w[2] / 2.0) * std::exp(-(double)k) + w[2] / 2.0;  // CentroidalMPC.cpp:205
+    double* q = d.qdiag[k];
+    q[0] = 2.0 * w[0];
+    q[1] = 2.0 * w[1];
+    q[2] = 2.0 * (wz * wz);  // sumsqr(weightCoMZ .* dz) squares the weight, :210
+    for (int j = 3; j < 9; ++j) q[j] = 2.0 * w[j];
+    for (int j = 0; j < 3; ++j) q[9 + j] = 2.0 * m.theta_weights[j];
+    q[12] = 0.0;
+  }
+  for (int r = 0; r < 5; ++r) d.ub[r] = m.force_ub[r];
+  const double* I = m.inertia;
+  const double c00 = I[4] * I[8] - I[5] * I[7], c01 = I[5] * I[6] - I[3] * I[8], c02 = I[3] * I[7] - I[4] * I[6];
+  const double det = I[0] * c00 + I[1] * c01 + I[2] * c02;
+  const double inv = 1.0 / det;
+  d.inv_inertia[0] = c00 * inv;
+  d.inv_inertia[1] = (I[2] * I[7] - I[1] * I[8]) * inv;
+  d.inv_inertia[2] = (I[1] * I[5] - I[2] * I[4]) * inv;
+  d.inv_inertia[3] = c01 * inv;
+  d.inv_inertia[4] = (I[0] * I[8] - I[2] * I[6]) * inv;
+  d.inv_inertia[5] = (I[2] * I[3] - I[0] * I[5]) * inv;
+  d.inv_inertia[6] = c02 * inv;
+  d.inv_inertia[7] = (I[1] * I[6] - I[0] * I[7]) * inv;
+  d.inv_inertia[8] = (I[0] * I[4] - I[1] * I[3]) * inv;
+}
+
+bool model_ok(const cmpc_model* m) {
+  return m && m->N >= 1 && m->N <= MAXN && m->n_legs == CMPC_MAX_LEGS && m->mass > 0 && m->dt > 0;
+}
+
+DevSettings dev_settings(const cmpc_settings& s) {
+  DevSettings d;
+  d.iter_max = s.iter_max;
+  d.alpha_min = s.alpha_min;
+  d.mu0 = s.mu0;
+  d.tol_stat = s.tol_stat;
+  d.tol_ineq = s.tol_ineq;
+  d.tol_comp = s.tol_comp;
+  d.reg_prim = s.reg_prim;
+  return d;
+}
+
+template <typename T>
+CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref, const double* foot,
+                              const uint8_t* contact) {
+  CondenseArgs<T> a;
+  a.model = c->d_model;
+  a.ld = c->ld;
+  a.x0 = x0;
+  a.xref = xref;
+  a.foot = foot;
+  a.contact = contact;
+  a.H = (T*)c->H;
+  a.g = (T*)c->g;
+  a.tri_mu = (T*)c->tri_mu;
+  a.tri_lo = (T*)c->tri_lo;
+  a.tri_hi = (T*)c->tri_hi;
+  a.tri_map = c->tri_map;
+  a.nvar = c->nvar;
+  a.status = c->status;
+  return a;
+}
+
+template <typename T>
+IpmArgs<T> ipm_args(cmpc_ctx* c) {
+  IpmArgs<T> a;
+  a.ld = c->ld;
+  a.H = (const T*)c->H;
+  a.g = (const T*)c->g;
+  a.tri_mu = (const T*)c->tri_mu;
+  a.tri_lo = (const T*)c->tri_lo;
+  a.tri_hi = (const T*)c->tri_hi;
+  a.nvar = c->nvar;
+  a.status = c->status;
+  a.iters = c->iters;
+  a.u = (T*)c->u;
+  a.s = dev_settings(c->settings);
+  return a;
+}
+
+int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                 const uint8_t* contact, hipStream_t st) {
+  int r;
+  if (c->precision == CMPC_F64) r = launch_srbd_condense<double>(condense_args<double>(c, x0, xref, foot, contact), B, st);
+  else r = launch_srbd_condense<float>(condense_args<float>(c, x0, xref, foot, contact), B, st);
+  return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
+}
+
+int run_ipm(cmpc_ctx* c, int B, hipStream_t st) {
+  int r;
+  if (c->precision == CMPC_F64) r = launch_ipm<double>(ipm_args<double>(c), B, st);
+  else r = launch_ipm<float>(ipm_args<float>(c), B, st);
+  return r == 0 ? CMPC_OK : CMPC_ERR_HIP;
+}
+
+int ensure_stage(cmpc_ctx* c, size_t bytes) {
+  if (c->stage_bytes >= bytes) return CMPC_OK;
+  if (c->stage) (void)hipFree(c->stage);
+  c->stage = nullptr;
+  c->stage_bytes = 0;
+  HIP_OK(hipMalloc((void**)&c->stage, bytes));
+  c->stage_bytes = bytes;
+  return CMPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void cmpc_settings_default(cmpc_settings* s) {
+  if (!s) return;
+  s->hpipm_mode = 0;
+  s->iter_max = 30;
+  s->alpha_min = 1e-12;
+  s->mu0 = 1e1;
+  s->tol_stat = 1e-6;
+  s->tol_eq = 1e-8;
+  s->tol_ineq = 1e-8;
+  s->tol_comp = 1e-8;
+  s->reg_prim = 1e-12;
+  s->warm_start = 0;
+  s->pred_corr = 1;
+  s->ric_alg = 0;
+}
+
+void cmpc_model_default(cmpc_model* m, int N) {
+  if (!m) return;
+  std::memset(m, 0, sizeof(*m));
+  // CentoidMPCTest.cpp:12-33
+  static const double w[CMPC_NUM_WEIGHTS] = {1,   1,   100, 0.5, 0.5, 0,   2,   2,   8,   0.2, 0.2, 0.2,
+                                             0.3, 0.3, 0.3, 0.1, 0.1, 0.1, 0.2, 0.2, 0.2, 0.3, 0.3, 0.3,
+                                             0.1, 0.1, 0.1, 0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                                             0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1};
+  m->N = N;
+  m->n_legs = CMPC_MAX_LEGS;
+  m->mass = 8.0;
+  m->dt = 0.01;
+  const double I[9] = {0.07, 0, 0, 0, 0.26, 0, 0, 0, 0.28};
+  std::memcpy(m->inertia, I, sizeof(I));
+  for (int i = 0; i < CMPC_MAX_LEGS; ++i) m->mu[i] = 0.8;
+  std::memcpy(m->weights, w, sizeof(w));
+  for (int r = 0; r < 4; ++r) m->force_ub[r] = 5000.0;       // CentroidalMPC.cpp:182-183
+  m->force_ub[4] = m->mass * 9.81 * m->n_legs;
+}
+
+size_t cmpc_memsize(const cmpc_model* model, int precision, int max_batch) {
+  if (!model_ok(model) || max_batch <= 0) return 0;
+  return layout(ld_for(*model), precision, max_batch).total;
+}
+
+int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int precision, int max_batch, void* dev_mem,
+                cmpc_ctx** out) {
+  if (!out || !model_ok(model) || max_batch <= 0 || (precision != CMPC_F64 && precision != CMPC_F32))
+    return CMPC_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CMPC_ERR_NO_DEVICE;
+  cmpc_ctx* c = new (std::nothrow) cmpc_ctx();
+  if (!c) return CMPC_ERR_ARG;
+  c->model = *model;
+  if (settings) c->settings = *settings;
+  else cmpc_settings_default(&c->settings);
+  c->precision = precision;
+  c->max_batch = max_batch;
+  c->ld = ld_for(*model);
+  (void)hipGetDevice(&c->device);
+  const Layout L = layout(c->ld, precision, max_batch);
+  c->ws_bytes = L.total;
+  if (dev_mem) {
+    c->ws = (char*)dev_mem;
+    c->own_ws = false;
+  } else {
+    if (hipMalloc((void**)&c->ws, L.total) != hipSuccess) {
+      delete c;
+      return CMPC_ERR_HIP;
+    }
+    c->own_ws = true;
+  }
+  c->H = c->ws + L.H;
+  c->g = c->ws + L.g;
+  c->tri_mu = c->ws + L.mu;
+  c->tri_lo = c->ws + L.lo;
+  c->tri_hi = c->ws + L.hi;
+  c->u = c->ws + L.u;
+  c->tri_map = (int*)(c->ws + L.map);
+  c->nvar = (int*)(c->ws + L.nvar);
+  c->status = (int*)(c->ws + L.status);
+  c->iters = (int*)(c->ws + L.iters);
+  if (hipMalloc((void**)&c->d_model, sizeof(DevModel)) != hipSuccess) {
+    if (c->own_ws) (void)hipFree(c->ws);
+    delete c;
+    return CMPC_ERR_HIP;
+  }
+  const int r = cmpc_set_model(c, model);
+  if (r != CMPC_OK) {
+    cmpc_destroy(c);
+    return r;
+  }
+  *out = c;
+  return CMPC_OK;
+}
+
+int cmpc_destroy(cmpc_ctx* c) {
+  if (!c) return CMPC_ERR_ARG;
+  if (c->own_ws && c->ws) (void)hipFree(c->ws);
+  if (c->d_model) (void)hipFree(c->d_model);
+  if (c->stage) (void)hipFree(c->stage);
+  for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+  delete c;
+  return CMPC_OK;
+}
+
+int cmpc_set_settings(cmpc_ctx* c, const cmpc_settings* s) {
+  if (!c || !s || s->iter_max < 0) return CMPC_ERR_ARG;
+  c->settings = *s;
+  return CMPC_OK;
+}
+
+int cmpc_set_model(cmpc_ctx* c, const cmpc_model* m) {
+  if (!c || !model_ok(m) || m->N != c->model.N) return CMPC_ERR_ARG;
+  c->model = *m;
+  DevModel d;
+  derive_model(*m, d);
+  HIP_OK(hipMemcpy(c->d_model, &d, sizeof(d), hipMemcpyHostToDevice));
+  return CMPC_OK;
+}
+
+int cmpc_get_model(const cmpc_ctx* c, cmpc_model* out) {
+  if (!c || !out) return CMPC_ERR_ARG;
+  *out = c->model;
+  return CMPC_OK;
+}
+
+int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
+
+int cmpc_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                     const uint8_t* contact, double* u, double* x, int* status, int* iters, void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !status) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  hipEvent_t* ev = nullptr;
+  if (c->profiling && c->prof_calls < c->prof_max) ev = &c->prof_ev[(size_t)4 * c->prof_calls++];
+  if (ev) HIP_OK(hipEventRecord(ev[0], st));
+  int r = run_condense(c, B, x0, xref, foot, contact, st);
+  if (r != CMPC_OK) return r;
+  if (ev) HIP_OK(hipEventRecord(ev[1], st));
+  r = run_ipm(c, B, st);
+  if (r != CMPC_OK) return r;
+  if (ev) HIP_OK(hipEventRecord(ev[2], st));
+  ExpandArgs e;
+  e.model = c->d_model;
+  e.ld = c->ld;
+  e.x0 = x0;
+  e.xref = xref;
+  e.foot = foot;
+  e.contact = contact;
+  e.tri_map = c->tri_map;
+  e.nvar = c->nvar;
+  e.status = c->status;
+  e.u_ws = c->u;
+  e.precision = c->precision;
+  e.u = u;
+  e.x = x;
+  e.status_out = status;
+  e.iters_ws = c->iters;
+  e.iters_out = iters;
+  if (launch_expand(e, B, st) != 0) return CMPC_ERR_HIP;
+  if (ev) HIP_OK(hipEventRecord(ev[3], st));
+  return CMPC_OK;
+}
+
+int cmpc_profile_begin(cmpc_ctx* c, int max_calls) {
+  if (!c || max_calls <= 0) return CMPC_ERR_ARG;
+  for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+  c->prof_ev.assign((size_t)4 * max_calls, nullptr);
+  for (auto& e : c->prof_ev) HIP_OK(hipEventCreate(&e));
+  c->prof_max = max_calls;
+  c->prof_calls = 0;
+  c->profiling = true;
+  return CMPC_OK;
+}
+
+int cmpc_profile_end(cmpc_ctx* c, double* ms_condense, double* ms_ipm, double* ms_expand, int* calls) {
+  if (!c || !c->profiling) return CMPC_ERR_ARG;
+  double acc[3] = {0, 0, 0};
+  for (int k = 0; k < c->prof_calls; ++k) {
+    hipEvent_t* ev = &c->prof_ev[(size_t)4 * k];
+    HIP_OK(hipEventSynchronize(ev[3]));
+    for (int j = 0; j < 3; ++j) {
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, ev[j], ev[j + 1]));
+      acc[j] += ms;
+    }
+  }
+  if (ms_condense) *ms_condense = acc[0];
+  if (ms_ipm) *ms_ipm = acc[1];
+  if (ms_expand) *ms_expand = acc[2];
+  if (calls) *calls = c->prof_calls;
+  c->profiling = false;
+  return CMPC_OK;
+}
+
+int cmpc_solve_batch_host(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                          const uint8_t* contact, double* u, double* x, int* status, int* iters) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !status) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  const int N = c->model.N;
+  const size_t n_x0 = (size_t)B * CMPC_NX, n_xr = (size_t)B * (N + 1) * CMPC_NX,
+               n_ft = (size_t)B * (N + 1) * CMPC_MAX_LEGS * 3, n_ct = (size_t)B * N * CMPC_MAX_LEGS,
+               n_u = (size_t)B * N * CMPC_NU, n_xo = x ? n_xr : 0;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bytes = al(n_x0 * 8) + al(n_xr * 8) + al(n_ft * 8) + al(n_ct) + al(n_u * 8) + al(n_xo * 8) +
+                       2 * al((size_t)B * sizeof(int));
+  int r = ensure_stage(c, bytes);
+  if (r != CMPC_OK) return r;
+  char* p = c->stage;
+  double* d_x0 = (double*)p; p += al(n_x0 * 8);
+  double* d_xr = (double*)p; p += al(n_xr * 8);
+  double* d_ft = (double*)p; p += al(n_ft * 8);
+  uint8_t* d_ct = (uint8_t*)p; p += al(n_ct);
+  double* d_u = (double*)p; p += al(n_u * 8);
+  double* d_xo = x ? (double*)p : nullptr; p += al(n_xo * 8);
+  int* d_st = (int*)p; p += al((size_t)B * sizeof(int));
+  int* d_it = (int*)p;
+  HIP_OK(hipMemcpy(d_x0, x0, n_x0 * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_xr, xref, n_xr * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_ft, foot, n_ft * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_ct, contact, n_ct, hipMemcpyHostToDevice));
+  r = cmpc_solve_batch(c, B, d_x0, d_xr, d_ft, d_ct, d_u, d_xo, d_st, d_it, nullptr);
+  if (r != CMPC_OK) return r;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(u, d_u, n_u * 8, hipMemcpyDeviceToHost));
+  if (x) HIP_OK(hipMemcpy(x, d_xo, n_xo * 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(status, d_st, (size_t)B * sizeof(int), hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, d_it, (size_t)B * sizeof(int), hipMemcpyDeviceToHost));
+  return CMPC_OK;
+}
+
+int cmpc_condense_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                        const uint8_t* contact, double* H, double* g, int* n, int* status, void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !H || !g || !n || !status) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int r = run_condense(c, B, x0, xref, foot, contact, st);
+  if (r != CMPC_OK) return r;
+  if (launch_unpack_qp(c->H, c->g, c->nvar, c->precision, c->ld, H, g, B, st) != 0) return CMPC_ERR_HIP;
+  HIP_OK(hipMemcpyAsync(n, c->nvar, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  HIP_OK(hipMemcpyAsync(status, c->status, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  return CMPC_OK;
+}
+
+int cmpc_qp_solve_batch(cmpc_ctx* c, int B, const double* H, const double* g, const int* n, const double* tri_mu,
+                        const double* tri_lo, const double* tri_hi, double* u, int* status, int* iters,
+                        void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !H || !g || !n || !tri_mu || !tri_lo || !tri_hi || !u || !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (launch_pack_qp(H, g, tri_mu, tri_lo, tri_hi, n, c->precision, c->ld, c->H, c->g, c->tri_mu, c->tri_lo,
+                     c->tri_hi, c->nvar, c->status, B, st) != 0)
+    return CMPC_ERR_HIP;
+  int r = run_ipm(c, B, st);
+  if (r != CMPC_OK) return r;
+  const size_t nu = (size_t)B * c->ld;
+  if (c->precision == CMPC_F64) {
+    HIP_OK(hipMemcpyAsync(u, c->u, nu * 8, hipMemcpyDeviceToDevice, st));
+  } else if (launch_convert_f32_to_f64((const float*)c->u, u, nu, st) != 0) {
+    return CMPC_ERR_HIP;
+  }
+  HIP_OK(hipMemcpyAsync(status, c->status, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  if (iters) HIP_OK(hipMemcpyAsync(iters, c->iters, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  return CMPC_OK;
+}
+
+int cmpc_generate_batch(const cmpc_model* m, uint64_t seed, int64_t qp_offset, int B, int gait, double* x0,
+                        double* xref, double* foot, uint8_t* contact, void* stream) {
+  if (!model_ok(m) || B < 0 || !x0 || !xref || !foot || !contact || (gait != 0 && gait != 1)) return CMPC_ERR_ARG;
+  return launch_generate(*m, seed, qp_offset, B, gait, x0, xref, foot, contact, (hipStream_t)stream) == 0
+             ? CMPC_OK
+             : CMPC_ERR_HIP;
+}
+
+size_t cmpc_ocp_record_size(int N, int nx, const int* nu) {
+  if (N <= 0 || nx <= 0 || !nu) return 0;
+  size_t o = 0;
+  for (int k = 0; k < N; ++k) o += (size_t)nx * nx + (size_t)nx * nu[k] + nx;
+  for (int k = 0; k <= N; ++k) {
+    const size_t m = k < N ? (size_t)nu[k] : 0;
+    o += (size_t)nx * nx + m * nx + m * m + nx + m;
+  }
+  return o;
+}
+
+int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
+                              double* u, int* status) {
+  if (B < 0 || N <= 0 || N > CMPC_OCP_MAX_N || nx <= 0 || nx > 64 || !nu || !x0 || !rec || !x || !u || !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  int nU = 0;
+  for (int k = 0; k < N; ++k) {
+    if (nu[k] < 0) return CMPC_ERR_ARG;
+    nU += nu[k];
+  }
+  const int ldo = nU > 0 ? nU : 1;
+  const size_t rs = cmpc_ocp_record_size(N, nx, nu);
+  std::vector<size_t> offs(8 * (size_t)(N + 1), 0);
+  {
+    size_t o = 0;
+    for (int k = 0; k < N; ++k) {
+      offs[0 * (N + 1) + k] = o; o += (size_t)nx * nx;
+      offs[1 * (N + 1) + k] = o; o += (size_t)nx * nu[k];
+      offs[2 * (N + 1) + k] = o; o += (size_t)nx;
+    }
+    for (int k = 0; k <= N; ++k) {
+      const size_t m = k < N ? (size_t)nu[k] : 0;
+      offs[3 * (N + 1) + k] = o; o += (size_t)nx * nx;
+      offs[4 * (N + 1) + k] = o; o += m * nx;
+      offs[5 * (N + 1) + k] = o; o += m * m;
+      offs[6 * (N + 1) + k] = o; o += (size_t)nx;
+      offs[7 * (N + 1) + k] = o; o += m;
+    }
+  }
+  std::vector<int> nuv(nu, nu + N);
+  nuv.push_back(0);
+  int *d_nu = nullptr, *d_st = nullptr;
+  size_t* d_offs = nullptr;
+  double *d_x0 = nullptr, *d_rec = nullptr, *d_H = nullptr, *d_g = nullptr, *d_sc = nullptr, *d_x = nullptr,
+         *d_u = nullptr;
+  int r = CMPC_OK;
+  const size_t scr = 2 * (size_t)nx * ldo + 4 * (size_t)nx;
+  if (hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)) != hipSuccess ||
+      hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()) != hipSuccess ||
+      hipMalloc((void**)&d_x0, sizeof(double) * B * nx) != hipSuccess ||
+      hipMalloc((void**)&d_rec, sizeof(double) * B * rs) != hipSuccess ||
+      hipMalloc((void**)&d_H, sizeof(double) * B * ldo * ldo) != hipSuccess ||
+      hipMalloc((void**)&d_g, sizeof(double) * B * ldo) != hipSuccess ||
+      hipMalloc((void**)&d_sc, sizeof(double) * B * scr) != hipSuccess ||
+      hipMalloc((void**)&d_x, sizeof(double) * B * (N + 1) * nx) != hipSuccess ||
+      hipMalloc((void**)&d_u, sizeof(double) * B * ldo) != hipSuccess ||
+      hipMalloc((void**)&d_st, sizeof(int) * B) != hipSuccess) {
+    r = CMPC_ERR_HIP;
+  }
+  if (r == CMPC_OK) {
+    (void)hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_x0, x0, sizeof(double) * B * nx, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice);
+    OcpArgs a;
+    a.N = N;
+    a.nx = nx;
+    a.nU = nU;
+    a.nu = d_nu;
+    a.offs = d_offs;
+    a.rec_size = rs;
+    a.x0 = d_x0;
+    a.rec = d_rec;
+    a.H = d_H;
+    a.g = d_g;
+    a.ldo = ldo;
+    a.scratch = d_sc;
+    a.x = d_x;
+    a.u = d_u;
+    a.status = d_st;
+    if (launch_ocp_solve(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess) r = CMPC_ERR_HIP;
+    if (r == CMPC_OK) {
+      (void)hipMemcpy(x, d_x, sizeof(double) * B * (N + 1) * nx, hipMemcpyDeviceToHost);
+      if (nU > 0)
+        for (int b = 0; b < B; ++b)
+          (void)hipMemcpy(u + (size_t)b * nU, d_u + (size_t)b * nU, sizeof(double) * nU, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(d_nu);
+  (void)hipFree(d_offs);
+  (void)hipFree(d_x0);
+  (void)hipFree(d_rec);
+  (void)hipFree(d_H);
+  (void)hipFree(d_g);
+  (void)hipFree(d_sc);
+  (void)hipFree(d_x);
+  (void)hipFree(d_u);
+  (void)hipFree(d_st);
+  return r;
+}
+
+const char* cmpc_status_string(int s) {
+  switch (s) {
+    case CMPC_SUCCESS: return "SUCCESS";
+    case CMPC_MAX_ITER: return "MAX_ITER";
+    case CMPC_MIN_STEP: return "MIN_STEP";
+    case CMPC_NAN_SOL: return "NAN_SOL";
+    case CMPC_INCONS_EQ: return "INCONS_EQ";
+    case CMPC_INVALID_CONTACT: return "INVALID_CONTACT";
+    case CMPC_TOO_LARGE: return "TOO_LARGE";
+    default: return "UNKNOWN";
+  }
+}
+
+const char* cmpc_error_string(int e) {
+  switch (e) {
+    case CMPC_OK: return "ok";
+    case CMPC_ERR_ARG: return "invalid argument";
+    case CMPC_ERR_HIP: return "HIP runtime error";
+    case CMPC_ERR_SIZE: return "size out of range";
+    case CMPC_ERR_NO_DEVICE: return "no HIP device";
+    default: return "unknown error";
+  }
+}
+
+int cmpc_device_info(int* num_cu, int* clock_khz, char* arch, int arch_len) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  hipDeviceProp_t p;
+  HIP_OK(hipGetDeviceProperties(&p, dev));
+  if (num_cu) *num_cu = p.multiProcessorCount;
+  if (clock_khz) *clock_khz = p.clockRate;
+  if (arch && arch_len > 0) {
+    std::snprintf(arch, (size_t)arch_len, "%s", p.gcnArchName);
+  }
+  return CMPC_OK;
+}
+
+const char* cmpc_version(void) { return "cheeta-mpc-amd 0.1.0 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// cmpc_kernels.hpp — internal host-side launcher declarations shared by the HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cmpc_device.hpp"
+
+namespace cmpc {
+
+// largest condensed size served by an IPM size class (classes: n <= 64, 64 < n <= 128)
+#define CMPC_IPM_MAX_N 128
+
+// class-padded size of a condensed problem
+__host__ __device__ inline int ipm_class(int n) { return n <= 64 ? 64 : 128; }
+
+// Per-QP workspace of one context (precision T), QP-major:
+//   H [B][ld][ld], g [B][ld], tri_mu [B][ld/3], tri_lo/tri_hi [B][ld/3][5], tri_map [B][ld/3], nvar [B],
+//   status [B], iters [B], u [B][ld]
+template <typename T>
+struct CondenseArgs {
+  const DevModel* model;
+  int ld;
+  const double* x0;
+  const double* xref;
+  const double* foot;
+  const uint8_t* contact;
+  T* H;
+  T* g;
+  T* tri_mu;
+  T* tri_lo;
+  T* tri_hi;
+  int* tri_map;
+  int* nvar;
+  int* status;
+};
+
+template <typename T>
+struct IpmArgs {
+  int ld;
+  const T* H;
+  const T* g;
+  const T* tri_mu;
+  const T* tri_lo;
+  const T* tri_hi;
+  const int* nvar;
+  int* status;  // in: condense status (non-zero = skip); out: solver status
+  int* iters;
+  T* u;         // [B][ld]
+  DevSettings s;
+};
+
+template <typename T>
+int launch_srbd_condense(const CondenseArgs<T>& a, int B, hipStream_t stream);
+
+// Runs every IPM size class over the batch; each QP is served by the class matching its condensed size.
+template <typename T>
+int launch_ipm(const IpmArgs<T>& a, int B, hipStream_t stream);
+
+struct ExpandArgs {
+  const DevModel* model;
+  int ld;
+  const double* x0;
+  const double* xref;
+  const double* foot;
+  const uint8_t* contact;
+  const int* tri_map;
+  const int* nvar;
+  const int* status;
+  const void* u_ws;  // T [B][ld]
+  int precision;
+  double* u;  // [B][N][L][3]
+  double* x;  // [B][N+1][13] or null
+  int* status_out;
+  const int* iters_ws;
+  int* iters_out;
+};
+int launch_expand(const ExpandArgs& a, int B, hipStream_t stream);
+
+int launch_generate(const cmpc_model& m, uint64_t seed, int64_t qp_offset, int B, int gait, double* x0, double* xref,
+                    double* foot, uint8_t* contact, hipStream_t stream);
+
+// test-hook layout conversions between user [B][ld][ld] double and the class-packed workspace
+int launch_unpack_qp(const void* H_ws, const void* g_ws, const int* nvar, int precision, int ld, double* H, double* g,
+                     int B, hipStream_t stream);
+int launch_pack_qp(const double* H, const double* g, const double* tri_mu, const double* tri_lo, const double* tri_hi,
+                   const int* nvar_in, int precision, int ld, void* H_ws, void* g_ws, void* mu_ws, void* lo_ws,
+                   void* hi_ws, int* nvar_ws, int* status_ws, int B, hipStream_t stream);
+
+// widen/narrow helpers used by the test hooks
+int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream);
+int launch_convert_f64_to_f32(const double* in, float* out, size_t n, hipStream_t stream);
+
+// generic OCP (HpipmInterface::solve semantics)
+struct OcpArgs {
+  int N, nx, nU;
+  const int* nu;       // device [N+1]
+  const size_t* offs;  // device [8][N+1] record offsets (A,B,b,Q,S,R,q,r)
+  size_t rec_size;
+  const double* x0;    // [B][nx]
+  const double* rec;   // [B][rec_size]
+  double* H;           // [B][ldo][ldo] workspace
+  double* g;           // [B][ldo]
+  int ldo;
+  double* scratch;     // [B][2*nx*ldo + 4*nx]
+  double* x;           // [B][N+1][nx]
+  double* u;           // [B][nU]
+  int* status;
+};
+#define CMPC_OCP_MAX_N 256
+int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream);
+
+}  // namespace cmpc

@@ -1,0 +1,483 @@
+// k_misc.hip — the small kernels around the hot path: synthetic input generation, result scatter/rollout,
+// precision conversion, and the generic OCP-QP path behind HpipmInterface::solve.
+#include "cmpc_device.hpp"
+#include "cmpc_kernels.hpp"
+
+namespace cmpc {
+
+// ------------------------------------------------------------------------------------------ generator
+// Philox4x32-10 keyed by seed, counter = (global QP id, draw block, "CMPC"); bit-identical to oracle_generate().
+
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n1 = lo1, n2 = hi0 ^ c[3] ^ k1, n3 = lo0;
+    c[0] = n0;
+    c[1] = n1;
+    c[2] = n2;
+    c[3] = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ double gen_uniform(uint64_t seed, uint64_t gid, int idx) {
+  uint32_t c[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)(idx >> 1), 0x43504D43u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint64_t v = (idx & 1) ? ((uint64_t)c[3] << 32 | c[2]) : ((uint64_t)c[1] << 32 | c[0]);
+  return (double)(v >> 11) * 0x1.0p-53;
+}
+
+__device__ __forceinline__ double urange(double a, double b, double u) { return __builtin_fma(b - a, u, a); }
+
+struct GenArgs {
+  int N, L;
+  double dt;
+  uint64_t seed;
+  int64_t qp_offset;
+  int gait;
+  double* x0;
+  double* xref;
+  double* foot;
+  uint8_t* contact;
+};
+
+__global__ __launch_bounds__(256) void k_generate(GenArgs a, int B) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B) return;
+  const int N = a.N, L = a.L;
+  const uint64_t gid = (uint64_t)(a.qp_offset + q);
+  const double nom[4][2] = {{0.35, 0.052}, {0.35, -0.054}, {-0.37, -0.053}, {-0.36, 0.054}};
+  const double PI = 3.14159265358979323846;
+  double U[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) U[i] = gen_uniform(a.seed, gid, i);
+  double* X0 = a.x0 + (size_t)q * NX;
+  double x0v[NX];
+  x0v[0] = urange(-0.2, 0.2, U[0]);
+  x0v[1] = urange(-0.2, 0.2, U[1]);
+  x0v[2] = urange(0.12, 0.20, U[2]);
+  x0v[3] = urange(-1.0, 1.0, U[3]);
+  x0v[4] = urange(-1.0, 1.0, U[4]);
+  x0v[5] = urange(-0.2, 0.2, U[5]);
+  for (int d = 0; d < 3; ++d) x0v[6 + d] = urange(-0.1, 0.1, U[6 + d]);
+  x0v[9] = urange(-0.1, 0.1, U[9]);
+  x0v[10] = urange(-0.1, 0.1, U[10]);
+  x0v[11] = urange(-PI, PI, U[11]);
+  x0v[12] = -GRAV;
+  for (int s = 0; s < NX; ++s) X0[s] = x0v[s];
+  const double vdx = urange(-1.0, 1.0, U[12]), vdy = urange(-1.0, 1.0, U[13]);
+  double* XR = a.xref + (size_t)q * (N + 1) * NX;
+  double* FT = a.foot + (size_t)q * (N + 1) * L * 3;
+  for (int k = 0; k <= N; ++k) {
+    double* xr = XR + k * NX;
+    const double tk = (double)k * a.dt;
+    const double cx = __builtin_fma(tk, vdx, x0v[0]), cy = __builtin_fma(tk, vdy, x0v[1]);
+    xr[0] = cx;
+    xr[1] = cy;
+    xr[2] = 0.15;
+    xr[3] = vdx;
+    xr[4] = vdy;
+    xr[5] = 0.0;
+    for (int d = 6; d < 11; ++d) xr[d] = 0.0;
+    xr[11] = x0v[11];
+    xr[12] = -GRAV;
+    for (int i = 0; i < L; ++i) {
+      double* p = FT + ((size_t)k * L + i) * 3;
+      p[0] = (cx + nom[i & 3][0]) + urange(-0.03, 0.03, U[14 + 2 * (i & 3)]);
+      p[1] = (cy + nom[i & 3][1]) + urange(-0.03, 0.03, U[15 + 2 * (i & 3)]);
+      p[2] = 0.0;
+    }
+  }
+  const int h = GAIT_HALF_PERIOD;
+  const int phase = (int)(U[22] * (double)(2 * h));
+  const int gsel = a.gait == 1 ? (int)(U[23] * 3.0) : 0;
+  uint8_t* C = a.contact + (size_t)q * N * L;
+  for (int k = 0; k < N; ++k) {
+    const bool first = ((k + phase) % (2 * h)) < h;
+    for (int i = 0; i < L; ++i) {
+      bool e;
+      if (gsel == 0) e = first ? (i == 0 || i == 2) : (i == 1 || i == 3);  // trot (CentoidMPCTest.cpp:68-73)
+      else if (gsel == 1) e = first ? (i < 2) : (i >= 2);                    // bound
+      else e = true;                                                          // pronk, stance phase
+      C[k * L + i] = (uint8_t)e;
+    }
+  }
+}
+
+int launch_generate(const cmpc_model& m, uint64_t seed, int64_t qp_offset, int B, int gait, double* x0, double* xref,
+                    double* foot, uint8_t* contact, hipStream_t stream) {
+  if (B <= 0) return 0;
+  GenArgs a{m.N, m.n_legs, m.dt, seed, qp_offset, gait, x0, xref, foot, contact};
+  hipLaunchKernelGGL(k_generate, dim3((B + 255) / 256), dim3(256), 0, stream, a, B);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ------------------------------------------------------------------------------------------ expand / rollout
+// Scatter the condensed solution back to u[N][L][3] (zeros for swing legs, as the reference's 0 <= F f <= 0 rows
+// force, CentroidalMPC.cpp:199) and roll the SRBD model forward (X = Aqp x0 + Bqp U) for the optional x output.
+
+template <typename T>
+__device__ void expand_one(const ExpandArgs& a, int q) {
+  const DevModel* M = a.model;
+  const int N = M->N, L = NL, ld = a.ld;
+  const int tid = threadIdx.x;
+  const int st = a.status[q];
+  const int n = st == CMPC_TOO_LARGE || st == CMPC_INVALID_CONTACT ? 0 : a.nvar[q];
+  const T* uw = reinterpret_cast<const T*>(a.u_ws) + (size_t)q * ld;
+  double* uo = a.u + (size_t)q * N * NU;
+  for (int i = tid; i < N * NU; i += blockDim.x) uo[i] = 0.0;
+  __syncthreads();
+  for (int t = tid; t < n / 3; t += blockDim.x) {
+    const int kl = a.tri_map[(size_t)q * (ld / 3) + t];
+    for (int d = 0; d < 3; ++d) uo[kl * 3 + d] = (double)uw[3 * t + d];
+  }
+  if (tid == 0) {
+    a.status_out[q] = st;
+    if (a.iters_out) a.iters_out[q] = (st == CMPC_TOO_LARGE || st == CMPC_INVALID_CONTACT) ? 0 : a.iters_ws[q];
+  }
+  if (a.x == nullptr) return;
+  __syncthreads();
+  if (tid != 0) return;
+  const double* xr = a.xref + (size_t)q * (N + 1) * NX;
+  const double* ft = a.foot + (size_t)q * (N + 1) * L * 3;
+  const uint8_t* ct = a.contact + (size_t)q * N * L;
+  double* xo = a.x + (size_t)q * (N + 1) * NX;
+  double x[NX];
+  for (int s = 0; s < NX; ++s) xo[s] = x[s] = a.x0[(size_t)q * NX + s];
+  for (int k = 0; k < N; ++k) {
+    const double dt = M->dt;
+    double xn[NX];
+    for (int s = 0; s < 3; ++s) xn[s] = x[s] + dt * x[3 + s];
+    for (int s = 3; s < 9; ++s) xn[s] = x[s];
+    xn[5] += dt * x[12];
+    double sp, cp;
+    sincos(xr[k * NX + 11], &sp, &cp);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int r = 0; r < 3; ++r) {
+      double acc = 0.0;
+      for (int c = 0; c < 3; ++c) {
+        double mrc = 0.0;
+        for (int t = 0; t < 3; ++t) mrc += M->inv_inertia[r * 3 + t] * RzT[t * 3 + c];
+        acc += dt * mrc * x[6 + c];
+      }
+      xn[9 + r] = x[9 + r] + acc;
+    }
+    xn[12] = x[12];
+    for (int i = 0; i < L; ++i) {
+      if (!ct[k * L + i]) continue;
+      const double* f = uo + (k * L + i) * 3;
+      const double* p = ft + (k * L + i) * 3;
+      const double rx = p[0] - xr[k * NX + 0], ry = p[1] - xr[k * NX + 1], rz = p[2] - xr[k * NX + 2];
+      for (int d = 0; d < 3; ++d) xn[3 + d] += M->dt_over_m * f[d];
+      xn[6] += dt * (ry * f[2] - rz * f[1]);
+      xn[7] += dt * (rz * f[0] - rx * f[2]);
+      xn[8] += dt * (rx * f[1] - ry * f[0]);
+    }
+    for (int s = 0; s < NX; ++s) xo[(k + 1) * NX + s] = x[s] = xn[s];
+  }
+}
+
+__global__ __launch_bounds__(64) void k_expand(ExpandArgs a) {
+  const int q = blockIdx.x;
+  if (a.precision == CMPC_F64) expand_one<double>(a, q);
+  else expand_one<float>(a, q);
+}
+
+int launch_expand(const ExpandArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_expand, dim3(B), dim3(64), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ------------------------------------------------------------------------------------------ conversions
+__global__ void k_f32_to_f64(const float* in, double* out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = (double)in[i];
+}
+__global__ void k_f64_to_f32(const double* in, float* out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = (float)in[i];
+}
+static unsigned grid_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  return (unsigned)(b > 4096 ? 4096 : (b == 0 ? 1 : b));
+}
+int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(k_f32_to_f64, dim3(grid_for(n)), dim3(256), 0, stream, in, out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int launch_convert_f64_to_f32(const double* in, float* out, size_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(k_f64_to_f32, dim3(grid_for(n)), dim3(256), 0, stream, in, out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ------------------------------------------------------------------------------------------ generic OCP-QP
+// HpipmInterface::Impl::solve semantics (HpipmInterface.cpp:166-301) for equality-free stages: x0 eliminated
+// (b0 = f0 + A0 x0, r0 += S0 x0, :177-208), condensed to U-space, Cholesky-solved, states rolled out, non-finite
+// solution -> NAN_SOL (:290-295). One 256-thread workgroup per problem; column-major stage matrices.
+
+#define OCP_CM(M, ld, r, c) ((M)[(size_t)(c) * (ld) + (r)])
+
+__global__ __launch_bounds__(256) void k_ocp_solve(OcpArgs a) {
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int N = a.N, nx = a.nx, nU = a.nU, ldo = a.ldo;
+  const double* rec = a.rec + (size_t)q * a.rec_size;
+  const size_t* oA = a.offs;
+  const size_t* oB = a.offs + (N + 1);
+  const size_t* ob = a.offs + 2 * (N + 1);
+  const size_t* oQ = a.offs + 3 * (N + 1);
+  const size_t* oS = a.offs + 4 * (N + 1);
+  const size_t* oR = a.offs + 5 * (N + 1);
+  const size_t* oq = a.offs + 6 * (N + 1);
+  const size_t* orr = a.offs + 7 * (N + 1);
+  double* H = a.H + (size_t)q * ldo * ldo;
+  double* g = a.g + (size_t)q * ldo;
+  double* G = a.scratch + (size_t)q * (2 * (size_t)nx * ldo + 4 * nx);
+  double* QG = G + (size_t)nx * ldo;
+  double* xb = QG + (size_t)nx * ldo;
+  double* tmp = xb + nx;
+  double* xb2 = tmp + nx;
+  double* u = a.u + (size_t)q * nU;
+  double* x = a.x + (size_t)q * (N + 1) * nx;
+  __shared__ int s_cu[CMPC_OCP_MAX_N + 2];
+  __shared__ int s_flag;
+  __shared__ double s_l;
+  if (tid == 0) {
+    int c = 0;
+    for (int k = 0; k < N; ++k) {
+      s_cu[k] = c;
+      c += a.nu[k];
+    }
+    s_cu[N] = c;
+    s_flag = 0;
+  }
+  for (int i = tid; i < nU * nU; i += nth) H[(size_t)(i / nU) * ldo + i % nU] = 0.0;
+  for (int i = tid; i < nU; i += nth) g[i] = 0.0;
+  for (int i = tid; i < nx * nU; i += nth) G[(size_t)(i / nU) * ldo + i % nU] = 0.0;
+  for (int i = tid; i < nx; i += nth) xb[i] = a.x0[(size_t)q * nx + i];
+  __syncthreads();
+  for (int k = 0; k <= N; ++k) {
+    const int m = k < N ? a.nu[k] : 0;
+    const int c0 = s_cu[k];
+    const double* Q = rec + oQ[k];
+    const double* S = rec + oS[k];
+    const double* R = rec + oR[k];
+    const double* qv = rec + oq[k];
+    const double* rv = rec + orr[k];
+    if (k >= 1) {
+      for (int i = tid; i < nx; i += nth) {
+        double s = qv[i];
+        for (int j = 0; j < nx; ++j) s += OCP_CM(Q, nx, i, j) * xb[j];
+        tmp[i] = s;
+      }
+      for (int e = tid; e < nx * c0; e += nth) {
+        const int i = e / c0, b = e % c0;
+        double s = 0.0;
+        for (int j = 0; j < nx; ++j) s += OCP_CM(Q, nx, i, j) * G[(size_t)j * ldo + b];
+        QG[(size_t)i * ldo + b] = s;
+      }
+      __syncthreads();
+      for (int aa = tid; aa < c0; aa += nth) {
+        double s = 0.0;
+        for (int i = 0; i < nx; ++i) s += G[(size_t)i * ldo + aa] * tmp[i];
+        g[aa] += s;
+      }
+      for (int e = tid; e < c0 * c0; e += nth) {
+        const int aa = e / c0, b = e % c0;
+        double s = 0.0;
+        for (int i = 0; i < nx; ++i) s += G[(size_t)i * ldo + aa] * QG[(size_t)i * ldo + b];
+        H[(size_t)aa * ldo + b] += s;
+      }
+      __syncthreads();
+    }
+    if (m > 0) {
+      for (int aa = tid; aa < m; aa += nth) {
+        double s = rv[aa];
+        for (int j = 0; j < nx; ++j) s += OCP_CM(S, m, aa, j) * xb[j];
+        g[c0 + aa] += s;
+      }
+      for (int e = tid; e < m * m; e += nth) {
+        const int aa = e / m, b = e % m;
+        H[(size_t)(c0 + aa) * ldo + c0 + b] += OCP_CM(R, m, aa, b);
+      }
+      if (k >= 1)
+        for (int e = tid; e < m * c0; e += nth) {
+          const int aa = e / c0, b = e % c0;
+          double s = 0.0;
+          for (int j = 0; j < nx; ++j) s += OCP_CM(S, m, aa, j) * G[(size_t)j * ldo + b];
+          H[(size_t)(c0 + aa) * ldo + b] += s;
+          H[(size_t)b * ldo + c0 + aa] += s;
+        }
+      __syncthreads();
+    }
+    if (k < N) {
+      const double* A = rec + oA[k];
+      const double* Bm = rec + oB[k];
+      const double* bv = rec + ob[k];
+      const int cn = c0 + m;
+      for (int e = tid; e < nx * cn; e += nth) {
+        const int i = e / cn, b = e % cn;
+        double s = b >= c0 ? OCP_CM(Bm, nx, i, b - c0) : 0.0;
+        for (int j = 0; j < nx; ++j) s += OCP_CM(A, nx, i, j) * G[(size_t)j * ldo + b];
+        QG[(size_t)i * ldo + b] = s;
+      }
+      for (int i = tid; i < nx; i += nth) {
+        double s = bv[i];
+        for (int j = 0; j < nx; ++j) s += OCP_CM(A, nx, i, j) * xb[j];
+        xb2[i] = s;
+      }
+      __syncthreads();
+      for (int e = tid; e < nx * cn; e += nth) G[(size_t)(e / cn) * ldo + e % cn] = QG[(size_t)(e / cn) * ldo + e % cn];
+      for (int i = tid; i < nx; i += nth) xb[i] = xb2[i];
+      __syncthreads();
+    }
+  }
+  // Cholesky (right-looking, lower) + triangular solves for u = -H^{-1} g
+  for (int k = 0; k < nU; ++k) {
+    if (tid == 0) {
+      const double d = H[(size_t)k * ldo + k];
+      if (!(d > 0.0)) s_flag = 1;
+      s_l = sqrt(d);
+      H[(size_t)k * ldo + k] = s_l;
+    }
+    __syncthreads();
+    const double l = s_l;
+    for (int i = k + 1 + tid; i < nU; i += nth) H[(size_t)i * ldo + k] /= l;
+    __syncthreads();
+    const int rem = nU - k - 1;
+    for (int e = tid; e < rem * rem; e += nth) {
+      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+      if (j <= i) H[(size_t)i * ldo + j] -= H[(size_t)i * ldo + k] * H[(size_t)j * ldo + k];
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < nU; i += nth) u[i] = -g[i];
+  __syncthreads();
+  for (int k = 0; k < nU; ++k) {
+    if (tid == 0) u[k] /= H[(size_t)k * ldo + k];
+    __syncthreads();
+    for (int i = k + 1 + tid; i < nU; i += nth) u[i] -= H[(size_t)i * ldo + k] * u[k];
+    __syncthreads();
+  }
+  for (int k = nU - 1; k >= 0; --k) {
+    if (tid == 0) u[k] /= H[(size_t)k * ldo + k];
+    __syncthreads();
+    for (int i = tid; i < k; i += nth) u[i] -= H[(size_t)k * ldo + i] * u[k];
+    __syncthreads();
+  }
+  // rollout x_{k+1} = A_k x_k + B_k u_k + b_k (x_0 = x0, HpipmInterface.cpp:303-315)
+  for (int i = tid; i < nx; i += nth) x[i] = a.x0[(size_t)q * nx + i];
+  __syncthreads();
+  for (int k = 0; k < N; ++k) {
+    const double* A = rec + oA[k];
+    const double* Bm = rec + oB[k];
+    const double* bv = rec + ob[k];
+    const int c0 = s_cu[k], m = a.nu[k];
+    for (int i = tid; i < nx; i += nth) {
+      double s = bv[i];
+      for (int j = 0; j < nx; ++j) s += OCP_CM(A, nx, i, j) * x[k * nx + j];
+      for (int b = 0; b < m; ++b) s += OCP_CM(Bm, nx, i, b) * u[c0 + b];
+      x[(k + 1) * nx + i] = s;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int st = s_flag ? CMPC_NAN_SOL : CMPC_SUCCESS;
+    for (int i = 0; i < nU; ++i)
+      if (!isfinite(u[i])) st = CMPC_NAN_SOL;
+    for (int i = 0; i < (N + 1) * nx; ++i)
+      if (!isfinite(x[i])) st = CMPC_NAN_SOL;
+    a.status[q] = st;
+  }
+}
+
+int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_ocp_solve, dim3(B), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace cmpc
+
+namespace cmpc {
+
+// ------------------------------------------------------------------------------------------ test-hook layouts
+template <typename T>
+__global__ __launch_bounds__(256) void k_unpack_qp(const T* H_ws, const T* g_ws, const int* nvar, int ld, double* H,
+                                                   double* g) {
+  const int q = blockIdx.x;
+  const int n = nvar[q];
+  const int np = ipm_class(n);
+  const T* hq = H_ws + (size_t)q * ld * ld;
+  double* ho = H + (size_t)q * ld * ld;
+  for (int e = threadIdx.x; e < ld * ld; e += blockDim.x) {
+    const int r = e / ld, c = e % ld;
+    ho[e] = (r < np && c < np) ? (double)hq[r * np + c] : (r == c ? 1.0 : 0.0);
+  }
+  for (int i = threadIdx.x; i < ld; i += blockDim.x) g[(size_t)q * ld + i] = i < np ? (double)g_ws[(size_t)q * ld + i] : 0.0;
+}
+
+int launch_unpack_qp(const void* H_ws, const void* g_ws, const int* nvar, int precision, int ld, double* H, double* g,
+                     int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (precision == CMPC_F64)
+    hipLaunchKernelGGL(k_unpack_qp<double>, dim3(B), dim3(256), 0, stream, (const double*)H_ws, (const double*)g_ws,
+                       nvar, ld, H, g);
+  else
+    hipLaunchKernelGGL(k_unpack_qp<float>, dim3(B), dim3(256), 0, stream, (const float*)H_ws, (const float*)g_ws, nvar,
+                       ld, H, g);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_qp(const double* H, const double* g, const double* tri_mu,
+                                                 const double* tri_lo, const double* tri_hi, const int* nvar_in, int ld,
+                                                 T* H_ws, T* g_ws, T* mu_ws, T* lo_ws, T* hi_ws, int* nvar_ws,
+                                                 int* status_ws) {
+  const int q = blockIdx.x;
+  const int n = nvar_in[q];
+  const bool ok = n >= 0 && n <= ld && n <= CMPC_IPM_MAX_N && n % 3 == 0;
+  const int np = ipm_class(n);
+  const int nt = ld / 3;
+  if (ok) {
+    for (int e = threadIdx.x; e < np * np; e += blockDim.x) {
+      const int r = e / np, c = e % np;
+      T v;
+      if (r < n && c < n) v = (T)H[(size_t)q * ld * ld + (size_t)r * ld + c];
+      else v = r == c ? T(1) : T(0);
+      H_ws[(size_t)q * ld * ld + e] = v;
+    }
+    for (int i = threadIdx.x; i < ld; i += blockDim.x) g_ws[(size_t)q * ld + i] = i < n ? (T)g[(size_t)q * ld + i] : T(0);
+    for (int t = threadIdx.x; t < nt; t += blockDim.x) {
+      mu_ws[(size_t)q * nt + t] = (T)tri_mu[(size_t)q * nt + t];
+      for (int r = 0; r < 5; ++r) {
+        lo_ws[((size_t)q * nt + t) * 5 + r] = (T)tri_lo[((size_t)q * nt + t) * 5 + r];
+        hi_ws[((size_t)q * nt + t) * 5 + r] = (T)tri_hi[((size_t)q * nt + t) * 5 + r];
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    nvar_ws[q] = ok ? n : 0;
+    status_ws[q] = ok ? CMPC_SUCCESS : CMPC_TOO_LARGE;
+  }
+}
+
+int launch_pack_qp(const double* H, const double* g, const double* tri_mu, const double* tri_lo, const double* tri_hi,
+                   const int* nvar_in, int precision, int ld, void* H_ws, void* g_ws, void* mu_ws, void* lo_ws,
+                   void* hi_ws, int* nvar_ws, int* status_ws, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (precision == CMPC_F64)
+    hipLaunchKernelGGL(k_pack_qp<double>, dim3(B), dim3(256), 0, stream, H, g, tri_mu, tri_lo, tri_hi, nvar_in, ld,
+                       (double*)H_ws, (double*)g_ws, (double*)mu_ws, (double*)lo_ws, (double*)hi_ws, nvar_ws,
+                       status_ws);
+  else
+    hipLaunchKernelGGL(k_pack_qp<float>, dim3(B), dim3(256), 0, stream, H, g, tri_mu, tri_lo, tri_hi, nvar_in, ld,
+                       (float*)H_ws, (float*)g_ws, (float*)mu_ws, (float*)lo_ws, (float*)hi_ws, nvar_ws, status_ws);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace cmpc

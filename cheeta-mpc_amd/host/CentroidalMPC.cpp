@@ -1,0 +1,112 @@
+// CentroidalMPC.cpp — host mirror of the reference CentroidalMPC (CentroidalMPC.cpp:21-370) over the C ABI.
+#include "cheeta_mpc/CentroidalMPC.h"
+
+#include <cassert>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+namespace {
+void check(int r, const char* what) {
+  if (r != CMPC_OK) throw std::runtime_error(std::string("[CentroidalMPC] ") + what + ": " + cmpc_error_string(r));
+}
+}  // namespace
+
+CentroidalMPC::CentroidalMPC(double mass, int num_legs, int predict_horizon, double time_step, const VectorXd& weights,
+                             const VectorXd& mu, IPOPT_SOLVER /*ipopt_solver*/, int precision, int max_batch)
+    : precision_(precision), max_batch_(max_batch) {
+  // CentroidalMPC.cpp:24-25
+  if (!(mass > 0 && num_legs > 0 && predict_horizon > 0)) throw std::invalid_argument("[CentroidalMPC] bad arguments");
+  if ((int)mu.size() != num_legs) throw std::invalid_argument("[CentroidalMPC] mu.size() != num_legs");
+  if (num_legs != CMPC_MAX_LEGS) throw std::invalid_argument("[CentroidalMPC] this build supports num_legs == 4");
+  if ((int)weights.size() != (num_legs + 1) * 9) throw std::invalid_argument("[CentroidalMPC] weights size");
+  cmpc_model_default(&model_, predict_horizon);
+  model_.mass = mass;
+  model_.dt = time_step;
+  model_.n_legs = num_legs;
+  for (int i = 0; i < num_legs; ++i) model_.mu[i] = mu[(size_t)i];
+  for (int i = 0; i < CMPC_NUM_WEIGHTS; ++i) model_.weights[i] = weights[(size_t)i];
+  model_.force_ub[4] = mass * 9.81 * num_legs;  // CentroidalMPC.cpp:183
+  cmpc_settings_default(&settings_);
+  current_time_ = 0.0;
+}
+
+CentroidalMPC::~CentroidalMPC() {
+  if (ctx_) cmpc_destroy(ctx_);
+}
+
+void CentroidalMPC::SetupMPC() {
+  if (ctx_) cmpc_destroy(ctx_);
+  ctx_ = nullptr;
+  check(cmpc_create(&model_, &settings_, precision_, max_batch_, nullptr, &ctx_), "cmpc_create");
+}
+
+void CentroidalMPC::UpdateWeights(const VectorXd& weights) {
+  if ((int)weights.size() != CMPC_NUM_WEIGHTS) throw std::invalid_argument("[CentroidalMPC] weights size");
+  for (int i = 0; i < CMPC_NUM_WEIGHTS; ++i) model_.weights[i] = weights[(size_t)i];
+  if (ctx_) check(cmpc_set_model(ctx_, &model_), "cmpc_set_model");
+}
+
+void CentroidalMPC::setSettings(const cmpc_settings& s) {
+  settings_ = s;
+  if (ctx_) check(cmpc_set_settings(ctx_, &settings_), "cmpc_set_settings");
+}
+
+void CentroidalMPC::PackRecord(const VectorXd& state, const VectorXd& des_state, const VectorXd& des_inputs,
+                               VectorXd& x0, VectorXd& xref, VectorXd& foot, std::vector<uint8_t>& contact) const {
+  const int N = model_.N, L = model_.n_legs;
+  if ((int)state.size() < 9 + 3 * L || (int)des_state.size() < 9 * (N + 1) || (int)des_inputs.size() < L * (4 * N + 3))
+    throw std::invalid_argument("[CentroidalMPC] input vector sizes");
+  x0.assign(CMPC_NX, 0.0);
+  for (int j = 0; j < 9; ++j) x0[(size_t)j] = state[(size_t)j];  // c, v, L (CentroidalMPC.cpp:284-286)
+  x0[12] = -9.81;
+  xref.assign((size_t)(N + 1) * CMPC_NX, 0.0);
+  for (int k = 0; k <= N; ++k) {
+    for (int b = 0; b < 3; ++b)  // des_com_pos | des_com_vel | des_angular_momentum, 3x(N+1) column-major (:297-299)
+      for (int d = 0; d < 3; ++d) xref[(size_t)k * CMPC_NX + 3 * b + d] = des_state[(size_t)b * 3 * (N + 1) + 3 * k + d];
+    xref[(size_t)k * CMPC_NX + 12] = -9.81;
+  }
+  foot.assign((size_t)(N + 1) * L * 3, 0.0);
+  contact.assign((size_t)N * L, 0);
+  for (int i = 0; i < L; ++i) {
+    const size_t base = (size_t)i * (4 * N + 3);  // [contact_enable (N) | des_foot_pos 3x(N+1)] (:315-317)
+    for (int k = 0; k < N; ++k) contact[(size_t)k * L + i] = des_inputs[base + k] > 0 ? 1 : 0;
+    for (int k = 0; k <= N; ++k)
+      for (int d = 0; d < 3; ++d) foot[((size_t)k * L + i) * 3 + d] = des_inputs[base + N + 3 * k + d];
+  }
+}
+
+CentroidalMPC::VectorXd CentroidalMPC::UpdateMPC(const VectorXd& state, const VectorXd& des_state,
+                                                 const VectorXd& des_inputs) {
+  if (!ctx_) throw std::runtime_error("[CentroidalMPC] SetupMPC() not called");
+  const int N = model_.N, L = model_.n_legs;
+  VectorXd x0, xref, foot;
+  std::vector<uint8_t> contact;
+  PackRecord(state, des_state, des_inputs, x0, xref, foot, contact);
+  for (int k = 0; k < N; ++k) {  // CentroidalMPC.cpp:326-330
+    int ns = 0;
+    for (int i = 0; i < L; ++i) ns += contact[(size_t)k * L + i];
+    if (ns <= 0) throw std::runtime_error("mpc table invalid");
+  }
+  VectorXd u((size_t)N * CMPC_NU);
+  int status = -1, iters = 0;
+  check(cmpc_solve_batch_host(ctx_, 1, x0.data(), xref.data(), foot.data(), contact.data(), u.data(), nullptr, &status,
+                              &iters),
+        "cmpc_solve_batch_host");
+  last_status_ = status;
+  last_iters_ = iters;
+  current_time_ += model_.dt;  // CentroidalMPC.cpp:368
+  // per leg: contact_force_i as 3 x N column-major (controller_ output order)
+  VectorXd out((size_t)L * 3 * N);
+  for (int i = 0; i < L; ++i)
+    for (int k = 0; k < N; ++k)
+      for (int d = 0; d < 3; ++d) out[(size_t)i * 3 * N + 3 * k + d] = u[((size_t)k * L + i) * 3 + d];
+  return out;
+}
+
+int CentroidalMPC::UpdateMPCBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                                  const uint8_t* d_contact, double* d_u, double* d_x, int* d_status, int* d_iters,
+                                  void* stream) {
+  if (!ctx_) return CMPC_ERR_ARG;
+  return cmpc_solve_batch(ctx_, B, d_x0, d_xref, d_foot, d_contact, d_u, d_x, d_status, d_iters, stream);
+}

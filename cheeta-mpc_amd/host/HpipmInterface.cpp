@@ -1,0 +1,129 @@
+// HpipmInterface.cpp — ocs2::HpipmInterface mirror (reference HpipmInterface.cpp:86-554) on the MI355X engine.
+#include "hpipm_catkin/HpipmInterface.h"
+
+#include <cmath>
+#include <cstdio>
+#include <string>
+
+namespace ocs2 {
+namespace hpipm_interface {
+
+bool operator==(const OcpSize& l, const OcpSize& r) noexcept {  // OcpSize.cpp:35-47
+  return l.numStages == r.numStages && l.numInputs == r.numInputs && l.numStates == r.numStates &&
+         l.numInputBoxConstraints == r.numInputBoxConstraints && l.numStateBoxConstraints == r.numStateBoxConstraints &&
+         l.numIneqConstraints == r.numIneqConstraints && l.numInputBoxSlack == r.numInputBoxSlack &&
+         l.numStateBoxSlack == r.numStateBoxSlack && l.numIneqSlack == r.numIneqSlack;
+}
+
+OcpSize extractSizesFromProblem(const std::vector<VectorFunctionLinearApproximation>& dynamics,
+                                const std::vector<ScalarFunctionQuadraticApproximation>& cost,
+                                const std::vector<VectorFunctionLinearApproximation>* constraints) {
+  (void)cost;  // OcpSize.cpp:49-75
+  const int N = (int)dynamics.size();
+  OcpSize s(N);
+  for (int k = 0; k < N; ++k) {
+    s.numStates[(size_t)k] = dynamics[(size_t)k].dfdx.cols();
+    s.numInputs[(size_t)k] = dynamics[(size_t)k].dfdu.cols();
+  }
+  s.numStates[(size_t)N] = N > 0 ? dynamics[(size_t)N - 1].dfdx.rows() : 0;
+  s.numInputs[(size_t)N] = 0;
+  if (constraints)
+    for (int k = 0; k <= N; ++k) s.numIneqConstraints[(size_t)k] = (*constraints)[(size_t)k].f.size();
+  return s;
+}
+
+}  // namespace hpipm_interface
+
+class HpipmInterface::Impl {
+ public:
+  Impl(OcpSize s, Settings st) : settings_(st) { initializeMemory(std::move(s)); }
+  void initializeMemory(OcpSize s) {
+    s.numStates[0] = 0;  // x0 eliminated (HpipmInterface.cpp:93-95)
+    size_ = std::move(s);
+  }
+  hpipm_status solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dyn,
+                     std::vector<ScalarFunctionQuadraticApproximation>& cost,
+                     std::vector<VectorFunctionLinearApproximation>* constraints, vector_array_t& xs, vector_array_t& us,
+                     bool verbose) {
+    const int N = size_.numStages;
+    // verifySizes (HpipmInterface.cpp:146-164)
+    if ((int)dyn.size() != N)
+      throw std::runtime_error("[HpipmInterface] Inconsistent size of dynamics: " + std::to_string(dyn.size()) +
+                               " with " + std::to_string(N) + " number of stages.");
+    if ((int)cost.size() != N + 1)
+      throw std::runtime_error("[HpipmInterface] Inconsistent size of cost: " + std::to_string(cost.size()) + " with " +
+                               std::to_string(N + 1) + " nodes.");
+    if (constraints != nullptr) {
+      if ((int)constraints->size() != N + 1)
+        throw std::runtime_error("[HpipmInterface] Inconsistent size of constraints: " +
+                                 std::to_string(constraints->size()) + " with " + std::to_string(N + 1) + " nodes.");
+      for (const auto& c : *constraints)
+        if (c.f.size() > 0) throw std::runtime_error("[HpipmInterface] equality-constrained stages are not supported");
+    }
+    const int nx = x0.size();
+    std::vector<int> nu((size_t)N);
+    for (int k = 0; k < N; ++k) {
+      nu[(size_t)k] = dyn[(size_t)k].dfdu.cols();
+      if (dyn[(size_t)k].dfdx.rows() != nx || dyn[(size_t)k].dfdx.cols() != nx)
+        throw std::runtime_error("[HpipmInterface] constant state dimension required");
+    }
+    const size_t rs = cmpc_ocp_record_size(N, nx, nu.data());
+    std::vector<double> rec(rs);
+    size_t o = 0;
+    auto put = [&](const double* p, size_t n) {
+      for (size_t i = 0; i < n; ++i) rec[o + i] = p ? p[i] : 0.0;
+      o += n;
+    };
+    for (int k = 0; k < N; ++k) {
+      const auto& d = dyn[(size_t)k];
+      put(d.dfdx.data(), (size_t)nx * nx);
+      put(d.dfdu.data(), (size_t)nx * nu[(size_t)k]);
+      put(d.f.data(), (size_t)nx);
+    }
+    for (int k = 0; k <= N; ++k) {
+      const auto& c = cost[(size_t)k];
+      const size_t m = k < N ? (size_t)nu[(size_t)k] : 0;
+      put(c.dfdxx.data(), (size_t)nx * nx);
+      put(m ? c.dfdux.data() : nullptr, m * nx);
+      put(m ? c.dfduu.data() : nullptr, m * m);
+      put(c.dfdx.data(), (size_t)nx);
+      put(m ? c.dfdu.data() : nullptr, m);
+    }
+    int nU = 0;
+    for (int v : nu) nU += v;
+    std::vector<double> x((size_t)(N + 1) * nx), u((size_t)(nU > 0 ? nU : 1));
+    int status = -1;
+    const int r = cmpc_ocp_solve_batch_host(1, N, nx, nu.data(), x0.data(), rec.data(), x.data(), u.data(), &status);
+    if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device solve failed: ") + cmpc_error_string(r));
+    xs.assign((size_t)N + 1, vector_t());
+    for (int k = 0; k <= N; ++k) {
+      xs[(size_t)k].resize(nx);
+      for (int i = 0; i < nx; ++i) xs[(size_t)k][i] = k == 0 ? x0[i] : x[(size_t)k * nx + i];
+    }
+    us.assign((size_t)N, vector_t());
+    int off = 0;
+    for (int k = 0; k < N; ++k) {
+      us[(size_t)k].resize(nu[(size_t)k]);
+      for (int i = 0; i < nu[(size_t)k]; ++i) us[(size_t)k][i] = u[(size_t)off + i];
+      off += nu[(size_t)k];
+    }
+    if (verbose) std::fprintf(stderr, "\n=== HPIPM (MI355X engine) ===\nstatus %d (%s)\n", status, cmpc_status_string(status));
+    return (hpipm_status)status;
+  }
+
+ private:
+  Settings settings_;
+  OcpSize size_;
+};
+
+HpipmInterface::HpipmInterface(OcpSize s, const Settings& st) : pImpl_(new Impl(std::move(s), st)) {}
+HpipmInterface::~HpipmInterface() = default;
+void HpipmInterface::resize(OcpSize s) { pImpl_->initializeMemory(std::move(s)); }
+hpipm_status HpipmInterface::solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dynamics,
+                                   std::vector<ScalarFunctionQuadraticApproximation>& cost,
+                                   std::vector<VectorFunctionLinearApproximation>* constraints, vector_array_t& x,
+                                   vector_array_t& u, bool verbose) {
+  return pImpl_->solve(x0, dynamics, cost, constraints, x, u, verbose);
+}
+
+}  // namespace ocs2

@@ -1,0 +1,288 @@
+"""ctypes bindings of the cheeta-mpc-amd C ABI (include/cmpc/cmpc.h) plus minimal HIP device-memory plumbing.
+
+The product is libcmpc.so (HIP kernels for gfx950 + the C ABI). This module only marshals arguments: it never
+computes a solution itself and raises if the native library is missing, so nothing here can silently fall back to
+a CPU path. Device memory is managed with the HIP runtime directly (libamdhip64, the one libcmpc.so links); PyTorch
+is not needed on the solve path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.abspath(os.path.join(_HERE, "..", ".."))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libcmpc.so")
+
+NX, NU, NL = 13, 12, 4
+F64, F32 = 0, 1
+STATUS = {0: "SUCCESS", 1: "MAX_ITER", 2: "MIN_STEP", 3: "NAN_SOL", 4: "INCONS_EQ", 5: "INVALID_CONTACT",
+          6: "TOO_LARGE"}
+
+# CentoidMPCTest.cpp:19-33
+TEST_WEIGHTS = [1, 1, 100, 0.5, 0.5, 0, 2, 2, 8,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
+                0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1]
+
+
+class Model(C.Structure):
+    _fields_ = [("N", C.c_int), ("n_legs", C.c_int), ("mass", C.c_double), ("dt", C.c_double),
+                ("inertia", C.c_double * 9), ("mu", C.c_double * 4), ("weights", C.c_double * 45),
+                ("force_ub", C.c_double * 5), ("theta_weights", C.c_double * 3)]
+
+
+class Settings(C.Structure):
+    _fields_ = [("hpipm_mode", C.c_int), ("iter_max", C.c_int), ("alpha_min", C.c_double), ("mu0", C.c_double),
+                ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double),
+                ("tol_comp", C.c_double), ("reg_prim", C.c_double), ("warm_start", C.c_int),
+                ("pred_corr", C.c_int), ("ric_alg", C.c_int)]
+
+
+_lib = None
+_hip = None
+
+
+def lib():
+    """Load libcmpc.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libcmpc.so not found at {LIB_PATH}; run `make -C cheeta-mpc_amd` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    vp, d, i, u8 = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
+    L.cmpc_settings_default.argtypes = [P(Settings)]
+    L.cmpc_settings_default.restype = None
+    L.cmpc_model_default.argtypes = [P(Model), C.c_int]
+    L.cmpc_model_default.restype = None
+    L.cmpc_memsize.argtypes = [P(Model), C.c_int, C.c_int]
+    L.cmpc_memsize.restype = C.c_size_t
+    L.cmpc_create.argtypes = [P(Model), P(Settings), C.c_int, C.c_int, vp, P(vp)]
+    L.cmpc_destroy.argtypes = [vp]
+    L.cmpc_set_settings.argtypes = [vp, P(Settings)]
+    L.cmpc_set_model.argtypes = [vp, P(Model)]
+    L.cmpc_get_model.argtypes = [vp, P(Model)]
+    L.cmpc_ctx_ld.argtypes = [vp]
+    L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
+    L.cmpc_solve_batch_host.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i]
+    L.cmpc_condense_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
+    L.cmpc_qp_solve_batch.argtypes = [vp, C.c_int, d, d, i, d, d, d, d, i, i, vp]
+    L.cmpc_generate_batch.argtypes = [P(Model), C.c_uint64, C.c_int64, C.c_int, C.c_int, d, d, d, u8, vp]
+    L.cmpc_ocp_record_size.argtypes = [C.c_int, C.c_int, i]
+    L.cmpc_ocp_record_size.restype = C.c_size_t
+    L.cmpc_ocp_solve_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, i]
+    L.cmpc_status_string.argtypes = [C.c_int]
+    L.cmpc_status_string.restype = C.c_char_p
+    L.cmpc_error_string.argtypes = [C.c_int]
+    L.cmpc_error_string.restype = C.c_char_p
+    L.cmpc_device_info.argtypes = [P(C.c_int), P(C.c_int), C.c_char_p, C.c_int]
+    L.cmpc_version.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def hip():
+    """HIP runtime (the libamdhip64 libcmpc.so is linked against)."""
+    global _hip
+    if _hip is None:
+        lib()
+        H = C.CDLL("libamdhip64.so.7", mode=C.RTLD_GLOBAL)
+        H.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        H.hipFree.argtypes = [C.c_void_p]
+        H.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        H.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+        H.hipDeviceSynchronize.argtypes = []
+        H.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+        H.hipStreamSynchronize.argtypes = [C.c_void_p]
+        H.hipStreamDestroy.argtypes = [C.c_void_p]
+        H.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+        H.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+        H.hipEventSynchronize.argtypes = [C.c_void_p]
+        H.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+        H.hipEventDestroy.argtypes = [C.c_void_p]
+        H.hipGetDeviceCount.argtypes = [C.POINTER(C.c_int)]
+        H.hipSetDevice.argtypes = [C.c_int]
+        H.hipGetErrorString.restype = C.c_char_p
+        _hip = H
+    return _hip
+
+
+def _chk(r, what):
+    if r != 0:
+        raise RuntimeError(f"{what} failed: {r} {lib().cmpc_error_string(r).decode() if r < 0 else ''}")
+
+
+def _hchk(r, what):
+    if r != 0:
+        raise RuntimeError(f"{what} failed: hipError {r} {hip().hipGetErrorString(r).decode()}")
+
+
+def device_count():
+    n = C.c_int(0)
+    if hip().hipGetDeviceCount(C.byref(n)) != 0:
+        return 0
+    return n.value
+
+
+class DeviceArray:
+    """A device allocation with a numpy shape/dtype (H2D/D2H via hipMemcpy)."""
+
+    def __init__(self, shape, dtype):
+        self.shape = tuple(int(s) for s in shape)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        self.ptr = C.c_void_p()
+        _hchk(hip().hipMalloc(C.byref(self.ptr), max(self.nbytes, 1)), "hipMalloc")
+
+    @classmethod
+    def from_host(cls, a):
+        a = np.ascontiguousarray(a)
+        d = cls(a.shape, a.dtype)
+        d.upload(a)
+        return d
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        assert a.nbytes == self.nbytes
+        _hchk(hip().hipMemcpy(self.ptr, a.ctypes.data_as(C.c_void_p), self.nbytes, 1), "hipMemcpy H2D")
+
+    def zero(self):
+        _hchk(hip().hipMemset(self.ptr, 0, self.nbytes), "hipMemset")
+
+    def host(self):
+        out = np.empty(self.shape, dtype=self.dtype)
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        _hchk(hip().hipMemcpy(out.ctypes.data_as(C.c_void_p), self.ptr, self.nbytes, 2), "hipMemcpy D2H")
+        return out
+
+    def __del__(self):
+        try:
+            if self.ptr and _hip is not None:
+                _hip.hipFree(self.ptr)
+        except Exception:
+            pass
+
+
+def default_model(N=10):
+    m = Model()
+    lib().cmpc_model_default(C.byref(m), N)
+    return m
+
+
+def default_settings(**kw):
+    s = Settings()
+    lib().cmpc_settings_default(C.byref(s))
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+class Engine:
+    """One cmpc context (device workspace for max_batch QPs of horizon model.N)."""
+
+    def __init__(self, model, settings=None, precision=F64, max_batch=4096):
+        self.model = model
+        self.settings = settings or default_settings()
+        self.precision = precision
+        self.max_batch = max_batch
+        self.ctx = C.c_void_p()
+        _chk(lib().cmpc_create(C.byref(model), C.byref(self.settings), precision, max_batch, None,
+                               C.byref(self.ctx)), "cmpc_create")
+        self.ld = lib().cmpc_ctx_ld(self.ctx)
+
+    def close(self):
+        if self.ctx:
+            lib().cmpc_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_settings(self, s):
+        self.settings = s
+        _chk(lib().cmpc_set_settings(self.ctx, C.byref(s)), "cmpc_set_settings")
+
+    # ---- device-pointer entry points (async on stream)
+    def solve_device(self, B, x0, xref, foot, contact, u, x, status, iters, stream=None):
+        _chk(lib().cmpc_solve_batch(self.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, u.ptr,
+                                    x.ptr if x is not None else None, status.ptr,
+                                    iters.ptr if iters is not None else None, stream), "cmpc_solve_batch")
+
+    # ---- host convenience
+    def solve(self, x0, xref, foot, contact, want_x=True):
+        B = x0.shape[0]
+        N = self.model.N
+        d = {k: DeviceArray.from_host(v) for k, v in
+             dict(x0=np.asarray(x0, np.float64), xref=np.asarray(xref, np.float64),
+                  foot=np.asarray(foot, np.float64), contact=np.asarray(contact, np.uint8)).items()}
+        u = DeviceArray((B, N, NL, 3), np.float64)
+        x = DeviceArray((B, N + 1, NX), np.float64) if want_x else None
+        st = DeviceArray((B,), np.int32)
+        it = DeviceArray((B,), np.int32)
+        self.solve_device(B, d["x0"], d["xref"], d["foot"], d["contact"], u, x, st, it)
+        return u.host(), (x.host() if want_x else None), st.host(), it.host()
+
+    def condense(self, x0, xref, foot, contact):
+        B = x0.shape[0]
+        d = [DeviceArray.from_host(np.asarray(a, t)) for a, t in
+             ((x0, np.float64), (xref, np.float64), (foot, np.float64), (contact, np.uint8))]
+        H = DeviceArray((B, self.ld, self.ld), np.float64)
+        g = DeviceArray((B, self.ld), np.float64)
+        n = DeviceArray((B,), np.int32)
+        st = DeviceArray((B,), np.int32)
+        _chk(lib().cmpc_condense_batch(self.ctx, B, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, H.ptr, g.ptr, n.ptr,
+                                       st.ptr, None), "cmpc_condense_batch")
+        return H.host(), g.host(), n.host(), st.host()
+
+    def qp_solve(self, H, g, n, mu, lo, hi):
+        B = H.shape[0]
+        ld = self.ld
+        assert H.shape == (B, ld, ld)
+        d = [DeviceArray.from_host(np.ascontiguousarray(a, t)) for a, t in
+             ((H, np.float64), (g, np.float64), (n, np.int32), (mu, np.float64), (lo, np.float64), (hi, np.float64))]
+        u = DeviceArray((B, ld), np.float64)
+        st = DeviceArray((B,), np.int32)
+        it = DeviceArray((B,), np.int32)
+        _chk(lib().cmpc_qp_solve_batch(self.ctx, B, *[a.ptr for a in d], u.ptr, st.ptr, it.ptr, None),
+             "cmpc_qp_solve_batch")
+        return u.host(), st.host(), it.host()
+
+
+def generate_device(model, seed, B, gait=0, offset=0, stream=None):
+    N = model.N
+    x0 = DeviceArray((B, NX), np.float64)
+    xref = DeviceArray((B, N + 1, NX), np.float64)
+    foot = DeviceArray((B, N + 1, NL, 3), np.float64)
+    contact = DeviceArray((B, N, NL), np.uint8)
+    _chk(lib().cmpc_generate_batch(C.byref(model), seed, offset, B, gait, x0.ptr, xref.ptr, foot.ptr, contact.ptr,
+                                   stream), "cmpc_generate_batch")
+    return x0, xref, foot, contact
+
+
+def ocp_solve(N, nx, nu, x0, rec):
+    """Batched generic OCP-QP (HpipmInterface semantics) on the device; x0 [B,nx], rec [B,record]."""
+    x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)
+    rec = np.ascontiguousarray(np.atleast_2d(rec), np.float64)
+    B = x0.shape[0]
+    nua = np.ascontiguousarray(nu, np.int32)
+    nU = int(nua.sum())
+    x = np.zeros((B, N + 1, nx))
+    u = np.zeros((B, max(nU, 1)))
+    st = np.zeros(B, np.int32)
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _chk(lib().cmpc_ocp_solve_batch_host(B, N, nx, vp(nua), vp(x0), vp(rec), vp(x), vp(u), vp(st)),
+         "cmpc_ocp_solve_batch_host")
+    return x, u[:, :nU], st
+
+
+def device_info():
+    cu, clk = C.c_int(0), C.c_int(0)
+    arch = C.create_string_buffer(64)
+    _chk(lib().cmpc_device_info(C.byref(cu), C.byref(clk), arch, 64), "cmpc_device_info")
+    return cu.value, clk.value, arch.value.decode()

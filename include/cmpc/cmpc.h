@@ -158,6 +158,12 @@ size_t cmpc_ocp_record_size(int N, int nx, const int* nu);
 int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
                               double* u, int* status);
 
+/* Per-stage device timing with HIP events recorded on the solve stream (used by bench.py for the roofline):
+ * after cmpc_profile_begin, each cmpc_solve_batch records events around its three stages (condense, IPM, expand);
+ * cmpc_profile_end synchronises and returns the summed milliseconds per stage and the number of calls. */
+int cmpc_profile_begin(cmpc_ctx* ctx, int max_calls);
+int cmpc_profile_end(cmpc_ctx* ctx, double* ms_condense, double* ms_ipm, double* ms_expand, int* calls);
+
 /* Human-readable names. */
 const char* cmpc_status_string(int status);
 const char* cmpc_error_string(int err);

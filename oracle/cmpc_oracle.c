@@ -303,8 +303,39 @@ static inline void pyr_applyT(double mu, const double* w, double* f) {
 }
 
 typedef struct ipm_ws {
-  double *K, *rg, *rhs, *du, *cu, *cdu, *tl, *tu, *ll, *lu, *rl, *ru, *dtl, *dtu, *dll, *dlu, *rml, *rmu, *w;
+  double *invd, *K, *rg, *rhs, *du, *cu, *cdu, *tl, *tu, *ll, *lu, *rl, *ru, *dtl, *dtu, *dll, *dlu, *rml, *rmu, *w;
 } ipm_ws;
+
+/* Cholesky with the kernels' pivot guard: a pivot <= 1e-200 gets inverse 0 (direction dropped, BLASFEO-style).
+ * Stores 1/L_ii in invd. Returns -1 only on a NaN pivot. */
+static int ipm_cholesky(int n, double* A, double* invd) {
+  for (int k = 0; k < n; ++k) {
+    double d = A[k * n + k];
+    for (int j = 0; j < k; ++j) d -= A[k * n + j] * A[k * n + j];
+    if (d != d) return -1;
+    const double il = d > 1e-200 ? 1.0 / sqrt(d) : 0.0;
+    A[k * n + k] = d > 1e-200 ? sqrt(d) : 0.0;
+    invd[k] = il;
+    for (int i = k + 1; i < n; ++i) {
+      double s = A[i * n + k];
+      for (int j = 0; j < k; ++j) s -= A[i * n + j] * A[k * n + j];
+      A[i * n + k] = s * il;
+    }
+  }
+  return 0;
+}
+static void ipm_chol_solve(int n, const double* Lm, const double* invd, double* b) {
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int j = 0; j < i; ++j) s -= Lm[i * n + j] * b[j];
+    b[i] = s * invd[i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int j = i + 1; j < n; ++j) s -= Lm[j * n + i] * b[j];
+    b[i] = s * invd[i];
+  }
+}
 
 static void ipm_dir(int n, int ld, int nt, const double* tri_mu, ipm_ws* W) {
   const int m = 5 * nt;
@@ -318,7 +349,7 @@ static void ipm_dir(int n, int ld, int nt, const double* tri_mu, ipm_ws* W) {
     for (int d = 0; d < 3; ++d) W->rhs[3 * t + d] -= f[d];
   }
   memcpy(W->du, W->rhs, sizeof(double) * n);
-  oracle_chol_solve(n, W->K, n, W->du);
+  ipm_chol_solve(n, W->K, W->invd, W->du);
   for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], W->du + 3 * t, W->cdu + 5 * t);
   for (int j = 0; j < m; ++j) {
     W->dtl[j] = W->cdu[j] + W->rl[j];
@@ -344,9 +375,10 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
                   double* res) {
   const int nt = n / 3, m = 5 * nt;
   ipm_ws W;
-  double* buf = (double*)calloc((size_t)n * n + 4 * (size_t)n + 15 * (size_t)(m + 1), sizeof(double));
+  double* buf = (double*)calloc((size_t)n * n + 5 * (size_t)n + 15 * (size_t)(m + 1), sizeof(double));
   double* p = buf;
   W.K = p; p += (size_t)n * n;
+  W.invd = p; p += n;
   W.rg = p; p += n;
   W.rhs = p; p += n;
   W.du = p; p += n;
@@ -430,7 +462,7 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
       W.K[(b + 2) * n + b + 1] += yz;
     }
     for (int i = 0; i < n; ++i) W.K[i * n + i] += s->reg_prim;
-    if (oracle_cholesky(n, W.K, n) != 0) {
+    if (ipm_cholesky(n, W.K, W.invd) != 0) {
       status = CMPC_NAN_SOL;
       break;
     }
@@ -516,7 +548,7 @@ void oracle_qp_kkt(int n, int ld, const double* H, const double* g, const double
 
 int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
                      const double* foot, const uint8_t* contact, double* u, double* x, int* iters) {
-  const int N = c->N, L = c->L, ld = NU * N;
+  const int N = c->N, ld = NU * N;
   double* H = (double*)malloc(sizeof(double) * ld * ld);
   double* g = (double*)malloc(sizeof(double) * ld);
   double* mu = (double*)malloc(sizeof(double) * ld);
