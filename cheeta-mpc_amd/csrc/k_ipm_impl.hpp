@@ -38,6 +38,16 @@ template <>
 struct PIVOT_MIN<float> {
   static constexpr float v = 1e-30f;
 };
+template <typename T>
+struct MU_MIN;
+template <>
+struct MU_MIN<double> {
+  static constexpr double v = 1e-300;
+};
+template <>
+struct MU_MIN<float> {
+  static constexpr float v = 1e-35f;
+};
 __device__ __forceinline__ bool uniform_flag(bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
 // Lane id the compiler cannot CSE or hoist: every region recomputes its own lane-vs-index masks instead of keeping
 // ~200 64-bit masks live in SGPRs across the iteration.
@@ -77,8 +87,8 @@ struct IpmLds {
   T dtl[MCP], dtu[MCP], dll[MCP], dlu[MCP], rml[MCP], rmu[MCP];
 };
 
-template <typename T, int NMAX>
-__global__ __launch_bounds__(64, (NMAX == 64) ? 2 : 1) void k_ipm_reg(IpmArgs<T> a) {
+template <typename T, int NMAX, int WPE>
+__global__ __launch_bounds__(64, WPE) void k_ipm_reg(IpmArgs<T> a) {
   constexpr int RPL = NMAX / 64;                  // Newton-matrix rows per lane
   constexpr int NTRI = NMAX / 3;                  // force triples
   constexpr int CPL = IpmLds<T, NMAX>::MCP / 64;  // constraint rows per lane
@@ -331,6 +341,11 @@ __global__ __launch_bounds__(64, (NMAX == 64) ? 2 : 1) void k_ipm_reg(IpmArgs<T>
     }
     if (it >= S.iter_max) {
       status = CMPC_MAX_ITER;
+      break;
+    }
+    // mu underflow (a stagnating primal residual below the precision of the bounds): stop instead of 0/0
+    if (uniform_flag(m > 0 && !(mu > T(MU_MIN<T>::v)))) {
+      status = CMPC_MIN_STEP;
       break;
     }
 

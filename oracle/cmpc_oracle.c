@@ -440,6 +440,10 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
       status = CMPC_MAX_ITER;
       break;
     }
+    if (m > 0 && !(mu > 1e-300)) { /* mu underflow guard, as the kernels */
+      status = CMPC_MIN_STEP;
+      break;
+    }
     /* Newton matrix K = H + C' diag(lam/t) C + reg I */
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) W.K[i * n + j] = H[(size_t)i * ld + j];

@@ -1,0 +1,165 @@
+// C++ mirror of the reference gtests ocs2_sqp/hpipm_catkin/test/testHpipmInterface.cpp (solve_and_check_dynamic
+// :37-69, solve_after_resize :71-110, knownSolution :112-152, noInputs :208-256) against the HpipmInterface
+// mirror, whose solve runs on the MI355X engine. Random problems from a fixed-seed generator (ocs2's
+// getRandomDynamics/getRandomCost are not vendored): uniform [-1,1) matrices, costs made positive definite.
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "hpipm_catkin/HpipmInterface.h"
+
+using namespace ocs2;
+
+static std::mt19937_64 rng(20221125);
+static double U() { return std::uniform_real_distribution<double>(-1.0, 1.0)(rng); }
+
+static matrix_t randm(int r, int c) {
+  matrix_t m(r, c);
+  for (int j = 0; j < c; ++j)
+    for (int i = 0; i < r; ++i) m(i, j) = U();
+  return m;
+}
+static vector_t randv(int n) {
+  vector_t v(n);
+  for (int i = 0; i < n; ++i) v[i] = U();
+  return v;
+}
+static VectorFunctionLinearApproximation randomDynamics(int nx, int nu) {
+  VectorFunctionLinearApproximation d;
+  d.dfdx = randm(nx, nx);
+  d.dfdu = randm(nx, nu);
+  d.f = randv(nx);
+  return d;
+}
+static ScalarFunctionQuadraticApproximation randomCost(int nx, int nu) {
+  const int n = nx + nu;
+  matrix_t M = randm(n, n), H(n, n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double s = (i == j) ? n : 0.0;
+      for (int k = 0; k < n; ++k) s += M(i, k) * M(j, k);
+      H(i, j) = s;
+    }
+  ScalarFunctionQuadraticApproximation c;
+  c.dfdxx.resize(nx, nx);
+  c.dfdux.resize(nu, nx);
+  c.dfduu.resize(nu, nu);
+  for (int i = 0; i < nx; ++i)
+    for (int j = 0; j < nx; ++j) c.dfdxx(i, j) = H(i, j);
+  for (int i = 0; i < nu; ++i)
+    for (int j = 0; j < nx; ++j) c.dfdux(i, j) = H(nx + i, j);
+  for (int i = 0; i < nu; ++i)
+    for (int j = 0; j < nu; ++j) c.dfduu(i, j) = H(nx + i, nx + j);
+  c.dfdx = randv(nx);
+  c.dfdu = randv(nu);
+  return c;
+}
+static vector_t mv(const matrix_t& A, const vector_t& x) {
+  vector_t y(A.rows());
+  for (int i = 0; i < A.rows(); ++i) {
+    double s = 0;
+    for (int j = 0; j < A.cols(); ++j) s += A(i, j) * x[j];
+    y[i] = s;
+  }
+  return y;
+}
+static vector_t mtv(const matrix_t& A, const vector_t& x) {  // A' x
+  vector_t y(A.cols());
+  for (int j = 0; j < A.cols(); ++j) {
+    double s = 0;
+    for (int i = 0; i < A.rows(); ++i) s += A(i, j) * x[i];
+    y[j] = s;
+  }
+  return y;
+}
+static double maxdiff(const vector_t& a, const vector_t& b) {
+  double m = a.size() == b.size() ? 0.0 : 1e300;
+  for (int i = 0; i < a.size() && i < b.size(); ++i) m = std::fmax(m, std::fabs(a[i] - b[i]));
+  return m;
+}
+
+static int failures = 0;
+#define CHECK(cond, what)                                \
+  do {                                                   \
+    if (!(cond)) {                                       \
+      std::printf("FAIL %s (%s:%d)\n", what, __FILE__, __LINE__); \
+      ++failures;                                        \
+    }                                                    \
+  } while (0)
+
+static void known_solution(bool no_inputs) {
+  const int nx = 3, N = 5;
+  std::vector<vector_t> xg{randv(nx)}, ug;
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    const int nu = (no_inputs && k == 1) ? 0 : 2;
+    ug.push_back(randv(nu));
+    sys.push_back(randomDynamics(nx, nu));
+    vector_t xn = sys[k].f;
+    const vector_t ax = mv(sys[k].dfdx, xg[k]), bu = mv(sys[k].dfdu, ug[k]);
+    for (int i = 0; i < nx; ++i) xn[i] += ax[i] + bu[i];
+    xg.push_back(xn);
+    cost.push_back(randomCost(nx, nu));
+    const vector_t qx = mv(cost[k].dfdxx, xg[k]), su = mtv(cost[k].dfdux, ug[k]);
+    for (int i = 0; i < nx; ++i) cost[k].dfdx[i] = -(qx[i] + su[i]);
+    const vector_t ru = mv(cost[k].dfduu, ug[k]), sx = mv(cost[k].dfdux, xg[k]);
+    for (int i = 0; i < nu; ++i) cost[k].dfdu[i] = -(ru[i] + sx[i]);
+  }
+  cost.push_back(randomCost(nx, 0));
+  const vector_t qN = mv(cost[N].dfdxx, xg[N]);
+  for (int i = 0; i < nx; ++i) cost[N].dfdx[i] = -qN[i];
+  HpipmInterface hpipm(hpipm_interface::extractSizesFromProblem(sys, cost, nullptr));
+  std::vector<vector_t> xs, us;
+  const auto status = hpipm.solve(xg[0], sys, cost, nullptr, xs, us, false);
+  CHECK(status == hpipm_status::SUCCESS, "knownSolution status");
+  for (int k = 0; k <= N; ++k) CHECK(maxdiff(xs[(size_t)k], xg[(size_t)k]) < 1e-9, "knownSolution x");
+  for (int k = 0; k < N; ++k) CHECK(maxdiff(us[(size_t)k], ug[(size_t)k]) < 1e-9, "knownSolution u");
+}
+
+static void dynamics_feasible(bool resize) {
+  const int nx = 3, nu = 2, N = 5;
+  const vector_t x0 = randv(nx);
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+  }
+  cost.push_back(randomCost(nx, 0));
+  HpipmInterface hpipm = resize ? HpipmInterface() : HpipmInterface(HpipmInterface::OcpSize(N, nx, nu));
+  if (resize) hpipm.resize(HpipmInterface::OcpSize(N, nx, nu));
+  std::vector<vector_t> xs, us;
+  auto status = hpipm.solve(x0, sys, cost, nullptr, xs, us, false);
+  if (resize) {
+    hpipm.resize(HpipmInterface::OcpSize(N, nx, nu));
+    status = hpipm.solve(x0, sys, cost, nullptr, xs, us, false);
+  }
+  CHECK(status == hpipm_status::SUCCESS, "dynamics status");
+  CHECK(maxdiff(xs[0], x0) < 1e-15, "x0");
+  for (int k = 0; k < N; ++k) {
+    vector_t xn = sys[k].f;
+    const vector_t ax = mv(sys[k].dfdx, xs[(size_t)k]), bu = mv(sys[k].dfdu, us[(size_t)k]);
+    for (int i = 0; i < nx; ++i) xn[i] += ax[i] + bu[i];
+    CHECK(maxdiff(xs[(size_t)k + 1], xn) < 1e-9, "dynamics feasibility");
+  }
+  // size mismatch throws like the reference (HpipmInterface.cpp:149-162)
+  bool threw = false;
+  try {
+    std::vector<VectorFunctionLinearApproximation> shorter(sys.begin(), sys.end() - 1);
+    hpipm.solve(x0, shorter, cost, nullptr, xs, us, false);
+  } catch (const std::runtime_error&) {
+    threw = true;
+  }
+  CHECK(threw, "size mismatch throws");
+}
+
+int main() {
+  dynamics_feasible(false);
+  dynamics_feasible(true);
+  known_solution(false);
+  known_solution(true);
+  std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
+  return failures ? 1 : 0;
+}

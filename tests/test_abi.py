@@ -1,0 +1,105 @@
+"""CPU suite: the C-ABI library (cheeta-mpc_amd/lib/libcmpc.so) loads, exports every symbol include/*.h declares,
+and its host-side defaults/struct layouts match the reference (no compute call needs a GPU here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions(header):
+    txt = open(header).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(cmpc_[a-z_0-9]+)\s*\(", txt, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    import cheeta_mpc
+    L = cheeta_mpc.lib()
+    names = declared_functions(os.path.join(ROOT, "include", "cmpc", "cmpc.h"))
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    out = subprocess.check_output(["nm", "-D", "--defined-only", cheeta_mpc.LIB_PATH], text=True)
+    for n in names:
+        assert re.search(rf"\bT {n}$", out, flags=re.M), n
+
+
+def test_settings_defaults_match_hpipm_interface():
+    import cheeta_mpc
+    s = cheeta_mpc.default_settings()
+    # hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57)
+    assert (s.iter_max, s.alpha_min, s.mu0, s.tol_stat, s.tol_eq, s.tol_ineq, s.tol_comp, s.reg_prim) == \
+        (30, 1e-12, 10.0, 1e-6, 1e-8, 1e-8, 1e-8, 1e-12)
+    assert (s.warm_start, s.pred_corr, s.ric_alg) == (0, 1, 0)
+
+
+def test_model_default_is_centoid_mpc_test(op):
+    import cheeta_mpc
+    m = cheeta_mpc.default_model(6)
+    o = op.default_model(6)
+    assert m.N == 6 and m.n_legs == 4 and m.mass == 8.0 and m.dt == 0.01
+    assert list(m.weights) == list(o.weights)
+    assert list(m.mu) == [0.8] * 4
+    assert list(m.force_ub) == [5000.0] * 4 + [8.0 * 9.81 * 4]
+
+
+def test_struct_layouts_match_c(tmp_path):
+    import cheeta_mpc
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "cmpc/cmpc.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
+                   ' sizeof(cmpc_model), sizeof(cmpc_settings), offsetof(cmpc_model, weights),'
+                   ' offsetof(cmpc_settings, warm_start)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    a, b, c, d = (int(v) for v in subprocess.check_output([str(exe)], text=True).split())
+    assert a == C.sizeof(cheeta_mpc.Model) and b == C.sizeof(cheeta_mpc.Settings)
+    assert c == cheeta_mpc.Model.weights.offset and d == cheeta_mpc.Settings.warm_start.offset
+
+
+def test_memsize_and_arg_checks():
+    import cheeta_mpc
+    L = cheeta_mpc.lib()
+    m = cheeta_mpc.default_model(10)
+    s64 = L.cmpc_memsize(C.byref(m), 0, 4096)
+    s32 = L.cmpc_memsize(C.byref(m), 1, 4096)
+    assert s64 > 4096 * 128 * 128 * 8 and s32 < s64
+    bad = cheeta_mpc.default_model(10)
+    bad.n_legs = 2
+    assert L.cmpc_memsize(C.byref(bad), 0, 16) == 0
+    ctx = C.c_void_p()
+    assert L.cmpc_create(C.byref(bad), None, 0, 16, None, C.byref(ctx)) == -1  # CMPC_ERR_ARG
+    assert L.cmpc_ocp_solve_batch_host(1, 0, 3, None, None, None, None, None, None) == -1
+    assert L.cmpc_status_string(5) == b"INVALID_CONTACT" and L.cmpc_status_string(0) == b"SUCCESS"
+    nu = np.array([2, 0, 2], dtype=np.int32)
+    assert L.cmpc_ocp_record_size(3, 3, nu.ctypes.data_as(C.c_void_p)) == \
+        cheeta_mpc.lib().cmpc_ocp_record_size(3, 3, nu.ctypes.data_as(C.c_void_p))
+
+
+def test_ocp_record_size_matches_oracle(op):
+    import cheeta_mpc
+    nu = np.array([2, 0, 2, 1], dtype=np.int32)
+    a = cheeta_mpc.lib().cmpc_ocp_record_size(4, 3, nu.ctypes.data_as(C.c_void_p))
+    b = op.lib().oracle_ocp_record_size(4, 3, nu.ctypes.data_as(C.POINTER(C.c_int)))
+    assert a == b
+
+
+def test_no_device_is_reported_not_faked():
+    import cheeta_mpc
+    if cheeta_mpc.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    m = cheeta_mpc.default_model(10)
+    ctx = C.c_void_p()
+    assert cheeta_mpc.lib().cmpc_create(C.byref(m), None, 0, 16, None, C.byref(ctx)) == -4  # CMPC_ERR_NO_DEVICE
+
+
+def test_cpp_mirror_headers_compile(tmp_path):
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "cheeta_mpc/CentroidalMPC.h"\n#include "hpipm_catkin/HpipmInterface.h"\n'
+                   'int main(){ ocs2::HpipmInterface::OcpSize s(5,3,2); return s.numInputs.back(); }\n')
+    subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)])

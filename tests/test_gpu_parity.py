@@ -94,13 +94,13 @@ def test_solve_fp32_n20(cm, op):
     N = 20
     m, mo = cm.default_model(N), op.default_model(N)
     B = 64
-    s = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-4, tol_comp=1e-4)
+    s = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3, tol_comp=1e-4)  # fp32: ulp(5000 N bound) = 4.9e-4
     eng = cm.Engine(m, settings=s, precision=1, max_batch=B)
     x0, xref, foot, contact = op.generate(mo, SEED, B, gait=0)
     u, x, st, it = eng.solve(x0, xref, foot, contact)
     ur, xr, sr, itr = op.solve_batch(mo, op.tight_settings(), x0, xref, foot, contact, nthreads=8)
     assert np.all(sr == 0)
-    assert np.mean(st == 0) > 0.95
+    assert np.all(st == 0)
     err = max(rel_err(u[q], ur[q]) for q in range(B) if st[q] == 0)
     assert err < 2e-3, err
 
@@ -126,3 +126,118 @@ def test_centoid_mpc_test_inputs(cm, op):
         ur = np_ref.solve(np_ref.model_arrays(mo), x0, xref, foot, contact)
         assert st[0] == 0
         assert rel_err(u[0], ur) < 1e-8
+
+
+# ---------------------------------------------------------------------------- golden fixtures on the device
+
+import glob  # noqa: E402
+import os  # noqa: E402
+import subprocess  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+GOLDEN = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "c*.npz")))
+
+
+def _load(name):
+    with np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_device_matches_golden_fp64(cm, name):
+    z = _load(name)
+    N = int(z["N"])
+    m = cm.default_model(N)
+    eng = cm.Engine(m, precision=0, max_batch=z["x0"].shape[0])
+    u, x, st, it = eng.solve(z["x0"], z["xref"], z["foot"], z["contact"])
+    assert np.all(st == 0)
+    err = max(rel_err(u[q], z["u"][q]) for q in range(u.shape[0]))
+    assert err < 1e-6, err   # HPIPM default tolerances; the north-star gate is 1e-5
+    # condensed Hessian / gradient of stance rows against the numpy restatement
+    H, g, n, stc = eng.condense(z["x0"], z["xref"], z["foot"], z["contact"])
+    for q in range(u.shape[0]):
+        idx = [12 * k + 3 * i + d for k in range(N) for i in range(4) if z["contact"][q, k, i] for d in range(3)]
+        Hr = z["H_full"][q][np.ix_(idx, idx)]
+        assert n[q] == len(idx)
+        assert np.abs(H[q, :n[q], :n[q]] - Hr).max() / np.abs(Hr).max() < 1e-12
+
+
+def test_generator_matches_golden_inputs(cm):
+    z = _load("config5_mixed_N10")
+    m = cm.default_model(10)
+    d = [a.host() for a in cm.generate_device(m, SEED, z["x0"].shape[0], gait=1)]
+    for got, key in zip(d, ("x0", "xref", "foot", "contact")):
+        assert np.array_equal(got, z[key])
+
+
+def test_qp_solve_hook_matches_oracle(cm, op):
+    N = 10
+    m, mo = cm.default_model(N), op.default_model(N)
+    eng = cm.Engine(m, precision=0, max_batch=16)
+    ld = eng.ld
+    x0, xref, foot, contact = op.generate(mo, SEED, 16, gait=1)
+    Hs, gs, ns, mus, los, his, refs = [], [], [], [], [], [], []
+    for q in range(16):
+        n, H, g, mu, lo, hi, mp, st = op.condense(mo, x0[q], xref[q], foot[q], contact[q], ld=ld)
+        Hs.append(H); gs.append(g); ns.append(n); mus.append(mu); los.append(lo); his.append(hi)
+        refs.append(op.qp_ipm(n, H, g, mu, lo, hi, op.default_settings())[0])
+    u, st, it = eng.qp_solve(np.array(Hs), np.array(gs), np.array(ns, np.int32), np.array(mus), np.array(los),
+                             np.array(his))
+    assert np.all(st == 0)
+    for q in range(16):
+        assert rel_err(u[q, :ns[q]], refs[q]) < 1e-8
+        assert np.all(u[q, ns[q]:] == 0)
+
+
+def test_hpipm_interface_path_on_device(cm, op):
+    """testHpipmInterface.cpp:112-152 known solution through the device OCP path (batched)."""
+    from test_oracle import random_ocp
+    rng = np.random.default_rng(42)
+    recs, x0s, xgs, ugs = [], [], [], []
+    N, nx, nu = 5, 3, [2, 0, 2, 2, 2]
+    for b in range(8):
+        A, B, bb, Q, S, R, q, r = random_ocp(rng, N, nx, nu)
+        xs = [rng.uniform(-1, 1, nx)]
+        us = []
+        for k in range(N):
+            us.append(rng.uniform(-1, 1, nu[k]))
+            xs.append(bb[k] + A[k] @ xs[k] + B[k] @ us[k])
+            q[k] = -(Q[k] @ xs[k] + S[k].T @ us[k])
+            r[k] = -(R[k] @ us[k] + S[k] @ xs[k])
+        q[N] = -Q[N] @ xs[N]
+        recs.append(op.ocp_pack(N, nx, nu, A, B, bb, Q, S, R, q, r))
+        x0s.append(xs[0]); xgs.append(np.array(xs)); ugs.append(np.concatenate(us))
+    x, u, st = cm.ocp_solve(N, nx, nu, np.array(x0s), np.array(recs))
+    assert np.all(st == 0)
+    assert np.abs(x - np.array(xgs)).max() < 1e-9
+    assert np.abs(u - np.array(ugs)).max() < 1e-9
+
+
+@pytest.fixture(scope="module")
+def cpp_bins(tmp_path_factory, cm):
+    out = tmp_path_factory.mktemp("cppbin")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp")
+    subprocess.check_call(["make", "-s", "-C", here, f"OUT={out}"])
+    return out
+
+
+def test_cpp_hpipm_interface_mirror(cpp_bins):
+    r = subprocess.run([str(cpp_bins / "test_hpipm_interface")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASSED" in r.stdout
+
+
+def test_cpp_centroidal_mpc_driver(cpp_bins):
+    """CentoidMPCTest.cpp equivalent through the C++ CentroidalMPC mirror vs the numpy golden (literal quirk)."""
+    r = subprocess.run([str(cpp_bins / "centroid_mpc_test")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "caught mpc table invalid" in r.stdout
+    z = _load("centoid_mpc_test_N6")
+    u = np.zeros((6, 4, 3))
+    for line in r.stdout.splitlines():
+        if line.startswith("status"):
+            assert line.split()[1] == "0"
+        if line.startswith("force"):
+            _, i, k, fx, fy, fz = line.split()
+            u[int(k), int(i)] = [float(fx), float(fy), float(fz)]
+    assert rel_err(u, z["u"][0]) < 1e-6
