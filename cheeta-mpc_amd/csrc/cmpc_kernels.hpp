@@ -14,6 +14,13 @@ namespace cmpc {
 // class-padded size of a condensed problem
 __host__ __device__ inline int ipm_class(int n) { return n <= 64 ? 64 : 128; }
 
+// Position of H[i][j] inside a QP's class-packed block. Class 64 is stored in the 4 x 16-cyclic register order of
+// k_ipm64 (element (i, j) is register 4*(i/4) + j/16 of lane 16*(i%4) + j%16), so each of that kernel's 64 loads
+// is one contiguous 512-B row; class 128 is row-major with stride 128.
+__host__ __device__ inline int h_index(int npad, int i, int j) {
+  return npad == 64 ? (((i >> 2) * 4 + (j >> 4)) * 64 + (i & 3) * 16 + (j & 15)) : i * npad + j;
+}
+
 // Per-QP workspace of one context (precision T), QP-major:
 //   H [B][ld][ld], g [B][ld], tri_mu [B][ld/3], tri_lo/tri_hi [B][ld/3][5], tri_map [B][ld/3], nvar [B],
 //   status [B], iters [B], u [B][ld]
@@ -56,6 +63,10 @@ int launch_srbd_condense(const CondenseArgs<T>& a, int B, hipStream_t stream);
 // Runs every IPM size class over the batch; each QP is served by the class matching its condensed size.
 template <typename T>
 int launch_ipm(const IpmArgs<T>& a, int B, hipStream_t stream);
+int launch_ipm64(const IpmArgs<double>& a, int B, hipStream_t stream);   // n <= 64 (k_ipm64.hpp)
+int launch_ipm64(const IpmArgs<float>& a, int B, hipStream_t stream);
+int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm_impl.hpp)
+int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);
 
 struct ExpandArgs {
   const DevModel* model;

@@ -299,8 +299,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
             if (rr < n && s_next[rr] == cc) v += s_offR[rr];
             if (cc < n && s_next[cc] == rr) v += s_offR[cc];
           }
-          Hq[(size_t)rr * npad + cc] = v;  // class-packed: the IPM of size class npad reads stride npad
-          if (ti != tj) Hq[(size_t)cc * npad + rr] = v;
+          Hq[h_index(npad, rr, cc)] = v;  // class-packed block in the order the IPM of class npad reads
+          if (ti != tj) Hq[h_index(npad, cc, rr)] = v;
         }
       }
     }

@@ -1,0 +1,15 @@
+// k_ipm128.hip — the 64 < n <= 128 size class (k_ipm_impl.hpp: row-per-lane register IPM, RPL = 2).
+#include "k_ipm_impl.hpp"
+
+namespace cmpc {
+
+int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream) {
+  hipLaunchKernelGGL((k_ipm_reg<double, 128, 1>), dim3(B), dim3(64), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream) {
+  hipLaunchKernelGGL((k_ipm_reg<float, 128, 1>), dim3(B), dim3(64), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace cmpc

@@ -1,0 +1,516 @@
+#pragma once
+// k_ipm64.hpp — stage 2 of the hot path for condensed sizes n <= 64 (every trot QP at N <= 10): the batched dense
+// friction-pyramid QP, primal-dual Mehrotra predictor-corrector interior point method. Replaces d_ocp_qp_ipm_solve
+// (HPIPM, called at HpipmInterface.cpp:284) / IPOPT's Newton loop (CentroidalMPC.cpp:354) for the condensed
+// centroidal QP; settings and stopping rule mirror hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57).
+// The iteration is the one restated in oracle/cmpc_oracle.c:oracle_qp_ipm; only the factorisation differs
+// (LDL' here, Cholesky there), so the two agree to rounding, not bit for bit.
+//
+//   min 1/2 u'Hu + g'u   s.t.  lo <= C u <= hi,   C = blkdiag_t F(mu_t) (5x3 pyramid per stance force triple)
+//
+// MI355X mapping — one wavefront (64 lanes) per QP, no workgroup barriers, 2 waves per SIMD (fp64):
+//   * Newton matrix K = H + C' Sigma C in a 4 x 16-cyclic register tile: lane l = 16a + b holds
+//     K[a + 4r][b + 16c] (r = 0..15, c = 0..3) in register e = 4r + c — 64 values per lane;
+//   * LDL' right-looking factorisation. Step s: K[i][j] -= K[i][s] K[s][j] / d_s for i, j > s. The 16 row
+//     multipliers K[i][s] of a lane live in its own 16-lane DPP row (column s sits in lane b = s % 16), so they
+//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp); only the 4 column
+//     multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent through LDS and
+//     its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
+//   * the factor is transposed once through LDS into row layout (lane i = row i), each row scaled by 1/d_i, so
+//     every step of the four triangular sweeps is one v_readlane pair + one FMA; finished unknowns are saved to
+//     LDS instead of masking the lanes that are already done;
+//   * vectors are lane-per-variable; the <= 105 pyramid rows are two slots per lane (j = lane + 64 cc) with the
+//     primal-dual state in registers and per-iteration scratch in lane-private LDS;
+//   * H is stored by the condensing kernel in the tile order (h_index, cmpc_kernels.hpp): 64 coalesced 512-B
+//     row loads per iteration;
+//   * lane-derived addresses come from an opaque lane id re-read every iteration (olane) so they are not hoisted
+//     out of the loop as ~100 live VGPRs; lane masks use the plain id and are hoisted into SGPR pairs.
+#include <type_traits>
+
+#include "cmpc_device.hpp"
+#include "cmpc_kernels.hpp"
+#include "dpp_rows.hpp"
+
+namespace cmpc {
+
+namespace ipm64 {
+
+template <typename T>
+struct Lim;
+template <>
+struct Lim<double> {
+  static constexpr double pivot_min = 1e-200;  // BLASFEO-style guard: smaller pivots drop their direction
+  static constexpr double mu_min = 1e-300;     // mu underflow -> MIN_STEP instead of 0/0
+};
+template <>
+struct Lim<float> {
+  static constexpr float pivot_min = 1e-30f;
+  static constexpr float mu_min = 1e-35f;
+};
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor_down(F&& f) {  // E-1 down to B
+  if constexpr (B < E) {
+    f(std::integral_constant<int, E - 1>{});
+    sfor_down<B, E - 1>(f);
+  }
+}
+// Compiler-only ordering of LDS accesses: one wave's DS instructions execute in order, so a read issued after a
+// write (or a write after a read) in program order sees the right data without s_waitcnt.
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
+__device__ __forceinline__ int olane() {
+  int l = (int)threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+__device__ __forceinline__ bool uflag(bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
+
+__device__ __forceinline__ double rcp_raw(double x) { return __builtin_amdgcn_rcp(x); }
+__device__ __forceinline__ float rcp_raw(float x) { return __builtin_amdgcn_rcpf(x); }
+// reciprocal of a pivot: hardware estimate + one Newton step, 0 for pivots at or below the guard (and NaN)
+template <typename T>
+__device__ __forceinline__ T pivot_inv(T p) {
+  T y = rcp_raw(p);
+  const T e = fma(-p, y, T(1));
+  y = fma(y, e, y);
+  return p > T(Lim<T>::pivot_min) ? y : T(0);
+}
+
+// row-layout column j after the transpose lives in the register the tile used for column j's chunk
+__host__ __device__ constexpr int ridx(int j) { return (j & 15) * 4 + (j >> 4); }
+
+template <typename T>
+struct Lds {
+  T v[64];          // lane-per-variable broadcast
+  T w[128];         // pyramid-row broadcast
+  T rowbuf[2][64];  // factorisation: row s of K as [c*16 + b]
+  T dg[64];         // pivots d_s
+  T z[64];          // sweep results
+  T blk[3][64];     // Newton 3x3 block rows
+  T rl[128], ru[128], itl[128], itu[128], rml[128], rmu[128];  // lane-private pyramid-row scratch
+  T scr[1024];      // Hu partial sums / factor transpose (16 columns at a time)
+};
+
+}  // namespace ipm64
+
+template <typename T, int WPE>
+__global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
+  using namespace ipm64;
+  const int q = blockIdx.x;
+  if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
+  const int n = A.nvar[q];
+  if (n > 64) return;  // served by the 128 class
+  const int ld = A.ld;
+  const int nt = n / 3;
+  const int m = 5 * nt;
+  const DevSettings S = A.s;
+  __shared__ Lds<T> L;
+  int lane = (int)threadIdx.x;         // re-read opaquely at the top of every iteration
+  const int lane0 = (int)threadIdx.x;  // plain lane id: lane masks only (hoisted into SGPR pairs)
+
+  // ---- lane-per-variable data
+  const bool vin = lane < n;
+  const T g_v = vin ? A.g[(size_t)q * ld + lane] : T(0);
+  const T mu_v = vin ? A.tri_mu[(size_t)q * (ld / 3) + lane / 3] : T(0);
+  T u_v = T(0);
+  // ---- pyramid rows j = lane + 64 cc; cold start (warm_start = 0): u = 0, slacks clipped at THR0, lam = mu0 / t
+  T tl[2], tu[2], ll[2], lu[2], lo[2], hi[2], muc[2];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) {
+    const int j = lane + 64 * cc;
+    const bool on = j < m;
+    const int t = j / 5;
+    lo[cc] = on ? A.tri_lo[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
+    hi[cc] = on ? A.tri_hi[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
+    muc[cc] = on ? A.tri_mu[(size_t)q * (ld / 3) + t] : T(0);
+    tl[cc] = on ? fmax(-lo[cc], T(THR0)) : T(1);
+    tu[cc] = on ? fmax(hi[cc], T(THR0)) : T(1);
+    ll[cc] = on ? T(S.mu0) / tl[cc] : T(0);
+    lu[cc] = on ? T(S.mu0) / tu[cc] : T(0);
+  }
+
+  // C x for the lane's two pyramid rows, x already in L.v (CentroidalMPC.cpp:186-190)
+  auto apply_C = [&](T (&out)[2]) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      const int t = j / 5;
+      T v = T(0);
+      if (j < m) v = pyr_row<T>(j % 5, muc[cc], L.v[3 * t], L.v[3 * t + 1], L.v[3 * t + 2]);
+      out[cc] = v;
+    }
+  };
+  // C' w, lane-per-variable
+  auto apply_CT = [&](const T (&wv)[2]) -> T {
+    L.w[lane] = wv[0];
+    L.w[lane + 64] = wv[1];
+    cbar();
+    T v = T(0);
+    if (vin) {
+      const int t = lane / 3, dd = lane % 3;
+      const T w0 = L.w[5 * t], w1 = L.w[5 * t + 1], w2 = L.w[5 * t + 2], w3 = L.w[5 * t + 3], w4 = L.w[5 * t + 4];
+      v = dd == 0 ? (w1 - w0) : (dd == 1 ? (w3 - w2) : (mu_v * (w0 + w1 + w2 + w3) + w4));
+    }
+    cbar();
+    return v;
+  };
+
+  T K[64];
+  T invd_v = T(1);
+  T rg_v = T(0), du_v = T(0);
+  T dtl[2], dtu[2], dll[2], dlu[2];
+
+  // LDL' solve with the row-scaled factor K'[i][k] = K[i][k] / d_i held in row layout (K[ridx(k)] = K'[lane][k]):
+  //   forward  w = D^-1 rhs; for k up:   z_k = w_k; w_i -= K'[i][k] z_k   (w = D^-1 L^-1 rhs)
+  //   backward v = z;        for k down: x_k = v_k; v_i -= K'[i][k] x_k   (x = L^-T z)
+  // A lane past its own step takes garbage updates; its value was saved to LDS at that step.
+  auto solve = [&](T& y) {
+    T w = y * invd_v;
+    sfor<0, 64>([&](auto k_) {
+      constexpr int k = decltype(k_)::value;
+      const T zk = readlane(w, k);
+      L.z[k] = zk;
+      w = fma(-K[ridx(k)], zk, w);
+    });
+    cbar();
+    w = L.z[lane];
+    cbar();
+    sfor_down<0, 64>([&](auto k_) {
+      constexpr int k = decltype(k_)::value;
+      const T xk = readlane(w, k);
+      L.z[k] = xk;
+      w = fma(-K[ridx(k)], xk, w);
+    });
+    cbar();
+    y = L.z[lane];
+    cbar();
+  };
+
+  // Newton direction for the complementarity targets in L.rml / L.rmu
+  auto direction = [&]() {
+    T wv[2];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      wv[cc] = (L.rml[j] + ll[cc] * L.rl[j]) * L.itl[j] - (L.rmu[j] + lu[cc] * L.ru[j]) * L.itu[j];
+    }
+    const T ctw = apply_CT(wv);
+    du_v = -rg_v - ctw;
+    solve(du_v);
+    L.v[lane] = du_v;
+    cbar();
+    T cdu[2];
+    apply_C(cdu);
+    cbar();
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      dtl[cc] = cdu[cc] + L.rl[j];
+      dtu[cc] = L.ru[j] - cdu[cc];
+      dll[cc] = -(L.rml[j] + ll[cc] * dtl[cc]) * L.itl[j];
+      dlu[cc] = -(L.rmu[j] + lu[cc] * dtu[cc]) * L.itu[j];
+    }
+  };
+  auto max_step = [&]() -> T {
+    T am = T(1e30);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      if (dtl[cc] < T(0)) am = fmin(am, -tl[cc] / dtl[cc]);
+      if (dtu[cc] < T(0)) am = fmin(am, -tu[cc] / dtu[cc]);
+      if (dll[cc] < T(0)) am = fmin(am, -ll[cc] / dll[cc]);
+      if (dlu[cc] < T(0)) am = fmin(am, -lu[cc] / dlu[cc]);
+    }
+    return wave_min(am);
+  };
+
+  const T* Hq = A.H + (size_t)q * ld * ld;
+  int status = CMPC_MAX_ITER;
+  int it = 0;
+  for (it = 0;; ++it) {
+    lane = olane();
+    const int la = lane >> 4, lb = lane & 15;
+    // ---- H in tile order (64 coalesced 512-B rows)
+#pragma unroll
+    for (int e = 0; e < 64; ++e) K[e] = Hq[e * 64 + lane];
+
+    // ---- residuals. Hu from the tile: 16 partial row sums per lane, reduced through LDS (row i's 16 partials
+    //      at i*16 + rotated 16-B slot, so both the writes and the row reads are conflict-free)
+    T hu = T(0);
+    L.v[lane] = u_v;
+    cbar();
+    {
+      T uc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) uc[c] = L.v[lb + 16 * c];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        T p = K[r * 4] * uc[0];
+        p = fma(K[r * 4 + 1], uc[1], p);
+        p = fma(K[r * 4 + 2], uc[2], p);
+        p = fma(K[r * 4 + 3], uc[3], p);
+        const int i = la + 4 * r;
+        L.scr[i * 16 + ((((lb >> 1) + i) & 7) << 1) + (lb & 1)] = p;
+      }
+      cbar();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = lane * 16 + (((k + lane) & 7) << 1);
+        hu += L.scr[idx] + L.scr[idx + 1];
+      }
+      cbar();
+    }
+    T cu[2];
+    apply_C(cu);  // L.v still holds u
+    cbar();
+    T rs = T(0), ri = T(0), rc = T(0), ms = T(0);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      const bool on = j < m;
+      const T rl = on ? cu[cc] - lo[cc] - tl[cc] : T(0);
+      const T ru = on ? hi[cc] - cu[cc] - tu[cc] : T(0);
+      L.rl[j] = rl;
+      L.ru[j] = ru;
+      ri = fmax(ri, fmax(fabs(rl), fabs(ru)));
+      const T cl = tl[cc] * ll[cc], ch = tu[cc] * lu[cc];
+      rc = fmax(rc, fmax(cl, ch));
+      ms += cl + ch;
+    }
+    {
+      const T wv[2] = {ll[0] - lu[0], ll[1] - lu[1]};
+      const T ctw = apply_CT(wv);
+      rg_v = vin ? hu + g_v - ctw : T(0);
+      rs = fabs(rg_v);
+    }
+    rs = wave_max(rs);
+    ri = wave_max(ri);
+    rc = wave_max(rc);
+    ms = wave_sum(ms);
+    const T mu = m > 0 ? ms / T(2 * m) : T(0);
+    if (uflag(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
+      status = CMPC_NAN_SOL;
+      break;
+    }
+    // HPIPM's absolute stopping rule (tol_stat / tol_ineq / tol_comp)
+    if (uflag(rs <= T(S.tol_stat) && ri <= T(S.tol_ineq) && rc <= T(S.tol_comp))) {
+      status = CMPC_SUCCESS;
+      break;
+    }
+    if (it >= S.iter_max) {
+      status = CMPC_MAX_ITER;
+      break;
+    }
+    if (uflag(m > 0 && !(mu > T(Lim<T>::mu_min)))) {
+      status = CMPC_MIN_STEP;
+      break;
+    }
+
+    // ---- Newton matrix K = H + C' diag(lam_l/t_l + lam_u/t_u) C + reg I: lane j writes the 3x3 block row of
+    //      variable j, tile lanes add it where entry (i, j) falls in j's force triple
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      const bool on = j < m;
+      const T itl = on ? T(1) / tl[cc] : T(0);
+      const T itu = on ? T(1) / tu[cc] : T(0);
+      L.itl[j] = itl;
+      L.itu[j] = itu;
+      L.w[j] = ll[cc] * itl + lu[cc] * itu;
+    }
+    cbar();
+    {
+      const int ti = lane / 3, dd = lane % 3;
+      T b0 = T(0), b1 = T(0), b2 = T(0);
+      if (vin) {
+        const T s0 = L.w[5 * ti], s1 = L.w[5 * ti + 1], s2 = L.w[5 * ti + 2], s3 = L.w[5 * ti + 3], s4 = L.w[5 * ti + 4];
+        const T xx = s0 + s1, yy = s2 + s3, zz = mu_v * mu_v * (s0 + s1 + s2 + s3) + s4;
+        const T xz = mu_v * (s1 - s0), yz = mu_v * (s3 - s2);
+        b0 = dd == 0 ? xx : (dd == 1 ? T(0) : xz);
+        b1 = dd == 0 ? T(0) : (dd == 1 ? yy : yz);
+        b2 = dd == 0 ? xz : (dd == 1 ? yz : zz);
+      }
+      const T reg = T(S.reg_prim);
+      b0 += dd == 0 ? reg : T(0);
+      b1 += dd == 1 ? reg : T(0);
+      b2 += dd == 2 ? reg : T(0);
+      L.blk[0][lane] = b0;
+      L.blk[1][lane] = b1;
+      L.blk[2][lane] = b2;
+    }
+    cbar();
+    sfor<0, 4>([&](auto c_) {
+      constexpr int c = decltype(c_)::value;
+      // rows that can share a triple with some column of chunk c: local rows rlo..rhi
+      constexpr int imin = 3 * ((16 * c) / 3);
+      constexpr int imax0 = 3 * ((16 * c + 15) / 3) + 2;
+      constexpr int imax = imax0 > 63 ? 63 : imax0;
+      constexpr int rlo = imin / 4;
+      constexpr int rhi = imax / 4;
+      const int j = lb + 16 * c;
+      const int t3 = 3 * (j / 3);
+      const int e = (la - t3) & 3;  // the one row i = t3 + e of j's triple with i % 4 == a (none if e == 3)
+      const int rstar = e <= 2 ? (t3 + e - la) >> 2 : -1;
+      const T val = L.blk[e <= 2 ? e : 0][j];
+      sfor<rlo, rhi + 1>([&](auto r_) {
+        constexpr int r = decltype(r_)::value;
+        K[r * 4 + c] += (rstar == r) ? val : T(0);
+      });
+    });
+    cbar();
+
+    // ---- LDL' factorisation in the tile (see header)
+    T piv = readlane(K[0], 0);
+    T invd = pivot_inv(piv);
+    T mm[4];
+    {
+      if (la == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) L.rowbuf[0][c * 16 + lb] = K[c];
+      }
+      L.dg[0] = piv;
+      cbar();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const T mv = -(L.rowbuf[0][c * 16 + lb] * invd);
+        mm[c] = c == 0 ? (lb > 0 ? mv : T(0)) : mv;
+      }
+      cbar();
+    }
+    sfor<0, 63>([&](auto s_) {
+      constexpr int s = decltype(s_)::value;
+      constexpr int c0 = s / 16, b0 = s % 16, a0 = s % 4;
+      constexpr int s1 = s + 1;
+      constexpr int r1 = s1 / 4, a1 = s1 % 4, c1 = s1 / 16, b1 = s1 % 16;
+      __builtin_amdgcn_sched_barrier(0);
+      const int lbo = olane() & 15;
+      const int la_m = lane0 >> 4, lb_m = lane0 & 15;
+      // look-ahead local row r1 (holds row s+1); for a0 < 3 it is the partial row: rows a + 4 r1 > s iff a > a0
+      if constexpr (a0 < 3) {
+        if (la_m > a0)
+          dpp_row<b0, c0, true, T>(K[r1 * 4], K[r1 * 4 + 1], K[r1 * 4 + 2], K[r1 * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+      } else {
+        dpp_row<b0, c0, true, T>(K[r1 * 4], K[r1 * 4 + 1], K[r1 * 4 + 2], K[r1 * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+      }
+      cbar();
+      if (la_m == a1) {
+#pragma unroll
+        for (int c = c1; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lbo] = K[r1 * 4 + c];
+      }
+      cbar();
+      T xn[4];
+#pragma unroll
+      for (int c = c1; c < 4; ++c) xn[c] = L.rowbuf[s1 & 1][c * 16 + lbo];
+      cbar();
+      const T pivn = readlane(K[r1 * 4 + c1], a1 * 16 + b1);
+      T invdn = pivot_inv(pivn);
+      asm volatile("" : "+v"(invdn));  // materialise the reciprocal here, ahead of the bulk rows
+      sfor<r1 + 1, 16>([&](auto r_) {
+        constexpr int r = decltype(r_)::value;
+        if constexpr (((r - r1 - 1) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        dpp_row<b0, c0, false, T>(K[r * 4], K[r * 4 + 1], K[r * 4 + 2], K[r * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = c1; c < 4; ++c) {
+        const T mv = -(xn[c] * invdn);
+        mm[c] = c == c1 ? (lb_m > b1 ? mv : T(0)) : mv;
+      }
+      L.dg[s1] = pivn;
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    cbar();
+
+    // ---- pivots -> 1/d_i (same reciprocal as the factorisation); a NaN pivot is NAN_SOL
+    {
+      const T d = L.dg[lane];
+      invd_v = pivot_inv(d);
+      if (uflag(__any(d != d))) {
+        status = CMPC_NAN_SOL;
+        break;
+      }
+    }
+    // ---- factor -> row layout through LDS, 16 columns at a time, row i scaled by 1/d_i
+    sfor<0, 4>([&](auto c_) {
+      constexpr int c = decltype(c_)::value;
+      const int ol = olane();
+      const int ola = ol >> 4, olb = ol & 15;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = ola + 4 * r;
+        L.scr[i * 16 + ((((olb >> 1) + i) & 7) << 1) + (olb & 1)] = K[r * 4 + c];
+      }
+      cbar();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = ol * 16 + (((k + ol) & 7) << 1);
+        K[ridx(16 * c + 2 * k)] = L.scr[idx] * invd_v;
+        K[ridx(16 * c + 2 * k + 1)] = L.scr[idx + 1] * invd_v;
+      }
+      cbar();
+    });
+
+    // ---- predictor (affine scaling direction)
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      L.rml[j] = tl[cc] * ll[cc];
+      L.rmu[j] = tu[cc] * lu[cc];
+    }
+    direction();
+    T alpha = fmin(T(1), max_step());
+    if (m > 0) {
+      T maff = T(0);
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const int j = lane + 64 * cc;
+        const bool on = j < m;
+        const T v = (tl[cc] + alpha * dtl[cc]) * (ll[cc] + alpha * dll[cc]) +
+                    (tu[cc] + alpha * dtu[cc]) * (lu[cc] + alpha * dlu[cc]);
+        maff += on ? v : T(0);
+      }
+      maff = wave_sum(maff) / T(2 * m);
+      const T ratio = maff / mu;
+      const T sigma = ratio * ratio * ratio;
+      // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const int j = lane + 64 * cc;
+        const bool on = j < m;
+        L.rml[j] = on ? tl[cc] * ll[cc] + dtl[cc] * dll[cc] - sigma * mu : T(0);
+        L.rmu[j] = on ? tu[cc] * lu[cc] + dtu[cc] * dlu[cc] - sigma * mu : T(0);
+      }
+      direction();
+      alpha = fmin(T(1), T(TAU) * max_step());
+    }
+    if (uflag(alpha < T(S.alpha_min))) {
+      status = CMPC_MIN_STEP;
+      break;
+    }
+    u_v = fma(alpha, du_v, u_v);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      tl[cc] = fma(alpha, dtl[cc], tl[cc]);
+      tu[cc] = fma(alpha, dtu[cc], tu[cc]);
+      ll[cc] = fma(alpha, dll[cc], ll[cc]);
+      lu[cc] = fma(alpha, dlu[cc], lu[cc]);
+    }
+  }
+
+  lane = olane();
+  const bool fin = isfinite(u_v);
+  if (lane < ld) A.u[(size_t)q * ld + lane] = vin ? u_v : T(0);
+  if (uflag(__any(!fin))) status = CMPC_NAN_SOL;
+  if (lane == 0) {
+    A.status[q] = status;
+    A.iters[q] = it;
+  }
+}
+
+}  // namespace cmpc

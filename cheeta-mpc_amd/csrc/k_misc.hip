@@ -416,7 +416,7 @@ __global__ __launch_bounds__(256) void k_unpack_qp(const T* H_ws, const T* g_ws,
   double* ho = H + (size_t)q * ld * ld;
   for (int e = threadIdx.x; e < ld * ld; e += blockDim.x) {
     const int r = e / ld, c = e % ld;
-    ho[e] = (r < np && c < np) ? (double)hq[r * np + c] : (r == c ? 1.0 : 0.0);
+    ho[e] = (r < np && c < np) ? (double)hq[h_index(np, r, c)] : (r == c ? 1.0 : 0.0);
   }
   for (int i = threadIdx.x; i < ld; i += blockDim.x) g[(size_t)q * ld + i] = i < np ? (double)g_ws[(size_t)q * ld + i] : 0.0;
 }
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void k_pack_qp(const double* H, const double* 
       T v;
       if (r < n && c < n) v = (T)H[(size_t)q * ld * ld + (size_t)r * ld + c];
       else v = r == c ? T(1) : T(0);
-      H_ws[(size_t)q * ld * ld + e] = v;
+      H_ws[(size_t)q * ld * ld + h_index(np, r, c)] = v;
     }
     for (int i = threadIdx.x; i < ld; i += blockDim.x) g_ws[(size_t)q * ld + i] = i < n ? (T)g[(size_t)q * ld + i] : T(0);
     for (int t = threadIdx.x; t < nt; t += blockDim.x) {
