@@ -167,6 +167,7 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.tri_map = c->tri_map;
   a.nvar = c->nvar;
   a.status = c->status;
+  a.skip_le64 = 0;
   return a;
 }
 
@@ -187,11 +188,27 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   return a;
 }
 
+// n <= 64 QPs go through the one-wave condensing kernel (possible only for N <= 21); the workgroup kernel serves
+// the 128 class and skips what the first one already did.
+template <typename T>
+int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                   const uint8_t* contact, hipStream_t st) {
+  CondenseArgs<T> a = condense_args<T>(c, x0, xref, foot, contact);
+  int r = 0;
+  const bool small = c->model.N <= CMPC_C64_MAXN;
+  if (small) r = launch_condense64<T>(a, B, st);
+  if (r == 0 && (c->ld > 64 || !small)) {
+    a.skip_le64 = small ? 1 : 0;
+    r = launch_srbd_condense<T>(a, B, st);
+  }
+  return r;
+}
+
 int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                  const uint8_t* contact, hipStream_t st) {
   int r;
-  if (c->precision == CMPC_F64) r = launch_srbd_condense<double>(condense_args<double>(c, x0, xref, foot, contact), B, st);
-  else r = launch_srbd_condense<float>(condense_args<float>(c, x0, xref, foot, contact), B, st);
+  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st);
+  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st);
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 

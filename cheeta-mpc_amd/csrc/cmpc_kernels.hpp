@@ -40,6 +40,7 @@ struct CondenseArgs {
   int* tri_map;
   int* nvar;
   int* status;
+  int skip_le64;  // k_srbd_condense: leave valid QPs with n <= 64 to k_condense64 (already done)
 };
 
 template <typename T>
@@ -59,6 +60,10 @@ struct IpmArgs {
 
 template <typename T>
 int launch_srbd_condense(const CondenseArgs<T>& a, int B, hipStream_t stream);
+// n <= 64 QPs, one wavefront each (k_condense64.hip); QPs with n > 64 are left to launch_srbd_condense
+template <typename T>
+int launch_condense64(const CondenseArgs<T>& a, int B, hipStream_t stream);
+#define CMPC_C64_MAXN 21
 
 // Runs every IPM size class over the batch; each QP is served by the class matching its condensed size.
 template <typename T>

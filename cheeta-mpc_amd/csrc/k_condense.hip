@@ -137,6 +137,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
   int st = CMPC_SUCCESS;
   if (s_flag) st = CMPC_INVALID_CONTACT;
   else if (n > NMAX || n > CMPC_IPM_MAX_N) st = CMPC_TOO_LARGE;
+  if (st == CMPC_SUCCESS && a.skip_le64 && n <= 64) return;  // served by k_condense64
   if (st != CMPC_SUCCESS) {
     if (tid == 0) {
       a.status[q] = st;
