@@ -185,6 +185,7 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.iters = c->iters;
   a.u = (T*)c->u;
   a.s = dev_settings(c->settings);
+  a.stamps = nullptr;
   return a;
 }
 

@@ -56,6 +56,7 @@ struct IpmArgs {
   int* iters;
   T* u;         // [B][ld]
   DevSettings s;
+  unsigned long long* stamps;  // diagnostic builds only (-DCMPC_IPM_STAMPS): per-QP phase cycles, else null
 };
 
 template <typename T>

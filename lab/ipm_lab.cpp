@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "cmpc/cmpc.h"
@@ -146,26 +147,39 @@ int main(int argc, char** argv) {
   std::vector<double> hu((size_t)B * ld);
   std::vector<int> hs(B), hit(B);
   std::vector<unsigned long long> hst((size_t)B * 9);
-  for (const Var& v : VARS) {
-    if (only && !strstr(v.name, only)) continue;
-    float tot = 0.f, best = 1e30f;
-    IpmArgs<double> va;
-    CC(v.prep(&a, B, st, &va));
+  // interleaved timing: every round launches each variant once (round-robin), after a warm-up of the GPU clock;
+  // medians over rounds are robust to DVFS drift between variants
+  std::vector<int> sel;
+  const int nv = (int)(sizeof(VARS) / sizeof(VARS[0]));
+  for (int i = 0; i < nv; ++i)
+    if (!only || strstr(VARS[i].name, only)) sel.push_back(i);
+  std::vector<IpmArgs<double>> vargs(nv);
+  for (int i : sel) {
+    CC(VARS[i].prep(&a, B, st, &vargs[i]));
     CK(hipStreamSynchronize(st));
-    for (int r = -2; r < reps; ++r) {
-      CK(hipMemcpyAsync(sw, s0, B * 4, hipMemcpyDeviceToDevice, st));
-      CK(hipMemsetAsync(uw, 0, (size_t)B * ld * 8, st));
-      CK(hipEventRecord(e0, st));
-      CC(v.fn(&va, B, st, v.stamps ? stamps : nullptr));
-      CK(hipEventRecord(e1, st));
-      CK(hipEventSynchronize(e1));
-      float ms = 0.f;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      if (r >= 0) {
-        tot += ms;
-        if (ms < best) best = ms;
-      }
-    }
+  }
+  auto run_once = [&](int i, bool with_stamps) -> float {
+    CK(hipMemcpyAsync(sw, s0, B * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemsetAsync(uw, 0, (size_t)B * ld * 8, st));
+    CK(hipEventRecord(e0, st));
+    CC(VARS[i].fn(&vargs[i], B, st, with_stamps ? stamps : nullptr));
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms;
+  };
+  for (int w = 0; w < 30; ++w)
+    for (int i : sel) run_once(i, false);
+  std::vector<std::vector<float>> times(nv);
+  for (int r = 0; r < reps; ++r)
+    for (int i : sel) times[i].push_back(run_once(i, false));
+  for (int i : sel) {
+    const Var& v = VARS[i];
+    std::vector<float> t = times[i];
+    std::sort(t.begin(), t.end());
+    const float med = t[t.size() / 2], best = t[0];
+    run_once(i, v.stamps != 0);  // final run: results (+ stamps)
     CK(hipMemcpy(hu.data(), uw, hu.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hs.data(), sw, B * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hit.data(), iw, B * 4, hipMemcpyDeviceToHost));
@@ -173,29 +187,27 @@ int main(int argc, char** argv) {
     int same_it = 0, same_st = 0, bitexact = 0;
     for (int q = 0; q < B; ++q) {
       double sc = 1.0, d = 0.0;
-      for (int i = 0; i < ld; ++i) sc = fmax(sc, fabs(hu_ref[(size_t)q * ld + i]));
+      for (int k = 0; k < ld; ++k) sc = fmax(sc, fabs(hu_ref[(size_t)q * ld + k]));
       bool be = true;
-      for (int i = 0; i < ld; ++i) {
-        d = fmax(d, fabs(hu[(size_t)q * ld + i] - hu_ref[(size_t)q * ld + i]));
-        be = be && hu[(size_t)q * ld + i] == hu_ref[(size_t)q * ld + i];
+      for (int k = 0; k < ld; ++k) {
+        d = fmax(d, fabs(hu[(size_t)q * ld + k] - hu_ref[(size_t)q * ld + k]));
+        be = be && hu[(size_t)q * ld + k] == hu_ref[(size_t)q * ld + k];
       }
-      if (!(d / sc <= maxrel)) maxrel = d / sc;  // NaN-propagating max
+      if (!(d / sc <= maxrel)) maxrel = d / sc;
       same_it += hit[q] == hi_ref[q];
       same_st += hs[q] == hs_ref[q];
       bitexact += be;
     }
-    printf("{\"variant\": \"%s\", \"ms_mean\": %.5f, \"ms_best\": %.5f, \"qps_ipm\": %.0f, \"max_rel_du\": %.3e, "
+    printf("{\"variant\": \"%s\", \"ms_median\": %.5f, \"ms_best\": %.5f, \"qps_ipm\": %.0f, \"max_rel_du\": %.3e, "
            "\"same_status\": %d, \"same_iters\": %d, \"bitexact\": %d",
-           v.name, tot / reps, best, B / (tot / reps * 1e-3), maxrel, same_st, same_it, bitexact);
+           v.name, med, best, B / (med * 1e-3), maxrel, same_st, same_it, bitexact);
     if (v.stamps) {
       CK(hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost));
       double seg[9] = {0}, its = 0;
-      int cnt = 0;
       for (int q = 0; q < B; ++q) {
         if (hs[q] != 0) continue;
         for (int k = 0; k < 9; ++k) seg[k] += (double)hst[(size_t)q * 9 + k];
         its += hit[q];
-        ++cnt;
       }
       static const char* names[9] = {"s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "total"};
       printf(", \"cycles_per_iter\": {");

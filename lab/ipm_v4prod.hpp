@@ -30,47 +30,10 @@
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
 #include "dpp_rows.hpp"
-#include "wave_dpp.hpp"
-
-// In-kernel s_memtime stamps, diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP cycles of each
-// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 transpose, 4 sweeps,
-// 5 predictor rest, 6 corrector rest, 7 update, 8 total.
-#ifdef CMPC_IPM_STAMPS
-#define IPM_STAMP_DECL                                                    \
-  unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};              \
-  const unsigned long long st_t0_ = ipm64::memtime();                   \
-  unsigned long long st_prev_ = st_t0_
-#define IPM_STAMP(k)                                      \
-  do {                                                    \
-    const unsigned long long t_ = ipm64::memtime();       \
-    st_acc_[k] += t_ - st_prev_;                          \
-    st_prev_ = t_;                                        \
-  } while (0)
-#define IPM_STAMP_STORE(ptr, q)                                                   \
-  do {                                                                            \
-    const unsigned long long t_ = ipm64::memtime();                               \
-    if ((ptr) && threadIdx.x == 0) {                                              \
-      for (int k_ = 0; k_ < 8; ++k_) (ptr)[(size_t)(q) * 9 + k_] = st_acc_[k_];   \
-      (ptr)[(size_t)(q) * 9 + 8] = t_ - st_t0_;                                   \
-    }                                                                             \
-  } while (0)
-#else
-#define IPM_STAMP_DECL (void)0
-#define IPM_STAMP(k) (void)0
-#define IPM_STAMP_STORE(ptr, q) (void)0
-#endif
 
 namespace cmpc {
 
 namespace ipm64 {
-
-__device__ __forceinline__ unsigned long long memtime() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
 
 template <typename T>
 struct Lim;
@@ -140,7 +103,6 @@ struct Lds {
 template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   using namespace ipm64;
-  IPM_STAMP_DECL;
   const int q = blockIdx.x;
   if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
   const int n = A.nvar[q];
@@ -231,20 +193,8 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     cbar();
   };
 
-  const T* Hq = A.H + (size_t)q * ld * ld;
-  // H in tile order (64 coalesced 512-B rows) into the registers of the factor
-  auto load_H = [&]() {
-    const int ln = olane();
-#pragma unroll
-    for (int e = 0; e < 64; ++e) K[e] = Hq[e * 64 + ln];
-  };
-
-  // Newton direction for the complementarity targets in L.rml / L.rmu. After the iteration's last solve the factor
-  // is dead: the next iteration's H is requested right there, so its latency hides behind the step-length work.
-  auto direction = [&](auto last_, auto seg_) {
-    constexpr bool last = decltype(last_)::value;
-    constexpr int seg = decltype(seg_)::value;
-    (void)seg;
+  // Newton direction for the complementarity targets in L.rml / L.rmu
+  auto direction = [&]() {
     T wv[2];
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
@@ -253,9 +203,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     }
     const T ctw = apply_CT(wv);
     du_v = -rg_v - ctw;
-    IPM_STAMP(seg);
     solve(du_v);
-    IPM_STAMP(4);
     L.v[lane] = du_v;
     cbar();
     T cdu[2];
@@ -279,43 +227,24 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       if (dll[cc] < T(0)) am = fmin(am, -ll[cc] / dll[cc]);
       if (dlu[cc] < T(0)) am = fmin(am, -lu[cc] / dlu[cc]);
     }
-    return wave_min_dpp(am);
+    return wave_min(am);
   };
 
+  const T* Hq = A.H + (size_t)q * ld * ld;
   int status = CMPC_MAX_ITER;
   int it = 0;
   for (it = 0;; ++it) {
-    load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
     lane = olane();
     const int la = lane >> 4, lb = lane & 15;
+    // ---- H in tile order (64 coalesced 512-B rows)
+#pragma unroll
+    for (int e = 0; e < 64; ++e) K[e] = Hq[e * 64 + lane];
 
-    // ---- residuals that do not need H: C u, slack/complementarity residuals, C' lam
+    // ---- residuals. Hu from the tile: 16 partial row sums per lane, reduced through LDS (row i's 16 partials
+    //      at i*16 + rotated 16-B slot, so both the writes and the row reads are conflict-free)
+    T hu = T(0);
     L.v[lane] = u_v;
     cbar();
-    T cu[2];
-    apply_C(cu);
-    T rs = T(0), ri = T(0), rc = T(0), ms = T(0);
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const int j = lane + 64 * cc;
-      const bool on = j < m;
-      const T rl = on ? cu[cc] - lo[cc] - tl[cc] : T(0);
-      const T ru = on ? hi[cc] - cu[cc] - tu[cc] : T(0);
-      L.rl[j] = rl;
-      L.ru[j] = ru;
-      ri = fmax(ri, fmax(fabs(rl), fabs(ru)));
-      const T cl = tl[cc] * ll[cc], ch = tu[cc] * lu[cc];
-      rc = fmax(rc, fmax(cl, ch));
-      ms += cl + ch;
-    }
-    T ctw;
-    {
-      const T wv[2] = {ll[0] - lu[0], ll[1] - lu[1]};
-      ctw = apply_CT(wv);
-    }
-    // ---- Hu from the tile: 16 partial row sums per lane, reduced through LDS (row i's 16 partials at i*16 +
-    //      rotated 16-B slot, so both the writes and the row reads are conflict-free)
-    T hu = T(0);
     {
       T uc[4];
 #pragma unroll
@@ -337,12 +266,33 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       }
       cbar();
     }
-    rg_v = vin ? hu + g_v - ctw : T(0);
-    rs = fabs(rg_v);
-    rs = wave_max_dpp(rs);
-    ri = wave_max_dpp(ri);
-    rc = wave_max_dpp(rc);
-    ms = wave_sum_dpp(ms);
+    T cu[2];
+    apply_C(cu);  // L.v still holds u
+    cbar();
+    T rs = T(0), ri = T(0), rc = T(0), ms = T(0);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane + 64 * cc;
+      const bool on = j < m;
+      const T rl = on ? cu[cc] - lo[cc] - tl[cc] : T(0);
+      const T ru = on ? hi[cc] - cu[cc] - tu[cc] : T(0);
+      L.rl[j] = rl;
+      L.ru[j] = ru;
+      ri = fmax(ri, fmax(fabs(rl), fabs(ru)));
+      const T cl = tl[cc] * ll[cc], ch = tu[cc] * lu[cc];
+      rc = fmax(rc, fmax(cl, ch));
+      ms += cl + ch;
+    }
+    {
+      const T wv[2] = {ll[0] - lu[0], ll[1] - lu[1]};
+      const T ctw = apply_CT(wv);
+      rg_v = vin ? hu + g_v - ctw : T(0);
+      rs = fabs(rg_v);
+    }
+    rs = wave_max(rs);
+    ri = wave_max(ri);
+    rc = wave_max(rc);
+    ms = wave_sum(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
     if (uflag(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
       status = CMPC_NAN_SOL;
@@ -361,7 +311,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       status = CMPC_MIN_STEP;
       break;
     }
-    IPM_STAMP(0);
 
     // ---- Newton matrix K = H + C' diag(lam_l/t_l + lam_u/t_u) C + reg I: lane j writes the 3x3 block row of
     //      variable j, tile lanes add it where entry (i, j) falls in j's force triple
@@ -415,7 +364,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       });
     });
     cbar();
-    IPM_STAMP(1);
 
     // ---- LDL' factorisation in the tile (see header)
     T piv = readlane(K[0], 0);
@@ -441,7 +389,8 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       constexpr int s1 = s + 1;
       constexpr int r1 = s1 / 4, a1 = s1 % 4, c1 = s1 / 16, b1 = s1 % 16;
       __builtin_amdgcn_sched_barrier(0);
-      const int la_m = lane0 >> 4, lb_m = lane0 & 15;  // masks and rowbuf addresses: hoisted, loop invariant
+      const int lbo = olane() & 15;
+      const int la_m = lane0 >> 4, lb_m = lane0 & 15;
       // look-ahead local row r1 (holds row s+1); for a0 < 3 it is the partial row: rows a + 4 r1 > s iff a > a0
       if constexpr (a0 < 3) {
         if (la_m > a0)
@@ -452,12 +401,12 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       cbar();
       if (la_m == a1) {
 #pragma unroll
-        for (int c = c1; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lb_m] = K[r1 * 4 + c];
+        for (int c = c1; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lbo] = K[r1 * 4 + c];
       }
       cbar();
       T xn[4];
 #pragma unroll
-      for (int c = c1; c < 4; ++c) xn[c] = L.rowbuf[s1 & 1][c * 16 + lb_m];
+      for (int c = c1; c < 4; ++c) xn[c] = L.rowbuf[s1 & 1][c * 16 + lbo];
       cbar();
       const T pivn = readlane(K[r1 * 4 + c1], a1 * 16 + b1);
       T invdn = pivot_inv(pivn);
@@ -477,7 +426,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     });
     __builtin_amdgcn_sched_barrier(0);
     cbar();
-    IPM_STAMP(2);
 
     // ---- pivots -> 1/d_i (same reciprocal as the factorisation); a NaN pivot is NAN_SOL
     {
@@ -507,7 +455,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       }
       cbar();
     });
-    IPM_STAMP(3);
 
     // ---- predictor (affine scaling direction)
 #pragma unroll
@@ -516,10 +463,9 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       L.rml[j] = tl[cc] * ll[cc];
       L.rmu[j] = tu[cc] * lu[cc];
     }
-    direction(std::false_type{}, std::integral_constant<int, 5>{});
-    T alpha;
+    direction();
+    T alpha = fmin(T(1), max_step());
     if (m > 0) {
-      alpha = fmin(T(1), max_step());
       T maff = T(0);
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
@@ -529,10 +475,9 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
                     (tu[cc] + alpha * dtu[cc]) * (lu[cc] + alpha * dlu[cc]);
         maff += on ? v : T(0);
       }
-      maff = wave_sum_dpp(maff) / T(2 * m);
+      maff = wave_sum(maff) / T(2 * m);
       const T ratio = maff / mu;
       const T sigma = ratio * ratio * ratio;
-      IPM_STAMP(5);
       // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
@@ -541,12 +486,9 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
         L.rml[j] = on ? tl[cc] * ll[cc] + dtl[cc] * dll[cc] - sigma * mu : T(0);
         L.rmu[j] = on ? tu[cc] * lu[cc] + dtu[cc] * dlu[cc] - sigma * mu : T(0);
       }
-      direction(std::false_type{}, std::integral_constant<int, 6>{});
+      direction();
       alpha = fmin(T(1), T(TAU) * max_step());
-    } else {
-      alpha = fmin(T(1), max_step());
     }
-    IPM_STAMP(6);
     if (uflag(alpha < T(S.alpha_min))) {
       status = CMPC_MIN_STEP;
       break;
@@ -559,7 +501,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       ll[cc] = fma(alpha, dll[cc], ll[cc]);
       lu[cc] = fma(alpha, dlu[cc], lu[cc]);
     }
-    IPM_STAMP(7);
   }
 
   lane = olane();
@@ -570,7 +511,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     A.status[q] = status;
     A.iters[q] = it;
   }
-  IPM_STAMP_STORE(A.stamps, q);
 }
 
 }  // namespace cmpc

@@ -111,13 +111,28 @@ __device__ __forceinline__ bool uflag(bool b) { return __builtin_amdgcn_readfirs
 
 __device__ __forceinline__ double rcp_raw(double x) { return __builtin_amdgcn_rcp(x); }
 __device__ __forceinline__ float rcp_raw(float x) { return __builtin_amdgcn_rcpf(x); }
-// reciprocal of a pivot: hardware estimate + one Newton step, 0 for pivots at or below the guard (and NaN)
+// Pivot guard on the bit pattern (positive pivots order like their bits): d > 1e-200 (fp64) / 1e-30 (fp32); NaN passes
+// and propagates into the factor, where the NaN-pivot check catches it.
+__device__ __forceinline__ bool pivot_ok(double p) {
+  return (int)(__builtin_bit_cast(unsigned long long, p) >> 32) > 0x16687E92;
+}
+__device__ __forceinline__ bool pivot_ok(float p) { return __builtin_bit_cast(int, p) > 0x0DA24260; }
+// reciprocal of a pivot: hardware estimate + one Newton step on a clamped input, 0 for guarded pivots. For a
+// wave-uniform pivot (the factorisation) the clamp and the 0/1 factor stay on the scalar unit.
 template <typename T>
 __device__ __forceinline__ T pivot_inv(T p) {
-  T y = rcp_raw(p);
-  const T e = fma(-p, y, T(1));
+#ifdef A5_NOGUARD
+  T y0 = rcp_raw(p);
+  const T e0 = fma(-p, y0, T(1));
+  y0 = fma(y0, e0, y0);
+  return p > T(Lim<T>::pivot_min) ? y0 : T(0);
+#endif
+  const bool ok = pivot_ok(p);
+  const T pc = ok ? p : T(1);
+  T y = rcp_raw(pc);
+  const T e = fma(-pc, y, T(1));
   y = fma(y, e, y);
-  return p > T(Lim<T>::pivot_min) ? y : T(0);
+  return y * (ok ? T(1) : T(0));
 }
 
 // row-layout column j after the transpose lives in the register the tile used for column j's chunk
@@ -279,7 +294,11 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       if (dll[cc] < T(0)) am = fmin(am, -ll[cc] / dll[cc]);
       if (dlu[cc] < T(0)) am = fmin(am, -lu[cc] / dlu[cc]);
     }
+#ifdef A5_NODPP
+    return wave_min(am);
+#else
     return wave_min_dpp(am);
+#endif
   };
 
   int status = CMPC_MAX_ITER;
@@ -339,10 +358,17 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     }
     rg_v = vin ? hu + g_v - ctw : T(0);
     rs = fabs(rg_v);
+#ifdef A5_NODPP
+    rs = wave_max(rs);
+    ri = wave_max(ri);
+    rc = wave_max(rc);
+    ms = wave_sum(ms);
+#else
     rs = wave_max_dpp(rs);
     ri = wave_max_dpp(ri);
     rc = wave_max_dpp(rc);
     ms = wave_sum_dpp(ms);
+#endif
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
     if (uflag(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
       status = CMPC_NAN_SOL;
@@ -442,6 +468,11 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       constexpr int r1 = s1 / 4, a1 = s1 % 4, c1 = s1 / 16, b1 = s1 % 16;
       __builtin_amdgcn_sched_barrier(0);
       const int la_m = lane0 >> 4, lb_m = lane0 & 15;  // masks and rowbuf addresses: hoisted, loop invariant
+#ifdef A5_NOLANE0
+      const int lbo = olane() & 15;
+#else
+      const int lbo = lb_m;
+#endif
       // look-ahead local row r1 (holds row s+1); for a0 < 3 it is the partial row: rows a + 4 r1 > s iff a > a0
       if constexpr (a0 < 3) {
         if (la_m > a0)
@@ -452,12 +483,12 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       cbar();
       if (la_m == a1) {
 #pragma unroll
-        for (int c = c1; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lb_m] = K[r1 * 4 + c];
+        for (int c = c1; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lbo] = K[r1 * 4 + c];
       }
       cbar();
       T xn[4];
 #pragma unroll
-      for (int c = c1; c < 4; ++c) xn[c] = L.rowbuf[s1 & 1][c * 16 + lb_m];
+      for (int c = c1; c < 4; ++c) xn[c] = L.rowbuf[s1 & 1][c * 16 + lbo];
       cbar();
       const T pivn = readlane(K[r1 * 4 + c1], a1 * 16 + b1);
       T invdn = pivot_inv(pivn);
@@ -529,7 +560,11 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
                     (tu[cc] + alpha * dtu[cc]) * (lu[cc] + alpha * dlu[cc]);
         maff += on ? v : T(0);
       }
+#ifdef A5_NODPP
+      maff = wave_sum(maff) / T(2 * m);
+#else
       maff = wave_sum_dpp(maff) / T(2 * m);
+#endif
       const T ratio = maff / mu;
       const T sigma = ratio * ratio * ratio;
       IPM_STAMP(5);

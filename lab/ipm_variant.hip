@@ -7,6 +7,10 @@
 #define LAB_STR(x) LAB_STR2(x)
 #define LAB_CAT2(a, b) a##b
 #define LAB_CAT(a, b) LAB_CAT2(a, b)
+#ifdef LAB_PRODUCT
+// the product kernel also lives in libcmpc.so (the lab's reference): give this copy its own name
+#define k_ipm64 LAB_CAT(k_ipm64_, LAB_FN)
+#endif
 #include LAB_STR(LAB_HDR)
 
 #ifndef LAB_WPE
@@ -14,18 +18,27 @@
 #endif
 
 extern "C" int LAB_FN(const cmpc::IpmArgs<double>* a, int B, hipStream_t s, unsigned long long* stamps) {
+#ifdef LAB_PRODUCT  // the product kernel (csrc/k_ipm64.hpp); stamps through IpmArgs when built with CMPC_IPM_STAMPS
+  cmpc::IpmArgs<double> b = *a;
+  b.stamps = stamps;
+  hipLaunchKernelGGL((cmpc::LAB_CAT(k_ipm64_, LAB_FN)<double, LAB_WPE>), dim3(B), dim3(64), 0, s, b);
+#else
   hipLaunchKernelGGL((k_ipm_reg<double, 64, LAB_WPE>), dim3(B), dim3(64), 0, s, *a, stamps);
+#endif
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // optional input re-layout (not timed): returns args pointing at a variant-owned copy
 extern "C" int LAB_CAT(LAB_FN, _prep)(const cmpc::IpmArgs<double>* a, int B, hipStream_t s, cmpc::IpmArgs<double>* out) {
   *out = *a;
-#ifdef LAB_PREP2D
+#if defined(LAB_PREP2D) && !defined(LAB_PRODUCT)
   static double* H2 = nullptr;
   if (!H2 && hipMalloc((void**)&H2, (size_t)B * a->ld * a->ld * sizeof(double)) != hipSuccess) return -2;
   hipLaunchKernelGGL(k_prep2d<double>, dim3(B), dim3(64), 0, s, a->H, H2, a->nvar, a->ld);
   out->H = H2;
+#endif
+#ifdef LAB_PRODUCT  // the product packs H in tile order already (launch_pack_qp -> h_index)
+  out->stamps = nullptr;
 #endif
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
