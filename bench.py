@@ -54,6 +54,18 @@ def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_
     return u, st, wall, done
 
 
+def pmc_traffic(path, prefix):
+    """HBM bytes per launch of the IPM stage from the committed rocprofv3 --pmc summary (profiles/rNN_traffic.json,
+    written by cheeta-mpc_amd/tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes of this same
+    command). PMC counters cannot be read inside a normal run, so the value comes from the profiled run."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        ks = json.load(f)["kernels"]
+    tot = sum(v["hbm_bytes"] for k, v in ks.items() if prefix in k)
+    return tot if tot > 0 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -65,6 +77,8 @@ def main():
     ap.add_argument("--gait", type=int, default=0, help="0 trot (configs 2-4), 1 mixed trot/bound/pronk (config 5)")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="QPs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
+                    help="PMC summary giving roofline.traffic (used only for the default headline workload)")
     args = ap.parse_args()
 
     import cheeta_mpc as cm
@@ -120,6 +134,9 @@ def main():
     peak = FP64_PEAK if prec == cm.F64 else FP32_PEAK
     achieved = flops_launch / (ms_ipm * 1e-3) if ms_ipm > 0 else 0.0
 
+    headline = (B == 4096 and N == 10 and prec == cm.F64 and args.gait == 0)
+    traffic = pmc_traffic(args.traffic_json, "k_ipm") if headline else None
+
     value = world * B * args.steps / elapsed
     result = {
         "metric": "centroidal QPs/sec (N=10, 13-state/12-input) at batch=4096; max|du| vs HPIPM",
@@ -140,7 +157,7 @@ def main():
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
         "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "k_ipm_reg (IPM stage)",
                      "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": None,
+                     "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
                      "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
         "stages_ms": {"condense": ms_cond, "ipm": ms_ipm, "expand": ms_exp},
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,

@@ -14,4 +14,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --stats -d $O/pmc_$c -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-sample 0 > $O/pmc_$c.log 2>&1; rc=$?; echo "pmc_$c exit=$rc"; fatal $rc pmc_$c
 done
-echo all_done
+python3 $R/cheeta-mpc_amd/tools/pmc_traffic.py $O $O/traffic.json && echo all_done
