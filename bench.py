@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--gait", type=int, default=0, help="0 trot (configs 2-4), 1 mixed trot/bound/pronk (config 5)")
+    ap.add_argument("--all-stance", action="store_true",
+                    help="every leg in stance at every step (pronk): n = 12 N, the largest condensed size class")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="QPs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
@@ -97,6 +99,8 @@ def main():
         settings = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3, tol_comp=1e-4)
     eng = cm.Engine(model, settings, precision=prec, max_batch=B)
     x0, xref, foot, contact = cm.generate_device(model, SEED, B, gait=args.gait, offset=rank * B)
+    if args.all_stance:
+        contact.upload(np.ones((B, N, 4), np.uint8))
     u = cm.DeviceArray((B, N, 4, 3), np.float64)
     st = cm.DeviceArray((B,), np.int32)
     it = cm.DeviceArray((B,), np.int32)
@@ -134,7 +138,7 @@ def main():
     peak = FP64_PEAK if prec == cm.F64 else FP32_PEAK
     achieved = flops_launch / (ms_ipm * 1e-3) if ms_ipm > 0 else 0.0
 
-    headline = (B == 4096 and N == 10 and prec == cm.F64 and args.gait == 0)
+    headline = (B == 4096 and N == 10 and prec == cm.F64 and args.gait == 0 and not args.all_stance)
     traffic = pmc_traffic(args.traffic_json, "k_ipm") if headline else None
 
     value = world * B * args.steps / elapsed
@@ -152,10 +156,10 @@ def main():
         "dtype": "f64" if prec == cm.F64 else "f32",
         "data": "synthetic (Philox4x32-10 counter-based generator, seed 20221125, CentoidMPCTest params)",
         "config": {"workload": f"batch {B} QPs/GPU, N={N}, 13-state/12-input SRBD, "
-                               f"{'4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk'}, "
+                               f"{'all-stance (pronk)' if args.all_stance else ('4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk')}, "
                                f"{'fp64' if prec == cm.F64 else 'fp32'}, full hot path per step",
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
-        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "k_ipm_reg (IPM stage)",
+        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "IPM stage (k_ipm64 n<=64, k_ipm_reg n<=128, k_ipm256 n<=256)",
                      "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
                      "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},

@@ -59,7 +59,7 @@ namespace {
 
 int ld_for(const cmpc_model& m) {
   const int nf = CMPC_NU * m.N;
-  return nf <= 64 ? 64 : 128;
+  return nf <= 64 ? 64 : (nf <= 128 ? 128 : 256);
 }
 
 struct Layout {
@@ -167,7 +167,7 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.tri_map = c->tri_map;
   a.nvar = c->nvar;
   a.status = c->status;
-  a.skip_le64 = 0;
+  a.n_lo = 0;
   return a;
 }
 
@@ -190,7 +190,7 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
 }
 
 // n <= 64 QPs go through the one-wave condensing kernel (possible only for N <= 21); the workgroup kernel serves
-// the 128 class and skips what the first one already did.
+// the 128 and 256 classes, each launch skipping at once what a smaller class already did (nvar hints).
 template <typename T>
 int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                    const uint8_t* contact, hipStream_t st) {
@@ -199,8 +199,12 @@ int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, con
   const bool small = c->model.N <= CMPC_C64_MAXN;
   if (small) r = launch_condense64<T>(a, B, st);
   if (r == 0 && (c->ld > 64 || !small)) {
-    a.skip_le64 = small ? 1 : 0;
-    r = launch_srbd_condense<T>(a, B, st);
+    a.n_lo = small ? 64 : 0;
+    r = launch_srbd_condense<T>(a, c->ld >= 128 ? 128 : 64, B, st);
+  }
+  if (r == 0 && c->ld > 128) {
+    a.n_lo = 128;
+    r = launch_srbd_condense<T>(a, 256, B, st);
   }
   return r;
 }

@@ -8,15 +8,15 @@
 
 namespace cmpc {
 
-// largest condensed size served by an IPM size class (classes: n <= 64, 64 < n <= 128)
-#define CMPC_IPM_MAX_N 128
+// largest condensed size served by an IPM size class (classes: n <= 64, 64 < n <= 128, 128 < n <= 256)
+#define CMPC_IPM_MAX_N 256
 
 // class-padded size of a condensed problem
-__host__ __device__ inline int ipm_class(int n) { return n <= 64 ? 64 : 128; }
+__host__ __device__ inline int ipm_class(int n) { return n <= 64 ? 64 : (n <= 128 ? 128 : 256); }
 
 // Position of H[i][j] inside a QP's class-packed block. Class 64 is stored in the 4 x 16-cyclic register order of
 // k_ipm64 (element (i, j) is register 4*(i/4) + j/16 of lane 16*(i%4) + j%16), so each of that kernel's 64 loads
-// is one contiguous 512-B row; class 128 is row-major with stride 128.
+// is one contiguous 512-B row; classes 128 and 256 are row-major with stride npad.
 __host__ __device__ inline int h_index(int npad, int i, int j) {
   return npad == 64 ? (((i >> 2) * 4 + (j >> 4)) * 64 + (i & 3) * 16 + (j & 15)) : i * npad + j;
 }
@@ -40,7 +40,8 @@ struct CondenseArgs {
   int* tri_map;
   int* nvar;
   int* status;
-  int skip_le64;  // k_srbd_condense: leave valid QPs with n <= 64 to k_condense64 (already done)
+  int n_lo;       // k_srbd_condense serves n_lo < n <= NMAX; when n_lo > 0 a smaller class ran first and left
+                  // nvar[q] = n for every QP, so QPs with nvar[q] <= n_lo exit before any work
 };
 
 template <typename T>
@@ -59,8 +60,9 @@ struct IpmArgs {
   unsigned long long* stamps;  // diagnostic builds only (-DCMPC_IPM_STAMPS): per-QP phase cycles, else null
 };
 
+// one size class of the workgroup condensing kernel: npad 128 (64 < n <= 128, or n <= 128 when n_lo = 0) or 256
 template <typename T>
-int launch_srbd_condense(const CondenseArgs<T>& a, int B, hipStream_t stream);
+int launch_srbd_condense(const CondenseArgs<T>& a, int npad, int B, hipStream_t stream);
 // n <= 64 QPs, one wavefront each (k_condense64.hip); QPs with n > 64 are left to launch_srbd_condense
 template <typename T>
 int launch_condense64(const CondenseArgs<T>& a, int B, hipStream_t stream);
@@ -73,6 +75,8 @@ int launch_ipm64(const IpmArgs<double>& a, int B, hipStream_t stream);   // n <=
 int launch_ipm64(const IpmArgs<float>& a, int B, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm_impl.hpp)
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);
+int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
+int launch_ipm256(const IpmArgs<float>& a, int B, hipStream_t stream);
 
 struct ExpandArgs {
   const DevModel* model;

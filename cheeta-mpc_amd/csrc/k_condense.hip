@@ -66,6 +66,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
 
   const DevModel* __restrict__ M = a.model;
   const int q = blockIdx.x;
+  if (a.n_lo > 0 && a.nvar[q] <= a.n_lo) return;  // finished (or rejected) by a smaller class
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = M->N, L = NL;
   const int ld = a.ld;
@@ -136,8 +137,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
   const int n = 3 * nt;
   int st = CMPC_SUCCESS;
   if (s_flag) st = CMPC_INVALID_CONTACT;
-  else if (n > NMAX || n > CMPC_IPM_MAX_N) st = CMPC_TOO_LARGE;
-  if (st == CMPC_SUCCESS && a.skip_le64 && n <= 64) return;  // served by k_condense64
+  else if (n > NMAX) {
+    if (NMAX < CMPC_IPM_MAX_N) {  // a bigger class follows: leave the hint, not the status
+      if (tid == 0) a.nvar[q] = n;
+      return;
+    }
+    st = CMPC_TOO_LARGE;
+  }
+  if (st == CMPC_SUCCESS && n <= a.n_lo) return;  // served by a smaller class
   if (st != CMPC_SUCCESS) {
     if (tid == 0) {
       a.status[q] = st;
@@ -280,7 +287,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
   __syncthreads();
 
   // ---- epilogue: Rbar, identity padding, write the class-padded block of H, g and the pyramid data
-  const int npad = n <= 64 ? 64 : 128;
+  const int npad = ipm_class(n);
   T* Hq = a.H + (size_t)q * ld * ld;
 #pragma unroll
   for (int p = 0; p < TPW; ++p) {
@@ -325,14 +332,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
 }
 
 template <typename T>
-int launch_srbd_condense(const CondenseArgs<T>& a, int B, hipStream_t stream) {
+int launch_srbd_condense(const CondenseArgs<T>& a, int npad, int B, hipStream_t stream) {
   if (B <= 0) return 0;
-  switch (a.ld) {
+  if (npad > a.ld) return -1;
+  switch (npad) {
     case 64:
       hipLaunchKernelGGL((k_srbd_condense<T, 64, 4>), dim3(B), dim3(256), 0, stream, a);
       break;
     case 128:
       hipLaunchKernelGGL((k_srbd_condense<T, 128, 4>), dim3(B), dim3(256), 0, stream, a);
+      break;
+    case 256:  // 17 lower 16x16 tiles per wave; one thread per Bqp column in waves 0-3
+      hipLaunchKernelGGL((k_srbd_condense<T, 256, 8>), dim3(B), dim3(512), 0, stream, a);
       break;
     default:
       return -1;
@@ -340,7 +351,7 @@ int launch_srbd_condense(const CondenseArgs<T>& a, int B, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template int launch_srbd_condense<double>(const CondenseArgs<double>&, int, hipStream_t);
-template int launch_srbd_condense<float>(const CondenseArgs<float>&, int, hipStream_t);
+template int launch_srbd_condense<double>(const CondenseArgs<double>&, int, int, hipStream_t);
+template int launch_srbd_condense<float>(const CondenseArgs<float>&, int, int, hipStream_t);
 
 }  // namespace cmpc

@@ -21,7 +21,8 @@
 //   - upper tiles are the lower tiles transposed once through LDS; Rbar (force tracking + force-rate coupling) and
 //     the identity padding are added per lane in the epilogue;
 //   - H leaves as 64 coalesced 512-B rows per QP in the order k_ipm64 reads it (h_index).
-// QPs with n > 64 are left untouched (status not written): the 128-class path (k_condense.hip) serves them.
+// QPs with n > 64 are left to the bigger classes (k_condense.hip): their status is not written here, only nvar = n as
+// a hint, so that k_srbd_condense can drop every QP this kernel finished without re-reading its contact table.
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
 
@@ -103,7 +104,10 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
     }
     return;
   }
-  if (n > 64) return;  // 128 class
+  if (n > 64) {  // a bigger class; the hint lets its condensing kernel skip every QP handled here at once
+    if (lane == 0) a.nvar[q] = n;
+    return;
+  }
 
   // ---- triples: t-th stance (k, leg) in k-major order
   {

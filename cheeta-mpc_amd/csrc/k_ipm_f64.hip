@@ -14,6 +14,7 @@ int launch_ipm(const IpmArgs<T>& a, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   int r = launch_ipm64(a, B, stream);
   if (r == 0 && a.ld >= 128) r = launch_ipm128(a, B, stream);
+  if (r == 0 && a.ld >= 256) r = launch_ipm256(a, B, stream);
   return r;
 }
 template int launch_ipm<double>(const IpmArgs<double>&, int, hipStream_t);

@@ -105,6 +105,100 @@ def test_solve_fp32_n20(cm, op):
     assert err < 2e-3, err
 
 
+def _ragged_contacts(rng, B, N, p_stance):
+    """Random per-QP contact tables (every step keeps >= 1 stance leg): condensed sizes spread over all three IPM
+    size classes (n <= 64, 64 < n <= 128, 128 < n <= 256)."""
+    c = (rng.random((B, N, 4)) < p_stance[:, None, None]).astype(np.uint8)
+    for b in range(B):
+        for k in range(N):
+            if not c[b, k].any():
+                c[b, k, rng.integers(4)] = 1
+    return c
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_condense_large_class_matches_oracle(cm, op, precision):
+    """256 class (128 < n <= 256): all-stance N = 20 gives n = 240 (SURVEY §8 a2/a3 sizes)."""
+    N = 20
+    m, mo = cm.default_model(N), op.default_model(N)
+    eng = cm.Engine(m, precision=precision, max_batch=8)
+    assert eng.ld == 256
+    x0, xref, foot, contact = op.generate(mo, SEED, 6, gait=0)
+    contact[:] = 1
+    H, g, n, st = eng.condense(x0, xref, foot, contact)
+    tol = 1e-12 if precision == 0 else 2e-5
+    for q in range(6):
+        nq, Hr, gr, mu, lo, hi, mp, sto = op.condense(mo, x0[q], xref[q], foot[q], contact[q], ld=eng.ld)
+        assert st[q] == sto == 0 and n[q] == nq == 240
+        assert np.abs(H[q, :nq, :nq] - Hr[:nq, :nq]).max() / np.abs(Hr[:nq, :nq]).max() < tol
+        assert np.abs(g[q, :nq] - gr[:nq]).max() / max(1.0, np.abs(gr[:nq]).max()) < tol
+
+
+def test_solve_fp64_large_class_all_stance(cm, op):
+    N = 20
+    m, mo = cm.default_model(N), op.default_model(N)
+    B = 16
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=0)
+    contact[:] = 1
+    u, x, st, it = eng.solve(x0, xref, foot, contact)
+    ur, xr, sr, itr = op.solve_batch(mo, op.default_settings(), x0, xref, foot, contact, nthreads=8)
+    assert np.all(sr == 0) and np.all(st == 0)
+    err = max(rel_err(u[q], ur[q]) for q in range(B))
+    assert err < 1e-6, err
+    assert np.abs(it - itr).max() <= 1
+
+
+def test_solve_fp64_ragged_all_classes(cm, op):
+    N = 20
+    m, mo = cm.default_model(N), op.default_model(N)
+    B = 48
+    rng = np.random.default_rng(7)
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=0)
+    contact[:] = _ragged_contacts(rng, B, N, np.linspace(0.2, 1.0, B))
+    nvar = 3 * contact.reshape(B, -1).sum(axis=1)
+    assert nvar.min() <= 64 and ((nvar > 64) & (nvar <= 128)).any() and nvar.max() > 128
+    u, x, st, it = eng.solve(x0, xref, foot, contact)
+    ur, xr, sr, itr = op.solve_batch(mo, op.default_settings(), x0, xref, foot, contact, nthreads=8)
+    assert np.all(st == sr)
+    ok = st == 0
+    assert ok.mean() > 0.9
+    err = max(rel_err(u[q], ur[q]) for q in range(B) if ok[q])
+    assert err < 1e-6, err
+    assert np.all(u[contact == 0] == 0.0)
+
+
+def test_solve_fp32_large_class(cm, op):
+    N = 20
+    m, mo = cm.default_model(N), op.default_model(N)
+    B = 16
+    s = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3, tol_comp=1e-4)
+    eng = cm.Engine(m, settings=s, precision=1, max_batch=B)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=0)
+    contact[:] = 1
+    u, x, st, it = eng.solve(x0, xref, foot, contact)
+    ur, xr, sr, itr = op.solve_batch(mo, op.tight_settings(), x0, xref, foot, contact, nthreads=8)
+    assert np.all(sr == 0) and np.all(st == 0)
+    err = max(rel_err(u[q], ur[q]) for q in range(B))
+    assert err < 2e-3, err
+
+
+def test_too_large_status(cm, op):
+    """n > 256 (all-stance N = 22: n = 264) -> TOO_LARGE (6), other QPs of the batch unaffected."""
+    N = 22
+    m, mo = cm.default_model(N), op.default_model(N)
+    eng = cm.Engine(m, precision=0, max_batch=4)
+    x0, xref, foot, contact = op.generate(mo, SEED, 3, gait=0)
+    contact[1] = 1
+    u, x, st, it = eng.solve(x0, xref, foot, contact)
+    assert st[1] == 6 and np.all(u[1] == 0)
+    ur, xr, sr, itr = op.solve_batch(mo, op.default_settings(), x0[[0, 2]], xref[[0, 2]], foot[[0, 2]],
+                                     contact[[0, 2]], nthreads=2)
+    assert st[0] == 0 and st[2] == 0
+    assert max(rel_err(u[q], ur[k]) for k, q in enumerate((0, 2))) < 1e-6
+
+
 def test_invalid_contact_status(cm, op):
     N = 10
     m, mo = cm.default_model(N), op.default_model(N)
