@@ -1,10 +1,10 @@
-// k_ipm128_f32.hip — the 64 < n <= 128 size class in float (k_ipm_impl.hpp: row-per-lane register IPM, RPL = 2).
+// k_ipm128_f32.hip — the 64 < n <= 128 size class in float (k_ipm_impl.hpp: one wave per QP, lower rows l and l + 64 per lane).
 #include "k_ipm_impl.hpp"
 
 namespace cmpc {
 
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream) {
-  hipLaunchKernelGGL((k_ipm_reg<float, 128, 1>), dim3(B), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL((k_ipm128<float, 1>), dim3(B), dim3(64), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -1,11 +1,12 @@
 #pragma once
-// k_ipm256.hpp — stage 2 of the hot path for the large size class 128 < n <= 256 (all-stance horizons N = 11..21,
-// e.g. pronk at N = 20: n = 240). Same batched dense friction-pyramid QP and the same primal-dual Mehrotra
+// k_ipm256.hpp — stage 2 of the hot path, workgroup-tiled IPM k_ipm_tiled<T, NT> for the size class
+// 8 NT < n <= 16 NT: NT = 16 serves 128 < n <= 256 (all-stance horizons N = 11..21, e.g. pronk at N = 20: n = 240),
+// NT = 8 serves 64 < n <= 128 in fp64 (one wave cannot hold that factor in its 256 arch VGPRs). Same batched dense friction-pyramid QP and the same primal-dual Mehrotra
 // predictor-corrector as k_ipm_reg / k_ipm64 (restated in oracle/cmpc_oracle.c:oracle_qp_ipm; settings and stopping
 // rule of hpipm_interface::Settings, HpipmInterfaceSettings.h:44-57); only the linear algebra is organised for a
 // matrix too big for one wavefront's registers.
 //
-// MI355X mapping — one 512-thread workgroup (8 waves, 2 per SIMD) per QP:
+// MI355X mapping — one workgroup of NT / 2 waves per QP (NT = 16: 512 threads, 2 waves per SIMD):
 //   * the Newton matrix K = H + C' Sigma C (256 x 256, symmetric) lives in registers as 136 lower 16x16 tiles in the
 //     C/D layout of the 16x16x4 MFMA (v_mfma_f64_16x16x4_f64 / v_mfma_f32_16x16x4_f32): wave w owns the tile rows
 //     w and 15 - w, 17 tiles each (balanced), "slot" s of wave w being tile (w, s) for s <= w, else
@@ -31,14 +32,8 @@
 namespace cmpc {
 namespace ipm256 {
 
-constexpr int NP = 256;          // class size
-constexpr int NT = 16;           // tile rows
-constexpr int W = 8;             // waves per workgroup
-constexpr int NTHR = 64 * W;     // threads
-constexpr int SL = 17;           // tiles (slots) per wave
 constexpr int PS = 17;           // LDS row stride of a 16 x 16 tile (bank-conflict padding)
 constexpr int TS = 16 * PS;      // LDS tile size
-static_assert(5 * (NP / 3) <= NTHR, "one thread per pyramid row");
 
 template <typename T>
 struct Mf;
@@ -92,8 +87,11 @@ __device__ __forceinline__ int opaque_wave() {
   (void)c16;                                   \
   (void)g4
 
-__device__ __forceinline__ int owner(int I) { return I < 8 ? I : 15 - I; }
-__device__ __forceinline__ int slot_I(int w, int s) { return s <= w ? w : 15 - w; }
+// NT tile rows over W = NT / 2 waves, snake order: wave w owns tile rows w and NT - 1 - w (NT + 1 tiles)
+template <int NT>
+__device__ __forceinline__ int owner(int I) { return I < NT / 2 ? I : NT - 1 - I; }
+template <int NT>
+__device__ __forceinline__ int slot_I(int w, int s) { return s <= w ? w : NT - 1 - w; }
 __device__ __forceinline__ int slot_J(int w, int s) { return s <= w ? s : s - w - 1; }
 
 // one wave's LDS is in order; this orders the compiler and drains LDS before cross-lane reuse
@@ -122,8 +120,9 @@ __device__ __forceinline__ T cross4_sum(T x) {
   return p0 + p1;
 }
 
-template <typename T>
+template <typename T, int NT>
 struct Lds {
+  static constexpr int NP = 16 * NT, W = NT / 2, NTHR = 64 * W;
   T P[2][NT][TS];   // panel tiles of the current step (parity double buffer), row-major stride PS
   T Dinv[NT][TS];   // inverted diagonal factor tiles
   T dg[TS];         // diagonal tile factor (row-major) for the inversion
@@ -142,21 +141,26 @@ struct Lds {
 
 }  // namespace ipm256
 
-template <typename T>
-__global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
+template <typename T, int NT>
+__global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 waves per SIMD
   using namespace ipm256;
   using MF = Mf<T>;
   using acc_t = typename MF::acc_t;
+  constexpr int NP = 16 * NT;      // class size
+  constexpr int W = NT / 2;        // waves per workgroup
+  constexpr int NTHR = 64 * W;     // threads
+  constexpr int SL = NT + 1;       // tiles (slots) per wave
+  static_assert(5 * (NP / 3) <= NTHR, "one thread per pyramid row");
 
   const int q = blockIdx.x;
   if (a.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
   const int n = a.nvar[q];
-  if (n <= 128 || n > NP) return;           // served by another size class
+  if (n <= NP / 2 || n > NP) return;        // served by another size class
   const int ld = a.ld;
   const int nt = n / 3;
   const int m = 5 * nt;
   const DevSettings S = a.s;
-  __shared__ Lds<T> L;
+  __shared__ Lds<T, NT> L;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g4 = lane >> 4;
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
     T pa0[4] = {T(0), T(0), T(0), T(0)}, pa1[4] = {T(0), T(0), T(0), T(0)};
     for (int J = 0; J < NT; ++J) {
       IPM256_LOCAL_IDS;
-      if (wave == owner(J)) {
+      if (wave == owner<NT>(J)) {
         const bool r0 = (J == wave);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
       __syncthreads();
       static_for<0, SL>([&](auto s_) {
         constexpr int s = decltype(s_)::value;
-        const int I = slot_I(wave, s), Jt = slot_J(wave, s);
+        const int I = slot_I<NT>(wave, s), Jt = slot_J(wave, s);
         if (Jt == J && I > J) {
           const T yc = L.y[16 * J + c16];
           if (s <= wave) {
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
     __syncthreads();
     for (int I = NT - 1; I >= 0; --I) {
       IPM256_LOCAL_IDS;
-      if (wave == owner(I)) {
+      if (wave == owner<NT>(I)) {
         if (lane < 16) L.tmp[lane] = L.y[16 * I + lane] - L.acc[16 * I + lane];
         wave_sync();
         if (lane < 16) {
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
         wave_sync();
         static_for<0, SL>([&](auto s_) {
           constexpr int s = decltype(s_)::value;
-          const int It = slot_I(wave, s), J = slot_J(wave, s);
+          const int It = slot_I<NT>(wave, s), J = slot_J(wave, s);
           if (It == I && J < I) {
             T p = T(0);
 #pragma unroll
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
     IPM256_LOCAL_IDS;
     static_for<0, SL>([&](auto s_) {
       constexpr int s = decltype(s_)::value;
-      const int I = slot_I(wave, s), J = slot_J(wave, s);
+      const int I = slot_I<NT>(wave, s), J = slot_J(wave, s);
       const T* hp = Hq + (size_t)(16 * I) * NP + 16 * J + c16;
 #pragma unroll
       for (int k = 0; k < 4; ++k) K[s][k] = hp[(size_t)MF::row(lane, k) * NP];
@@ -353,8 +357,8 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
 
     // ---- residuals: C u, H u
     if (isv) L.vec[tid] = u_i;
-    L.part[wave][lane] = T(0), L.part[wave][lane + 64] = T(0), L.part[wave][lane + 128] = T(0),
-    L.part[wave][lane + 192] = T(0);
+#pragma unroll
+    for (int e = 0; e < NP; e += 64) L.part[wave][lane + e] = T(0);
     __syncthreads();
     const T cu = C_row();
     {
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
       T pa0[4] = {T(0), T(0), T(0), T(0)}, pa1[4] = {T(0), T(0), T(0), T(0)};
       static_for<0, SL>([&](auto s_) {
         constexpr int s = decltype(s_)::value;
-        const int I = slot_I(wave, s), J = slot_J(wave, s);
+        const int I = slot_I<NT>(wave, s), J = slot_J(wave, s);
         const T uc = L.vec[16 * J + c16];
         if (s <= wave) {
 #pragma unroll
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
           if (lane < 16) L.part[wave][16 * J + lane] += p;
         }
       });
-      const int R0 = wave, R1 = 15 - wave;
+      const int R0 = wave, R1 = NT - 1 - wave;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const T t0 = row16_sum(pa0[k]);
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
     IPM256_LOCAL_IDS;
     static_for<0, SL>([&](auto s_) {
       constexpr int s = decltype(s_)::value;
-      const int I = slot_I(wave, s), J = slot_J(wave, s);
+      const int I = slot_I<NT>(wave, s), J = slot_J(wave, s);
       if (I - J <= 1) {
         const int gj = 16 * J + c16;
 #pragma unroll
@@ -471,13 +475,13 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
     for (int p = 0; p < NT; ++p) {
       const int buf = p & 1;
       IPM256_LOCAL_IDS;
-      if (wave == owner(p)) {
+      if (wave == owner<NT>(p)) {
         // diagonal tile (selected out of its slot once, so the factorisation code exists once); column s
         // broadcast through LDS
         acc_t D = K[0];
         static_for<1, SL>([&](auto s_) {
           constexpr int s = decltype(s_)::value;
-          if (slot_I(wave, s) == p && slot_J(wave, s) == p) D = K[s];
+          if (slot_I<NT>(wave, s) == p && slot_J(wave, s) == p) D = K[s];
         });
         static_for<0, 16>([&](auto c_) {
           constexpr int sc = decltype(c_)::value;
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
       // raw panel tiles A_ip (i > p) -> LDS
       static_for<0, SL>([&](auto s_) {
         constexpr int s = decltype(s_)::value;
-        const int I = slot_I(wave, s), J = slot_J(wave, s);
+        const int I = slot_I<NT>(wave, s), J = slot_J(wave, s);
         if (J == p && I > p) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) L.P[buf][I][MF::row(lane, k) * PS + c16] = K[s][k];
@@ -537,7 +541,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
       // L_ip = A_ip L_pp^-T on the matrix cores (A in the operand layout from LDS, B[k][j] = Linv[j][k])
       static_for<0, SL>([&](auto s_) {
         constexpr int s = decltype(s_)::value;
-        const int I = slot_I(wave, s), J = slot_J(wave, s);
+        const int I = slot_I<NT>(wave, s), J = slot_J(wave, s);
         if (J == p && I > p) {
           acc_t c = acc_t{T(0), T(0), T(0), T(0)};
 #pragma unroll
@@ -557,7 +561,7 @@ __global__ __launch_bounds__(512, 1) void k_ipm256(IpmArgs<T> a) {
       // trailing update A_ij -= L_ip L_jp' (i >= j > p)
       static_for<0, SL>([&](auto s_) {
         constexpr int s = decltype(s_)::value;
-        const int I = slot_I(wave, s), J = slot_J(wave, s);
+        const int I = slot_I<NT>(wave, s), J = slot_J(wave, s);
         if (J > p) {
           acc_t c = K[s];
 #pragma unroll
