@@ -234,6 +234,26 @@ int ensure_stage(cmpc_ctx* c, size_t bytes) {
   return CMPC_OK;
 }
 
+// Offsets of A, B, b (k < N) and Q, S, R, q, r (k <= N) inside one packed OCP record ([8][N+1], cmpc.h layout).
+std::vector<size_t> ocp_offsets(int N, int nx, const int* nu) {
+  std::vector<size_t> offs(8 * (size_t)(N + 1), 0);
+  size_t o = 0;
+  for (int k = 0; k < N; ++k) {
+    offs[0 * (N + 1) + k] = o; o += (size_t)nx * nx;
+    offs[1 * (N + 1) + k] = o; o += (size_t)nx * nu[k];
+    offs[2 * (N + 1) + k] = o; o += (size_t)nx;
+  }
+  for (int k = 0; k <= N; ++k) {
+    const size_t m = k < N ? (size_t)nu[k] : 0;
+    offs[3 * (N + 1) + k] = o; o += (size_t)nx * nx;
+    offs[4 * (N + 1) + k] = o; o += m * nx;
+    offs[5 * (N + 1) + k] = o; o += m * m;
+    offs[6 * (N + 1) + k] = o; o += (size_t)nx;
+    offs[7 * (N + 1) + k] = o; o += m;
+  }
+  return offs;
+}
+
 }  // namespace
 
 extern "C" {
@@ -534,23 +554,7 @@ int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double*
   }
   const int ldo = nU > 0 ? nU : 1;
   const size_t rs = cmpc_ocp_record_size(N, nx, nu);
-  std::vector<size_t> offs(8 * (size_t)(N + 1), 0);
-  {
-    size_t o = 0;
-    for (int k = 0; k < N; ++k) {
-      offs[0 * (N + 1) + k] = o; o += (size_t)nx * nx;
-      offs[1 * (N + 1) + k] = o; o += (size_t)nx * nu[k];
-      offs[2 * (N + 1) + k] = o; o += (size_t)nx;
-    }
-    for (int k = 0; k <= N; ++k) {
-      const size_t m = k < N ? (size_t)nu[k] : 0;
-      offs[3 * (N + 1) + k] = o; o += (size_t)nx * nx;
-      offs[4 * (N + 1) + k] = o; o += m * nx;
-      offs[5 * (N + 1) + k] = o; o += m * m;
-      offs[6 * (N + 1) + k] = o; o += (size_t)nx;
-      offs[7 * (N + 1) + k] = o; o += m;
-    }
-  }
+  std::vector<size_t> offs = ocp_offsets(N, nx, nu);
   std::vector<int> nuv(nu, nu + N);
   nuv.push_back(0);
   int *d_nu = nullptr, *d_st = nullptr;
@@ -610,6 +614,80 @@ int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double*
   (void)hipFree(d_sc);
   (void)hipFree(d_x);
   (void)hipFree(d_u);
+  (void)hipFree(d_st);
+  return r;
+}
+
+int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const double* rec, double* Sm, double* sv,
+                                double* K, double* kff, int* status) {
+  if (B < 0 || N <= 0 || N > CMPC_OCP_MAX_N || nx <= 0 || nx > CMPC_RIC_MAX_DIM || !nu || !rec || !Sm || !sv ||
+      !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  int nU = 0;
+  for (int k = 0; k < N; ++k) {
+    if (nu[k] < 0 || nu[k] > CMPC_RIC_MAX_DIM) return CMPC_ERR_ARG;
+    nU += nu[k];
+  }
+  if (nU > 0 && (!K || !kff)) return CMPC_ERR_ARG;
+  const size_t rs = cmpc_ocp_record_size(N, nx, nu);
+  std::vector<size_t> offs = ocp_offsets(N, nx, nu);
+  std::vector<int> nuv(nu, nu + N);
+  nuv.push_back(0);
+  const size_t nK = (size_t)nU * nx, nSm = (size_t)(N + 1) * nx * nx, nsv = (size_t)(N + 1) * nx;
+  int* d_nu = nullptr;
+  int* d_st = nullptr;
+  size_t* d_offs = nullptr;
+  double *d_rec = nullptr, *d_Sm = nullptr, *d_sv = nullptr, *d_K = nullptr, *d_k = nullptr, *d_sc = nullptr;
+  int r = CMPC_OK;
+  if (hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)) != hipSuccess ||
+      hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()) != hipSuccess ||
+      hipMalloc((void**)&d_rec, sizeof(double) * B * rs) != hipSuccess ||
+      hipMalloc((void**)&d_Sm, sizeof(double) * B * nSm) != hipSuccess ||
+      hipMalloc((void**)&d_sv, sizeof(double) * B * nsv) != hipSuccess ||
+      hipMalloc((void**)&d_K, sizeof(double) * B * (nK > 0 ? nK : 1)) != hipSuccess ||
+      hipMalloc((void**)&d_k, sizeof(double) * B * (nU > 0 ? nU : 1)) != hipSuccess ||
+      hipMalloc((void**)&d_sc, sizeof(double) * B * ric_scratch(nx)) != hipSuccess ||
+      hipMalloc((void**)&d_st, sizeof(int) * B) != hipSuccess)
+    r = CMPC_ERR_HIP;
+  if (r == CMPC_OK) {
+    (void)hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice);
+    RiccatiArgs a;
+    a.N = N;
+    a.nx = nx;
+    a.nu = d_nu;
+    a.offs = d_offs;
+    a.rec_size = rs;
+    a.rec = d_rec;
+    a.Sm = d_Sm;
+    a.sv = d_sv;
+    a.K = d_K;
+    a.kff = d_k;
+    a.scratch = d_sc;
+    a.nK = (int)nK;
+    a.nU = nU;
+    a.status = d_st;
+    if (launch_ocp_riccati(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess) r = CMPC_ERR_HIP;
+    if (r == CMPC_OK) {
+      (void)hipMemcpy(Sm, d_Sm, sizeof(double) * B * nSm, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(sv, d_sv, sizeof(double) * B * nsv, hipMemcpyDeviceToHost);
+      if (nU > 0) {
+        (void)hipMemcpy(K, d_K, sizeof(double) * B * nK, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(kff, d_k, sizeof(double) * B * nU, hipMemcpyDeviceToHost);
+      }
+      (void)hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(d_nu);
+  (void)hipFree(d_offs);
+  (void)hipFree(d_rec);
+  (void)hipFree(d_Sm);
+  (void)hipFree(d_sv);
+  (void)hipFree(d_K);
+  (void)hipFree(d_k);
+  (void)hipFree(d_sc);
   (void)hipFree(d_st);
   return r;
 }

@@ -131,4 +131,26 @@ struct OcpArgs {
 #define CMPC_OCP_MAX_N 256
 int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream);
 
+// Riccati recursion of the same OCP (HpipmInterface::getRiccati*, HpipmInterface.cpp:330-455)
+struct RiccatiArgs {
+  int N, nx;
+  const int* nu;       // device [N+1]
+  const size_t* offs;  // device [8][N+1] record offsets
+  size_t rec_size;
+  const double* rec;   // [B][rec_size]
+  double* Sm;          // [B][N+1][nx*nx] column-major
+  double* sv;          // [B][N+1][nx]
+  double* K;           // [B][sum nu_k * nx] stage blocks nu_k x nx column-major
+  double* kff;         // [B][sum nu_k]
+  double* scratch;     // [B][RIC_SCRATCH(nx)]
+  int nK, nU;          // sum nu_k * nx, sum nu_k (per problem)
+  int* status;
+};
+#define CMPC_RIC_MAX_DIM 64
+__host__ __device__ inline size_t ric_scratch(int nx) {
+  const size_t m = CMPC_RIC_MAX_DIM;
+  return (size_t)nx * nx + nx * m + nx + m * nx + m * m + m + m * (nx + 1);
+}
+int launch_ocp_riccati(const RiccatiArgs& a, int B, hipStream_t stream);
+
 }  // namespace cmpc

@@ -401,6 +401,170 @@ int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// ------------------------------------------------------------------------------------------ Riccati recursion
+// Cost-to-go (Sm, sv) and affine policy u_k = K_k x_k + k_k of the equality-free OCP, backward from Sm_N = Q_N,
+// sv_N = q_N (testHpipmInterface.cpp:280-304; the quantities HpipmInterface::getRiccati* rebuild from HPIPM's
+// ric_P / ric_p / ric_Lr / ric_Ls / ric_k, HpipmInterface.cpp:330-455):
+//   P = S + B'Sm A,  Rt = R + B'Sm B = Lr Lr',  rr = r + B'(sv + Sm b)
+//   K = -Rt^-1 P,  k = -Rt^-1 rr,  Sm_k = Q + A'Sm A - P'Rt^-1 P,  sv_k = q + A'(sv + Sm b) - P'Rt^-1 rr
+// One 256-thread workgroup per problem, stage products thread-parallel, Rt factored in place (Cholesky; a
+// non-positive pivot -> NAN_SOL), one thread per right-hand-side column for the two triangular solves.
+__global__ __launch_bounds__(256) void k_ocp_riccati(RiccatiArgs a) {
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int N = a.N, nx = a.nx;
+  constexpr int M = CMPC_RIC_MAX_DIM;
+  const double* rec = a.rec + (size_t)q * a.rec_size;
+  const size_t* oA = a.offs;
+  const size_t* oB = a.offs + (N + 1);
+  const size_t* ob = a.offs + 2 * (N + 1);
+  const size_t* oQ = a.offs + 3 * (N + 1);
+  const size_t* oS = a.offs + 4 * (N + 1);
+  const size_t* oR = a.offs + 5 * (N + 1);
+  const size_t* oq = a.offs + 6 * (N + 1);
+  const size_t* orr = a.offs + 7 * (N + 1);
+  double* Sm = a.Sm + (size_t)q * (N + 1) * nx * nx;
+  double* sv = a.sv + (size_t)q * (N + 1) * nx;
+  double* Kq = a.K + (size_t)q * a.nK;
+  double* kq = a.kff + (size_t)q * a.nU;
+  double* SmA = a.scratch + (size_t)q * ric_scratch(nx);  // nx x nx
+  double* SmB = SmA + (size_t)nx * nx;                     // nx x m   (ld nx)
+  double* w = SmB + (size_t)nx * M;                        // nx: sv + Sm b
+  double* P = w + nx;                                      // m x nx   (ld m)
+  double* Rt = P + (size_t)M * nx;                         // m x m    (ld m)
+  double* rr = Rt + (size_t)M * M;                         // m
+  double* X = rr + M;                                      // m x (nx + 1) (ld m)
+  __shared__ int s_koff[CMPC_OCP_MAX_N + 1], s_uoff[CMPC_OCP_MAX_N + 1];
+  __shared__ int s_bad;
+  if (tid == 0) {
+    int ok = 0, ou = 0;
+    for (int k = 0; k < N; ++k) {
+      s_koff[k] = ok;
+      s_uoff[k] = ou;
+      ok += a.nu[k] * nx;
+      ou += a.nu[k];
+    }
+    s_bad = 0;
+  }
+  for (int i = tid; i < nx * nx; i += nth) Sm[(size_t)N * nx * nx + i] = rec[oQ[N] + i];
+  for (int i = tid; i < nx; i += nth) sv[(size_t)N * nx + i] = rec[oq[N] + i];
+  __syncthreads();
+  for (int k = N - 1; k >= 0; --k) {
+    const int m = a.nu[k];
+    const double* A = rec + oA[k];
+    const double* Bm = rec + oB[k];
+    const double* b = rec + ob[k];
+    const double* Q = rec + oQ[k];
+    const double* S = rec + oS[k];
+    const double* R = rec + oR[k];
+    const double* qv = rec + oq[k];
+    const double* r = rec + orr[k];
+    const double* Sn = Sm + (size_t)(k + 1) * nx * nx;
+    const double* sn = sv + (size_t)(k + 1) * nx;
+    double* Sk = Sm + (size_t)k * nx * nx;
+    double* sk = sv + (size_t)k * nx;
+    // Sm A, Sm B, sv + Sm b
+    for (int e = tid; e < nx * nx; e += nth) {
+      const int i = e % nx, j = e / nx;
+      double acc = 0.0;
+      for (int t = 0; t < nx; ++t) acc += OCP_CM(Sn, nx, i, t) * OCP_CM(A, nx, t, j);
+      SmA[e] = acc;
+    }
+    for (int e = tid; e < nx * m; e += nth) {
+      const int i = e % nx, c = e / nx;
+      double acc = 0.0;
+      for (int t = 0; t < nx; ++t) acc += OCP_CM(Sn, nx, i, t) * OCP_CM(Bm, nx, t, c);
+      SmB[e] = acc;
+    }
+    for (int i = tid; i < nx; i += nth) {
+      double acc = sn[i];
+      for (int t = 0; t < nx; ++t) acc += OCP_CM(Sn, nx, i, t) * b[t];
+      w[i] = acc;
+    }
+    __syncthreads();
+    if (m > 0) {
+      for (int e = tid; e < m * nx; e += nth) {
+        const int c = e % m, j = e / m;
+        double acc = OCP_CM(S, m, c, j);
+        for (int t = 0; t < nx; ++t) acc += OCP_CM(Bm, nx, t, c) * OCP_CM(SmA, nx, t, j);
+        P[e] = acc;
+      }
+      for (int e = tid; e < m * m; e += nth) {
+        const int c = e % m, d = e / m;
+        double acc = OCP_CM(R, m, c, d);
+        for (int t = 0; t < nx; ++t) acc += OCP_CM(Bm, nx, t, c) * OCP_CM(SmB, nx, t, d);
+        Rt[e] = acc;
+      }
+      for (int c = tid; c < m; c += nth) {
+        double acc = r[c];
+        for (int t = 0; t < nx; ++t) acc += OCP_CM(Bm, nx, t, c) * w[t];
+        rr[c] = acc;
+      }
+      __syncthreads();
+      // Rt = Lr Lr' in place (lower)
+      for (int s2 = 0; s2 < m; ++s2) {
+        if (tid == 0) {
+          const double d = OCP_CM(Rt, m, s2, s2);
+          if (!(d > 0.0)) s_bad = 1;
+          OCP_CM(Rt, m, s2, s2) = d > 0.0 ? sqrt(d) : 1.0;
+        }
+        __syncthreads();
+        const double piv = OCP_CM(Rt, m, s2, s2);
+        for (int i = s2 + 1 + tid; i < m; i += nth) OCP_CM(Rt, m, i, s2) /= piv;
+        __syncthreads();
+        const int rem = m - s2 - 1;
+        for (int e = tid; e < rem * rem; e += nth) {
+          const int i = s2 + 1 + e % rem, j = s2 + 1 + e / rem;
+          if (j <= i) OCP_CM(Rt, m, i, j) -= OCP_CM(Rt, m, i, s2) * OCP_CM(Rt, m, j, s2);
+        }
+        __syncthreads();
+      }
+      // X = Rt^-1 [P | rr], one column per thread
+      for (int c = tid; c <= nx; c += nth) {
+        double* xc = X + (size_t)c * m;
+        for (int i = 0; i < m; ++i) xc[i] = c < nx ? OCP_CM(P, m, i, c) : rr[i];
+        for (int i = 0; i < m; ++i) {
+          double v = xc[i];
+          for (int t = 0; t < i; ++t) v -= OCP_CM(Rt, m, i, t) * xc[t];
+          xc[i] = v / OCP_CM(Rt, m, i, i);
+        }
+        for (int i = m - 1; i >= 0; --i) {
+          double v = xc[i];
+          for (int t = i + 1; t < m; ++t) v -= OCP_CM(Rt, m, t, i) * xc[t];
+          xc[i] = v / OCP_CM(Rt, m, i, i);
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < m * nx; e += nth) Kq[s_koff[k] + e] = -X[e];  // column-major m x nx, same as X
+      for (int c = tid; c < m; c += nth) kq[s_uoff[k] + c] = -X[(size_t)nx * m + c];
+    }
+    // Sm_k = Q + A'Sm A - P'X,  sv_k = q + A'w - P'x_rr
+    for (int e = tid; e < nx * nx; e += nth) {
+      const int i = e % nx, j = e / nx;
+      double acc = OCP_CM(Q, nx, i, j);
+      for (int t = 0; t < nx; ++t) acc += OCP_CM(A, nx, t, i) * OCP_CM(SmA, nx, t, j);
+      for (int c = 0; c < m; ++c) acc -= OCP_CM(P, m, c, i) * OCP_CM(X, m, c, j);
+      if (!isfinite(acc)) s_bad = 1;
+      Sk[e] = acc;
+    }
+    for (int i = tid; i < nx; i += nth) {
+      double acc = qv[i];
+      for (int t = 0; t < nx; ++t) acc += OCP_CM(A, nx, t, i) * w[t];
+      for (int c = 0; c < m; ++c) acc -= OCP_CM(P, m, c, i) * X[(size_t)nx * m + c];
+      if (!isfinite(acc)) s_bad = 1;
+      sk[i] = acc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) a.status[q] = s_bad ? CMPC_NAN_SOL : CMPC_SUCCESS;
+}
+
+int launch_ocp_riccati(const RiccatiArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_ocp_riccati, dim3(B), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 }  // namespace cmpc
 
 namespace cmpc {

@@ -108,12 +108,83 @@ class HpipmInterface::Impl {
       off += nu[(size_t)k];
     }
     if (verbose) std::fprintf(stderr, "\n=== HPIPM (MI355X engine) ===\nstatus %d (%s)\n", status, cmpc_status_string(status));
+    lastRec_ = std::move(rec);
+    lastNu_ = nu;
+    lastNx_ = nx;
+    riccatiValid_ = false;
     return (hpipm_status)status;
+  }
+
+  // Device Riccati recursion over the last problem, computed once per solve on first use.
+  void riccati(const VectorFunctionLinearApproximation& dyn0, const ScalarFunctionQuadraticApproximation& cost0) {
+    const int N = (int)lastNu_.size();
+    if (N == 0) throw std::runtime_error("[HpipmInterface] no solved problem to take Riccati quantities from");
+    if (dyn0.dfdx.rows() != lastNx_ || dyn0.dfdu.cols() != lastNu_[0] || cost0.dfdxx.rows() != lastNx_)
+      throw std::runtime_error("[HpipmInterface] dynamics0 / cost0 do not match the last solved problem");
+    if (riccatiValid_) return;
+    const int nx = lastNx_;
+    int nU = 0;
+    for (int v : lastNu_) nU += v;
+    Sm_.assign((size_t)(N + 1) * nx * nx, 0.0);
+    sv_.assign((size_t)(N + 1) * nx, 0.0);
+    K_.assign((size_t)(nU > 0 ? nU : 1) * nx, 0.0);
+    k_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
+    int st = -1;
+    const int r = cmpc_ocp_riccati_batch_host(1, N, nx, lastNu_.data(), lastRec_.data(), Sm_.data(), sv_.data(),
+                                              K_.data(), k_.data(), &st);
+    if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
+    if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati recursion: R + B'PB not positive definite");
+    riccatiValid_ = true;
+  }
+  std::vector<ScalarFunctionQuadraticApproximation> costToGo(const VectorFunctionLinearApproximation& d0,
+                                                              const ScalarFunctionQuadraticApproximation& c0) {
+    riccati(d0, c0);
+    const int N = (int)lastNu_.size(), nx = lastNx_;
+    std::vector<ScalarFunctionQuadraticApproximation> out((size_t)N + 1);
+    for (int k = 0; k <= N; ++k) {
+      out[(size_t)k].dfdxx.resize(nx, nx);
+      out[(size_t)k].dfdx.resize(nx);
+      for (int e = 0; e < nx * nx; ++e) out[(size_t)k].dfdxx.a[(size_t)e] = Sm_[(size_t)k * nx * nx + e];
+      for (int i = 0; i < nx; ++i) out[(size_t)k].dfdx[i] = sv_[(size_t)k * nx + i];
+      out[(size_t)k].f = 0.0;
+    }
+    return out;
+  }
+  matrix_array_t feedback(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
+    riccati(d0, c0);
+    const int N = (int)lastNu_.size(), nx = lastNx_;
+    matrix_array_t out((size_t)N);
+    size_t o = 0;
+    for (int k = 0; k < N; ++k) {
+      const int m = lastNu_[(size_t)k];
+      out[(size_t)k].resize(m, nx);
+      for (int e = 0; e < m * nx; ++e) out[(size_t)k].a[(size_t)e] = K_[o + (size_t)e];
+      o += (size_t)m * nx;
+    }
+    return out;
+  }
+  vector_array_t feedforward(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
+    riccati(d0, c0);
+    const int N = (int)lastNu_.size();
+    vector_array_t out((size_t)N);
+    size_t o = 0;
+    for (int k = 0; k < N; ++k) {
+      const int m = lastNu_[(size_t)k];
+      out[(size_t)k].resize(m);
+      for (int i = 0; i < m; ++i) out[(size_t)k][i] = k_[o + (size_t)i];
+      o += (size_t)m;
+    }
+    return out;
   }
 
  private:
   Settings settings_;
   OcpSize size_;
+  std::vector<double> lastRec_;
+  std::vector<int> lastNu_;
+  int lastNx_ = 0;
+  bool riccatiValid_ = false;
+  std::vector<double> Sm_, sv_, K_, k_;
 };
 
 HpipmInterface::HpipmInterface(OcpSize s, const Settings& st) : pImpl_(new Impl(std::move(s), st)) {}
@@ -124,6 +195,18 @@ hpipm_status HpipmInterface::solve(const vector_t& x0, std::vector<VectorFunctio
                                    std::vector<VectorFunctionLinearApproximation>* constraints, vector_array_t& x,
                                    vector_array_t& u, bool verbose) {
   return pImpl_->solve(x0, dynamics, cost, constraints, x, u, verbose);
+}
+std::vector<ScalarFunctionQuadraticApproximation> HpipmInterface::getRiccatiCostToGo(
+    const VectorFunctionLinearApproximation& dynamics0, const ScalarFunctionQuadraticApproximation& cost0) {
+  return pImpl_->costToGo(dynamics0, cost0);
+}
+matrix_array_t HpipmInterface::getRiccatiFeedback(const VectorFunctionLinearApproximation& dynamics0,
+                                                  const ScalarFunctionQuadraticApproximation& cost0) {
+  return pImpl_->feedback(dynamics0, cost0);
+}
+vector_array_t HpipmInterface::getRiccatiFeedforward(const VectorFunctionLinearApproximation& dynamics0,
+                                                     const ScalarFunctionQuadraticApproximation& cost0) {
+  return pImpl_->feedforward(dynamics0, cost0);
 }
 
 }  // namespace ocs2

@@ -74,6 +74,7 @@ def lib():
     L.cmpc_ocp_record_size.argtypes = [C.c_int, C.c_int, i]
     L.cmpc_ocp_record_size.restype = C.c_size_t
     L.cmpc_ocp_solve_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, i]
+    L.cmpc_ocp_riccati_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, d, i]
     L.cmpc_status_string.argtypes = [C.c_int]
     L.cmpc_status_string.restype = C.c_char_p
     L.cmpc_error_string.argtypes = [C.c_int]
@@ -279,6 +280,36 @@ def ocp_solve(N, nx, nu, x0, rec):
     _chk(lib().cmpc_ocp_solve_batch_host(B, N, nx, vp(nua), vp(x0), vp(rec), vp(x), vp(u), vp(st)),
          "cmpc_ocp_solve_batch_host")
     return x, u[:, :nU], st
+
+
+def ocp_riccati(N, nx, nu, rec):
+    """Batched device Riccati recursion of the OCP (HpipmInterface::getRiccati*): returns Sm [B,N+1,nx,nx],
+    sv [B,N+1,nx], K (per problem a list of nu_k x nx arrays), kff (per problem a list of nu_k vectors), status [B]."""
+    rec = np.ascontiguousarray(np.atleast_2d(rec), np.float64)
+    B = rec.shape[0]
+    nua = np.ascontiguousarray(nu, np.int32)
+    nU = int(nua.sum())
+    Sm = np.zeros((B, N + 1, nx * nx))
+    sv = np.zeros((B, N + 1, nx))
+    K = np.zeros((B, max(nU * nx, 1)))
+    kff = np.zeros((B, max(nU, 1)))
+    st = np.zeros(B, np.int32)
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _chk(lib().cmpc_ocp_riccati_batch_host(B, N, nx, vp(nua), vp(rec), vp(Sm), vp(sv), vp(K), vp(kff), vp(st)),
+         "cmpc_ocp_riccati_batch_host")
+    Sm = Sm.reshape(B, N + 1, nx, nx).transpose(0, 1, 3, 2)  # column-major blocks
+    Ks, ks = [], []
+    for b in range(B):
+        o, ok, Kb, kb = 0, 0, [], []
+        for k in range(N):
+            m = int(nua[k])
+            Kb.append(K[b, o:o + m * nx].reshape(nx, m).T)
+            kb.append(kff[b, ok:ok + m])
+            o += m * nx
+            ok += m
+        Ks.append(Kb)
+        ks.append(kb)
+    return Sm, sv, Ks, ks, st
 
 
 def device_info():

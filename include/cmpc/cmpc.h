@@ -158,6 +158,15 @@ size_t cmpc_ocp_record_size(int N, int nx, const int* nu);
 int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
                               double* u, int* status);
 
+/* Discrete Riccati recursion of the same equality-free OCP on the device: the cost-to-go and affine policy that
+ * HpipmInterface::getRiccatiCostToGo / getRiccatiFeedback / getRiccatiFeedforward return (reference
+ * HpipmInterface.cpp:330-455, from HPIPM's ric_P / ric_p / ric_Lr / ric_Ls / ric_k; recursion as
+ * testHpipmInterface.cpp:280-304). Per problem, all blocks COLUMN-major:
+ *   Sm [(N+1)][nx*nx], sv [(N+1)][nx], K [sum_k nu_k*nx] (stage blocks nu_k x nx), kff [sum nu_k].
+ * status[b]: 0 SUCCESS, 3 NAN_SOL (R + B'Sm B not positive definite, or a non-finite result). */
+int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const double* rec, double* Sm, double* sv,
+                                double* K, double* kff, int* status);
+
 /* Per-stage device timing with HIP events recorded on the solve stream (used by bench.py for the roofline):
  * after cmpc_profile_begin, each cmpc_solve_batch records events around its three stages (condense, IPM, expand);
  * cmpc_profile_end synchronises and returns the summed milliseconds per stage and the number of calls. */

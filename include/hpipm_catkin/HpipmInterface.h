@@ -131,6 +131,17 @@ class HpipmInterface {
                      std::vector<VectorFunctionLinearApproximation>* constraints, vector_array_t& stateTrajectory,
                      vector_array_t& inputTrajectory, bool verbose = false);
 
+  /* Riccati quantities of the previously solved problem (reference HpipmInterface.h:93-123, .cpp:330-455), from the
+   * device recursion cmpc_ocp_riccati_batch_host. The reference rebuilds stage 0 from (dynamics0, cost0) because
+   * HPIPM eliminates x0; the recursion here runs over stage 0 directly, so the arguments are accepted and must equal
+   * the stage-0 data of the last solve (size-checked). Cost-to-go f is 0, as in the reference. */
+  std::vector<ScalarFunctionQuadraticApproximation> getRiccatiCostToGo(const VectorFunctionLinearApproximation& dynamics0,
+                                                                       const ScalarFunctionQuadraticApproximation& cost0);
+  matrix_array_t getRiccatiFeedback(const VectorFunctionLinearApproximation& dynamics0,
+                                    const ScalarFunctionQuadraticApproximation& cost0);
+  vector_array_t getRiccatiFeedforward(const VectorFunctionLinearApproximation& dynamics0,
+                                       const ScalarFunctionQuadraticApproximation& cost0);
+
  private:
   class Impl;
   std::unique_ptr<Impl> pImpl_;

@@ -1,5 +1,6 @@
 // C++ mirror of the reference gtests ocs2_sqp/hpipm_catkin/test/testHpipmInterface.cpp (solve_and_check_dynamic
-// :37-69, solve_after_resize :71-110, knownSolution :112-152, noInputs :208-256) against the HpipmInterface
+// :37-69, solve_after_resize :71-110, knownSolution :112-152, noInputs :208-256, retrieveRiccati :258-340) against the
+// HpipmInterface
 // mirror, whose solve runs on the MI355X engine. Random problems from a fixed-seed generator (ocs2's
 // getRandomDynamics/getRandomCost are not vendored): uniform [-1,1) matrices, costs made positive definite.
 #include <cmath>
@@ -155,11 +156,129 @@ static void dynamics_feasible(bool resize) {
   CHECK(threw, "size mismatch throws");
 }
 
+// small dense helpers for the reference recursion (testHpipmInterface.cpp:280-304)
+static matrix_t mm(const matrix_t& A, const matrix_t& B) {
+  matrix_t C(A.rows(), B.cols());
+  for (int i = 0; i < A.rows(); ++i)
+    for (int j = 0; j < B.cols(); ++j) {
+      double s = 0;
+      for (int k = 0; k < A.cols(); ++k) s += A(i, k) * B(k, j);
+      C(i, j) = s;
+    }
+  return C;
+}
+static matrix_t tr(const matrix_t& A) {
+  matrix_t C(A.cols(), A.rows());
+  for (int i = 0; i < A.rows(); ++i)
+    for (int j = 0; j < A.cols(); ++j) C(j, i) = A(i, j);
+  return C;
+}
+static matrix_t add(const matrix_t& A, const matrix_t& B, double sb = 1.0) {
+  matrix_t C = A;
+  for (size_t e = 0; e < C.a.size(); ++e) C.a[e] += sb * B.a[e];
+  return C;
+}
+static vector_t addv(const vector_t& a, const vector_t& b, double sb = 1.0) {
+  vector_t c = a;
+  for (int i = 0; i < c.size(); ++i) c[i] += sb * b[i];
+  return c;
+}
+static matrix_t inv(const matrix_t& A) {  // Gauss-Jordan with partial pivoting (small, well conditioned)
+  const int n = A.rows();
+  matrix_t M = A, I(n, n);
+  for (int i = 0; i < n; ++i) I(i, i) = 1.0;
+  for (int c = 0; c < n; ++c) {
+    int p = c;
+    for (int r = c + 1; r < n; ++r)
+      if (std::fabs(M(r, c)) > std::fabs(M(p, c))) p = r;
+    for (int j = 0; j < n; ++j) {
+      std::swap(M(c, j), M(p, j));
+      std::swap(I(c, j), I(p, j));
+    }
+    const double d = M(c, c);
+    for (int j = 0; j < n; ++j) {
+      M(c, j) /= d;
+      I(c, j) /= d;
+    }
+    for (int r = 0; r < n; ++r)
+      if (r != c) {
+        const double f = M(r, c);
+        for (int j = 0; j < n; ++j) {
+          M(r, j) -= f * M(c, j);
+          I(r, j) -= f * I(c, j);
+        }
+      }
+  }
+  return I;
+}
+static double maxdiffm(const matrix_t& a, const matrix_t& b) {
+  if (a.rows() != b.rows() || a.cols() != b.cols()) return 1e300;
+  double m = 0.0;
+  for (size_t e = 0; e < a.a.size(); ++e) m = std::fmax(m, std::fabs(a.a[e] - b.a[e]));
+  return m;
+}
+
+// testHpipmInterface.cpp:258-340 retrieveRiccati
+static void retrieve_riccati() {
+  const int nx = 3, nu = 2, N = 5;
+  const vector_t x0 = randv(nx);
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+  }
+  cost.push_back(randomCost(nx, 0));
+  std::vector<matrix_t> SmG((size_t)N + 1), KG((size_t)N);
+  std::vector<vector_t> svG((size_t)N + 1), kG((size_t)N);
+  SmG[(size_t)N] = cost[(size_t)N].dfdxx;
+  svG[(size_t)N] = cost[(size_t)N].dfdx;
+  for (int k = N - 1; k >= 0; --k) {
+    const matrix_t& Sm = SmG[(size_t)k + 1];
+    const vector_t& sv = svG[(size_t)k + 1];
+    const auto& A = sys[(size_t)k].dfdx;
+    const auto& B = sys[(size_t)k].dfdu;
+    const auto& b = sys[(size_t)k].f;
+    const auto& c = cost[(size_t)k];
+    const matrix_t P_BTSmA = add(c.dfdux, mm(tr(B), mm(Sm, A)));
+    const matrix_t invR = inv(add(c.dfduu, mm(tr(B), mm(Sm, B))));
+    const vector_t rr = addv(addv(c.dfdu, mtv(B, sv)), mtv(B, mv(Sm, b)));
+    SmG[(size_t)k] = add(add(c.dfdxx, mm(tr(A), mm(Sm, A))), mm(tr(P_BTSmA), mm(invR, P_BTSmA)), -1.0);
+    svG[(size_t)k] = addv(addv(addv(c.dfdx, mtv(A, sv)), mtv(A, mv(Sm, b))), mv(tr(P_BTSmA), mv(invR, rr)), -1.0);
+    KG[(size_t)k] = mm(invR, P_BTSmA);
+    for (auto& v : KG[(size_t)k].a) v = -v;
+    kG[(size_t)k] = mv(invR, rr);
+    for (auto& v : kG[(size_t)k].v) v = -v;
+  }
+  HpipmInterface hpipm(HpipmInterface::OcpSize(N, nx, nu));
+  vector_array_t xs, us;
+  const auto st = hpipm.solve(x0, sys, cost, nullptr, xs, us, false);
+  CHECK(st == SUCCESS, "retrieveRiccati status");
+  const auto K = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  const auto kf = hpipm.getRiccatiFeedforward(sys[0], cost[0]);
+  const auto ctg = hpipm.getRiccatiCostToGo(sys[0], cost[0]);
+  double e = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    e = std::fmax(e, maxdiffm(ctg[(size_t)k].dfdxx, SmG[(size_t)k]));
+    e = std::fmax(e, maxdiff(ctg[(size_t)k].dfdx, svG[(size_t)k]));
+    e = std::fmax(e, std::fabs(ctg[(size_t)k].f));
+  }
+  for (int k = 0; k < N; ++k) {
+    e = std::fmax(e, maxdiffm(K[(size_t)k], KG[(size_t)k]));
+    e = std::fmax(e, maxdiff(kf[(size_t)k], kG[(size_t)k]));
+    // self-consistency u = K x + k
+    e = std::fmax(e, maxdiff(us[(size_t)k], addv(mv(K[(size_t)k], xs[(size_t)k]), kf[(size_t)k])));
+  }
+  std::printf("retrieveRiccati max err %.3e\n", e);
+  CHECK(e < 1e-9, "retrieveRiccati 1e-9");
+}
+
 int main() {
   dynamics_feasible(false);
   dynamics_feasible(true);
   known_solution(false);
   known_solution(true);
+  retrieve_riccati();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;
 }

@@ -307,6 +307,58 @@ def test_hpipm_interface_path_on_device(cm, op):
     assert np.abs(u - np.array(ugs)).max() < 1e-9
 
 
+def test_riccati_on_device_matches_recursion(cm, op):
+    """testHpipmInterface.cpp:258-340 retrieveRiccati: device recursion vs the closed-form one (1e-9) and vs the
+    oracle's, batched over problems with ragged inputs (nu_k = 0 stages included); u = K x + k self-consistency."""
+    from test_oracle import random_ocp
+    rng = np.random.default_rng(11)
+    N, nx, nu = 6, 4, [3, 0, 2, 3, 1, 3]
+    recs, probs = [], []
+    for b in range(5):
+        A, B, bb, Q, S, R, q, r = random_ocp(rng, N, nx, nu)
+        recs.append(op.ocp_pack(N, nx, nu, A, B, bb, Q, S, R, q, r))
+        probs.append((A, B, bb, Q, S, R, q, r))
+    Sm, sv, K, kff, st = cm.ocp_riccati(N, nx, nu, np.array(recs))
+    assert np.all(st == 0)
+    for b, (A, B, bb, Q, S, R, q, r) in enumerate(probs):
+        Sg, sg = Q[N], q[N]
+        assert np.abs(Sm[b, N] - Sg).max() < 1e-12
+        for k in range(N - 1, -1, -1):
+            m = nu[k]
+            if m:
+                P = S[k] + B[k].T @ Sg @ A[k]
+                iR = np.linalg.inv(R[k] + B[k].T @ Sg @ B[k])
+                rr = r[k] + B[k].T @ sg + B[k].T @ Sg @ bb[k]
+                Sn = Q[k] + A[k].T @ Sg @ A[k] - P.T @ iR @ P
+                sn = q[k] + A[k].T @ sg + A[k].T @ Sg @ bb[k] - P.T @ iR @ rr
+                assert np.abs(K[b][k] - (-iR @ P)).max() < 1e-9
+                assert np.abs(kff[b][k] - (-iR @ rr)).max() < 1e-9
+            else:
+                Sn = Q[k] + A[k].T @ Sg @ A[k]
+                sn = q[k] + A[k].T @ sg + A[k].T @ Sg @ bb[k]
+            assert np.abs(Sm[b, k] - Sn).max() < 1e-9 and np.abs(sv[b, k] - sn).max() < 1e-9
+            Sg, sg = Sn, sn
+        Smo, svo, Ko, ko, sto = op.ocp_riccati(N, nx, nu, recs[b])
+        assert sto == 0 and np.abs(Sm[b] - Smo).max() < 1e-9
+        x0 = rng.uniform(-1, 1, nx)
+        x, u, _ = op.ocp_solve(N, nx, nu, x0, recs[b])
+        o = 0
+        for k in range(N):
+            assert np.allclose(u[o:o + nu[k]], K[b][k] @ x[k] + kff[b][k], atol=1e-9)
+            o += nu[k]
+
+
+def test_riccati_not_pd_status(cm, op):
+    from test_oracle import random_ocp
+    rng = np.random.default_rng(3)
+    N, nx, nu = 3, 2, [2, 2, 2]
+    A, B, bb, Q, S, R, q, r = random_ocp(rng, N, nx, nu)
+    R[1] = -1000.0 * np.eye(2)  # R + B'Sm B indefinite at stage 1
+    rec = op.ocp_pack(N, nx, nu, A, B, bb, Q, S, R, q, r)
+    *_, st = cm.ocp_riccati(N, nx, nu, rec[None])
+    assert st[0] == 3
+
+
 @pytest.fixture(scope="module")
 def cpp_bins(tmp_path_factory, cm):
     out = tmp_path_factory.mktemp("cppbin")
