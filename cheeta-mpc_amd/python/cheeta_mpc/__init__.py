@@ -40,6 +40,15 @@ class Settings(C.Structure):
                 ("pred_corr", C.c_int), ("ric_alg", C.c_int)]
 
 
+GAIT_MAX_MODES = 16
+
+
+class Gait(C.Structure):
+    """cmpc_gait: ocs2 ModeSequenceTemplate (gait.info modeSequence + switchingTimes)."""
+    _fields_ = [("n_modes", C.c_int), ("mode", C.c_int * GAIT_MAX_MODES),
+                ("switching_time", C.c_double * (GAIT_MAX_MODES + 1))]
+
+
 _lib = None
 _hip = None
 
@@ -74,6 +83,10 @@ def lib():
     L.cmpc_ocp_record_size.argtypes = [C.c_int, C.c_int, i]
     L.cmpc_ocp_record_size.restype = C.c_size_t
     L.cmpc_ocp_solve_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, i]
+    L.cmpc_gait_builtin.argtypes = [C.c_char_p, P(Gait)]
+    L.cmpc_gait_table_create.argtypes = [P(Gait), C.c_int, i, P(vp)]
+    L.cmpc_gait_table_destroy.argtypes = [vp]
+    L.cmpc_gait_contact_batch.argtypes = [vp, C.c_int, i, d, C.c_double, C.c_double, C.c_int, u8, vp]
     L.cmpc_ocp_riccati_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, d, i]
     L.cmpc_status_string.argtypes = [C.c_int]
     L.cmpc_status_string.restype = C.c_char_p
@@ -310,6 +323,43 @@ def ocp_riccati(N, nx, nu, rec):
         Ks.append(Kb)
         ks.append(kb)
     return Sm, sv, Ks, ks, st
+
+
+def gait_builtin(name):
+    g = Gait()
+    _chk(lib().cmpc_gait_builtin(name.encode(), C.byref(g)), f"cmpc_gait_builtin({name})")
+    return g
+
+
+class GaitTable:
+    """Device table of gait templates (cmpc_gait_table); contact() fills a [B,N,4] device contact table."""
+
+    def __init__(self, gaits, leg_map=None):
+        arr = (Gait * len(gaits))(*gaits)
+        self.ptr = C.c_void_p()
+        lm = None if leg_map is None else (C.c_int * 4)(*leg_map)
+        _chk(lib().cmpc_gait_table_create(arr, len(gaits), C.cast(lm, C.POINTER(C.c_int)) if lm else None,
+                                          C.byref(self.ptr)), "cmpc_gait_table_create")
+
+    def contact_device(self, B, gait_id, t_start, t0, dt, N, contact, stream=None):
+        _chk(lib().cmpc_gait_contact_batch(self.ptr, B, gait_id.ptr, t_start.ptr, t0, dt, N, contact.ptr, stream),
+             "cmpc_gait_contact_batch")
+
+    def contact(self, gait_id, t_start, t0, dt, N):
+        gid = DeviceArray.from_host(np.ascontiguousarray(gait_id, np.int32))
+        ts = DeviceArray.from_host(np.ascontiguousarray(t_start, np.float64))
+        B = gid.shape[0]
+        out = DeviceArray((B, N, 4), np.uint8)
+        self.contact_device(B, gid, ts, t0, dt, N, out)
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return out.host()
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().cmpc_gait_table_destroy(self.ptr)
+        except Exception:
+            pass
 
 
 def device_info():

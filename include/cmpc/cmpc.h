@@ -167,6 +167,35 @@ int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double*
 int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const double* rec, double* Sm, double* sv,
                                 double* K, double* kff, int* status);
 
+/* ---- Contact schedules from gait templates ----
+ * A template is ocs2's ModeSequenceTemplate (gait.info: modeSequence + switchingTimes, ModeNumber encoding of
+ * MotionPhaseDefinition.h:48-63, stance legs of modeNumber2StanceLeg :69-124, ocs2 leg order {LF, RF, LH, RH}).
+ * Each QP q follows its own schedule: STANCE before t_start[q] (GaitSchedule's default initial stance phase,
+ * GaitSchedule.cpp:78-101), then the template tiled from t_start[q] (tileModeSequenceTemplate, :106-127). Step k of
+ * the horizon takes the mode at the start of its interval, t = t0 + k dt (post-event, as the SQP's
+ * getIntervalStart, TimeDiscretization.cpp:38-44), with left-closed mode intervals. contact[q][k][leg_map[j]] is
+ * the stance flag of ocs2 leg j. A step whose mode is FLY yields a row without stance leg, which the solver reports
+ * as CMPC_INVALID_CONTACT ("mpc table invalid", CentroidalMPC.cpp:328-330). */
+#define CMPC_GAIT_MAX_MODES 16
+#define CMPC_GAIT_MAX_TEMPLATES 64
+typedef struct cmpc_gait {
+  int n_modes;                                    /* M >= 1 */
+  int mode[CMPC_GAIT_MAX_MODES];                  /* ModeNumber 0 (FLY) .. 15 (STANCE) */
+  double switching_time[CMPC_GAIT_MAX_MODES + 1]; /* M + 1 increasing times; period = t[M] - t[0] */
+} cmpc_gait;
+typedef struct cmpc_gait_table cmpc_gait_table;
+/* The gait.info templates by name (stance, trot, standing_trot, flying_trot, pace, standing_pace, dynamic_walk,
+ * static_walk, amble, lindyhop, skipping, pawup). CMPC_ERR_ARG for an unknown name. */
+int cmpc_gait_builtin(const char* name, cmpc_gait* out);
+/* Device copy of n templates; leg_map[j] = contact column of ocs2 leg j (NULL: {0, 1, 3, 2}, i.e. LF, RF, LH, RH
+ * onto CentroidalMPC's lf, rf, rh, lh order of CentoidMPCTest.cpp:43-46). */
+int cmpc_gait_table_create(const cmpc_gait* gaits, int n, const int* leg_map, cmpc_gait_table** out);
+int cmpc_gait_table_destroy(cmpc_gait_table* table);
+/* contact [B][N][4] (device) from per-QP template ids and start times (device arrays). Asynchronous on stream. An
+ * id outside the table gives all-swing rows (-> CMPC_INVALID_CONTACT downstream). */
+int cmpc_gait_contact_batch(const cmpc_gait_table* table, int B, const int* d_gait_id, const double* d_t_start,
+                            double t0, double dt, int N, uint8_t* d_contact, void* stream);
+
 /* Per-stage device timing with HIP events recorded on the solve stream (used by bench.py for the roofline):
  * after cmpc_profile_begin, each cmpc_solve_batch records events around its three stages (condense, IPM, expand);
  * cmpc_profile_end synchronises and returns the summed milliseconds per stage and the number of calls. */

@@ -1036,3 +1036,28 @@ int oracle_ocp_riccati(int N, int nx, const int* nu, const double* rec, double* 
   free(SmB);
   return st;
 }
+
+/* ---------------------------------------------------------------------------------------------- gait schedule */
+/* GaitSchedule::getModeSchedule keeps a STANCE phase before the tiled template (GaitSchedule.cpp:78-101);
+ * tileModeSequenceTemplate repeats (mode_i, switching_time_{i+1} - switching_time_i) from the start time (:106-127);
+ * modeNumber2StanceLeg decodes ModeNumber bits {LF, RF, LH, RH} = {8, 4, 2, 1} (MotionPhaseDefinition.h:69-124).
+ * The mode of step k is the one in force at t = t0 + k dt, intervals closed on the left. */
+void oracle_gait_contact(const cmpc_gait* g, const int* leg_map, double t_start, double t0, double dt, int N,
+                         uint8_t* contact) {
+  static const int def_map[4] = {0, 1, 3, 2};
+  const int* lm = leg_map ? leg_map : def_map;
+  for (int k = 0; k < N; ++k) {
+    const double t = t0 + (double)k * dt;
+    int mode = 15; /* STANCE */
+    if (!(t < t_start)) {
+      const int M = g->n_modes;
+      const double period = g->switching_time[M] - g->switching_time[0];
+      const double tau = fmod(t - t_start, period) + g->switching_time[0];
+      int i = 0;
+      for (int j = 1; j < M; ++j)
+        if (g->switching_time[j] <= tau) i = j;
+      mode = g->mode[i];
+    }
+    for (int j = 0; j < 4; ++j) contact[k * 4 + lm[j]] = (uint8_t)((mode >> (3 - j)) & 1);
+  }
+}

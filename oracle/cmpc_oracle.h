@@ -89,6 +89,11 @@ int oracle_ocp_solve(int N, int nx, const int* nu, const double* x0, const doubl
 int oracle_ocp_riccati(int N, int nx, const int* nu, const double* rec, double* Sm, double* sv, double* K,
                        double* kff);
 
+/* Contact table of one QP from a gait template (cmpc.h cmpc_gait semantics): GaitSchedule.cpp:78-127 tiling,
+ * MotionPhaseDefinition.h:69-124 stance legs, mode at the start of each interval (left-closed). contact [N][4]. */
+void oracle_gait_contact(const cmpc_gait* g, const int* leg_map, double t_start, double t0, double dt, int N,
+                         uint8_t* contact);
+
 /* Small dense helpers exported for tests. */
 int oracle_cholesky(int n, double* A, int lda);                       /* in place, lower; 0 ok, -1 not PD */
 void oracle_chol_solve(int n, const double* L, int lda, double* b);   /* solves (L L^T) x = b in place */

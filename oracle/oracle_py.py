@@ -88,6 +88,9 @@ def lib():
         L.oracle_ocp_condense.argtypes = [C.c_int, C.c_int, i, d, d, d, d]
         L.oracle_ocp_solve.argtypes = [C.c_int, C.c_int, i, d, d, d, d]
         L.oracle_ocp_riccati.argtypes = [C.c_int, C.c_int, i, d, d, d, d, d]
+        L.oracle_gait_contact.argtypes = [C.c_void_p, i, C.c_double, C.c_double, C.c_double, C.c_int,
+                                          C.POINTER(C.c_uint8)]
+        L.oracle_gait_contact.restype = None
         L.oracle_cholesky.argtypes = [C.c_int, d, C.c_int]
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         _lib = L
@@ -251,6 +254,15 @@ def ocp_riccati(N, nx, nu, rec):
         o += nu[k] * nx
         ok += nu[k]
     return Sm, sv, Ks, ks, st
+
+
+def gait_contact(gait, t_start, t0, dt, N, leg_map=None):
+    """Contact table [N,4] of one QP; gait is a cheeta_mpc.Gait (same struct layout as cmpc_gait)."""
+    out = np.zeros((N, 4), np.uint8)
+    lm = None if leg_map is None else np.ascontiguousarray(leg_map, np.int32)
+    lib().oracle_gait_contact(C.byref(gait), _p(lm, C.c_int) if lm is not None else None, t_start, t0, dt, N,
+                              _p(out, C.c_uint8))
+    return out
 
 
 def philox(ctr, key):

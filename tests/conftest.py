@@ -25,3 +25,10 @@ def cm():
 def op():
     import oracle_py
     return oracle_py
+
+
+@pytest.fixture(scope="session")
+def cmh():
+    """The package for host-only calls (no device needed: defaults, built-in tables, struct layouts)."""
+    import cheeta_mpc
+    return cheeta_mpc
