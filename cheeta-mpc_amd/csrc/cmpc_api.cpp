@@ -184,6 +184,7 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.status = c->status;
   a.iters = c->iters;
   a.u = (T*)c->u;
+  a.warm = 0;
   a.s = dev_settings(c->settings);
   a.stamps = nullptr;
   return a;
@@ -217,10 +218,17 @@ int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 
-int run_ipm(cmpc_ctx* c, int B, hipStream_t st) {
+int run_ipm(cmpc_ctx* c, int B, hipStream_t st, int warm = 0) {
   int r;
-  if (c->precision == CMPC_F64) r = launch_ipm<double>(ipm_args<double>(c), B, st);
-  else r = launch_ipm<float>(ipm_args<float>(c), B, st);
+  if (c->precision == CMPC_F64) {
+    IpmArgs<double> a = ipm_args<double>(c);
+    a.warm = warm;
+    r = launch_ipm<double>(a, B, st);
+  } else {
+    IpmArgs<float> a = ipm_args<float>(c);
+    a.warm = warm;
+    r = launch_ipm<float>(a, B, st);
+  }
   return r == 0 ? CMPC_OK : CMPC_ERR_HIP;
 }
 
@@ -386,6 +394,12 @@ int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
 
 int cmpc_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                      const uint8_t* contact, double* u, double* x, int* status, int* iters, void* stream) {
+  return cmpc_solve_batch_warm(c, B, x0, xref, foot, contact, nullptr, u, x, status, iters, stream);
+}
+
+int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                          const uint8_t* contact, const double* u_init, double* u, double* x, int* status, int* iters,
+                          void* stream) {
   if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !status) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
   hipStream_t st = (hipStream_t)stream;
@@ -394,8 +408,12 @@ int cmpc_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, c
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   int r = run_condense(c, B, x0, xref, foot, contact, st);
   if (r != CMPC_OK) return r;
+  const int warm = (u_init && c->settings.warm_start != 0) ? 1 : 0;
+  if (warm && launch_pack_warm(u_init, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B,
+                               st) != 0)
+    return CMPC_ERR_HIP;
   if (ev) HIP_OK(hipEventRecord(ev[1], st));
-  r = run_ipm(c, B, st);
+  r = run_ipm(c, B, st, warm);
   if (r != CMPC_OK) return r;
   if (ev) HIP_OK(hipEventRecord(ev[2], st));
   ExpandArgs e;
@@ -418,6 +436,11 @@ int cmpc_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, c
   if (launch_expand(e, B, st) != 0) return CMPC_ERR_HIP;
   if (ev) HIP_OK(hipEventRecord(ev[3], st));
   return CMPC_OK;
+}
+
+int cmpc_shift_inputs(int B, int N, const double* d_u, int shift, double* d_u_out, void* stream) {
+  if (B < 0 || N < 1 || shift < 0 || !d_u || !d_u_out || d_u == d_u_out) return CMPC_ERR_ARG;
+  return launch_shift_inputs(d_u, N, shift, d_u_out, B, (hipStream_t)stream) == 0 ? CMPC_OK : CMPC_ERR_HIP;
 }
 
 int cmpc_profile_begin(cmpc_ctx* c, int max_calls) {

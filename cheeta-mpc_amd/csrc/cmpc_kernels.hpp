@@ -55,7 +55,8 @@ struct IpmArgs {
   const int* nvar;
   int* status;  // in: condense status (non-zero = skip); out: solver status
   int* iters;
-  T* u;         // [B][ld]
+  T* u;         // [B][ld]: out; in as the initial point when warm != 0
+  int warm;     // warm start (hpipm_interface::Settings::warm_start, HpipmInterfaceSettings.h:54): u from a.u
   DevSettings s;
   unsigned long long* stamps;  // diagnostic builds only (-DCMPC_IPM_STAMPS): per-QP phase cycles, else null
 };
@@ -107,6 +108,12 @@ int launch_unpack_qp(const void* H_ws, const void* g_ws, const int* nvar, int pr
 int launch_pack_qp(const double* H, const double* g, const double* tri_mu, const double* tri_lo, const double* tri_hi,
                    const int* nvar_in, int precision, int ld, void* H_ws, void* g_ws, void* mu_ws, void* lo_ws,
                    void* hi_ws, int* nvar_ws, int* status_ws, int B, hipStream_t stream);
+
+// warm start: scatter a previous solution u_init [B][N][L][3] into the condensed order of each QP (tri_map)
+int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, const int* status, int precision,
+                     int ld, int N, void* u_ws, int B, hipStream_t stream);
+// receding-horizon shift of a solution: out[k] = in[min(k + shift, N - 1)] per QP
+int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, hipStream_t stream);
 
 // widen/narrow helpers used by the test hooks
 int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream);

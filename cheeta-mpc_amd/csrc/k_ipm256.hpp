@@ -171,20 +171,25 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
   const bool var = tid < n;
   const T g_i = var ? a.g[(size_t)q * ld + i] : T(0);
   const T mu_i = var ? a.tri_mu[(size_t)q * (ld / 3) + i / 3] : T(0);
-  T u_i = T(0), rg_i = T(0), du_i = T(0);
+  // cold start (warm_start = 0): u = 0; warm start: u from the workspace (cmpc_solve_batch_warm)
+  T u_i = (a.warm && var) ? a.u[(size_t)q * ld + i] : T(0), rg_i = T(0), du_i = T(0);
   const int j = tid;
   const bool con = j < m;
   const int tj = j / 5, rj = j % 5;
   const T lo = con ? a.tri_lo[((size_t)q * (ld / 3) + tj) * 5 + rj] : T(0);
   const T hi = con ? a.tri_hi[((size_t)q * (ld / 3) + tj) * 5 + rj] : T(0);
   const T muj = con ? a.tri_mu[(size_t)q * (ld / 3) + tj] : T(0);
-  T tl = con ? fmax(-lo, T(THR0)) : T(1);
-  T tu = con ? fmax(hi, T(THR0)) : T(1);
+  if (isv) L.vec[tid] = u_i;
+  __syncthreads();
+  const T cu0 = con ? pyr_row<T>(rj, muj, L.vec[3 * tj], L.vec[3 * tj + 1], L.vec[3 * tj + 2]) : T(0);
+  T tl = con ? fmax(cu0 - lo, T(THR0)) : T(1);
+  T tu = con ? fmax(hi - cu0, T(THR0)) : T(1);
   T ll = con ? T(S.mu0) / tl : T(0);
   T lu = con ? T(S.mu0) / tu : T(0);
   T rl = T(0), ru = T(0), itl = T(0), itu = T(0), dtl = T(0), dtu = T(0), dll = T(0), dlu = T(0), rml = T(0),
     rmu = T(0);
   if (tid < NP / 3) L.mut[tid] = tid < nt ? a.tri_mu[(size_t)q * (ld / 3) + tid] : T(0);
+  __syncthreads();  // every thread has read L.vec (initial C u) before the first iteration rewrites it
 
   // ---- block reduction of (max, max, max, sum)
   auto block_reduce = [&](T& r0, T& r1, T& r2, T& r3) {

@@ -157,8 +157,11 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   const bool vin = lane < n;
   const T g_v = vin ? A.g[(size_t)q * ld + lane] : T(0);
   const T mu_v = vin ? A.tri_mu[(size_t)q * (ld / 3) + lane / 3] : T(0);
-  T u_v = T(0);
-  // ---- pyramid rows j = lane + 64 cc; cold start (warm_start = 0): u = 0, slacks clipped at THR0, lam = mu0 / t
+  // cold start (warm_start = 0): u = 0; warm start: u from the workspace (previous solution, cmpc_solve_batch_warm)
+  T u_v = (A.warm && vin) ? A.u[(size_t)q * ld + lane] : T(0);
+  if (A.warm) L.v[lane] = u_v;
+  cbar();
+  // ---- pyramid rows j = lane + 64 cc: slacks of C u clipped at THR0, lam = mu0 / t
   T tl[2], tu[2], ll[2], lu[2], lo[2], hi[2], muc[2];
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc) {
@@ -168,11 +171,14 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     lo[cc] = on ? A.tri_lo[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
     hi[cc] = on ? A.tri_hi[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
     muc[cc] = on ? A.tri_mu[(size_t)q * (ld / 3) + t] : T(0);
-    tl[cc] = on ? fmax(-lo[cc], T(THR0)) : T(1);
-    tu[cc] = on ? fmax(hi[cc], T(THR0)) : T(1);
+    T cu0 = T(0);
+    if (A.warm && on) cu0 = pyr_row<T>(j % 5, muc[cc], L.v[3 * t], L.v[3 * t + 1], L.v[3 * t + 2]);
+    tl[cc] = on ? fmax(cu0 - lo[cc], T(THR0)) : T(1);
+    tu[cc] = on ? fmax(hi[cc] - cu0, T(THR0)) : T(1);
     ll[cc] = on ? T(S.mu0) / tl[cc] : T(0);
     lu[cc] = on ? T(S.mu0) / tu[cc] : T(0);
   }
+  cbar();
 
   // C x for the lane's two pyramid rows, x already in L.v (CentroidalMPC.cpp:186-190)
   auto apply_C = [&](T (&out)[2]) {

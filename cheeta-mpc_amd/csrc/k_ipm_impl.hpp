@@ -107,10 +107,12 @@ __global__ __launch_bounds__(64, WPE) void k_ipm128(IpmArgs<T> a) {
       const int i = lane + 64 * r;
       g_r[r] = i < n ? a.g[(size_t)q * ld + i] : T(0);
       mu_r[r] = i < n ? a.tri_mu[(size_t)q * (ld / 3) + i / 3] : T(0);
-      u_r[r] = T(0);
+      // cold start (warm_start = 0): u = 0; warm start: u from the workspace (cmpc_solve_batch_warm)
+      u_r[r] = (a.warm && i < n) ? a.u[(size_t)q * ld + i] : T(0);
+      L.v[i] = u_r[r];
     }
-    // ---- constraint data (row j = lane + 64 c), cold start (warm_start = 0): u = 0, slacks clipped at THR0,
-    //      lam = mu0 / t
+    wave_sync();
+    // ---- constraint data (row j = lane + 64 c): slacks of C u clipped at THR0, lam = mu0 / t
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int j = lane + 64 * c;
@@ -121,13 +123,15 @@ __global__ __launch_bounds__(64, WPE) void k_ipm128(IpmArgs<T> a) {
       L.lo[j] = lo;
       L.hi[j] = hi;
       L.mu[j] = on ? a.tri_mu[(size_t)q * (ld / 3) + t] : T(0);
-      const T tl = on ? fmax(-lo, T(THR0)) : T(1);
-      const T tu = on ? fmax(hi, T(THR0)) : T(1);
+      const T cu0 = on ? pyr_row<T>(j % 5, L.mu[j], L.v[3 * t], L.v[3 * t + 1], L.v[3 * t + 2]) : T(0);
+      const T tl = on ? fmax(cu0 - lo, T(THR0)) : T(1);
+      const T tu = on ? fmax(hi - cu0, T(THR0)) : T(1);
       L.tl[j] = tl;
       L.tu[j] = tu;
       L.ll[j] = on ? T(S.mu0) / tl : T(0);
       L.lu[j] = on ? T(S.mu0) / tu : T(0);
     }
+    wave_sync();
   }
 
   // out_c = C x_r  (pyramid rows of each triple), written to an LDS constraint array

@@ -645,3 +645,59 @@ int launch_pack_qp(const double* H, const double* g, const double* tri_mu, const
 }
 
 }  // namespace cmpc
+
+namespace cmpc {
+
+// ------------------------------------------------------------------------------------------------ warm start
+// Previous solution u_init [B][N][L][3] -> condensed order of each QP (the stance triples listed by tri_map), the
+// initial point of the IPM when hpipm_interface::Settings::warm_start != 0 (HpipmInterfaceSettings.h:54). One
+// thread per condensed variable slot; QPs rejected by the condensing (status != SUCCESS) are left alone.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_warm(const double* u_init, const int* tri_map, const int* nvar,
+                                                   const int* status, int ld, int N, T* u_ws, int B) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)B * ld) return;
+  const int q = (int)(e / ld), i = (int)(e % ld);
+  if (status[q] != CMPC_SUCCESS) return;
+  const int n = nvar[q];
+  T v = T(0);
+  if (i < n) {
+    const int km = tri_map[(size_t)q * (ld / 3) + i / 3];  // k * L + leg
+    v = (T)u_init[(size_t)q * N * NU + (size_t)km * 3 + i % 3];
+  }
+  u_ws[e] = v;
+}
+
+int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, const int* status, int precision,
+                     int ld, int N, void* u_ws, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  const long total = (long)B * ld;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (precision == CMPC_F64)
+    hipLaunchKernelGGL((k_pack_warm<double>), grid, dim3(256), 0, stream, u_init, tri_map, nvar, status, ld, N,
+                       (double*)u_ws, B);
+  else
+    hipLaunchKernelGGL((k_pack_warm<float>), grid, dim3(256), 0, stream, u_init, tri_map, nvar, status, ld, N,
+                       (float*)u_ws, B);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Receding-horizon shift (the role of MultipleShootingSolver::initializeStateInputTrajectories,
+// MultipleShootingSolver.cpp:220-266, for a fixed grid): out[q][k] = in[q][min(k + shift, N - 1)].
+__global__ __launch_bounds__(256) void k_shift_inputs(const double* in, int N, int shift, double* out, int B) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)B * N * NU) return;
+  const int q = (int)(e / (N * NU)), r = (int)(e % (N * NU));
+  const int k = r / NU, j = r % NU;
+  const int ks = k + shift < N ? k + shift : N - 1;
+  out[e] = in[(size_t)q * N * NU + (size_t)ks * NU + j];
+}
+
+int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  const long total = (long)B * N * NU;
+  hipLaunchKernelGGL(k_shift_inputs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, in, N, shift, out, B);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace cmpc

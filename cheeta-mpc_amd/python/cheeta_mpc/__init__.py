@@ -76,6 +76,8 @@ def lib():
     L.cmpc_get_model.argtypes = [vp, P(Model)]
     L.cmpc_ctx_ld.argtypes = [vp]
     L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
+    L.cmpc_solve_batch_warm.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, i, i, vp]
+    L.cmpc_shift_inputs.argtypes = [C.c_int, C.c_int, d, C.c_int, d, vp]
     L.cmpc_solve_batch_host.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i]
     L.cmpc_condense_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
     L.cmpc_qp_solve_batch.argtypes = [vp, C.c_int, d, d, i, d, d, d, d, i, i, vp]
@@ -223,23 +225,28 @@ class Engine:
         _chk(lib().cmpc_set_settings(self.ctx, C.byref(s)), "cmpc_set_settings")
 
     # ---- device-pointer entry points (async on stream)
-    def solve_device(self, B, x0, xref, foot, contact, u, x, status, iters, stream=None):
-        _chk(lib().cmpc_solve_batch(self.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, u.ptr,
-                                    x.ptr if x is not None else None, status.ptr,
-                                    iters.ptr if iters is not None else None, stream), "cmpc_solve_batch")
+    def solve_device(self, B, x0, xref, foot, contact, u, x, status, iters, stream=None, u_init=None):
+        """u_init (DeviceArray [B,N,L,3], may be u itself): warm start when settings.warm_start != 0."""
+        _chk(lib().cmpc_solve_batch_warm(self.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr,
+                                         u_init.ptr if u_init is not None else None, u.ptr,
+                                         x.ptr if x is not None else None, status.ptr,
+                                         iters.ptr if iters is not None else None, stream), "cmpc_solve_batch_warm")
 
     # ---- host convenience
-    def solve(self, x0, xref, foot, contact, want_x=True):
+    def solve(self, x0, xref, foot, contact, want_x=True, u_init=None):
         B = x0.shape[0]
         N = self.model.N
         d = {k: DeviceArray.from_host(v) for k, v in
              dict(x0=np.asarray(x0, np.float64), xref=np.asarray(xref, np.float64),
                   foot=np.asarray(foot, np.float64), contact=np.asarray(contact, np.uint8)).items()}
         u = DeviceArray((B, N, NL, 3), np.float64)
+        if u_init is not None:
+            u.upload(np.asarray(u_init, np.float64).reshape(B, N, NL, 3))
         x = DeviceArray((B, N + 1, NX), np.float64) if want_x else None
         st = DeviceArray((B,), np.int32)
         it = DeviceArray((B,), np.int32)
-        self.solve_device(B, d["x0"], d["xref"], d["foot"], d["contact"], u, x, st, it)
+        self.solve_device(B, d["x0"], d["xref"], d["foot"], d["contact"], u, x, st, it,
+                          u_init=u if u_init is not None else None)
         return u.host(), (x.host() if want_x else None), st.host(), it.host()
 
     def condense(self, x0, xref, foot, contact):
@@ -360,6 +367,17 @@ class GaitTable:
                 lib().cmpc_gait_table_destroy(self.ptr)
         except Exception:
             pass
+
+
+def shift_inputs(u, shift=1):
+    """Receding-horizon shift on the device (cmpc_shift_inputs): out[:, k] = u[:, min(k + shift, N - 1)]."""
+    u = np.ascontiguousarray(u, np.float64)
+    B, N = u.shape[0], u.shape[1]
+    din = DeviceArray.from_host(u)
+    dout = DeviceArray(u.shape, np.float64)
+    _chk(lib().cmpc_shift_inputs(B, N, din.ptr, shift, dout.ptr, None), "cmpc_shift_inputs")
+    _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+    return dout.host()
 
 
 def device_info():

@@ -67,7 +67,8 @@ enum cmpc_qp_status {
 enum cmpc_precision { CMPC_F64 = 0, CMPC_F32 = 1 };
 
 /* Interior-point settings. Field-for-field mirror of hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57),
- * defaults identical (cmpc_settings_default). hpipm_mode / warm_start / ric_alg are accepted for ABI parity. */
+ * defaults identical (cmpc_settings_default). hpipm_mode / ric_alg are accepted for ABI parity; warm_start != 0
+ * makes cmpc_solve_batch_warm start from the given inputs. */
 typedef struct cmpc_settings {
   int hpipm_mode;   /* 0 = SPEED (default) */
   int iter_max;     /* 30 */
@@ -122,6 +123,18 @@ int cmpc_ctx_ld(const cmpc_ctx* ctx);
 int cmpc_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                      const uint8_t* d_contact, double* d_u, double* d_x, int* d_status, int* d_iters, void* stream);
 /* Same, host pointers; synchronous. */
+/* Warm-started hot path (hpipm_interface::Settings::warm_start, HpipmInterfaceSettings.h:54; HPIPM's warm_start = 1,
+ * primal): with settings.warm_start != 0 and d_u_init != NULL, the IPM of each QP starts from d_u_init
+ * [B][N][L][3] (e.g. the previous MPC tick's solution shifted by cmpc_shift_inputs; swing entries ignored) with
+ * slacks of C u clipped at 1 and lam = mu0 / t; otherwise identical to cmpc_solve_batch (cold start). d_u_init may
+ * alias d_u. */
+int cmpc_solve_batch_warm(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                          const uint8_t* d_contact, const double* d_u_init, double* d_u, double* d_x, int* d_status,
+                          int* d_iters, void* stream);
+/* Receding-horizon shift of a batch of solutions on the device: out[q][k] = u[q][min(k + shift, N - 1)] (the role of
+ * MultipleShootingSolver::initializeStateInputTrajectories, MultipleShootingSolver.cpp:220-266, on a fixed grid).
+ * d_u_out must not alias d_u. */
+int cmpc_shift_inputs(int B, int N, const double* d_u, int shift, double* d_u_out, void* stream);
 int cmpc_solve_batch_host(cmpc_ctx* ctx, int B, const double* x0, const double* xref, const double* foot,
                           const uint8_t* contact, double* u, double* x, int* status, int* iters);
 

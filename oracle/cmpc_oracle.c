@@ -389,8 +389,10 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
     *mv[i] = p;
     p += m + 1;
   }
-  for (int i = 0; i < n; ++i) u[i] = 0.0;
-  /* cold start (warm_start = 0): u = 0, slacks clipped at THR0, lam = mu0 / t */
+  /* cold start (warm_start = 0): u = 0; warm start (HPIPM warm_start = 1, primal): u as given on entry.
+   * Then slacks of C u clipped at THR0, lam = mu0 / t */
+  if (!s->warm_start)
+    for (int i = 0; i < n; ++i) u[i] = 0.0;
   for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], u + 3 * t, W.cu + 5 * t);
   for (int j = 0; j < m; ++j) {
     W.tl[j] = dmax(W.cu[j] - tri_lo[j], THR0);
@@ -561,9 +563,17 @@ int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const doubl
   double* uc = (double*)malloc(sizeof(double) * ld);
   int* map = (int*)malloc(sizeof(int) * ld);
   int n = 0, it = 0;
+  double* u_in = NULL;
+  if (s->warm_start) { /* u holds the initial guess [N][L][3] on entry */
+    u_in = (double*)malloc(sizeof(double) * N * NU);
+    memcpy(u_in, u, sizeof(double) * N * NU);
+  }
   memset(u, 0, sizeof(double) * N * NU);
   int st = oracle_condense(c, x0, xref, foot, contact, ld, &n, H, g, mu, lo, hi, map);
   if (st == CMPC_SUCCESS) {
+    if (u_in)
+      for (int t = 0; t < n / 3; ++t)
+        for (int d = 0; d < 3; ++d) uc[3 * t + d] = u_in[map[t] * 3 + d];
     st = oracle_qp_ipm(n, ld, H, g, mu, lo, hi, s, uc, NULL, NULL, &it, NULL);
     for (int t = 0; t < n / 3; ++t)
       for (int d = 0; d < 3; ++d) u[map[t] * 3 + d] = uc[3 * t + d];
@@ -592,6 +602,7 @@ int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const doubl
   free(hi);
   free(uc);
   free(map);
+  free(u_in);
   return st;
 }
 

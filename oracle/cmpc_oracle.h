@@ -60,6 +60,7 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
                   double* res);
 
 /* Whole hot path for one QP: u [N][L][3] (zeros for swing), x [(N+1)][13] (may be NULL). */
+/* u [N][L][3] out; with s->warm_start != 0 it is also the initial guess on entry (HPIPM warm_start = 1). */
 int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
                      const double* foot, const uint8_t* contact, double* u, double* x, int* iters);
 

@@ -124,12 +124,13 @@ def generate(model, seed, B, gait=0, offset=0):
     return x0, xref, foot, contact
 
 
-def solve_batch(model, settings, x0, xref, foot, contact, nthreads=1, want_x=True):
+def solve_batch(model, settings, x0, xref, foot, contact, nthreads=1, want_x=True, u_init=None):
+    """u_init [B,N,L,3]: initial guess, used when settings.warm_start != 0."""
     B = x0.shape[0]
     N = model.N
     x0, xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot))
     contact = np.ascontiguousarray(contact, dtype=np.uint8)
-    u = np.zeros((B, N, NL, 3))
+    u = np.zeros((B, N, NL, 3)) if u_init is None else np.array(u_init, dtype=np.float64).reshape(B, N, NL, 3)
     x = np.zeros((B, N + 1, NX)) if want_x else None
     st = np.zeros(B, dtype=np.int32)
     it = np.zeros(B, dtype=np.int32)
