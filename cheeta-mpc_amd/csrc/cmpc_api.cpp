@@ -40,6 +40,8 @@ struct cmpc_ctx {
   int* nvar;
   int* status;
   int* iters;
+  double *lin, *uj, *uq;
+  int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   // host-API staging (grown on demand, outside the async path)
   char* stage;
   size_t stage_bytes;
@@ -63,7 +65,7 @@ int ld_for(const cmpc_model& m) {
 }
 
 struct Layout {
-  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, total;
+  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, lin, uj, uq, stq, itq, done, sqpi, qpi, cnt, total;
 };
 
 Layout layout(int ld, int precision, int B) {
@@ -86,6 +88,16 @@ Layout layout(int ld, int precision, int B) {
   L.nvar = take((size_t)B * sizeof(int));
   L.status = take((size_t)B * sizeof(int));
   L.iters = take((size_t)B * sizeof(int));
+  // SQP (cmpc_sqp_solve_batch): linearisation points, iterate, QP solution, per-QP flags and counters
+  L.lin = take((size_t)B * MAXN * 6 * 8);
+  L.uj = take((size_t)B * MAXN * NU * 8);
+  L.uq = take((size_t)B * MAXN * NU * 8);
+  L.stq = take((size_t)B * sizeof(int));
+  L.itq = take((size_t)B * sizeof(int));
+  L.done = take((size_t)B * sizeof(int));
+  L.sqpi = take((size_t)B * sizeof(int));
+  L.qpi = take((size_t)B * sizeof(int));
+  L.cnt = take(sizeof(int));
   L.total = o;
   return L;
 }
@@ -159,6 +171,7 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.xref = xref;
   a.foot = foot;
   a.contact = contact;
+  a.lin = nullptr;
   a.H = (T*)c->H;
   a.g = (T*)c->g;
   a.tri_mu = (T*)c->tri_mu;
@@ -194,8 +207,9 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
 // the 128 and 256 classes, each launch skipping at once what a smaller class already did (nvar hints).
 template <typename T>
 int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                   const uint8_t* contact, hipStream_t st) {
+                   const uint8_t* contact, hipStream_t st, const double* lin) {
   CondenseArgs<T> a = condense_args<T>(c, x0, xref, foot, contact);
+  a.lin = lin;
   int r = 0;
   const bool small = c->model.N <= CMPC_C64_MAXN;
   if (small) r = launch_condense64<T>(a, B, st);
@@ -211,10 +225,10 @@ int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, con
 }
 
 int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                 const uint8_t* contact, hipStream_t st) {
+                 const uint8_t* contact, hipStream_t st, const double* lin = nullptr) {
   int r;
-  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st);
-  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st);
+  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin);
+  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin);
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 
@@ -345,6 +359,15 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->nvar = (int*)(c->ws + L.nvar);
   c->status = (int*)(c->ws + L.status);
   c->iters = (int*)(c->ws + L.iters);
+  c->lin = (double*)(c->ws + L.lin);
+  c->uj = (double*)(c->ws + L.uj);
+  c->uq = (double*)(c->ws + L.uq);
+  c->stq = (int*)(c->ws + L.stq);
+  c->itq = (int*)(c->ws + L.itq);
+  c->done = (int*)(c->ws + L.done);
+  c->sqpi = (int*)(c->ws + L.sqpi);
+  c->qpi = (int*)(c->ws + L.qpi);
+  c->cnt = (int*)(c->ws + L.cnt);
   if (hipMalloc((void**)&c->d_model, sizeof(DevModel)) != hipSuccess) {
     if (c->own_ws) (void)hipFree(c->ws);
     delete c;
@@ -435,6 +458,77 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
   e.iters_out = iters;
   if (launch_expand(e, B, st) != 0) return CMPC_ERR_HIP;
   if (ev) HIP_OK(hipEventRecord(ev[3], st));
+  return CMPC_OK;
+}
+
+int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, int sqp_iter_max, double sqp_tol, double* u, double* x, int* status,
+                         int* qp_iters, int* sqp_iters, void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !status || sqp_iter_max < 0 ||
+      !(sqp_tol >= 0.0))
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  // U_0: the QP at the reference linearisation, cold (oracle_sqp_solve)
+  int r = cmpc_solve_batch_warm(c, B, x0, xref, foot, contact, nullptr, u, nullptr, status, c->qpi, stream);
+  if (r != CMPC_OK) return r;
+  SqpArgs a;
+  a.model = c->d_model;
+  a.x0 = x0;
+  a.xref = xref;
+  a.foot = foot;
+  a.contact = contact;
+  a.u = u;
+  a.x = x;
+  a.status = status;
+  a.iters = c->qpi;
+  a.uj = c->uj;
+  a.uq = c->uq;
+  a.status_q = c->stq;
+  a.iters_q = c->itq;
+  a.lin = c->lin;
+  a.done = c->done;
+  a.qp_iters = c->qpi;  // the cold iterations (written there by the solve above) accumulate in place
+  a.sqp_iters = c->sqpi;
+  a.count = c->cnt;
+  a.tol = sqp_tol;
+  if (launch_sqp(0, a, B, st) != 0) return CMPC_ERR_HIP;
+  for (int it = 0; it < sqp_iter_max; ++it) {
+    r = run_condense(c, B, x0, xref, foot, contact, st, c->lin);
+    if (r != CMPC_OK) return r;
+    if (launch_pack_warm(c->uj, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B, st) != 0)
+      return CMPC_ERR_HIP;
+    r = run_ipm(c, B, st, 1);
+    if (r != CMPC_OK) return r;
+    ExpandArgs e;
+    e.model = c->d_model;
+    e.ld = c->ld;
+    e.x0 = x0;
+    e.xref = xref;
+    e.foot = foot;
+    e.contact = contact;
+    e.tri_map = c->tri_map;
+    e.nvar = c->nvar;
+    e.status = c->status;
+    e.u_ws = c->u;
+    e.precision = c->precision;
+    e.u = c->uq;
+    e.x = nullptr;
+    e.status_out = c->stq;
+    e.iters_ws = c->iters;
+    e.iters_out = c->itq;
+    if (launch_expand(e, B, st) != 0) return CMPC_ERR_HIP;
+    if (launch_sqp(1, a, B, st) != 0) return CMPC_ERR_HIP;
+    // early exit once every QP has converged (one 4-byte read-back per SQP iteration)
+    if (launch_sqp(3, a, B, st) != 0) return CMPC_ERR_HIP;
+    int left = 0;
+    HIP_OK(hipMemcpyAsync(&left, c->cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (left == 0) break;
+  }
+  if (launch_sqp(2, a, B, st) != 0) return CMPC_ERR_HIP;
+  if (qp_iters) HIP_OK(hipMemcpyAsync(qp_iters, c->qpi, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  if (sqp_iters) HIP_OK(hipMemcpyAsync(sqp_iters, c->sqpi, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
   return CMPC_OK;
 }
 

@@ -32,6 +32,10 @@ struct CondenseArgs {
   const double* xref;
   const double* foot;
   const uint8_t* contact;
+  // SQP linearisation point [B][N][6] = (c_bar_k, F_bar_k = sum_i e_ik f_bar_ik), or null for (c_ref_k, 0): the
+  // lever arm becomes p_ik - c_bar_k and L+ gains dt F_bar_k x (c_k - c_bar_k) (Taylor expansion of the bilinear
+  // dt sum_i e_ik (p_ik - c_k) x f_ik of CentroidalMPC.cpp:86)
+  const double* lin;
   T* H;
   T* g;
   T* tri_mu;
@@ -108,6 +112,30 @@ int launch_unpack_qp(const void* H_ws, const void* g_ws, const int* nvar, int pr
 int launch_pack_qp(const double* H, const double* g, const double* tri_mu, const double* tri_lo, const double* tri_hi,
                    const int* nvar_in, int precision, int ld, void* H_ws, void* g_ws, void* mu_ws, void* lo_ws,
                    void* hi_ws, int* nvar_ws, int* status_ws, int B, hipStream_t stream);
+
+// batched SQP on the bilinear NLP (k_sqp.hip)
+struct SqpArgs {
+  const DevModel* model;
+  const double* x0;
+  const double* xref;
+  const double* foot;
+  const uint8_t* contact;
+  double* u;           // [B][N][L][3]: in = the cold QP's solution (k_sqp_init), out = the SQP solution (final)
+  double* x;           // [B][N+1][13] nonlinear rollout (final) or null
+  int* status;         // [B] in: cold status; out: SQP status
+  const int* iters;    // [B] cold QP iterations (may be null)
+  double* uj;          // [B][N][12] iterate
+  const double* uq;    // [B][N][12] QP solution at lin
+  const int* status_q; // [B]
+  const int* iters_q;  // [B]
+  double* lin;         // [B][N][6]
+  int* done;           // [B]
+  int* qp_iters;       // [B] total IPM iterations
+  int* sqp_iters;      // [B]
+  int* count;          // [1] QPs not done (k_sqp_count)
+  double tol;
+};
+int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream);  // 0 init, 1 step, 2 final, 3 count
 
 // warm start: scatter a previous solution u_init [B][N][L][3] into the condensed order of each QP (tri_map)
 int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, const int* status, int precision,

@@ -190,9 +190,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     s_next[c] = nx;
     if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)s_ns[kc]));
     const double* p = s_foot + (kc * L + leg) * 3;
-    rx = p[0] - s_xref[kc * NX + 0];
-    ry = p[1] - s_xref[kc * NX + 1];
-    rz = p[2] - s_xref[kc * NX + 2];
+    const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : s_xref + kc * NX;
+    rx = p[0] - cb[0];
+    ry = p[1] - cb[1];
+    rz = p[2] - cb[2];
   }
   // free response x_hat_k = Aqp x0 (thread 0)
   double xh[NX];
@@ -210,10 +211,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     const int buf = k & 1;
     const int km = k - 1;
     // (a) gamma <- A_{k-1} gamma + B_{k-1}[:, c]
+    const double* lk = a.lin ? a.lin + ((size_t)q * N + km) * 6 : nullptr;
     if (col && kc <= km) {
-      const T* Mk = nullptr;
-      (void)Mk;
       T Lx = gam[6], Ly = gam[7], Lz = gam[8];
+      if (lk) {  // L+ += dt F_bar x c (SQP linearisation)
+        const T Fx = T(lk[3]), Fy = T(lk[4]), Fz = T(lk[5]);
+        const T c0 = gam[0], c1 = gam[1], c2 = gam[2];
+        gam[6] += dt * (Fy * c2 - Fz * c1);
+        gam[7] += dt * (Fz * c0 - Fx * c2);
+        gam[8] += dt * (Fx * c1 - Fy * c0);
+      }
 #pragma unroll
       for (int s = 0; s < 3; ++s) gam[s] += dt * gam[3 + s];
       gam[9] += T(s_M[km][0]) * Lx + T(s_M[km][1]) * Ly + T(s_M[km][2]) * Lz;
@@ -243,6 +250,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
       xn[5] += M->dt * xh[12];
       for (int r = 0; r < 3; ++r)
         xn[9 + r] = xh[9 + r] + s_M[km][r * 3 + 0] * xh[6] + s_M[km][r * 3 + 1] * xh[7] + s_M[km][r * 3 + 2] * xh[8];
+      if (lk) {  // dt F_bar x (c - c_bar)
+        const double d0 = xh[0] - lk[0], d1 = xh[1] - lk[1], d2 = xh[2] - lk[2];
+        xn[6] += M->dt * (lk[4] * d2 - lk[5] * d1);
+        xn[7] += M->dt * (lk[5] * d0 - lk[3] * d2);
+        xn[8] += M->dt * (lk[3] * d1 - lk[4] * d0);
+      }
       xn[12] = xh[12];
       for (int s = 0; s < NX; ++s) {
         xh[s] = xn[s];

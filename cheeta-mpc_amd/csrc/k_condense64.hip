@@ -181,10 +181,10 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
       }
       if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)__popc(sb)));
       const double* p = a.foot + (((size_t)q * (N + 1) + kc) * L + leg) * 3;
-      const double* xr = a.xref + ((size_t)q * (N + 1) + kc) * NX;
-      rx = p[0] - xr[0];
-      ry = p[1] - xr[1];
-      rz = p[2] - xr[2];
+      const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : a.xref + ((size_t)q * (N + 1) + kc) * NX;
+      rx = p[0] - cb[0];
+      ry = p[1] - cb[1];
+      rz = p[2] - cb[2];
     }
     S.nx[c] = nx;
     S.pv[c] = pv;
@@ -208,8 +208,16 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
   for (int k = 1; k <= N; ++k) {
     const int km = k - 1;
     // (a) gamma <- A_{k-1} gamma + B_{k-1}[:, c]
+    const double* lk = a.lin ? a.lin + ((size_t)q * N + km) * 6 : nullptr;
     if (colv && kc <= km) {
       const T Lx = gam[6], Ly = gam[7], Lz = gam[8];
+      if (lk) {  // L+ += dt F_bar x c (SQP linearisation)
+        const T Fx = T(lk[3]), Fy = T(lk[4]), Fz = T(lk[5]);
+        const T c0 = gam[0], c1 = gam[1], c2 = gam[2];
+        gam[6] += dt * (Fy * c2 - Fz * c1);
+        gam[7] += dt * (Fz * c0 - Fx * c2);
+        gam[8] += dt * (Fx * c1 - Fy * c0);
+      }
 #pragma unroll
       for (int s = 0; s < 3; ++s) gam[s] += dt * gam[3 + s];
       gam[9] += T(S.M[km][0]) * Lx + T(S.M[km][1]) * Ly + T(S.M[km][2]) * Lz;
@@ -243,6 +251,11 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
       if (s >= 9 && s < 12) {
         const int r = s - 9;
         xn += S.M[km][r * 3 + 0] * S.xh[6] + S.M[km][r * 3 + 1] * S.xh[7] + S.M[km][r * 3 + 2] * S.xh[8];
+      }
+      if (lk && s >= 6 && s < 9) {  // dt F_bar x (c - c_bar)
+        const double d0 = S.xh[0] - lk[0], d1 = S.xh[1] - lk[1], d2 = S.xh[2] - lk[2];
+        const double cr = s == 6 ? lk[4] * d2 - lk[5] * d1 : (s == 7 ? lk[5] * d0 - lk[3] * d2 : lk[3] * d1 - lk[4] * d0);
+        xn += M->dt * cr;
       }
       xs = xn;
       const double qd = M->qdiag[k][s];

@@ -1,0 +1,220 @@
+// k_sqp.hip — device side of the batched Gauss-Newton SQP on the bilinear centroidal NLP.
+//
+// The reference's NLP keeps the lever arm bilinear, L+ = L + dt sum_i e_i (p_i - c) x f_i (CentroidalMPC.cpp:86),
+// and IPOPT solves it; ocs2's SQP counterpart is MultipleShootingSolver::runImpl (MultipleShootingSolver.cpp:146-214)
+// with its line search takeStep (:509-619). Here every QP of the batch iterates (cmpc_sqp_solve_batch, cmpc_api.cpp):
+//   lin_j = (c_k, F_k = sum_i e_ik f_ik) of the nonlinear rollout of U_j   (k_sqp_init / k_sqp_step)
+//   U_qp  = the condensed QP linearised at lin_j, warm-started from U_j  (the hot path itself, CondenseArgs::lin)
+//   alpha = the first of 1, 1/2, ..., 1/128 with J(U_j + alpha d) <= J(U_j), d = U_qp - U_j, else 0
+// with J the NLP cost of the nonlinear rollout (single shooting: no defects, so the cost alone is the merit).
+// The restatement is oracle/cmpc_oracle.c:oracle_sqp_solve / oracle_nlp_rollout_cost; the rollout and cost follow
+// its floating-point order with contraction off, so the line-search decisions are the oracle's.
+//
+// One wave per QP: lanes 0..7 evaluate the eight trial steps, lane 8 the current iterate (alpha = 0), each lane a
+// whole rollout (13 states x N steps, scalar); the step, the convergence test and the next linearisation point are
+// then lane-parallel over the 12 N inputs.
+#include <hip/hip_runtime.h>
+
+#include "cmpc/cmpc.h"
+#include "cmpc_device.hpp"
+#include "cmpc_kernels.hpp"
+
+namespace cmpc {
+
+namespace {
+
+#pragma clang fp contract(off)
+
+// Nonlinear rollout + NLP cost of the inputs u0 + alpha (u1 - u0) (u1 may be null: alpha unused). Writes
+// lin [N][6] and x [(N+1)][13] when non-null. Mirrors oracle_nlp_rollout_cost operation for operation.
+__device__ double rollout_cost(const DevModel* M, const double* x0, const double* xref, const double* foot,
+                               const uint8_t* ct, const double* u0, const double* u1, double alpha, double* lin,
+                               double* xo) {
+  const int N = M->N;
+  const double dt = M->dt;
+  double xs[NX], xn[NX];
+  for (int s = 0; s < NX; ++s) xs[s] = x0[s];
+  if (xo)
+    for (int s = 0; s < NX; ++s) xo[s] = xs[s];
+  double J = 0.0;
+  double unext[NU];
+  auto input = [&](int k, int j) -> double {
+    const double a = u0[(size_t)k * NU + j];
+    return u1 ? a + alpha * (u1[(size_t)k * NU + j] - a) : a;
+  };
+  for (int j = 0; j < NU; ++j) unext[j] = input(0, j);
+  for (int k = 0; k < N; ++k) {
+    double uk[NU];
+    for (int j = 0; j < NU; ++j) uk[j] = unext[j];
+    if (k + 1 < N)
+      for (int j = 0; j < NU; ++j) unext[j] = input(k + 1, j);
+    double F[3] = {0.0, 0.0, 0.0}, Tq[3] = {0.0, 0.0, 0.0};
+    int ns = 0;
+    for (int i = 0; i < NL; ++i) {
+      if (!ct[k * NL + i]) continue;
+      ++ns;
+      const double* p = foot + ((size_t)k * NL + i) * 3;
+      const double* f = uk + 3 * i;
+      const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
+      F[0] += f[0];
+      F[1] += f[1];
+      F[2] += f[2];
+      Tq[0] += ry * f[2] - rz * f[1];
+      Tq[1] += rz * f[0] - rx * f[2];
+      Tq[2] += rx * f[1] - ry * f[0];
+    }
+    if (lin)
+      for (int d = 0; d < 3; ++d) {
+        lin[k * 6 + d] = xs[d];
+        lin[k * 6 + 3 + d] = F[d];
+      }
+    for (int j = 0; j < NU; ++j) {
+      const int i = j / 3;
+      const double fd = (j % 3 == 2 && ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
+      const double e = uk[j] - fd;
+      J += M->Wf[j] * e * e;
+      if (k + 1 < N) {
+        const double r = unext[j] - uk[j];
+        J += M->Wr[j] * r * r;
+      }
+    }
+    double sp, cp;
+    sincos(xref[k * NX + 11], &sp, &cp);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int d = 0; d < 3; ++d) xn[d] = xs[d] + dt * xs[3 + d];
+    xn[3] = xs[3] + dt * (F[0] / M->mass);
+    xn[4] = xs[4] + dt * (F[1] / M->mass);
+    xn[5] = xs[5] + dt * (xs[12] + F[2] / M->mass);
+    for (int d = 0; d < 3; ++d) xn[6 + d] = xs[6 + d] + dt * Tq[d];
+    for (int a = 0; a < 3; ++a) {
+      double m = 0.0;
+      for (int b = 0; b < 3; ++b) {
+        double s2 = 0.0;
+        for (int e = 0; e < 3; ++e) s2 += M->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
+        m += dt * s2 * xs[6 + b];
+      }
+      xn[9 + a] = xs[9 + a] + m;
+    }
+    xn[12] = xs[12];
+    for (int s = 0; s < NX; ++s) xs[s] = xn[s];
+    if (xo)
+      for (int s = 0; s < NX; ++s) xo[(size_t)(k + 1) * NX + s] = xs[s];
+    for (int s = 0; s < NX; ++s) {
+      const double e = xs[s] - xref[(k + 1) * NX + s];
+      J += 0.5 * M->qdiag[k + 1][s] * e * e;
+    }
+  }
+  return J;
+}
+
+// U_j <- the cold QP's solution, lin <- its rollout; QPs the cold QP rejected are done from the start.
+__global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
+  const int q = blockIdx.x;
+  const DevModel* M = a.model;
+  const int N = M->N;
+  const int nu = N * NU;
+  for (int i = threadIdx.x; i < nu; i += 64) a.uj[(size_t)q * nu + i] = a.u[(size_t)q * nu + i];
+  if (threadIdx.x == 0) {
+    a.done[q] = a.status[q] != CMPC_SUCCESS ? 1 : 0;
+    a.sqp_iters[q] = 0;
+    a.qp_iters[q] = a.iters ? a.iters[q] : 0;
+    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, a.foot + (size_t)q * (N + 1) * NL * 3,
+                 a.contact + (size_t)q * N * NL, a.u + (size_t)q * nu, nullptr, 0.0, a.lin + (size_t)q * N * 6,
+                 nullptr);
+  }
+}
+
+// One SQP step for every QP not yet done, after the QP at lin returned uq / status_q / iters_q.
+__global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
+  const int q = blockIdx.x;
+  if (a.done[q]) return;
+  const int lane = threadIdx.x;
+  const DevModel* M = a.model;
+  const int N = M->N;
+  const int nu = N * NU;
+  double* uj = a.uj + (size_t)q * nu;
+  const double* uq = a.uq + (size_t)q * nu;
+  const double* x0 = a.x0 + (size_t)q * NX;
+  const double* xr = a.xref + (size_t)q * (N + 1) * NX;
+  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
+  const uint8_t* ct = a.contact + (size_t)q * N * NL;
+  if (lane == 0) {
+    a.sqp_iters[q] += 1;
+    a.qp_iters[q] += a.iters_q[q];
+  }
+  if (a.status_q[q] != CMPC_SUCCESS) {  // keep U_j, report the subproblem's status (oracle_sqp_solve)
+    if (lane == 0) {
+      a.status[q] = a.status_q[q];
+      a.done[q] = 1;
+    }
+    return;
+  }
+  // trial steps: lane m < 8 -> alpha = 2^-m, lane 8 -> the current iterate
+  double J = 0.0;
+  if (lane <= 8) {
+    const double alpha = lane < 8 ? ldexp(1.0, -lane) : 0.0;
+    J = lane < 8 ? rollout_cost(M, x0, xr, ft, ct, uj, uq, alpha, nullptr, nullptr)
+                 : rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, nullptr, nullptr);
+  }
+  const double J0 = __shfl(J, 8, 64);
+  const unsigned long long ok = __ballot(lane < 8 && J <= J0);
+  const double alpha = ok ? ldexp(1.0, -(__ffsll((long long)ok) - 1)) : 0.0;
+  // |d|_inf, |U_j|_inf, then the step (lane-parallel over the inputs)
+  double dm = 0.0, um = 0.0;
+  for (int i = lane; i < nu; i += 64) {
+    dm = fmax(dm, fabs(uq[i] - uj[i]));
+    um = fmax(um, fabs(uj[i]));
+  }
+  dm = wave_max(dm);
+  um = wave_max(um);
+  __syncthreads();
+  if (alpha > 0.0)
+    for (int i = lane; i < nu; i += 64) uj[i] = uj[i] + alpha * (uq[i] - uj[i]);
+  const bool conv = alpha == 0.0 || alpha * dm <= a.tol * fmax(1.0, um);
+  __syncthreads();
+  if (lane == 0) {
+    if (conv) a.done[q] = 1;
+    rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, a.lin + (size_t)q * N * 6, nullptr);
+  }
+}
+
+// Final outputs: u <- U_j, x <- its nonlinear rollout, status stays, iteration counts reported.
+__global__ __launch_bounds__(64) void k_sqp_final(SqpArgs a) {
+  const int q = blockIdx.x;
+  const DevModel* M = a.model;
+  const int N = M->N;
+  const int nu = N * NU;
+  for (int i = threadIdx.x; i < nu; i += 64) a.u[(size_t)q * nu + i] = a.uj[(size_t)q * nu + i];
+  __syncthreads();
+  if (threadIdx.x == 0 && a.x)
+    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, a.foot + (size_t)q * (N + 1) * NL * 3,
+                 a.contact + (size_t)q * N * NL, a.u + (size_t)q * nu, nullptr, 0.0, nullptr,
+                 a.x + (size_t)q * (N + 1) * NX);
+}
+
+// number of QPs not yet done -> count[0]
+__global__ __launch_bounds__(256) void k_sqp_count(const int* done, int B, int* count) {
+  int c = 0;
+  for (int q = threadIdx.x; q < B; q += 256) c += done[q] ? 0 : 1;
+  c = wave_sum(c);
+  __shared__ int s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) count[0] = s[0] + s[1] + s[2] + s[3];
+}
+
+}  // namespace
+
+int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  switch (which) {
+    case 0: hipLaunchKernelGGL(k_sqp_init, dim3(B), dim3(64), 0, stream, a); break;
+    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL(k_sqp_final, dim3(B), dim3(64), 0, stream, a); break;
+    case 3: hipLaunchKernelGGL(k_sqp_count, dim3(1), dim3(256), 0, stream, a.done, B, a.count); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace cmpc

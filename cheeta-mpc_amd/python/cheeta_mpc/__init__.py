@@ -77,6 +77,7 @@ def lib():
     L.cmpc_ctx_ld.argtypes = [vp]
     L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
     L.cmpc_solve_batch_warm.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, i, i, vp]
+    L.cmpc_sqp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, i, i, i, vp]
     L.cmpc_shift_inputs.argtypes = [C.c_int, C.c_int, d, C.c_int, d, vp]
     L.cmpc_solve_batch_host.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i]
     L.cmpc_condense_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
@@ -248,6 +249,24 @@ class Engine:
         self.solve_device(B, d["x0"], d["xref"], d["foot"], d["contact"], u, x, st, it,
                           u_init=u if u_init is not None else None)
         return u.host(), (x.host() if want_x else None), st.host(), it.host()
+
+    def sqp_solve(self, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7, want_x=True):
+        """Batched SQP on the bilinear NLP (cmpc_sqp_solve_batch): (u, x, status, qp_iters, sqp_iters)."""
+        B = x0.shape[0]
+        N = self.model.N
+        d = {k: DeviceArray.from_host(v) for k, v in
+             dict(x0=np.asarray(x0, np.float64), xref=np.asarray(xref, np.float64),
+                  foot=np.asarray(foot, np.float64), contact=np.asarray(contact, np.uint8)).items()}
+        u = DeviceArray((B, N, NL, 3), np.float64)
+        x = DeviceArray((B, N + 1, NX), np.float64) if want_x else None
+        st = DeviceArray((B,), np.int32)
+        qi = DeviceArray((B,), np.int32)
+        si = DeviceArray((B,), np.int32)
+        _chk(lib().cmpc_sqp_solve_batch(self.ctx, B, d["x0"].ptr, d["xref"].ptr, d["foot"].ptr, d["contact"].ptr,
+                                        sqp_iter_max, sqp_tol, u.ptr, x.ptr if want_x else None, st.ptr, qi.ptr,
+                                        si.ptr, None), "cmpc_sqp_solve_batch")
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return u.host(), (x.host() if want_x else None), st.host(), qi.host(), si.host()
 
     def condense(self, x0, xref, foot, contact):
         B = x0.shape[0]

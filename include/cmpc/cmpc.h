@@ -131,6 +131,18 @@ int cmpc_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_x
 int cmpc_solve_batch_warm(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                           const uint8_t* d_contact, const double* d_u_init, double* d_u, double* d_x, int* d_status,
                           int* d_iters, void* stream);
+/* Batched Gauss-Newton SQP on the bilinear centroidal NLP: the reference's NLP keeps the lever
+ * arm (p_i - c) x f_i bilinear (CentroidalMPC.cpp:86). Per QP: U_0 = the QP at the reference linearisation (as
+ * cmpc_solve_batch); then up to sqp_iter_max times: linearise at the nonlinear rollout of U_j (lever arm p - c_k,
+ * dt F_k x (c - c_k) coupling), solve that QP warm-started from U_j, and take the first step of 1, 1/2, ..., 1/128
+ * that does not raise the NLP cost of the nonlinear rollout (MultipleShootingSolver::runImpl / takeStep,
+ * MultipleShootingSolver.cpp:146-214, :509-619, play this role in ocs2). A QP stops when its accepted step is
+ * <= sqp_tol max(1, |U_j|_inf) or no step is accepted. d_x (optional) receives the nonlinear rollout. d_qp_iters:
+ * total IPM iterations, d_sqp_iters: SQP iterations (both optional). Synchronises the stream once per SQP iteration
+ * (early exit when every QP has converged). */
+int cmpc_sqp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                         const uint8_t* d_contact, int sqp_iter_max, double sqp_tol, double* d_u, double* d_x,
+                         int* d_status, int* d_qp_iters, int* d_sqp_iters, void* stream);
 /* Receding-horizon shift of a batch of solutions on the device: out[q][k] = u[q][min(k + shift, N - 1)] (the role of
  * MultipleShootingSolver::initializeStateInputTrajectories, MultipleShootingSolver.cpp:220-266, on a fixed grid).
  * d_u_out must not alias d_u. */

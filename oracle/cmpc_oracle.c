@@ -74,9 +74,26 @@ void oracle_consts_init(const cmpc_model* m, oracle_consts* c) {
 
 void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                           double* A, double* B) {
+  oracle_srbd_dynamics_lin(c, xref, foot, contact, NULL, A, B, NULL);
+}
+
+/* lin [N][6] = (c_bar_k, F_bar_k): Taylor expansion of the bilinear dt sum_i e_ik (p_ik - c_k) x f_ik
+ * (CentroidalMPC.cpp:86) at (c_bar, f_bar): lever arm p_ik - c_bar_k, A_k gains dt [F_bar_k]x in the L rows / c
+ * columns, affine term b_k = -dt F_bar_k x c_bar_k. lin = NULL: (c_ref_k, 0), b = 0. b [N][13] may be NULL. */
+void oracle_srbd_dynamics_lin(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                              const double* lin, double* A, double* B, double* b) {
   const int N = c->N, L = c->L;
   const double dt = c->dt;
   for (int k = 0; k < N; ++k) {
+    if (b) {
+      memset(b + (size_t)k * NX, 0, sizeof(double) * NX);
+      if (lin) {
+        const double* lk = lin + (size_t)k * 6;
+        b[k * NX + 6] = -dt * (lk[4] * lk[2] - lk[5] * lk[1]);
+        b[k * NX + 7] = -dt * (lk[5] * lk[0] - lk[3] * lk[2]);
+        b[k * NX + 8] = -dt * (lk[3] * lk[1] - lk[4] * lk[0]);
+      }
+    }
     double* Ak = A + (size_t)k * NX * NX;
     double* Bk = B + (size_t)k * NX * NU;
     memset(Ak, 0, sizeof(double) * NX * NX);
@@ -96,11 +113,18 @@ void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const doub
         for (int e = 0; e < 3; ++e) s += c->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
         Ak[(9 + a) * NX + 6 + b] = dt * s;
       }
+    if (lin) { /* L+ += dt [F_bar]x c */
+      const double* F = lin + (size_t)k * 6 + 3;
+      const double SF[9] = {0.0, -F[2], F[1], F[2], 0.0, -F[0], -F[1], F[0], 0.0};
+      for (int a2 = 0; a2 < 3; ++a2)
+        for (int b2 = 0; b2 < 3; ++b2) Ak[(6 + a2) * NX + b2] = dt * SF[a2 * 3 + b2];
+    }
     /* inputs: v+ += dt/m f_i, L+ += dt [r_ik]x f_i for stance legs */
+    const double* cb = lin ? lin + (size_t)k * 6 : xref + (size_t)k * NX;
     for (int i = 0; i < L; ++i) {
       if (!contact[k * L + i]) continue;
       const double* p = foot + ((size_t)k * L + i) * 3;
-      const double rx = p[0] - xref[k * NX + 0], ry = p[1] - xref[k * NX + 1], rz = p[2] - xref[k * NX + 2];
+      const double rx = p[0] - cb[0], ry = p[1] - cb[1], rz = p[2] - cb[2];
       const double S[9] = {0.0, -rz, ry, rz, 0.0, -rx, -ry, rx, 0.0};
       for (int d = 0; d < 3; ++d) Bk[(3 + d) * NU + 3 * i + d] = dt / c->mass;
       for (int a = 0; a < 3; ++a)
@@ -122,6 +146,11 @@ static int fdes_and_check(const oracle_consts* c, const uint8_t* contact, double
 
 int oracle_condense_full(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
                          const uint8_t* contact, double* H, double* g) {
+  return oracle_condense_full_lin(c, x0, xref, foot, contact, NULL, H, g);
+}
+
+int oracle_condense_full_lin(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                             const uint8_t* contact, const double* lin, double* H, double* g) {
   const int N = c->N, L = c->L, n = NU * N;
   double* fdes = (double*)malloc(sizeof(double) * N * L);
   const int st = fdes_and_check(c, contact, fdes);
@@ -131,7 +160,8 @@ int oracle_condense_full(const oracle_consts* c, const double* x0, const double*
   }
   double* A = (double*)malloc(sizeof(double) * N * NX * NX);
   double* B = (double*)malloc(sizeof(double) * N * NX * NU);
-  oracle_srbd_dynamics(c, xref, foot, contact, A, B);
+  double* bb = (double*)malloc(sizeof(double) * N * NX);
+  oracle_srbd_dynamics_lin(c, xref, foot, contact, lin, A, B, bb);
   double* G = (double*)calloc((size_t)NX * n, sizeof(double));  /* block row of Bqp for x_k: 13 x 12N */
   double* G2 = (double*)malloc(sizeof(double) * NX * n);
   double xh[NX], xh2[NX], e[NX];
@@ -151,7 +181,7 @@ int oracle_condense_full(const oracle_consts* c, const double* x0, const double*
       for (int j = 0; j < NU; ++j) G2[r * n + NU * k + j] += Bk[r * NU + j];
       double s = 0.0;
       for (int t = 0; t < NX; ++t) s += Ak[r * NX + t] * xh[t];
-      xh2[r] = s;
+      xh2[r] = s + bb[k * NX + r];
     }
     memcpy(G, G2, sizeof(double) * NX * n);
     memcpy(xh, xh2, sizeof(xh));
@@ -186,6 +216,7 @@ int oracle_condense_full(const oracle_consts* c, const double* x0, const double*
   free(fdes);
   free(A);
   free(B);
+  free(bb);
   free(G);
   free(G2);
   return CMPC_SUCCESS;
@@ -194,6 +225,12 @@ int oracle_condense_full(const oracle_consts* c, const double* x0, const double*
 int oracle_condense(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
                     const uint8_t* contact, int ld, int* n_out, double* H, double* g, double* tri_mu, double* tri_lo,
                     double* tri_hi, int* tri_map) {
+  return oracle_condense_lin(c, x0, xref, foot, contact, NULL, ld, n_out, H, g, tri_mu, tri_lo, tri_hi, tri_map);
+}
+
+int oracle_condense_lin(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                        const uint8_t* contact, const double* lin, int ld, int* n_out, double* H, double* g,
+                        double* tri_mu, double* tri_lo, double* tri_hi, int* tri_map) {
   const int N = c->N, L = c->L, nf = NU * N;
   *n_out = 0;
   int idx[NU * 64];
@@ -217,7 +254,7 @@ int oracle_condense(const oracle_consts* c, const double* x0, const double* xref
   if (n > ld) return CMPC_TOO_LARGE;
   double* Hf = (double*)malloc(sizeof(double) * nf * nf);
   double* gf = (double*)malloc(sizeof(double) * nf);
-  const int st = oracle_condense_full(c, x0, xref, foot, contact, Hf, gf);
+  const int st = oracle_condense_full_lin(c, x0, xref, foot, contact, lin, Hf, gf);
   if (st != CMPC_SUCCESS) {
     free(Hf);
     free(gf);
@@ -554,6 +591,12 @@ void oracle_qp_kkt(int n, int ld, const double* H, const double* g, const double
 
 int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
                      const double* foot, const uint8_t* contact, double* u, double* x, int* iters) {
+  return oracle_solve_one_lin(c, s, x0, xref, foot, contact, NULL, u, x, iters);
+}
+
+int oracle_solve_one_lin(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                         const double* foot, const uint8_t* contact, const double* lin, double* u, double* x,
+                         int* iters) {
   const int N = c->N, ld = NU * N;
   double* H = (double*)malloc(sizeof(double) * ld * ld);
   double* g = (double*)malloc(sizeof(double) * ld);
@@ -569,7 +612,7 @@ int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const doubl
     memcpy(u_in, u, sizeof(double) * N * NU);
   }
   memset(u, 0, sizeof(double) * N * NU);
-  int st = oracle_condense(c, x0, xref, foot, contact, ld, &n, H, g, mu, lo, hi, map);
+  int st = oracle_condense_lin(c, x0, xref, foot, contact, lin, ld, &n, H, g, mu, lo, hi, map);
   if (st == CMPC_SUCCESS) {
     if (u_in)
       for (int t = 0; t < n / 3; ++t)
@@ -582,17 +625,19 @@ int oracle_solve_one(const oracle_consts* c, const cmpc_settings* s, const doubl
     /* rollout x_{k+1} = A_k x_k + B_k u_k */
     double* A = (double*)malloc(sizeof(double) * N * NX * NX);
     double* B = (double*)malloc(sizeof(double) * N * NX * NU);
-    oracle_srbd_dynamics(c, xref, foot, contact, A, B);
+    double* bb = (double*)malloc(sizeof(double) * N * NX);
+    oracle_srbd_dynamics_lin(c, xref, foot, contact, lin, A, B, bb);
     memcpy(x, x0, sizeof(double) * NX);
     for (int k = 0; k < N; ++k)
       for (int r = 0; r < NX; ++r) {
         double acc = 0.0;
         for (int t = 0; t < NX; ++t) acc += A[(size_t)k * NX * NX + r * NX + t] * x[k * NX + t];
         for (int j = 0; j < NU; ++j) acc += B[(size_t)k * NX * NU + r * NU + j] * u[k * NU + j];
-        x[(k + 1) * NX + r] = acc;
+        x[(k + 1) * NX + r] = acc + bb[k * NX + r];
       }
     free(A);
     free(B);
+    free(bb);
   }
   if (iters) *iters = it;
   free(H);
@@ -1071,4 +1116,140 @@ void oracle_gait_contact(const cmpc_gait* g, const int* leg_map, double t_start,
     }
     for (int j = 0; j < 4; ++j) contact[k * 4 + lm[j]] = (uint8_t)((mode >> (3 - j)) & 1);
   }
+}
+
+/* ------------------------------------------------------------------------------------------------- SQP (§8f) */
+/* Nonlinear SRBD rollout with the bilinear lever arm of CentroidalMPC.cpp:85-92 (L+ = L + dt sum_i e_i (p_i - c) x
+ * f_i, c+ = c + dt v, v+ = v + dt (g e_z + sum_i e_i f_i / m)), Theta as the QP (A.2), and the NLP cost of
+ * CentroidalMPC.cpp:203-231 in its sumsqr form: sum_k w (x_k - xref_k)^2 (Q-bar / 2) + sum w_f (f - f^des)^2 +
+ * sum w_r (f_{k+1} - f_k)^2 over all legs (swing forces are 0). x [(N+1)][13] and lin [N][6] (c_k, sum_i e_ik f_ik)
+ * may be NULL. Returns the cost. Floating-point order is the one k_sqp_step follows. */
+double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                               const uint8_t* contact, const double* u, double* x, double* lin) {
+  const int N = c->N, L = c->L;
+  const double dt = c->dt;
+  double xs[NX], xn[NX];
+  memcpy(xs, x0, sizeof(xs));
+  if (x) memcpy(x, x0, sizeof(double) * NX);
+  double J = 0.0;
+  for (int k = 0; k < N; ++k) {
+    const double* uk = u + (size_t)k * NU;
+    double F[3] = {0.0, 0.0, 0.0}, T[3] = {0.0, 0.0, 0.0};
+    int ns = 0;
+    for (int i = 0; i < L; ++i) {
+      if (!contact[k * L + i]) continue;
+      ++ns;
+      const double* p = foot + ((size_t)k * L + i) * 3;
+      const double* f = uk + 3 * i;
+      const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
+      F[0] += f[0];
+      F[1] += f[1];
+      F[2] += f[2];
+      T[0] += ry * f[2] - rz * f[1];
+      T[1] += rz * f[0] - rx * f[2];
+      T[2] += rx * f[1] - ry * f[0];
+    }
+    if (lin) {
+      for (int d = 0; d < 3; ++d) {
+        lin[k * 6 + d] = xs[d];
+        lin[k * 6 + 3 + d] = F[d];
+      }
+    }
+    /* force tracking and force rate */
+    for (int j = 0; j < NU; ++j) {
+      const int i = j / 3;
+      const double fd = (j % 3 == 2 && contact[k * L + i] && ns > 0) ? c->mass * GRAV / (double)ns : 0.0;
+      const double e = uk[j] - fd;
+      J += c->Wf[j] * e * e;
+      if (k + 1 < N) {
+        const double r = u[(size_t)(k + 1) * NU + j] - uk[j];
+        J += c->Wr[j] * r * r;
+      }
+    }
+    const double psi = xref[k * NX + 11];
+    const double cp = cos(psi), sp = sin(psi);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int d = 0; d < 3; ++d) xn[d] = xs[d] + dt * xs[3 + d];
+    xn[3] = xs[3] + dt * (F[0] / c->mass);
+    xn[4] = xs[4] + dt * (F[1] / c->mass);
+    xn[5] = xs[5] + dt * (xs[12] + F[2] / c->mass);
+    for (int d = 0; d < 3; ++d) xn[6 + d] = xs[6 + d] + dt * T[d];
+    for (int a = 0; a < 3; ++a) {
+      double m = 0.0;
+      for (int b = 0; b < 3; ++b) {
+        double s2 = 0.0;
+        for (int e = 0; e < 3; ++e) s2 += c->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
+        m += dt * s2 * xs[6 + b];
+      }
+      xn[9 + a] = xs[9 + a] + m;
+    }
+    xn[12] = xs[12];
+    memcpy(xs, xn, sizeof(xs));
+    if (x) memcpy(x + (size_t)(k + 1) * NX, xs, sizeof(double) * NX);
+    for (int sI = 0; sI < NX; ++sI) {
+      const double e = xs[sI] - xref[(k + 1) * NX + sI];
+      J += 0.5 * c->qdiag[k + 1][sI] * e * e;
+    }
+  }
+  return J;
+}
+
+/* Gauss-Newton SQP on the centroidal NLP (the role of MultipleShootingSolver::runImpl, MultipleShootingSolver.cpp:
+ * 146-214, for this problem; single shooting, so the merit is the NLP cost of the nonlinear rollout):
+ *   U_0 = QP at the reference (lin = NULL);
+ *   repeat: lin = (c_k, F_k) of the rollout of U_j; U_qp = QP at lin, warm-started from U_j; d = U_qp - U_j;
+ *           alpha = the first of 1, 1/2, ..., 1/128 with J(U_j + alpha d) <= J(U_j) (else 0);
+ *           U_{j+1} = U_j + alpha d; stop when alpha |d|_inf <= sqp_tol max(1, |U_j|_inf) or alpha = 0.
+ * The pyramid constraints are linear in f, so every trial point stays feasible. */
+int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
+                     const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
+                     double* x, int* qp_iters, int* sqp_iters) {
+  const int N = c->N, nu = N * NU;
+  double* uq = (double*)malloc(sizeof(double) * nu);
+  double* ut = (double*)malloc(sizeof(double) * nu);
+  double* lin = (double*)malloc(sizeof(double) * N * 6);
+  cmpc_settings sw = *s;
+  sw.warm_start = 0;
+  int it = 0, its = 0;
+  int st = oracle_solve_one_lin(c, &sw, x0, xref, foot, contact, NULL, u, NULL, &it);
+  int tot = it;
+  if (st == CMPC_SUCCESS) {
+    sw.warm_start = 1;
+    for (its = 0; its < sqp_iter_max; ++its) {
+      const double J0 = oracle_nlp_rollout_cost(c, x0, xref, foot, contact, u, NULL, lin);
+      memcpy(uq, u, sizeof(double) * nu);
+      const int sq = oracle_solve_one_lin(c, &sw, x0, xref, foot, contact, lin, uq, NULL, &it);
+      tot += it;
+      if (sq != CMPC_SUCCESS) {
+        st = sq;
+        break;
+      }
+      double dmax_ = 0.0, umax = 0.0;
+      for (int i = 0; i < nu; ++i) {
+        dmax_ = dmax(dmax_, fabs(uq[i] - u[i]));
+        umax = dmax(umax, fabs(u[i]));
+      }
+      double alpha = 0.0, a = 1.0;
+      for (int m = 0; m < 8; ++m, a *= 0.5) {
+        for (int i = 0; i < nu; ++i) ut[i] = u[i] + a * (uq[i] - u[i]);
+        if (oracle_nlp_rollout_cost(c, x0, xref, foot, contact, ut, NULL, NULL) <= J0) {
+          alpha = a;
+          break;
+        }
+      }
+      if (alpha > 0.0)
+        for (int i = 0; i < nu; ++i) u[i] = u[i] + alpha * (uq[i] - u[i]);
+      if (alpha == 0.0 || alpha * dmax_ <= sqp_tol * dmax(1.0, umax)) {
+        ++its;
+        break;
+      }
+    }
+  }
+  if (x) oracle_nlp_rollout_cost(c, x0, xref, foot, contact, u, x, NULL);
+  if (qp_iters) *qp_iters = tot;
+  if (sqp_iters) *sqp_iters = its;
+  free(uq);
+  free(ut);
+  free(lin);
+  return st;
 }

@@ -39,6 +39,25 @@ void oracle_consts_init(const cmpc_model* m, oracle_consts* c);
 void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                           double* A, double* B);
 
+/* Linearisation at lin [N][6] = (c_bar_k, F_bar_k) (NULL: (c_ref_k, 0)); affine term b [N][13] (may be NULL). */
+void oracle_srbd_dynamics_lin(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                              const double* lin, double* A, double* B, double* b);
+int oracle_condense_full_lin(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                             const uint8_t* contact, const double* lin, double* Hfull, double* gfull);
+int oracle_condense_lin(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                        const uint8_t* contact, const double* lin, int ld, int* n, double* H, double* g,
+                        double* tri_mu, double* tri_lo, double* tri_hi, int* tri_map);
+int oracle_solve_one_lin(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                         const double* foot, const uint8_t* contact, const double* lin, double* u, double* x,
+                         int* iters);
+/* Nonlinear (bilinear lever arm) rollout + NLP cost; x [(N+1)][13], lin [N][6] outputs may be NULL. */
+double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                               const uint8_t* contact, const double* u, double* x, double* lin);
+/* Gauss-Newton SQP on the bilinear NLP; u [N][L][3] out, x [(N+1)][13] nonlinear rollout. */
+int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
+                     const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
+                     double* x, int* qp_iters, int* sqp_iters);
+
 /* Full condensing over all 12N inputs (no elimination): Hfull [12N][12N], gfull [12N]. Returns 0 or
  * CMPC_INVALID_CONTACT. */
 int oracle_condense_full(const oracle_consts* c, const double* x0, const double* xref, const double* foot,

@@ -92,6 +92,11 @@ def lib():
                                           C.POINTER(C.c_uint8)]
         L.oracle_gait_contact.restype = None
         L.oracle_cholesky.argtypes = [C.c_int, d, C.c_int]
+        L.oracle_nlp_rollout_cost.argtypes = [C.c_void_p, d, d, d, u8, d, d, d]
+        L.oracle_nlp_rollout_cost.restype = C.c_double
+        L.oracle_sqp_solve.argtypes = [C.c_void_p, P(Settings), C.c_int, C.c_double, d, d, d, u8, d, d, i, i]
+        L.oracle_srbd_dynamics_lin.argtypes = [C.c_void_p, d, d, u8, d, d, d, d]
+        L.oracle_srbd_dynamics_lin.restype = None
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         _lib = L
     return _lib
@@ -180,6 +185,48 @@ def srbd_dynamics(model, xref, foot, contact):
     contact = np.ascontiguousarray(contact, dtype=np.uint8)
     lib().oracle_srbd_dynamics(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(A), _p(B))
     return A, B
+
+
+def srbd_dynamics_lin(model, xref, foot, contact, lin):
+    """A, B, b of the dynamics linearised at lin [N,6] = (c_bar, F_bar) (None: the reference, b = 0)."""
+    N = model.N
+    c = consts(model)
+    A = np.zeros((N, NX, NX))
+    B = np.zeros((N, NX, NU))
+    b = np.zeros((N, NX))
+    xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    ln = None if lin is None else np.ascontiguousarray(lin, np.float64)
+    lib().oracle_srbd_dynamics_lin(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8),
+                                   _p(ln) if ln is not None else None, _p(A), _p(B), _p(b))
+    return A, B, b
+
+
+def nlp_rollout_cost(model, x0, xref, foot, contact, u):
+    """Nonlinear (bilinear lever arm) rollout and NLP cost of one QP: (J, x [N+1,13], lin [N,6])."""
+    N = model.N
+    c = consts(model)
+    x = np.zeros((N + 1, NX))
+    lin = np.zeros((N, 6))
+    x0, xref, foot, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot, u))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    J = lib().oracle_nlp_rollout_cost(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u), _p(x),
+                                      _p(lin))
+    return J, x, lin
+
+
+def sqp_solve(model, settings, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7):
+    """Gauss-Newton SQP of one QP on the bilinear NLP: (u [N,L,3], x [N+1,13], status, qp_iters, sqp_iters)."""
+    N = model.N
+    c = consts(model)
+    u = np.zeros((N, NL, 3))
+    x = np.zeros((N + 1, NX))
+    x0, xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    qi, si = C.c_int(0), C.c_int(0)
+    st = lib().oracle_sqp_solve(C.byref(c), C.byref(settings), sqp_iter_max, sqp_tol, _p(x0), _p(xref), _p(foot),
+                                _p(contact, C.c_uint8), _p(u), _p(x), C.byref(qi), C.byref(si))
+    return u, x, st, qi.value, si.value
 
 
 def qp_ipm(n, H, g, mu, lo, hi, settings):
