@@ -77,6 +77,9 @@ def main():
     ap.add_argument("--gait", type=int, default=0, help="0 trot (configs 2-4), 1 mixed trot/bound/pronk (config 5)")
     ap.add_argument("--all-stance", action="store_true",
                     help="every leg in stance at every step (pronk): n = 12 N, the largest condensed size class")
+    ap.add_argument("--sqp-iters", type=int, default=0,
+                    help="> 0: one step = the batched SQP on the bilinear NLP (cmpc_sqp_solve_batch), this many "
+                         "SQP iterations at most; not the headline metric")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="QPs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
@@ -109,8 +112,18 @@ def main():
     stream = C.c_void_p()
     H.hipStreamCreate(C.byref(stream))
 
+    sqp_qi = cm.DeviceArray((B,), np.int32)
+    sqp_si = cm.DeviceArray((B,), np.int32)
+
+    def step():
+        if args.sqp_iters > 0:
+            cm.lib().cmpc_sqp_solve_batch(eng.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, args.sqp_iters, 1e-7,
+                                          u.ptr, None, st.ptr, sqp_qi.ptr, sqp_si.ptr, stream)
+        else:
+            eng.solve_device(B, x0, xref, foot, contact, u, None, st, it, stream)
+
     for _ in range(args.warmup):
-        eng.solve_device(B, x0, xref, foot, contact, u, None, st, it, stream)
+        step()
     H.hipStreamSynchronize(stream)
 
     cm.lib().cmpc_profile_begin(eng.ctx, args.steps)
@@ -118,7 +131,7 @@ def main():
     H.hipDeviceSynchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.solve_device(B, x0, xref, foot, contact, u, None, st, it, stream)
+        step()
     H.hipStreamSynchronize(stream)
     H.hipDeviceSynchronize()
     t1 = time.perf_counter()
@@ -130,7 +143,7 @@ def main():
     ms_cond, ms_ipm, ms_exp = (m.value / max(ncalls.value, 1) for m in ms)
 
     status = st.host()
-    iters = it.host()
+    iters = it.host() if args.sqp_iters <= 0 else sqp_qi.host()
     ct = contact.host()
     nvar = 3 * ct.reshape(B, -1).sum(axis=1)
     ok = status == 0
@@ -159,7 +172,7 @@ def main():
                                f"{'all-stance (pronk)' if args.all_stance else ('4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk')}, "
                                f"{'fp64' if prec == cm.F64 else 'fp32'}, full hot path per step",
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
-        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "IPM stage (k_ipm64 n<=64, k_ipm_reg n<=128, k_ipm256 n<=256)",
+        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128 / k_ipm_tiled<8> n<=128, k_ipm_tiled<16> n<=256)",
                      "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
                      "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
@@ -167,8 +180,15 @@ def main():
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,
                    "mean_n": float(nvar.mean())},
     }
+    if args.sqp_iters > 0:
+        si = sqp_si.host()
+        result["metric"] = "centroidal NLP solves/sec by batched SQP (bilinear lever arm), not the headline metric"
+        result["unit"] = "NLPs/s"
+        result["solver"]["mean_sqp_iters"] = float(si.mean())
+        result["solver"]["mean_iters"] = float(iters[ok].mean()) if ok.any() else 0.0
+        result["roofline"] = None
 
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.sqp_iters <= 0:
         S = min(args.cpu_sample, B)
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         hx0, hxr, hft = x0.host()[:S], xref.host()[:S], foot.host()[:S]

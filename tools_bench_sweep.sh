@@ -12,6 +12,8 @@ run c5_mixed_n10_f64 --gait 1
 run pronk_n20_f64 --horizon 20 --all-stance
 run pronk_n20_f32 --horizon 20 --all-stance --precision f32
 run c4_shard_b32768 --batch 32768
+run sqp_mixed_n10_f64 --gait 1 --sqp-iters 10 --steps 5
+run sqp_trot_n10_f64 --sqp-iters 10 --steps 5
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_pronk -o run --output-format csv -- python3 $R/bench.py --horizon 20 --all-stance --steps 5 --cpu-sample 0 > $O/prof_pronk.log 2>&1 || { echo "prof fail"; exit 1; }
 echo sweep_done
