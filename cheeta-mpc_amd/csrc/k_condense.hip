@@ -286,8 +286,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
         int ti, tj;
         tile_of(idx, ti, tj);
         if (16 * ti < ncols) {
+          // K = 12: Bqp row 12 (g_z) is identically 0 and unweighted, rows 13..15 are padding
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
+          for (int s4 = 0; s4 < 3; ++s4) {
             const int s = 4 * s4 + (lane >> 4);
             const T av = s_q[buf][s] * s_G[buf][s][16 * ti + (lane & 15)];
             const T bv = s_G[buf][s][16 * tj + (lane & 15)];

@@ -284,8 +284,10 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
 #pragma unroll
     for (int I = 0; I < 4; ++I) {
       if (16 * I < ncols) {
+        // K = 12: state row 12 (g_z) of Bqp is identically 0 (no input reaches it) and carries no weight
+        // (Qbar_k[12] = 0), rows 13..15 are padding -- the fourth K-slab would add exact zeros
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
+        for (int kk = 0; kk < 3; ++kk) {
           const int s = 4 * kk + g4;
           const T av = S.qg[s][16 * I + rowA];
 #pragma unroll

@@ -4,24 +4,21 @@
 // (HPIPM, called at HpipmInterface.cpp:284) / IPOPT's Newton loop (CentroidalMPC.cpp:354) for the condensed
 // centroidal QP; settings and stopping rule mirror hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57).
 // The iteration is the one restated in oracle/cmpc_oracle.c:oracle_qp_ipm; only the factorisation differs
-// (LDL' with an explicit L^-1 here, Cholesky and triangular solves there), so the two agree to rounding.
+// (LDL' here, Cholesky there), so the two agree to rounding, not bit for bit.
 //
 //   min 1/2 u'Hu + g'u   s.t.  lo <= C u <= hi,   C = blkdiag_t F(mu_t) (5x3 pyramid per stance force triple)
 //
 // MI355X mapping — one wavefront (64 lanes) per QP, no workgroup barriers, 2 waves per SIMD (fp64):
 //   * Newton matrix K = H + C' Sigma C in a 4 x 16-cyclic register tile: lane l = 16a + b holds
 //     K[a + 4r][b + 16c] (r = 0..15, c = 0..3) in register e = 4r + c — 64 values per lane;
-//   * LDL' elimination that also builds L^-1 in place. Step s, every row i > s and every column j != s:
-//     K[i][j] -= K[i][s] K[s][j] / d_s. For j > s this is the right-looking LDL' update; for j < s the same
-//     update accumulates the strict lower part S of the explicit inverse, X = L^-1 with X[i][j] = -S[i][j] / d_j
-//     (column s is left as it is, so the row operations on the identity need no extra storage). The 16 row
+//   * LDL' right-looking factorisation. Step s: K[i][j] -= K[i][s] K[s][j] / d_s for i, j > s. The 16 row
 //     multipliers K[i][s] of a lane live in its own 16-lane DPP row (column s sits in lane b = s % 16), so they
-//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp: dpp_rowf); only the
-//     4 column multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent
-//     through LDS and its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
-//   * solves are K^-1 y = X' D^-1 X y: two matrix-vector products over the 40 registers of the strict lower part
-//     (forward: row sums reduced through LDS; backward: column sums reduced through LDS), no serial sweeps and no
-//     transpose of the factor (lab v6: 0.506 -> 0.449 ms per 4096 QPs, same iteration counts, 5e-16 vs v0);
+//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp); only the 4 column
+//     multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent through LDS and
+//     its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
+//   * the factor is transposed once through LDS into row layout (lane i = row i), each row scaled by 1/d_i, so
+//     every step of the four triangular sweeps is one v_readlane pair + one FMA; finished unknowns are saved to
+//     LDS instead of masking the lanes that are already done;
 //   * vectors are lane-per-variable; the <= 105 pyramid rows are two slots per lane (j = lane + 64 cc) with the
 //     primal-dual state in registers and per-iteration scratch in lane-private LDS;
 //   * H is stored by the condensing kernel in the tile order (h_index, cmpc_kernels.hpp): 64 coalesced 512-B
@@ -32,11 +29,11 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
-#include "dpp_rows.hpp"
+#include <dpp_rows.hpp>
 #include "wave_dpp.hpp"
 
 // In-kernel s_memtime stamps, diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP cycles of each
-// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 lower-part mask, 4 solves,
+// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 transpose, 4 sweeps,
 // 5 predictor rest, 6 corrector rest, 7 update, 8 total.
 #ifdef CMPC_IPM_STAMPS
 #define IPM_STAMP_DECL                                                    \
@@ -123,6 +120,8 @@ __device__ __forceinline__ T pivot_inv(T p) {
   return p > T(Lim<T>::pivot_min) ? y : T(0);
 }
 
+// row-layout column j after the transpose lives in the register the tile used for column j's chunk
+__host__ __device__ constexpr int ridx(int j) { return (j & 15) * 4 + (j >> 4); }
 
 template <typename T>
 struct Lds {
@@ -130,12 +129,63 @@ struct Lds {
   T w[128];         // pyramid-row broadcast
   T rowbuf[2][64];  // factorisation: row s of K as [c*16 + b]
   T dg[64];         // pivots d_s
-  T z[64];          // solve: z permuted as [i % 4][i / 4]
+  T z[64];          // sweep results
   T blk[3][64];     // Newton 3x3 block rows
   T rl[128], ru[128], itl[128], itu[128], rml[128], rmu[128];  // lane-private pyramid-row scratch
-  T scr[1024];      // Hu and solve partial sums
+  T scr[1024];      // Hu partial sums / factor transpose (16 columns at a time)
 };
 
+
+// One DPP-row FMA of the elimination: k += row_newbcast<B0>(src) * m (src = column s of the lane's own rows).
+template <int B0, bool NOP, typename T>
+__device__ __forceinline__ void dfma(T& k, const T& src, T m) {
+  if constexpr (sizeof(T) == 8) {
+    if constexpr (NOP)
+      asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                   : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+    else
+      asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                   : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+  } else {
+    if constexpr (NOP)
+      asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                   : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+    else
+      asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                   : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+  }
+}
+// the same with the DPP source as destination (chunk C0; its lane B0 carries m = 0 and keeps its value)
+template <int B0, bool NOP, typename T>
+__device__ __forceinline__ void dfma_self(T& k, T m) {
+  if constexpr (sizeof(T) == 8) {
+    if constexpr (NOP)
+      asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                   : "+v"(k) : "v"(m), "n"(B0));
+    else
+      asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(k) : "v"(m), "n"(B0));
+  } else {
+    if constexpr (NOP)
+      asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+                   : "+v"(k) : "v"(m), "n"(B0));
+    else
+      asm volatile("v_fmac_f32_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(k) : "v"(m), "n"(B0));
+  }
+}
+// highest chunk of row group r that holds lower-triangle entries (j <= i for some lane)
+__host__ __device__ constexpr int cmax(int r) { return (4 * r + 3) / 16; }
+// Lower-part update of row group R by pivot column s (lane B0 of chunk C0): chunks 0..cmax(R) except SKIP,
+// the DPP source chunk C0 last.
+template <int R, int B0, int C0, int SKIP, bool NOP, typename T>
+__device__ __forceinline__ void row_lower(T (&K)[64], const T (&mm)[4]) {
+  constexpr int CM = cmax(R);
+  constexpr int first = (0 != C0 && 0 != SKIP) ? 0 : (1 != C0 && 1 != SKIP && 1 <= CM) ? 1 : (2 != C0 && 2 != SKIP && 2 <= CM) ? 2 : (3 != C0 && 3 != SKIP && 3 <= CM) ? 3 : -1;
+  sfor<0, CM + 1>([&](auto c_) {
+    constexpr int c = decltype(c_)::value;
+    if constexpr (c != C0 && c != SKIP) dfma<B0, NOP && c == first, T>(K[R * 4 + c], K[R * 4 + C0], mm[c]);
+  });
+  if constexpr (C0 != SKIP) dfma_self<B0, NOP && first < 0, T>(K[R * 4 + C0], mm[C0]);
+}
 }  // namespace ipm64
 
 template <typename T, int WPE>
@@ -457,7 +507,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     IPM_STAMP(1);
 
     // ---- LDL' factorisation in the tile (see header)
-    const bool full = uflag(n > 60);
     T piv = readlane(K[0], 0);
     T invd = pivot_inv(piv);
     T mm[4];
@@ -480,29 +529,35 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       constexpr int c0 = s / 16, b0 = s % 16, a0 = s % 4;
       constexpr int s1 = s + 1;
       constexpr int r1 = s1 / 4, a1 = s1 % 4, c1 = s1 / 16, b1 = s1 % 16;
-      if constexpr (s1 >= 60) {
-        // pivots 60..63 exist only for n > 60; padding rows keep S = 0 and get d = 1
-        if (!full) {
-          L.dg[s1] = T(1);
-          return;
-        }
-      }
       __builtin_amdgcn_sched_barrier(0);
-#ifdef LDL_SPLIT
-      if constexpr (s == LDL_SPLIT) IPM_STAMP(2);
-#endif
       const int la_m = lane0 >> 4, lb_m = lane0 & 15;  // masks and rowbuf addresses: hoisted, loop invariant
-      // look-ahead local row r1 (holds row s+1); for a0 < 3 it is the partial row: rows a + 4 r1 > s iff a > a0
+      // look-ahead: row group r1 (rows > s) and column s+1 of every later row group (lower part only)
       if constexpr (a0 < 3) {
-        if (la_m > a0)
-          dpp_rowf<b0, c0, true, T>(K[r1 * 4], K[r1 * 4 + 1], K[r1 * 4 + 2], K[r1 * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+        if (la_m > a0) row_lower<r1, b0, c0, -1, true, T>(K, mm);
       } else {
-        dpp_rowf<b0, c0, true, T>(K[r1 * 4], K[r1 * 4 + 1], K[r1 * 4 + 2], K[r1 * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+        row_lower<r1, b0, c0, -1, true, T>(K, mm);
       }
+      sfor<r1 + 1, 16>([&](auto r_) {
+        constexpr int r = decltype(r_)::value;
+        if constexpr (c1 == c0)
+          dfma_self<b0, r == r1 + 1, T>(K[r * 4 + c1], mm[c1]);
+        else
+          dfma<b0, r == r1 + 1, T>(K[r * 4 + c1], K[r * 4 + c0], mm[c1]);
+      });
       cbar();
+      // row s+1 into rowbuf: columns <= s+1 from the row itself (chunks 0..c1), columns > s+1 from column s+1
+      // (symmetry of the trailing block; the later column writes overwrite the stale part of chunk c1)
       if (la_m == a1) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lb_m] = K[r1 * 4 + c];
+        for (int c = 0; c <= c1; ++c) L.rowbuf[s1 & 1][c * 16 + lb_m] = K[r1 * 4 + c];
+      }
+      cbar();
+      if (lb_m == b1) {
+        if (la_m > a1) L.rowbuf[s1 & 1][la_m + 4 * r1] = K[r1 * 4 + c1];
+        sfor<r1 + 1, 16>([&](auto r_) {
+          constexpr int r = decltype(r_)::value;
+          L.rowbuf[s1 & 1][la_m + 4 * r] = K[r * 4 + c1];
+        });
       }
       cbar();
       T xn[4];
@@ -515,28 +570,20 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       sfor<r1 + 1, 16>([&](auto r_) {
         constexpr int r = decltype(r_)::value;
         if constexpr (((r - r1 - 1) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-        if constexpr (r == 15) {
-          if (full)  // rows 60..63 are padding when n <= 60 (every trot / bound QP at N = 10): S stays 0 there
-            dpp_rowf<b0, c0, true, T>(K[r * 4], K[r * 4 + 1], K[r * 4 + 2], K[r * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
-        } else {
-          dpp_rowf<b0, c0, false, T>(K[r * 4], K[r * 4 + 1], K[r * 4 + 2], K[r * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
-        }
+        row_lower<r, b0, c0, c1, r == r1 + 1, T>(K, mm);
       });
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const T mv = -(xn[c] * invdn);
         mm[c] = (c == c1 && lb_m == b1) ? T(0) : mv;
+        asm volatile("" : "+v"(mm[c]));  // keep the multipliers here (not sunk into the next step's look-ahead)
       }
       L.dg[s1] = pivn;
     });
     __builtin_amdgcn_sched_barrier(0);
     cbar();
-#ifdef LDL_SPLIT
-    IPM_STAMP(3);
-#else
     IPM_STAMP(2);
-#endif
 
     // ---- pivots -> 1/d_i (same reciprocal as the factorisation); a NaN pivot is NAN_SOL
     {

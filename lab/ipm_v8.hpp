@@ -4,24 +4,21 @@
 // (HPIPM, called at HpipmInterface.cpp:284) / IPOPT's Newton loop (CentroidalMPC.cpp:354) for the condensed
 // centroidal QP; settings and stopping rule mirror hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57).
 // The iteration is the one restated in oracle/cmpc_oracle.c:oracle_qp_ipm; only the factorisation differs
-// (LDL' with an explicit L^-1 here, Cholesky and triangular solves there), so the two agree to rounding.
+// (LDL' here, Cholesky there), so the two agree to rounding, not bit for bit.
 //
 //   min 1/2 u'Hu + g'u   s.t.  lo <= C u <= hi,   C = blkdiag_t F(mu_t) (5x3 pyramid per stance force triple)
 //
 // MI355X mapping — one wavefront (64 lanes) per QP, no workgroup barriers, 2 waves per SIMD (fp64):
 //   * Newton matrix K = H + C' Sigma C in a 4 x 16-cyclic register tile: lane l = 16a + b holds
 //     K[a + 4r][b + 16c] (r = 0..15, c = 0..3) in register e = 4r + c — 64 values per lane;
-//   * LDL' elimination that also builds L^-1 in place. Step s, every row i > s and every column j != s:
-//     K[i][j] -= K[i][s] K[s][j] / d_s. For j > s this is the right-looking LDL' update; for j < s the same
-//     update accumulates the strict lower part S of the explicit inverse, X = L^-1 with X[i][j] = -S[i][j] / d_j
-//     (column s is left as it is, so the row operations on the identity need no extra storage). The 16 row
+//   * LDL' right-looking factorisation. Step s: K[i][j] -= K[i][s] K[s][j] / d_s for i, j > s. The 16 row
 //     multipliers K[i][s] of a lane live in its own 16-lane DPP row (column s sits in lane b = s % 16), so they
-//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp: dpp_rowf); only the
-//     4 column multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent
-//     through LDS and its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
-//   * solves are K^-1 y = X' D^-1 X y: two matrix-vector products over the 40 registers of the strict lower part
-//     (forward: row sums reduced through LDS; backward: column sums reduced through LDS), no serial sweeps and no
-//     transpose of the factor (lab v6: 0.506 -> 0.449 ms per 4096 QPs, same iteration counts, 5e-16 vs v0);
+//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp); only the 4 column
+//     multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent through LDS and
+//     its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
+//   * the factor is transposed once through LDS into row layout (lane i = row i), each row scaled by 1/d_i, so
+//     every step of the four triangular sweeps is one v_readlane pair + one FMA; finished unknowns are saved to
+//     LDS instead of masking the lanes that are already done;
 //   * vectors are lane-per-variable; the <= 105 pyramid rows are two slots per lane (j = lane + 64 cc) with the
 //     primal-dual state in registers and per-iteration scratch in lane-private LDS;
 //   * H is stored by the condensing kernel in the tile order (h_index, cmpc_kernels.hpp): 64 coalesced 512-B
@@ -32,11 +29,11 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
-#include "dpp_rows.hpp"
+#include <dpp_rows.hpp>
 #include "wave_dpp.hpp"
 
 // In-kernel s_memtime stamps, diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP cycles of each
-// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 lower-part mask, 4 solves,
+// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 transpose, 4 sweeps,
 // 5 predictor rest, 6 corrector rest, 7 update, 8 total.
 #ifdef CMPC_IPM_STAMPS
 #define IPM_STAMP_DECL                                                    \
@@ -123,6 +120,8 @@ __device__ __forceinline__ T pivot_inv(T p) {
   return p > T(Lim<T>::pivot_min) ? y : T(0);
 }
 
+// row-layout column j after the transpose lives in the register the tile used for column j's chunk
+__host__ __device__ constexpr int ridx(int j) { return (j & 15) * 4 + (j >> 4); }
 
 template <typename T>
 struct Lds {
@@ -130,10 +129,10 @@ struct Lds {
   T w[128];         // pyramid-row broadcast
   T rowbuf[2][64];  // factorisation: row s of K as [c*16 + b]
   T dg[64];         // pivots d_s
-  T z[64];          // solve: z permuted as [i % 4][i / 4]
+  T z[64];          // sweep results
   T blk[3][64];     // Newton 3x3 block rows
   T rl[128], ru[128], itl[128], itu[128], rml[128], rmu[128];  // lane-private pyramid-row scratch
-  T scr[1024];      // Hu and solve partial sums
+  T scr[1024];      // Hu partial sums / factor transpose (16 columns at a time)
 };
 
 }  // namespace ipm64

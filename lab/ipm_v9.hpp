@@ -4,24 +4,21 @@
 // (HPIPM, called at HpipmInterface.cpp:284) / IPOPT's Newton loop (CentroidalMPC.cpp:354) for the condensed
 // centroidal QP; settings and stopping rule mirror hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57).
 // The iteration is the one restated in oracle/cmpc_oracle.c:oracle_qp_ipm; only the factorisation differs
-// (LDL' with an explicit L^-1 here, Cholesky and triangular solves there), so the two agree to rounding.
+// (LDL' here, Cholesky there), so the two agree to rounding, not bit for bit.
 //
 //   min 1/2 u'Hu + g'u   s.t.  lo <= C u <= hi,   C = blkdiag_t F(mu_t) (5x3 pyramid per stance force triple)
 //
 // MI355X mapping — one wavefront (64 lanes) per QP, no workgroup barriers, 2 waves per SIMD (fp64):
 //   * Newton matrix K = H + C' Sigma C in a 4 x 16-cyclic register tile: lane l = 16a + b holds
 //     K[a + 4r][b + 16c] (r = 0..15, c = 0..3) in register e = 4r + c — 64 values per lane;
-//   * LDL' elimination that also builds L^-1 in place. Step s, every row i > s and every column j != s:
-//     K[i][j] -= K[i][s] K[s][j] / d_s. For j > s this is the right-looking LDL' update; for j < s the same
-//     update accumulates the strict lower part S of the explicit inverse, X = L^-1 with X[i][j] = -S[i][j] / d_j
-//     (column s is left as it is, so the row operations on the identity need no extra storage). The 16 row
+//   * LDL' right-looking factorisation. Step s: K[i][j] -= K[i][s] K[s][j] / d_s for i, j > s. The 16 row
 //     multipliers K[i][s] of a lane live in its own 16-lane DPP row (column s sits in lane b = s % 16), so they
-//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp: dpp_rowf); only the
-//     4 column multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent
-//     through LDS and its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
-//   * solves are K^-1 y = X' D^-1 X y: two matrix-vector products over the 40 registers of the strict lower part
-//     (forward: row sums reduced through LDS; backward: column sums reduced through LDS), no serial sweeps and no
-//     transpose of the factor (lab v6: 0.506 -> 0.449 ms per 4096 QPs, same iteration counts, 5e-16 vs v0);
+//     arrive through row_newbcast inside v_fmac_f64_dpp at no instruction cost (dpp_rows.hpp); only the 4 column
+//     multipliers K[s][j] / d_s come from LDS. One-step look-ahead: row s+1 is updated first, sent through LDS and
+//     its pivot read and inverted before the bulk of step s, so both round trips overlap the FMAs;
+//   * the factor is transposed once through LDS into row layout (lane i = row i), each row scaled by 1/d_i, so
+//     every step of the four triangular sweeps is one v_readlane pair + one FMA; finished unknowns are saved to
+//     LDS instead of masking the lanes that are already done;
 //   * vectors are lane-per-variable; the <= 105 pyramid rows are two slots per lane (j = lane + 64 cc) with the
 //     primal-dual state in registers and per-iteration scratch in lane-private LDS;
 //   * H is stored by the condensing kernel in the tile order (h_index, cmpc_kernels.hpp): 64 coalesced 512-B
@@ -32,11 +29,11 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
-#include "dpp_rows.hpp"
+#include <dpp_rows.hpp>
 #include "wave_dpp.hpp"
 
 // In-kernel s_memtime stamps, diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP cycles of each
-// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 lower-part mask, 4 solves,
+// phase into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 LDL', 3 transpose, 4 sweeps,
 // 5 predictor rest, 6 corrector rest, 7 update, 8 total.
 #ifdef CMPC_IPM_STAMPS
 #define IPM_STAMP_DECL                                                    \
@@ -123,6 +120,8 @@ __device__ __forceinline__ T pivot_inv(T p) {
   return p > T(Lim<T>::pivot_min) ? y : T(0);
 }
 
+// row-layout column j after the transpose lives in the register the tile used for column j's chunk
+__host__ __device__ constexpr int ridx(int j) { return (j & 15) * 4 + (j >> 4); }
 
 template <typename T>
 struct Lds {
@@ -130,10 +129,10 @@ struct Lds {
   T w[128];         // pyramid-row broadcast
   T rowbuf[2][64];  // factorisation: row s of K as [c*16 + b]
   T dg[64];         // pivots d_s
-  T z[64];          // solve: z permuted as [i % 4][i / 4]
+  T z[64];          // sweep results
   T blk[3][64];     // Newton 3x3 block rows
   T rl[128], ru[128], itl[128], itu[128], rml[128], rmu[128];  // lane-private pyramid-row scratch
-  T scr[1024];      // Hu and solve partial sums
+  T scr[1024];      // Hu partial sums / factor transpose (16 columns at a time)
 };
 
 }  // namespace ipm64
@@ -458,77 +457,134 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
 
     // ---- LDL' factorisation in the tile (see header)
     const bool full = uflag(n > 60);
-    T piv = readlane(K[0], 0);
-    T invd = pivot_inv(piv);
-    T mm[4];
+    // Two pivots per block (p = 2b, q = p + 1; both rows in one row group), one LDS round trip per block: the
+    // look-ahead applies both pivots to the next block's two rows, which travel through LDS together, while
+    // both next pivots come from registers by scalar arithmetic (d_q after step p = K[q][q] + K[q][p] *
+    // (-K[p][q] / d_p)), off the LDS path. Bit-identical to one pivot per step.
+    auto kat = [&](auto i_, auto j_) -> T {  // K[i][j] from the tile (uniform)
+      constexpr int i = decltype(i_)::value, j = decltype(j_)::value;
+      return readlane(K[(i / 4) * 4 + j / 16], (i % 4) * 16 + j % 16);
+    };
+    T mp[4], mq[4];
+    T l_pq = T(0);
+    auto pivots = [&](auto p_, T& dp, T& dq, T& invp, T& invq) {
+      constexpr int p = decltype(p_)::value, q = p + 1;
+      dp = kat(std::integral_constant<int, p>{}, std::integral_constant<int, p>{});
+      l_pq = kat(std::integral_constant<int, q>{}, std::integral_constant<int, p>{});
+      const T kpq = kat(std::integral_constant<int, p>{}, std::integral_constant<int, q>{});
+      const T kqq = kat(std::integral_constant<int, q>{}, std::integral_constant<int, q>{});
+      invp = pivot_inv(dp);
+      dq = fma(l_pq, -(kpq * invp), kqq);
+      invq = pivot_inv(dq);
+    };
+    // multipliers of pivots p, q from the broadcast rows (row q gets step p first, as the look-ahead would)
+    auto multipliers = [&](auto p_, const T (&xp)[4], const T (&xq)[4], T invp, T invq) {
+      constexpr int p = decltype(p_)::value, q = p + 1;
+      constexpr int cp = p / 16, bp = p % 16, cq = q / 16, bq = q % 16;
+      const int lb_m = lane0 & 15;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const T mv = -(xp[c] * invp);
+        mp[c] = (c == cp && lb_m == bp) ? T(0) : mv;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const T x2 = fma(l_pq, mp[c], xq[c]);
+        const T mv = -(x2 * invq);
+        mq[c] = (c == cq && lb_m == bq) ? T(0) : mv;
+        asm volatile("" : "+v"(mq[c]));
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) asm volatile("" : "+v"(mp[c]));
+    };
+    // both pivots on row group R: pass p (source column p) then pass q (source column q, just updated)
+    auto two_pass = [&](auto R_, auto p_, auto nop_) {
+      constexpr int R = decltype(R_)::value, p = decltype(p_)::value, q = p + 1;
+      constexpr bool nop = decltype(nop_)::value;
+      dpp_rowf<p % 16, p / 16, nop, T>(K[R * 4], K[R * 4 + 1], K[R * 4 + 2], K[R * 4 + 3], mp[0], mp[1], mp[2], mp[3]);
+      dpp_rowf<q % 16, q / 16, true, T>(K[R * 4], K[R * 4 + 1], K[R * 4 + 2], K[R * 4 + 3], mq[0], mq[1], mq[2], mq[3]);
+    };
     {
+      T xp[4], xq[4];
       if (la == 0) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) L.rowbuf[0][c * 16 + lb] = K[c];
       }
-      L.dg[0] = piv;
+      if (la == 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) L.rowbuf[1][c * 16 + lb] = K[c];
+      }
       cbar();
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const T mv = -(L.rowbuf[0][c * 16 + lb] * invd);
-        mm[c] = (c == 0 && lb == 0) ? T(0) : mv;
+        xp[c] = L.rowbuf[0][c * 16 + lb];
+        xq[c] = L.rowbuf[1][c * 16 + lb];
       }
       cbar();
+      T dp, dq, invp, invq;
+      pivots(std::integral_constant<int, 0>{}, dp, dq, invp, invq);
+      L.dg[0] = dp;
+      L.dg[1] = dq;
+      multipliers(std::integral_constant<int, 0>{}, xp, xq, invp, invq);
     }
-    sfor<0, 63>([&](auto s_) {
-      constexpr int s = decltype(s_)::value;
-      constexpr int c0 = s / 16, b0 = s % 16, a0 = s % 4;
-      constexpr int s1 = s + 1;
-      constexpr int r1 = s1 / 4, a1 = s1 % 4, c1 = s1 / 16, b1 = s1 % 16;
-      if constexpr (s1 >= 60) {
+    sfor<0, 31>([&](auto b_) {
+      constexpr int b = decltype(b_)::value;
+      constexpr int p = 2 * b;
+      constexpr int p2 = p + 2, q2 = p + 3;
+      constexpr int R2 = p2 / 4;
+      if constexpr (p2 >= 60) {
         // pivots 60..63 exist only for n > 60; padding rows keep S = 0 and get d = 1
         if (!full) {
-          L.dg[s1] = T(1);
+          L.dg[p2] = T(1);
+          L.dg[q2] = T(1);
           return;
         }
       }
       __builtin_amdgcn_sched_barrier(0);
 #ifdef LDL_SPLIT
-      if constexpr (s == LDL_SPLIT) IPM_STAMP(2);
+      if constexpr (p == LDL_SPLIT) IPM_STAMP(2);
 #endif
-      const int la_m = lane0 >> 4, lb_m = lane0 & 15;  // masks and rowbuf addresses: hoisted, loop invariant
-      // look-ahead local row r1 (holds row s+1); for a0 < 3 it is the partial row: rows a + 4 r1 > s iff a > a0
-      if constexpr (a0 < 3) {
-        if (la_m > a0)
-          dpp_rowf<b0, c0, true, T>(K[r1 * 4], K[r1 * 4 + 1], K[r1 * 4 + 2], K[r1 * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+      const int la_m = lane0 >> 4, lb_m = lane0 & 15;
+      // look-ahead: rows p+2, p+3 (row group R2; when p % 4 == 0 they are its lanes a = 2, 3)
+      if constexpr (p % 4 == 0) {
+        if (la_m >= 2) two_pass(std::integral_constant<int, R2>{}, std::integral_constant<int, p>{}, std::true_type{});
       } else {
-        dpp_rowf<b0, c0, true, T>(K[r1 * 4], K[r1 * 4 + 1], K[r1 * 4 + 2], K[r1 * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+        two_pass(std::integral_constant<int, R2>{}, std::integral_constant<int, p>{}, std::true_type{});
       }
       cbar();
-      if (la_m == a1) {
+      if (la_m == p2 % 4) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) L.rowbuf[s1 & 1][c * 16 + lb_m] = K[r1 * 4 + c];
+        for (int c = 0; c < 4; ++c) L.rowbuf[0][c * 16 + lb_m] = K[R2 * 4 + c];
+      }
+      if (la_m == q2 % 4) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) L.rowbuf[1][c * 16 + lb_m] = K[R2 * 4 + c];
       }
       cbar();
-      T xn[4];
+      T xp[4], xq[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) xn[c] = L.rowbuf[s1 & 1][c * 16 + lb_m];
+      for (int c = 0; c < 4; ++c) {
+        xp[c] = L.rowbuf[0][c * 16 + lb_m];
+        xq[c] = L.rowbuf[1][c * 16 + lb_m];
+      }
       cbar();
-      const T pivn = readlane(K[r1 * 4 + c1], a1 * 16 + b1);
-      T invdn = pivot_inv(pivn);
-      asm volatile("" : "+v"(invdn));  // materialise the reciprocal here, ahead of the bulk rows
-      sfor<r1 + 1, 16>([&](auto r_) {
+      T dp, dq, invp, invq;
+      pivots(std::integral_constant<int, p2>{}, dp, dq, invp, invq);
+      asm volatile("" : "+v"(invp), "+v"(invq));
+      // bulk: row groups after R2, both pivots
+      sfor<R2 + 1, 16>([&](auto r_) {
         constexpr int r = decltype(r_)::value;
-        if constexpr (((r - r1 - 1) & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (((r - R2 - 1) & 1) == 0) __builtin_amdgcn_sched_barrier(0);
         if constexpr (r == 15) {
-          if (full)  // rows 60..63 are padding when n <= 60 (every trot / bound QP at N = 10): S stays 0 there
-            dpp_rowf<b0, c0, true, T>(K[r * 4], K[r * 4 + 1], K[r * 4 + 2], K[r * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+          if (full) two_pass(std::integral_constant<int, r>{}, std::integral_constant<int, p>{}, std::true_type{});
         } else {
-          dpp_rowf<b0, c0, false, T>(K[r * 4], K[r * 4 + 1], K[r * 4 + 2], K[r * 4 + 3], mm[0], mm[1], mm[2], mm[3]);
+          two_pass(std::integral_constant<int, r>{}, std::integral_constant<int, p>{}, std::false_type{});
         }
       });
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const T mv = -(xn[c] * invdn);
-        mm[c] = (c == c1 && lb_m == b1) ? T(0) : mv;
-      }
-      L.dg[s1] = pivn;
+      multipliers(std::integral_constant<int, p2>{}, xp, xq, invp, invq);
+      L.dg[p2] = dp;
+      L.dg[q2] = dq;
     });
     __builtin_amdgcn_sched_barrier(0);
     cbar();
