@@ -324,6 +324,11 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   int it = 0;
   for (it = 0;; ++it) {
     load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
+#ifdef H_WAIT_STAMP  // diagnostic: time to the last H row (segment 3)
+    IPM_STAMP(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    IPM_STAMP(3);
+#endif
     lane = olane();
     const int la = lane >> 4, lb = lane & 15;
 
@@ -378,17 +383,15 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     }
     rg_v = vin ? hu + g_v - ctw : T(0);
     rs = fabs(rg_v);
-    rs = wave_max_dpp(rs);
-    ri = wave_max_dpp(ri);
-    rc = wave_max_dpp(rc);
     ms = wave_sum_dpp(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
-    if (uflag(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
+    // a non-finite residual anywhere -> NAN_SOL; HPIPM's absolute stopping rule (tol_stat / tol_ineq / tol_comp)
+    // as a wave vote: max over lanes <= tol iff every lane <= tol (no max-reductions needed)
+    if (__any(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
       status = CMPC_NAN_SOL;
       break;
     }
-    // HPIPM's absolute stopping rule (tol_stat / tol_ineq / tol_comp)
-    if (uflag(rs <= T(S.tol_stat) && ri <= T(S.tol_ineq) && rc <= T(S.tol_comp))) {
+    if (__all(rs <= T(S.tol_stat) && ri <= T(S.tol_ineq) && rc <= T(S.tol_comp))) {
       status = CMPC_SUCCESS;
       break;
     }
