@@ -1,0 +1,657 @@
+#pragma once
+// k_ipm128x.hpp — stage 2 of the hot path for the size class 64 < n <= 128 (pronk / all-stance at N <= 10, trot at
+// N = 11..21): the same batched dense friction-pyramid QP and primal-dual Mehrotra predictor-corrector as k_ipm64
+// (restated in oracle/cmpc_oracle.c:oracle_qp_ipm; settings and stopping rule of hpipm_interface::Settings,
+// HpipmInterfaceSettings.h:44-57; replaces d_ocp_qp_ipm_solve at HpipmInterface.cpp:284), with k_ipm64's linear
+// algebra spread over one workgroup of four waves.
+//
+// MI355X mapping — one workgroup of 4 waves per QP (two workgroups per CU, 2 waves per SIMD):
+//   * the Newton matrix K (128 x 128, both triangles) lives in registers: wave w owns the row groups
+//     R = 4 rho + w (rho = 0..7, cyclic, so every wave keeps rows below any pivot), lane l = 16a + b holding
+//     K[16 rho + 4w + a][16c + b] in register 8 rho + c — 64 values per lane, as k_ipm64's tile per wave;
+//   * elimination that builds L^-1 in place (k_ipm64): pivot s, every row i > s and column j != s:
+//     K[i][j] -= K[i][s] K[s][j] / d_s. The row multipliers K[i][s] arrive by row_newbcast inside v_fmac_*_dpp
+//     (column s sits in lane b = s % 16 of the lane's own 16-lane row); row s+1 is updated first by its owner wave
+//     (look-ahead), published in LDS and read by all four waves after one workgroup barrier per pivot;
+//   * the pivots run in 16-column chunks c0, a run-time loop (the unrolled code is one chunk long); after every
+//     chunk the register tile is rotated by one row group and one column chunk, so the chunk's pivot row group is
+//     always register row 0 and its DPP-source column chunk always register column 0 — compile-time register
+//     indices under a run-time loop; eight rotations restore the order;
+//   * the Newton matrix adds C' Sigma C + reg I from 3x3 block columns staged in LDS by the variable threads;
+//   * solves K^-1 y = X' D^-1 X y (X = L^-1, X[i][j] = -S[i][j] / d_j from the strict lower part S): forward row
+//     sums and backward column sums over the lower registers (c <= rho), partials reduced through LDS;
+//   * one thread per variable (tid < 128) and per pyramid row (tid < 5 n / 3 <= 210); block reductions are DPP
+//     wave reductions + 4 partials through LDS.
+#include <type_traits>
+
+#include "cmpc_device.hpp"
+#include "cmpc_kernels.hpp"
+#include "wave_dpp.hpp"
+
+// In-kernel s_memtime stamps (wave 0's view), diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP
+// cycles into IpmArgs::stamps[q][9]. Segments: 0 H + residuals, 1 Newton matrix, 2 elimination, 3 pivots/mask,
+// 4 solves, 5 predictor rest, 6 corrector rest, 7 update, 8 total.
+#ifdef CMPC_IPM_STAMPS
+#define X_STAMP_DECL                                               \
+  unsigned long long xs_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};       \
+  const unsigned long long xs_t0_ = ipm128x::memtime();            \
+  unsigned long long xs_prev_ = xs_t0_
+#define X_STAMP(k)                                       \
+  do {                                                   \
+    const unsigned long long t_ = ipm128x::memtime();    \
+    xs_acc_[k] += t_ - xs_prev_;                         \
+    xs_prev_ = t_;                                       \
+  } while (0)
+#define X_STAMP_STORE(ptr, q)                                                   \
+  do {                                                                          \
+    const unsigned long long t_ = ipm128x::memtime();                           \
+    if ((ptr) && threadIdx.x == 0) {                                            \
+      for (int k_ = 0; k_ < 8; ++k_) (ptr)[(size_t)(q) * 9 + k_] = xs_acc_[k_]; \
+      (ptr)[(size_t)(q) * 9 + 8] = t_ - xs_t0_;                                 \
+    }                                                                           \
+  } while (0)
+#else
+#define X_STAMP_DECL (void)0
+#define X_STAMP(k) (void)0
+#define X_STAMP_STORE(ptr, q) (void)0
+#endif
+
+namespace cmpc {
+namespace ipm128x {
+
+__device__ __forceinline__ unsigned long long memtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <typename T>
+struct Lim;
+template <>
+struct Lim<double> {
+  static constexpr double pivot_min = 1e-200;
+  static constexpr double mu_min = 1e-300;
+};
+template <>
+struct Lim<float> {
+  static constexpr float pivot_min = 1e-30f;
+  static constexpr float mu_min = 1e-35f;
+};
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ double rcp_raw(double x) { return __builtin_amdgcn_rcp(x); }
+__device__ __forceinline__ float rcp_raw(float x) { return __builtin_amdgcn_rcpf(x); }
+template <typename T>
+__device__ __forceinline__ T pivot_inv(T p) {
+  T y = rcp_raw(p);
+  const T e = fma(-p, y, T(1));
+  y = fma(y, e, y);
+  return p > T(Lim<T>::pivot_min) ? y : T(0);
+}
+
+// k += row_newbcast<B0>(src) * m
+template <int B0, typename T>
+__device__ __forceinline__ void dfma(T& k, const T& src, T m) {
+  if constexpr (sizeof(T) == 8)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+  else
+    asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+}
+template <int B0, typename T>
+__device__ __forceinline__ void dfma_nn(T& k, const T& src, T m) {  // no leading s_nop (caller ordered)
+  if constexpr (sizeof(T) == 8)
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+  else
+    asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(k) : "v"(src), "v"(m), "n"(B0));
+}
+template <int B0, typename T>
+__device__ __forceinline__ void dfma_self(T& k, T m) {  // the DPP source itself (its lane B0 carries m = 0)
+  if constexpr (sizeof(T) == 8)
+    asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(k) : "v"(m), "n"(B0));
+  else
+    asm volatile("v_fmac_f32_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(k) : "v"(m), "n"(B0));
+}
+
+__device__ __forceinline__ int olane() {
+  int l = (int)threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+__device__ __forceinline__ int owave() {
+  int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  asm volatile("" : "+s"(w));
+  return w;
+}
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
+
+template <typename T>
+struct Lds {
+  T scr[128 * 16];  // row / column partial sums (16 per variable)
+  T rowbuf[2][2][128];  // pivot-pair rows broadcast (parity double buffer)
+  T v[128];         // variable broadcast
+  T z[128];         // backward-solve input, permuted [i % 16][i / 16]
+  T dg[128];        // pivots
+  T w[256];         // pyramid-row broadcast (C' input, Newton block weights)
+  T mut[43];        // friction coefficient per triple
+  T red[4][4];
+  T blk[3][128];     // Newton 3x3 block columns
+  // parked per-row state (one pyramid row per thread)
+  T p_lo[256], p_hi[256], p_rl[256], p_ru[256], p_itl[256], p_itu[256], p_rml[256], p_rmu[256];
+  T p_tl[256], p_tu[256], p_ll[256], p_lu[256], p_u[128], p_rg[128];  // iterate parked across the elimination
+};
+
+}  // namespace ipm128x
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void k_ipm128x(IpmArgs<T> a) {
+  using namespace ipm128x;
+  X_STAMP_DECL;
+  constexpr int NP = 128;
+  const int q = blockIdx.x;
+  if (a.status[q] != CMPC_SUCCESS) return;
+  const int n = a.nvar[q];
+  if (n <= 64 || n > NP) return;  // served by another size class
+  const int ld = a.ld;
+  const int nt = n / 3;
+  const int m = 5 * nt;
+  const DevSettings S = a.s;
+  __shared__ Lds<T> L;
+
+  const int tid = threadIdx.x;
+  const int lane0 = tid & 63, wave0 = tid >> 6;
+  const int la0 = lane0 >> 4, lb0 = lane0 & 15;
+
+  // ---- variable role (tid < 128) and pyramid-row role (tid < m)
+  const bool isv = tid < NP;
+  const bool var = tid < n;
+  const T g_i = var ? a.g[(size_t)q * ld + tid] : T(0);
+  const T mu_i = var ? a.tri_mu[(size_t)q * (ld / 3) + tid / 3] : T(0);
+  T u_i = (a.warm && var) ? a.u[(size_t)q * ld + tid] : T(0), rg_i = T(0), du_i = T(0);
+  const bool con = tid < m;
+  const int tj = tid / 5, rj = tid % 5;
+  {
+    L.p_lo[tid] = con ? a.tri_lo[((size_t)q * (ld / 3) + tj) * 5 + rj] : T(0);
+    L.p_hi[tid] = con ? a.tri_hi[((size_t)q * (ld / 3) + tj) * 5 + rj] : T(0);
+  }
+  if (tid < 43) L.mut[tid] = tid < nt ? a.tri_mu[(size_t)q * (ld / 3) + tid] : T(0);
+  if (isv) L.v[tid] = u_i;
+  __syncthreads();
+  auto C_row = [&]() -> T {
+    return con ? pyr_row<T>(rj, L.mut[tj], L.v[3 * tj], L.v[3 * tj + 1], L.v[3 * tj + 2]) : T(0);
+  };
+  T tl, tu, ll, lu;
+  {
+    const T cu0 = C_row();
+    tl = con ? fmax(cu0 - L.p_lo[tid], T(THR0)) : T(1);
+    tu = con ? fmax(L.p_hi[tid] - cu0, T(THR0)) : T(1);
+    ll = con ? T(S.mu0) / tl : T(0);
+    lu = con ? T(S.mu0) / tu : T(0);
+  }
+  T dtl = T(0), dtu = T(0), dll = T(0), dlu = T(0);
+  __syncthreads();
+
+  auto block_sum = [&](T r) -> T {
+    r = wave_sum_dpp(r);
+    if (lane0 == 0) L.red[wave0][0] = r;
+    __syncthreads();
+    const T o = (L.red[0][0] + L.red[1][0]) + (L.red[2][0] + L.red[3][0]);
+    __syncthreads();
+    return o;
+  };
+  auto block_min = [&](T r) -> T {
+    r = wave_min_dpp(r);
+    if (lane0 == 0) L.red[wave0][0] = r;
+    __syncthreads();
+    const T o = fmin(fmin(L.red[0][0], L.red[1][0]), fmin(L.red[2][0], L.red[3][0]));
+    __syncthreads();
+    return o;
+  };
+  // (C' w)_i with w in L.w (caller synchronised)
+  auto CT_var = [&]() -> T {
+    if (!var) return T(0);
+    const int t = tid / 3, dd = tid % 3;
+    const T w0 = L.w[5 * t], w1 = L.w[5 * t + 1], w2 = L.w[5 * t + 2], w3 = L.w[5 * t + 3], w4 = L.w[5 * t + 4];
+    return dd == 0 ? (w1 - w0) : (dd == 1 ? (w3 - w2) : (mu_i * (w0 + w1 + w2 + w3) + w4));
+  };
+
+  T K[64];
+  T invd_i = T(1);
+
+  // row partial sums of the lane's rows into L.scr (16 per row, rotated 16-B slots: conflict-free both ways);
+  // FULL = all 8 chunks (H u), else the lower registers c <= rho (forward solve). Input chunk values in xc.
+  auto row_partials = [&](const T (&xc)[8], auto full_) {
+    constexpr bool full = decltype(full_)::value;
+    const int ol = olane(), w = owave();
+    const int a = ol >> 4, b = ol & 15;
+    // row i = 16 rho + 4w + a: slot i * 16 + ((b/2 + i) & 7) * 2 + (b & 1); i & 7 = (4w + a) & 7 for every rho
+    const int i0 = 4 * w + a;
+    const int base = i0 * 16 + ((((b >> 1) + i0) & 7) << 1) + (b & 1);
+    sfor<0, 8>([&](auto r_) {
+      constexpr int rho = decltype(r_)::value;
+      constexpr int ce = full ? 8 : rho + 1;
+      T p = K[rho * 8] * xc[0];
+      sfor<1, ce>([&](auto c_) {
+        constexpr int c = decltype(c_)::value;
+        p = fma(K[rho * 8 + c], xc[c], p);
+      });
+      L.scr[base + 256 * rho] = p;
+    });
+  };
+  auto row_sum = [&]() -> T {  // variable tid's 16 partials (caller synchronised)
+    T sv = T(0);
+    if (isv) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = tid * 16 + (((k + tid) & 7) << 1);
+        sv += L.scr[idx] + L.scr[idx + 1];
+      }
+    }
+    return sv;
+  };
+
+  // K x = y for the thread's variable (y = 0 outside): see the header
+  auto solve = [&](T& y) {
+    if (isv) L.v[tid] = y * invd_i;
+    __syncthreads();
+    {
+      const int ol = olane();
+      const int b = ol & 15;
+      T tc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) tc[c] = L.v[b + 16 * c];
+      row_partials(tc, std::false_type{});
+    }
+    __syncthreads();
+    const T z = (y - row_sum()) * invd_i;
+    if (isv) L.z[(tid & 15) * 8 + (tid >> 4)] = z;
+    __syncthreads();
+    {
+      const int ol = olane(), w = owave();
+      const int a = ol >> 4, b = ol & 15;
+      T zr[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) zr[r] = L.z[(4 * w + a) * 8 + r];
+      sfor<0, 8>([&](auto c_) {
+        constexpr int c = decltype(c_)::value;
+        T qv = K[c * 8 + c] * zr[c];
+        sfor<c + 1, 8>([&](auto r_) {
+          constexpr int rho = decltype(r_)::value;
+          qv = fma(K[rho * 8 + c], zr[rho], qv);
+        });
+        L.scr[(c * 16 + b) * 16 + 4 * w + a] = qv;
+      });
+    }
+    __syncthreads();
+    T qs = T(0);
+    if (isv) {
+#pragma unroll
+      for (int k = 0; k < 16; k += 2) qs += L.scr[tid * 16 + k] + L.scr[tid * 16 + k + 1];
+    }
+    y = var ? fma(-invd_i, qs, z) : T(0);
+    __syncthreads();  // L.scr / L.v are rewritten next
+  };
+
+  const T* Hq = a.H + (size_t)q * ld * ld;  // class-packed 128 x 128 block (row-major) at the start of the slab
+  int status = CMPC_MAX_ITER;
+  int it = 0;
+
+  auto direction = [&]() {
+    const T rl = L.p_rl[tid], ru = L.p_ru[tid], itl = L.p_itl[tid], itu = L.p_itu[tid];
+    const T rml = L.p_rml[tid], rmu = L.p_rmu[tid];
+    L.w[tid] = (rml + ll * rl) * itl - (rmu + lu * ru) * itu;
+    __syncthreads();
+    const T ctw = CT_var();
+    T y = var ? -rg_i - ctw : T(0);
+    X_STAMP(5);
+    solve(y);
+    X_STAMP(4);
+    du_i = y;
+    if (isv) L.v[tid] = du_i;
+    __syncthreads();
+    const T cdu = C_row();
+    dtl = con ? cdu + rl : T(0);
+    dtu = con ? ru - cdu : T(0);
+    dll = -(rml + ll * dtl) * itl;
+    dlu = -(rmu + lu * dtu) * itu;
+    __syncthreads();  // L.v is rewritten next
+  };
+  auto max_step = [&]() -> T {
+    T am = T(1e30);
+    if (dtl < T(0)) am = fmin(am, -tl / dtl);
+    if (dtu < T(0)) am = fmin(am, -tu / dtu);
+    if (dll < T(0)) am = fmin(am, -ll / dll);
+    if (dlu < T(0)) am = fmin(am, -lu / dlu);
+    return block_min(am);
+  };
+
+  for (it = 0;; ++it) {
+    // ---- H: 64 loads per lane, 4 rows x 16 consecutive columns per instruction
+    {
+      const int ol = olane(), w = owave();
+      const T* hp = Hq + (size_t)(4 * w + (ol >> 4)) * NP + (ol & 15);
+#pragma unroll
+      for (int rho = 0; rho < 8; ++rho)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) K[rho * 8 + c] = hp[16 * rho * NP + 16 * c];
+    }
+    // ---- residuals: C u, H u
+    if (isv) L.v[tid] = u_i;
+    __syncthreads();
+    const T cu = C_row();
+    {
+      const int ol = olane();
+      const int b = ol & 15;
+      T uc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) uc[c] = L.v[b + 16 * c];
+      row_partials(uc, std::true_type{});
+    }
+    __syncthreads();
+    const T hu = row_sum();
+    const T lo = L.p_lo[tid], hi = L.p_hi[tid];
+    const T rl = con ? cu - lo - tl : T(0);
+    const T ru = con ? hi - cu - tu : T(0);
+    L.p_rl[tid] = rl;
+    L.p_ru[tid] = ru;
+    const T ri = fmax(fabs(rl), fabs(ru));
+    T rc, ms;
+    {
+      const T cl = tl * ll, ch = tu * lu;
+      rc = con ? fmax(cl, ch) : T(0);
+      ms = con ? cl + ch : T(0);
+    }
+    L.w[tid] = ll - lu;
+    __syncthreads();
+    {
+      const T ctw = CT_var();
+      rg_i = isv ? hu + g_i - ctw : T(0);
+    }
+    const T rs = fabs(rg_i);
+    ms = block_sum(ms);
+    const T mu = m > 0 ? ms / T(2 * m) : T(0);
+    // non-finite residual anywhere -> NAN_SOL; stopping rule as a block vote (max <= tol iff all <= tol)
+    if (__syncthreads_or(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
+      status = CMPC_NAN_SOL;
+      break;
+    }
+    if (__syncthreads_and(rs <= T(S.tol_stat) && ri <= T(S.tol_ineq) && rc <= T(S.tol_comp))) {
+      status = CMPC_SUCCESS;
+      break;
+    }
+    if (it >= S.iter_max) {
+      status = CMPC_MAX_ITER;
+      break;
+    }
+    if (m > 0 && !(mu > T(Lim<T>::mu_min))) {
+      status = CMPC_MIN_STEP;
+      break;
+    }
+    X_STAMP(0);
+
+    // ---- Newton matrix K = H + C' diag(lam_l/t_l + lam_u/t_u) C + reg I: thread j < 128 writes the 3x3 block
+    //      column of variable j (rows t3 .. t3 + 2 of its triple), the tile adds it where entry (i, j) falls there
+    {
+      const T itl = con ? T(1) / tl : T(0);
+      const T itu = con ? T(1) / tu : T(0);
+      L.p_itl[tid] = itl;
+      L.p_itu[tid] = itu;
+      L.w[tid] = ll * itl + lu * itu;
+    }
+    __syncthreads();
+    if (isv) {
+      const int t = tid / 3, dd = tid % 3;
+      T b0 = T(0), b1 = T(0), b2 = T(0);
+      if (var) {
+        const T s0 = L.w[5 * t], s1 = L.w[5 * t + 1], s2 = L.w[5 * t + 2], s3 = L.w[5 * t + 3], s4 = L.w[5 * t + 4];
+        const T xx = s0 + s1, yy = s2 + s3, zz = mu_i * mu_i * (s0 + s1 + s2 + s3) + s4;
+        const T xz = mu_i * (s1 - s0), yz = mu_i * (s3 - s2);
+        b0 = dd == 0 ? xx : (dd == 1 ? T(0) : xz);
+        b1 = dd == 0 ? T(0) : (dd == 1 ? yy : yz);
+        b2 = dd == 0 ? xz : (dd == 1 ? yz : zz);
+      }
+      const T reg = T(S.reg_prim);
+      L.blk[0][tid] = b0 + (dd == 0 ? reg : T(0));
+      L.blk[1][tid] = b1 + (dd == 1 ? reg : T(0));
+      L.blk[2][tid] = b2 + (dd == 2 ? reg : T(0));
+    }
+    __syncthreads();
+    {
+      const int ol = olane(), w = owave();
+      const int a = ol >> 4, b = ol & 15;
+      // entry (i, j) = (16 rho + 4w + a, 16c + b) is in j's triple iff 0 <= i - 3 (j / 3) <= 2: only registers
+      // c = rho - 1 .. rho + 1 can hold such entries
+      sfor<0, 8>([&](auto r_) {
+        constexpr int rho = decltype(r_)::value;
+        sfor<(rho > 0 ? rho - 1 : 0), (rho < 7 ? rho + 2 : 8)>([&](auto c_) {
+          constexpr int c = decltype(c_)::value;
+          const int j = 16 * c + b;
+          const int e = 16 * rho + 4 * w + a - 3 * (j / 3);
+          const bool in = e >= 0 && e <= 2;
+          const T val = L.blk[in ? e : 0][j];
+          K[rho * 8 + c] += in ? val : T(0);
+        });
+      });
+    }
+    X_STAMP(1);
+    // park the per-thread iterate in LDS across the elimination (its registers hold the pivot pairs instead)
+    L.p_tl[tid] = tl;
+    L.p_tu[tid] = tu;
+    L.p_ll[tid] = ll;
+    L.p_lu[tid] = lu;
+    if (isv) {
+      L.p_u[tid] = u_i;
+      L.p_rg[tid] = rg_i;
+    }
+    // ---- elimination with L^-1 in place (see the header), 16-pivot chunks. The register tile is rotated by one
+    //      row group and one column chunk after every chunk (K[rho][c] <- K[rho + 1][c + 1], indices mod 8), so
+    //      the pivot row group is always register row 0 and the pivot column chunk always register column 0:
+    //      compile-time register indices under a run-time chunk loop. Eight rotations restore the order.
+    const int nch = (n + 15) >> 4;
+    // Pivots in pairs (p = 16 c0 + 2 b, q = p + 1; both rows in the same wave, register row 0): one barrier and one
+    // LDS round trip per pair. Row q gets pivot p from the broadcast copy (xq' = xq + K[q][p] mp, the look-ahead's
+    // own FMA), its pivot from uniform LDS reads (d_q = K[q][q] + K[q][p] (-K[p][q] / d_p)): bit-identical to one
+    // pivot at a time.
+    T mp[8], mq[8];
+    // multipliers of the pair from the two broadcast rows
+    auto pair_mult = [&](const T (&xp)[8], const T (&xq)[8], T dp, T kqp, T kpq, T kqq, int s, auto tp_) {
+      constexpr int tp = decltype(tp_)::value, tq = tp + 1;
+      const T invp = pivot_inv(dp);
+      const T dq = fma(kqp, -(kpq * invp), kqq);
+      const T invq = pivot_inv(dq);
+      if (tid == 0) {
+        L.dg[s] = dp;
+        L.dg[s + 1] = dq;
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const T mv = -(xp[c] * invp);
+        mp[c] = (c == 0 && lb0 == tp) ? T(0) : mv;
+        asm volatile("" : "+v"(mp[c]));
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const T x2 = fma(kqp, mp[c], xq[c]);
+        const T mv = -(x2 * invq);
+        mq[c] = (c == 0 && lb0 == tq) ? T(0) : mv;
+        asm volatile("" : "+v"(mq[c]));
+      }
+    };
+    // register row rho by the pair (source columns tp, tq of register chunk 0): pass p then pass q
+    auto row_update2 = [&](auto rho_, auto tp_) {
+      constexpr int rho = decltype(rho_)::value, tp = decltype(tp_)::value, tq = tp + 1;
+      dfma<tp, T>(K[rho * 8 + 1], K[rho * 8], mp[1]);
+      sfor<2, 8>([&](auto c_) {
+        constexpr int c = decltype(c_)::value;
+        dfma_nn<tp, T>(K[rho * 8 + c], K[rho * 8], mp[c]);
+      });
+      dfma_self<tp, T>(K[rho * 8], mp[0]);
+      dfma<tq, T>(K[rho * 8 + 1], K[rho * 8], mq[1]);
+      sfor<2, 8>([&](auto c_) {
+        constexpr int c = decltype(c_)::value;
+        dfma_nn<tq, T>(K[rho * 8 + c], K[rho * 8], mq[c]);
+      });
+      dfma_self<tq, T>(K[rho * 8], mq[0]);
+    };
+    auto read_pair = [&](int buf, T (&xp)[8], T (&xq)[8], T& dp, T& kqp, T& kpq, T& kqq, int tp) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        xp[c] = L.rowbuf[buf][0][16 * c + lb0];
+        xq[c] = L.rowbuf[buf][1][16 * c + lb0];
+      }
+      dp = L.rowbuf[buf][0][tp];
+      kpq = L.rowbuf[buf][0][tp + 1];
+      kqp = L.rowbuf[buf][1][tp];
+      kqq = L.rowbuf[buf][1][tp + 1];
+    };
+    for (int c0 = 0; c0 < 8; ++c0) {
+      if (c0 < nch) {
+        // rows 16 c0, 16 c0 + 1 = wave 0, rows a = 0, 1 of register row 0: final (every earlier pivot applied)
+        if (wave0 == 0 && la0 < 2) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) L.rowbuf[0][la0][16 * c + lb0] = K[c];
+        }
+        __syncthreads();
+        {
+          T xp[8], xq[8], dp, kqp, kpq, kqq;
+          read_pair(0, xp, xq, dp, kqp, kpq, kqq, 0);
+          pair_mult(xp, xq, dp, kqp, kpq, kqq, 16 * c0, std::integral_constant<int, 0>{});
+        }
+        sfor<0, 8>([&](auto b_) {
+          constexpr int b = decltype(b_)::value;
+          constexpr int tp = 2 * b;                            // pivots 16 c0 + tp, + tp + 1
+          constexpr int w2 = (tp + 2) / 4, a2 = (tp + 2) % 4;  // owner wave and first row of the next pair (b < 7)
+          constexpr int nb = (b + 1) & 1;
+          const int wv = owave();
+          if constexpr (b < 7) {
+            // register row 0 (rows 16 c0 + 4 wv + a) below the pair: 4 wv + a > tp + 1; the next pair's owner
+            // first, then its two rows to LDS
+            if (wv == w2) {
+              if constexpr (a2 == 2) {
+                if (la0 >= 2) row_update2(std::integral_constant<int, 0>{}, std::integral_constant<int, tp>{});
+              } else {
+                row_update2(std::integral_constant<int, 0>{}, std::integral_constant<int, tp>{});
+              }
+              if (la0 == a2 || la0 == a2 + 1) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) L.rowbuf[nb][la0 - a2][16 * c + lb0] = K[c];
+              }
+            }
+            if (wv > w2) row_update2(std::integral_constant<int, 0>{}, std::integral_constant<int, tp>{});
+          }
+          // next pair published: its first row and pivot scalars are read here, landing while the bulk runs (the
+          // second row after it: registers)
+          T xp[8], xq[8], dp = T(0), kqp = T(0), kpq = T(0), kqq = T(0);
+          if constexpr (b < 7) {
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 8; ++c) xp[c] = L.rowbuf[nb][0][16 * c + lb0];
+            dp = L.rowbuf[nb][0][tp + 2];
+            kpq = L.rowbuf[nb][0][tp + 3];
+            kqp = L.rowbuf[nb][1][tp + 2];
+            kqq = L.rowbuf[nb][1][tp + 3];
+          }
+          // bulk: register rows 1 .. 7 - c0 (row groups below the chunk), padding groups skipped
+          sfor<1, 8>([&](auto r_) {
+            constexpr int rho = decltype(r_)::value;
+            if (rho <= 7 - c0 && 16 * (c0 + rho) < n) row_update2(r_, std::integral_constant<int, tp>{});
+          });
+          if constexpr (b < 7) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) xq[c] = L.rowbuf[nb][1][16 * c + lb0];
+            pair_mult(xp, xq, dp, kqp, kpq, kqq, 16 * c0 + tp + 2, std::integral_constant<int, tp + 2>{});
+          }
+        });
+        __syncthreads();  // rowbuf[0] is rewritten by the next chunk's first pair
+      }
+      // rotate: K[rho][c] <- K[rho + 1][c + 1]
+      T K0[64];
+#pragma unroll
+      for (int e = 0; e < 64; ++e) K0[e] = K[e];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) K[r * 8 + c] = K0[((r + 1) & 7) * 8 + ((c + 1) & 7)];
+    }
+    X_STAMP(2);
+    tl = L.p_tl[tid];
+    tu = L.p_tu[tid];
+    ll = L.p_ll[tid];
+    lu = L.p_lu[tid];
+    if (isv) {
+      u_i = L.p_u[tid];
+      rg_i = L.p_rg[tid];
+    }
+    // pivots beyond the last chunk (n < 16 nch never leaves any: nch covers n) -> padding pivots are 1
+    if (isv && tid >= 16 * nch) L.dg[tid] = T(1);
+    __syncthreads();
+    {
+      const T d = isv ? L.dg[tid] : T(1);
+      invd_i = pivot_inv(d);
+      if (__syncthreads_or(isv && d != d)) {
+        status = CMPC_NAN_SOL;
+        break;
+      }
+    }
+    // strict lower part only in the diagonal-straddling registers (rho, c = rho): keep j < i  <=>  b < 4w + a
+    {
+      const int w = owave();
+      sfor<0, 8>([&](auto r_) {
+        constexpr int rho = decltype(r_)::value;
+        K[rho * 8 + rho] = (lb0 < 4 * w + la0) ? K[rho * 8 + rho] : T(0);
+      });
+    }
+
+    X_STAMP(3);
+    // ---- predictor (affine scaling direction)
+    L.p_rml[tid] = tl * ll;
+    L.p_rmu[tid] = tu * lu;
+    direction();
+    T alpha = fmin(T(1), max_step());
+    if (m > 0) {
+      T maff = con ? (tl + alpha * dtl) * (ll + alpha * dll) + (tu + alpha * dtu) * (lu + alpha * dlu) : T(0);
+      maff = block_sum(maff) / T(2 * m);
+      const T ratio = maff / mu;
+      const T sigma = ratio * ratio * ratio;
+      // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
+      L.p_rml[tid] = con ? tl * ll + dtl * dll - sigma * mu : T(0);
+      L.p_rmu[tid] = con ? tu * lu + dtu * dlu - sigma * mu : T(0);
+      direction();
+      alpha = fmin(T(1), T(TAU) * max_step());
+    }
+    X_STAMP(6);
+    if (alpha < T(S.alpha_min)) {
+      status = CMPC_MIN_STEP;
+      break;
+    }
+    u_i = fma(alpha, du_i, u_i);
+    tl = fma(alpha, dtl, tl);
+    tu = fma(alpha, dtu, tu);
+    ll = fma(alpha, dll, ll);
+    lu = fma(alpha, dlu, lu);
+    X_STAMP(7);
+  }
+
+  const bool fin = !var || isfinite(u_i);
+  if (__syncthreads_or(fin ? 0 : 1)) status = CMPC_NAN_SOL;
+  if (isv && tid < ld) a.u[(size_t)q * ld + tid] = var ? u_i : T(0);
+  if (tid == 0) {
+    a.status[q] = status;
+    a.iters[q] = it;
+  }
+  X_STAMP_STORE(a.stamps, q);
+}
+
+}  // namespace cmpc

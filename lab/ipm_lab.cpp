@@ -78,6 +78,8 @@ int main(int argc, char** argv) {
   double* foot = dmalloc<double>((size_t)B * (N + 1) * 12);
   uint8_t* contact = dmalloc<uint8_t>((size_t)B * N * 4);
   CC(cmpc_generate_batch(&m, 20221125ull, 0, B, 0, x0, xref, foot, contact, st));
+  // LAB_ALLSTANCE=1: every leg in stance (n = 120, the 64 < n <= 128 class)
+  if (getenv("LAB_ALLSTANCE") && atoi(getenv("LAB_ALLSTANCE"))) CK(hipMemsetAsync(contact, 1, (size_t)B * N * 4, st));
   double* H = dmalloc<double>((size_t)B * ld * ld);
   double* g = dmalloc<double>((size_t)B * ld);
   int* n = dmalloc<int>(B);

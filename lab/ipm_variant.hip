@@ -10,6 +10,7 @@
 #ifdef LAB_PRODUCT
 // the product kernel also lives in libcmpc.so (the lab's reference): give this copy its own name
 #define k_ipm64 LAB_CAT(k_ipm64_, LAB_FN)
+#define k_ipm128x LAB_CAT(k_ipm128x_, LAB_FN)
 #endif
 #include LAB_STR(LAB_HDR)
 
@@ -18,7 +19,11 @@
 #endif
 
 extern "C" int LAB_FN(const cmpc::IpmArgs<double>* a, int B, hipStream_t s, unsigned long long* stamps) {
-#ifdef LAB_PRODUCT  // the product kernel (csrc/k_ipm64.hpp); stamps through IpmArgs when built with CMPC_IPM_STAMPS
+#if defined(LAB_PRODUCT) && defined(LAB_K128)  // the 64 < n <= 128 class (csrc/k_ipm128x.hpp), 4 waves per QP
+  cmpc::IpmArgs<double> b = *a;
+  b.stamps = stamps;
+  hipLaunchKernelGGL((cmpc::LAB_CAT(k_ipm128x_, LAB_FN)<double>), dim3(B), dim3(256), 0, s, b);
+#elif defined(LAB_PRODUCT)  // the product kernel (csrc/k_ipm64.hpp); stamps through IpmArgs when built with CMPC_IPM_STAMPS
   cmpc::IpmArgs<double> b = *a;
   b.stamps = stamps;
   hipLaunchKernelGGL((cmpc::LAB_CAT(k_ipm64_, LAB_FN)<double, LAB_WPE>), dim3(B), dim3(64), 0, s, b);
