@@ -79,7 +79,7 @@ int launch_ipm(const IpmArgs<T>& a, int B, hipStream_t stream);
 int launch_ipm64(const IpmArgs<double>& a, int B, hipStream_t stream);   // n <= 64 (k_ipm64.hpp)
 int launch_ipm64(const IpmArgs<float>& a, int B, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
-int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm_impl.hpp, 1 wave)
+int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
 int launch_ipm256(const IpmArgs<float>& a, int B, hipStream_t stream);
 

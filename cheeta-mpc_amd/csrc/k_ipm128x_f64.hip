@@ -4,7 +4,7 @@
 namespace cmpc {
 
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream) {
-  hipLaunchKernelGGL((k_ipm128x<double>), dim3(B), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL((k_ipm128x<double, 2>), dim3(B), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

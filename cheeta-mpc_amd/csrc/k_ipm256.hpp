@@ -1,7 +1,7 @@
 #pragma once
 // k_ipm256.hpp — stage 2 of the hot path, workgroup-tiled IPM k_ipm_tiled<T, NT> for the size class
 // 8 NT < n <= 16 NT: NT = 16 serves 128 < n <= 256 (all-stance horizons N = 11..21, e.g. pronk at N = 20: n = 240),
-// NT = 8 serves 64 < n <= 128 in fp64 (one wave cannot hold that factor in its 256 arch VGPRs). Same batched dense friction-pyramid QP and the same primal-dual Mehrotra
+// (the 64 < n <= 128 class runs on k_ipm128x.hpp). Same batched dense friction-pyramid QP and the same primal-dual Mehrotra
 // predictor-corrector as k_ipm_reg / k_ipm64 (restated in oracle/cmpc_oracle.c:oracle_qp_ipm; settings and stopping
 // rule of hpipm_interface::Settings, HpipmInterfaceSettings.h:44-57); only the linear algebra is organised for a
 // matrix too big for one wavefront's registers.
