@@ -555,7 +555,13 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
           // second row after it: registers)
           T xp[8], xq[8], dp = T(0), kqp = T(0), kpq = T(0), kqq = T(0);
           if constexpr (b < 7) {
+#ifdef X_BARRIER_STAMP  // diagnostic: time waiting at the pair barrier (segment 3)
+            X_STAMP(2);
             __syncthreads();
+            X_STAMP(3);
+#else
+            __syncthreads();
+#endif
 #pragma unroll
             for (int c = 0; c < 8; ++c) xp[c] = L.rowbuf[nb][0][16 * c + lb0];
             dp = L.rowbuf[nb][0][tp + 2];

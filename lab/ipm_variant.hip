@@ -22,7 +22,7 @@ extern "C" int LAB_FN(const cmpc::IpmArgs<double>* a, int B, hipStream_t s, unsi
 #if defined(LAB_PRODUCT) && defined(LAB_K128)  // the 64 < n <= 128 class (csrc/k_ipm128x.hpp), 4 waves per QP
   cmpc::IpmArgs<double> b = *a;
   b.stamps = stamps;
-  hipLaunchKernelGGL((cmpc::LAB_CAT(k_ipm128x_, LAB_FN)<double>), dim3(B), dim3(256), 0, s, b);
+  hipLaunchKernelGGL((cmpc::LAB_CAT(k_ipm128x_, LAB_FN)<double, 2>), dim3(B), dim3(256), 0, s, b);
 #elif defined(LAB_PRODUCT)  // the product kernel (csrc/k_ipm64.hpp); stamps through IpmArgs when built with CMPC_IPM_STAMPS
   cmpc::IpmArgs<double> b = *a;
   b.stamps = stamps;

@@ -16,4 +16,6 @@ run sqp_mixed_n10_f64 --gait 1 --sqp-iters 10 --steps 5
 run sqp_trot_n10_f64 --sqp-iters 10 --steps 5
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_pronk -o run --output-format csv -- python3 $R/bench.py --horizon 20 --all-stance --steps 5 --cpu-sample 0 > $O/prof_pronk.log 2>&1 || { echo "prof fail"; exit 1; }
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_mixed -o run --output-format csv -- python3 $R/bench.py --gait 1 --steps 10 --cpu-sample 0 > $O/prof_mixed.log 2>&1 || { echo "prof fail"; exit 1; }
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_n20f32 -o run --output-format csv -- python3 $R/bench.py --horizon 20 --precision f32 --steps 10 --cpu-sample 0 > $O/prof_n20f32.log 2>&1 || { echo "prof fail"; exit 1; }
 echo sweep_done
