@@ -204,6 +204,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
   acc_t acc[TPW];
 #pragma unroll
   for (int p = 0; p < TPW; ++p) acc[p] = acc_t{T(0), T(0), T(0), T(0)};
+  // this wave's lower tiles (slot p = tile wave + WAVES p, row-major lower order)
+  constexpr int TT = NMAX <= 128 ? TPW : 1;  // tile table (NMAX <= 128 only)
+  int tile_i[TT], tile_j[TT];
+  bool tile_ok[TT];
+#pragma unroll
+  for (int p = 0; p < TT; ++p) {
+    const int idx = wave + p * WAVES;
+    tile_ok[p] = idx < NLT;
+    tile_of(tile_ok[p] ? idx : 0, tile_i[p], tile_j[p]);
+  }
 
   const T dt = T(M->dt);
   const T dtm = T(M->dt_over_m);
@@ -277,22 +287,44 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
       for (int s = 0; s < NX; ++s) acc_g += gam[s] * s_w[buf][s];
       gcol += acc_g;
     }
-    // (e) H += Bqp_k' Q_k Bqp_k on the matrix cores; tiles of not-yet-active columns skipped
+    // (e) H += Bqp_k' Q_k Bqp_k on the matrix cores; tiles of not-yet-active columns skipped. The wave's tiles are
+    //     in row-major order, so the active ones are a prefix (p < np). NMAX <= 128: K-slab outer, tiles inner, so
+    //     consecutive MFMAs are independent accumulators and pipeline instead of waiting out each chain (the 256
+    //     class keeps tile-outer order: its 17 tiles per wave leave no registers for the tile table)
     const int ncols = s_cb[k];
+    if constexpr (NMAX <= 128) {
+      int np = 0;
 #pragma unroll
-    for (int p = 0; p < TPW; ++p) {
-      const int idx = wave + p * WAVES;
-      if (idx < NLT) {
-        int ti, tj;
-        tile_of(idx, ti, tj);
-        if (16 * ti < ncols) {
-          // K = 12: Bqp row 12 (g_z) is identically 0 and unweighted, rows 13..15 are padding
+      for (int p = 0; p < TPW; ++p) np += (tile_ok[p] && 16 * tile_i[p] < ncols) ? 1 : 0;
+      // K = 12: Bqp row 12 (g_z) is identically 0 and unweighted, rows 13..15 are padding
 #pragma unroll
-          for (int s4 = 0; s4 < 3; ++s4) {
-            const int s = 4 * s4 + (lane >> 4);
-            const T av = s_q[buf][s] * s_G[buf][s][16 * ti + (lane & 15)];
-            const T bv = s_G[buf][s][16 * tj + (lane & 15)];
+      for (int s4 = 0; s4 < 3; ++s4) {
+        const int s = 4 * s4 + (lane >> 4);
+        const T qs = s_q[buf][s];
+#pragma unroll
+        for (int p = 0; p < TPW; ++p) {
+          if (p < np) {
+            const T av = qs * s_G[buf][s][16 * tile_i[p] + (lane & 15)];
+            const T bv = s_G[buf][s][16 * tile_j[p] + (lane & 15)];
             acc[p] = MF::run(av, bv, acc[p]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < TPW; ++p) {
+        const int idx = wave + p * WAVES;
+        if (idx < NLT) {
+          int ti, tj;
+          tile_of(idx, ti, tj);
+          if (16 * ti < ncols) {
+#pragma unroll
+            for (int s4 = 0; s4 < 3; ++s4) {
+              const int s = 4 * s4 + (lane >> 4);
+              const T av = s_q[buf][s] * s_G[buf][s][16 * ti + (lane & 15)];
+              const T bv = s_G[buf][s][16 * tj + (lane & 15)];
+              acc[p] = MF::run(av, bv, acc[p]);
+            }
           }
         }
       }
