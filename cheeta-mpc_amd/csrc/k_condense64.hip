@@ -205,6 +205,8 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
   const T dt = T(M->dt);
   const T dtm = T(M->dt_over_m);
   const double* xrq = a.xref + (size_t)q * (N + 1) * NX;
+  double xr_k = lane < NX ? xrq[NX + lane] : 0.0;          // xref_k[lane] and Qbar_k[lane] for the coming step
+  double qd_k = lane < NX ? M->qdiag[1][lane] : 0.0;
   for (int k = 1; k <= N; ++k) {
     const int km = k - 1;
     // (a) gamma <- A_{k-1} gamma + B_{k-1}[:, c]
@@ -258,8 +260,12 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
         xn += M->dt * cr;
       }
       xs = xn;
-      const double qd = M->qdiag[k][s];
-      S.w[s] = T(qd * (xn - xrq[k * NX + s]));
+      S.w[s] = T(qd_k * (xn - xr_k));
+    }
+    // next step's reference and weight, requested now so the loads are off the next step's critical path
+    if (lane < NX && k < N) {
+      xr_k = xrq[(k + 1) * NX + lane];
+      qd_k = M->qdiag[k + 1][lane];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
