@@ -172,7 +172,7 @@ def main():
                                f"{'all-stance (pronk)' if args.all_stance else ('4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk')}, "
                                f"{'fp64' if prec == cm.F64 else 'fp32'}, full hot path per step",
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
-        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128 / k_ipm_tiled<8> n<=128, k_ipm_tiled<16> n<=256)",
+        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)",
                      "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
                      "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},

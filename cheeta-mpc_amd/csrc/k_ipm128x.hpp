@@ -5,7 +5,7 @@
 // HpipmInterfaceSettings.h:44-57; replaces d_ocp_qp_ipm_solve at HpipmInterface.cpp:284), with k_ipm64's linear
 // algebra spread over one workgroup of four waves.
 //
-// MI355X mapping — one workgroup of 4 waves per QP (fp64: two workgroups per CU, 2 waves per SIMD; fp32: three):
+// MI355X mapping — one workgroup of 4 waves per QP (fp64: two workgroups per CU, 2 waves per SIMD; fp32: four):
 //   * the Newton matrix K (128 x 128, both triangles) lives in registers: wave w owns the row groups
 //     R = 4 rho + w (rho = 0..7, cyclic, so every wave keeps rows below any pivot), lane l = 16a + b holding
 //     K[16 rho + 4w + a][16c + b] in register 8 rho + c — 64 values per lane, as k_ipm64's tile per wave;
@@ -155,7 +155,7 @@ struct Lds {
 
 }  // namespace ipm128x
 
-template <typename T, int MINB>  // MINB workgroups per CU: 2 (fp64, 2 waves per SIMD), 3 (fp32)
+template <typename T, int MINB>  // MINB workgroups per CU: 2 (fp64, 2 waves per SIMD), 4 (fp32)
 __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   using namespace ipm128x;
   X_STAMP_DECL;
