@@ -172,7 +172,10 @@ def main():
                                f"{'all-stance (pronk)' if args.all_stance else ('4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk')}, "
                                f"{'fp64' if prec == cm.F64 else 'fp32'}, full hot path per step",
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
-        "roofline": {"bound": "fp64-valu" if prec == cm.F64 else "fp32-valu", "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)",
+        # compute roof at the dtype's dense peak (the contract's "mfma" class); the arithmetic itself runs on the
+        # VALU, which on gfx950 issues fp64 at twice the rate of v_mfma_f64_16x16x4
+        "roofline": {"bound": "mfma", "compute_unit": "fp64 VALU" if prec == cm.F64 else "fp32 VALU",
+                     "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)",
                      "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
                      "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
