@@ -45,6 +45,9 @@ struct cmpc_ctx {
   // host-API staging (grown on demand, outside the async path)
   char* stage;
   size_t stage_bytes;
+  // size-class fork/join: the bigger IPM classes run on `side` concurrently with the n <= 64 class (disjoint QPs)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // stage profiling (cmpc_profile_begin/end)
   std::vector<hipEvent_t> prof_ev;
   int prof_max;
@@ -232,16 +235,33 @@ int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 
+// The size classes solve disjoint QPs (each kernel skips the others' at once), so the 128 / 256 classes run on the
+// context's side stream, forked from and joined back into the caller's stream: a mixed batch overlaps the n <= 64
+// class with the bigger ones, and a single-class batch hides the empty launches. Capturable into a hipGraph.
+template <typename T>
+int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (c->ld < 128 || !c->side) return launch_ipm<T>(a, B, st);
+  if (hipEventRecord(c->ev_fork, st) != hipSuccess || hipStreamWaitEvent(c->side, c->ev_fork, 0) != hipSuccess)
+    return -2;
+  int r = launch_ipm64(a, B, st);
+  if (r == 0) r = launch_ipm128(a, B, c->side);
+  if (r == 0 && a.ld >= 256) r = launch_ipm256(a, B, c->side);
+  if (hipEventRecord(c->ev_join, c->side) != hipSuccess || hipStreamWaitEvent(st, c->ev_join, 0) != hipSuccess)
+    return -2;
+  return r;
+}
+
 int run_ipm(cmpc_ctx* c, int B, hipStream_t st, int warm = 0) {
   int r;
   if (c->precision == CMPC_F64) {
     IpmArgs<double> a = ipm_args<double>(c);
     a.warm = warm;
-    r = launch_ipm<double>(a, B, st);
+    r = run_ipm_classes<double>(c, a, B, st);
   } else {
     IpmArgs<float> a = ipm_args<float>(c);
     a.warm = warm;
-    r = launch_ipm<float>(a, B, st);
+    r = run_ipm_classes<float>(c, a, B, st);
   }
   return r == 0 ? CMPC_OK : CMPC_ERR_HIP;
 }
@@ -373,6 +393,12 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     delete c;
     return CMPC_ERR_HIP;
   }
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    cmpc_destroy(c);
+    return CMPC_ERR_HIP;
+  }
   const int r = cmpc_set_model(c, model);
   if (r != CMPC_OK) {
     cmpc_destroy(c);
@@ -387,6 +413,9 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (c->own_ws && c->ws) (void)hipFree(c->ws);
   if (c->d_model) (void)hipFree(c->d_model);
   if (c->stage) (void)hipFree(c->stage);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->side) (void)hipStreamDestroy(c->side);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   delete c;
   return CMPC_OK;
