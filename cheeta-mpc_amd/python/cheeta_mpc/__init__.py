@@ -12,7 +12,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.abspath(os.path.join(_HERE, "..", ".."))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libcmpc.so")
+LIB_PATH = os.environ.get("CMPC_LIB") or os.path.join(PKG_ROOT, "lib", "libcmpc.so")  # CMPC_LIB: lab builds only
 
 NX, NU, NL = 13, 12, 4
 F64, F32 = 0, 1
