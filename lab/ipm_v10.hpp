@@ -22,9 +22,6 @@
 //   * solves are K^-1 y = X' D^-1 X y: two matrix-vector products over the 40 registers of the strict lower part
 //     (forward: row sums reduced through LDS; backward: column sums reduced through LDS), no serial sweeps and no
 //     transpose of the factor (lab v6: 0.506 -> 0.449 ms per 4096 QPs, same iteration counts, 5e-16 vs v0);
-//   * H u is formed from the tile once (first iteration) and then carried: H du = rhs - (C' Sigma C + reg I) du from
-//     the last solve's right-hand side and the 3x3 blocks, so later iterations skip the 64-FMA product and its two
-//     LDS reductions (lab: 1.8 % per launch, iterates within 1e-14 of the direct product, same iteration counts);
 //   * vectors are lane-per-variable; the <= 105 pyramid rows are two slots per lane (j = lane + 64 cc) with the
 //     primal-dual state in registers and per-iteration scratch in lane-private LDS;
 //   * H is stored by the condensing kernel in the tile order (h_index, cmpc_kernels.hpp): 64 coalesced 512-B
@@ -35,7 +32,7 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
-#include "dpp_rows.hpp"
+#include <dpp_rows.hpp>
 #include "wave_dpp.hpp"
 
 // In-kernel s_memtime stamps, diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP cycles of each
