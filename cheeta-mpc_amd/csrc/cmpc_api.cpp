@@ -45,6 +45,9 @@ struct cmpc_ctx {
   // host-API staging (grown on demand, outside the async path)
   char* stage;
   size_t stage_bytes;
+  // feedback-policy scratch (cmpc_policy_batch, grown on demand)
+  double* pol = nullptr;
+  size_t pol_bytes = 0;
   // size-class fork/join: the bigger IPM classes run on `side` concurrently with the n <= 64 class (disjoint QPs)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -413,6 +416,7 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (c->own_ws && c->ws) (void)hipFree(c->ws);
   if (c->d_model) (void)hipFree(c->d_model);
   if (c->stage) (void)hipFree(c->stage);
+  if (c->pol) (void)hipFree(c->pol);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -558,6 +562,45 @@ int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xre
   if (launch_sqp(2, a, B, st) != 0) return CMPC_ERR_HIP;
   if (qp_iters) HIP_OK(hipMemcpyAsync(qp_iters, c->qpi, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
   if (sqp_iters) HIP_OK(hipMemcpyAsync(sqp_iters, c->sqpi, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  return CMPC_OK;
+}
+
+int cmpc_policy_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                      const uint8_t* contact, const double* u, double act_tol, double* K, int* nfree, int* status,
+                      void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !K || !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int r = run_condense(c, B, x0, xref, foot, contact, st);
+  if (r != CMPC_OK) return r;
+  // scratch for at most `chunk` QPs per launch; launches on one stream reuse it in order
+  const size_t stride = policy_scratch_doubles(c->model.N, c->ld);
+  const int chunk = B < 2048 ? B : 2048;
+  const size_t bytes = stride * sizeof(double) * (size_t)chunk;
+  if (c->pol_bytes < bytes) {
+    HIP_OK(hipStreamSynchronize(st));
+    if (c->pol) (void)hipFree(c->pol);
+    c->pol = nullptr;
+    c->pol_bytes = 0;
+    HIP_OK(hipMalloc((void**)&c->pol, bytes));
+    c->pol_bytes = bytes;
+  }
+  if (!(act_tol > 0.0)) act_tol = c->precision == CMPC_F64 ? 1e-5 : 2e-3;
+  for (int q0 = 0; q0 < B; q0 += chunk) {
+    const int nq = B - q0 < chunk ? B - q0 : chunk;
+    int rr;
+    if (c->precision == CMPC_F64) {
+      PolicyArgs<double> a{c->d_model, c->ld, q0, xref, foot, contact, u, (const double*)c->H, c->tri_map, c->nvar,
+                           c->status, act_tol, K, nfree, status, c->pol, stride};
+      rr = launch_policy<double>(a, nq, st);
+    } else {
+      PolicyArgs<float> a{c->d_model, c->ld, q0, xref, foot, contact, u, (const float*)c->H, c->tri_map, c->nvar,
+                          c->status, act_tol, K, nfree, status, c->pol, stride};
+      rr = launch_policy<float>(a, nq, st);
+    }
+    if (rr != 0) return CMPC_ERR_HIP;
+  }
   return CMPC_OK;
 }
 

@@ -147,6 +147,31 @@ int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, 
 int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream);
 int launch_convert_f64_to_f32(const double* in, float* out, size_t n, hipStream_t stream);
 
+// feedback policy dU/dx0 at a solution (k_policy.hip); reads the condensing workspace (H, tri_map, nvar, status)
+template <typename T>
+struct PolicyArgs {
+  const DevModel* model;
+  int ld;
+  int q0;               // first QP of this launch (blockIdx.x + q0); scratch is indexed by blockIdx.x
+  const double* xref;
+  const double* foot;
+  const uint8_t* contact;
+  const double* u;      // [B][N][L][3] solution
+  const T* H;
+  const int* tri_map;
+  const int* nvar;
+  const int* status;    // condense status
+  double act_tol;
+  double* K;            // [B][12N][13]
+  int* nfree;           // [B] or null
+  int* status_out;      // [B]
+  double* scratch;      // [launch QPs][stride]
+  size_t stride;
+};
+size_t policy_scratch_doubles(int N, int ld);
+template <typename T>
+int launch_policy(const PolicyArgs<T>& a, int nq, hipStream_t stream);
+
 // generic OCP (HpipmInterface::solve semantics)
 struct OcpArgs {
   int N, nx, nU;

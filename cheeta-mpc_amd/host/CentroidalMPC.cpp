@@ -104,6 +104,13 @@ CentroidalMPC::VectorXd CentroidalMPC::UpdateMPC(const VectorXd& state, const Ve
   return out;
 }
 
+int CentroidalMPC::FeedbackPolicyBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                                       const uint8_t* d_contact, const double* d_u, double act_tol, double* d_K,
+                                       int* d_nfree, int* d_status, void* stream) {
+  if (!ctx_) return CMPC_ERR_ARG;
+  return cmpc_policy_batch(ctx_, B, d_x0, d_xref, d_foot, d_contact, d_u, act_tol, d_K, d_nfree, d_status, stream);
+}
+
 int CentroidalMPC::UpdateMPCBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,
                                   const uint8_t* d_contact, double* d_u, double* d_x, int* d_status, int* d_iters,
                                   void* stream) {

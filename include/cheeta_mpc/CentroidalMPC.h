@@ -43,6 +43,12 @@ class CentroidalMPC {
   int UpdateMPCBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot, const uint8_t* d_contact,
                      double* d_u, double* d_x, int* d_status, int* d_iters, void* stream);
 
+  /* Feedback policy dU/dx0 of each QP at its solution d_u (cmpc_policy_batch; the condensed counterpart of
+   * HpipmInterface::getRiccatiFeedback, HpipmInterface.cpp:330-455): d_K [B][N][L][3][13]. */
+  int FeedbackPolicyBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                          const uint8_t* d_contact, const double* d_u, double act_tol, double* d_K, int* d_nfree,
+                          int* d_status, void* stream);
+
   /* The 13-state record UpdateMPC builds from the reference's flat layouts (exposed for tests). */
   void PackRecord(const VectorXd& state, const VectorXd& des_state, const VectorXd& des_inputs, VectorXd& x0,
                   VectorXd& xref, VectorXd& foot, std::vector<uint8_t>& contact) const;

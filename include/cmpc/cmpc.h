@@ -143,6 +143,18 @@ int cmpc_solve_batch_warm(cmpc_ctx* ctx, int B, const double* d_x0, const double
 int cmpc_sqp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                          const uint8_t* d_contact, int sqp_iter_max, double sqp_tol, double* d_u, double* d_x,
                          int* d_status, int* d_qp_iters, int* d_sqp_iters, void* stream);
+/* Feedback policy of each QP at its solution d_u [B][N][L][3] (e.g. from cmpc_solve_batch): d_K [B][N][L][3][13]
+ * = dU/dx0, the condensed counterpart of HpipmInterface::getRiccatiFeedback (HpipmInterface.cpp:330-455; ocs2 uses
+ * it as the linear feedback policy, MultipleShootingSolver.cpp:334-362). K = -Z (Z'HZ)^{-1} Z' Bqp'Q Aqp, where Z
+ * spans the directions of each stance force triple left free by its active pyramid rows (slack <= act_tol, absolute,
+ * in N; act_tol <= 0 selects 1e-5 for fp64 contexts, 2e-3 for fp32): the mu -> 0 limit of HPIPM's K, i.e. the
+ * derivative of the QP solution map on its active set. Swing rows are 0. d_nfree [B] (optional) = dim Z;
+ * d_status [B]: CMPC_SUCCESS, the condensing status, or CMPC_NAN_SOL (Z'HZ not positive definite). Recomputes the
+ * condensed QP into the context workspace; the first call (or a larger B) allocates a scratch slab and
+ * synchronises the stream. */
+int cmpc_policy_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                      const uint8_t* d_contact, const double* d_u, double act_tol, double* d_K, int* d_nfree,
+                      int* d_status, void* stream);
 /* Receding-horizon shift of a batch of solutions on the device: out[q][k] = u[q][min(k + shift, N - 1)] (the role of
  * MultipleShootingSolver::initializeStateInputTrajectories, MultipleShootingSolver.cpp:220-266, on a fixed grid).
  * d_u_out must not alias d_u. */

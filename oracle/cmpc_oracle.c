@@ -1253,3 +1253,170 @@ int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_ite
   free(lin);
   return st;
 }
+
+/* ------------------------------------------------------------------------------------------------ policy */
+
+/* Null space of the active pyramid rows of one force triple (the condensed analogue of HPIPM's Riccati feedback at
+ * the solution, HpipmInterface.cpp:330-455, in its mu -> 0 limit: an active row has Sigma = lambda / s -> inf, so
+ * the triple may only move inside the null space of its active rows). Row r is active when its slack to lo = 0 or
+ * to hi = ub[r] is <= tol. Active rows are orthonormalised in order r = 0..4 (modified Gram-Schmidt, a row whose
+ * residual is below 1e-6 of its norm is dependent); the free directions are then taken greedily from e_0, e_1, e_2,
+ * each time the unit vector with the largest residual against everything chosen so far. Z[a*3 + c] = component a of
+ * free direction c. Returns the number of free directions (0..3). The device kernel k_policy applies the same rule. */
+int oracle_policy_triple(double mu, const double* ub, const double* f, double tol, double* Z) {
+  const double nr[5][3] = {{-1.0, 0.0, mu}, {1.0, 0.0, mu}, {0.0, -1.0, mu}, {0.0, 1.0, mu}, {0.0, 0.0, 1.0}};
+  double Q[3][3];
+  int nq = 0;
+  for (int r = 0; r < 5 && nq < 3; ++r) {
+    const double v = nr[r][0] * f[0] + nr[r][1] * f[1] + nr[r][2] * f[2];
+    if (!(v <= tol || ub[r] - v <= tol)) continue;
+    double w[3] = {nr[r][0], nr[r][1], nr[r][2]};
+    const double n0 = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    for (int p = 0; p < nq; ++p) {
+      const double d = Q[p][0] * w[0] + Q[p][1] * w[1] + Q[p][2] * w[2];
+      for (int a = 0; a < 3; ++a) w[a] -= d * Q[p][a];
+    }
+    const double nw = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    if (!(nw > 1e-6 * n0)) continue;
+    for (int a = 0; a < 3; ++a) Q[nq][a] = w[a] / nw;
+    ++nq;
+  }
+  const int rank = nq;
+  for (int c = 0; c < 3 - rank; ++c) {
+    double best[3] = {0.0, 0.0, 0.0}, bn = -1.0;
+    for (int e = 0; e < 3; ++e) {
+      double w[3] = {0.0, 0.0, 0.0};
+      w[e] = 1.0;
+      for (int p = 0; p < nq; ++p) {
+        const double d = Q[p][0] * w[0] + Q[p][1] * w[1] + Q[p][2] * w[2];
+        for (int a = 0; a < 3; ++a) w[a] -= d * Q[p][a];
+      }
+      const double nw = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+      if (nw > bn) {
+        bn = nw;
+        for (int a = 0; a < 3; ++a) best[a] = w[a];
+      }
+    }
+    for (int a = 0; a < 3; ++a) Q[nq][a] = best[a] / bn;
+    for (int a = 0; a < 3; ++a) Z[a * 3 + c] = Q[nq][a];
+    ++nq;
+  }
+  return 3 - rank;
+}
+
+/* dU/dx0 of the condensed QP at its solution u [N][L][3] (swing entries ignored): K [12N][13] row-major, row
+ * 12k + 3i + a = d u_{k,i,a} / d x0. g(x0) = Bqp' Q (Aqp x0 - X_ref) + r is affine in x0 with slope
+ * F = Bqp' Q Aqp (the free response of SURVEY App. A.3), H does not depend on x0, so on a fixed active set
+ *   K = -Z (Z' H Z)^{-1} Z' F,   Z = blkdiag of the per-triple free directions (oracle_policy_triple);
+ * swing rows are 0 (those forces are eliminated). This is the condensed counterpart of HPIPM's Riccati
+ * feedback/feedforward getters (HpipmInterface.cpp:330-455) that ocs2 uses as the feedback policy
+ * (MultipleShootingSolver.cpp:334-362, useFeedbackPolicy, MultipleShootingSettings.h:57). *n_free = dim(Z).
+ * Returns CMPC_SUCCESS, CMPC_INVALID_CONTACT, or CMPC_NAN_SOL when Z' H Z is not positive definite. */
+int oracle_policy(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                  const double* u, double act_tol, double* K, int* n_free) {
+  const int N = c->N, L = c->L, nf = NU * N;
+  *n_free = 0;
+  memset(K, 0, sizeof(double) * nf * NX);
+  double* Hf = (double*)malloc(sizeof(double) * nf * nf);
+  double* gf = (double*)malloc(sizeof(double) * nf);
+  double x0z[NX] = {0};
+  int st = oracle_condense_full(c, x0z, xref, foot, contact, Hf, gf);
+  if (st != CMPC_SUCCESS) {
+    free(Hf);
+    free(gf);
+    return st;
+  }
+  /* F = sum_k G_k' Q_{k+1} P_{k+1}, P_{k+1} = A_k P_k (P_0 = I), G_{k+1} = A_k G_k + [B_k at step k] */
+  double* A = (double*)malloc(sizeof(double) * N * NX * NX);
+  double* Bm = (double*)malloc(sizeof(double) * N * NX * NU);
+  oracle_srbd_dynamics(c, xref, foot, contact, A, Bm);
+  double* G = (double*)calloc((size_t)NX * nf, sizeof(double));
+  double* G2 = (double*)malloc(sizeof(double) * NX * nf);
+  double* F = (double*)calloc((size_t)nf * NX, sizeof(double));
+  double P[NX * NX], P2[NX * NX];
+  memset(P, 0, sizeof(P));
+  for (int r = 0; r < NX; ++r) P[r * NX + r] = 1.0;
+  for (int k = 0; k < N; ++k) {
+    const double* Ak = A + (size_t)k * NX * NX;
+    const double* Bk = Bm + (size_t)k * NX * NU;
+    for (int r = 0; r < NX; ++r) {
+      for (int j = 0; j < nf; ++j) {
+        double s = 0.0;
+        for (int t = 0; t < NX; ++t) s += Ak[r * NX + t] * G[t * nf + j];
+        G2[r * nf + j] = s;
+      }
+      for (int j = 0; j < NU; ++j) G2[r * nf + NU * k + j] += Bk[r * NU + j];
+      for (int j = 0; j < NX; ++j) {
+        double s = 0.0;
+        for (int t = 0; t < NX; ++t) s += Ak[r * NX + t] * P[t * NX + j];
+        P2[r * NX + j] = s;
+      }
+    }
+    memcpy(G, G2, sizeof(double) * NX * nf);
+    memcpy(P, P2, sizeof(P));
+    const double* q = c->qdiag[k + 1];
+    for (int a = 0; a < NU * (k + 1); ++a)
+      for (int j = 0; j < NX; ++j) {
+        double s = 0.0;
+        for (int r = 0; r < NX; ++r) s += G[r * nf + a] * q[r] * P[r * NX + j];
+        F[a * NX + j] += s;
+      }
+  }
+  /* free directions of every stance triple */
+  int nt = 0;
+  int* idx = (int*)malloc(sizeof(int) * N * L);
+  int* off = (int*)malloc(sizeof(int) * (N * L + 1));
+  double* Z = (double*)calloc((size_t)N * L * 9, sizeof(double));
+  int* kt = (int*)malloc(sizeof(int) * N * L);
+  int m = 0;
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < L; ++i) {
+      if (!contact[k * L + i]) continue;
+      idx[nt] = NU * k + 3 * i;
+      off[nt] = m;
+      kt[nt] = oracle_policy_triple(c->mu[i], c->force_ub, u + ((size_t)k * L + i) * 3, act_tol, Z + nt * 9);
+      m += kt[nt];
+      ++nt;
+    }
+  double* Hr = (double*)malloc(sizeof(double) * (m > 0 ? m * m : 1));
+  double* Y = (double*)malloc(sizeof(double) * (m > 0 ? m * NX : 1));
+  for (int t1 = 0; t1 < nt; ++t1)
+    for (int c1 = 0; c1 < kt[t1]; ++c1) {
+      const int r1 = off[t1] + c1;
+      for (int t2 = 0; t2 < nt; ++t2)
+        for (int c2 = 0; c2 < kt[t2]; ++c2) {
+          double s = 0.0;
+          for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b)
+              s += Z[t1 * 9 + a * 3 + c1] * Hf[(size_t)(idx[t1] + a) * nf + idx[t2] + b] * Z[t2 * 9 + b * 3 + c2];
+          Hr[r1 * m + off[t2] + c2] = s;
+        }
+      for (int j = 0; j < NX; ++j) {
+        double s = 0.0;
+        for (int a = 0; a < 3; ++a) s += Z[t1 * 9 + a * 3 + c1] * F[(idx[t1] + a) * NX + j];
+        Y[r1 * NX + j] = -s;
+      }
+    }
+  st = CMPC_SUCCESS;
+  if (m > 0 && oracle_cholesky(m, Hr, m) != 0) st = CMPC_NAN_SOL;
+  if (st == CMPC_SUCCESS && m > 0) {
+    double* col = (double*)malloc(sizeof(double) * m);
+    for (int j = 0; j < NX; ++j) {
+      for (int r = 0; r < m; ++r) col[r] = Y[r * NX + j];
+      oracle_chol_solve(m, Hr, m, col);
+      for (int r = 0; r < m; ++r) Y[r * NX + j] = col[r];
+    }
+    free(col);
+    for (int t = 0; t < nt; ++t)
+      for (int a = 0; a < 3; ++a)
+        for (int j = 0; j < NX; ++j) {
+          double s = 0.0;
+          for (int cc = 0; cc < kt[t]; ++cc) s += Z[t * 9 + a * 3 + cc] * Y[(off[t] + cc) * NX + j];
+          K[(size_t)(idx[t] + a) * NX + j] = s;
+        }
+  }
+  *n_free = m;
+  free(Hf); free(gf); free(A); free(Bm); free(G); free(G2); free(F);
+  free(idx); free(off); free(Z); free(kt); free(Hr); free(Y);
+  return st;
+}

@@ -118,6 +118,13 @@ void oracle_gait_contact(const cmpc_gait* g, const int* leg_map, double t_start,
 int oracle_cholesky(int n, double* A, int lda);                       /* in place, lower; 0 ok, -1 not PD */
 void oracle_chol_solve(int n, const double* L, int lda, double* b);   /* solves (L L^T) x = b in place */
 
+
+/* Feedback policy dU/dx0 at a solution u [N][L][3] on its active set (act_tol = slack threshold, absolute):
+ * K [12N][13] row-major; *n_free = reduced dimension. oracle_policy_triple: free directions of one triple. */
+int oracle_policy_triple(double mu, const double* ub, const double* f, double tol, double* Z);
+int oracle_policy(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                  const double* u, double act_tol, double* K, int* n_free);
+
 #ifdef __cplusplus
 }
 #endif

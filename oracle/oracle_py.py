@@ -97,6 +97,8 @@ def lib():
         L.oracle_sqp_solve.argtypes = [C.c_void_p, P(Settings), C.c_int, C.c_double, d, d, d, u8, d, d, i, i]
         L.oracle_srbd_dynamics_lin.argtypes = [C.c_void_p, d, d, u8, d, d, d, d]
         L.oracle_srbd_dynamics_lin.restype = None
+        L.oracle_policy.argtypes = [C.c_void_p, d, d, u8, d, C.c_double, d, i]
+        L.oracle_policy_triple.argtypes = [C.c_double, d, d, C.c_double, d]
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         _lib = L
     return _lib
@@ -311,6 +313,26 @@ def gait_contact(gait, t_start, t0, dt, N, leg_map=None):
     lib().oracle_gait_contact(C.byref(gait), _p(lm, C.c_int) if lm is not None else None, t_start, t0, dt, N,
                               _p(out, C.c_uint8))
     return out
+
+
+def policy(model, xref, foot, contact, u, act_tol=1e-5):
+    """Feedback policy dU/dx0 of one QP at its solution u [N,L,3] (oracle_policy): (K [N,L,3,13], n_free, status)."""
+    N = model.N
+    c = consts(model)
+    K = np.zeros((N, NL, 3, NX))
+    nfree = C.c_int(0)
+    xref, foot, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (xref, foot, u))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    st = lib().oracle_policy(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u), act_tol, _p(K),
+                             C.byref(nfree))
+    return K, nfree.value, st
+
+
+def policy_triple(mu, ub, f, tol):
+    Z = np.zeros((3, 3))
+    ub, f = (np.ascontiguousarray(a, dtype=np.float64) for a in (ub, f))
+    k = lib().oracle_policy_triple(mu, _p(ub), _p(f), tol, _p(Z))
+    return Z[:, :k]
 
 
 def philox(ctr, key):
