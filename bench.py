@@ -90,7 +90,11 @@ def main():
     from cheeta_mpc.shard import Dist
     dist = Dist()  # gloo barriers + max-over-ranks only; no collective on the data path
     world, rank = dist.world, dist.rank
-    cm.hip().hipSetDevice(dist.local_rank)
+    ndev = cm.device_count()
+    if ndev <= 0:
+        raise RuntimeError("bench.py: no HIP device visible")
+    # one GPU per rank; the modulo covers launchers that expose only the rank's own GPU (HIP_VISIBLE_DEVICES)
+    cm._hchk(cm.hip().hipSetDevice(dist.local_rank % ndev), "hipSetDevice")
     barrier, max_over_ranks = dist.barrier, dist.max
 
     B, N = args.batch, args.horizon
