@@ -36,9 +36,10 @@ def ipm_flops(n, iters):
     return it * (n ** 3 / 3.0 + 4.0 * n ** 2) + (it + 1.0) * 2.0 * n ** 2
 
 
-def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_wall_s=5.0):
+def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_wall_s=5.0, riccati=False):
     """The CPU oracle (same algorithm, fp64) on a bounded sample of the same batch, repeated until it has done about
-    min_cpu_s of thread-time (capped at max_wall_s wall): QPs/s = QPs solved / wall time."""
+    min_cpu_s of thread-time (capped at max_wall_s wall): QPs/s = QPs solved / wall time. riccati=True times the
+    HPIPM-style restatement instead (no condensing; Riccati Newton steps over the stages, same iterates)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as op  # test infrastructure: the CPU restatement, timed as the baseline
     mo = op.default_model(model_n)
@@ -46,7 +47,10 @@ def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_
     done, wall, u, st = 0, 0.0, None, None
     while True:
         t0 = time.perf_counter()
-        u, _, st, _ = op.solve_batch(mo, s, x0, xref, foot, contact, nthreads=threads, want_x=False)
+        if riccati:
+            u, st, _ = op.riccati_solve_batch(mo, s, x0, xref, foot, contact, nthreads=threads)
+        else:
+            u, _, st, _ = op.solve_batch(mo, s, x0, xref, foot, contact, nthreads=threads, want_x=False)
         wall += time.perf_counter() - t0
         done += x0.shape[0]
         if wall * threads >= min_cpu_s or wall >= max_wall_s:
@@ -208,6 +212,14 @@ def main():
                                   "sample": f"first {S} QPs of the same batch x{done // S}, oracle/cmpc_oracle.c "
                                             f"fp64 (same algorithm), {threads} pthreads, {dtc:.2f} s wall"}
         result["max_rel_du_vs_cpu_fp64"] = float(rel[both].max()) if both.any() else None
+        ur, str_, dtr, doner = cpu_baseline(N, hx0, hxr, hft, ct[:S], threads, riccati=True)
+        relr = np.abs(ug - ur).reshape(S, -1).max(axis=1) / np.maximum(1.0, np.abs(ur).reshape(S, -1).max(axis=1))
+        bothr = (str_ == 0) & (status[:S] == 0)
+        result["cpu_baseline_riccati"] = {
+            "value": doner / dtr, "unit": "QPs/s", "cores": threads, "kind": "port",
+            "sample": f"first {S} QPs x{doner // S}, oracle_riccati_solve_batch (HPIPM-style: no condensing, Riccati "
+                      f"Newton steps over the stages, same IPM), {threads} pthreads, {dtr:.2f} s wall",
+            "max_rel_du_vs_gpu": float(relr[bothr].max()) if bothr.any() else None}
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()

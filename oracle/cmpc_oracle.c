@@ -339,6 +339,17 @@ static inline void pyr_applyT(double mu, const double* w, double* f) {
   f[2] = mu * (w[0] + w[1] + w[2] + w[3]) + w[4];
 }
 
+/* The two operations the IPM needs from the QP's Hessian: the gradient H u + g, and solves with the Newton matrix
+ * H + C' Sigma C + reg I. Dense (oracle_qp_ipm: Cholesky of the condensed H) or structured (oracle_riccati_solve_one:
+ * rollout / adjoint and a Riccati recursion over the stages, HPIPM's approach); the iteration itself is shared. */
+typedef struct qp_ops {
+  void* ctx;
+  void (*grad)(void* ctx, const double* u, double* hug);
+  int (*factor)(void* ctx, int nt, const double* tri_mu, const double* ll, const double* lu, const double* tl,
+                const double* tu, double reg);
+  void (*solve)(void* ctx, double* b);
+} qp_ops;
+
 typedef struct ipm_ws {
   double *invd, *K, *rg, *rhs, *du, *cu, *cdu, *tl, *tu, *ll, *lu, *rl, *ru, *dtl, *dtu, *dll, *dlu, *rml, *rmu, *w;
 } ipm_ws;
@@ -374,9 +385,8 @@ static void ipm_chol_solve(int n, const double* Lm, const double* invd, double* 
   }
 }
 
-static void ipm_dir(int n, int ld, int nt, const double* tri_mu, ipm_ws* W) {
+static void ipm_dir(int n, const qp_ops* ops, int nt, const double* tri_mu, ipm_ws* W) {
   const int m = 5 * nt;
-  (void)ld;
   for (int j = 0; j < m; ++j)
     W->w[j] = (W->rml[j] + W->ll[j] * W->rl[j]) / W->tl[j] - (W->rmu[j] + W->lu[j] * W->ru[j]) / W->tu[j];
   for (int i = 0; i < n; ++i) W->rhs[i] = -W->rg[i];
@@ -386,7 +396,7 @@ static void ipm_dir(int n, int ld, int nt, const double* tri_mu, ipm_ws* W) {
     for (int d = 0; d < 3; ++d) W->rhs[3 * t + d] -= f[d];
   }
   memcpy(W->du, W->rhs, sizeof(double) * n);
-  ipm_chol_solve(n, W->K, W->invd, W->du);
+  ops->solve(ops->ctx, W->du);
   for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], W->du + 3 * t, W->cdu + 5 * t);
   for (int j = 0; j < m; ++j) {
     W->dtl[j] = W->cdu[j] + W->rl[j];
@@ -407,15 +417,77 @@ static double ipm_maxstep(int m, const ipm_ws* W) {
   return a;
 }
 
+typedef struct dense_ops_ctx {
+  int n, ld;
+  const double *H, *g;
+  double *K, *invd;
+} dense_ops_ctx;
+
+static void dense_grad(void* vc, const double* u, double* hug) {
+  const dense_ops_ctx* d = (const dense_ops_ctx*)vc;
+  for (int i = 0; i < d->n; ++i) {
+    double acc = 0.0;
+    for (int j = 0; j < d->n; ++j) acc += d->H[(size_t)i * d->ld + j] * u[j];
+    hug[i] = acc + d->g[i];
+  }
+}
+
+/* Newton matrix K = H + C' diag(lam/t) C + reg I, Cholesky */
+static int dense_factor(void* vc, int nt, const double* tri_mu, const double* lla, const double* lua,
+                        const double* tla, const double* tua, double reg) {
+  dense_ops_ctx* d = (dense_ops_ctx*)vc;
+  const int n = d->n;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) d->K[i * n + j] = d->H[(size_t)i * d->ld + j];
+  for (int t = 0; t < nt; ++t) {
+    const double* ll = lla + 5 * t;
+    const double* lu = lua + 5 * t;
+    const double* tl = tla + 5 * t;
+    const double* tu = tua + 5 * t;
+    double sg[5];
+    for (int r = 0; r < 5; ++r) sg[r] = ll[r] / tl[r] + lu[r] / tu[r];
+    const double mu_t = tri_mu[t];
+    const int b = 3 * t;
+    d->K[b * n + b] += sg[0] + sg[1];
+    d->K[(b + 1) * n + b + 1] += sg[2] + sg[3];
+    d->K[(b + 2) * n + b + 2] += mu_t * mu_t * (sg[0] + sg[1] + sg[2] + sg[3]) + sg[4];
+    const double xz = mu_t * (-sg[0] + sg[1]), yz = mu_t * (-sg[2] + sg[3]);
+    d->K[b * n + b + 2] += xz;
+    d->K[(b + 2) * n + b] += xz;
+    d->K[(b + 1) * n + b + 2] += yz;
+    d->K[(b + 2) * n + b + 1] += yz;
+  }
+  for (int i = 0; i < n; ++i) d->K[i * n + i] += reg;
+  return ipm_cholesky(n, d->K, d->invd);
+}
+
+static void dense_solve(void* vc, double* b) {
+  const dense_ops_ctx* d = (const dense_ops_ctx*)vc;
+  ipm_chol_solve(d->n, d->K, d->invd, b);
+}
+
+static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const double* tri_lo, const double* tri_hi,
+                      const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters, double* res);
+
 int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
                   const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters,
                   double* res) {
+  double* buf = (double*)calloc((size_t)n * n + (size_t)n + 1, sizeof(double));
+  dense_ops_ctx d = {n, ld, H, g, buf, buf + (size_t)n * n};
+  qp_ops ops = {&d, dense_grad, dense_factor, dense_solve};
+  const int st = qp_ipm_run(n, &ops, tri_mu, tri_lo, tri_hi, s, u, lam_lo, lam_hi, iters, res);
+  free(buf);
+  return st;
+}
+
+static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const double* tri_lo, const double* tri_hi,
+                      const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters, double* res) {
   const int nt = n / 3, m = 5 * nt;
   ipm_ws W;
-  double* buf = (double*)calloc((size_t)n * n + 5 * (size_t)n + 15 * (size_t)(m + 1), sizeof(double));
+  double* buf = (double*)calloc(4 * (size_t)n + 1 + 15 * (size_t)(m + 1), sizeof(double));
   double* p = buf;
-  W.K = p; p += (size_t)n * n;
-  W.invd = p; p += n;
+  W.K = NULL;
+  W.invd = NULL;
   W.rg = p; p += n;
   W.rhs = p; p += n;
   W.du = p; p += n;
@@ -442,16 +514,12 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
   for (it = 0;; ++it) {
     /* residuals */
     for (int t = 0; t < nt; ++t) pyr_apply(tri_mu[t], u + 3 * t, W.cu + 5 * t);
-    for (int i = 0; i < n; ++i) {
-      double acc = 0.0;
-      for (int j = 0; j < n; ++j) acc += H[(size_t)i * ld + j] * u[j];
-      hu[i] = acc;
-    }
+    ops->grad(ops->ctx, u, hu); /* H u + g */
     for (int j = 0; j < m; ++j) W.w[j] = W.ll[j] - W.lu[j];
     for (int t = 0; t < nt; ++t) {
       double f[3];
       pyr_applyT(tri_mu[t], W.w + 5 * t, f);
-      for (int d = 0; d < 3; ++d) W.rg[3 * t + d] = hu[3 * t + d] + g[3 * t + d] - f[d];
+      for (int d = 0; d < 3; ++d) W.rg[3 * t + d] = hu[3 * t + d] - f[d];
     }
     double musum = 0.0;
     rs = 0.0;
@@ -483,29 +551,7 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
       status = CMPC_MIN_STEP;
       break;
     }
-    /* Newton matrix K = H + C' diag(lam/t) C + reg I */
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) W.K[i * n + j] = H[(size_t)i * ld + j];
-    for (int t = 0; t < nt; ++t) {
-      const double* ll = W.ll + 5 * t;
-      const double* lu = W.lu + 5 * t;
-      const double* tl = W.tl + 5 * t;
-      const double* tu = W.tu + 5 * t;
-      double sg[5];
-      for (int r = 0; r < 5; ++r) sg[r] = ll[r] / tl[r] + lu[r] / tu[r];
-      const double mu_t = tri_mu[t];
-      const int b = 3 * t;
-      W.K[b * n + b] += sg[0] + sg[1];
-      W.K[(b + 1) * n + b + 1] += sg[2] + sg[3];
-      W.K[(b + 2) * n + b + 2] += mu_t * mu_t * (sg[0] + sg[1] + sg[2] + sg[3]) + sg[4];
-      const double xz = mu_t * (-sg[0] + sg[1]), yz = mu_t * (-sg[2] + sg[3]);
-      W.K[b * n + b + 2] += xz;
-      W.K[(b + 2) * n + b] += xz;
-      W.K[(b + 1) * n + b + 2] += yz;
-      W.K[(b + 2) * n + b + 1] += yz;
-    }
-    for (int i = 0; i < n; ++i) W.K[i * n + i] += s->reg_prim;
-    if (ipm_cholesky(n, W.K, W.invd) != 0) {
+    if (ops->factor(ops->ctx, nt, tri_mu, W.ll, W.lu, W.tl, W.tu, s->reg_prim) != 0) {
       status = CMPC_NAN_SOL;
       break;
     }
@@ -514,7 +560,7 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
       W.rml[j] = W.tl[j] * W.ll[j];
       W.rmu[j] = W.tu[j] * W.lu[j];
     }
-    ipm_dir(n, ld, nt, tri_mu, &W);
+    ipm_dir(n, ops, nt, tri_mu, &W);
     double alpha = dmin(1.0, ipm_maxstep(m, &W));
     if (m > 0) {
       double maff = 0.0;
@@ -529,7 +575,7 @@ int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double*
         W.rml[j] = W.tl[j] * W.ll[j] + W.dtl[j] * W.dll[j] - sigma * mu;
         W.rmu[j] = W.tu[j] * W.lu[j] + W.dtu[j] * W.dlu[j] - sigma * mu;
       }
-      ipm_dir(n, ld, nt, tri_mu, &W);
+      ipm_dir(n, ops, nt, tri_mu, &W);
       alpha = dmin(1.0, TAU * ipm_maxstep(m, &W));
     }
     if (alpha < s->alpha_min) {
@@ -1419,4 +1465,388 @@ int oracle_policy(const oracle_consts* c, const double* xref, const double* foot
   free(Hf); free(gf); free(A); free(Bm); free(G); free(G2); free(F);
   free(idx); free(off); free(Z); free(kt); free(Hr); free(Y);
   return st;
+}
+
+/* ------------------------------------------------------------------------------------------------ Riccati IPM */
+
+/* The same QP solved the way HPIPM solves the reference's OCP (d_ocp_qp_ipm_solve, HpipmInterface.cpp:282-284;
+ * ric_alg 0, HpipmInterfaceSettings.h:56): no condensing. The Newton system (H + C' Sigma C + reg I) du = b is the
+ * KKT system of an OCP over the stages with state z_k = [x_k (13); u_{k-1} (12, the previous forces, which carry
+ * the force-rate coupling of CentroidalMPC.cpp:227-231)], input v_k = the stance forces of step k, z_0 = 0:
+ *   z_{k+1} = blkdiag(A_k, 0) z_k + [B_k S_k; S_k] v_k        (S_k: stance selection, 12 x 3 ns_k)
+ *   stage   1/2 x'diag(q_k)x [k >= 1] + sum_j Wr_j (S v - u_prev)_j^2 [k >= 1] + sum_j Wf_j (S v)_j^2
+ *           + 1/2 v'(C'Sigma C + reg I)v - b_k'v;            terminal 1/2 x_N'diag(q_N) x_N,
+ * solved by the backward Riccati recursion and a forward sweep; H u + g is a rollout plus an adjoint sweep.
+ * O(N (25^3 + 25^2 nu)) per iteration instead of O(n^3): an independent restatement of the same optimum (its
+ * iterates agree with oracle_qp_ipm to rounding) and the CPU line closest to the reference's own solver. */
+#define NZ (NX + NU)
+
+typedef struct ric_ops_ctx {
+  const oracle_consts* c;
+  int N;
+  const double *A, *B, *x0, *xref, *fdes; /* A [N][13][13], B [N][13][12], fdes [N][L] (z) */
+  int nu[64], off[64], nst[64], legs[64][CMPC_MAX_LEGS];
+  double *Bt; /* [N][NZ][12]  B~_k (first nu_k columns used) */
+  double *St; /* [N][12][NZ] */
+  double *Kf; /* [N][12][NZ] */
+  double *Lr; /* [N][12][12] Cholesky of Rt_k, and Lri [N][12] = 1 / L_ii */
+  double *Lri;
+  double *P;  /* scratch [NZ][NZ] x 2 */
+  int n;
+} ric_ops_ctx;
+
+static void ric_grad(void* vc, const double* u, double* hug) {
+  const ric_ops_ctx* r = (const ric_ops_ctx*)vc;
+  const oracle_consts* c = r->c;
+  const int N = r->N, L = c->L;
+  double* uf = (double*)calloc((size_t)N * NU, sizeof(double));
+  double* X = (double*)malloc(sizeof(double) * (N + 1) * NX);
+  for (int k = 0; k < N; ++k)
+    for (int t = 0; t < r->nst[k]; ++t)
+      for (int d = 0; d < 3; ++d) uf[k * NU + 3 * r->legs[k][t] + d] = u[r->off[k] + 3 * t + d];
+  memcpy(X, r->x0, sizeof(double) * NX);
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < NX; ++i) {
+      double acc = 0.0;
+      for (int t = 0; t < NX; ++t) acc += r->A[(size_t)k * NX * NX + i * NX + t] * X[k * NX + t];
+      for (int j = 0; j < NU; ++j) acc += r->B[(size_t)k * NX * NU + i * NU + j] * uf[k * NU + j];
+      X[(k + 1) * NX + i] = acc;
+    }
+  double lam[NX], lam2[NX], gk[NU];
+  for (int i = 0; i < NX; ++i) lam[i] = c->qdiag[N][i] * (X[N * NX + i] - r->xref[N * NX + i]);
+  for (int k = N - 1; k >= 0; --k) {
+    for (int j = 0; j < NU; ++j) {
+      double acc = 0.0;
+      for (int i = 0; i < NX; ++i) acc += r->B[(size_t)k * NX * NU + i * NU + j] * lam[i];
+      const double fd = (j % 3 == 2) ? r->fdes[k * L + j / 3] : 0.0;
+      acc += 2.0 * c->Wf[j] * (uf[k * NU + j] - fd);
+      if (k > 0) acc += 2.0 * c->Wr[j] * (uf[k * NU + j] - uf[(k - 1) * NU + j]);
+      if (k < N - 1) acc -= 2.0 * c->Wr[j] * (uf[(k + 1) * NU + j] - uf[k * NU + j]);
+      gk[j] = acc;
+    }
+    for (int t = 0; t < r->nst[k]; ++t)
+      for (int d = 0; d < 3; ++d) hug[r->off[k] + 3 * t + d] = gk[3 * r->legs[k][t] + d];
+    if (k > 0) {
+      for (int i = 0; i < NX; ++i) {
+        double acc = c->qdiag[k][i] * (X[k * NX + i] - r->xref[k * NX + i]);
+        for (int t = 0; t < NX; ++t) acc += r->A[(size_t)k * NX * NX + t * NX + i] * lam[t];
+        lam2[i] = acc;
+      }
+      memcpy(lam, lam2, sizeof(lam));
+    }
+  }
+  free(uf);
+  free(X);
+}
+
+static int ric_factor(void* vc, int nt, const double* tri_mu, const double* lla, const double* lua,
+                      const double* tla, const double* tua, double reg) {
+  ric_ops_ctx* r = (ric_ops_ctx*)vc;
+  const oracle_consts* c = r->c;
+  const int N = r->N;
+  double* P = r->P;
+  double* Pn = r->P + NZ * NZ;
+  double PB[NZ * NU], PA[NZ * NX], Rt[NU * NU];
+  (void)nt;
+  memset(P, 0, sizeof(double) * NZ * NZ);
+  for (int i = 0; i < NX; ++i) P[i * NZ + i] = c->qdiag[N][i];
+  for (int k = N - 1; k >= 0; --k) {
+    const int m = r->nu[k];
+    const double* Ak = r->A + (size_t)k * NX * NX;
+    const double* Bt = r->Bt + (size_t)k * NZ * NU;
+    double* St = r->St + (size_t)k * NU * NZ;
+    double* Kf = r->Kf + (size_t)k * NU * NZ;
+    double* Lr = r->Lr + (size_t)k * NU * NU;
+    double* Lri = r->Lri + (size_t)k * NU;
+    for (int i = 0; i < NZ; ++i) {
+      for (int j = 0; j < m; ++j) {
+        double acc = 0.0;
+        for (int t = 0; t < NZ; ++t) acc += P[i * NZ + t] * Bt[t * NU + j];
+        PB[i * NU + j] = acc;
+      }
+      for (int j = 0; j < NX; ++j) {
+        double acc = 0.0;
+        for (int t = 0; t < NX; ++t) acc += P[i * NZ + t] * Ak[t * NX + j];
+        PA[i * NX + j] = acc;
+      }
+    }
+    /* Rt = R_k + B~' P B~, R_k = diag(2 Wf + 2 Wr [k >= 1]) + C'Sigma C + reg I on the stance triples */
+    for (int a = 0; a < m; ++a)
+      for (int b = 0; b < m; ++b) {
+        double acc = 0.0;
+        for (int t = 0; t < NZ; ++t) acc += Bt[t * NU + a] * PB[t * NU + b];
+        Rt[a * NU + b] = acc;
+      }
+    for (int tt = 0; tt < r->nst[k]; ++tt) {
+      const int tg = r->off[k] / 3 + tt, b = 3 * tt;
+      const double* ll = lla + 5 * tg;
+      const double* lu = lua + 5 * tg;
+      const double* tl = tla + 5 * tg;
+      const double* tu = tua + 5 * tg;
+      double sg[5];
+      for (int q = 0; q < 5; ++q) sg[q] = ll[q] / tl[q] + lu[q] / tu[q];
+      const double mu_t = tri_mu[tg];
+      Rt[b * NU + b] += sg[0] + sg[1];
+      Rt[(b + 1) * NU + b + 1] += sg[2] + sg[3];
+      Rt[(b + 2) * NU + b + 2] += mu_t * mu_t * (sg[0] + sg[1] + sg[2] + sg[3]) + sg[4];
+      const double xz = mu_t * (-sg[0] + sg[1]), yz = mu_t * (-sg[2] + sg[3]);
+      Rt[b * NU + b + 2] += xz;
+      Rt[(b + 2) * NU + b] += xz;
+      Rt[(b + 1) * NU + b + 2] += yz;
+      Rt[(b + 2) * NU + b + 1] += yz;
+      for (int d = 0; d < 3; ++d) {
+        const int j = 3 * r->legs[k][tt] + d;
+        Rt[(b + d) * NU + b + d] += 2.0 * c->Wf[j] + (k > 0 ? 2.0 * c->Wr[j] : 0.0) + reg;
+      }
+    }
+    /* St = S_k + B~' P A~ (A~ = blkdiag(A_k, 0)); S_k = -2 Wr on the u_prev columns (k >= 1) */
+    for (int a = 0; a < m; ++a) {
+      for (int j = 0; j < NZ; ++j) {
+        double acc = 0.0;
+        if (j < NX)
+          for (int t = 0; t < NZ; ++t) acc += Bt[t * NU + a] * PA[t * NX + j];
+        St[a * NZ + j] = acc;
+      }
+      if (k > 0) {
+        const int jl = 3 * r->legs[k][a / 3] + a % 3;
+        St[a * NZ + NX + jl] += -2.0 * c->Wr[jl];
+      }
+    }
+    /* Cholesky of Rt with the kernels' pivot guard */
+    for (int a = 0; a < m; ++a)
+      for (int b = 0; b < m; ++b) Lr[a * NU + b] = Rt[a * NU + b];
+    for (int q = 0; q < m; ++q) {
+      double d = Lr[q * NU + q];
+      for (int j = 0; j < q; ++j) d -= Lr[q * NU + j] * Lr[q * NU + j];
+      if (d != d) return -1;
+      const double il = d > 1e-200 ? 1.0 / sqrt(d) : 0.0;
+      Lr[q * NU + q] = d > 1e-200 ? sqrt(d) : 0.0;
+      Lri[q] = il;
+      for (int i = q + 1; i < m; ++i) {
+        double sacc = Lr[i * NU + q];
+        for (int j = 0; j < q; ++j) sacc -= Lr[i * NU + j] * Lr[q * NU + j];
+        Lr[i * NU + q] = sacc * il;
+      }
+    }
+    /* K = -Rt^{-1} St, column by column */
+    for (int j = 0; j < NZ; ++j) {
+      double col[NU];
+      for (int a = 0; a < m; ++a) col[a] = St[a * NZ + j];
+      for (int a = 0; a < m; ++a) {
+        double sacc = col[a];
+        for (int b = 0; b < a; ++b) sacc -= Lr[a * NU + b] * col[b];
+        col[a] = sacc * Lri[a];
+      }
+      for (int a = m - 1; a >= 0; --a) {
+        double sacc = col[a];
+        for (int b = a + 1; b < m; ++b) sacc -= Lr[b * NU + a] * col[b];
+        col[a] = sacc * Lri[a];
+      }
+      for (int a = 0; a < m; ++a) Kf[a * NZ + j] = -col[a];
+    }
+    /* P_k = Q_k + A~' P A~ + St' K */
+    for (int i = 0; i < NZ; ++i)
+      for (int j = 0; j < NZ; ++j) {
+        double acc = 0.0;
+        if (i < NX && j < NX)
+          for (int t = 0; t < NX; ++t) acc += Ak[t * NX + i] * PA[t * NX + j];
+        for (int a = 0; a < m; ++a) acc += St[a * NZ + i] * Kf[a * NZ + j];
+        Pn[i * NZ + j] = acc;
+      }
+    if (k > 0) {
+      for (int i = 0; i < NX; ++i) Pn[i * NZ + i] += c->qdiag[k][i];
+      for (int j = 0; j < NU; ++j) Pn[(NX + j) * NZ + NX + j] += 2.0 * c->Wr[j];
+    }
+    for (int i = 0; i < NZ; ++i)
+      for (int j = 0; j < i; ++j) {
+        const double v = 0.5 * (Pn[i * NZ + j] + Pn[j * NZ + i]);
+        Pn[i * NZ + j] = v;
+        Pn[j * NZ + i] = v;
+      }
+    double* tmp = P;
+    P = Pn;
+    Pn = tmp;
+  }
+  return 0;
+}
+
+static void ric_solve(void* vc, double* bvec) {
+  const ric_ops_ctx* r = (const ric_ops_ctx*)vc;
+  const int N = r->N;
+  double p[NZ], p2[NZ], z[NZ], z2[NZ];
+  double* kff = (double*)malloc(sizeof(double) * N * NU);
+  memset(p, 0, sizeof(p));
+  for (int k = N - 1; k >= 0; --k) {
+    const int m = r->nu[k];
+    const double* Ak = r->A + (size_t)k * NX * NX;
+    const double* Bt = r->Bt + (size_t)k * NZ * NU;
+    const double* St = r->St + (size_t)k * NU * NZ;
+    const double* Lr = r->Lr + (size_t)k * NU * NU;
+    const double* Lri = r->Lri + (size_t)k * NU;
+    double col[NU];
+    for (int a = 0; a < m; ++a) {
+      double acc = -bvec[r->off[k] + a];
+      for (int t = 0; t < NZ; ++t) acc += Bt[t * NU + a] * p[t];
+      col[a] = acc;
+    }
+    for (int a = 0; a < m; ++a) {
+      double sacc = col[a];
+      for (int b = 0; b < a; ++b) sacc -= Lr[a * NU + b] * col[b];
+      col[a] = sacc * Lri[a];
+    }
+    for (int a = m - 1; a >= 0; --a) {
+      double sacc = col[a];
+      for (int b = a + 1; b < m; ++b) sacc -= Lr[b * NU + a] * col[b];
+      col[a] = sacc * Lri[a];
+    }
+    for (int a = 0; a < m; ++a) kff[k * NU + a] = -col[a];
+    for (int i = 0; i < NZ; ++i) {
+      double acc = 0.0;
+      if (i < NX)
+        for (int t = 0; t < NX; ++t) acc += Ak[t * NX + i] * p[t];
+      for (int a = 0; a < m; ++a) acc += St[a * NZ + i] * kff[k * NU + a];
+      p2[i] = acc;
+    }
+    memcpy(p, p2, sizeof(p));
+  }
+  memset(z, 0, sizeof(z));
+  for (int k = 0; k < N; ++k) {
+    const int m = r->nu[k];
+    const double* Ak = r->A + (size_t)k * NX * NX;
+    const double* Bt = r->Bt + (size_t)k * NZ * NU;
+    const double* Kf = r->Kf + (size_t)k * NU * NZ;
+    double v[NU];
+    for (int a = 0; a < m; ++a) {
+      double acc = kff[k * NU + a];
+      for (int j = 0; j < NZ; ++j) acc += Kf[a * NZ + j] * z[j];
+      v[a] = acc;
+      bvec[r->off[k] + a] = acc;
+    }
+    for (int i = 0; i < NZ; ++i) {
+      double acc = 0.0;
+      if (i < NX)
+        for (int t = 0; t < NX; ++t) acc += Ak[i * NX + t] * z[t];
+      for (int a = 0; a < m; ++a) acc += Bt[i * NU + a] * v[a];
+      z2[i] = acc;
+    }
+    memcpy(z, z2, sizeof(z));
+  }
+  free(kff);
+}
+
+int oracle_riccati_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                             const double* foot, const uint8_t* contact, double* u, int* iters) {
+  const int N = c->N, L = c->L;
+  memset(u, 0, sizeof(double) * N * NU);
+  if (iters) *iters = 0;
+  if (N > 63) return CMPC_TOO_LARGE;
+  double* fdes = (double*)malloc(sizeof(double) * N * L);
+  int st = fdes_and_check(c, contact, fdes);
+  if (st != CMPC_SUCCESS) {
+    free(fdes);
+    return st;
+  }
+  ric_ops_ctx r;
+  memset(&r, 0, sizeof(r));
+  r.c = c;
+  r.N = N;
+  r.x0 = x0;
+  r.xref = xref;
+  r.fdes = fdes;
+  double* A = (double*)malloc(sizeof(double) * N * NX * NX);
+  double* Bm = (double*)malloc(sizeof(double) * N * NX * NU);
+  oracle_srbd_dynamics(c, xref, foot, contact, A, Bm);
+  r.A = A;
+  r.B = Bm;
+  int n = 0;
+  for (int k = 0; k < N; ++k) {
+    r.off[k] = n;
+    r.nst[k] = 0;
+    for (int i = 0; i < L; ++i)
+      if (contact[k * L + i]) r.legs[k][r.nst[k]++] = i;
+    r.nu[k] = 3 * r.nst[k];
+    n += r.nu[k];
+  }
+  r.n = n;
+  double* mem = (double*)calloc((size_t)N * (NZ * NU * 3 + NU * NU + NU) + 2 * NZ * NZ, sizeof(double));
+  r.Bt = mem;
+  r.St = r.Bt + (size_t)N * NZ * NU;
+  r.Kf = r.St + (size_t)N * NU * NZ;
+  r.Lr = r.Kf + (size_t)N * NU * NZ;
+  r.Lri = r.Lr + (size_t)N * NU * NU;
+  r.P = r.Lri + (size_t)N * NU;
+  for (int k = 0; k < N; ++k) /* B~_k = [B_k S_k; S_k] */
+    for (int t = 0; t < r.nst[k]; ++t)
+      for (int d = 0; d < 3; ++d) {
+        const int a = 3 * t + d, j = 3 * r.legs[k][t] + d;
+        for (int i = 0; i < NX; ++i) r.Bt[(size_t)k * NZ * NU + i * NU + a] = Bm[(size_t)k * NX * NU + i * NU + j];
+        r.Bt[(size_t)k * NZ * NU + (NX + j) * NU + a] = 1.0;
+      }
+  const int nt = n / 3;
+  double* mu = (double*)malloc(sizeof(double) * (nt + 1));
+  double* lo = (double*)calloc(5 * (size_t)(nt + 1), sizeof(double));
+  double* hi = (double*)malloc(sizeof(double) * 5 * (nt + 1));
+  double* uc = (double*)calloc((size_t)n + 1, sizeof(double));
+  for (int k = 0, t = 0; k < N; ++k)
+    for (int q = 0; q < r.nst[k]; ++q, ++t) {
+      mu[t] = c->mu[r.legs[k][q]];
+      for (int j = 0; j < 5; ++j) hi[5 * t + j] = c->force_ub[j];
+    }
+  qp_ops ops = {&r, ric_grad, ric_factor, ric_solve};
+  cmpc_settings s2 = *s;
+  s2.warm_start = 0;
+  int it = 0;
+  st = qp_ipm_run(n, &ops, mu, lo, hi, &s2, uc, NULL, NULL, &it, NULL);
+  for (int k = 0; k < N; ++k)
+    for (int t = 0; t < r.nst[k]; ++t)
+      for (int d = 0; d < 3; ++d) u[(k * L + r.legs[k][t]) * 3 + d] = uc[r.off[k] + 3 * t + d];
+  if (iters) *iters = it;
+  free(fdes); free(A); free(Bm); free(mem); free(mu); free(lo); free(hi); free(uc);
+  return st;
+}
+
+typedef struct ric_job {
+  const oracle_consts* c;
+  const cmpc_settings* s;
+  int B, tid, nthreads;
+  const double *x0, *xref, *foot;
+  const uint8_t* contact;
+  double* u;
+  int *status, *iters;
+} ric_job;
+
+static void* ric_worker(void* arg) {
+  ric_job* j = (ric_job*)arg;
+  const int N = j->c->N, L = j->c->L;
+  for (int q = j->tid; q < j->B; q += j->nthreads) {
+    int it = 0;
+    const int st = oracle_riccati_solve_one(j->c, j->s, j->x0 + (size_t)q * NX, j->xref + (size_t)q * (N + 1) * NX,
+                                            j->foot + (size_t)q * (N + 1) * L * 3, j->contact + (size_t)q * N * L,
+                                            j->u + (size_t)q * N * NU, &it);
+    if (j->status) j->status[q] = st;
+    if (j->iters) j->iters[q] = it;
+  }
+  return NULL;
+}
+
+int oracle_riccati_solve_batch(const cmpc_model* m, const cmpc_settings* s, int B, const double* x0,
+                               const double* xref, const double* foot, const uint8_t* contact, double* u,
+                               int* status, int* iters, int nthreads) {
+  oracle_consts c;
+  oracle_consts_init(m, &c);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  ric_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; ++t) {
+    ric_job jb = {&c, s, B, t, nthreads, x0, xref, foot, contact, u, status, iters};
+    jobs[t] = jb;
+  }
+  if (nthreads == 1) {
+    ric_worker(&jobs[0]);
+    return 0;
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, ric_worker, &jobs[t]);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  return 0;
 }

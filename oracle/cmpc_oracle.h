@@ -125,6 +125,16 @@ int oracle_policy_triple(double mu, const double* ub, const double* f, double to
 int oracle_policy(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                   const double* u, double act_tol, double* K, int* n_free);
 
+
+/* The same QP solved without condensing, HPIPM-style: the shared Mehrotra IPM with its Newton systems solved by a
+ * Riccati recursion over the stages (state [x; u_prev], 25) and H u + g by rollout + adjoint. Cold start only.
+ * u [N][L][3] out. oracle_riccati_solve_batch: QP-major batch over nthreads pthreads. */
+int oracle_riccati_solve_one(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                             const double* foot, const uint8_t* contact, double* u, int* iters);
+int oracle_riccati_solve_batch(const cmpc_model* m, const cmpc_settings* s, int B, const double* x0,
+                               const double* xref, const double* foot, const uint8_t* contact, double* u,
+                               int* status, int* iters, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,7 @@ def lib():
         L.oracle_srbd_dynamics_lin.restype = None
         L.oracle_policy.argtypes = [C.c_void_p, d, d, u8, d, C.c_double, d, i]
         L.oracle_policy_triple.argtypes = [C.c_double, d, d, C.c_double, d]
+        L.oracle_riccati_solve_batch.argtypes = [P(Model), P(Settings), C.c_int, d, d, d, u8, d, i, i, C.c_int]
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         _lib = L
     return _lib
@@ -313,6 +314,20 @@ def gait_contact(gait, t_start, t0, dt, N, leg_map=None):
     lib().oracle_gait_contact(C.byref(gait), _p(lm, C.c_int) if lm is not None else None, t_start, t0, dt, N,
                               _p(out, C.c_uint8))
     return out
+
+
+def riccati_solve_batch(model, settings, x0, xref, foot, contact, nthreads=1):
+    """The QP solved HPIPM-style (no condensing, Riccati Newton steps): (u [B,N,L,3], status, iters)."""
+    B = x0.shape[0]
+    N = model.N
+    x0, xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    u = np.zeros((B, N, NL, 3))
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    lib().oracle_riccati_solve_batch(C.byref(model), C.byref(settings), B, _p(x0), _p(xref), _p(foot),
+                                     _p(contact, C.c_uint8), _p(u), _p(st, C.c_int), _p(it, C.c_int), nthreads)
+    return u, st, it
 
 
 def policy(model, xref, foot, contact, u, act_tol=1e-5):

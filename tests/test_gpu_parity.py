@@ -387,3 +387,20 @@ def test_cpp_centroidal_mpc_driver(cpp_bins):
             _, i, k, fx, fy, fz = line.split()
             u[int(k), int(i)] = [float(fx), float(fy), float(fz)]
     assert rel_err(u, z["u"][0]) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,gait", [(10, 0), (10, 1), (20, 0)])
+def test_device_matches_riccati_restatement(cm, op, N, gait):
+    """The device hot path (condensing + size-class IPM) against the HPIPM-style OCP restatement of the same QP
+    (oracle_riccati_solve_batch: no condensing, Riccati Newton steps): statuses equal, iterations within 1,
+    forces within the north star's 1e-5 (measured ~1e-15)."""
+    B = 128
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=gait)
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    u, _, st, it = eng.solve(x0, xref, foot, contact, want_x=False)
+    ur, sr, itr = op.riccati_solve_batch(mo, op.default_settings(), x0, xref, foot, contact, nthreads=8)
+    assert np.array_equal(st, sr) and np.all(st == 0)
+    assert np.abs(it - itr).max() <= 1
+    assert np.abs(u - ur).max() / max(1.0, np.abs(ur).max()) < 1e-9

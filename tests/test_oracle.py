@@ -220,3 +220,32 @@ def test_hpipm_riccati(op):
     x, u, st = op.ocp_solve(N, nx, nu, x0, rec)
     for k in range(N):
         assert np.allclose(u[2 * k:2 * k + 2], K[k] @ x[k] + kff[k], atol=1e-9)
+
+
+@pytest.mark.parametrize("N,gait,ub4,all_stance", [(10, 0, None, False), (10, 1, None, False), (10, 1, 15.0, False),
+                                                    (20, 0, None, False), (20, 0, 15.0, True), (6, 0, None, False)])
+def test_riccati_ipm_matches_condensed_ipm(op, N, gait, ub4, all_stance):
+    """The HPIPM-style restatement (no condensing: Riccati over [x; u_prev] stages, rollout/adjoint gradient) runs the
+    same Mehrotra iteration as the condensed oracle, so statuses and iteration counts agree exactly and the forces to
+    rounding: the condensing (H, g, swing elimination, force-rate coupling) is pinned against the OCP form HPIPM
+    solves for the reference (HpipmInterface.cpp:166-301)."""
+    m = op.default_model(N)
+    if ub4 is not None:
+        m.force_ub[4] = ub4
+    s = op.default_settings()
+    x0, xref, foot, contact = op.generate(m, 20221125, 64, gait=gait)
+    if all_stance:
+        contact[:] = 1
+    u, _, st, it = op.solve_batch(m, s, x0, xref, foot, contact, nthreads=8, want_x=False)
+    ur, sr, itr = op.riccati_solve_batch(m, s, x0, xref, foot, contact, nthreads=8)
+    assert np.array_equal(st, sr) and np.all(st == 0)
+    assert np.array_equal(it, itr)
+    assert np.abs(u - ur).max() / max(1.0, np.abs(u).max()) < 1e-12
+
+
+def test_riccati_ipm_invalid_contact(op):
+    m = op.default_model(10)
+    x0, xref, foot, contact = op.generate(m, 20221125, 2, gait=0)
+    contact[1, 4, :] = 0
+    ur, sr, _ = op.riccati_solve_batch(m, op.default_settings(), x0, xref, foot, contact)
+    assert sr[0] == 0 and sr[1] == 5 and np.all(ur[1] == 0.0)
