@@ -1850,3 +1850,61 @@ int oracle_riccati_solve_batch(const cmpc_model* m, const cmpc_settings* s, int 
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   return 0;
 }
+
+/* Stage-0 Riccati feedback of the unconstrained problem (Sigma = 0, no regularisation): rows of the stance forces of
+ * step 0, columns x0 (K0 [L][3][13], swing rows 0) — the matrix HPIPM's getRiccatiFeedback(0) returns for the
+ * reference's OCP (HpipmInterface.cpp:330-455, test retrieveRiccati testHpipmInterface.cpp:258-340) when no
+ * inequality is active; the condensed policy of oracle_policy must equal it on such a QP. */
+int oracle_riccati_gain0(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                         double* K0) {
+  const int N = c->N, L = c->L;
+  memset(K0, 0, sizeof(double) * NU * NX);
+  double* fdes = (double*)malloc(sizeof(double) * N * L);
+  int st = fdes_and_check(c, contact, fdes);
+  if (st != CMPC_SUCCESS) {
+    free(fdes);
+    return st;
+  }
+  ric_ops_ctx r;
+  memset(&r, 0, sizeof(r));
+  r.c = c;
+  r.N = N;
+  double* A = (double*)malloc(sizeof(double) * N * NX * NX);
+  double* Bm = (double*)malloc(sizeof(double) * N * NX * NU);
+  oracle_srbd_dynamics(c, xref, foot, contact, A, Bm);
+  r.A = A;
+  r.B = Bm;
+  int n = 0;
+  for (int k = 0; k < N; ++k) {
+    r.off[k] = n;
+    for (int i = 0; i < L; ++i)
+      if (contact[k * L + i]) r.legs[k][r.nst[k]++] = i;
+    r.nu[k] = 3 * r.nst[k];
+    n += r.nu[k];
+  }
+  double* mem = (double*)calloc((size_t)N * (NZ * NU * 3 + NU * NU + NU) + 2 * NZ * NZ, sizeof(double));
+  r.Bt = mem;
+  r.St = r.Bt + (size_t)N * NZ * NU;
+  r.Kf = r.St + (size_t)N * NU * NZ;
+  r.Lr = r.Kf + (size_t)N * NU * NZ;
+  r.Lri = r.Lr + (size_t)N * NU * NU;
+  r.P = r.Lri + (size_t)N * NU;
+  for (int k = 0; k < N; ++k)
+    for (int t = 0; t < r.nst[k]; ++t)
+      for (int d = 0; d < 3; ++d) {
+        const int a = 3 * t + d, j = 3 * r.legs[k][t] + d;
+        for (int i = 0; i < NX; ++i) r.Bt[(size_t)k * NZ * NU + i * NU + a] = Bm[(size_t)k * NX * NU + i * NU + j];
+        r.Bt[(size_t)k * NZ * NU + (NX + j) * NU + a] = 1.0;
+      }
+  const int nt = n / 3;
+  double* zero = (double*)calloc(5 * (size_t)(nt + 1), sizeof(double));
+  double* one = (double*)malloc(sizeof(double) * 5 * (nt + 1));
+  double* mu = (double*)calloc((size_t)nt + 1, sizeof(double));
+  for (int j = 0; j < 5 * (nt + 1); ++j) one[j] = 1.0;
+  st = ric_factor(&r, nt, mu, zero, zero, one, one, 0.0) == 0 ? CMPC_SUCCESS : CMPC_NAN_SOL;
+  for (int t = 0; t < r.nst[0]; ++t)
+    for (int d = 0; d < 3; ++d)
+      for (int j = 0; j < NX; ++j) K0[(3 * r.legs[0][t] + d) * NX + j] = r.Kf[(3 * t + d) * NZ + j];
+  free(fdes); free(A); free(Bm); free(mem); free(zero); free(one); free(mu);
+  return st;
+}

@@ -135,6 +135,10 @@ int oracle_riccati_solve_batch(const cmpc_model* m, const cmpc_settings* s, int 
                                const double* xref, const double* foot, const uint8_t* contact, double* u,
                                int* status, int* iters, int nthreads);
 
+/* Stage-0 Riccati feedback (unconstrained) of the OCP form: K0 [L][3][13] (HpipmInterface::getRiccatiFeedback(0)). */
+int oracle_riccati_gain0(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                         double* K0);
+
 #ifdef __cplusplus
 }
 #endif

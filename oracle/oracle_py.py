@@ -100,6 +100,7 @@ def lib():
         L.oracle_policy.argtypes = [C.c_void_p, d, d, u8, d, C.c_double, d, i]
         L.oracle_policy_triple.argtypes = [C.c_double, d, d, C.c_double, d]
         L.oracle_riccati_solve_batch.argtypes = [P(Model), P(Settings), C.c_int, d, d, d, u8, d, i, i, C.c_int]
+        L.oracle_riccati_gain0.argtypes = [C.c_void_p, d, d, u8, d]
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         _lib = L
     return _lib
@@ -328,6 +329,16 @@ def riccati_solve_batch(model, settings, x0, xref, foot, contact, nthreads=1):
     lib().oracle_riccati_solve_batch(C.byref(model), C.byref(settings), B, _p(x0), _p(xref), _p(foot),
                                      _p(contact, C.c_uint8), _p(u), _p(st, C.c_int), _p(it, C.c_int), nthreads)
     return u, st, it
+
+
+def riccati_gain0(model, xref, foot, contact):
+    """Unconstrained stage-0 Riccati feedback of the OCP form: (K0 [L,3,13], status)."""
+    c = consts(model)
+    K0 = np.zeros((NL, 3, NX))
+    xref, foot = (np.ascontiguousarray(a, dtype=np.float64) for a in (xref, foot))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    st = lib().oracle_riccati_gain0(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(K0))
+    return K0, st
 
 
 def policy(model, xref, foot, contact, u, act_tol=1e-5):

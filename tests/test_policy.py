@@ -132,3 +132,20 @@ def test_device_policy_invalid_contact(cm, op):
     K, nfree, st = eng.policy(x0, xref, foot, contact, u)
     assert st[1] == 5 and nfree[1] == 0 and np.all(K[1] == 0.0)
     assert st[0] == 0 and st[2] == 0 and nfree[0] > 0
+
+
+@pytest.mark.parametrize("N,gait", [(10, 0), (10, 1), (20, 0)])
+def test_oracle_policy_equals_riccati_feedback_when_unconstrained(op, N, gait):
+    """SURVEY §8c property: the condensed solution's sensitivity equals the Riccati u = K x + k of the OCP form.
+    On QPs with no active row (every slack >= 1 at the default bounds) the condensed policy's step-0 rows equal the
+    stage-0 Riccati feedback (HpipmInterface::getRiccatiFeedback(0), HpipmInterface.cpp:330-455) of the
+    unconstrained OCP."""
+    m = op.default_model(N)
+    x0, xref, foot, contact = op.generate(m, SEED, 4, gait=gait)
+    u, _, st, _ = op.solve_batch(m, op.default_settings(), x0, xref, foot, contact, nthreads=4, want_x=False)
+    for q in range(4):
+        K, nfree, pst = op.policy(m, xref[q], foot[q], contact[q], u[q])
+        assert pst == 0 and nfree == 3 * int(contact[q].sum())  # nothing active
+        K0, rst = op.riccati_gain0(m, xref[q], foot[q], contact[q])
+        assert rst == 0
+        assert np.abs(K[0] - K0).max() / max(1.0, np.abs(K0).max()) < 1e-9
