@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
   double* uw = dmalloc<double>((size_t)B * ld);
   unsigned long long* stamps = dmalloc<unsigned long long>((size_t)B * 9);
   CC(launch_pack_qp(H, g, mu, lo, hi, n, CMPC_F64, ld, Hw, gw, muw, low, hiw, nw, s0, B, st));
-  IpmArgs<double> a;
+  IpmArgs<double> a{};
   a.ld = ld;
   a.H = Hw;
   a.g = gw;
