@@ -63,6 +63,10 @@ struct IpmArgs {
   int warm;     // warm start (hpipm_interface::Settings::warm_start, HpipmInterfaceSettings.h:54): u from a.u
   DevSettings s;
   unsigned long long* stamps;  // diagnostic builds only (-DCMPC_IPM_STAMPS): per-QP phase cycles, else null
+  // per-class QP lists (k_class_lists), or null: size class c's kernel maps workgroup b < qcount[c] to QP
+  // qlist[c][b] and lets the rest exit, so a mixed batch dispatches the real QPs of a class first
+  const int* qlist[3];
+  const int* qcount;
 };
 
 // one size class of the workgroup condensing kernel: npad 128 (64 < n <= 128, or n <= 128 when n_lo = 0) or 256
@@ -142,6 +146,9 @@ int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, 
                      int ld, int N, void* u_ws, int B, hipStream_t stream);
 // receding-horizon shift of a solution: out[k] = in[min(k + shift, N - 1)] per QP
 int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, hipStream_t stream);
+
+// per-class QP lists after condensing: lists [3][B] (ascending QP ids), counts [3]; one workgroup
+int launch_class_lists(const int* status, const int* nvar, int B, int* lists, int* counts, hipStream_t stream);
 
 // widen/narrow helpers used by the test hooks
 int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream);

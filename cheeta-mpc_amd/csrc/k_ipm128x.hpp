@@ -160,7 +160,11 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   using namespace ipm128x;
   X_STAMP_DECL;
   constexpr int NP = 128;
-  const int q = blockIdx.x;
+  int q = blockIdx.x;
+  if (a.qlist[1]) {  // compacted class list: real QPs first, the surplus workgroups exit
+    if (q >= a.qcount[1]) return;
+    q = a.qlist[1][q];
+  }
   if (a.status[q] != CMPC_SUCCESS) return;
   const int n = a.nvar[q];
   if (n <= 64 || n > NP) return;  // served by another size class

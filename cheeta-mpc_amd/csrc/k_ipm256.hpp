@@ -152,7 +152,11 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
   constexpr int SL = NT + 1;       // tiles (slots) per wave
   static_assert(5 * (NP / 3) <= NTHR, "one thread per pyramid row");
 
-  const int q = blockIdx.x;
+  int q = blockIdx.x;
+  if (a.qlist[2]) {  // compacted class list: real QPs first, the surplus workgroups exit
+    if (q >= a.qcount[2]) return;
+    q = a.qlist[2][q];
+  }
   if (a.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
   const int n = a.nvar[q];
   if (n <= NP / 2 || n > NP) return;        // served by another size class

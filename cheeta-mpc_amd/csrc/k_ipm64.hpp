@@ -145,7 +145,11 @@ template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   using namespace ipm64;
   IPM_STAMP_DECL;
-  const int q = blockIdx.x;
+  int q = blockIdx.x;
+  if (A.qlist[0]) {  // compacted class list: real QPs first, the surplus workgroups exit
+    if (q >= A.qcount[0]) return;
+    q = A.qlist[0][q];
+  }
   if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
   const int n = A.nvar[q];
   if (n > 64) return;  // served by the 128 class

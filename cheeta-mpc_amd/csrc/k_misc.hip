@@ -192,6 +192,54 @@ int launch_expand(const ExpandArgs& a, int B, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// ------------------------------------------------------------------------------------------ size-class lists
+// One workgroup of 16 waves walks the batch in 1024-QP tiles: per class a wave ballot gives each QP its rank inside
+// the wave, wave totals through LDS give the tile offsets, so every list is in ascending QP order (deterministic).
+__global__ __launch_bounds__(1024) void k_class_lists(const int* status, const int* nvar, int B, int* lists,
+                                                      int* counts) {
+  __shared__ int s_wtot[3][16];
+  __shared__ int s_base[3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid < 3) s_base[tid] = 0;
+  __syncthreads();
+  for (int q0 = 0; q0 < B; q0 += 1024) {
+    const int q = q0 + tid;
+    int cls = -1;
+    if (q < B && status[q] == CMPC_SUCCESS) {
+      const int n = nvar[q];
+      cls = n <= 64 ? 0 : (n <= 128 ? 1 : 2);
+    }
+    int pre = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const unsigned long long mask = __ballot(cls == c);
+      if (cls == c) pre = __popcll(mask & below);
+      if (lane == 0) s_wtot[c][w] = __popcll(mask);
+    }
+    __syncthreads();
+    if (cls >= 0) {
+      int off = s_base[cls];
+      for (int v = 0; v < w; ++v) off += s_wtot[cls][v];
+      lists[(size_t)cls * B + off + pre] = q;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      int t = 0;
+      for (int v = 0; v < 16; ++v) t += s_wtot[tid][v];
+      s_base[tid] += t;
+    }
+    __syncthreads();
+  }
+  if (tid < 3) counts[tid] = s_base[tid];
+}
+
+int launch_class_lists(const int* status, const int* nvar, int B, int* lists, int* counts, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_class_lists, dim3(1), dim3(1024), 0, stream, status, nvar, B, lists, counts);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // ------------------------------------------------------------------------------------------ conversions
 __global__ void k_f32_to_f64(const float* in, double* out, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
