@@ -188,6 +188,8 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.nvar = c->nvar;
   a.status = c->status;
   a.n_lo = 0;
+  a.qlist = nullptr;
+  a.qcount = nullptr;
   return a;
 }
 
@@ -213,31 +215,43 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
 }
 
 // n <= 64 QPs go through the one-wave condensing kernel (possible only for N <= 21); the workgroup kernel serves
-// the 128 and 256 classes, each launch skipping at once what a smaller class already did (nvar hints).
+// the 128 and 256 classes. When the context holds more than one class, the first condensing kernel leaves
+// nvar[q] = n (0 if rejected) for every QP; k_class_lists turns those hints into per-class lists, so each bigger
+// class's kernel dispatches only its own QPs first, and the IPM reuses the same lists (*lists = true).
 template <typename T>
 int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                   const uint8_t* contact, hipStream_t st, const double* lin) {
+                   const uint8_t* contact, hipStream_t st, const double* lin, bool* lists) {
   CondenseArgs<T> a = condense_args<T>(c, x0, xref, foot, contact);
   a.lin = lin;
-  int r = 0;
+  *lists = false;
   const bool small = c->model.N <= CMPC_C64_MAXN;
-  if (small) r = launch_condense64<T>(a, B, st);
-  if (r == 0 && (c->ld > 64 || !small)) {
-    a.n_lo = small ? 64 : 0;
-    r = launch_srbd_condense<T>(a, c->ld >= 128 ? 128 : 64, B, st);
+  int r = small ? launch_condense64<T>(a, B, st) : 0;
+  if (r == 0 && !small) r = launch_srbd_condense<T>(a, 128, B, st);  // n_lo = 0: classes 64 and 128
+  if (r != 0 || c->ld < 128) return r;
+  if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
+  *lists = true;
+  if (small) {
+    a.n_lo = 64;
+    a.qlist = c->qlist + (size_t)1 * B;
+    a.qcount = c->qcount + 1;
+    r = launch_srbd_condense<T>(a, 128, B, st);
   }
   if (r == 0 && c->ld > 128) {
     a.n_lo = 128;
+    a.qlist = c->qlist + (size_t)2 * B;
+    a.qcount = c->qcount + 2;
     r = launch_srbd_condense<T>(a, 256, B, st);
   }
   return r;
 }
 
 int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                 const uint8_t* contact, hipStream_t st, const double* lin = nullptr) {
+                 const uint8_t* contact, hipStream_t st, const double* lin = nullptr, bool* lists = nullptr) {
+  bool dummy = false;
+  if (!lists) lists = &dummy;
   int r;
-  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin);
-  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin);
+  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin, lists);
+  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin, lists);
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 
@@ -248,10 +262,10 @@ int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const
 // the bigger classes concurrently on a forked side stream: +1.5 % on the mixed batch, -1.5..-2.5 % on the headline
 // (events and an empty launch on the critical path), so the classes run back to back.
 template <typename T>
-int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st) {
+int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, bool lists_ready) {
   if (B <= 0) return 0;
   if (c->ld < 128) return launch_ipm<T>(a, B, st);  // one class
-  if (launch_class_lists(a.status, a.nvar, B, c->qlist, c->qcount, st) != 0) return -2;
+  if (!lists_ready && launch_class_lists(a.status, a.nvar, B, 1, c->qlist, c->qcount, st) != 0) return -2;
   IpmArgs<T> al = a;
   for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
   al.qcount = c->qcount;
@@ -261,16 +275,17 @@ int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st) {
   return r;
 }
 
-int run_ipm(cmpc_ctx* c, int B, hipStream_t st, int warm = 0) {
+// lists_ready: the condensing of this call built the class lists (run_condense), else they are built here
+int run_ipm(cmpc_ctx* c, int B, hipStream_t st, int warm, bool lists_ready) {
   int r;
   if (c->precision == CMPC_F64) {
     IpmArgs<double> a = ipm_args<double>(c);
     a.warm = warm;
-    r = run_ipm_classes<double>(c, a, B, st);
+    r = run_ipm_classes<double>(c, a, B, st, lists_ready);
   } else {
     IpmArgs<float> a = ipm_args<float>(c);
     a.warm = warm;
-    r = run_ipm_classes<float>(c, a, B, st);
+    r = run_ipm_classes<float>(c, a, B, st, lists_ready);
   }
   return r == 0 ? CMPC_OK : CMPC_ERR_HIP;
 }
@@ -461,14 +476,15 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
   hipEvent_t* ev = nullptr;
   if (c->profiling && c->prof_calls < c->prof_max) ev = &c->prof_ev[(size_t)4 * c->prof_calls++];
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
-  int r = run_condense(c, B, x0, xref, foot, contact, st);
+  bool lists = false;
+  int r = run_condense(c, B, x0, xref, foot, contact, st, nullptr, &lists);
   if (r != CMPC_OK) return r;
   const int warm = (u_init && c->settings.warm_start != 0) ? 1 : 0;
   if (warm && launch_pack_warm(u_init, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B,
                                st) != 0)
     return CMPC_ERR_HIP;
   if (ev) HIP_OK(hipEventRecord(ev[1], st));
-  r = run_ipm(c, B, st, warm);
+  r = run_ipm(c, B, st, warm, lists);
   if (r != CMPC_OK) return r;
   if (ev) HIP_OK(hipEventRecord(ev[2], st));
   ExpandArgs e;
@@ -526,11 +542,12 @@ int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xre
   a.tol = sqp_tol;
   if (launch_sqp(0, a, B, st) != 0) return CMPC_ERR_HIP;
   for (int it = 0; it < sqp_iter_max; ++it) {
-    r = run_condense(c, B, x0, xref, foot, contact, st, c->lin);
+    bool lists = false;
+    r = run_condense(c, B, x0, xref, foot, contact, st, c->lin, &lists);
     if (r != CMPC_OK) return r;
     if (launch_pack_warm(c->uj, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B, st) != 0)
       return CMPC_ERR_HIP;
-    r = run_ipm(c, B, st, 1);
+    r = run_ipm(c, B, st, 1, lists);
     if (r != CMPC_OK) return r;
     ExpandArgs e;
     e.model = c->d_model;
@@ -698,7 +715,7 @@ int cmpc_qp_solve_batch(cmpc_ctx* c, int B, const double* H, const double* g, co
   if (launch_pack_qp(H, g, tri_mu, tri_lo, tri_hi, n, c->precision, c->ld, c->H, c->g, c->tri_mu, c->tri_lo,
                      c->tri_hi, c->nvar, c->status, B, st) != 0)
     return CMPC_ERR_HIP;
-  int r = run_ipm(c, B, st);
+  int r = run_ipm(c, B, st, 0, false);
   if (r != CMPC_OK) return r;
   const size_t nu = (size_t)B * c->ld;
   if (c->precision == CMPC_F64) {

@@ -46,6 +46,8 @@ struct CondenseArgs {
   int* status;
   int n_lo;       // k_srbd_condense serves n_lo < n <= NMAX; when n_lo > 0 a smaller class ran first and left
                   // nvar[q] = n for every QP, so QPs with nvar[q] <= n_lo exit before any work
+  const int* qlist;   // or null: workgroup b < *qcount serves QP qlist[b] (the class list of k_class_lists)
+  const int* qcount;
 };
 
 template <typename T>
@@ -147,8 +149,11 @@ int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, 
 // receding-horizon shift of a solution: out[k] = in[min(k + shift, N - 1)] per QP
 int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, hipStream_t stream);
 
-// per-class QP lists after condensing: lists [3][B] (ascending QP ids), counts [3]; one workgroup
-int launch_class_lists(const int* status, const int* nvar, int B, int* lists, int* counts, hipStream_t stream);
+// per-class QP lists: lists [3][B] (ascending QP ids), counts [3]; one workgroup. by_status != 0: QPs with
+// status == CMPC_SUCCESS, classed by nvar; by_status == 0: QPs with nvar > 0 (the condensing hints, written for every
+// QP by the first condensing kernel)
+int launch_class_lists(const int* status, const int* nvar, int B, int by_status, int* lists, int* counts,
+                       hipStream_t stream);
 
 // widen/narrow helpers used by the test hooks
 int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream);

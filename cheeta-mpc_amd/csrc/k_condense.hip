@@ -65,7 +65,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
   using acc_t = typename MF::acc_t;
 
   const DevModel* __restrict__ M = a.model;
-  const int q = blockIdx.x;
+  int q = blockIdx.x;
+  if (a.qlist) {  // class list: this class's QPs first, the surplus workgroups exit
+    if (q >= *a.qcount) return;
+    q = a.qlist[q];
+    if ((unsigned)q >= gridDim.x) return;  // grid = batch
+  }
   if (a.n_lo > 0 && a.nvar[q] <= a.n_lo) return;  // finished (or rejected) by a smaller class
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = M->N, L = NL;

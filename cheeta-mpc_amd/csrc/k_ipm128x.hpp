@@ -164,6 +164,7 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   if (a.qlist[1]) {  // compacted class list: real QPs first, the surplus workgroups exit
     if (q >= a.qcount[1]) return;
     q = a.qlist[1][q];
+    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
   if (a.status[q] != CMPC_SUCCESS) return;
   const int n = a.nvar[q];

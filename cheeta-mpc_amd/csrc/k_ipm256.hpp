@@ -156,6 +156,7 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
   if (a.qlist[2]) {  // compacted class list: real QPs first, the surplus workgroups exit
     if (q >= a.qcount[2]) return;
     q = a.qlist[2][q];
+    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
   if (a.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
   const int n = a.nvar[q];

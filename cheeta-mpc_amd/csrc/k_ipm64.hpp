@@ -149,6 +149,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   if (A.qlist[0]) {  // compacted class list: real QPs first, the surplus workgroups exit
     if (q >= A.qcount[0]) return;
     q = A.qlist[0][q];
+    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
   if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
   const int n = A.nvar[q];

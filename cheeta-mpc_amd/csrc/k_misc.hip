@@ -195,8 +195,8 @@ int launch_expand(const ExpandArgs& a, int B, hipStream_t stream) {
 // ------------------------------------------------------------------------------------------ size-class lists
 // One workgroup of 16 waves walks the batch in 1024-QP tiles: per class a wave ballot gives each QP its rank inside
 // the wave, wave totals through LDS give the tile offsets, so every list is in ascending QP order (deterministic).
-__global__ __launch_bounds__(1024) void k_class_lists(const int* status, const int* nvar, int B, int* lists,
-                                                      int* counts) {
+__global__ __launch_bounds__(1024) void k_class_lists(const int* status, const int* nvar, int B, int by_status,
+                                                      int* lists, int* counts) {
   __shared__ int s_wtot[3][16];
   __shared__ int s_base[3];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -205,9 +205,9 @@ __global__ __launch_bounds__(1024) void k_class_lists(const int* status, const i
   for (int q0 = 0; q0 < B; q0 += 1024) {
     const int q = q0 + tid;
     int cls = -1;
-    if (q < B && status[q] == CMPC_SUCCESS) {
+    if (q < B && (by_status ? status[q] == CMPC_SUCCESS : true)) {
       const int n = nvar[q];
-      cls = n <= 64 ? 0 : (n <= 128 ? 1 : 2);
+      if (by_status || n > 0) cls = n <= 64 ? 0 : (n <= 128 ? 1 : 2);
     }
     int pre = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -234,9 +234,10 @@ __global__ __launch_bounds__(1024) void k_class_lists(const int* status, const i
   if (tid < 3) counts[tid] = s_base[tid];
 }
 
-int launch_class_lists(const int* status, const int* nvar, int B, int* lists, int* counts, hipStream_t stream) {
+int launch_class_lists(const int* status, const int* nvar, int B, int by_status, int* lists, int* counts,
+                       hipStream_t stream) {
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_class_lists, dim3(1), dim3(1024), 0, stream, status, nvar, B, lists, counts);
+  hipLaunchKernelGGL(k_class_lists, dim3(1), dim3(1024), 0, stream, status, nvar, B, by_status, lists, counts);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
