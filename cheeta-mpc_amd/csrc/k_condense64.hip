@@ -55,8 +55,11 @@ struct Mf64<float> {
 
 template <typename T>
 struct C64Lds {
-  T g[16][64];       // Bqp_k rows (13 used)
-  T qg[16][64];      // Q_k Bqp_k rows
+  // Bqp_k rows 0..11 and Q_k Bqp_k rows 0..11: the MFMA contraction runs K = 12 (row 12, g_z, of Bqp is identically
+  // zero and unweighted); keeping the LDS block at 18 KB (fp64) lets 8 one-wave workgroups share a CU's 160 KB
+  // (at 22 KB with 16 staged rows only 7 fitted: 4096 QPs took three rounds of 1792 instead of two of 2048)
+  T g[12][64];
+  T qg[12][64];
   T tr[16][17];      // tile transpose (padded rows)
   double M[C64_MAXN][9];  // dt * I_b^-1 R_z(psi_k)^T (Theta rows of A_k)
   int tk[22], tleg[22];   // step and leg of each force triple
@@ -140,11 +143,6 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
     if (p >= 64) cnt = __popcll(b0) + __popcll(b1 & ((p - 64 >= 64) ? ~0ull : ((1ull << (p - 64)) - 1ull)));
     else cnt = __popcll(b0 & ((1ull << p) - 1ull));
     S.cb[lane] = 3 * cnt;
-  }
-  // rows 13..15 of the staging buffers stay zero (MFMA K padding)
-  for (int s = 13; s < 16; ++s) {
-    S.g[s][lane] = T(0);
-    S.qg[s][lane] = T(0);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
@@ -276,8 +274,10 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
       for (int s = 0; s < NX; ++s) {
         const double qd = M->qdiag[k][s];
         accg += gam[s] * S.w[s];
-        S.g[s][lane] = gam[s];
-        S.qg[s][lane] = T(qd) * gam[s];
+        if (s < 12) {
+          S.g[s][lane] = gam[s];
+          S.qg[s][lane] = T(qd) * gam[s];
+        }
       }
       gcol += accg;  // (c) g += Bqp_k' w_k
     }
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
     for (int I = 0; I < 4; ++I) {
       if (16 * I < ncols) {
         // K = 12: state row 12 (g_z) of Bqp is identically 0 (no input reaches it) and carries no weight
-        // (Qbar_k[12] = 0), rows 13..15 are padding -- the fourth K-slab would add exact zeros
+        // (Qbar_k[12] = 0) -- a fourth K-slab would add exact zeros
 #pragma unroll
         for (int kk = 0; kk < 3; ++kk) {
           const int s = 4 * kk + g4;
