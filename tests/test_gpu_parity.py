@@ -404,3 +404,24 @@ def test_device_matches_riccati_restatement(cm, op, N, gait):
     assert np.array_equal(st, sr) and np.all(st == 0)
     assert np.abs(it - itr).max() <= 1
     assert np.abs(u - ur).max() / max(1.0, np.abs(ur).max()) < 1e-9
+
+
+@pytest.mark.gpu
+def test_long_horizon_mixed_classes(cm, op):
+    """N = 25 (no one-wave condensing: the first workgroup condensing kernel serves n <= 128 and leaves hints, the class
+    lists then route 128 < n <= 256 to the 256 class): trot / bound (n = 150) solve and match the oracle, pronk
+    (n = 300 > 256) is TOO_LARGE, on one mixed batch."""
+    N, B = 25, 24
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=1)
+    n = 3 * contact.reshape(B, -1).sum(axis=1)
+    assert (n > 256).any() and ((n > 128) & (n <= 256)).any()
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    u, _, st, it = eng.solve(x0, xref, foot, contact, want_x=False)
+    assert np.all(st[n > 256] == 6) and np.all(u[n > 256] == 0)
+    ok = n <= 256
+    assert np.all(st[ok] == 0)
+    ur, _, sr, itr = op.solve_batch(mo, op.default_settings(), x0[ok], xref[ok], foot[ok], contact[ok], nthreads=8,
+                                    want_x=False)
+    assert np.all(sr == 0)
+    assert max(rel_err(a, b) for a, b in zip(u[ok], ur)) < 1e-6
