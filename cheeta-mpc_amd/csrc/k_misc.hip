@@ -201,14 +201,19 @@ __global__ __launch_bounds__(1024) void k_class_lists(const int* status, const i
   __shared__ int s_base[3];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid < 3) s_base[tid] = 0;
+  // the next tile's hints are requested before this tile's scans, so the loads overlap the barriers
+  int nv_next = tid < B ? nvar[tid] : 0;
+  int st_next = (by_status && tid < B) ? status[tid] : CMPC_SUCCESS;
   __syncthreads();
   for (int q0 = 0; q0 < B; q0 += 1024) {
     const int q = q0 + tid;
-    int cls = -1;
-    if (q < B && (by_status ? status[q] == CMPC_SUCCESS : true)) {
-      const int n = nvar[q];
-      if (by_status || n > 0) cls = n <= 64 ? 0 : (n <= 128 ? 1 : 2);
+    const int nv = nv_next, stv = st_next;
+    if (q + 1024 < B) {
+      nv_next = nvar[q + 1024];
+      if (by_status) st_next = status[q + 1024];
     }
+    int cls = -1;
+    if (q < B && stv == CMPC_SUCCESS && (by_status || nv > 0)) cls = nv <= 64 ? 0 : (nv <= 128 ? 1 : 2);
     int pre = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
