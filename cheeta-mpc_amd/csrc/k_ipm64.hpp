@@ -318,16 +318,24 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       dlu[cc] = -(L.rmu[j] + lu[cc] * dtu[cc]) * L.itu[j];
     }
   };
+  // fraction-to-boundary ratio: the smallest v / (-d) over the lane's eight candidates with d < 0 is selected by
+  // cross-multiplication (v, -d > 0) and divided once, instead of one IEEE division per candidate
   auto max_step = [&]() -> T {
-    T am = T(1e30);
+    T num = T(1e30), den = T(1);
+    auto cand = [&](T v, T d) {
+      if (d < T(0) && v * den < num * (-d)) {
+        num = v;
+        den = -d;
+      }
+    };
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
-      if (dtl[cc] < T(0)) am = fmin(am, -tl[cc] / dtl[cc]);
-      if (dtu[cc] < T(0)) am = fmin(am, -tu[cc] / dtu[cc]);
-      if (dll[cc] < T(0)) am = fmin(am, -ll[cc] / dll[cc]);
-      if (dlu[cc] < T(0)) am = fmin(am, -lu[cc] / dlu[cc]);
+      cand(tl[cc], dtl[cc]);
+      cand(tu[cc], dtu[cc]);
+      cand(ll[cc], dll[cc]);
+      cand(lu[cc], dlu[cc]);
     }
-    return wave_min_dpp(am);
+    return wave_min_dpp(num / den);
   };
 
   int status = CMPC_MAX_ITER;
