@@ -85,6 +85,43 @@ __device__ __forceinline__ float rsqrt_acc(float d) {
   return fmaf(0.5f * y, r, y);
 }
 
+// Lever-arm point of leg `leg` at a stance step k: the reference's foot_pos[leg] node k. A stance foot does not move
+// (foot_pos+ = foot_pos + (1 - e) foot_vel dt, CentroidalMPC.cpp:93), so one position holds over a stance run's nodes
+// s..e+1 (steps s..e in stance). Record node 0 is the current foot position (state[9+3i..], :288-291), to which the
+// reference pins foot_pos(:,0) (:165-167): a run that starts at step 0 stays there. A later run (touch-down after a
+// swing step) has a free position in the reference NLP; the QP freezes it at the minimiser of the foot tracking cost
+// w9..w20 (:218-221) under the pinning, the mean of des_foot_pos over nodes s..e+1, formed as p_s + sum (p_j - p_s)/cnt
+// so that a planted (constant) run returns p_s bit for bit. oracle_stance_point restates this operation for operation.
+// st(k, leg) -> stance flag of step k.
+template <typename StanceFn>
+__device__ __forceinline__ void stance_point(const double* foot, int N, int k, int leg, StanceFn st, double p[3]) {
+  int s = k;
+  while (s > 0 && st(s - 1, leg)) --s;
+  const double* ps = foot + (s * NL + leg) * 3;
+  p[0] = ps[0];
+  p[1] = ps[1];
+  p[2] = ps[2];
+  if (s == 0) return;
+  int e = k;
+  while (e + 1 < N && st(e + 1, leg)) ++e;
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+  for (int j = s + 1; j <= e + 1; ++j) {
+    const double* pj = foot + (j * NL + leg) * 3;
+    d0 += pj[0] - p[0];
+    d1 += pj[1] - p[1];
+    d2 += pj[2] - p[2];
+  }
+  const double cnt = (double)(e + 2 - s);
+  p[0] += d0 / cnt;
+  p[1] += d1 / cnt;
+  p[2] += d2 / cnt;
+}
+// Same, stance flags from one QP's contact record [N][NL].
+__device__ __forceinline__ void stance_point(const double* foot, const uint8_t* ct, int N, int k, int leg,
+                                             double p[3]) {
+  stance_point(foot, N, k, leg, [ct](int kk, int l) { return ct[kk * NL + l] != 0; }, p);
+}
+
 // Friction pyramid row rho of F(mu) applied to (fx, fy, fz)  (CentroidalMPC.cpp:186-190)
 template <typename T>
 __device__ __forceinline__ T pyr_row(int rho, T mu, T fx, T fy, T fz) {

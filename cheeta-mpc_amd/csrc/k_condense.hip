@@ -2,7 +2,8 @@
 // friction-pyramid stacking for a batch of centroidal MPC problems. One workgroup (WAVES wavefronts) per QP.
 //
 // Reference semantics (paths relative to the reference repo):
-//   dynamics  CentroidalMPC.cpp:85-92 forward Euler, lever arm linearised at r = p^des_{i,k} - c^ref_k
+//   dynamics  CentroidalMPC.cpp:85-92 forward Euler, lever arm linearised at r = p_{i,k} - c^ref_k, p the
+//             stance foot position of stance_point (cmpc_device.hpp: :93 pinning, node 0 = current foot :165-167)
 //   horizon   CentroidalMPC.cpp:159-176 multiple shooting -> condensed X = Aqp x0 + Bqp U
 //   cost      CentroidalMPC.cpp:203-231 -> H = Bqp' Qbar Bqp + Rbar, g = Bqp' Qbar (Aqp x0 - Xref) + rbar (A.3)
 //   f^des     CentroidalMPC.cpp:326-335 (m*9.81/n_stance, "mpc table invalid" when a step has no stance leg)
@@ -194,7 +195,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     }
     s_next[c] = nx;
     if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)s_ns[kc]));
-    const double* p = s_foot + (kc * L + leg) * 3;
+    double p[3];
+    stance_point(s_foot, N, kc, leg, [&](int k, int l) { return s_e[k * L + l] != 0; }, p);
     const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : s_xref + kc * NX;
     rx = p[0] - cb[0];
     ry = p[1] - cb[1];

@@ -2,7 +2,8 @@
 // SRBD linearisation, horizon propagation, dense condensing and friction-pyramid stacking. One wavefront per QP.
 //
 // Reference semantics (paths relative to the reference repo), identical to k_condense.hip:
-//   dynamics  CentroidalMPC.cpp:85-92 forward Euler, lever arm linearised at r = p^des_{i,k} - c^ref_k
+//   dynamics  CentroidalMPC.cpp:85-92 forward Euler, lever arm linearised at r = p_{i,k} - c^ref_k, p the
+//             stance foot position of stance_point (cmpc_device.hpp: :93 pinning, node 0 = current foot :165-167)
 //   horizon   CentroidalMPC.cpp:159-176 multiple shooting -> condensed X = Aqp x0 + Bqp U
 //   cost      CentroidalMPC.cpp:203-231 -> H = Bqp' Qbar Bqp + Rbar, g = Bqp' Qbar (Aqp x0 - Xref) + rbar (A.3)
 //   f^des     CentroidalMPC.cpp:326-335 (m*9.81/n_stance, "mpc table invalid" when a step has no stance leg)
@@ -178,7 +179,9 @@ __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
         pv = S.cb[kc - 1] + 3 * rank + d;
       }
       if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)__popc(sb)));
-      const double* p = a.foot + (((size_t)q * (N + 1) + kc) * L + leg) * 3;
+      double p[3];
+      stance_point(a.foot + (size_t)q * (N + 1) * L * 3, N, kc, leg,
+                   [&](int k, int l) { return ((stance_bits(k) >> l) & 1) != 0; }, p);
       const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : a.xref + ((size_t)q * (N + 1) + kc) * NX;
       rx = p[0] - cb[0];
       ry = p[1] - cb[1];

@@ -51,9 +51,9 @@ __global__ __launch_bounds__(256) void k_generate(GenArgs a, int B) {
   const uint64_t gid = (uint64_t)(a.qp_offset + q);
   const double nom[4][2] = {{0.35, 0.052}, {0.35, -0.054}, {-0.37, -0.053}, {-0.36, 0.054}};
   const double PI = 3.14159265358979323846;
-  double U[24];
+  double U[32];
 #pragma unroll
-  for (int i = 0; i < 24; ++i) U[i] = gen_uniform(a.seed, gid, i);
+  for (int i = 0; i < 32; ++i) U[i] = gen_uniform(a.seed, gid, i);
   double* X0 = a.x0 + (size_t)q * NX;
   double x0v[NX];
   x0v[0] = urange(-0.2, 0.2, U[0]);
@@ -69,6 +69,21 @@ __global__ __launch_bounds__(256) void k_generate(GenArgs a, int B) {
   x0v[12] = -GRAV;
   for (int s = 0; s < NX; ++s) X0[s] = x0v[s];
   const double vdx = urange(-1.0, 1.0, U[12]), vdy = urange(-1.0, 1.0, U[13]);
+  // contact schedule first: the stance runs decide where the feet are planted
+  const int h = GAIT_HALF_PERIOD;
+  const int phase = (int)(U[22] * (double)(2 * h));
+  const int gsel = a.gait == 1 ? (int)(U[23] * 3.0) : 0;
+  uint8_t* C = a.contact + (size_t)q * N * L;
+  for (int k = 0; k < N; ++k) {
+    const bool first = ((k + phase) % (2 * h)) < h;
+    for (int i = 0; i < L; ++i) {
+      bool e;
+      if (gsel == 0) e = first ? (i == 0 || i == 2) : (i == 1 || i == 3);  // trot (CentoidMPCTest.cpp:68-73)
+      else if (gsel == 1) e = first ? (i < 2) : (i >= 2);                    // bound
+      else e = true;                                                          // pronk, stance phase
+      C[k * L + i] = (uint8_t)e;
+    }
+  }
   double* XR = a.xref + (size_t)q * (N + 1) * NX;
   double* FT = a.foot + (size_t)q * (N + 1) * L * 3;
   for (int k = 0; k <= N; ++k) {
@@ -84,25 +99,28 @@ __global__ __launch_bounds__(256) void k_generate(GenArgs a, int B) {
     for (int d = 6; d < 11; ++d) xr[d] = 0.0;
     xr[11] = x0v[11];
     xr[12] = -GRAV;
+  }
+  // Feet: a node pinned by a stance run (step k or step k-1 in stance) holds the foothold planted at the run's
+  // touch-down step s, nominal offset + per-leg perturbation around c^ref_s; a swing node follows the body. Node 0
+  // is the measured current foot (cmpc.h record), the planted foothold plus a +-1 cm measurement offset.
+  for (int k = 0; k <= N; ++k) {
     for (int i = 0; i < L; ++i) {
+      const bool st_k = k < N && C[k * L + i], st_p = k > 0 && C[(k - 1) * L + i];
+      int s = k;
+      if (st_k || st_p) {
+        s = st_k ? k : k - 1;
+        while (s > 0 && C[(s - 1) * L + i]) --s;
+      }
+      const double ts = (double)s * a.dt;
+      const double cx = __builtin_fma(ts, vdx, x0v[0]), cy = __builtin_fma(ts, vdy, x0v[1]);
       double* p = FT + ((size_t)k * L + i) * 3;
       p[0] = (cx + nom[i & 3][0]) + urange(-0.03, 0.03, U[14 + 2 * (i & 3)]);
       p[1] = (cy + nom[i & 3][1]) + urange(-0.03, 0.03, U[15 + 2 * (i & 3)]);
       p[2] = 0.0;
-    }
-  }
-  const int h = GAIT_HALF_PERIOD;
-  const int phase = (int)(U[22] * (double)(2 * h));
-  const int gsel = a.gait == 1 ? (int)(U[23] * 3.0) : 0;
-  uint8_t* C = a.contact + (size_t)q * N * L;
-  for (int k = 0; k < N; ++k) {
-    const bool first = ((k + phase) % (2 * h)) < h;
-    for (int i = 0; i < L; ++i) {
-      bool e;
-      if (gsel == 0) e = first ? (i == 0 || i == 2) : (i == 1 || i == 3);  // trot (CentoidMPCTest.cpp:68-73)
-      else if (gsel == 1) e = first ? (i < 2) : (i >= 2);                    // bound
-      else e = true;                                                          // pronk, stance phase
-      C[k * L + i] = (uint8_t)e;
+      if (k == 0) {
+        p[0] += urange(-0.01, 0.01, U[24 + 2 * (i & 3)]);
+        p[1] += urange(-0.01, 0.01, U[25 + 2 * (i & 3)]);
+      }
     }
   }
 }
@@ -169,7 +187,8 @@ __device__ void expand_one(const ExpandArgs& a, int q) {
     for (int i = 0; i < L; ++i) {
       if (!ct[k * L + i]) continue;
       const double* f = uo + (k * L + i) * 3;
-      const double* p = ft + (k * L + i) * 3;
+      double p[3];
+      stance_point(ft, ct, N, k, i, p);
       const double rx = p[0] - xr[k * NX + 0], ry = p[1] - xr[k * NX + 1], rz = p[2] - xr[k * NX + 2];
       for (int d = 0; d < 3; ++d) xn[3 + d] += M->dt_over_m * f[d];
       xn[6] += dt * (ry * f[2] - rz * f[1]);

@@ -27,7 +27,7 @@ namespace {
 constexpr int PT = 256;  // threads per QP
 
 // Row-major A_k (13 x 13) into ab[0..168] and B_k (13 x 12) into ab[169..324] (no SQP linearisation term): the
-// forward-Euler SRBD map of CentroidalMPC.cpp:85-92 with the lever arm frozen at p^des_{k,i} - c^ref_k
+// forward-Euler SRBD map of CentroidalMPC.cpp:85-92 with the lever arm frozen at p_{k,i} - c^ref_k (p: stance_point)
 // (oracle_srbd_dynamics). Entry-parallel over the workgroup.
 __device__ void build_ab(const DevModel* M, const double* xr, const double* ft, const uint8_t* ct, int k,
                          double* ab) {
@@ -54,7 +54,8 @@ __device__ void build_ab(const DevModel* M, const double* xr, const double* ft, 
       if (ct[k * NL + i]) {
         if (r >= 3 && r < 6 && r - 3 == b) v = dt / M->mass;
         if (r >= 6 && r < 9) {
-          const double* p = ft + ((size_t)k * NL + i) * 3;
+          double p[3];
+          stance_point(ft, ct, M->N, k, i, p);
           const double* cb = xr + (size_t)k * NX;
           const double rx = p[0] - cb[0], ry = p[1] - cb[1], rz = p[2] - cb[2];
           const double S[9] = {0.0, -rz, ry, rz, 0.0, -rx, -ry, rx, 0.0};

@@ -53,7 +53,8 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
     for (int i = 0; i < NL; ++i) {
       if (!ct[k * NL + i]) continue;
       ++ns;
-      const double* p = foot + ((size_t)k * NL + i) * 3;
+      double p[3];
+      stance_point(foot, ct, N, k, i, p);
       const double* f = uk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
       F[0] += f[0];

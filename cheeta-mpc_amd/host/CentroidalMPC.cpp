@@ -71,7 +71,10 @@ void CentroidalMPC::PackRecord(const VectorXd& state, const VectorXd& des_state,
   for (int i = 0; i < L; ++i) {
     const size_t base = (size_t)i * (4 * N + 3);  // [contact_enable (N) | des_foot_pos 3x(N+1)] (:315-317)
     for (int k = 0; k < N; ++k) contact[(size_t)k * L + i] = des_inputs[base + k] > 0 ? 1 : 0;
-    for (int k = 0; k <= N; ++k)
+    // node 0: cur_foot_pos = state[9+3i..] (:288-291), to which the reference pins foot_pos(:,0) (:165-167); its
+    // des_foot_pos column only enters a constant tracking term. Nodes 1..N: des_foot_pos.
+    for (int d = 0; d < 3; ++d) foot[(size_t)i * 3 + d] = state[(size_t)(9 + 3 * i + d)];
+    for (int k = 1; k <= N; ++k)
       for (int d = 0; d < 3; ++d) foot[((size_t)k * L + i) * 3 + d] = des_inputs[base + N + 3 * k + d];
   }
 }

@@ -23,7 +23,12 @@
  * Per-QP record layouts (N = horizon, L = n_legs = 4):
  *   x0      [13]              = [c(3), v(3), L(3), Theta(3), g_z]        (c,v,L as CentroidalMPC.cpp:284-286)
  *   xref    [(N+1)][13]       node k = 0..N                              (des_state, CentroidalMPC.cpp:297-299, extended)
- *   foot    [(N+1)][L][3]     desired foot position p^des_{i,k}          (des_inputs, CentroidalMPC.cpp:316-317)
+ *   foot    [(N+1)][L][3]     node 0: current foot position p_i (state[9+3i..], CentroidalMPC.cpp:288-291);
+ *                             nodes 1..N: desired foot position p^des_{i,k} (des_inputs, :316-317). The reference
+ *                             pins foot_pos(:,0) to the current position (:165-167), so des_foot_pos node 0 only adds
+ *                             a constant and is not carried. Stance lever arms follow the reference's foot dynamics
+ *                             (a stance foot does not move, :93): a stance run from step 0 acts at node 0; a later
+ *                             run (nodes s..e+1, touch-down after a swing step) at the mean of p^des over its nodes.
  *   contact [N][L]  (uint8)   e_{i,k} in {0,1}                           (mpc_table, CentroidalMPC.cpp:315-335)
  *   u       [N][L][3]         world-frame contact forces (0 for swing legs)
  *   x       [(N+1)][13]       optional state rollout of the solution

@@ -5,7 +5,8 @@
  *   oracle_consts_init   weights indexing CentroidalMPC.cpp:203-231 (force weights w[9+3L+3i+c], rate w[9+6L+3i+c]),
  *                        CoM-z weight (w2/2)e^{-k}+w2/2 squared by sumsqr (:203-206, :210), force_ub :182-183.
  *   oracle_srbd_dynamics forward-Euler centroidal map CentroidalMPC.cpp:85-92 (gravity :70-73), bilinear lever arm
- *                        linearised at r = p^des - c^ref; Theta/g_z rows are the 13-state extension.
+ *                        linearised at r = p - c^ref, p = oracle_stance_point (:93 pinning, node 0 =
+ *                        current foot :165-167, :288-291); Theta/g_z rows are the 13-state extension.
  *   oracle_condense*     multiple shooting of CentroidalMPC.cpp:159-176 eliminated into Aqp/Bqp (App. A.3);
  *                        f^des_z = m*9.81/n_stance with the "mpc table invalid" check CentroidalMPC.cpp:326-335;
  *                        friction pyramid rows CentroidalMPC.cpp:179-201 (swing legs eliminated, App. A.4).
@@ -72,6 +73,42 @@ void oracle_consts_init(const cmpc_model* m, oracle_consts* c) {
   R[6] = a20 * id; R[7] = a21 * id; R[8] = a22 * id;
 }
 
+/* Stance foot position of leg i at step k (the reference's foot_pos[i] node k). A stance foot does not move
+ * (foot_pos+ = foot_pos + (1 - e) foot_vel dt, CentroidalMPC.cpp:93): one position holds over a stance run's nodes
+ * s..e+1. Record node 0 is the current foot position (state[9+3i..], :288-291), to which foot_pos(:,0) is pinned
+ * (:165-167), so a run starting at step 0 stays there. A later run (after a swing step) is frozen at the mean of
+ * des_foot_pos over nodes s..e+1 (minimiser of the w9..w20 foot tracking cost :218-221 under the pinning), formed as
+ * p_s + sum_j (p_j - p_s) / cnt. Same operations as the device's stance_point (cmpc_device.hpp). */
+void oracle_stance_point(const double* foot, const uint8_t* contact, int N, int L, int k, int i, double p[3]) {
+  int s = k;
+  while (s > 0 && contact[(s - 1) * L + i]) --s;
+  const double* ps = foot + ((size_t)s * L + i) * 3;
+  p[0] = ps[0];
+  p[1] = ps[1];
+  p[2] = ps[2];
+  if (s == 0) return;
+  int e = k;
+  while (e + 1 < N && contact[(e + 1) * L + i]) ++e;
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+  for (int j = s + 1; j <= e + 1; ++j) {
+    const double* pj = foot + ((size_t)j * L + i) * 3;
+    d0 += pj[0] - p[0];
+    d1 += pj[1] - p[1];
+    d2 += pj[2] - p[2];
+  }
+  const double cnt = (double)(e + 2 - s);
+  p[0] += d0 / cnt;
+  p[1] += d1 / cnt;
+  p[2] += d2 / cnt;
+}
+
+void oracle_stance_feet(int N, int L, const double* foot, const uint8_t* contact, double* out) {
+  memset(out, 0, sizeof(double) * (size_t)N * L * 3);
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < L; ++i)
+      if (contact[k * L + i]) oracle_stance_point(foot, contact, N, L, k, i, out + ((size_t)k * L + i) * 3);
+}
+
 void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                           double* A, double* B) {
   oracle_srbd_dynamics_lin(c, xref, foot, contact, NULL, A, B, NULL);
@@ -123,7 +160,8 @@ void oracle_srbd_dynamics_lin(const oracle_consts* c, const double* xref, const 
     const double* cb = lin ? lin + (size_t)k * 6 : xref + (size_t)k * NX;
     for (int i = 0; i < L; ++i) {
       if (!contact[k * L + i]) continue;
-      const double* p = foot + ((size_t)k * L + i) * 3;
+      double p[3];
+      oracle_stance_point(foot, contact, N, L, k, i, p);
       const double rx = p[0] - cb[0], ry = p[1] - cb[1], rz = p[2] - cb[2];
       const double S[9] = {0.0, -rz, ry, rz, 0.0, -rx, -ry, rx, 0.0};
       for (int d = 0; d < 3; ++d) Bk[(3 + d) * NU + 3 * i + d] = dt / c->mass;
@@ -793,8 +831,8 @@ void oracle_generate(const cmpc_model* m, uint64_t seed, int64_t qp_offset, int 
   const double PI = 3.14159265358979323846;
   for (int q = 0; q < B; ++q) {
     const uint64_t gid = (uint64_t)(qp_offset + q);
-    double U[24];
-    for (int i = 0; i < 24; ++i) U[i] = gen_uniform(seed, gid, i);
+    double U[32];
+    for (int i = 0; i < 32; ++i) U[i] = gen_uniform(seed, gid, i);
     double* X0 = x0 + (size_t)q * NX;
     X0[0] = urange(-0.2, 0.2, U[0]);
     X0[1] = urange(-0.2, 0.2, U[1]);
@@ -808,27 +846,6 @@ void oracle_generate(const cmpc_model* m, uint64_t seed, int64_t qp_offset, int 
     X0[11] = urange(-PI, PI, U[11]);
     X0[12] = -GRAV;
     const double vdx = urange(-1.0, 1.0, U[12]), vdy = urange(-1.0, 1.0, U[13]);
-    double* XR = xref + (size_t)q * (N + 1) * NX;
-    double* FT = foot + (size_t)q * (N + 1) * L * 3;
-    for (int k = 0; k <= N; ++k) {
-      double* xr = XR + k * NX;
-      const double tk = (double)k * m->dt;
-      xr[0] = fma(tk, vdx, X0[0]);
-      xr[1] = fma(tk, vdy, X0[1]);
-      xr[2] = 0.15;
-      xr[3] = vdx;
-      xr[4] = vdy;
-      xr[5] = 0.0;
-      for (int d = 6; d < 11; ++d) xr[d] = 0.0;
-      xr[11] = X0[11];
-      xr[12] = -GRAV;
-      for (int i = 0; i < L; ++i) {
-        double* p = FT + ((size_t)k * L + i) * 3;
-        p[0] = (xr[0] + kNomFoot[i & 3][0]) + urange(-0.03, 0.03, U[14 + 2 * (i & 3)]);
-        p[1] = (xr[1] + kNomFoot[i & 3][1]) + urange(-0.03, 0.03, U[15 + 2 * (i & 3)]);
-        p[2] = 0.0;
-      }
-    }
     const int h = GAIT_HALF_PERIOD;
     const int phase = (int)(U[22] * (double)(2 * h));
     int gsel = 0;
@@ -845,6 +862,43 @@ void oracle_generate(const cmpc_model* m, uint64_t seed, int64_t qp_offset, int 
         else /* pronk, stance phase: all legs */
           e = 1;
         C[k * L + i] = (uint8_t)e;
+      }
+    }
+    double* XR = xref + (size_t)q * (N + 1) * NX;
+    double* FT = foot + (size_t)q * (N + 1) * L * 3;
+    for (int k = 0; k <= N; ++k) {
+      double* xr = XR + k * NX;
+      const double tk = (double)k * m->dt;
+      xr[0] = fma(tk, vdx, X0[0]);
+      xr[1] = fma(tk, vdy, X0[1]);
+      xr[2] = 0.15;
+      xr[3] = vdx;
+      xr[4] = vdy;
+      xr[5] = 0.0;
+      for (int d = 6; d < 11; ++d) xr[d] = 0.0;
+      xr[11] = X0[11];
+      xr[12] = -GRAV;
+    }
+    /* planted feet: a node pinned by a stance run (step k or k-1 in stance) holds the foothold placed at the run's
+     * touch-down step s around c^ref_s; swing nodes follow the body; node 0 (current foot) adds a +-1 cm offset */
+    for (int k = 0; k <= N; ++k) {
+      for (int i = 0; i < L; ++i) {
+        const int st_k = k < N && C[k * L + i], st_p = k > 0 && C[(k - 1) * L + i];
+        int s = k;
+        if (st_k || st_p) {
+          s = st_k ? k : k - 1;
+          while (s > 0 && C[(s - 1) * L + i]) --s;
+        }
+        const double ts = (double)s * m->dt;
+        const double cx = fma(ts, vdx, X0[0]), cy = fma(ts, vdy, X0[1]);
+        double* p = FT + ((size_t)k * L + i) * 3;
+        p[0] = (cx + kNomFoot[i & 3][0]) + urange(-0.03, 0.03, U[14 + 2 * (i & 3)]);
+        p[1] = (cy + kNomFoot[i & 3][1]) + urange(-0.03, 0.03, U[15 + 2 * (i & 3)]);
+        p[2] = 0.0;
+        if (k == 0) {
+          p[0] += urange(-0.01, 0.01, U[24 + 2 * (i & 3)]);
+          p[1] += urange(-0.01, 0.01, U[25 + 2 * (i & 3)]);
+        }
       }
     }
   }
@@ -1185,7 +1239,8 @@ double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const d
     for (int i = 0; i < L; ++i) {
       if (!contact[k * L + i]) continue;
       ++ns;
-      const double* p = foot + ((size_t)k * L + i) * 3;
+      double p[3];
+      oracle_stance_point(foot, contact, N, L, k, i, p);
       const double* f = uk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
       F[0] += f[0];

@@ -35,6 +35,11 @@ typedef struct oracle_consts {
 
 void oracle_consts_init(const cmpc_model* m, oracle_consts* c);
 
+/* Stance foot position of leg i at stance step k (foot record [(N+1)][L][3]: node 0 = current foot, nodes 1..N =
+ * des_foot_pos; CentroidalMPC.cpp:93, :165-167, :288-291) and all of them: out [N][L][3] (0 for swing). */
+void oracle_stance_point(const double* foot, const uint8_t* contact, int N, int L, int k, int i, double p[3]);
+void oracle_stance_feet(int N, int L, const double* foot, const uint8_t* contact, double* out);
+
 /* SRBD linearisation (SURVEY App. A.2 from CentroidalMPC.cpp:41-100): A [N][13][13], B [N][13][12] row-major. */
 void oracle_srbd_dynamics(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                           double* A, double* B);

@@ -3,7 +3,8 @@
 TEST INFRASTRUCTURE ONLY. Written independently of oracle/cmpc_oracle.c (explicit Aqp/Bqp block products and a
 difference-operator force-rate term instead of recursions; a stacked-inequality IPM instead of the pyramid-structured
 one) so that the two cross-check each other. Follows:
-  CentroidalMPC.cpp:85-92   forward-Euler centroidal dynamics, lever arm linearised at p^des - c^ref
+  CentroidalMPC.cpp:85-92   forward-Euler centroidal dynamics, lever arm linearised at p - c^ref,
+                            p the stance foot position (:93 pinning; node 0 = current foot, :165-167, :288-291)
   CentroidalMPC.cpp:203-231 cost (CoM-z weight squared, force tracking, force-rate), x2 folded (App. A.3)
   CentroidalMPC.cpp:179-201 friction pyramid + force bounds; swing legs eliminated (App. A.4)
   CentroidalMPC.cpp:326-335 f^des_z = m*9.81/n_stance and the "mpc table invalid" rule
@@ -33,10 +34,35 @@ def skew(r):
     return np.array([[0, -r[2], r[1]], [r[2], 0, -r[0]], [-r[1], r[0], 0]])
 
 
+def stance_feet(foot, contact):
+    """Foot position behind every stance force, P[k, i] (CentroidalMPC.cpp:93: a stance foot does not move).
+
+    foot[0] is the current foot position (state[9+3i..], :288-291, pinned as foot_pos(:,0) by :165-167), foot[1..N]
+    is des_foot_pos. Each maximal stance run of a leg (steps s..e) holds one position over nodes s..e+1: foot[0] for a
+    run that starts at step 0, otherwise the mean of des_foot_pos over nodes s..e+1 (the tracking-cost minimiser).
+    Restated from run boundaries found with numpy diffs (independent of oracle_stance_point's scans).
+    """
+    N = contact.shape[0]
+    P = np.zeros((N, NL, 3))
+    for i in range(NL):
+        e = np.concatenate([[0], contact[:, i].astype(np.int64), [0]])
+        starts = np.flatnonzero(np.diff(e) == 1)      # first stance step of each run
+        ends = np.flatnonzero(np.diff(e) == -1) - 1    # last stance step of each run
+        for s0, e0 in zip(starts, ends):
+            if s0 == 0:
+                pos = foot[0, i]
+            else:
+                nodes = foot[s0:e0 + 2, i]
+                pos = nodes[0] + (nodes - nodes[0]).sum(axis=0) / len(nodes)
+            P[s0:e0 + 1, i] = pos
+    return P
+
+
 def dynamics(M, xref, foot, contact):
     N, dt, m = M["N"], M["dt"], M["m"]
     A = np.zeros((N, NX, NX))
     B = np.zeros((N, NX, NU))
+    P = stance_feet(foot, contact)
     for k in range(N):
         Ak = np.eye(NX)
         Ak[0:3, 3:6] = dt * np.eye(3)
@@ -48,7 +74,7 @@ def dynamics(M, xref, foot, contact):
         for i in range(NL):
             if contact[k, i]:
                 B[k, 3:6, 3 * i:3 * i + 3] = dt / m * np.eye(3)
-                B[k, 6:9, 3 * i:3 * i + 3] = dt * skew(foot[k, i] - xref[k, 0:3])
+                B[k, 6:9, 3 * i:3 * i + 3] = dt * skew(P[k, i] - xref[k, 0:3])
     return A, B
 
 
@@ -214,6 +240,7 @@ def centoid_test_inputs(N=6, literal_quirk=True):
         xref[k, 6:9] = blocks[2][kk]
         xref[k, 12] = -GRAV
         foot[k] = feet6[:, kk, :]
+    foot[0] = state[9:21].reshape(NL, 3)  # node 0 = cur_foot_pos from the state (CentroidalMPC.cpp:288-291)
     contact = np.zeros((N, NL), dtype=np.uint8)
     for k in range(N):
         contact[k] = table6[k % 6]

@@ -102,6 +102,8 @@ def lib():
         L.oracle_riccati_solve_batch.argtypes = [P(Model), P(Settings), C.c_int, d, d, d, u8, d, i, i, C.c_int]
         L.oracle_riccati_gain0.argtypes = [C.c_void_p, d, d, u8, d]
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
+        L.oracle_stance_feet.argtypes = [C.c_int, C.c_int, d, u8, d]
+        L.oracle_stance_feet.restype = None
         _lib = L
     return _lib
 
@@ -121,6 +123,16 @@ def consts(model):
     c = _Consts()
     L.oracle_consts_init(C.byref(model), C.byref(c))
     return c
+
+
+def stance_feet(foot, contact):
+    """Foot position behind every stance force [N][4][3] of one QP (oracle_stance_feet; 0 for swing)."""
+    foot = np.ascontiguousarray(foot, np.float64)
+    contact = np.ascontiguousarray(contact, np.uint8)
+    N = contact.shape[0]
+    out = np.zeros((N, NL, 3))
+    lib().oracle_stance_feet(N, NL, _p(foot), _p(contact, C.c_uint8), _p(out))
+    return out
 
 
 def generate(model, seed, B, gait=0, offset=0):

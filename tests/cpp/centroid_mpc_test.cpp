@@ -45,6 +45,16 @@ int main() {
     for (int k = 0; k < horizon; ++k)
       std::printf("force %d %d %.17g %.17g %.17g\n", i, k, f[(size_t)i * 3 * horizon + 3 * k],
                   f[(size_t)i * 3 * horizon + 3 * k + 1], f[(size_t)i * 3 * horizon + 3 * k + 2]);
+  // the current foot positions state[9..20] are an input (CentroidalMPC.cpp:288-291, pinned as foot_pos(:,0) by
+  // :165-167): move the rh foot (leg 2, in stance from step 0) 2 cm forward
+  std::vector<double> state2 = state;
+  state2[9 + 3 * 2] += 0.02;
+  const std::vector<double> f2 = mpc.UpdateMPC(state2, des_state, des_input);
+  std::printf("status2 %d\n", mpc.lastStatus());
+  for (int i = 0; i < num_legs; ++i)
+    for (int k = 0; k < horizon; ++k)
+      std::printf("force2 %d %d %.17g %.17g %.17g\n", i, k, f2[(size_t)i * 3 * horizon + 3 * k],
+                  f2[(size_t)i * 3 * horizon + 3 * k + 1], f2[(size_t)i * 3 * horizon + 3 * k + 2]);
   // "mpc table invalid" (CentroidalMPC.cpp:328-330)
   std::vector<double> bad = des_input;
   for (int i = 0; i < num_legs; ++i) bad[(size_t)i * (4 * horizon + 3) + 2] = 0;

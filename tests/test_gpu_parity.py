@@ -3,6 +3,8 @@
 Bars: bit-exact for the integer/byte work (input generator); fp64 contact forces within 1e-5 relative to
 max(|u_ref|_inf, 1) (north_star), checked far tighter in practice; fp32 within 2e-3 relative.
 """
+import pathlib
+
 import numpy as np
 import pytest
 
@@ -360,11 +362,11 @@ def test_riccati_not_pd_status(cm, op):
 
 
 @pytest.fixture(scope="module")
-def cpp_bins(tmp_path_factory, cm):
-    out = tmp_path_factory.mktemp("cppbin")
+def cpp_bins(cm):
+    """The C++ mirrors, prebuilt in-tree by __graft_entry__.build() (make is a no-op when they are current)."""
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp")
-    subprocess.check_call(["make", "-s", "-C", here, f"OUT={out}"])
-    return out
+    subprocess.check_call(["make", "-s", "-C", here])
+    return pathlib.Path(here) / "bin"
 
 
 def test_cpp_hpipm_interface_mirror(cpp_bins):
@@ -373,20 +375,29 @@ def test_cpp_hpipm_interface_mirror(cpp_bins):
     assert "PASSED" in r.stdout
 
 
-def test_cpp_centroidal_mpc_driver(cpp_bins):
+def test_cpp_centroidal_mpc_driver(cpp_bins, op):
     """CentoidMPCTest.cpp equivalent through the C++ CentroidalMPC mirror vs the numpy golden (literal quirk)."""
     r = subprocess.run([str(cpp_bins / "centroid_mpc_test")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "caught mpc table invalid" in r.stdout
     z = _load("centoid_mpc_test_N6")
     u = np.zeros((6, 4, 3))
+    u2 = np.zeros((6, 4, 3))
     for line in r.stdout.splitlines():
         if line.startswith("status"):
             assert line.split()[1] == "0"
         if line.startswith("force"):
-            _, i, k, fx, fy, fz = line.split()
-            u[int(k), int(i)] = [float(fx), float(fy), float(fz)]
+            tag, i, k, fx, fy, fz = line.split()
+            (u if tag == "force" else u2)[int(k), int(i)] = [float(fx), float(fy), float(fz)]
     assert rel_err(u, z["u"][0]) < 1e-6
+    # second call: state[9+6] (rh foot x) moved 2 cm -> the record's node 0 moves, U changes, oracle agrees
+    foot2 = z["foot"].copy()
+    foot2[0, 0, 2, 0] += 0.02
+    mo = op.default_model(6)
+    ur2, _, sr2, _ = op.solve_batch(mo, op.tight_settings(), z["x0"], z["xref"], foot2, z["contact"])
+    assert sr2[0] == 0
+    assert rel_err(u2, ur2[0]) < 1e-6
+    assert rel_err(u2, u) > 1e-4
 
 
 @pytest.mark.gpu
@@ -425,3 +436,34 @@ def test_long_horizon_mixed_classes(cm, op):
                                     want_x=False)
     assert np.all(sr == 0)
     assert max(rel_err(a, b) for a, b in zip(u[ok], ur)) < 1e-6
+
+
+@pytest.mark.parametrize("gait", [0, 1])
+def test_device_foot_semantics(cm, op, gait):
+    """Stance lever arms on the device follow the reference's foot dynamics (CentroidalMPC.cpp:93, :165-167,
+    :288-291) exactly as the oracle: moving the current feet (record node 0) moves U and the device tracks the oracle;
+    moving the des_foot_pos nodes of an initial stance run changes nothing, bit for bit; a later run acts at the mean
+    of its nodes (perturbed, non-planted feet) and still matches the oracle."""
+    N, B = 10, 64
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=gait)
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    H0, g0, n0, st0 = eng.condense(x0, xref, foot, contact)
+    f2 = foot.copy()
+    for q in range(B):
+        for i in range(4):
+            k = 0
+            while k < N and contact[q, k, i]:
+                k += 1
+            if k > 0:
+                f2[q, 1:k + 1, i, :2] += 0.05
+    H2, g2, n2, st2 = eng.condense(x0, xref, f2, contact)
+    assert np.array_equal(H2, H0) and np.array_equal(g2, g0)
+    rng = np.random.default_rng(3)
+    f1 = foot + rng.uniform(-0.02, 0.02, foot.shape) * np.array([1.0, 1.0, 0.0])  # every node moves: means matter
+    u1, _, s1, _ = eng.solve(x0, xref, f1, contact, want_x=False)
+    ur1, _, sr1, _ = op.solve_batch(mo, op.default_settings(), x0, xref, f1, contact, nthreads=8, want_x=False)
+    u0, _, _, _ = eng.solve(x0, xref, foot, contact, want_x=False)
+    assert np.array_equal(s1, sr1) and np.all(s1 == 0)
+    assert max(rel_err(u1[q], ur1[q]) for q in range(B)) < 1e-9
+    assert rel_err(u1, u0) > 1e-4

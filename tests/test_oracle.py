@@ -249,3 +249,64 @@ def test_riccati_ipm_invalid_contact(op):
     contact[1, 4, :] = 0
     ur, sr, _ = op.riccati_solve_batch(m, op.default_settings(), x0, xref, foot, contact)
     assert sr[0] == 0 and sr[1] == 5 and np.all(ur[1] == 0.0)
+
+
+def test_stance_feet_matches_numpy_restatement(op):
+    """oracle_stance_point (C scans) vs np_ref.stance_feet (numpy run boundaries) on random contact tables: the
+    reference's foot dynamics (CentroidalMPC.cpp:93) with foot_pos(:,0) pinned to the state's feet (:165-167)."""
+    import np_ref
+    rng = np.random.default_rng(5)
+    for N in (1, 2, 6, 10, 20):
+        for _ in range(40):
+            contact = (rng.random((N, 4)) < 0.6).astype(np.uint8)
+            foot = rng.normal(size=(N + 1, 4, 3))
+            P = op.stance_feet(foot, contact)
+            R = np_ref.stance_feet(foot, contact)
+            assert np.max(np.abs(P - R)) < 1e-14
+            for i in range(4):
+                run0 = 0
+                while run0 < N and contact[run0, i]:
+                    run0 += 1
+                # the initial stance run acts at the current foot position, bit for bit
+                assert np.array_equal(P[:run0, i], np.broadcast_to(foot[0, i], (run0, 3)))
+                assert np.all(P[contact[:, i] == 0, i] == 0.0)
+
+
+def test_planted_feet_are_exact(op):
+    """A stance run whose des_foot_pos is constant (the generator plants feet) acts at that foothold exactly."""
+    m = op.default_model(10)
+    x0, xref, foot, contact = op.generate(m, 20221125, 32, gait=1)
+    for q in range(32):
+        P = op.stance_feet(foot[q], contact[q])
+        for k in range(10):
+            for i in range(4):
+                if not contact[q, k, i]:
+                    continue
+                s = k
+                while s > 0 and contact[q, s - 1, i]:
+                    s -= 1
+                assert np.array_equal(P[k, i], foot[q, s, i])
+
+
+def test_current_foot_position_is_an_input(op):
+    """UpdateMPC's state[9..20] (CentroidalMPC.cpp:288-291) moves U; the des_foot_pos nodes of the initial stance run
+    do not (the reference pins those nodes to the current foot, :165-167 with :93)."""
+    m = op.default_model(10)
+    x0, xref, foot, contact = op.generate(m, 20221125, 4, gait=0)
+    s = op.tight_settings()
+    u0, _, st0, _ = op.solve_batch(m, s, x0, xref, foot, contact)
+    f1 = foot.copy()
+    f1[:, 0, :, 0] += 0.02  # current feet 2 cm forward
+    u1, _, st1, _ = op.solve_batch(m, s, x0, xref, f1, contact)
+    assert np.all(st0 == 0) and np.all(st1 == 0)
+    assert rel(u1, u0) > 1e-4
+    f2 = foot.copy()
+    for q in range(4):
+        for i in range(4):
+            k = 0
+            while k < 10 and contact[q, k, i]:
+                k += 1
+            if k > 0:  # initial stance run: nodes 1..k pinned to node 0 in the reference
+                f2[q, 1:k + 1, i, :2] += 0.05
+    u2, _, _, _ = op.solve_batch(m, s, x0, xref, f2, contact)
+    assert np.array_equal(u2, u0)
