@@ -36,12 +36,42 @@ def ipm_flops(n, iters):
     return it * (n ** 3 / 3.0 + 4.0 * n ** 2) + (it + 1.0) * 2.0 * n ** 2
 
 
+def condense_flops(contact):
+    """Algorithmic FLOPs of the condensing stage per QP: for every horizon node k = 1..N the dense
+    contraction of the 12 force-driven state rows, 2 * 12 * m_k^2 (Bqp_k' Q_k Bqp_k), and the propagation of the m_k
+    Bqp columns through the dense 13 x 13 A_k, 2 * 13 * 13 * m_k, where m_k = 3 x (stance leg-steps before node k)."""
+    m = 3 * np.cumsum(contact.reshape(contact.shape[0], contact.shape[1], -1).sum(axis=2), axis=1).astype(np.float64)
+    return (2.0 * 12.0 * m ** 2 + 2.0 * 13.0 * 13.0 * m).sum(axis=1)
+
+
+def cpu_share():
+    """(threads to use, how it was decided): the CPUs this process may run on (affinity), capped by the cgroup CPU
+    quota and by OMP_NUM_THREADS when the host declares its CPU share that way (the GPU box sets it to the box's
+    share of the machine's cores; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    why = f"affinity {n}"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            qc = max(1, int(float(q) / float(per)))
+            if qc < n:
+                n, why = qc, f"cgroup cpu.max {qc}"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, why = int(omp), f"OMP_NUM_THREADS {omp}"
+    return n, why
+
+
 def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_wall_s=5.0, riccati=False):
-    """The CPU oracle (same algorithm, fp64) on a bounded sample of the same batch, repeated until it has done about
-    min_cpu_s of thread-time (capped at max_wall_s wall): QPs/s = QPs solved / wall time. riccati=True times the
-    HPIPM-style restatement instead (no condensing; Riccati Newton steps over the stages, same iterates)."""
+    """The CPU oracle (same algorithm, fp64; the -O3 liboracle_fast.so build) on a bounded sample of the same batch,
+    repeated until it has done about min_cpu_s of thread-time (capped at max_wall_s wall): QPs/s = QPs solved / wall
+    time. riccati=True times the HPIPM-style restatement instead (no condensing; Riccati Newton steps over the stages,
+    same iterates)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as op  # test infrastructure: the CPU restatement, timed as the baseline
+    op.select_build("liboracle_fast.so")
     mo = op.default_model(model_n)
     s = op.default_settings()
     done, wall, u, st = 0, 0.0, None, None
@@ -58,16 +88,27 @@ def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_
     return u, st, wall, done
 
 
+def lib_md5():
+    import hashlib
+    import cheeta_mpc as cm
+    with open(cm.LIB_PATH, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
 def pmc_traffic(path, prefix):
-    """HBM bytes per launch of the IPM stage from the committed rocprofv3 --pmc summary (profiles/rNN_traffic.json,
-    written by cheeta-mpc_amd/tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes of this same
-    command). PMC counters cannot be read inside a normal run, so the value comes from the profiled run."""
+    """HBM bytes per launch of the kernels whose name contains `prefix`, from the committed rocprofv3 --pmc summary
+    of this workload (profiles/traffic_<workload key>.json, written by cheeta-mpc_amd/tools/pmc_traffic.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of this same bench command). PMC counters cannot be read inside a normal
+    run, so the value comes from the profiled run; it is reported only when the summary was taken on this exact
+    build of libcmpc.so (md5), else None with the reason."""
     if not path or not os.path.exists(path):
-        return None
+        return None, "no PMC summary for this workload"
     with open(path) as f:
-        ks = json.load(f)["kernels"]
-    tot = sum(v["hbm_bytes"] for k, v in ks.items() if prefix in k)
-    return tot if tot > 0 else None
+        doc = json.load(f)
+    if doc.get("lib_md5") and doc["lib_md5"] != lib_md5():
+        return None, f"PMC summary {os.path.basename(path)} was taken on another build of libcmpc.so"
+    tot = sum(v["hbm_bytes"] for k, v in doc["kernels"].items() if prefix in k)
+    return (tot if tot > 0 else None), os.path.basename(path)
 
 
 def main():
@@ -85,9 +126,9 @@ def main():
                     help="> 0: one step = the batched SQP on the bilinear NLP (cmpc_sqp_solve_batch), this many "
                          "SQP iterations at most; not the headline metric")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="QPs in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
-                    help="PMC summary giving roofline.traffic (used only for the default headline workload)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's CPU share (cpu_share())")
+    ap.add_argument("--traffic-json", default="",
+                    help="PMC summary giving roofline.traffic (default: profiles/traffic_<workload key>.json)")
     args = ap.parse_args()
 
     import cheeta_mpc as cm
@@ -150,6 +191,23 @@ def main():
     cm.lib().cmpc_profile_end(eng.ctx, *[C.byref(m) for m in ms], C.byref(ncalls))
     ms_cond, ms_ipm, ms_exp = (m.value / max(ncalls.value, 1) for m in ms)
 
+    # result gather beside the timed region ("xGMI only for result gather"): every rank writes its U
+    # shard into rank 0's buffer (IPC-mapped device-to-device copy; no collective). A failure is reported, not fatal.
+    gather = {"what": "U of every rank into rank 0's GPU (cmpc_ipc_open + cmpc_gather_shard), after the timed steps",
+              "bytes": world * B * N * 12 * 8, "ms": 0.0 if world == 1 else None}
+    if world > 1:
+        try:
+            from cheeta_mpc.shard import ResultGather
+            row = N * 12 * 8
+            rg = ResultGather(dist, world * B * row)
+            barrier()
+            tg = time.perf_counter()
+            rg.gather(u.ptr, rank * B * row, B * row, stream)
+            gather["ms"] = max_over_ranks(time.perf_counter() - tg) * 1e3
+            rg.close()
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            gather["error"] = repr(e)[:200]
+
     status = st.host()
     iters = it.host() if args.sqp_iters <= 0 else sqp_qi.host()
     ct = contact.host()
@@ -160,11 +218,21 @@ def main():
     achieved = flops_launch / (ms_ipm * 1e-3) if ms_ipm > 0 else 0.0
 
     headline = (B == 4096 and N == 10 and prec == cm.F64 and args.gait == 0 and not args.all_stance)
-    traffic = pmc_traffic(args.traffic_json, "k_ipm") if headline else None
+    wkey = (f"N{N}_B{B}_{'f64' if prec == cm.F64 else 'f32'}_"
+            f"{'allstance' if args.all_stance else ('trot' if args.gait == 0 else 'mixed')}")
+    tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{wkey}.json")
+    traffic, traffic_src = pmc_traffic(tpath, "k_ipm")
+    traffic_c, _ = pmc_traffic(tpath, "condense")
+    fl_cond = float(condense_flops(ct).sum())
+    achieved_c = fl_cond / (ms_cond * 1e-3) if ms_cond > 0 else 0.0
 
     value = world * B * args.steps / elapsed
     result = {
-        "metric": "centroidal QPs/sec (N=10, 13-state/12-input) at batch=4096; max|du| vs HPIPM",
+        # BASELINE.json's metric for the headline configuration; other workloads name their own N and batch.
+        # "vs HPIPM" is the metric's name: HPIPM cannot be built offline, so max_rel_du_vs_cpu_fp64 below is
+        # measured against the fp64 CPU oracle (oracle/cmpc_oracle.c) and HPIPM parity itself is unpinned.
+        "metric": ("centroidal QPs/sec (N=10, 13-state/12-input) at batch=4096; max|\u0394u| vs HPIPM" if headline else
+                   f"centroidal QPs/sec (N={N}, 13-state/12-input) at batch={B}; max|du| vs fp64 CPU oracle"),
         "value": value,
         "unit": "QPs/s",
         "n_gpus": world,
@@ -180,14 +248,20 @@ def main():
                                f"{'all-stance (pronk)' if args.all_stance else ('4-contact trot' if args.gait == 0 else 'mixed trot/bound/pronk')}, "
                                f"{'fp64' if prec == cm.F64 else 'fp32'}, full hot path per step",
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
-        # compute roof at the dtype's dense peak (the contract's "mfma" class); the arithmetic itself runs on the
-        # VALU, which on gfx950 issues fp64 at twice the rate of v_mfma_f64_16x16x4
-        "roofline": {"bound": "mfma", "compute_unit": "fp64 VALU" if prec == cm.F64 else "fp32 VALU",
+        # compute-bound on the vector ALU: the IPM's arithmetic runs on the fp64/fp32 VALU (on gfx950 the VALU issues
+        # fp64 at twice the rate of v_mfma_f64_16x16x4); peak = the dtype's vector datasheet peak
+        "roofline": {"bound": "valu", "compute_unit": "fp64 VALU" if prec == cm.F64 else "fp32 VALU",
                      "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)",
                      "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
-                     "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
+                     "traffic_source": traffic_src, "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
+        # the condensing stage's Bqp' Q Bqp contraction runs on MFMA (v_mfma_f64_16x16x4 / f32_16x16x4)
+        "roofline_condense": {"bound": "mfma", "kernel": "condensing stage (k_condense64 / k_srbd_condense)",
+                              "achieved": achieved_c / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
+                              "frac": achieved_c / peak, "traffic": traffic_c,
+                              "flops_per_launch": fl_cond, "ms_per_launch": ms_cond},
         "stages_ms": {"condense": ms_cond, "ipm": ms_ipm, "expand": ms_exp},
+        "gather_ms": gather["ms"], "gather": gather,
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,
                    "mean_n": float(nvar.mean())},
     }
@@ -201,7 +275,8 @@ def main():
 
     if rank == 0 and world == 1 and args.cpu_sample > 0 and args.sqp_iters <= 0:
         S = min(args.cpu_sample, B)
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        share, share_why = cpu_share()
+        threads = args.cpu_threads or share
         hx0, hxr, hft = x0.host()[:S], xref.host()[:S], foot.host()[:S]
         uc, stc, dtc, done = cpu_baseline(N, hx0, hxr, hft, ct[:S], threads)
         ug = u.host()[:S]
@@ -209,8 +284,10 @@ def main():
         rel = (np.abs(ug - uc).reshape(S, -1).max(axis=1) / scale)
         both = (stc == 0) & (status[:S] == 0)
         result["cpu_baseline"] = {"value": done / dtc, "unit": "QPs/s", "cores": threads, "kind": "port",
+                                  "host_cpus": os.cpu_count(), "cpu_share": f"{share} ({share_why})",
                                   "sample": f"first {S} QPs of the same batch x{done // S}, oracle/cmpc_oracle.c "
-                                            f"fp64 (same algorithm), {threads} pthreads, {dtc:.2f} s wall"}
+                                            f"fp64 (same algorithm) built -O3 -march=x86-64-v3 (liboracle_fast.so), "
+                                            f"{threads} pthreads, {dtc:.2f} s wall"}
         result["max_rel_du_vs_cpu_fp64"] = float(rel[both].max()) if both.any() else None
         ur, str_, dtr, doner = cpu_baseline(N, hx0, hxr, hft, ct[:S], threads, riccati=True)
         relr = np.abs(ug - ur).reshape(S, -1).max(axis=1) / np.maximum(1.0, np.abs(ur).reshape(S, -1).max(axis=1))

@@ -152,6 +152,13 @@ void derive_model(const cmpc_model& m, DevModel& d) {
   d.inv_inertia[8] = (I[0] * I[4] - I[1] * I[3]) * inv;
 }
 
+// hpipm_interface::Settings ranges (cmpc.h): modes 0..3, predictor-corrector only, positive tolerances.
+bool settings_ok(const cmpc_settings& s) {
+  return s.hpipm_mode >= 0 && s.hpipm_mode <= 3 && s.iter_max >= 0 && s.alpha_min > 0 && s.mu0 > 0 &&
+         s.tol_stat > 0 && s.tol_eq > 0 && s.tol_ineq > 0 && s.tol_comp > 0 && s.reg_prim >= 0 &&
+         (s.warm_start == 0 || s.warm_start == 1) && s.pred_corr == 1 && (s.ric_alg == 0 || s.ric_alg == 1);
+}
+
 bool model_ok(const cmpc_model* m) {
   return m && m->N >= 1 && m->N <= MAXN && m->n_legs == CMPC_MAX_LEGS && m->mass > 0 && m->dt > 0;
 }
@@ -326,7 +333,7 @@ extern "C" {
 
 void cmpc_settings_default(cmpc_settings* s) {
   if (!s) return;
-  s->hpipm_mode = 0;
+  s->hpipm_mode = 1;  // SPEED (HpipmInterfaceSettings.h:45)
   s->iter_max = 30;
   s->alpha_min = 1e-12;
   s->mu0 = 1e1;
@@ -367,7 +374,8 @@ size_t cmpc_memsize(const cmpc_model* model, int precision, int max_batch) {
 
 int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int precision, int max_batch, void* dev_mem,
                 cmpc_ctx** out) {
-  if (!out || !model_ok(model) || max_batch <= 0 || (precision != CMPC_F64 && precision != CMPC_F32))
+  if (!out || !model_ok(model) || max_batch <= 0 || (precision != CMPC_F64 && precision != CMPC_F32) ||
+      (settings && !settings_ok(*settings)))
     return CMPC_ERR_ARG;
   *out = nullptr;
   int ndev = 0;
@@ -440,7 +448,7 @@ int cmpc_destroy(cmpc_ctx* c) {
 }
 
 int cmpc_set_settings(cmpc_ctx* c, const cmpc_settings* s) {
-  if (!c || !s || s->iter_max < 0) return CMPC_ERR_ARG;
+  if (!c || !s || !settings_ok(*s)) return CMPC_ERR_ARG;
   c->settings = *s;
   return CMPC_OK;
 }
@@ -625,6 +633,38 @@ int cmpc_shift_inputs(int B, int N, const double* d_u, int shift, double* d_u_ou
   return launch_shift_inputs(d_u, N, shift, d_u_out, B, (hipStream_t)stream) == 0 ? CMPC_OK : CMPC_ERR_HIP;
 }
 
+static_assert(sizeof(cmpc_ipc_handle) == sizeof(hipIpcMemHandle_t), "IPC handle size");
+
+int cmpc_ipc_export(void* d_ptr, cmpc_ipc_handle* out) {
+  if (!d_ptr || !out) return CMPC_ERR_ARG;
+  hipIpcMemHandle_t h;
+  HIP_OK(hipIpcGetMemHandle(&h, d_ptr));
+  std::memcpy(out->bytes, &h, sizeof(h));
+  return CMPC_OK;
+}
+
+int cmpc_ipc_open(const cmpc_ipc_handle* handle, void** d_ptr) {
+  if (!handle || !d_ptr) return CMPC_ERR_ARG;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle->bytes, sizeof(h));
+  *d_ptr = nullptr;
+  HIP_OK(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+  return CMPC_OK;
+}
+
+int cmpc_ipc_close(void* d_ptr) {
+  if (!d_ptr) return CMPC_ERR_ARG;
+  HIP_OK(hipIpcCloseMemHandle(d_ptr));
+  return CMPC_OK;
+}
+
+int cmpc_gather_shard(void* d_dst, size_t dst_offset_bytes, const void* d_src, size_t bytes, void* stream) {
+  if (!d_dst || (!d_src && bytes > 0)) return CMPC_ERR_ARG;
+  if (bytes == 0) return CMPC_OK;
+  HIP_OK(hipMemcpyAsync((char*)d_dst + dst_offset_bytes, d_src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return CMPC_OK;
+}
+
 int cmpc_profile_begin(cmpc_ctx* c, int max_calls) {
   if (!c || max_calls <= 0) return CMPC_ERR_ARG;
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
@@ -747,44 +787,86 @@ size_t cmpc_ocp_record_size(int N, int nx, const int* nu) {
   return o;
 }
 
-int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
-                              double* u, int* status) {
+size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* nc) {
+  if (N <= 0 || nx <= 0 || !nu || !nc) return 0;
+  size_t o = 0;
+  for (int k = 0; k <= N; ++k) {
+    const size_t m = k < N ? (size_t)nu[k] : 0;
+    o += (size_t)nc[k] * (nx + m + 1);
+  }
+  return o;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Shared host path of cmpc_ocp_solve_batch_host / cmpc_ocp_solve_batch_eq_host (nc == nullptr: no constraints).
+int ocp_solve_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
+                   const double* crec, double* x, double* u, int* status) {
   if (B < 0 || N <= 0 || N > CMPC_OCP_MAX_N || nx <= 0 || nx > 64 || !nu || !x0 || !rec || !x || !u || !status)
     return CMPC_ERR_ARG;
+  if (nc && !crec) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
-  int nU = 0;
+  int nU = 0, nE = 0;
   for (int k = 0; k < N; ++k) {
     if (nu[k] < 0) return CMPC_ERR_ARG;
     nU += nu[k];
   }
+  if (nc)
+    for (int k = 0; k <= N; ++k) {
+      if (nc[k] < 0) return CMPC_ERR_ARG;
+      nE += nc[k];
+    }
   const int ldo = nU > 0 ? nU : 1;
   const size_t rs = cmpc_ocp_record_size(N, nx, nu);
+  const size_t crs = nE ? cmpc_ocp_constraint_record_size(N, nx, nu, nc) : 0;
   std::vector<size_t> offs = ocp_offsets(N, nx, nu);
+  std::vector<size_t> coffs(3 * (size_t)(N + 1), 0);
+  {
+    size_t o = 0;
+    for (int k = 0; k <= N && nE; ++k) {
+      const size_t m = k < N ? (size_t)nu[k] : 0;
+      coffs[(size_t)k] = o; o += (size_t)nc[k] * nx;
+      coffs[(size_t)(N + 1) + k] = o; o += (size_t)nc[k] * m;
+      coffs[2 * (size_t)(N + 1) + k] = o; o += (size_t)nc[k];
+    }
+  }
   std::vector<int> nuv(nu, nu + N);
   nuv.push_back(0);
-  int *d_nu = nullptr, *d_st = nullptr;
-  size_t* d_offs = nullptr;
+  int *d_nu = nullptr, *d_st = nullptr, *d_nc = nullptr;
+  size_t *d_offs = nullptr, *d_coffs = nullptr;
   double *d_x0 = nullptr, *d_rec = nullptr, *d_H = nullptr, *d_g = nullptr, *d_sc = nullptr, *d_x = nullptr,
-         *d_u = nullptr;
+         *d_u = nullptr, *d_crec = nullptr, *d_esc = nullptr;
   int r = CMPC_OK;
+  auto ck = [&r](hipError_t e) { if (e != hipSuccess) r = CMPC_ERR_HIP; };
   const size_t scr = 2 * (size_t)nx * ldo + 4 * (size_t)nx;
-  if (hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)) != hipSuccess ||
-      hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()) != hipSuccess ||
-      hipMalloc((void**)&d_x0, sizeof(double) * B * nx) != hipSuccess ||
-      hipMalloc((void**)&d_rec, sizeof(double) * B * rs) != hipSuccess ||
-      hipMalloc((void**)&d_H, sizeof(double) * B * ldo * ldo) != hipSuccess ||
-      hipMalloc((void**)&d_g, sizeof(double) * B * ldo) != hipSuccess ||
-      hipMalloc((void**)&d_sc, sizeof(double) * B * scr) != hipSuccess ||
-      hipMalloc((void**)&d_x, sizeof(double) * B * (N + 1) * nx) != hipSuccess ||
-      hipMalloc((void**)&d_u, sizeof(double) * B * ldo) != hipSuccess ||
-      hipMalloc((void**)&d_st, sizeof(int) * B) != hipSuccess) {
-    r = CMPC_ERR_HIP;
+  ck(hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)));
+  ck(hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()));
+  ck(hipMalloc((void**)&d_x0, sizeof(double) * B * nx));
+  ck(hipMalloc((void**)&d_rec, sizeof(double) * B * rs));
+  ck(hipMalloc((void**)&d_H, sizeof(double) * B * ldo * ldo));
+  ck(hipMalloc((void**)&d_g, sizeof(double) * B * ldo));
+  ck(hipMalloc((void**)&d_sc, sizeof(double) * B * scr));
+  ck(hipMalloc((void**)&d_x, sizeof(double) * B * (N + 1) * nx));
+  ck(hipMalloc((void**)&d_u, sizeof(double) * B * ldo));
+  ck(hipMalloc((void**)&d_st, sizeof(int) * B));
+  if (nE) {
+    ck(hipMalloc((void**)&d_nc, sizeof(int) * (N + 1)));
+    ck(hipMalloc((void**)&d_coffs, sizeof(size_t) * coffs.size()));
+    ck(hipMalloc((void**)&d_crec, sizeof(double) * B * crs));
+    ck(hipMalloc((void**)&d_esc, sizeof(double) * B * ocp_eq_scratch(nE, ldo)));
   }
   if (r == CMPC_OK) {
-    (void)hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_x0, x0, sizeof(double) * B * nx, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice);
+    ck(hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice));
+    ck(hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice));
+    ck(hipMemcpy(d_x0, x0, sizeof(double) * B * nx, hipMemcpyHostToDevice));
+    ck(hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice));
+    if (nE) {
+      ck(hipMemcpy(d_nc, nc, sizeof(int) * (N + 1), hipMemcpyHostToDevice));
+      ck(hipMemcpy(d_coffs, coffs.data(), sizeof(size_t) * coffs.size(), hipMemcpyHostToDevice));
+      ck(hipMemcpy(d_crec, crec, sizeof(double) * B * crs, hipMemcpyHostToDevice));
+    }
     OcpArgs a;
     a.N = N;
     a.nx = nx;
@@ -801,26 +883,42 @@ int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double*
     a.x = d_x;
     a.u = d_u;
     a.status = d_st;
-    if (launch_ocp_solve(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess) r = CMPC_ERR_HIP;
+    if (nE) {
+      a.nc = d_nc;
+      a.coffs = d_coffs;
+      a.crec_size = crs;
+      a.crec = d_crec;
+      a.nE = nE;
+      a.escratch = d_esc;
+    }
+    if (r == CMPC_OK && (launch_ocp_solve(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess)) r = CMPC_ERR_HIP;
     if (r == CMPC_OK) {
-      (void)hipMemcpy(x, d_x, sizeof(double) * B * (N + 1) * nx, hipMemcpyDeviceToHost);
+      ck(hipMemcpy(x, d_x, sizeof(double) * B * (N + 1) * nx, hipMemcpyDeviceToHost));
       if (nU > 0)
         for (int b = 0; b < B; ++b)
-          (void)hipMemcpy(u + (size_t)b * nU, d_u + (size_t)b * nU, sizeof(double) * nU, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost);
+          ck(hipMemcpy(u + (size_t)b * nU, d_u + (size_t)b * nU, sizeof(double) * nU, hipMemcpyDeviceToHost));
+      ck(hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost));
     }
   }
-  (void)hipFree(d_nu);
-  (void)hipFree(d_offs);
-  (void)hipFree(d_x0);
-  (void)hipFree(d_rec);
-  (void)hipFree(d_H);
-  (void)hipFree(d_g);
-  (void)hipFree(d_sc);
-  (void)hipFree(d_x);
-  (void)hipFree(d_u);
-  (void)hipFree(d_st);
+  for (void* pfree : {(void*)d_nu, (void*)d_offs, (void*)d_x0, (void*)d_rec, (void*)d_H, (void*)d_g, (void*)d_sc,
+                      (void*)d_x, (void*)d_u, (void*)d_st, (void*)d_nc, (void*)d_coffs, (void*)d_crec, (void*)d_esc})
+    if (pfree) (void)hipFree(pfree);
   return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
+                              double* u, int* status) {
+  return ocp_solve_host(B, N, nx, nu, nullptr, x0, rec, nullptr, x, u, status);
+}
+
+int cmpc_ocp_solve_batch_eq_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0,
+                                 const double* rec, const double* crec, double* x, double* u, int* status) {
+  if (!nc) return CMPC_ERR_ARG;
+  return ocp_solve_host(B, N, nx, nu, nc, x0, rec, crec, x, u, status);
 }
 
 int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const double* rec, double* Sm, double* sv,
@@ -845,6 +943,7 @@ int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const doubl
   size_t* d_offs = nullptr;
   double *d_rec = nullptr, *d_Sm = nullptr, *d_sv = nullptr, *d_K = nullptr, *d_k = nullptr, *d_sc = nullptr;
   int r = CMPC_OK;
+  auto ck = [&r](hipError_t e) { if (e != hipSuccess) r = CMPC_ERR_HIP; };
   if (hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)) != hipSuccess ||
       hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()) != hipSuccess ||
       hipMalloc((void**)&d_rec, sizeof(double) * B * rs) != hipSuccess ||
@@ -856,9 +955,9 @@ int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const doubl
       hipMalloc((void**)&d_st, sizeof(int) * B) != hipSuccess)
     r = CMPC_ERR_HIP;
   if (r == CMPC_OK) {
-    (void)hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice);
+    ck(hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice));
+    ck(hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice));
+    ck(hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice));
     RiccatiArgs a;
     a.N = N;
     a.nx = nx;
@@ -874,15 +973,16 @@ int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const doubl
     a.nK = (int)nK;
     a.nU = nU;
     a.status = d_st;
-    if (launch_ocp_riccati(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess) r = CMPC_ERR_HIP;
+    if (r == CMPC_OK && (launch_ocp_riccati(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess))
+      r = CMPC_ERR_HIP;
     if (r == CMPC_OK) {
-      (void)hipMemcpy(Sm, d_Sm, sizeof(double) * B * nSm, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(sv, d_sv, sizeof(double) * B * nsv, hipMemcpyDeviceToHost);
+      ck(hipMemcpy(Sm, d_Sm, sizeof(double) * B * nSm, hipMemcpyDeviceToHost));
+      ck(hipMemcpy(sv, d_sv, sizeof(double) * B * nsv, hipMemcpyDeviceToHost));
       if (nU > 0) {
-        (void)hipMemcpy(K, d_K, sizeof(double) * B * nK, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(kff, d_k, sizeof(double) * B * nU, hipMemcpyDeviceToHost);
+        ck(hipMemcpy(K, d_K, sizeof(double) * B * nK, hipMemcpyDeviceToHost));
+        ck(hipMemcpy(kff, d_k, sizeof(double) * B * nU, hipMemcpyDeviceToHost));
       }
-      (void)hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost);
+      ck(hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost));
     }
   }
   (void)hipFree(d_nu);

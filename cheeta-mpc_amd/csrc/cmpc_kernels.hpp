@@ -199,8 +199,19 @@ struct OcpArgs {
   double* x;           // [B][N+1][nx]
   double* u;           // [B][nU]
   int* status;
+  // equality constraints C_k x_k + D_k u_k + e_k = 0 (cmpc_ocp_solve_batch_eq_host); crec == nullptr: none
+  const int* nc = nullptr;        // device [N+1] rows per node
+  const size_t* coffs = nullptr;  // device [3][N+1] constraint-record offsets (C, D, e)
+  size_t crec_size = 0;
+  const double* crec = nullptr;   // [B][crec_size]
+  int nE = 0;                     // sum_k nc_k
+  double* escratch = nullptr;     // [B][ocp_eq_scratch(nE, ldo)]
 };
 #define CMPC_OCP_MAX_N 256
+// per-problem scratch of the equality-constrained solve: E [nE][ldo], W [ldo][nE+1], S [nE][nE], f, lam, drop [nE]
+__host__ __device__ inline size_t ocp_eq_scratch(int nE, int ldo) {
+  return (size_t)nE * ldo + (size_t)ldo * (nE + 1) + (size_t)nE * nE + 3 * (size_t)nE;
+}
 int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream);
 
 // Riccati recursion of the same OCP (HpipmInterface::getRiccati*, HpipmInterface.cpp:330-455)

@@ -26,6 +26,7 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
+#include "step_ratio.hpp"
 #include "wave_dpp.hpp"
 
 // In-kernel s_memtime stamps (wave 0's view), diagnostic builds only (-DCMPC_IPM_STAMPS; lab/run_lab.sh): per-QP
@@ -336,18 +337,13 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   // fraction-to-boundary ratio: the smallest v / (-d) over the thread's four candidates with d < 0 is selected by
   // cross-multiplication (v, -d > 0) and divided once (k_ipm64: the per-candidate IEEE divisions cost ~3 %)
   auto max_step = [&]() -> T {
-    T num = T(1e30), den = T(1);
-    auto cand = [&](T v, T d) {
-      if (d < T(0) && v * den < num * (-d)) {
-        num = v;
-        den = -d;
-      }
-    };
+    MinRatio<T> mr;
+    auto cand = [&](T v, T d) { mr.cand(v, d); };
     cand(tl, dtl);
     cand(tu, dtu);
     cand(ll, dll);
     cand(lu, dlu);
-    return block_min(num / den);
+    return block_min(mr.value());
   };
 
   for (it = 0;; ++it) {

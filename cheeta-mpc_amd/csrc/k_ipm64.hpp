@@ -35,6 +35,7 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
+#include "step_ratio.hpp"
 #include "dpp_rows.hpp"
 #include "wave_dpp.hpp"
 
@@ -321,13 +322,8 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   // fraction-to-boundary ratio: the smallest v / (-d) over the lane's eight candidates with d < 0 is selected by
   // cross-multiplication (v, -d > 0) and divided once, instead of one IEEE division per candidate
   auto max_step = [&]() -> T {
-    T num = T(1e30), den = T(1);
-    auto cand = [&](T v, T d) {
-      if (d < T(0) && v * den < num * (-d)) {
-        num = v;
-        den = -d;
-      }
-    };
+    MinRatio<T> mr;
+    auto cand = [&](T v, T d) { mr.cand(v, d); };
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
       cand(tl[cc], dtl[cc]);
@@ -335,7 +331,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
       cand(ll[cc], dll[cc]);
       cand(lu[cc], dlu[cc]);
     }
-    return wave_min_dpp(num / den);
+    return wave_min_dpp(mr.value());
   };
 
   int status = CMPC_MAX_ITER;

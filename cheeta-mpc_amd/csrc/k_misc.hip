@@ -288,9 +288,15 @@ int launch_convert_f64_to_f32(const double* in, float* out, size_t n, hipStream_
 }
 
 // ------------------------------------------------------------------------------------------ generic OCP-QP
-// HpipmInterface::Impl::solve semantics (HpipmInterface.cpp:166-301) for equality-free stages: x0 eliminated
-// (b0 = f0 + A0 x0, r0 += S0 x0, :177-208), condensed to U-space, Cholesky-solved, states rolled out, non-finite
-// solution -> NAN_SOL (:290-295). One 256-thread workgroup per problem; column-major stage matrices.
+// HpipmInterface::Impl::solve semantics (HpipmInterface.cpp:166-301): x0 eliminated (b0 = f0 + A0 x0, r0 += S0 x0,
+// :177-208), condensed to U-space, Cholesky-solved, states rolled out, non-finite solution -> NAN_SOL (:290-295).
+// Equality constraints C_k x_k + D_k u_k + e_k = 0 (the reference hands them to HPIPM as lg = ug = -e, :223-264, with
+// the stage-0 rows bounded by -e_0 - C_0 x0, :236-244) are condensed alongside the cost, row by row at their node:
+// E U = f with E = C_k dx_k/dU + D_k, f = -e_k - C_k x_k(U = 0). The KKT system [H E'; E 0] is solved by the
+// range-space method: H = L L', W = L^-1 E', S = W'W = M M' (pivots at or below 1e-12 of the largest diagonal drop
+// their row: redundant rows), lam from S lam = W'(-L^-1 g) - f, U = -L^-T (L^-1 g + W lam). Rows that stay violated
+// (|E U - f| above 1e-8 of the data scale: inconsistent constraints) -> INCONS_EQ. One 256-thread workgroup per
+// problem; column-major stage matrices.
 
 #define OCP_CM(M, ld, r, c) ((M)[(size_t)(c) * (ld) + (r)])
 
@@ -317,15 +323,28 @@ __global__ __launch_bounds__(256) void k_ocp_solve(OcpArgs a) {
   double* u = a.u + (size_t)q * nU;
   double* x = a.x + (size_t)q * (N + 1) * nx;
   __shared__ int s_cu[CMPC_OCP_MAX_N + 2];
+  __shared__ int s_ro[CMPC_OCP_MAX_N + 2];
   __shared__ int s_flag;
   __shared__ double s_l;
+  const int nE = a.crec ? a.nE : 0;
+  const double* crec = a.crec ? a.crec + (size_t)q * a.crec_size : nullptr;
+  double* E = nE ? a.escratch + (size_t)q * ocp_eq_scratch(nE, ldo) : nullptr;
+  double* W = nE ? E + (size_t)nE * ldo : nullptr;       // [ldo][nE + 1]: L^-1 E' and, in column nE, L^-1 g
+  double* Sm = nE ? W + (size_t)ldo * (nE + 1) : nullptr;  // [nE][nE]
+  double* fe = nE ? Sm + (size_t)nE * nE : nullptr;        // [nE]
+  double* lam = nE ? fe + nE : nullptr;                    // [nE]
+  double* drop = nE ? lam + nE : nullptr;                  // [nE] 1 for a dropped (redundant) row
   if (tid == 0) {
-    int c = 0;
+    int c = 0, r = 0;
     for (int k = 0; k < N; ++k) {
       s_cu[k] = c;
       c += a.nu[k];
     }
     s_cu[N] = c;
+    for (int k = 0; k <= N; ++k) {
+      s_ro[k] = r;
+      r += nE ? a.nc[k] : 0;
+    }
     s_flag = 0;
   }
   for (int i = tid; i < nU * nU; i += nth) H[(size_t)(i / nU) * ldo + i % nU] = 0.0;
@@ -341,6 +360,27 @@ __global__ __launch_bounds__(256) void k_ocp_solve(OcpArgs a) {
     const double* R = rec + oR[k];
     const double* qv = rec + oq[k];
     const double* rv = rec + orr[k];
+    if (nE && a.nc[k] > 0) {  // constraint rows of node k against x_k = G U + xb (G, xb not modified until below)
+      const int nck = a.nc[k], r0 = s_ro[k];
+      const double* Ck = crec + a.coffs[k];
+      const double* Dk = crec + a.coffs[(N + 1) + k];
+      const double* ek = crec + a.coffs[2 * (N + 1) + k];
+      for (int e = tid; e < nck * nU; e += nth) {
+        const int rr = e / nU, b = e % nU;
+        double v = 0.0;
+        if (b < c0) {
+          for (int j = 0; j < nx; ++j) v += OCP_CM(Ck, nck, rr, j) * G[(size_t)j * ldo + b];
+        } else if (b < c0 + m) {
+          v = OCP_CM(Dk, nck, rr, b - c0);
+        }
+        E[(size_t)(r0 + rr) * ldo + b] = v;
+      }
+      for (int rr = tid; rr < nck; rr += nth) {
+        double v = -ek[rr];
+        for (int j = 0; j < nx; ++j) v -= OCP_CM(Ck, nck, rr, j) * xb[j];
+        fe[r0 + rr] = v;
+      }
+    }
     if (k >= 1) {
       for (int i = tid; i < nx; i += nth) {
         double s = qv[i];
@@ -436,10 +476,98 @@ __global__ __launch_bounds__(256) void k_ocp_solve(OcpArgs a) {
     for (int i = k + 1 + tid; i < nU; i += nth) u[i] -= H[(size_t)i * ldo + k] * u[k];
     __syncthreads();
   }
+  if (nE) {
+    // W = L^-1 E' (one thread per constraint row); column nE is L^-1 (-g) = the forward-solved u above
+    for (int rr = tid; rr < nE; rr += nth) {
+      for (int i = 0; i < nU; ++i) {
+        double v = E[(size_t)rr * ldo + i];
+        for (int j = 0; j < i; ++j) v -= H[(size_t)i * ldo + j] * W[(size_t)j * (nE + 1) + rr];
+        W[(size_t)i * (nE + 1) + rr] = v / H[(size_t)i * ldo + i];
+      }
+    }
+    for (int i = tid; i < nU; i += nth) W[(size_t)i * (nE + 1) + nE] = u[i];
+    __syncthreads();
+    // S = W'W, rhs = W'(-L^-1 g) - f
+    for (int e = tid; e < nE * nE; e += nth) {
+      const int r1 = e / nE, r2 = e % nE;
+      double v = 0.0;
+      for (int i = 0; i < nU; ++i) v += W[(size_t)i * (nE + 1) + r1] * W[(size_t)i * (nE + 1) + r2];
+      Sm[e] = v;
+    }
+    for (int rr = tid; rr < nE; rr += nth) {
+      double v = -fe[rr];
+      for (int i = 0; i < nU; ++i) v += W[(size_t)i * (nE + 1) + rr] * W[(size_t)i * (nE + 1) + nE];
+      lam[rr] = v;
+      drop[rr] = 0.0;
+    }
+    __syncthreads();
+    // S = M M' (right-looking, lower); a pivot at or below 1e-12 of the largest diagonal drops its row (lam = 0)
+    if (tid == 0) {
+      double dmax = 0.0;
+      for (int r = 0; r < nE; ++r) dmax = fmax(dmax, Sm[(size_t)r * nE + r]);
+      s_l = dmax;
+    }
+    __syncthreads();
+    const double smin = 1e-12 * s_l;
+    for (int k = 0; k < nE; ++k) {
+      const double d = Sm[(size_t)k * nE + k];
+      const bool dr = !(d > smin);
+      if (tid == 0) {
+        drop[k] = dr ? 1.0 : 0.0;
+        Sm[(size_t)k * nE + k] = dr ? 1.0 : sqrt(d);
+      }
+      __syncthreads();
+      const double l = Sm[(size_t)k * nE + k];
+      for (int i = k + 1 + tid; i < nE; i += nth) Sm[(size_t)i * nE + k] = dr ? 0.0 : Sm[(size_t)i * nE + k] / l;
+      __syncthreads();
+      const int rem = nE - k - 1;
+      for (int e = tid; e < rem * rem; e += nth) {
+        const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+        if (j <= i) Sm[(size_t)i * nE + j] -= Sm[(size_t)i * nE + k] * Sm[(size_t)j * nE + k];
+      }
+      __syncthreads();
+    }
+    // lam = S^-1 rhs with the dropped rows held at 0 (serial sweeps; nE is small on this path)
+    if (tid == 0) {
+      for (int k = 0; k < nE; ++k) {
+        double v = drop[k] != 0.0 ? 0.0 : lam[k];
+        for (int j = 0; j < k; ++j) v -= Sm[(size_t)k * nE + j] * lam[j];
+        lam[k] = drop[k] != 0.0 ? 0.0 : v / Sm[(size_t)k * nE + k];
+      }
+      for (int k = nE - 1; k >= 0; --k) {
+        double v = lam[k];
+        for (int j = k + 1; j < nE; ++j) v -= Sm[(size_t)j * nE + k] * lam[j];
+        lam[k] = drop[k] != 0.0 ? 0.0 : v / Sm[(size_t)k * nE + k];
+      }
+    }
+    __syncthreads();
+    // forward part of U: -L^-1 g - W lam
+    for (int i = tid; i < nU; i += nth) {
+      double v = u[i];
+      for (int rr = 0; rr < nE; ++rr) v -= W[(size_t)i * (nE + 1) + rr] * lam[rr];
+      u[i] = v;
+    }
+    __syncthreads();
+  }
   for (int k = nU - 1; k >= 0; --k) {
     if (tid == 0) u[k] /= H[(size_t)k * ldo + k];
     __syncthreads();
     for (int i = tid; i < k; i += nth) u[i] -= H[(size_t)k * ldo + i] * u[k];
+    __syncthreads();
+  }
+  if (nE) {  // consistency: E U = f to 1e-8 of the data scale, else the rows are inconsistent (HPIPM's INCONS_EQ)
+    if (tid == 0) {
+      double worst = 0.0;
+      for (int rr = 0; rr < nE; ++rr) {
+        double v = -fe[rr], sc = fabs(fe[rr]);
+        for (int i = 0; i < nU; ++i) {
+          v += E[(size_t)rr * ldo + i] * u[i];
+          sc = fmax(sc, fabs(E[(size_t)rr * ldo + i] * u[i]));
+        }
+        worst = fmax(worst, fabs(v) / (1.0 + sc));
+      }
+      if (!(worst <= 1e-8) && s_flag == 0) s_flag = 2;
+    }
     __syncthreads();
   }
   // rollout x_{k+1} = A_k x_k + B_k u_k + b_k (x_0 = x0, HpipmInterface.cpp:303-315)
@@ -459,7 +587,7 @@ __global__ __launch_bounds__(256) void k_ocp_solve(OcpArgs a) {
     __syncthreads();
   }
   if (tid == 0) {
-    int st = s_flag ? CMPC_NAN_SOL : CMPC_SUCCESS;
+    int st = s_flag == 1 ? CMPC_NAN_SOL : (s_flag == 2 ? CMPC_INCONS_EQ : CMPC_SUCCESS);
     for (int i = 0; i < nU; ++i)
       if (!isfinite(u[i])) st = CMPC_NAN_SOL;
     for (int i = 0; i < (N + 1) * nx; ++i)

@@ -43,6 +43,11 @@ class Settings(C.Structure):
 GAIT_MAX_MODES = 16
 
 
+class IpcHandle(C.Structure):
+    """cmpc_ipc_handle (hipIpcMemHandle_t bytes)."""
+    _fields_ = [("bytes", C.c_ubyte * 64)]
+
+
 class Gait(C.Structure):
     """cmpc_gait: ocs2 ModeSequenceTemplate (gait.info modeSequence + switchingTimes)."""
     _fields_ = [("n_modes", C.c_int), ("mode", C.c_int * GAIT_MAX_MODES),
@@ -87,11 +92,18 @@ def lib():
     L.cmpc_ocp_record_size.argtypes = [C.c_int, C.c_int, i]
     L.cmpc_ocp_record_size.restype = C.c_size_t
     L.cmpc_ocp_solve_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, i]
+    L.cmpc_ocp_constraint_record_size.argtypes = [C.c_int, C.c_int, i, i]
+    L.cmpc_ocp_constraint_record_size.restype = C.c_size_t
+    L.cmpc_ocp_solve_batch_eq_host.argtypes = [C.c_int, C.c_int, C.c_int, i, i, d, d, d, d, d, i]
     L.cmpc_gait_builtin.argtypes = [C.c_char_p, P(Gait)]
     L.cmpc_gait_table_create.argtypes = [P(Gait), C.c_int, i, P(vp)]
     L.cmpc_gait_table_destroy.argtypes = [vp]
     L.cmpc_gait_contact_batch.argtypes = [vp, C.c_int, i, d, C.c_double, C.c_double, C.c_int, u8, vp]
     L.cmpc_ocp_riccati_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, d, i]
+    L.cmpc_ipc_export.argtypes = [vp, P(IpcHandle)]
+    L.cmpc_ipc_open.argtypes = [P(IpcHandle), P(vp)]
+    L.cmpc_ipc_close.argtypes = [vp]
+    L.cmpc_gather_shard.argtypes = [vp, C.c_size_t, vp, C.c_size_t, vp]
     L.cmpc_status_string.argtypes = [C.c_int]
     L.cmpc_status_string.restype = C.c_char_p
     L.cmpc_error_string.argtypes = [C.c_int]
@@ -335,6 +347,25 @@ def ocp_solve(N, nx, nu, x0, rec):
     vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     _chk(lib().cmpc_ocp_solve_batch_host(B, N, nx, vp(nua), vp(x0), vp(rec), vp(x), vp(u), vp(st)),
          "cmpc_ocp_solve_batch_host")
+    return x, u[:, :nU], st
+
+
+def ocp_solve_eq(N, nx, nu, nc, x0, rec, crec):
+    """ocp_solve with equality constraints C_k x_k + D_k u_k + e_k = 0 (nc_k rows at node k = 0..N); crec [B,record]
+    as cmpc_ocp_constraint_record_size (cmpc.h)."""
+    x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)
+    rec = np.ascontiguousarray(np.atleast_2d(rec), np.float64)
+    crec = np.ascontiguousarray(np.atleast_2d(crec), np.float64)
+    B = x0.shape[0]
+    nua = np.ascontiguousarray(nu, np.int32)
+    nca = np.ascontiguousarray(nc, np.int32)
+    nU = int(nua.sum())
+    x = np.zeros((B, N + 1, nx))
+    u = np.zeros((B, max(nU, 1)))
+    st = np.zeros(B, np.int32)
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _chk(lib().cmpc_ocp_solve_batch_eq_host(B, N, nx, vp(nua), vp(nca), vp(x0), vp(rec), vp(crec), vp(x), vp(u),
+                                            vp(st)), "cmpc_ocp_solve_batch_eq_host")
     return x, u[:, :nU], st
 
 

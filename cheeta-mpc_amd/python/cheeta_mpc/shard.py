@@ -1,7 +1,10 @@
 """Multi-GPU sharding of a QP batch: one process per GPU, contiguous QP-id ranges, no data-path
 collective. The counter-based generator keys every QP's inputs by its global id, so a QP's inputs and solution are
-the same whatever the number of ranks; torch.distributed (gloo) is used only for barriers and the max-over-ranks
-time."""
+the same whatever the number of ranks; torch.distributed (gloo) is used only for barriers, the max-over-ranks time
+and exchanging the 64-byte IPC handle of the result buffer. Results reach rank 0's GPU through ResultGather: each
+rank writes its shard into rank 0's buffer with one device-to-device copy (xGMI peer write across GPUs, dmabuf IPC
+mapping), so no collective and no reduction runs on the data path."""
+import ctypes as C
 import os
 
 
@@ -56,3 +59,51 @@ class Dist:
     def close(self):
         if self._d and self._d.is_initialized():
             self._d.destroy_process_group()
+
+
+class ResultGather:
+    """Rank 0's gathered result buffer ([total_bytes] on rank 0's device), mapped into every rank's address space once
+    (cmpc_ipc_export / cmpc_ipc_open, include/cmpc/cmpc.h) and reused for every gather. gather() copies this rank's
+    shard to its byte offset with cmpc_gather_shard on `stream`, waits for it, then meets the other ranks at a
+    barrier, after which rank 0's buffer holds every shard."""
+
+    def __init__(self, dist, total_bytes):
+        import cheeta_mpc as cm
+        self.cm, self.dist, self.total = cm, dist, int(total_bytes)
+        self.buf = None
+        self.dst = C.c_void_p()
+        self.mapped = False
+        if dist.rank == 0:
+            self.buf = cm.DeviceArray((max(self.total, 1),), "uint8")
+            self.dst = self.buf.ptr
+        if dist.world > 1:
+            hb = None
+            if dist.rank == 0:
+                h = cm.IpcHandle()
+                cm._chk(cm.lib().cmpc_ipc_export(self.buf.ptr, C.byref(h)), "cmpc_ipc_export")
+                hb = bytes(h.bytes)
+            hb = dist.gather_object(hb)[0]
+            if dist.rank != 0:
+                h = cm.IpcHandle()
+                C.memmove(C.addressof(h), hb, len(hb))
+                cm._chk(cm.lib().cmpc_ipc_open(C.byref(h), C.byref(self.dst)), "cmpc_ipc_open")
+                self.mapped = True
+
+    def gather(self, src_ptr, offset_bytes, nbytes, stream=None):
+        cm = self.cm
+        if offset_bytes < 0 or offset_bytes + nbytes > self.total:
+            raise ValueError("shard outside the gathered buffer")
+        cm._chk(cm.lib().cmpc_gather_shard(self.dst, int(offset_bytes), src_ptr, int(nbytes), stream), "cmpc_gather_shard")
+        cm._hchk(cm.hip().hipStreamSynchronize(stream), "hipStreamSynchronize")
+        self.dist.barrier()
+
+    def host(self, dtype, shape):
+        """Rank 0: the gathered buffer as a host array."""
+        import numpy as np
+        raw = self.buf.host()[: self.total]
+        return raw.view(np.dtype(dtype)).reshape(shape)
+
+    def close(self):
+        if self.mapped:
+            self.cm.lib().cmpc_ipc_close(self.dst)
+            self.mapped = False

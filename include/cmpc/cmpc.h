@@ -5,7 +5,8 @@
  *   - CentroidalMPC::UpdateMPC            (reference CentroidalMPC.cpp:278-370 / CentroidalMPC.h:32)
  *       → cmpc_solve_batch (B = 1 is one UpdateMPC call)
  *   - HpipmInterface::Impl::solve          (reference ocs2_sqp/hpipm_catkin/src/HpipmInterface.cpp:166-301)
- *       → cmpc_ocp_solve_batch (condensed OCP-QP, x0 eliminated as :177-208)
+ *       → cmpc_ocp_solve_batch_host (condensed OCP-QP, x0 eliminated as :177-208) and, with equality
+ *         constraints (:223-264), cmpc_ocp_solve_batch_eq_host
  *   - hpipm_interface::Settings            (reference hpipm_catkin/include/hpipm_catkin/HpipmInterfaceSettings.h:44-57)
  *       → cmpc_settings
  *   - d_ocp_qp_ipm_get_status codes        (reference HpipmInterface.h:79-85, HpipmInterface.cpp:462-473)
@@ -72,10 +73,19 @@ enum cmpc_qp_status {
 enum cmpc_precision { CMPC_F64 = 0, CMPC_F32 = 1 };
 
 /* Interior-point settings. Field-for-field mirror of hpipm_interface::Settings (HpipmInterfaceSettings.h:44-57),
- * defaults identical (cmpc_settings_default). hpipm_mode / ric_alg are accepted for ABI parity; warm_start != 0
- * makes cmpc_solve_batch_warm start from the given inputs. */
+ * defaults identical (cmpc_settings_default). Validated by cmpc_create / cmpc_set_settings (CMPC_ERR_ARG otherwise):
+ *   hpipm_mode  0..3 = HPIPM's SPEED_ABS, SPEED, BALANCE, ROBUST (same numbering as hpipm_catkin's hpipm_mode enum).
+ *               As in HpipmInterface.cpp:131-144 the mode only selects defaults that the explicit fields below then
+ *               override; the build runs one iteration (Mehrotra predictor-corrector) for every mode.
+ *   pred_corr   must be 1 (the only iteration the build restates); 0 is rejected.
+ *   ric_alg     0 or 1: HPIPM's classical / square-root Riccati factorisation choice. Both give the same iterates in
+ *               exact arithmetic; the build's dense factorisation serves both.
+ *   tol_eq      stopping tolerance on equality residuals: the centroidal QP has none; the equality-constrained OCP
+ *               path (cmpc_ocp_solve_batch_eq_host) solves its KKT system directly and reports the residual.
+ *   warm_start  0 or 1: 1 makes cmpc_solve_batch_warm start from the given inputs.
+ *   iter_max >= 0; alpha_min, mu0, tol_* > 0; reg_prim >= 0. */
 typedef struct cmpc_settings {
-  int hpipm_mode;   /* 0 = SPEED (default) */
+  int hpipm_mode;   /* 1 = SPEED (default, HpipmInterfaceSettings.h:45) */
   int iter_max;     /* 30 */
   double alpha_min; /* 1e-12 */
   double mu0;       /* 10 */
@@ -200,6 +210,20 @@ size_t cmpc_ocp_record_size(int N, int nx, const int* nu);
 int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
                               double* u, int* status);
 
+/* The same OCP with equality constraints at the nodes (HpipmInterface::solve with constraints != nullptr; the
+ * reference passes them to HPIPM as lg = ug = -e, HpipmInterface.cpp:223-264):
+ *   C_k x_k + D_k u_k + e_k = 0   (nc_k rows at node k = 0..N; D_N empty; nc_k = 0 leaves a node free).
+ * Per-problem constraint record (size cmpc_ocp_constraint_record_size), all blocks COLUMN-major:
+ *   C_k (nc_k*nx), D_k (nc_k*nu_k), e_k (nc_k)          k = 0..N
+ * The stage-0 rows are bounded through x0 exactly as the reference does (D_0 u_0 = -e_0 - C_0 x0, :236-244). Solved
+ * on the device by condensing the cost and the constraint rows to U-space and a range-space KKT solve (Cholesky of H
+ * and of the Schur complement E H^-1 E'). Redundant consistent rows are dropped; status CMPC_INCONS_EQ when the rows
+ * cannot all be met (|E U - f| > 1e-8 of the data scale), CMPC_NAN_SOL when H is not positive definite or the
+ * solution is non-finite. nc == NULL is CMPC_ERR_ARG (use cmpc_ocp_solve_batch_host). */
+size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* nc);
+int cmpc_ocp_solve_batch_eq_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0,
+                                 const double* rec, const double* crec, double* x, double* u, int* status);
+
 /* Discrete Riccati recursion of the same equality-free OCP on the device: the cost-to-go and affine policy that
  * HpipmInterface::getRiccatiCostToGo / getRiccatiFeedback / getRiccatiFeedforward return (reference
  * HpipmInterface.cpp:330-455, from HPIPM's ric_P / ric_p / ric_Lr / ric_Ls / ric_k; recursion as
@@ -237,6 +261,22 @@ int cmpc_gait_table_destroy(cmpc_gait_table* table);
  * id outside the table gives all-swing rows (-> CMPC_INVALID_CONTACT downstream). */
 int cmpc_gait_contact_batch(const cmpc_gait_table* table, int B, const int* d_gait_id, const double* d_t_start,
                             double t0, double dt, int N, uint8_t* d_contact, void* stream);
+
+/* ---- Multi-GPU result gather (north_star: "xGMI only for result gather, no RCCL reductions") ----
+ * One process per GPU, each solving a contiguous QP-id shard (cheeta_mpc/shard.py). Rank 0 owns the gathered
+ * buffer on its device and exports it (cmpc_ipc_export); every other rank maps it into its own address space
+ * (cmpc_ipc_open: dmabuf IPC, peer access over xGMI) and copies its shard straight into place with
+ * cmpc_gather_shard (a device-to-device copy issued on the rank's stream: a peer write over xGMI when the ranks sit on
+ * different GPUs). No collective and no reduction runs on the data path; the caller orders the copies with a
+ * barrier (exported handle before the opens, copies done before rank 0 reads). */
+#define CMPC_IPC_HANDLE_BYTES 64
+typedef struct cmpc_ipc_handle {
+  unsigned char bytes[CMPC_IPC_HANDLE_BYTES];
+} cmpc_ipc_handle;
+int cmpc_ipc_export(void* d_ptr, cmpc_ipc_handle* out);
+int cmpc_ipc_open(const cmpc_ipc_handle* handle, void** d_ptr);
+int cmpc_ipc_close(void* d_ptr);
+int cmpc_gather_shard(void* d_dst, size_t dst_offset_bytes, const void* d_src, size_t bytes, void* stream);
 
 /* Per-stage device timing with HIP events recorded on the solve stream (used by bench.py for the roofline):
  * after cmpc_profile_begin, each cmpc_solve_batch records events around its three stages (condense, IPM, expand);

@@ -245,3 +245,87 @@ def centoid_test_inputs(N=6, literal_quirk=True):
     for k in range(N):
         contact[k] = table6[k % 6]
     return x0, xref, foot, contact
+
+
+def ocp_eq_fullspace(N, nx, nu, x0, A, B, b, Q, S, R, q, r, Cc=None, D=None, e=None):
+    """HpipmInterface::solve's OCP-QP (HpipmInterface.cpp:166-301) restated in the FULL (x, u) space, independent of
+    the device's condensing: decision vector z = [u_0, x_1, u_1, ..., x_N] (x_0 = x0 given), cost
+    sum_k 1/2 x'Q x + u'S x + 1/2 u'R u + q'x + r'u, equalities x_{k+1} = A x_k + B u_k + b_k and, when given,
+    C_k x_k + D_k u_k + e_k = 0 (the rows the reference passes to HPIPM as lg = ug = -e, :223-264). One dense KKT
+    solve (least squares, so consistent redundant rows are fine). Returns (x [N+1][nx], u list, residual of the
+    constraint rows)."""
+    xo = [None] + [0] * N  # offset of x_k in z (k >= 1)
+    uo = [0] * N
+    n = 0
+    for k in range(N + 1):
+        if k >= 1:
+            xo[k] = n
+            n += nx
+        if k < N:
+            uo[k] = n
+            n += nu[k]
+    P = np.zeros((n, n))
+    p = np.zeros(n)
+    rows, rhs = [], []
+    x0 = np.asarray(x0, np.float64)
+
+    def xs(k):
+        return slice(xo[k], xo[k] + nx)
+
+    def us(k):
+        return slice(uo[k], uo[k] + nu[k])
+    for k in range(N + 1):
+        m = nu[k] if k < N else 0
+        if k >= 1:
+            P[xs(k), xs(k)] += Q[k]
+            p[xs(k)] += q[k]
+        if m:
+            P[us(k), us(k)] += R[k]
+            p[us(k)] += r[k]
+            if k >= 1:
+                P[us(k), xs(k)] += S[k]
+                P[xs(k), us(k)] += S[k].T
+            else:
+                p[us(k)] += S[k] @ x0
+    for k in range(N):  # dynamics rows: x_{k+1} - A x_k - B u_k = b_k
+        row = np.zeros((nx, n))
+        row[:, xs(k + 1)] = np.eye(nx)
+        rh = np.array(b[k], dtype=np.float64)
+        if k >= 1:
+            row[:, xs(k)] = -A[k]
+        else:
+            rh = rh + A[k] @ x0
+        if nu[k]:
+            row[:, us(k)] = -B[k]
+        rows.append(row)
+        rhs.append(rh)
+    ncon = 0
+    if Cc is not None:
+        for k in range(N + 1):
+            if Cc[k] is None or len(e[k]) == 0:
+                continue
+            nck = len(e[k])
+            row = np.zeros((nck, n))
+            rh = -np.asarray(e[k], dtype=np.float64)
+            if k >= 1:
+                row[:, xs(k)] = Cc[k]
+            else:
+                rh = rh - Cc[k] @ x0
+            if k < N and nu[k]:
+                row[:, us(k)] = D[k]
+            rows.append(row)
+            rhs.append(rh)
+            ncon += nck
+    Aeq = np.vstack(rows)
+    beq = np.concatenate(rhs)
+    m_eq = Aeq.shape[0]
+    K = np.block([[P, Aeq.T], [Aeq, np.zeros((m_eq, m_eq))]])
+    sol = np.linalg.lstsq(K, np.concatenate([-p, beq]), rcond=None)[0]
+    z = sol[:n]
+    x = np.zeros((N + 1, nx))
+    x[0] = x0
+    for k in range(1, N + 1):
+        x[k] = z[xs(k)]
+    u = [z[us(k)] for k in range(N)]
+    res = float(np.abs(Aeq @ z - beq).max()) if m_eq else 0.0
+    return x, u, res

@@ -55,7 +55,7 @@ def default_model(N=10):
 
 def default_settings(**kw):
     """hpipm_interface::Settings defaults (HpipmInterfaceSettings.h:44-57)."""
-    s = Settings(hpipm_mode=0, iter_max=30, alpha_min=1e-12, mu0=10.0, tol_stat=1e-6, tol_eq=1e-8, tol_ineq=1e-8,
+    s = Settings(hpipm_mode=1, iter_max=30, alpha_min=1e-12, mu0=10.0, tol_stat=1e-6, tol_eq=1e-8, tol_ineq=1e-8,
                  tol_comp=1e-8, reg_prim=1e-12, warm_start=0, pred_corr=1, ric_alg=0)
     for k, v in kw.items():
         setattr(s, k, v)
@@ -67,12 +67,22 @@ def tight_settings():
 
 
 _lib = None
+_LIBNAME = os.environ.get("CMPC_ORACLE_LIB", "liboracle.so")
+
+
+def select_build(name):
+    """Choose the oracle build before first use: "liboracle.so" (the checker, -ffp-contract=off) or
+    "liboracle_fast.so" (bench.py's cpu_baseline: -O3, FMA contraction)."""
+    global _LIBNAME
+    if _lib is not None and name != _LIBNAME:
+        raise RuntimeError("oracle library already loaded as " + _LIBNAME)
+    _LIBNAME = name
 
 
 def lib():
     global _lib
     if _lib is None:
-        path = os.path.join(HERE, "liboracle.so")
+        path = os.path.join(HERE, _LIBNAME)
         if not os.path.exists(path):
             import subprocess
             subprocess.check_call(["make", "-s", "-C", HERE])
@@ -282,6 +292,20 @@ def ocp_pack(N, nx, nu, A, B, b, Q, S, R, q, r):
                   np.asarray(R[k]).reshape(m, m).flatten(order="F") if m else np.zeros(0),
                   np.asarray(q[k]).reshape(nx), np.asarray(r[k]).reshape(m) if m else np.zeros(0)]
     return np.concatenate(parts).astype(np.float64)
+
+
+def ocp_constraint_pack(N, nx, nu, nc, Cc, D, e):
+    """Pack per-node equality constraints C_k x + D_k u + e_k = 0 into the column-major record of
+    cmpc_ocp_constraint_record_size (k = 0..N; D_N empty)."""
+    parts = []
+    for k in range(N + 1):
+        m = nu[k] if k < N else 0
+        if nc[k] == 0:
+            continue
+        parts += [np.asarray(Cc[k]).reshape(nc[k], nx).flatten(order="F"),
+                  np.asarray(D[k]).reshape(nc[k], m).flatten(order="F") if m else np.zeros(0),
+                  np.asarray(e[k]).reshape(nc[k])]
+    return np.concatenate(parts).astype(np.float64) if parts else np.zeros(0)
 
 
 def ocp_solve(N, nx, nu, x0, rec):

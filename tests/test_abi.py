@@ -37,6 +37,20 @@ def test_settings_defaults_match_hpipm_interface():
     assert (s.iter_max, s.alpha_min, s.mu0, s.tol_stat, s.tol_eq, s.tol_ineq, s.tol_comp, s.reg_prim) == \
         (30, 1e-12, 10.0, 1e-6, 1e-8, 1e-8, 1e-8, 1e-12)
     assert (s.warm_start, s.pred_corr, s.ric_alg) == (0, 1, 0)
+    assert s.hpipm_mode == 1  # hpipm_mode::SPEED, same numbering as the mirrored enum (HpipmInterface.h)
+
+
+@pytest.mark.parametrize("field,value", [("pred_corr", 0), ("hpipm_mode", 4), ("hpipm_mode", -1), ("ric_alg", 2),
+                                         ("warm_start", 2), ("tol_stat", 0.0), ("mu0", -1.0), ("iter_max", -1)])
+def test_unsupported_settings_rejected(field, value):
+    """Settings the build does not implement are refused (CMPC_ERR_ARG) before any device call, not ignored."""
+    import ctypes as C
+    import cheeta_mpc
+    s = cheeta_mpc.default_settings(**{field: value})
+    m = cheeta_mpc.default_model(10)
+    ctx = C.c_void_p()
+    assert cheeta_mpc.lib().cmpc_create(C.byref(m), C.byref(s), 0, 16, None, C.byref(ctx)) == -1
+    assert cheeta_mpc.lib().cmpc_set_settings(None, C.byref(s)) == -1
 
 
 def test_model_default_is_centoid_mpc_test(op):
@@ -103,3 +117,11 @@ def test_cpp_mirror_headers_compile(tmp_path):
     src.write_text('#include "cheeta_mpc/CentroidalMPC.h"\n#include "hpipm_catkin/HpipmInterface.h"\n'
                    'int main(){ ocs2::HpipmInterface::OcpSize s(5,3,2); return s.numInputs.back(); }\n')
     subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)])
+
+
+def test_step_ratio_extreme_fp32_values():
+    """The IPM kernels' fraction-to-boundary selection (csrc/step_ratio.hpp) compared in double: fp32 slacks and
+    directions near 1e-20 / 1e+20 still select the binding candidate (host build of the same header)."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp"), "bin/test_step_ratio"])
+    out = subprocess.check_output([os.path.join(ROOT, "tests", "cpp", "bin", "test_step_ratio")], text=True)
+    assert "step_ratio: ok" in out, out
