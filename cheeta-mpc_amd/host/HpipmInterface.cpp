@@ -53,13 +53,9 @@ class HpipmInterface::Impl {
     if ((int)cost.size() != N + 1)
       throw std::runtime_error("[HpipmInterface] Inconsistent size of cost: " + std::to_string(cost.size()) + " with " +
                                std::to_string(N + 1) + " nodes.");
-    if (constraints != nullptr) {
-      if ((int)constraints->size() != N + 1)
-        throw std::runtime_error("[HpipmInterface] Inconsistent size of constraints: " +
-                                 std::to_string(constraints->size()) + " with " + std::to_string(N + 1) + " nodes.");
-      for (const auto& c : *constraints)
-        if (c.f.size() > 0) throw std::runtime_error("[HpipmInterface] equality-constrained stages are not supported");
-    }
+    if (constraints != nullptr && (int)constraints->size() != N + 1)
+      throw std::runtime_error("[HpipmInterface] Inconsistent size of constraints: " +
+                               std::to_string(constraints->size()) + " with " + std::to_string(N + 1) + " nodes.");
     const int nx = x0.size();
     std::vector<int> nu((size_t)N);
     for (int k = 0; k < N; ++k) {
@@ -91,9 +87,33 @@ class HpipmInterface::Impl {
     }
     int nU = 0;
     for (int v : nu) nU += v;
+    // === Constraints === C dx + D du + e = 0 per node, handed to the device as they come (the reference maps them to
+    // HPIPM's lg = ug = -e, with the stage-0 rows bounded through x0, HpipmInterface.cpp:223-264); an empty node
+    // (f.size() == 0) has no rows
+    std::vector<int> nc((size_t)N + 1, 0);
+    std::vector<double> crec;
+    int nE = 0;
+    if (constraints != nullptr) {
+      for (int k = 0; k <= N; ++k) {
+        const auto& c = (*constraints)[(size_t)k];
+        const int rows = c.f.size();
+        const int m = k < N ? nu[(size_t)k] : 0;
+        if (rows == 0) continue;
+        if (c.dfdx.rows() != rows || c.dfdx.cols() != nx || (m > 0 && (c.dfdu.rows() != rows || c.dfdu.cols() != m)))
+          throw std::runtime_error("[HpipmInterface] constraint " + std::to_string(k) + " has inconsistent sizes");
+        nc[(size_t)k] = rows;
+        nE += rows;
+        crec.insert(crec.end(), c.dfdx.a.begin(), c.dfdx.a.end());
+        if (m > 0) crec.insert(crec.end(), c.dfdu.a.begin(), c.dfdu.a.end());
+        crec.insert(crec.end(), c.f.v.begin(), c.f.v.end());
+      }
+    }
     std::vector<double> x((size_t)(N + 1) * nx), u((size_t)(nU > 0 ? nU : 1));
     int status = -1;
-    const int r = cmpc_ocp_solve_batch_host(1, N, nx, nu.data(), x0.data(), rec.data(), x.data(), u.data(), &status);
+    const int r = nE > 0 ? cmpc_ocp_solve_batch_eq_host(1, N, nx, nu.data(), nc.data(), x0.data(), rec.data(),
+                                                         crec.data(), x.data(), u.data(), &status)
+                         : cmpc_ocp_solve_batch_host(1, N, nx, nu.data(), x0.data(), rec.data(), x.data(), u.data(),
+                                                     &status);
     if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device solve failed: ") + cmpc_error_string(r));
     xs.assign((size_t)N + 1, vector_t());
     for (int k = 0; k <= N; ++k) {
@@ -111,6 +131,7 @@ class HpipmInterface::Impl {
     lastRec_ = std::move(rec);
     lastNu_ = nu;
     lastNx_ = nx;
+    lastConstrained_ = nE > 0;
     riccatiValid_ = false;
     return (hpipm_status)status;
   }
@@ -121,6 +142,9 @@ class HpipmInterface::Impl {
     if (N == 0) throw std::runtime_error("[HpipmInterface] no solved problem to take Riccati quantities from");
     if (dyn0.dfdx.rows() != lastNx_ || dyn0.dfdu.cols() != lastNu_[0] || cost0.dfdxx.rows() != lastNx_)
       throw std::runtime_error("[HpipmInterface] dynamics0 / cost0 do not match the last solved problem");
+    if (lastConstrained_)
+      throw std::runtime_error(
+          "[HpipmInterface] Riccati quantities of an equality-constrained solve are not provided by this build");
     if (riccatiValid_) return;
     const int nx = lastNx_;
     int nU = 0;
@@ -183,6 +207,7 @@ class HpipmInterface::Impl {
   std::vector<double> lastRec_;
   std::vector<int> lastNu_;
   int lastNx_ = 0;
+  bool lastConstrained_ = false;
   bool riccatiValid_ = false;
   std::vector<double> Sm_, sv_, K_, k_;
 };

@@ -1,5 +1,6 @@
 // C++ mirror of the reference gtests ocs2_sqp/hpipm_catkin/test/testHpipmInterface.cpp (solve_and_check_dynamic
-// :37-69, solve_after_resize :71-110, knownSolution :112-152, noInputs :208-256, retrieveRiccati :258-340) against the
+// :37-69, solve_after_resize :71-110, knownSolution :112-152, with_constraints :154-206, noInputs :208-256,
+// retrieveRiccati :258-340) against the
 // HpipmInterface
 // mirror, whose solve runs on the MI355X engine. Random problems from a fixed-seed generator (ocs2's
 // getRandomDynamics/getRandomCost are not vendored): uniform [-1,1) matrices, costs made positive definite.
@@ -156,6 +157,88 @@ static void dynamics_feasible(bool resize) {
   CHECK(threw, "size mismatch throws");
 }
 
+// Eigen's isApprox: |a - b| <= prec * min(|a|, |b|) (2-norms)
+static bool is_approx(const vector_t& a, const vector_t& b, double prec) {
+  if (a.size() != b.size()) return false;
+  double d = 0, na = 0, nb = 0;
+  for (int i = 0; i < a.size(); ++i) {
+    d += (a[i] - b[i]) * (a[i] - b[i]);
+    na += a[i] * a[i];
+    nb += b[i] * b[i];
+  }
+  return std::sqrt(d) <= prec * std::sqrt(std::fmin(na, nb));
+}
+static VectorFunctionLinearApproximation randomConstraints(int nx, int nu, int nc) {
+  VectorFunctionLinearApproximation c;
+  c.dfdx = randm(nc, nx);
+  c.dfdu = randm(nc, nu);
+  c.f = randv(nc);
+  return c;
+}
+
+// testHpipmInterface.cpp:154-206 with_constraints: one row per node, node 1 left empty, through getOCPSolution's
+// non-projection branch (MultipleShootingSolver.cpp:275-277: resize from extractSizesFromProblem with constraints)
+static void with_constraints() {
+  const int nx = 3, nu = 2, nc = 1, N = 5;
+  const vector_t x0 = randv(nx);
+  std::vector<VectorFunctionLinearApproximation> sys, con;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+    con.push_back(randomConstraints(nx, nu, nc));
+  }
+  cost.push_back(randomCost(nx, 0));
+  con.push_back(randomConstraints(nx, 0, nc));
+  con[1] = VectorFunctionLinearApproximation();  // "Set one of the constraints to empty"
+  HpipmInterface hpipm;
+  hpipm.resize(hpipm_interface::extractSizesFromProblem(sys, cost, &con));
+  vector_array_t xs, us;
+  const auto status = hpipm.solve(x0, sys, cost, &con, xs, us, false);
+  CHECK(status == hpipm_status::SUCCESS, "with_constraints status");
+  CHECK(is_approx(xs[0], x0, 1e-15), "with_constraints x0");
+  for (int k = 0; k < N; ++k) {
+    vector_t xn = sys[k].f;
+    const vector_t ax = mv(sys[k].dfdx, xs[(size_t)k]), bu = mv(sys[k].dfdu, us[(size_t)k]);
+    for (int i = 0; i < nx; ++i) xn[i] += ax[i] + bu[i];
+    CHECK(is_approx(xs[(size_t)k + 1], xn, 1e-9), "with_constraints dynamics");
+  }
+  for (int k = 0; k <= N; ++k) {
+    if (con[(size_t)k].f.size() == 0) continue;
+    vector_t r = mv(con[(size_t)k].dfdx, xs[(size_t)k]);
+    if (k < N) {
+      const vector_t du = mv(con[(size_t)k].dfdu, us[(size_t)k]);
+      for (int i = 0; i < r.size(); ++i) r[i] += du[i];
+    }
+    for (int i = 0; i < r.size(); ++i) r[i] = -r[i];
+    CHECK(is_approx(con[(size_t)k].f, r, 1e-9), "with_constraints constraint rows");
+  }
+  // the unconstrained solve of the same problem differs (the constraints bind)
+  vector_array_t xu, uu;
+  hpipm.resize(hpipm_interface::extractSizesFromProblem(sys, cost, nullptr));
+  hpipm.solve(x0, sys, cost, nullptr, xu, uu, false);
+  CHECK(maxdiff(uu[0], us[0]) > 1e-6, "constraints change the solution");
+  // contradictory duplicate rows at one node -> INCONS_EQ
+  auto bad = con;
+  bad[2].dfdx.resize(2, nx);
+  bad[2].dfdu.resize(2, nu);
+  bad[2].f.resize(2);
+  for (int r = 0; r < 2; ++r) {
+    for (int j = 0; j < nx; ++j) bad[2].dfdx(r, j) = con[2].dfdx(0, j);
+    for (int j = 0; j < nu; ++j) bad[2].dfdu(r, j) = con[2].dfdu(0, j);
+    bad[2].f[r] = con[2].f[0] + (r == 0 ? 0.0 : 1.0);
+  }
+  hpipm.resize(hpipm_interface::extractSizesFromProblem(sys, cost, &bad));
+  CHECK(hpipm.solve(x0, sys, cost, &bad, xu, uu, false) == hpipm_status::INCONS_EQ, "inconsistent rows");
+  // the same duplicate row, consistent: redundant, same solution as with one row
+  bad[2].f[1] = bad[2].f[0];
+  CHECK(hpipm.solve(x0, sys, cost, &bad, xu, uu, false) == hpipm_status::SUCCESS, "redundant rows status");
+  double e = 0.0;
+  for (int k = 0; k < N; ++k) e = std::fmax(e, maxdiff(uu[(size_t)k], us[(size_t)k]));
+  CHECK(e < 1e-9, "redundant rows solution");
+  std::printf("with_constraints ok (redundant-row max diff %.2e)\n", e);
+}
+
 // small dense helpers for the reference recursion (testHpipmInterface.cpp:280-304)
 static matrix_t mm(const matrix_t& A, const matrix_t& B) {
   matrix_t C(A.rows(), B.cols());
@@ -278,6 +361,7 @@ int main() {
   dynamics_feasible(true);
   known_solution(false);
   known_solution(true);
+  with_constraints();
   retrieve_riccati();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;
