@@ -135,4 +135,18 @@ __device__ __forceinline__ T pyr_row(int rho, T mu, T fx, T fy, T fz) {
   }
 }
 
+// Issue priority falls with the QP's progress: 3 for iterations 0-1, 2 for 2-3, 1 for 4-5, 0 from 6 on. Two waves
+// share a SIMD; at equal priority the older one takes the issue slots and the younger gets the leftovers, so the
+// two slots of a SIMD drift apart (lab timeline, B = 4096: the older wave's QP 145 us, the younger's up to 230 us)
+// and the launch ends with one wave per SIMD for ~60 us. Letting the less advanced QP win arbitration keeps the
+// pair closer together: k_ipm64 0.411 -> 0.396 ms in the lab (per-iteration thirds and a round-aware variant measured
+// within 1 % of this); iterates are bit-identical.
+__device__ __forceinline__ void progress_prio(int it) {
+  const int pr = 3 - min(3, it >> 1);
+  if (pr == 3) __builtin_amdgcn_s_setprio(3);
+  else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+  else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 }  // namespace cmpc

@@ -347,6 +347,7 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   };
 
   for (it = 0;; ++it) {
+    progress_prio(it);  // cmpc_device.hpp (lab, n = 120 fp64: 3.94 -> 3.91 ms)
     // ---- H: 64 loads per lane, 4 rows x 16 consecutive columns per instruction
     {
       const int ol = olane(), w = owave();

@@ -61,6 +61,26 @@
       (ptr)[(size_t)(q) * 9 + 8] = t_ - st_t0_;                                   \
     }                                                                             \
   } while (0)
+#elif defined(CMPC_IPM_TIMELINE)
+// diagnostic: per-QP wave start / end on the 100-MHz real-time counter and the hardware slot (HW_ID, XCC_ID)
+#define IPM_STAMP_DECL                                                                      \
+  unsigned long long tl_t0_;                                                                \
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tl_t0_)::"memory")
+#define IPM_STAMP(k) (void)0
+#define IPM_STAMP_STORE(ptr, q)                                                             \
+  do {                                                                                      \
+    unsigned long long t_;                                                                  \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+    unsigned hw_, xcc_;                                                                     \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                       \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                     \
+    if ((ptr) && threadIdx.x == 0) {                                                        \
+      (ptr)[(size_t)(q) * 9 + 0] = tl_t0_;                                                  \
+      (ptr)[(size_t)(q) * 9 + 1] = t_;                                                      \
+      (ptr)[(size_t)(q) * 9 + 2] = hw_;                                                     \
+      (ptr)[(size_t)(q) * 9 + 3] = xcc_;                                                    \
+    }                                                                                       \
+  } while (0)
 #else
 #define IPM_STAMP_DECL (void)0
 #define IPM_STAMP(k) (void)0
@@ -337,6 +357,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   int status = CMPC_MAX_ITER;
   int it = 0;
   for (it = 0;; ++it) {
+    progress_prio(it);  // cmpc_device.hpp
     load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
 #ifdef H_WAIT_STAMP  // diagnostic: time to the last H row (segment 3)
     IPM_STAMP(0);

@@ -23,6 +23,6 @@ with open(os.path.join(here, "variants.mk"), "w") as f:
     for r in rows:
         st = "-DLAB_STAMPS" if r[3] == "1" else ""
         extra = " ".join(r[4:])
-        st = "-DLAB_STAMPS -DCMPC_IPM_STAMPS" if r[3] == "1" else ""
+        st = {"1": "-DLAB_STAMPS -DCMPC_IPM_STAMPS", "2": "-DCMPC_IPM_TIMELINE"}.get(r[3], "")
         f.write(f"build/{r[0]}.o: ipm_variant.hip {r[1]} lab_stamps.hpp ../cheeta-mpc_amd/csrc/k_ipm64.hpp ../cheeta-mpc_amd/csrc/k_ipm128x.hpp\n\t@mkdir -p build\n"
                 f"\t$(HIPCC) $(FLAGS) -DLAB_HDR={r[1]} -DLAB_FN={r[0]} -DLAB_WPE={r[2]} {st} {extra} -c $< -o $@\n")

@@ -203,7 +203,16 @@ int main(int argc, char** argv) {
     printf("{\"variant\": \"%s\", \"ms_median\": %.5f, \"ms_best\": %.5f, \"qps_ipm\": %.0f, \"max_rel_du\": %.3e, "
            "\"same_status\": %d, \"same_iters\": %d, \"bitexact\": %d",
            v.name, med, best, B / (med * 1e-3), maxrel, same_st, same_it, bitexact);
-    if (v.stamps) {
+    if (v.stamps == 2) {  // timeline build: raw [start, end, HW_ID, XCC_ID] per QP to a file for offline analysis
+      CK(hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost));
+      char path[256];
+      snprintf(path, sizeof(path), "%s/timeline_%s.bin", getenv("LAB_OUT") ? getenv("LAB_OUT") : ".", v.name);
+      FILE* f = fopen(path, "wb");
+      if (f) {
+        fwrite(hst.data(), 8, hst.size(), f);
+        fclose(f);
+      }
+    } else if (v.stamps) {
       CK(hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost));
       double seg[9] = {0}, its = 0;
       for (int q = 0; q < B; ++q) {

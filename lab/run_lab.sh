@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/lab; mkdir -p $O
 cd $R
 fatal() { case $1 in 124|134|137|139) echo "fatal exit $1 in $2"; exit 1;; esac; }
-timeout -k 10 240 ./lab/ipm_lab 4096 25 > $O/lab.json 2> $O/lab.err; rc=$?; echo "lab rc=$rc"; cat $O/lab.json; fatal $rc lab
+LAB_OUT=$O timeout -k 10 240 ./lab/ipm_lab ${LAB_B:-4096} 25 > $O/lab.json 2> $O/lab.err; rc=$?; echo "lab rc=$rc"; cat $O/lab.json; fatal $rc lab
 [ $rc -ne 0 ] && exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1; echo "list rc=$?"
