@@ -189,6 +189,7 @@ def main():
     ms = [C.c_double(0), C.c_double(0), C.c_double(0)]
     ncalls = C.c_int(0)
     cm.lib().cmpc_profile_end(eng.ctx, *[C.byref(m) for m in ms], C.byref(ncalls))
+    # stage 1 / 2 / 3 (cmpc.h): condensing / IPM / expand, or on the fused path fused n<=64 / bigger classes / expand
     ms_cond, ms_ipm, ms_exp = (m.value / max(ncalls.value, 1) for m in ms)
 
     # result gather beside the timed region ("xGMI only for result gather"): every rank writes its U
@@ -213,18 +214,43 @@ def main():
     ct = contact.host()
     nvar = 3 * ct.reshape(B, -1).sum(axis=1)
     ok = status == 0
-    flops_launch = float(ipm_flops(nvar[ok], iters[ok]).sum())
+    fused = bool(cm.lib().cmpc_ctx_fused(eng.ctx)) and args.sqp_iters <= 0
     peak = FP64_PEAK if prec == cm.F64 else FP32_PEAK
-    achieved = flops_launch / (ms_ipm * 1e-3) if ms_ipm > 0 else 0.0
+    fl_ipm = ipm_flops(nvar, iters) * ok
+    fl_cond = condense_flops(ct) * (nvar > 0)
+    small = nvar <= 64
 
     headline = (B == 4096 and N == 10 and prec == cm.F64 and args.gait == 0 and not args.all_stance)
     wkey = (f"N{N}_B{B}_{'f64' if prec == cm.F64 else 'f32'}_"
             f"{'allstance' if args.all_stance else ('trot' if args.gait == 0 else 'mixed')}")
     tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{wkey}.json")
-    traffic, traffic_src = pmc_traffic(tpath, "k_ipm")
-    traffic_c, _ = pmc_traffic(tpath, "condense")
-    fl_cond = float(condense_flops(ct).sum())
-    achieved_c = fl_cond / (ms_cond * 1e-3) if ms_cond > 0 else 0.0
+    unit_name = "fp64 VALU" if prec == cm.F64 else "fp32 VALU"
+
+    def roof(kernel, flops, ms, bound, prefix, what):
+        tr, src = pmc_traffic(tpath, prefix)
+        a = flops / (ms * 1e-3) if ms > 0 else 0.0
+        return {"bound": bound, "compute_unit": unit_name if bound == "valu" else "fp64/fp32 MFMA", "kernel": kernel,
+                "achieved": a / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s", "frac": a / peak, "traffic": tr,
+                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": src, "flops_per_launch": flops,
+                "ms_per_launch": ms, "flops_counted": what}
+
+    if fused:
+        # dominant kernel = k_solve64: condensing and IPM of the n <= 64 class in one launch; its algorithmic work is
+        # both stages' FLOPs of those QPs, its time the first profiled stage
+        f_small = float(fl_ipm[small].sum() + fl_cond[small].sum())
+        roofline = roof("k_solve64 (fused condensing + IPM, n<=64)", f_small, ms_cond, "valu", "k_solve64",
+                        "IPM + condensing FLOPs of the n<=64 QPs")
+        stages = {"solve64_fused": ms_cond, "bigger_classes": ms_ipm, "expand": ms_exp}
+        f_all = float(fl_ipm.sum() + fl_cond.sum())
+        extra = {"roofline_solve": roof("whole solve (all classes, condensing + IPM)", f_all, ms_cond + ms_ipm,
+                                        "valu", "cmpc::k_", "IPM + condensing FLOPs of every QP")}
+    else:
+        roofline = roof("IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)", float(fl_ipm.sum()),
+                        ms_ipm, "valu", "k_ipm", "IPM FLOPs")
+        stages = {"condense": ms_cond, "ipm": ms_ipm, "expand": ms_exp}
+        # the condensing stage's Bqp' Q Bqp contraction runs on MFMA (v_mfma_f64_16x16x4 / f32_16x16x4)
+        extra = {"roofline_condense": roof("condensing stage (k_condense64 / k_srbd_condense)", float(fl_cond.sum()),
+                                           ms_cond, "mfma", "condense", "condensing FLOPs")}
 
     value = world * B * args.steps / elapsed
     result = {
@@ -250,17 +276,10 @@ def main():
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"shard{world}"},
         # compute-bound on the vector ALU: the IPM's arithmetic runs on the fp64/fp32 VALU (on gfx950 the VALU issues
         # fp64 at twice the rate of v_mfma_f64_16x16x4); peak = the dtype's vector datasheet peak
-        "roofline": {"bound": "valu", "compute_unit": "fp64 VALU" if prec == cm.F64 else "fp32 VALU",
-                     "kernel": "IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)",
-                     "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
-                     "traffic_source": traffic_src, "flops_per_launch": flops_launch, "ms_per_launch": ms_ipm},
-        # the condensing stage's Bqp' Q Bqp contraction runs on MFMA (v_mfma_f64_16x16x4 / f32_16x16x4)
-        "roofline_condense": {"bound": "mfma", "kernel": "condensing stage (k_condense64 / k_srbd_condense)",
-                              "achieved": achieved_c / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                              "frac": achieved_c / peak, "traffic": traffic_c,
-                              "flops_per_launch": fl_cond, "ms_per_launch": ms_cond},
-        "stages_ms": {"condense": ms_cond, "ipm": ms_ipm, "expand": ms_exp},
+        "roofline": roofline,
+        **extra,
+        "stages_ms": stages,
+        "fused_n64": fused,
         "gather_ms": gather["ms"], "gather": gather,
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,
                    "mean_n": float(nvar.mean())},

@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -42,6 +43,9 @@ struct cmpc_ctx {
   int* iters;
   int* qlist;   // [3][max_batch] per-class QP lists (k_class_lists)
   int* qcount;  // [3]
+  // cold-start cmpc_solve_batch runs the fused n <= 64 kernel (k_solve64) when N <= 21; CMPC_FUSED=0 in the
+  // environment at cmpc_create selects the separate condensing + IPM launches (A/B measurement)
+  bool fused;
   double *lin, *uj, *uq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   // host-API staging (grown on demand, outside the async path)
@@ -282,6 +286,39 @@ int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, boo
   return r;
 }
 
+// Fused path (cold-start cmpc_solve_batch, N <= 21): k_solve64 condenses and solves the whole n <= 64 class in one
+// launch (the condensing's MFMA/latency-bound phase overlaps the IPM of the co-resident wave, and the first Newton
+// matrix starts from the condensing's registers instead of an H round trip); the bigger classes follow as before:
+// their nvar hints -> k_class_lists -> workgroup condensing -> their IPM kernels. ev1 (profiling) is recorded after
+// the fused launch.
+template <typename T>
+int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot, const uint8_t* contact,
+                hipStream_t st, hipEvent_t ev1) {
+  CondenseArgs<T> ca = condense_args<T>(c, x0, xref, foot, contact);
+  const IpmArgs<T> ia = ipm_args<T>(c);
+  if (launch_solve64(ia, ca, B, st) != 0) return -2;
+  if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
+  if (c->ld < 128) return 0;
+  if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
+  ca.n_lo = 64;
+  ca.qlist = c->qlist + (size_t)1 * B;
+  ca.qcount = c->qcount + 1;
+  int r = launch_srbd_condense<T>(ca, 128, B, st);
+  if (r == 0 && c->ld > 128) {
+    ca.n_lo = 128;
+    ca.qlist = c->qlist + (size_t)2 * B;
+    ca.qcount = c->qcount + 2;
+    r = launch_srbd_condense<T>(ca, 256, B, st);
+  }
+  if (r != 0) return r;
+  IpmArgs<T> al = ia;
+  for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
+  al.qcount = c->qcount;
+  r = launch_ipm128(al, B, st);
+  if (r == 0 && c->ld >= 256) r = launch_ipm256(al, B, st);
+  return r;
+}
+
 // lists_ready: the condensing of this call built the class lists (run_condense), else they are built here
 int run_ipm(cmpc_ctx* c, int B, hipStream_t st, int warm, bool lists_ready) {
   int r;
@@ -388,6 +425,10 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->precision = precision;
   c->max_batch = max_batch;
   c->ld = ld_for(*model);
+  {
+    const char* f = std::getenv("CMPC_FUSED");
+    c->fused = model->N <= CMPC_C64_MAXN && !(f && f[0] == '0');
+  }
   (void)hipGetDevice(&c->device);
   const Layout L = layout(c->ld, precision, max_batch);
   c->ws_bytes = L.total;
@@ -469,6 +510,7 @@ int cmpc_get_model(const cmpc_ctx* c, cmpc_model* out) {
 }
 
 int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
+int cmpc_ctx_fused(const cmpc_ctx* c) { return c && c->fused ? 1 : 0; }
 
 int cmpc_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                      const uint8_t* contact, double* u, double* x, int* status, int* iters, void* stream) {
@@ -484,16 +526,22 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
   hipEvent_t* ev = nullptr;
   if (c->profiling && c->prof_calls < c->prof_max) ev = &c->prof_ev[(size_t)4 * c->prof_calls++];
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
-  bool lists = false;
-  int r = run_condense(c, B, x0, xref, foot, contact, st, nullptr, &lists);
-  if (r != CMPC_OK) return r;
   const int warm = (u_init && c->settings.warm_start != 0) ? 1 : 0;
-  if (warm && launch_pack_warm(u_init, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B,
-                               st) != 0)
-    return CMPC_ERR_HIP;
-  if (ev) HIP_OK(hipEventRecord(ev[1], st));
-  r = run_ipm(c, B, st, warm, lists);
-  if (r != CMPC_OK) return r;
+  if (!warm && c->fused) {
+    const int rf = c->precision == CMPC_F64 ? run_fused_t<double>(c, B, x0, xref, foot, contact, st, ev ? ev[1] : nullptr)
+                                            : run_fused_t<float>(c, B, x0, xref, foot, contact, st, ev ? ev[1] : nullptr);
+    if (rf != 0) return CMPC_ERR_HIP;
+  } else {
+    bool lists = false;
+    int r = run_condense(c, B, x0, xref, foot, contact, st, nullptr, &lists);
+    if (r != CMPC_OK) return r;
+    if (warm && launch_pack_warm(u_init, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B,
+                                 st) != 0)
+      return CMPC_ERR_HIP;
+    if (ev) HIP_OK(hipEventRecord(ev[1], st));
+    r = run_ipm(c, B, st, warm, lists);
+    if (r != CMPC_OK) return r;
+  }
   if (ev) HIP_OK(hipEventRecord(ev[2], st));
   ExpandArgs e;
   e.model = c->d_model;

@@ -84,6 +84,9 @@ template <typename T>
 int launch_ipm(const IpmArgs<T>& a, int B, hipStream_t stream);
 int launch_ipm64(const IpmArgs<double>& a, int B, hipStream_t stream);   // n <= 64 (k_ipm64.hpp)
 int launch_ipm64(const IpmArgs<float>& a, int B, hipStream_t stream);
+// fused condensing + IPM of the n <= 64 class (k_solve64, k_ipm64.hpp); QPs with n > 64 only get their nvar hint
+int launch_solve64(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream);
+int launch_solve64(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)

@@ -35,6 +35,7 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
+#include "condense64.hpp"
 #include "step_ratio.hpp"
 #include "dpp_rows.hpp"
 #include "wave_dpp.hpp"
@@ -162,47 +163,93 @@ struct Lds {
 
 }  // namespace ipm64
 
-template <typename T, int WPE>
-__global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
+// LDS of the IPM; the fused kernel (k_solve64) runs the condensing first in the same bytes
+template <typename T, bool FUSED>
+struct IpmShared {
+  ipm64::Lds<T> ipm;
+};
+template <typename T>
+struct IpmShared<T, true> {
+  union {
+    ipm64::Lds<T> ipm;
+    c64::C64Lds<T> cond;
+  };
+};
+
+// One QP per wavefront. FUSED (k_solve64): the QP is condensed first by the same wave (condense64_qp, which also
+// writes H and the QP data to the workspace for the later iterations and the other stages) and the first Newton
+// matrix starts from the H the condensing leaves in registers; otherwise (k_ipm64) everything is read from the
+// workspace that a separate condensing launch filled.
+template <typename T, int WPE, bool FUSED>
+__device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseArgs<T>* C) {
   using namespace ipm64;
   IPM_STAMP_DECL;
   int q = blockIdx.x;
-  if (A.qlist[0]) {  // compacted class list: real QPs first, the surplus workgroups exit
+  if (!FUSED && A.qlist[0]) {  // compacted class list: real QPs first, the surplus workgroups exit
     if (q >= A.qcount[0]) return;
     q = A.qlist[0][q];
     if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
-  if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
-  const int n = A.nvar[q];
-  if (n > 64) return;  // served by the 128 class
+  __shared__ IpmShared<T, FUSED> SH;
+  Lds<T>& L = SH.ipm;
+  T K[64];
+  T g_v, mu_v;
+  T lo[2], hi[2], muc[2];
+  int n;
+  if constexpr (FUSED) {
+    n = condense64_qp<T>(*C, q, SH.cond, K, g_v, mu_v);
+    if (n < 0) return;  // invalid contact table (status written) or a bigger class (nvar hint written)
+    // pyramid rows j = lane + 64 cc: the bounds and friction coefficients the condensing just wrote to the
+    // workspace, taken from the model and its triple table in LDS before the IPM reuses those bytes
+    const DevModel* M = C->model;
+    const int lane_ = (int)threadIdx.x;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int j = lane_ + 64 * cc;
+      const bool on = j < 5 * (n / 3);
+      lo[cc] = T(0);
+      hi[cc] = on ? T(M->ub[j % 5]) : T(0);
+      muc[cc] = on ? T(M->mu[SH.cond.tleg[j / 5]]) : T(0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
+    n = A.nvar[q];
+    if (n > 64) return;  // served by the 128 class
+  }
   const int ld = A.ld;
   const int nt = n / 3;
   const int m = 5 * nt;
   const DevSettings S = A.s;
-  __shared__ Lds<T> L;
   int lane = (int)threadIdx.x;         // re-read opaquely at the top of every iteration
   const int lane0 = (int)threadIdx.x;  // plain lane id: lane masks only (hoisted into SGPR pairs)
 
   // ---- lane-per-variable data
   const bool vin = lane < n;
-  const T g_v = vin ? A.g[(size_t)q * ld + lane] : T(0);
-  const T mu_v = vin ? A.tri_mu[(size_t)q * (ld / 3) + lane / 3] : T(0);
+  if constexpr (!FUSED) {
+    g_v = vin ? A.g[(size_t)q * ld + lane] : T(0);
+    mu_v = vin ? A.tri_mu[(size_t)q * (ld / 3) + lane / 3] : T(0);
+  }
   // cold start (warm_start = 0): u = 0; warm start: u from the workspace (previous solution, cmpc_solve_batch_warm)
-  T u_v = (A.warm && vin) ? A.u[(size_t)q * ld + lane] : T(0);
-  if (A.warm) L.v[lane] = u_v;
+  T u_v = (!FUSED && A.warm && vin) ? A.u[(size_t)q * ld + lane] : T(0);
+  if (!FUSED && A.warm) L.v[lane] = u_v;
   cbar();
   // ---- pyramid rows j = lane + 64 cc: slacks of C u clipped at THR0, lam = mu0 / t
-  T tl[2], tu[2], ll[2], lu[2], lo[2], hi[2], muc[2];
+  T tl[2], tu[2], ll[2], lu[2];
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc) {
     const int j = lane + 64 * cc;
     const bool on = j < m;
     const int t = j / 5;
-    lo[cc] = on ? A.tri_lo[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
-    hi[cc] = on ? A.tri_hi[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
-    muc[cc] = on ? A.tri_mu[(size_t)q * (ld / 3) + t] : T(0);
+    if constexpr (!FUSED) {
+      lo[cc] = on ? A.tri_lo[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
+      hi[cc] = on ? A.tri_hi[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
+      muc[cc] = on ? A.tri_mu[(size_t)q * (ld / 3) + t] : T(0);
+    }
     T cu0 = T(0);
-    if (A.warm && on) cu0 = pyr_row<T>(j % 5, muc[cc], L.v[3 * t], L.v[3 * t + 1], L.v[3 * t + 2]);
+    if (!FUSED && A.warm && on) cu0 = pyr_row<T>(j % 5, muc[cc], L.v[3 * t], L.v[3 * t + 1], L.v[3 * t + 2]);
     tl[cc] = on ? fmax(cu0 - lo[cc], T(THR0)) : T(1);
     tu[cc] = on ? fmax(hi[cc] - cu0, T(THR0)) : T(1);
     ll[cc] = on ? T(S.mu0) / tl[cc] : T(0);
@@ -236,7 +283,6 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     return v;
   };
 
-  T K[64];
   T invd_v = T(1);
   T hu_v = T(0), rhs_v = T(0);
   T rg_v = T(0), du_v = T(0);
@@ -358,7 +404,12 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
   int it = 0;
   for (it = 0;; ++it) {
     progress_prio(it);  // cmpc_device.hpp
-    load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
+    if (!FUSED || it > 0) {
+      // fused: iteration 0 starts from the condensing's registers; the rows it stored are re-read from iteration 1
+      // on by the same lanes (the wait drains the stores before the first re-read)
+      if (FUSED && it == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
+    }
 #ifdef H_WAIT_STAMP  // diagnostic: time to the last H row (segment 3)
     IPM_STAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -672,6 +723,19 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     A.iters[q] = it;
   }
   IPM_STAMP_STORE(A.stamps, q);
+}
+
+template <typename T, int WPE>
+__global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
+  ipm64_body<T, WPE, false>(A, nullptr);
+}
+
+// Fused stage 1 + stage 2 for the n <= 64 class (cmpc_solve_batch, cold start): one launch condenses and solves
+// every QP of the class; QPs of the bigger classes only leave their nvar hint (k_class_lists, k_srbd_condense and
+// the 128 / 256 IPM kernels follow).
+template <typename T, int WPE>
+__global__ __launch_bounds__(64, WPE) void k_solve64(IpmArgs<T> A, CondenseArgs<T> C) {
+  ipm64_body<T, WPE, true>(A, &C);
 }
 
 }  // namespace cmpc

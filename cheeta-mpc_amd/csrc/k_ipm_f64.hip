@@ -7,6 +7,12 @@ int launch_ipm64(const IpmArgs<double>& a, int B, hipStream_t stream) {
   hipLaunchKernelGGL((k_ipm64<double, 2>), dim3(B), dim3(64), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+int launch_solve64(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL((k_solve64<double, 2>), dim3(B), dim3(64), 0, stream, a, c);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 
 // every QP is served by the size class of its condensed size (the other class's blocks exit at once)
 template <typename T>

@@ -80,6 +80,7 @@ def lib():
     L.cmpc_set_model.argtypes = [vp, P(Model)]
     L.cmpc_get_model.argtypes = [vp, P(Model)]
     L.cmpc_ctx_ld.argtypes = [vp]
+    L.cmpc_ctx_fused.argtypes = [vp]
     L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
     L.cmpc_solve_batch_warm.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, i, i, vp]
     L.cmpc_sqp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, i, i, i, vp]

@@ -131,6 +131,9 @@ int cmpc_set_model(cmpc_ctx* ctx, const cmpc_model* model); /* horizon N must no
 int cmpc_get_model(const cmpc_ctx* ctx, cmpc_model* out);
 /* Leading dimension (padded max condensed size) of the context's H workspace. */
 int cmpc_ctx_ld(const cmpc_ctx* ctx);
+/* 1 when a cold-start cmpc_solve_batch runs the fused condensing + IPM kernel for the n <= 64 class (N <= 21; the
+ * environment variable CMPC_FUSED=0 at cmpc_create selects the two separate launches instead), else 0. */
+int cmpc_ctx_fused(const cmpc_ctx* ctx);
 
 /* Full hot path: SRBD linearisation -> condensing (H, g) -> friction/force-bound stacking -> batched IPM ->
  * scatter to [N][L][3] (zeros for swing legs) and optional rollout. Device pointers, async on stream.
@@ -280,7 +283,9 @@ int cmpc_gather_shard(void* d_dst, size_t dst_offset_bytes, const void* d_src, s
 
 /* Per-stage device timing with HIP events recorded on the solve stream (used by bench.py for the roofline):
  * after cmpc_profile_begin, each cmpc_solve_batch records events around its three stages (condense, IPM, expand);
- * cmpc_profile_end synchronises and returns the summed milliseconds per stage and the number of calls. */
+ * cmpc_profile_end synchronises and returns the summed milliseconds per stage and the number of calls. On the fused
+ * path (cmpc_ctx_fused) the first stage is the fused condensing + IPM launch of the n <= 64 class and the second
+ * the bigger classes (class lists, their condensing and their IPM). */
 int cmpc_profile_begin(cmpc_ctx* ctx, int max_calls);
 int cmpc_profile_end(cmpc_ctx* ctx, double* ms_condense, double* ms_ipm, double* ms_expand, int* calls);
 

@@ -160,7 +160,12 @@ int main(int argc, char** argv) {
     CC(VARS[i].prep(&a, B, st, &vargs[i]));
     CK(hipStreamSynchronize(st));
   }
+  const bool repack = getenv("LAB_REPACK") && atoi(getenv("LAB_REPACK"));  // H freshly written before every run
   auto run_once = [&](int i, bool with_stamps) -> float {
+    if (repack) {
+      CC(cmpc_condense_batch(ctx, B, x0, xref, foot, contact, H, g, n, cst, st));
+      CC(launch_pack_qp(H, g, mu, lo, hi, n, CMPC_F64, ld, Hw, gw, muw, low, hiw, nw, s0, B, st));
+    }
     CK(hipMemcpyAsync(sw, s0, B * 4, hipMemcpyDeviceToDevice, st));
     CK(hipMemsetAsync(uw, 0, (size_t)B * ld * 8, st));
     CK(hipEventRecord(e0, st));
