@@ -48,6 +48,8 @@ struct cmpc_ctx {
   bool fused;
   double *lin, *uj, *uq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
+  void* res_scr;
+  double* res;
   // host-API staging (grown on demand, outside the async path)
   char* stage;
   size_t stage_bytes;
@@ -74,7 +76,8 @@ int ld_for(const cmpc_model& m) {
 }
 
 struct Layout {
-  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, qlist, qcount, lin, uj, uq, stq, itq, done, sqpi, qpi, cnt, total;
+  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, qlist, qcount, lin, uj, uq, stq, itq, done, sqpi, qpi, cnt, res_scr,
+      res, total;
 };
 
 Layout layout(int ld, int precision, int B) {
@@ -109,6 +112,8 @@ Layout layout(int ld, int precision, int B) {
   L.sqpi = take((size_t)B * sizeof(int));
   L.qpi = take((size_t)B * sizeof(int));
   L.cnt = take(sizeof(int));
+  L.res_scr = take((size_t)B * 3 * 256 * es);  // per-thread residual terms of the last IPM iteration
+  L.res = take((size_t)B * 4 * sizeof(double));  // final residuals (cmpc_get_residuals)
   L.total = o;
   return L;
 }
@@ -220,6 +225,8 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.warm = 0;
   a.s = dev_settings(c->settings);
   a.stamps = nullptr;
+  a.res_scr = (T*)c->res_scr;
+  a.res = c->res;
   for (int k = 0; k < 3; ++k) a.qlist[k] = nullptr;
   a.qcount = nullptr;
   return a;
@@ -461,6 +468,8 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->sqpi = (int*)(c->ws + L.sqpi);
   c->qpi = (int*)(c->ws + L.qpi);
   c->cnt = (int*)(c->ws + L.cnt);
+  c->res_scr = c->ws + L.res_scr;
+  c->res = (double*)(c->ws + L.res);
   c->qlist = (int*)(c->ws + L.qlist);
   c->qcount = (int*)(c->ws + L.qcount);
   if (hipMalloc((void**)&c->d_model, sizeof(DevModel)) != hipSuccess) {
@@ -511,6 +520,12 @@ int cmpc_get_model(const cmpc_ctx* c, cmpc_model* out) {
 
 int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
 int cmpc_ctx_fused(const cmpc_ctx* c) { return c && c->fused ? 1 : 0; }
+
+int cmpc_get_residuals(cmpc_ctx* c, int B, double* d_res, void* stream) {
+  if (!c || B < 0 || B > c->max_batch || (B > 0 && !d_res)) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  return launch_residuals(c->res, c->status, B, d_res, (hipStream_t)stream) == 0 ? CMPC_OK : CMPC_ERR_HIP;
+}
 
 int cmpc_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                      const uint8_t* contact, double* u, double* x, int* status, int* iters, void* stream) {

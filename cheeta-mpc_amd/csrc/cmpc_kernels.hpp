@@ -65,6 +65,10 @@ struct IpmArgs {
   int warm;     // warm start (hpipm_interface::Settings::warm_start, HpipmInterfaceSettings.h:54): u from a.u
   DevSettings s;
   unsigned long long* stamps;  // diagnostic builds only (-DCMPC_IPM_STAMPS): per-QP phase cycles, else null
+  // final residuals (cmpc_get_residuals), or null: res[q][4] = (stat, eq = 0, ineq, comp) at the iterate where the
+  // IPM stopped; res_scr [B][3][256] holds each thread's last (stat, ineq, comp) terms until the exit reduction
+  T* res_scr;
+  double* res;
   // per-class QP lists (k_class_lists), or null: size class c's kernel maps workgroup b < qcount[c] to QP
   // qlist[c][b] and lets the rest exit, so a mixed batch dispatches the real QPs of a class first
   const int* qlist[3];
@@ -91,6 +95,9 @@ int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 <
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
 int launch_ipm256(const IpmArgs<float>& a, int B, hipStream_t stream);
+
+// res[q][4] of the QPs the IPM ran; NaN for the others (status 5 / 6)
+int launch_residuals(const double* res_ws, const int* status, int B, double* out, hipStream_t stream);
 
 struct ExpandArgs {
   const DevModel* model;

@@ -152,6 +152,7 @@ struct Lds {
   // parked per-row state (one pyramid row per thread)
   T p_lo[256], p_hi[256], p_rl[256], p_ru[256], p_itl[256], p_itu[256], p_rml[256], p_rmu[256];
   T p_tl[256], p_tu[256], p_ll[256], p_lu[256], p_u[128], p_rg[128];  // iterate parked across the elimination
+  T p_res[3][256];  // this iteration's residual terms per thread (stat, ineq, comp), reduced at the exit
 };
 
 }  // namespace ipm128x
@@ -390,6 +391,9 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
       rg_i = isv ? hu + g_i - ctw : T(0);
     }
     const T rs = fabs(rg_i);
+    L.p_res[0][tid] = rs;  // this iteration's residual terms, reduced once at the exit
+    L.p_res[1][tid] = ri;
+    L.p_res[2][tid] = rc;
     ms = block_sum(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
     // non-finite residual anywhere -> NAN_SOL; stopping rule as a block vote (max <= tol iff all <= tol)
@@ -666,6 +670,23 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   if (tid == 0) {
     a.status[q] = status;
     a.iters[q] = it;
+  }
+  if (a.res) {  // block max of the last residual terms (each thread reads back what it stored)
+    const T r0 = wave_max_dpp(L.p_res[0][tid]), r1 = wave_max_dpp(L.p_res[1][tid]), r2 = wave_max_dpp(L.p_res[2][tid]);
+    __syncthreads();
+    if (lane0 == 0) {
+      L.red[wave0][0] = r0;
+      L.red[wave0][1] = r1;
+      L.red[wave0][2] = r2;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double* o = a.res + (size_t)q * 4;
+      o[0] = (double)fmax(fmax(L.red[0][0], L.red[1][0]), fmax(L.red[2][0], L.red[3][0]));
+      o[1] = 0.0;
+      o[2] = (double)fmax(fmax(L.red[0][1], L.red[1][1]), fmax(L.red[2][1], L.red[3][1]));
+      o[3] = (double)fmax(fmax(L.red[0][2], L.red[1][2]), fmax(L.red[2][2], L.red[3][2]));
+    }
   }
   X_STAMP_STORE(a.stamps, q);
 }

@@ -432,6 +432,13 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
       rs = fabs(rg_i);
     }
     block_reduce(rs, ri, rc, ms);
+    if (a.res && tid == 0) {  // block maxima of this iteration's residuals (the last write is the final one)
+      double* o = a.res + (size_t)q * 4;
+      o[0] = (double)rs;
+      o[1] = 0.0;
+      o[2] = (double)ri;
+      o[3] = (double)rc;
+    }
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
     if (!(isfinite(rs) && isfinite(ri) && isfinite(rc))) {
       status = CMPC_NAN_SOL;

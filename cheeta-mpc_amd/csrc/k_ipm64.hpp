@@ -470,6 +470,12 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
     }
     rg_v = vin ? hu + g_v - ctw : T(0);
     rs = fabs(rg_v);
+    if (A.res_scr) {  // this iteration's residual terms, reduced once at the exit
+      T* rp = A.res_scr + (size_t)q * 3 * 256 + lane;
+      rp[0] = rs;
+      rp[256] = ri;
+      rp[512] = rc;
+    }
     ms = wave_sum_dpp(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
     // a non-finite residual anywhere -> NAN_SOL; HPIPM's absolute stopping rule (tol_stat / tol_ineq / tol_comp)
@@ -721,6 +727,17 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
   if (lane == 0) {
     A.status[q] = status;
     A.iters[q] = it;
+  }
+  if (A.res) {  // max over the lanes of the last residual terms (the same lanes stored them)
+    const T* rp = A.res_scr + (size_t)q * 3 * 256 + lane;
+    const T r0 = wave_max_dpp(rp[0]), r1 = wave_max_dpp(rp[256]), r2 = wave_max_dpp(rp[512]);
+    if (lane == 0) {
+      double* o = A.res + (size_t)q * 4;
+      o[0] = (double)r0;
+      o[1] = 0.0;
+      o[2] = (double)r1;
+      o[3] = (double)r2;
+    }
   }
   IPM_STAMP_STORE(A.stamps, q);
 }

@@ -265,6 +265,20 @@ int launch_class_lists(const int* status, const int* nvar, int B, int by_status,
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// ------------------------------------------------------------------------------------------ solver statistics
+// cmpc_get_residuals: the IPM kernels' final residuals, NaN for QPs they did not run (status 5 / 6 or unset)
+__global__ void k_residuals(const double* res, const int* status, int B, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * B) return;
+  const int st = status[i / 4];
+  out[i] = (st >= CMPC_SUCCESS && st <= CMPC_NAN_SOL) ? res[i] : __builtin_nan("");
+}
+int launch_residuals(const double* res_ws, const int* status, int B, double* out, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_residuals, dim3((4 * B + 255) / 256), dim3(256), 0, stream, res_ws, status, B, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // ------------------------------------------------------------------------------------------ conversions
 __global__ void k_f32_to_f64(const float* in, double* out, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)

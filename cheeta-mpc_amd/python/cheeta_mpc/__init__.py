@@ -81,6 +81,7 @@ def lib():
     L.cmpc_get_model.argtypes = [vp, P(Model)]
     L.cmpc_ctx_ld.argtypes = [vp]
     L.cmpc_ctx_fused.argtypes = [vp]
+    L.cmpc_get_residuals.argtypes = [vp, C.c_int, d, vp]
     L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
     L.cmpc_solve_batch_warm.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, i, i, vp]
     L.cmpc_sqp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, i, i, i, vp]
@@ -263,6 +264,13 @@ class Engine:
         self.solve_device(B, d["x0"], d["xref"], d["foot"], d["contact"], u, x, st, it,
                           u_init=u if u_init is not None else None)
         return u.host(), (x.host() if want_x else None), st.host(), it.host()
+
+    def residuals(self, B):
+        """Final residuals of the last IPM run, [B, 4] = (stat, eq, ineq, comp) (cmpc_get_residuals)."""
+        r = DeviceArray((B, 4), np.float64)
+        _chk(lib().cmpc_get_residuals(self.ctx, B, r.ptr, None), "cmpc_get_residuals")
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return r.host()
 
     def sqp_solve(self, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7, want_x=True):
         """Batched SQP on the bilinear NLP (cmpc_sqp_solve_batch): (u, x, status, qp_iters, sqp_iters)."""

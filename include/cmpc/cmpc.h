@@ -289,6 +289,15 @@ int cmpc_gather_shard(void* d_dst, size_t dst_offset_bytes, const void* d_src, s
 int cmpc_profile_begin(cmpc_ctx* ctx, int max_calls);
 int cmpc_profile_end(cmpc_ctx* ctx, double* ms_condense, double* ms_ipm, double* ms_expand, int* calls);
 
+/* Solver statistics of the last IPM run on this context (cmpc_solve_batch[_warm], cmpc_qp_solve_batch,
+ * cmpc_sqp_solve_batch's last QP), mirroring d_ocp_qp_ipm_get_max_res_stat / _eq / _ineq / _comp as the reference
+ * reads them after a solve (HpipmInterface.cpp:459-489): d_res[q][4] = inf-norms at the iterate where the IPM stopped
+ * of the stationarity residual H u + g - C' lam, the equality residual (0: the condensed QP has no equality rows), the
+ * inequality residual (C u - lo - t_lo, hi - C u - t_hi) and the largest complementarity product t lam. NaN for QPs
+ * the IPM did not run (status INVALID_CONTACT / TOO_LARGE). Iteration counts come with the solve (d_iters). Device
+ * pointer, async on stream. */
+int cmpc_get_residuals(cmpc_ctx* ctx, int B, double* d_res, void* stream);
+
 /* Human-readable names. */
 const char* cmpc_status_string(int status);
 const char* cmpc_error_string(int err);
