@@ -64,7 +64,7 @@ enum cmpc_qp_status {
   CMPC_MAX_ITER = 1,         /* maximum number of iterations reached */
   CMPC_MIN_STEP = 2,         /* minimum step length reached */
   CMPC_NAN_SOL = 3,          /* NaN in computations / non-finite solution (HpipmInterface.cpp:290-295) */
-  CMPC_INCONS_EQ = 4,        /* inconsistent equality constraints (kept for ABI parity; never produced) */
+  CMPC_INCONS_EQ = 4,        /* inconsistent equality constraints (HpipmInterface path with constraints) */
   CMPC_INVALID_CONTACT = 5,  /* a horizon step has no stance leg: reference throws "mpc table invalid"
                                 (CentroidalMPC.cpp:328-330) */
   CMPC_TOO_LARGE = 6         /* condensed size exceeds what this build's kernels support */

@@ -124,8 +124,9 @@ class HpipmInterface {
   explicit HpipmInterface(OcpSize ocpSize = OcpSize(), const Settings& settings = Settings());
   ~HpipmInterface();
   void resize(OcpSize ocpSize);
-  /* Equality-free stages are solved on the device; a non-empty constraint set raises std::runtime_error
-   * (the reference maps constraints to lg = ug rows, HpipmInterface.cpp:223-264; see DESIGN.md scope). */
+  /* Solved on the device. constraints == nullptr: equality-free stages (cmpc_ocp_solve_batch_host); otherwise the
+   * rows C dx + D du + e = 0 are imposed as the reference's lg = ug rows (HpipmInterface.cpp:223-264) by
+   * cmpc_ocp_solve_batch_eq_host (x0-eliminated stage 0, redundant rows dropped, inconsistent rows -> INCONS_EQ). */
   hpipm_status solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dynamics,
                      std::vector<ScalarFunctionQuadraticApproximation>& cost,
                      std::vector<VectorFunctionLinearApproximation>* constraints, vector_array_t& stateTrajectory,
