@@ -235,14 +235,20 @@ def main():
                 "ms_per_launch": ms, "flops_counted": what}
 
     if fused:
-        # dominant kernel = k_solve64: condensing and IPM of the n <= 64 class in one launch; its algorithmic work is
-        # both stages' FLOPs of those QPs, its time the first profiled stage
+        # stage 1 = k_solve64: condensing and IPM of the n <= 64 class in one launch (its algorithmic work is both
+        # stages' FLOPs of those QPs); stage 2 = the bigger classes (their condensing + IPM).
+        # The roofline line is the dominant (longer) stage.
         f_small = float(fl_ipm[small].sum() + fl_cond[small].sum())
-        roofline = roof("k_solve64 (fused condensing + IPM, n<=64)", f_small, ms_cond, "valu", "k_solve64",
-                        "IPM + condensing FLOPs of the n<=64 QPs")
+        f_big = float(fl_ipm[~small].sum() + fl_cond[~small].sum())
+        r_small = roof("k_solve64 (fused condensing + IPM, n<=64)", f_small, ms_cond, "valu", "k_solve64",
+                       "IPM + condensing FLOPs of the n<=64 QPs")
+        r_big = roof("bigger classes (k_srbd_condense + k_ipm128x n<=128 / k_ipm_tiled n<=256)", f_big, ms_ipm,
+                     "valu", "k_ipm1", "IPM + condensing FLOPs of the n>64 QPs")
+        roofline, other = (r_small, r_big) if ms_cond >= ms_ipm else (r_big, r_small)
         stages = {"solve64_fused": ms_cond, "bigger_classes": ms_ipm, "expand": ms_exp}
-        f_all = float(fl_ipm.sum() + fl_cond.sum())
-        extra = {"roofline_solve": roof("whole solve (all classes, condensing + IPM)", f_all, ms_cond + ms_ipm,
+        f_all = f_small + f_big
+        extra = {"roofline_other_stage": other,
+                 "roofline_solve": roof("whole solve (all classes, condensing + IPM)", f_all, ms_cond + ms_ipm,
                                         "valu", "cmpc::k_", "IPM + condensing FLOPs of every QP")}
     else:
         roofline = roof("IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)", float(fl_ipm.sum()),

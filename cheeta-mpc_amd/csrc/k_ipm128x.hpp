@@ -480,15 +480,19 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
     // pivot at a time.
     T mp[8], mq[8];
     // multipliers of the pair from the two broadcast rows
-    auto pair_mult = [&](const T (&xp)[8], const T (&xq)[8], T dp, T kqp, T kpq, T kqq, int s, auto tp_) {
-      constexpr int tp = decltype(tp_)::value, tq = tp + 1;
-      const T invp = pivot_inv(dp);
+    // the pair's pivots and their reciprocals: scalar chain, started as soon as the pair's scalars are read so
+    // that its latency (two reciprocals in sequence) runs under the bulk FMAs of the previous pair
+    auto pair_piv = [&](T dp, T kqp, T kpq, T kqq, int s, T& invp, T& invq) {
+      invp = pivot_inv(dp);
       const T dq = fma(kqp, -(kpq * invp), kqq);
-      const T invq = pivot_inv(dq);
+      invq = pivot_inv(dq);
       if (tid == 0) {
         L.dg[s] = dp;
         L.dg[s + 1] = dq;
       }
+    };
+    auto pair_vec = [&](const T (&xp)[8], const T (&xq)[8], T kqp, T invp, T invq, auto tp_) {
+      constexpr int tp = decltype(tp_)::value, tq = tp + 1;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const T mv = -(xp[c] * invp);
@@ -539,9 +543,10 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
         }
         __syncthreads();
         {
-          T xp[8], xq[8], dp, kqp, kpq, kqq;
+          T xp[8], xq[8], dp, kqp, kpq, kqq, invp, invq;
           read_pair(0, xp, xq, dp, kqp, kpq, kqq, 0);
-          pair_mult(xp, xq, dp, kqp, kpq, kqq, 16 * c0, std::integral_constant<int, 0>{});
+          pair_piv(dp, kqp, kpq, kqq, 16 * c0, invp, invq);
+          pair_vec(xp, xq, kqp, invp, invq, std::integral_constant<int, 0>{});
         }
         sfor<0, 8>([&](auto b_) {
           constexpr int b = decltype(b_)::value;
@@ -567,7 +572,7 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
           }
           // next pair published: its first row and pivot scalars are read here, landing while the bulk runs (the
           // second row after it: registers)
-          T xp[8], xq[8], dp = T(0), kqp = T(0), kpq = T(0), kqq = T(0);
+          T xp[8], xq[8], dp = T(0), kqp = T(0), kpq = T(0), kqq = T(0), invp = T(0), invq = T(0);
           if constexpr (b < 7) {
 #ifdef X_BARRIER_STAMP  // diagnostic: time waiting at the pair barrier (segment 3)
             X_STAMP(2);
@@ -582,6 +587,7 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
             kpq = L.rowbuf[nb][0][tp + 3];
             kqp = L.rowbuf[nb][1][tp + 2];
             kqq = L.rowbuf[nb][1][tp + 3];
+            pair_piv(dp, kqp, kpq, kqq, 16 * c0 + tp + 2, invp, invq);
           }
           // bulk: register rows 1 .. 7 - c0 (row groups below the chunk), padding groups skipped
           sfor<1, 8>([&](auto r_) {
@@ -591,7 +597,7 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
           if constexpr (b < 7) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) xq[c] = L.rowbuf[nb][1][16 * c + lb0];
-            pair_mult(xp, xq, dp, kqp, kpq, kqq, 16 * c0 + tp + 2, std::integral_constant<int, tp + 2>{});
+            pair_vec(xp, xq, kqp, invp, invq, std::integral_constant<int, tp + 2>{});
           }
         });
         __syncthreads();  // rowbuf[0] is rewritten by the next chunk's first pair
