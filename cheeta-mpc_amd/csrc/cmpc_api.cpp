@@ -50,6 +50,8 @@ struct cmpc_ctx {
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
   double* res;
+  double* stats = nullptr;  // [max_batch][stats_rows][CMPC_STAT_COLS] (cmpc_enable_stats)
+  int stats_rows = 0;
   // host-API staging (grown on demand, outside the async path)
   char* stage;
   size_t stage_bytes;
@@ -227,6 +229,8 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.stamps = nullptr;
   a.res_scr = (T*)c->res_scr;
   a.res = c->res;
+  a.stats = c->stats;
+  a.stats_cap = c->stats_rows;
   for (int k = 0; k < 3; ++k) a.qlist[k] = nullptr;
   a.qcount = nullptr;
   return a;
@@ -490,6 +494,7 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (!c) return CMPC_ERR_ARG;
   if (c->own_ws && c->ws) (void)hipFree(c->ws);
   if (c->d_model) (void)hipFree(c->d_model);
+  if (c->stats) (void)hipFree(c->stats);
   if (c->stage) (void)hipFree(c->stage);
   if (c->pol) (void)hipFree(c->pol);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
@@ -520,6 +525,28 @@ int cmpc_get_model(const cmpc_ctx* c, cmpc_model* out) {
 
 int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
 int cmpc_ctx_fused(const cmpc_ctx* c) { return c && c->fused ? 1 : 0; }
+
+int cmpc_enable_stats(cmpc_ctx* c, int rows) {
+  if (!c || rows < 0 || rows > 4096) return CMPC_ERR_ARG;
+  if (c->stats) (void)hipFree(c->stats);
+  c->stats = nullptr;
+  c->stats_rows = 0;
+  if (rows == 0) return CMPC_OK;
+  if (hipMalloc((void**)&c->stats, (size_t)c->max_batch * rows * CMPC_STAT_COLS * sizeof(double)) != hipSuccess) {
+    c->stats = nullptr;
+    return CMPC_ERR_HIP;
+  }
+  c->stats_rows = rows;
+  return CMPC_OK;
+}
+
+int cmpc_get_stats(cmpc_ctx* c, int B, double* d_stats, void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !c->stats || (B > 0 && !d_stats)) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  HIP_OK(hipMemcpyAsync(d_stats, c->stats, (size_t)B * c->stats_rows * CMPC_STAT_COLS * sizeof(double),
+                        hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return CMPC_OK;
+}
 
 int cmpc_get_residuals(cmpc_ctx* c, int B, double* d_res, void* stream) {
   if (!c || B < 0 || B > c->max_batch || (B > 0 && !d_res)) return CMPC_ERR_ARG;

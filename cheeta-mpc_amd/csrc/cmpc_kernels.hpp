@@ -69,6 +69,9 @@ struct IpmArgs {
   // IPM stopped; res_scr [B][3][256] holds each thread's last (stat, ineq, comp) terms until the exit reduction
   T* res_scr;
   double* res;
+  // per-iteration statistics (cmpc_enable_stats), or null: stats[q][it][CMPC_STAT_COLS] for it < stats_cap
+  double* stats;
+  int stats_cap;
   // per-class QP lists (k_class_lists), or null: size class c's kernel maps workgroup b < qcount[c] to QP
   // qlist[c][b] and lets the rest exit, so a mixed batch dispatches the real QPs of a class first
   const int* qlist[3];

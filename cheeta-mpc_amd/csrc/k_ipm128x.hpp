@@ -153,6 +153,7 @@ struct Lds {
   T p_lo[256], p_hi[256], p_rl[256], p_ru[256], p_itl[256], p_itu[256], p_rml[256], p_rmu[256];
   T p_tl[256], p_tu[256], p_ll[256], p_lu[256], p_u[128], p_rg[128];  // iterate parked across the elimination
   T p_res[3][256];  // this iteration's residual terms per thread (stat, ineq, comp), reduced at the exit
+  T mu_st;          // this iteration's mu for the statistics row
 };
 
 }  // namespace ipm128x
@@ -347,6 +348,23 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
     return block_min(mr.value());
   };
 
+  // residual block maxima of the iteration whose terms are in L.p_res (written before a barrier) and its mu into a
+  // statistics row; run by wave 0 only
+  auto stats_res = [&](double* sr) {
+    T r[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      T v = fmax(fmax(L.p_res[k][lane0], L.p_res[k][lane0 + 64]), fmax(L.p_res[k][lane0 + 128], L.p_res[k][lane0 + 192]));
+      r[k] = wave_max_dpp(v);
+    }
+    if (lane0 == 0) {
+      sr[5] = (double)L.mu_st;
+      sr[6] = (double)r[0];
+      sr[7] = 0.0;
+      sr[8] = (double)r[1];
+      sr[9] = (double)r[2];
+    }
+  };
   for (it = 0;; ++it) {
     progress_prio(it);  // cmpc_device.hpp (lab, n = 120 fp64: 3.94 -> 3.91 ms)
     // ---- H: 64 loads per lane, 4 rows x 16 consecutive columns per instruction
@@ -396,6 +414,9 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
     L.p_res[2][tid] = rc;
     ms = block_sum(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
+    const bool st_on = a.stats && it < a.stats_cap;  // statistics row of this iteration (cmpc_enable_stats)
+    auto st_row = [&]() { return a.stats + ((size_t)q * a.stats_cap + it) * CMPC_STAT_COLS; };
+    if (st_on && tid == 0) L.mu_st = mu;  // the row's residual part is written at the end of the iteration / the exit
     // non-finite residual anywhere -> NAN_SOL; stopping rule as a block vote (max <= tol iff all <= tol)
     if (__syncthreads_or(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
       status = CMPC_NAN_SOL;
@@ -651,6 +672,12 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
       maff = block_sum(maff) / T(2 * m);
       const T ratio = maff / mu;
       const T sigma = ratio * ratio * ratio;
+      if (st_on && tid == 0) {
+        double* sr = st_row();
+        sr[0] = (double)alpha;
+        sr[1] = (double)maff;
+        sr[2] = (double)sigma;
+      }
       // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
       L.p_rml[tid] = con ? tl * ll + dtl * dll - sigma * mu : T(0);
       L.p_rmu[tid] = con ? tu * lu + dtu * dlu - sigma * mu : T(0);
@@ -658,6 +685,11 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
       alpha = fmin(T(1), T(TAU) * max_step());
     }
     X_STAMP(6);
+    if (st_on && tid == 0) {
+      double* sr = st_row();
+      if (m == 0) sr[0] = sr[1] = sr[2] = __builtin_nan("");
+      sr[3] = sr[4] = (double)alpha;
+    }  // one step length for primal and dual
     if (alpha < T(S.alpha_min)) {
       status = CMPC_MIN_STEP;
       break;
@@ -667,6 +699,7 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
     tu = fma(alpha, dtu, tu);
     ll = fma(alpha, dll, ll);
     lu = fma(alpha, dlu, lu);
+    if (st_on && wave0 == 0) stats_res(st_row());  // this iteration's residuals, still in L.p_res
     X_STAMP(7);
   }
 
@@ -676,6 +709,14 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
   if (tid == 0) {
     a.status[q] = status;
     a.iters[q] = it;
+  }
+  if (a.stats && it < a.stats_cap) {  // the stopping iteration's row: residuals and mu, no step
+    __syncthreads();
+    if (wave0 == 0) {
+      double* sr = a.stats + ((size_t)q * a.stats_cap + it) * CMPC_STAT_COLS;
+      if (lane0 < 5) sr[lane0] = __builtin_nan("");
+      stats_res(sr);
+    }
   }
   if (a.res) {  // block max of the last residual terms (each thread reads back what it stored)
     const T r0 = wave_max_dpp(L.p_res[0][tid]), r1 = wave_max_dpp(L.p_res[1][tid]), r2 = wave_max_dpp(L.p_res[2][tid]);

@@ -440,6 +440,17 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
       o[3] = (double)rc;
     }
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
+    const bool st_on = a.stats && it < a.stats_cap;  // statistics row of this iteration (cmpc_enable_stats)
+    auto st_row = [&]() { return a.stats + ((size_t)q * a.stats_cap + it) * CMPC_STAT_COLS; };
+    if (st_on && tid == 0) {  // statistics row: residuals (block maxima) and mu now, the step below
+      double* sr = st_row();
+      for (int k = 0; k < 5; ++k) sr[k] = __builtin_nan("");
+      sr[5] = (double)mu;
+      sr[6] = (double)rs;
+      sr[7] = 0.0;
+      sr[8] = (double)ri;
+      sr[9] = (double)rc;
+    }
     if (!(isfinite(rs) && isfinite(ri) && isfinite(rc))) {
       status = CMPC_NAN_SOL;
       break;
@@ -611,12 +622,22 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
       maff = block_sum(maff) / T(2 * m);
       const T ratio = maff / mu;
       const T sigma = ratio * ratio * ratio;
+      if (st_on && tid == 0) {
+        double* sr = st_row();
+        sr[0] = (double)alpha;
+        sr[1] = (double)maff;
+        sr[2] = (double)sigma;
+      }
       // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
       rml = con ? tl * ll + dtl * dll - sigma * mu : T(0);
       rmu = con ? tu * lu + dtu * dlu - sigma * mu : T(0);
       direction();
       alpha = fmin(T(1), T(TAU) * max_step());
     }
+    if (st_on && tid == 0) {
+      double* sr = st_row();
+      sr[3] = sr[4] = (double)alpha;
+    }  // one step length for primal and dual
     if (alpha < T(S.alpha_min)) {
       status = CMPC_MIN_STEP;
       break;

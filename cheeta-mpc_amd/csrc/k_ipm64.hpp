@@ -478,6 +478,24 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
     }
     ms = wave_sum_dpp(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
+#ifdef CMPC_NO_STATS  // lab: the statistics code compiled out (A/B of its cost)
+    constexpr bool st_on = false;
+#else
+    const bool st_on = A.stats && it < A.stats_cap;  // statistics row of this iteration (cmpc_enable_stats)
+#endif
+    auto st_row = [&]() { return A.stats + ((size_t)q * A.stats_cap + it) * CMPC_STAT_COLS; };
+    if (st_on) {  // statistics row of this iteration: residuals and mu now, the step below (NaN if none is taken)
+      const T r0 = wave_max_dpp(rs), r1 = wave_max_dpp(ri), r2 = wave_max_dpp(rc);
+      if (lane == 0) {
+        double* sr = st_row();
+        for (int k = 0; k < 5; ++k) sr[k] = __builtin_nan("");
+        sr[5] = (double)mu;
+        sr[6] = (double)r0;
+        sr[7] = 0.0;
+        sr[8] = (double)r1;
+        sr[9] = (double)r2;
+      }
+    }
     // a non-finite residual anywhere -> NAN_SOL; HPIPM's absolute stopping rule (tol_stat / tol_ineq / tol_comp)
     // as a wave vote: max over lanes <= tol iff every lane <= tol (no max-reductions needed)
     if (__any(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
@@ -679,6 +697,12 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
       maff = wave_sum_dpp(maff) / T(2 * m);
       const T ratio = maff / mu;
       const T sigma = ratio * ratio * ratio;
+      if (st_on && lane == 0) {
+        double* sr = st_row();
+        sr[0] = (double)alpha;
+        sr[1] = (double)maff;
+        sr[2] = (double)sigma;
+      }
       IPM_STAMP(5);
       // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
 #pragma unroll
@@ -694,6 +718,10 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
       alpha = fmin(T(1), max_step());
     }
     IPM_STAMP(6);
+    if (st_on && lane == 0) {
+      double* sr = st_row();
+      sr[3] = sr[4] = (double)alpha;
+    }  // one step length for primal and dual
     if (uflag(alpha < T(S.alpha_min))) {
       status = CMPC_MIN_STEP;
       break;

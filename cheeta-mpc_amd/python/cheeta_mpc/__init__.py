@@ -82,6 +82,8 @@ def lib():
     L.cmpc_ctx_ld.argtypes = [vp]
     L.cmpc_ctx_fused.argtypes = [vp]
     L.cmpc_get_residuals.argtypes = [vp, C.c_int, d, vp]
+    L.cmpc_enable_stats.argtypes = [vp, C.c_int]
+    L.cmpc_get_stats.argtypes = [vp, C.c_int, d, vp]
     L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
     L.cmpc_solve_batch_warm.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, i, i, vp]
     L.cmpc_sqp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, i, i, i, vp]
@@ -269,6 +271,21 @@ class Engine:
         """Final residuals of the last IPM run, [B, 4] = (stat, eq, ineq, comp) (cmpc_get_residuals)."""
         r = DeviceArray((B, 4), np.float64)
         _chk(lib().cmpc_get_residuals(self.ctx, B, r.ptr, None), "cmpc_get_residuals")
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return r.host()
+
+    STAT_COLS = ("alpha_aff", "mu_aff", "sigma", "alpha_prim", "alpha_dual", "mu", "res_stat", "res_eq", "res_ineq",
+                 "res_comp")
+
+    def enable_stats(self, rows):
+        """Record the per-iteration statistics table of every following IPM run (cmpc_enable_stats); 0 disables."""
+        _chk(lib().cmpc_enable_stats(self.ctx, rows), "cmpc_enable_stats")
+        self.stats_rows = rows
+
+    def stats(self, B):
+        """[B, rows, 10] per-iteration statistics of the last IPM run (columns STAT_COLS; cmpc_get_stats)."""
+        r = DeviceArray((B, self.stats_rows, len(self.STAT_COLS)), np.float64)
+        _chk(lib().cmpc_get_stats(self.ctx, B, r.ptr, None), "cmpc_get_stats")
         _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
         return r.host()
 

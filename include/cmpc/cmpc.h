@@ -298,6 +298,18 @@ int cmpc_profile_end(cmpc_ctx* ctx, double* ms_condense, double* ms_ipm, double*
  * pointer, async on stream. */
 int cmpc_get_residuals(cmpc_ctx* ctx, int B, double* d_res, void* stream);
 
+/* Per-iteration IPM statistics: the table HPIPM's printStatus prints from d_ocp_qp_ipm_get_stat after a solve
+ * (HpipmInterface.cpp:457-502). After cmpc_enable_stats(ctx, rows) every IPM run records, per QP and iteration
+ * it < rows, CMPC_STAT_COLS values: alpha_aff, mu_aff, sigma, alpha_prim, alpha_dual (one step length: equal), mu,
+ * res_stat, res_eq (0), res_ineq, res_comp, with the residuals and mu taken at the top of iteration it and the step
+ * quantities of the step taken from there (NaN where none was taken: the stopping row). Rows past a QP's last iteration
+ * are not written. rows = 0 disables recording (the default) and frees the buffer; enabling allocates
+ * max_batch * rows * CMPC_STAT_COLS doubles of device memory. cmpc_get_stats copies d_stats[B][rows][CMPC_STAT_COLS]
+ * (device pointer, async on stream); CMPC_ERR_ARG when recording is off. */
+#define CMPC_STAT_COLS 10
+int cmpc_enable_stats(cmpc_ctx* ctx, int rows);
+int cmpc_get_stats(cmpc_ctx* ctx, int B, double* d_stats, void* stream);
+
 /* Human-readable names. */
 const char* cmpc_status_string(int status);
 const char* cmpc_error_string(int err);

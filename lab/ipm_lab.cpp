@@ -143,6 +143,10 @@ int main(int argc, char** argv) {
   a.s.tol_ineq = s.tol_ineq;
   a.s.tol_comp = s.tol_comp;
   a.s.reg_prim = s.reg_prim;
+  if (getenv("LAB_RES") && atoi(getenv("LAB_RES"))) {  // the product's residual export buffers (cmpc_get_residuals)
+    a.res_scr = dmalloc<double>((size_t)B * 3 * 256);
+    a.res = dmalloc<double>((size_t)B * 4);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

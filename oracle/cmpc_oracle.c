@@ -505,21 +505,33 @@ static void dense_solve(void* vc, double* b) {
 }
 
 static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const double* tri_lo, const double* tri_hi,
-                      const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters, double* res);
+                      const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters, double* res,
+                      double* stats, int stats_rows);
 
 int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
                   const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters,
                   double* res) {
+  return oracle_qp_ipm_stats(n, ld, H, g, tri_mu, tri_lo, tri_hi, s, u, lam_lo, lam_hi, iters, res, NULL, 0);
+}
+
+int oracle_qp_ipm_stats(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
+                        const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi,
+                        int* iters, double* res, double* stats, int stats_rows) {
   double* buf = (double*)calloc((size_t)n * n + (size_t)n + 1, sizeof(double));
   dense_ops_ctx d = {n, ld, H, g, buf, buf + (size_t)n * n};
   qp_ops ops = {&d, dense_grad, dense_factor, dense_solve};
-  const int st = qp_ipm_run(n, &ops, tri_mu, tri_lo, tri_hi, s, u, lam_lo, lam_hi, iters, res);
+  const int st = qp_ipm_run(n, &ops, tri_mu, tri_lo, tri_hi, s, u, lam_lo, lam_hi, iters, res, stats, stats_rows);
   free(buf);
   return st;
 }
 
+/* Per-iteration statistics row (cmpc_enable_stats; the columns of HPIPM's stat table, HpipmInterface.cpp:476-502):
+ * alpha_aff, mu_aff, sigma, alpha_prim, alpha_dual, mu, res_stat, res_eq, res_ineq, res_comp; NaN for no step. */
+static double* stat_row(double* stats, int rows, int it) { return (stats && it < rows) ? stats + (size_t)it * 10 : NULL; }
+
 static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const double* tri_lo, const double* tri_hi,
-                      const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters, double* res) {
+                      const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters, double* res,
+                      double* stats, int stats_rows) {
   const int nt = n / 3, m = 5 * nt;
   ipm_ws W;
   double* buf = (double*)calloc(4 * (size_t)n + 1 + 15 * (size_t)(m + 1), sizeof(double));
@@ -573,6 +585,15 @@ static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const doub
       musum += cl + cu;
     }
     const double mu = m > 0 ? musum / (2.0 * m) : 0.0;
+    double* sr = stat_row(stats, stats_rows, it);
+    if (sr) {
+      for (int k = 0; k < 5; ++k) sr[k] = NAN;
+      sr[5] = mu;
+      sr[6] = rs;
+      sr[7] = 0.0;
+      sr[8] = ri;
+      sr[9] = rc;
+    }
     if (!isfinite(rs) || !isfinite(ri) || !isfinite(rc)) {
       status = CMPC_NAN_SOL;
       break;
@@ -608,6 +629,11 @@ static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const doub
       maff /= 2.0 * m;
       const double ratio = maff / mu;
       const double sigma = ratio * ratio * ratio;
+      if (sr) {
+        sr[0] = alpha;
+        sr[1] = maff;
+        sr[2] = sigma;
+      }
       /* corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu */
       for (int j = 0; j < m; ++j) {
         W.rml[j] = W.tl[j] * W.ll[j] + W.dtl[j] * W.dll[j] - sigma * mu;
@@ -616,6 +642,7 @@ static int qp_ipm_run(int n, const qp_ops* ops, const double* tri_mu, const doub
       ipm_dir(n, ops, nt, tri_mu, &W);
       alpha = dmin(1.0, TAU * ipm_maxstep(m, &W));
     }
+    if (sr) sr[3] = sr[4] = alpha;
     if (alpha < s->alpha_min) {
       status = CMPC_MIN_STEP;
       break;
@@ -1851,7 +1878,7 @@ int oracle_riccati_solve_one(const oracle_consts* c, const cmpc_settings* s, con
   cmpc_settings s2 = *s;
   s2.warm_start = 0;
   int it = 0;
-  st = qp_ipm_run(n, &ops, mu, lo, hi, &s2, uc, NULL, NULL, &it, NULL);
+  st = qp_ipm_run(n, &ops, mu, lo, hi, &s2, uc, NULL, NULL, &it, NULL, NULL, 0);
   for (int k = 0; k < N; ++k)
     for (int t = 0; t < r.nst[k]; ++t)
       for (int d = 0; d < 3; ++d) u[(k * L + r.legs[k][t]) * 3 + d] = uc[r.off[k] + 3 * t + d];

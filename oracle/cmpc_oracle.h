@@ -82,6 +82,10 @@ int oracle_condense(const oracle_consts* c, const double* x0, const double* xref
 int oracle_qp_ipm(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
                   const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi, int* iters,
                   double* res);
+/* Same, also recording the per-iteration statistics table stats[rows][10] (columns of cmpc_enable_stats). */
+int oracle_qp_ipm_stats(int n, int ld, const double* H, const double* g, const double* tri_mu, const double* tri_lo,
+                        const double* tri_hi, const cmpc_settings* s, double* u, double* lam_lo, double* lam_hi,
+                        int* iters, double* res, double* stats, int stats_rows);
 
 /* Whole hot path for one QP: u [N][L][3] (zeros for swing), x [(N+1)][13] (may be NULL). */
 /* u [N][L][3] out; with s->warm_start != 0 it is also the initial guess on entry (HPIPM warm_start = 1). */

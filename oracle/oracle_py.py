@@ -92,6 +92,7 @@ def lib():
         L.oracle_solve_batch.argtypes = [P(Model), P(Settings), C.c_int, d, d, d, u8, d, d, i, i, C.c_int]
         L.oracle_generate.argtypes = [P(Model), C.c_uint64, C.c_int64, C.c_int, C.c_int, d, d, d, u8]
         L.oracle_qp_ipm.argtypes = [C.c_int, C.c_int, d, d, d, d, d, P(Settings), d, d, d, i, d]
+        L.oracle_qp_ipm_stats.argtypes = [C.c_int, C.c_int, d, d, d, d, d, P(Settings), d, d, d, i, d, d, C.c_int]
         L.oracle_qp_kkt.argtypes = [C.c_int, C.c_int, d, d, d, d, d, d, d, d, d]
         L.oracle_ocp_record_size.restype = C.c_size_t
         L.oracle_ocp_record_size.argtypes = [C.c_int, C.c_int, i]
@@ -253,6 +254,22 @@ def sqp_solve(model, settings, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol
     st = lib().oracle_sqp_solve(C.byref(c), C.byref(settings), sqp_iter_max, sqp_tol, _p(x0), _p(xref), _p(foot),
                                 _p(contact, C.c_uint8), _p(u), _p(x), C.byref(qi), C.byref(si))
     return u, x, st, qi.value, si.value
+
+
+def qp_ipm_stats(n, H, g, mu, lo, hi, settings, rows):
+    """qp_ipm plus the per-iteration statistics table [rows, 10] (columns of cmpc_enable_stats; NaN = not written)."""
+    ld = H.shape[0]
+    H, g, mu, lo, hi = (np.ascontiguousarray(a, dtype=np.float64) for a in (H, g, mu, lo, hi))
+    u = np.zeros(max(n, 1))
+    m = max(5 * (n // 3), 1)
+    ll = np.zeros(m)
+    lu = np.zeros(m)
+    it = C.c_int(0)
+    res = np.zeros(4)
+    stats = np.full((rows, 10), np.nan)
+    st = lib().oracle_qp_ipm_stats(n, ld, _p(H), _p(g), _p(mu), _p(lo), _p(hi), C.byref(settings), _p(u), _p(ll),
+                                   _p(lu), C.byref(it), _p(res), _p(stats), rows)
+    return u[:n], st, it.value, res, stats
 
 
 def qp_ipm(n, H, g, mu, lo, hi, settings):
