@@ -50,6 +50,10 @@ struct cmpc_ctx {
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
   double* res;
+  void* mig;
+  int num_cu;  // compute units of the device (work-item kernel: one workgroup per CU)
+  bool items;  // fused path as IPM-iteration work items (k_solve64q), opt-in: CMPC_ITEMS=1 at cmpc_create (measured
+               // 7-17 % slower than k_solve64 on the headline; DESIGN.md "work items")
   double* stats = nullptr;  // [max_batch][stats_rows][CMPC_STAT_COLS] (cmpc_enable_stats)
   int stats_rows = 0;
   // host-API staging (grown on demand, outside the async path)
@@ -79,7 +83,7 @@ int ld_for(const cmpc_model& m) {
 
 struct Layout {
   size_t H, g, mu, lo, hi, u, map, nvar, status, iters, qlist, qcount, lin, uj, uq, stq, itq, done, sqpi, qpi, cnt, res_scr,
-      res, total;
+      res, mig, total;
 };
 
 Layout layout(int ld, int precision, int B) {
@@ -116,6 +120,7 @@ Layout layout(int ld, int precision, int B) {
   L.cnt = take(sizeof(int));
   L.res_scr = take((size_t)B * 3 * 256 * es);  // per-thread residual terms of the last IPM iteration
   L.res = take((size_t)B * 4 * sizeof(double));  // final residuals (cmpc_get_residuals)
+  L.mig = take((size_t)B * 10 * 64 * es);         // parked IPM state of the work-item kernel (k_solve64q)
   L.total = o;
   return L;
 }
@@ -229,6 +234,12 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.stamps = nullptr;
   a.res_scr = (T*)c->res_scr;
   a.res = c->res;
+  a.mig = (T*)c->mig;
+  {
+    const char* e = std::getenv("CMPC_ITEMS_PERIOD");  // diagnostics: iterations per work item
+    a.mig_period = e ? std::atoi(e) : 1;
+    if (a.mig_period < 1) a.mig_period = 1;
+  }
   a.stats = c->stats;
   a.stats_cap = c->stats_rows;
   for (int k = 0; k < 3; ++k) a.qlist[k] = nullptr;
@@ -307,7 +318,14 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
                 hipStream_t st, hipEvent_t ev1) {
   CondenseArgs<T> ca = condense_args<T>(c, x0, xref, foot, contact);
   const IpmArgs<T> ia = ipm_args<T>(c);
-  if (launch_solve64(ia, ca, B, st) != 0) return -2;
+  if (c->items && c->settings.iter_max < 4000) {  // an item carries its iteration in 12 bits
+    // one 8-wave workgroup per CU, each owning qpw consecutive QPs (8 <= qpw <= 256)
+    int qpw = (B + c->num_cu - 1) / c->num_cu;
+    qpw = qpw < 8 ? 8 : (qpw > 256 ? 256 : qpw);
+    if (launch_solve64q(ia, ca, B, qpw, st) != 0) return -2;
+  } else if (launch_solve64(ia, ca, B, st) != 0) {
+    return -2;
+  }
   if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
   if (c->ld < 128) return 0;
   if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
@@ -439,8 +457,14 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   {
     const char* f = std::getenv("CMPC_FUSED");
     c->fused = model->N <= CMPC_C64_MAXN && !(f && f[0] == '0');
+    const char* it = std::getenv("CMPC_ITEMS");
+    c->items = it && it[0] == '1';
   }
   (void)hipGetDevice(&c->device);
+  c->num_cu = 0;
+  if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+      c->num_cu <= 0)
+    c->num_cu = 256;
   const Layout L = layout(c->ld, precision, max_batch);
   c->ws_bytes = L.total;
   if (dev_mem) {
@@ -474,6 +498,7 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->cnt = (int*)(c->ws + L.cnt);
   c->res_scr = c->ws + L.res_scr;
   c->res = (double*)(c->ws + L.res);
+  c->mig = c->ws + L.mig;
   c->qlist = (int*)(c->ws + L.qlist);
   c->qcount = (int*)(c->ws + L.qcount);
   if (hipMalloc((void**)&c->d_model, sizeof(DevModel)) != hipSuccess) {

@@ -69,6 +69,9 @@ struct IpmArgs {
   // IPM stopped; res_scr [B][3][256] holds each thread's last (stat, ineq, comp) terms until the exit reduction
   T* res_scr;
   double* res;
+  // parked IPM state of the work-item kernel k_solve64q: [B][10][64] (u, H u, t_lo, t_hi, lam_lo, lam_hi)
+  T* mig;
+  int mig_period;  // k_solve64q: IPM iterations per work item (1)
   // per-iteration statistics (cmpc_enable_stats), or null: stats[q][it][CMPC_STAT_COLS] for it < stats_cap
   double* stats;
   int stats_cap;
@@ -94,6 +97,9 @@ int launch_ipm64(const IpmArgs<float>& a, int B, hipStream_t stream);
 // fused condensing + IPM of the n <= 64 class (k_solve64, k_ipm64.hpp); QPs with n > 64 only get their nvar hint
 int launch_solve64(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream);
 int launch_solve64(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream);
+// work-item form (k_solve64q): one 8-wave workgroup per qpw consecutive QPs, IPM iterations as items (a.mig)
+int launch_solve64q(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, int qpw, hipStream_t stream);
+int launch_solve64q(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, int qpw, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)

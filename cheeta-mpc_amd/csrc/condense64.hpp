@@ -90,7 +90,10 @@ __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int
   using MF = Mf64<T>;
   using acc_t = typename MF::acc_t;
   const DevModel* __restrict__ M = a.model;
-  const int lane = threadIdx.x;
+  // one wave per QP (also inside multi-wave workgroups); read opaquely so that lane-derived values are computed per
+  // QP, not hoisted out of an enclosing work-item loop (k_solve64q)
+  int lane = (int)(threadIdx.x & 63u);
+  asm volatile("" : "+v"(lane));
   const int g4 = lane >> 4, col = lane & 15;
   const int N = M->N;
   constexpr int L = NL;

@@ -131,7 +131,7 @@ __device__ __forceinline__ void sfor_down(F&& f) {  // E-1 down to B
 // write (or a write after a read) in program order sees the right data without s_waitcnt.
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ int olane() {
-  int l = (int)threadIdx.x;
+  int l = (int)(threadIdx.x & 63u);
   asm volatile("" : "+v"(l));
   return l;
 }
@@ -176,61 +176,71 @@ struct IpmShared<T, true> {
   };
 };
 
-// One QP per wavefront. FUSED (k_solve64): the QP is condensed first by the same wave (condense64_qp, which also
-// writes H and the QP data to the workspace for the later iterations and the other stages) and the first Newton
-// matrix starts from the H the condensing leaves in registers; otherwise (k_ipm64) everything is read from the
-// workspace that a separate condensing launch filled.
-template <typename T, int WPE, bool FUSED>
-__device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseArgs<T>* C) {
+// Body of one QP on one wavefront. MODE 0 (k_ipm64): everything is read from the workspace a separate condensing
+// launch filled. MODE 1 (k_solve64): the QP is condensed first by the same wave (condense64_qp, which also writes H
+// and the QP data to the workspace for the later iterations and the other stages) and the first Newton matrix starts
+// from the H the condensing leaves in registers. MODE 2 (k_solve64q, one work item): as MODE 1 when it0 == 0 (the
+// item condenses the QP), else the QP resumes at iteration it0 from the state an earlier item parked in A.mig; the
+// item runs ONE iteration and parks the state again. Returns the next iteration to run (MODE 2) or -1 when the QP
+// is finished (or not of this class).
+template <typename T, int WPE, int MODE>
+__device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArgs<T>* C,
+                                          IpmShared<T, (MODE > 0)>& SH, int q, int it0, int n_in = 0) {
+  constexpr bool FUSED = MODE > 0;
   using namespace ipm64;
   IPM_STAMP_DECL;
-  int q = blockIdx.x;
-  if (!FUSED && A.qlist[0]) {  // compacted class list: real QPs first, the surplus workgroups exit
-    if (q >= A.qcount[0]) return;
-    q = A.qlist[0][q];
-    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
-  }
-  __shared__ IpmShared<T, FUSED> SH;
+  const bool fresh = MODE < 2 || it0 == 0;
   Lds<T>& L = SH.ipm;
   T K[64];
   T g_v, mu_v;
   T lo[2], hi[2], muc[2];
   int n;
   if constexpr (FUSED) {
-    n = condense64_qp<T>(*C, q, SH.cond, K, g_v, mu_v);
-    if (n < 0) return;  // invalid contact table (status written) or a bigger class (nvar hint written)
-    // pyramid rows j = lane + 64 cc: the bounds and friction coefficients the condensing just wrote to the
-    // workspace, taken from the model and its triple table in LDS before the IPM reuses those bytes
-    const DevModel* M = C->model;
-    const int lane_ = (int)threadIdx.x;
+    if (fresh) {
+      n = condense64_qp<T>(*C, q, SH.cond, K, g_v, mu_v);
+      if (n < 0) return -1;  // invalid contact table (status written) or a bigger class (nvar hint written)
+      // pyramid rows j = lane + 64 cc: the bounds and friction coefficients the condensing just wrote to the
+      // workspace, taken from the model and its triple table in LDS before the IPM reuses those bytes
+      const DevModel* M = C->model;
+      const int lane_ = ipm64::olane();
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const int j = lane_ + 64 * cc;
-      const bool on = j < 5 * (n / 3);
-      lo[cc] = T(0);
-      hi[cc] = on ? T(M->ub[j % 5]) : T(0);
-      muc[cc] = on ? T(M->mu[SH.cond.tleg[j / 5]]) : T(0);
+      for (int cc = 0; cc < 2; ++cc) {
+        const int j = lane_ + 64 * cc;
+        const bool on = j < 5 * (n / 3);
+        lo[cc] = T(0);
+        hi[cc] = on ? T(M->ub[j % 5]) : T(0);
+        muc[cc] = on ? T(M->mu[SH.cond.tleg[j / 5]]) : T(0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+      // resumed item: n travels with the item. (Reading nvar[q] here would be a uniform load, i.e. a scalar-cache
+      // load, and the scalar cache does not see the vector store of another wave of this launch.)
+      n = n_in;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   } else {
-    if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
+    if (A.status[q] != CMPC_SUCCESS) return -1;  // invalid contact table / too large: status already set
     n = A.nvar[q];
-    if (n > 64) return;  // served by the 128 class
+    if (n > 64) return -1;  // served by the 128 class
   }
   const int ld = A.ld;
   const int nt = n / 3;
   const int m = 5 * nt;
   const DevSettings S = A.s;
-  int lane = (int)threadIdx.x;         // re-read opaquely at the top of every iteration
-  const int lane0 = (int)threadIdx.x;  // plain lane id: lane masks only (hoisted into SGPR pairs)
+  int lane = (int)(threadIdx.x & 63u);  // re-read opaquely at the top of every iteration
+  // plain lane id: lane masks only (hoisted into SGPR pairs); in item mode read opaquely per item, so that the masks
+  // are not hoisted out of the scheduler's loop (they would stay live across it and spill)
+  const int lane0 = MODE == 2 ? ipm64::olane() : (int)(threadIdx.x & 63u);
 
   // ---- lane-per-variable data
   const bool vin = lane < n;
-  if constexpr (!FUSED) {
-    g_v = vin ? A.g[(size_t)q * ld + lane] : T(0);
-    mu_v = vin ? A.tri_mu[(size_t)q * (ld / 3) + lane / 3] : T(0);
+  // item mode: data another wave of this workgroup wrote is visible after the ring's workgroup-scope acquire (one
+  // CU, one vector L1, no threadgroup split), so plain loads serve; nontemporal loads here cost 36 VGPR spills
+  auto ldx = [&](const T* p) -> T { return *p; };
+  if (!(FUSED && fresh)) {
+    g_v = vin ? ldx(A.g + (size_t)q * ld + lane) : T(0);
+    mu_v = vin ? ldx(A.tri_mu + (size_t)q * (ld / 3) + lane / 3) : T(0);
   }
   // cold start (warm_start = 0): u = 0; warm start: u from the workspace (previous solution, cmpc_solve_batch_warm)
   T u_v = (!FUSED && A.warm && vin) ? A.u[(size_t)q * ld + lane] : T(0);
@@ -243,10 +253,10 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
     const int j = lane + 64 * cc;
     const bool on = j < m;
     const int t = j / 5;
-    if constexpr (!FUSED) {
-      lo[cc] = on ? A.tri_lo[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
-      hi[cc] = on ? A.tri_hi[((size_t)q * (ld / 3) + t) * 5 + j % 5] : T(0);
-      muc[cc] = on ? A.tri_mu[(size_t)q * (ld / 3) + t] : T(0);
+    if (!(FUSED && fresh)) {
+      lo[cc] = on ? ldx(A.tri_lo + ((size_t)q * (ld / 3) + t) * 5 + j % 5) : T(0);
+      hi[cc] = on ? ldx(A.tri_hi + ((size_t)q * (ld / 3) + t) * 5 + j % 5) : T(0);
+      muc[cc] = on ? ldx(A.tri_mu + (size_t)q * (ld / 3) + t) : T(0);
     }
     T cu0 = T(0);
     if (!FUSED && A.warm && on) cu0 = pyr_row<T>(j % 5, muc[cc], L.v[3 * t], L.v[3 * t + 1], L.v[3 * t + 2]);
@@ -286,6 +296,20 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
   T invd_v = T(1);
   T hu_v = T(0), rhs_v = T(0);
   T rg_v = T(0), du_v = T(0);
+  // parked state of a resumed item (MODE 2): [u, H u, t_lo, t_hi, lam_lo, lam_hi (2 slots each)] x 64 lanes
+  auto mig_at = [&]() { return A.mig + (size_t)q * 10 * 64 + olane(); };  // recomputed where used (no live VGPR pair)
+  if (MODE == 2 && !fresh) {
+    const T* mig = mig_at();
+    u_v = ldx(mig);
+    hu_v = ldx(mig + 64);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      tl[cc] = ldx(mig + (2 + cc) * 64);
+      tu[cc] = ldx(mig + (4 + cc) * 64);
+      ll[cc] = ldx(mig + (6 + cc) * 64);
+      lu[cc] = ldx(mig + (8 + cc) * 64);
+    }
+  }
   T dtl[2], dtu[2], dll[2], dlu[2];
 
   // Solve K x = y with the eliminated tile (see the factorisation): strictly lower part S (X = L^-1 with
@@ -402,12 +426,13 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
 
   int status = CMPC_MAX_ITER;
   int it = 0;
-  for (it = 0;; ++it) {
-    progress_prio(it);  // cmpc_device.hpp
-    if (!FUSED || it > 0) {
+  for (it = (MODE == 2 ? it0 : 0);; ++it) {
+    if constexpr (MODE < 2) progress_prio(it);  // cmpc_device.hpp (item mode: items, not waves, balance the SIMD)
+    if (!(FUSED && fresh && it == 0)) {
       // fused: iteration 0 starts from the condensing's registers; the rows it stored are re-read from iteration 1
-      // on by the same lanes (the wait drains the stores before the first re-read)
-      if (FUSED && it == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // on by the same lanes (the wait drains the stores before the first re-read; in item mode the hand-off's
+      // release fence does)
+      if (MODE == 1 && it == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
     }
 #ifdef H_WAIT_STAMP  // diagnostic: time to the last H row (segment 3)
@@ -746,6 +771,19 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
       lu[cc] = fma(alpha, dlu[cc], lu[cc]);
     }
     IPM_STAMP(7);
+    if (MODE == 2 && it + 1 - it0 >= A.mig_period) {  // park the state; the next iteration is a new work item
+      T* mig = mig_at();
+      mig[0] = u_v;
+      mig[64] = hu_v;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        mig[(2 + cc) * 64] = tl[cc];
+        mig[(4 + cc) * 64] = tu[cc];
+        mig[(6 + cc) * 64] = ll[cc];
+        mig[(8 + cc) * 64] = lu[cc];
+      }
+      return (it + 1) | (n << 16);  // next iteration and the QP's size (k_solve64q item)
+    }
   }
 
   lane = olane();
@@ -768,11 +806,19 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
     }
   }
   IPM_STAMP_STORE(A.stamps, q);
+  return -1;
 }
 
 template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
-  ipm64_body<T, WPE, false>(A, nullptr);
+  int q = blockIdx.x;
+  if (A.qlist[0]) {  // compacted class list: real QPs first, the surplus workgroups exit
+    if (q >= A.qcount[0]) return;
+    q = A.qlist[0][q];
+    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
+  }
+  __shared__ IpmShared<T, false> SH;
+  (void)ipm64_body<T, WPE, 0>(A, nullptr, SH, q, 0);
 }
 
 // Fused stage 1 + stage 2 for the n <= 64 class (cmpc_solve_batch, cold start): one launch condenses and solves
@@ -780,7 +826,103 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
 // the 128 / 256 IPM kernels follow).
 template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_solve64(IpmArgs<T> A, CondenseArgs<T> C) {
-  ipm64_body<T, WPE, true>(A, &C);
+  __shared__ IpmShared<T, true> SH;
+  (void)ipm64_body<T, WPE, 1>(A, &C, SH, (int)blockIdx.x, 0);
+}
+
+// Work-item form of k_solve64 (cmpc_solve_batch, cold start, n <= 64 class): one workgroup of 8 waves per CU owns
+// qpw consecutive QPs and hands their IPM iterations to its waves one at a time from a FIFO in LDS; a wave runs one
+// iteration of one QP (the first item of a QP also condenses it), parks the QP's state in A.mig (≈ 5 KB) and takes
+// the next item. Why: with one QP per wave, the batch runs in rounds of whole QPs and the two waves of a SIMD finish
+// theirs at different times (the older wave wins arbitration; lab timeline: 145 vs 190-230 us), so a 4096-QP launch
+// ends with one wave per SIMD for ~60 us; with iteration items every wave stays busy until the last few items.
+// The hand-off stays inside the CU: state stores, a workgroup-scope release, the FIFO entry (LDS); the consumer's
+// workgroup-scope acquire, then the loads (HIP's workgroup scope: every wave of the workgroup is on this CU).
+// FIFO: ring of R = qpw + 8 entries {sequence (position + 1), item (QP index | iteration << 16)}; a wave reserves
+// a position with an LDS atomic and waits for that position's sequence; pushes go to the tail position. At most qpw
+// items are queued and at most 8 positions are reserved and unread, so R never wraps onto an unread entry. Waves
+// leave when every QP of the workgroup is finished; waits are bounded (no hang if an item is ever lost).
+constexpr int kSolve64qMaxQpw = 256;
+template <typename T>
+__global__ __launch_bounds__(512, 1) void k_solve64q(IpmArgs<T> A, CondenseArgs<T> C, int B, int qpw,
+                                                      unsigned spin_max) {
+  __shared__ IpmShared<T, true> SH[8];
+  __shared__ unsigned long long ring[kSolve64qMaxQpw + 8];
+  __shared__ int qhead, qtail, qdone;
+  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+  const int q0 = (int)blockIdx.x * qpw;
+  const int qn = min(qpw, B - q0);
+  if (qn <= 0) return;
+  const unsigned R = (unsigned)qpw + 8u;
+  // every entry is written: positions < qn hold the fresh QPs (iteration 0), the rest sequence 0, which no position
+  // waits for (LDS keeps the previous launch's FIFO, whose sequences would otherwise match)
+  for (int p = (int)threadIdx.x; p < (int)R; p += (int)blockDim.x)
+    ring[p] = p < qn ? (((unsigned long long)(p + 1) << 32) | (unsigned)p) : 0ull;
+  if (threadIdx.x == 0) {
+    qhead = 0;
+    qtail = qn;
+    qdone = 0;
+  }
+  __syncthreads();
+  // FIFO words are read and written by LDS atomics (ds_*: the shared arrays keep their address space); every
+  // decision is taken on wave-uniform values (readfirstlane), so the waits are scalar loops
+  auto ld_entry = [&](unsigned slot) -> unsigned long long {
+    return __hip_atomic_load(&ring[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  // every wave handles at most qn * (iter_max + 1) items (a guard: the FIFO never holds more)
+  const int item_max = qn * (A.s.iter_max + 1);
+  for (int items = 0; items < item_max; ++items) {
+    int pos = 0;
+    if (lane == 0) pos = atomicAdd(&qhead, 1);
+    pos = __builtin_amdgcn_readfirstlane(pos);
+    const unsigned slot = (unsigned)pos % R;
+    unsigned item = 0;
+    bool got = false;
+    for (unsigned spins = 0; spins < spin_max; ++spins) {
+      const unsigned long long e = ld_entry(slot);
+      const unsigned seq = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(e >> 32));
+      if (seq == (unsigned)(pos + 1)) {
+        item = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)e);
+        got = true;
+        break;
+      }
+      const int d = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&qdone, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (d >= qn) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!got) {
+#ifdef CMPC_ITEMS_DEBUG
+      if (lane == 0 && qdone < qn) printf("k_solve64q wg %d wave %d: gave up at pos %d (head %d tail %d done %d/%d)\n",
+                                          (int)blockIdx.x, w, pos, qhead, qtail, qdone, qn);
+#endif
+      break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // item: QP index (8 bits) | iteration (12 bits) << 8 | n (7 bits) << 20
+    const int ql = (int)(item & 0xffu), it = (int)((item >> 8) & 0xfffu), n_item = (int)(item >> 20);
+    if (ql >= qn || n_item > 64) break;  // not an item of this launch (cannot happen; never touch memory for it)
+    // the item's result is wave-uniform by construction; readfirstlane makes that explicit to the compiler (the
+    // scheduler's branches then stay scalar), and a result outside [1, iter_max + 1] ends the QP
+    const int r = __builtin_amdgcn_readfirstlane(ipm64_body<T, 2, 2>(A, &C, SH[w], q0 + ql, it, n_item));
+    int next = r < 0 ? -1 : (r & 0xffff);
+    const int n_next = r < 0 ? 0 : (r >> 16);
+    if (next <= it || next > A.s.iter_max + 1 || next > 0xfff) next = -1;
+    if (next < 0) {
+      if (lane == 0) atomicAdd(&qdone, 1);
+    } else {
+      // the parked state (and H, g, the pyramid data of a first item) must be written before the FIFO entry: the
+      // workgroup-scope release alone lowers to an LDS wait only (no vmcnt) on gfx950, hence the explicit drain
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) {
+        const int p = atomicAdd(&qtail, 1);
+        __hip_atomic_store(&ring[(unsigned)p % R],
+                           ((unsigned long long)(p + 1) << 32) | (unsigned)(ql | (next << 8) | (n_next << 20)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
 }
 
 }  // namespace cmpc
