@@ -52,6 +52,7 @@ struct cmpc_ctx {
   double* res;
   void* mig;
   int num_cu;  // compute units of the device (work-item kernel: one workgroup per CU)
+  bool direct;  // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   bool items;  // fused path as IPM-iteration work items (k_solve64q), opt-in: CMPC_ITEMS=1 at cmpc_create (measured
                // 7-17 % slower than k_solve64 on the headline; DESIGN.md "work items")
   double* stats = nullptr;  // [max_batch][stats_rows][CMPC_STAT_COLS] (cmpc_enable_stats)
@@ -244,6 +245,11 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.stats_cap = c->stats_rows;
   for (int k = 0; k < 3; ++k) a.qlist[k] = nullptr;
   a.qcount = nullptr;
+  a.out_u = nullptr;
+  a.out_status = nullptr;
+  a.out_iters = nullptr;
+  a.tri_map = c->tri_map;
+  a.out_nu = c->model.N * 12;
   return a;
 }
 
@@ -313,11 +319,16 @@ int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, boo
 // matrix starts from the condensing's registers instead of an H round trip); the bigger classes follow as before:
 // their nvar hints -> k_class_lists -> workgroup condensing -> their IPM kernels. ev1 (profiling) is recorded after
 // the fused launch.
+// out_u != null: every IPM kernel scatters its QPs' results into the caller's u / status / iters (no k_expand launch;
+// the rejected QPs are written by k_solve64, which sees them first).
 template <typename T>
 int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot, const uint8_t* contact,
-                hipStream_t st, hipEvent_t ev1) {
+                hipStream_t st, hipEvent_t ev1, double* out_u, int* out_status, int* out_iters) {
   CondenseArgs<T> ca = condense_args<T>(c, x0, xref, foot, contact);
-  const IpmArgs<T> ia = ipm_args<T>(c);
+  IpmArgs<T> ia = ipm_args<T>(c);
+  ia.out_u = out_u;
+  ia.out_status = out_status;
+  ia.out_iters = out_iters;
   if (c->items && c->settings.iter_max < 4000) {  // an item carries its iteration in 12 bits
     // one 8-wave workgroup per CU, each owning qpw consecutive QPs (8 <= qpw <= 256)
     int qpw = (B + c->num_cu - 1) / c->num_cu;
@@ -459,6 +470,8 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     c->fused = model->N <= CMPC_C64_MAXN && !(f && f[0] == '0');
     const char* it = std::getenv("CMPC_ITEMS");
     c->items = it && it[0] == '1';
+    const char* di = std::getenv("CMPC_DIRECT");  // diagnostics: 0 = results through k_expand on the fused path
+    c->direct = !(di && di[0] == '0');
   }
   (void)hipGetDevice(&c->device);
   c->num_cu = 0;
@@ -594,9 +607,15 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
   if (c->profiling && c->prof_calls < c->prof_max) ev = &c->prof_ev[(size_t)4 * c->prof_calls++];
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   const int warm = (u_init && c->settings.warm_start != 0) ? 1 : 0;
+  // fused path without rollout: the IPM kernels write u / status / iters themselves (no k_expand)
+  const bool direct = c->direct && !warm && c->fused && x == nullptr && c->model.N * 12 <= 256;
   if (!warm && c->fused) {
-    const int rf = c->precision == CMPC_F64 ? run_fused_t<double>(c, B, x0, xref, foot, contact, st, ev ? ev[1] : nullptr)
-                                            : run_fused_t<float>(c, B, x0, xref, foot, contact, st, ev ? ev[1] : nullptr);
+    double* du = direct ? u : nullptr;
+    int* ds = direct ? status : nullptr;
+    int* di = direct ? iters : nullptr;
+    const int rf = c->precision == CMPC_F64
+                       ? run_fused_t<double>(c, B, x0, xref, foot, contact, st, ev ? ev[1] : nullptr, du, ds, di)
+                       : run_fused_t<float>(c, B, x0, xref, foot, contact, st, ev ? ev[1] : nullptr, du, ds, di);
     if (rf != 0) return CMPC_ERR_HIP;
   } else {
     bool lists = false;
@@ -610,6 +629,10 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
     if (r != CMPC_OK) return r;
   }
   if (ev) HIP_OK(hipEventRecord(ev[2], st));
+  if (direct) {
+    if (ev) HIP_OK(hipEventRecord(ev[3], st));
+    return CMPC_OK;
+  }
   ExpandArgs e;
   e.model = c->d_model;
   e.ld = c->ld;

@@ -149,4 +149,25 @@ __device__ __forceinline__ void progress_prio(int it) {
   else __builtin_amdgcn_s_setprio(0);
 }
 
+// Result scatter of one QP into the caller's arrays from the IPM kernel's epilogue (the fused path without rollout;
+// k_misc.hip:expand_one is the stand-alone k_expand form; layout of CentroidalMPC.cpp:337-345): out_u[q] =
+// [N][4][3] doubles, zero for swing legs and everywhere for a QP without a solution (n = 0), variable i at
+// (tri_map[i / 3], i % 3); out_status[q], out_iters[q]. Every thread of the QP's group calls it (tid < nthr); thread
+// i < n supplies variable i; buf: >= out_nu entries of LDS the group no longer reads; sync: the group's barrier.
+template <typename T, typename Args, typename Sync>
+__device__ __forceinline__ void scatter_result(const Args& a, int q, int n, T ui, int status, int iters, T* buf,
+                                               int tid, int nthr, Sync sync) {
+  const int nu = a.out_nu;
+  for (int p = tid; p < nu; p += nthr) buf[p] = T(0);
+  sync();
+  if (tid < n) buf[a.tri_map[(size_t)q * (a.ld / 3) + tid / 3] * 3 + tid % 3] = ui;
+  sync();
+  double* uo = a.out_u + (size_t)q * nu;
+  for (int p = tid; p < nu; p += nthr) uo[p] = (double)buf[p];
+  if (tid == 0) {
+    a.out_status[q] = status;
+    if (a.out_iters) a.out_iters[q] = iters;
+  }
+}
+
 }  // namespace cmpc

@@ -79,6 +79,14 @@ struct IpmArgs {
   // qlist[c][b] and lets the rest exit, so a mixed batch dispatches the real QPs of a class first
   const int* qlist[3];
   const int* qcount;
+  // result scatter in the kernel's epilogue (fused cold-start path without rollout: no k_expand launch), or
+  // out_u = null: out_u[q] = [N][4][3] doubles (zero for swing legs), out_status[q], out_iters[q] (may be null);
+  // tri_map[q][ld / 3] = k * 4 + leg of the QP's triple t (written by the condensing); out_nu = 12 N <= 256
+  double* out_u;
+  int* out_status;
+  int* out_iters;
+  const int* tri_map;
+  int out_nu;
 };
 
 // one size class of the workgroup condensing kernel: npad 128 (64 < n <= 128, or n <= 128 when n_lo = 0) or 256

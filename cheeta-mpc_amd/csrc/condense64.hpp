@@ -80,9 +80,9 @@ struct C64Lds {
 // One QP's condensing (lane c owns Bqp column c). Writes H (tile order), g, the pyramid data, tri_map, status and
 // nvar to the workspace exactly as the stand-alone kernel always did, and also hands the result to a fused caller:
 // K = H in the 4 x 16-cyclic register tile of k_ipm64, g_out = g[lane], mu_out = the friction coefficient of the
-// lane's force triple. Returns n, or -1 when the IPM has nothing to do here (invalid contact table: status written;
-// n > 64: left to the bigger classes with the nvar hint).
-template <typename T>
+// lane's force triple. Returns n, or < 0 when the IPM has nothing to do here: -2 invalid contact table (status
+// written), -1 n > 64 (left to the bigger classes with the nvar hint).
+template <typename T, bool MASK = false>
 __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int q, c64::C64Lds<T>& S, T (&K)[64],
                                              T& g_out, T& mu_out) {
   using namespace c64;
@@ -90,10 +90,10 @@ __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int
   using MF = Mf64<T>;
   using acc_t = typename MF::acc_t;
   const DevModel* __restrict__ M = a.model;
-  // one wave per QP (also inside multi-wave workgroups); read opaquely so that lane-derived values are computed per
-  // QP, not hoisted out of an enclosing work-item loop (k_solve64q)
-  int lane = (int)(threadIdx.x & 63u);
-  asm volatile("" : "+v"(lane));
+  // one wave per QP; MASK (k_solve64q: eight waves per workgroup): the lane is read opaquely so that lane-derived
+  // values are computed per QP, not hoisted out of the enclosing work-item loop
+  int lane = MASK ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
+  if constexpr (MASK) asm volatile("" : "+v"(lane));
   const int g4 = lane >> 4, col = lane & 15;
   const int N = M->N;
   constexpr int L = NL;
@@ -119,7 +119,7 @@ __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int
       a.status[q] = CMPC_INVALID_CONTACT;
       a.nvar[q] = 0;
     }
-    return -1;
+    return -2;
   }
   if (n > 64) {  // a bigger class; the hint lets its condensing kernel skip every QP handled here at once
     if (lane == 0) a.nvar[q] = n;

@@ -710,6 +710,10 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
     a.status[q] = status;
     a.iters[q] = it;
   }
+  if (a.out_u) {  // the pyramid bounds in L.p_lo are dead by now
+    __syncthreads();
+    scatter_result<T>(a, q, n, u_i, status, it, L.p_lo, tid, 256, [] { __syncthreads(); });
+  }
   if (a.stats && it < a.stats_cap) {  // the stopping iteration's row: residuals and mu, no step
     __syncthreads();
     if (wave0 == 0) {

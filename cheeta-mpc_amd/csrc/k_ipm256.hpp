@@ -657,6 +657,10 @@ __global__ __launch_bounds__(32 * NT, 2) void k_ipm_tiled(IpmArgs<T> a) {  // 2 
     a.status[q] = status;
     a.iters[q] = it;
   }
+  if (a.out_u) {  // the constraint-side vector L.w (NTHR >= 256 entries) is dead by now
+    __syncthreads();
+    scatter_result<T>(a, q, n, u_i, status, it, L.w, tid, NTHR, [] { __syncthreads(); });
+  }
 }
 
 }  // namespace cmpc

@@ -130,8 +130,10 @@ __device__ __forceinline__ void sfor_down(F&& f) {  // E-1 down to B
 // Compiler-only ordering of LDS accesses: one wave's DS instructions execute in order, so a read issued after a
 // write (or a write after a read) in program order sees the right data without s_waitcnt.
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
+// MASK: the wave's lane inside a multi-wave workgroup (k_solve64q); the one-wave kernels take threadIdx.x as is
+template <bool MASK = false>
 __device__ __forceinline__ int olane() {
-  int l = (int)(threadIdx.x & 63u);
+  int l = MASK ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
   asm volatile("" : "+v"(l));
   return l;
 }
@@ -185,7 +187,12 @@ struct IpmShared<T, true> {
 // is finished (or not of this class).
 template <typename T, int WPE, int MODE>
 __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArgs<T>* C,
-                                          IpmShared<T, (MODE > 0)>& SH, int q, int it0, int n_in = 0) {
+                                          IpmShared<T, (MODE > 0)>* SHp, int q, int it0, int n_in = 0) {
+  // one-wave kernels: the LDS block is declared here, so its accesses keep a constant base (as a reference from the
+  // kernel, ds_write2 / ds_read2 pairing is lost: +640 instructions, +3 % time); item mode: the wave's block
+  // (item mode: the wave's block of the kernel's array; the pairing is lost there either way, by the wave's base)
+  __shared__ IpmShared<T, (MODE > 0)> SHl;
+  IpmShared<T, (MODE > 0)>& SH = MODE == 2 ? *SHp : SHl;
   constexpr bool FUSED = MODE > 0;
   using namespace ipm64;
   IPM_STAMP_DECL;
@@ -197,12 +204,17 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   int n;
   if constexpr (FUSED) {
     if (fresh) {
-      n = condense64_qp<T>(*C, q, SH.cond, K, g_v, mu_v);
-      if (n < 0) return -1;  // invalid contact table (status written) or a bigger class (nvar hint written)
+      n = condense64_qp<T, MODE == 2>(*C, q, SH.cond, K, g_v, mu_v);
+      if (n < 0) {  // invalid contact table (status written) or a bigger class (nvar hint written)
+        if (n == -2 && A.out_u)  // the rejected QP's result: zeros, INVALID_CONTACT, no iterations
+          scatter_result<T>(A, q, 0, T(0), CMPC_INVALID_CONTACT, 0, SH.ipm.scr, olane<MODE == 2>(), 64,
+                            [] { ipm64::cbar(); });
+        return -1;
+      }
       // pyramid rows j = lane + 64 cc: the bounds and friction coefficients the condensing just wrote to the
       // workspace, taken from the model and its triple table in LDS before the IPM reuses those bytes
       const DevModel* M = C->model;
-      const int lane_ = ipm64::olane();
+      const int lane_ = MODE == 2 ? ipm64::olane<true>() : (int)threadIdx.x;
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
         const int j = lane_ + 64 * cc;
@@ -228,10 +240,10 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   const int nt = n / 3;
   const int m = 5 * nt;
   const DevSettings S = A.s;
-  int lane = (int)(threadIdx.x & 63u);  // re-read opaquely at the top of every iteration
+  int lane = MODE == 2 ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;  // re-read opaquely at every iteration
   // plain lane id: lane masks only (hoisted into SGPR pairs); in item mode read opaquely per item, so that the masks
   // are not hoisted out of the scheduler's loop (they would stay live across it and spill)
-  const int lane0 = MODE == 2 ? ipm64::olane() : (int)(threadIdx.x & 63u);
+  const int lane0 = MODE == 2 ? ipm64::olane<true>() : (int)threadIdx.x;
 
   // ---- lane-per-variable data
   const bool vin = lane < n;
@@ -297,7 +309,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   T hu_v = T(0), rhs_v = T(0);
   T rg_v = T(0), du_v = T(0);
   // parked state of a resumed item (MODE 2): [u, H u, t_lo, t_hi, lam_lo, lam_hi (2 slots each)] x 64 lanes
-  auto mig_at = [&]() { return A.mig + (size_t)q * 10 * 64 + olane(); };  // recomputed where used (no live VGPR pair)
+  auto mig_at = [&]() { return A.mig + (size_t)q * 10 * 64 + olane<MODE == 2>(); };  // recomputed where used (no live VGPR pair)
   if (MODE == 2 && !fresh) {
     const T* mig = mig_at();
     u_v = ldx(mig);
@@ -318,7 +330,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   //   forward  t = D^-1 y;  z = D^-1 (y - S t)            row sums: 16 partials per lane, reduced through LDS
   //   backward x = z - D^-1 (S' z)                         column sums: 4 partials per lane, reduced through LDS
   auto solve = [&](T& y) {
-    const int ol = olane();
+    const int ol = olane<MODE == 2>();
     const int ola = ol >> 4, olb = ol & 15;
     L.v[ol] = y * invd_v;
     cbar();
@@ -372,7 +384,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   const T* Hq = A.H + (size_t)q * ld * ld;
   // H in tile order (64 coalesced 512-B rows) into the registers of the factor
   auto load_H = [&]() {
-    const int ln = olane();
+    const int ln = olane<MODE == 2>();
 #pragma unroll
     for (int e = 0; e < 64; ++e) K[e] = Hq[e * 64 + ln];
   };
@@ -440,7 +452,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     IPM_STAMP(3);
 #endif
-    lane = olane();
+    lane = olane<MODE == 2>();
     const int la = lane >> 4, lb = lane & 15;
 
     // ---- residuals that do not need H: C u, slack/complementarity residuals, C' lam
@@ -754,7 +766,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     u_v = fma(alpha, du_v, u_v);
     // H du = K du - (C' Sigma C + reg I) du = rhs - D du (D: the 3x3 blocks of this iteration, du still in L.v)
     {
-      const int ln = olane();
+      const int ln = olane<MODE == 2>();
       const int t3 = 3 * (ln / 3), e = ln - t3;
       T ddu = T(0);
       if (vin) {
@@ -786,7 +798,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     }
   }
 
-  lane = olane();
+  lane = olane<MODE == 2>();
   const bool fin = isfinite(u_v);
   if (lane < ld) A.u[(size_t)q * ld + lane] = vin ? u_v : T(0);
   if (uflag(__any(!fin))) status = CMPC_NAN_SOL;
@@ -794,6 +806,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     A.status[q] = status;
     A.iters[q] = it;
   }
+  if (A.out_u) scatter_result<T>(A, q, n, u_v, status, it, L.scr, lane, 64, [] { cbar(); });
   if (A.res) {  // max over the lanes of the last residual terms (the same lanes stored them)
     const T* rp = A.res_scr + (size_t)q * 3 * 256 + lane;
     const T r0 = wave_max_dpp(rp[0]), r1 = wave_max_dpp(rp[256]), r2 = wave_max_dpp(rp[512]);
@@ -817,8 +830,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     q = A.qlist[0][q];
     if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
-  __shared__ IpmShared<T, false> SH;
-  (void)ipm64_body<T, WPE, 0>(A, nullptr, SH, q, 0);
+  (void)ipm64_body<T, WPE, 0>(A, nullptr, nullptr, q, 0);
 }
 
 // Fused stage 1 + stage 2 for the n <= 64 class (cmpc_solve_batch, cold start): one launch condenses and solves
@@ -826,8 +838,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
 // the 128 / 256 IPM kernels follow).
 template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_solve64(IpmArgs<T> A, CondenseArgs<T> C) {
-  __shared__ IpmShared<T, true> SH;
-  (void)ipm64_body<T, WPE, 1>(A, &C, SH, (int)blockIdx.x, 0);
+  (void)ipm64_body<T, WPE, 1>(A, &C, nullptr, (int)blockIdx.x, 0);
 }
 
 // Work-item form of k_solve64 (cmpc_solve_batch, cold start, n <= 64 class): one workgroup of 8 waves per CU owns
@@ -846,9 +857,9 @@ constexpr int kSolve64qMaxQpw = 256;
 template <typename T>
 __global__ __launch_bounds__(512, 1) void k_solve64q(IpmArgs<T> A, CondenseArgs<T> C, int B, int qpw,
                                                       unsigned spin_max) {
-  __shared__ IpmShared<T, true> SH[8];
   __shared__ unsigned long long ring[kSolve64qMaxQpw + 8];
   __shared__ int qhead, qtail, qdone;
+  __shared__ IpmShared<T, true> SH[8];
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
   const int q0 = (int)blockIdx.x * qpw;
   const int qn = min(qpw, B - q0);
@@ -904,7 +915,7 @@ __global__ __launch_bounds__(512, 1) void k_solve64q(IpmArgs<T> A, CondenseArgs<
     if (ql >= qn || n_item > 64) break;  // not an item of this launch (cannot happen; never touch memory for it)
     // the item's result is wave-uniform by construction; readfirstlane makes that explicit to the compiler (the
     // scheduler's branches then stay scalar), and a result outside [1, iter_max + 1] ends the QP
-    const int r = __builtin_amdgcn_readfirstlane(ipm64_body<T, 2, 2>(A, &C, SH[w], q0 + ql, it, n_item));
+    const int r = __builtin_amdgcn_readfirstlane(ipm64_body<T, 2, 2>(A, &C, &SH[w], q0 + ql, it, n_item));
     int next = r < 0 ? -1 : (r & 0xffff);
     const int n_next = r < 0 ? 0 : (r >> 16);
     if (next <= it || next > A.s.iter_max + 1 || next > 0xfff) next = -1;

@@ -1,0 +1,43 @@
+"""Result scatter in the IPM kernels' epilogues (fused cold-start path without rollout: k_solve64, k_ipm128x and
+k_ipm_tiled write u[N][4][3], status and iterations themselves; no k_expand launch) against the k_expand path
+(CMPC_DIRECT=0 at cmpc_create): identical outputs, bit for bit, on batches that reach every size class (N = 10 and
+N = 20 mixed gaits: n <= 64, 64 < n <= 128, 128 < n <= 256) and carry rejected QPs (a step without a stance leg:
+INVALID_CONTACT, zero forces, zero iterations)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20221125
+
+
+def _solve(cm, N, B, gait, monkeypatch, direct, invalid=()):
+    monkeypatch.setenv("CMPC_DIRECT", "1" if direct else "0")
+    m = cm.default_model(N)
+    eng = cm.Engine(m, precision=cm.F64, max_batch=B)
+    x0, xref, foot, contact = cm.generate_device(m, SEED, B, gait=gait)
+    if invalid:
+        c = contact.host()
+        for q in invalid:
+            c[q, N // 2, :] = 0  # one step in flight: "mpc table invalid" (CentroidalMPC.cpp:328-330)
+        contact = cm.DeviceArray.from_host(c)
+    u = cm.DeviceArray((B, N, 4, 3), np.float64)
+    u.upload(np.full((B, N, 4, 3), 7.0))  # stale values: every entry must be written
+    st = cm.DeviceArray((B,), np.int32)
+    it = cm.DeviceArray((B,), np.int32)
+    eng.solve_device(B, x0, xref, foot, contact, u, None, st, it)
+    cm.hip().hipDeviceSynchronize()
+    return u.host(), st.host(), it.host()
+
+
+@pytest.mark.parametrize("N,B,gait", [(10, 300, 1), (20, 96, 1), (10, 64, 0)])
+def test_direct_results_equal_expand_path(cm, monkeypatch, N, B, gait):
+    bad = (3, 17, B - 1)
+    u0, st0, it0 = _solve(cm, N, B, gait, monkeypatch, direct=False, invalid=bad)
+    u1, st1, it1 = _solve(cm, N, B, gait, monkeypatch, direct=True, invalid=bad)
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(it1, it0)
+    np.testing.assert_array_equal(u1, u0)
+    assert np.all(st1[list(bad)] == 5)  # INVALID_CONTACT
+    assert np.all(u1[list(bad)] == 0.0) and np.all(it1[list(bad)] == 0)
+    assert np.all(st1[[q for q in range(B) if q not in bad]] == 0)
