@@ -52,6 +52,7 @@ struct cmpc_ctx {
   double* res;
   void* mig;
   int num_cu;  // compute units of the device (work-item kernel: one workgroup per CU)
+  bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;  // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   bool items;  // fused path as IPM-iteration work items (k_solve64q), opt-in: CMPC_ITEMS=1 at cmpc_create (measured
                // 7-17 % slower than k_solve64 on the headline; DESIGN.md "work items")
@@ -340,22 +341,22 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
   if (c->ld < 128) return 0;
   if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
+  IpmArgs<T> al = ia;
+  for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
+  al.qcount = c->qcount;
   ca.n_lo = 64;
   ca.qlist = c->qlist + (size_t)1 * B;
   ca.qcount = c->qcount + 1;
-  int r = launch_srbd_condense<T>(ca, 128, B, st);
+  // 64 < n <= 128: condensing and IPM in one launch (k_solve128), or (CMPC_FUSED128=0) two
+  int r = c->fused128 ? launch_solve128(al, ca, B, st) : launch_srbd_condense<T>(ca, 128, B, st);
+  if (r == 0 && !c->fused128) r = launch_ipm128(al, B, st);
   if (r == 0 && c->ld > 128) {
     ca.n_lo = 128;
     ca.qlist = c->qlist + (size_t)2 * B;
     ca.qcount = c->qcount + 2;
     r = launch_srbd_condense<T>(ca, 256, B, st);
+    if (r == 0) r = launch_ipm256(al, B, st);
   }
-  if (r != 0) return r;
-  IpmArgs<T> al = ia;
-  for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
-  al.qcount = c->qcount;
-  r = launch_ipm128(al, B, st);
-  if (r == 0 && c->ld >= 256) r = launch_ipm256(al, B, st);
   return r;
 }
 
@@ -470,6 +471,10 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     c->fused = model->N <= CMPC_C64_MAXN && !(f && f[0] == '0');
     const char* it = std::getenv("CMPC_ITEMS");
     c->items = it && it[0] == '1';
+    // 128 class fused for fp32 only (config 3: 2.267 -> 2.243 ms); fp64 measured slower fused (config 5 class
+    // stage 1.615 -> 1.657 ms, all-stance 4.19 -> 4.29 ms). CMPC_FUSED128=0/1 overrides (diagnostics).
+    const char* f128 = std::getenv("CMPC_FUSED128");
+    c->fused128 = f128 ? f128[0] == '1' : precision == CMPC_F32;
     const char* di = std::getenv("CMPC_DIRECT");  // diagnostics: 0 = results through k_expand on the fused path
     c->direct = !(di && di[0] == '0');
   }

@@ -105,6 +105,9 @@ int launch_ipm64(const IpmArgs<float>& a, int B, hipStream_t stream);
 // fused condensing + IPM of the n <= 64 class (k_solve64, k_ipm64.hpp); QPs with n > 64 only get their nvar hint
 int launch_solve64(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream);
 int launch_solve64(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream);
+// fused workgroup condensing + IPM of the 64 < n <= 128 class over its class list (k_solve128, k_ipm128x.hpp)
+int launch_solve128(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream);
+int launch_solve128(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream);
 // work-item form (k_solve64q): one 8-wave workgroup per qpw consecutive QPs, IPM iterations as items (a.mig)
 int launch_solve64q(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, int qpw, hipStream_t stream);
 int launch_solve64q(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, int qpw, hipStream_t stream);

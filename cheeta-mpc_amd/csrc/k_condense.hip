@@ -1,71 +1,11 @@
-// k_condense.hip — stage 1 of the hot path: SRBD linearisation, horizon propagation, dense condensing and
-// friction-pyramid stacking for a batch of centroidal MPC problems. One workgroup (WAVES wavefronts) per QP.
-//
-// Reference semantics (paths relative to the reference repo):
-//   dynamics  CentroidalMPC.cpp:85-92 forward Euler, lever arm linearised at r = p_{i,k} - c^ref_k, p the
-//             stance foot position of stance_point (cmpc_device.hpp: :93 pinning, node 0 = current foot :165-167)
-//   horizon   CentroidalMPC.cpp:159-176 multiple shooting -> condensed X = Aqp x0 + Bqp U
-//   cost      CentroidalMPC.cpp:203-231 -> H = Bqp' Qbar Bqp + Rbar, g = Bqp' Qbar (Aqp x0 - Xref) + rbar (A.3)
-//   f^des     CentroidalMPC.cpp:326-335 (m*9.81/n_stance, "mpc table invalid" when a step has no stance leg)
-//   pyramid   CentroidalMPC.cpp:179-201; swing legs (0 <= F f <= 0) eliminated (A.4)
-//
-// MI355X mapping:
-//   - column c of Bqp (one stance force component) lives in thread c: its 13-state image gamma is propagated through
-//     the SRBD transition with the A_k sparsity pattern (13 FMAs/step, not a dense 13x13 product);
-//   - every step k the block row Bqp_k (13 x n) is staged in LDS (double-buffered) and the rank-13 update
-//     H += Bqp_k' Q_k Bqp_k runs on the matrix cores: v_mfma_f64_16x16x4_f64 (fp64) / v_mfma_f32_16x16x4_f32 (fp32),
-//     16x16 lower tiles of H spread round-robin over the workgroup's wavefronts, accumulators in registers;
-//   - tiles whose columns are still all-zero at step k (inputs of later steps) are skipped, so the MFMA work follows
-//     the block-triangular structure of Bqp;
-//   - Rbar (diagonal + force-rate off-diagonals) and the identity padding are folded into the accumulator epilogue.
-#include "cmpc_device.hpp"
-#include "cmpc_kernels.hpp"
+// k_condense.hip — stage 1 of the hot path for the workgroup size classes: one workgroup (WAVES wavefronts) per
+// QP, the condensing itself in srbd_condense.hpp (shared with the fused 128-class kernel k_solve128).
+#include "srbd_condense.hpp"
 
 namespace cmpc {
 
-namespace {
-
-template <typename T>
-struct Mfma;
-template <>
-struct Mfma<double> {
-  typedef double acc_t __attribute__((ext_vector_type(4)));
-  static __device__ __forceinline__ acc_t run(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  // C/D layout of v_mfma_f64_16x16x4_f64: col = lane&15, row = (lane>>4) + 4*reg
-  static __device__ __forceinline__ int row(int lane, int reg) { return (lane >> 4) + 4 * reg; }
-};
-template <>
-struct Mfma<float> {
-  typedef float acc_t __attribute__((ext_vector_type(4)));
-  static __device__ __forceinline__ acc_t run(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  // C/D layout of v_mfma_f32_16x16x4_f32: col = lane&15, row = 4*(lane>>4) + reg
-  static __device__ __forceinline__ int row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
-};
-
-__device__ __forceinline__ void tile_of(int idx, int& ti, int& tj) {
-  ti = 0;
-  while ((ti + 1) * (ti + 2) / 2 <= idx) ++ti;
-  tj = idx - ti * (ti + 1) / 2;
-}
-
-}  // namespace
-
 template <typename T, int NMAX, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a) {
-  constexpr int NT = NMAX / 16;              // 16x16 tiles per dimension
-  constexpr int NLT = NT * (NT + 1) / 2;     // lower tiles
-  constexpr int TPW = (NLT + WAVES - 1) / WAVES;
-  constexpr int NTRI = NMAX / 3;
-  constexpr int NTHR = 64 * WAVES;
-  static_assert(NMAX <= NTHR, "one thread per column");
-  using MF = Mfma<T>;
-  using acc_t = typename MF::acc_t;
-
-  const DevModel* __restrict__ M = a.model;
   int q = blockIdx.x;
   if (a.qlist) {  // class list: this class's QPs first, the surplus workgroups exit
     if (q >= *a.qcount) return;
@@ -73,315 +13,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     if ((unsigned)q >= gridDim.x) return;  // grid = batch
   }
   if (a.n_lo > 0 && a.nvar[q] <= a.n_lo) return;  // finished (or rejected) by a smaller class
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int N = M->N, L = NL;
-  const int ld = a.ld;
-
-  __shared__ T s_G[2][16][NMAX];
-  __shared__ T s_w[2][16];
-  __shared__ T s_q[2][16];
-  __shared__ double s_xref[(MAXN + 1) * NX];
-  __shared__ double s_foot[(MAXN + 1) * NL * 3];
-  __shared__ double s_M[MAXN][9];
-  __shared__ uint8_t s_e[MAXN * NL];
-  __shared__ int s_ns[MAXN];
-  __shared__ int s_cb[MAXN + 1];  // 3 * #triples of steps < k
-  __shared__ int s_tk[NTRI], s_tleg[NTRI], s_tbase[MAXN];
-  __shared__ T s_diagR[NMAX], s_offR[NMAX];
-  __shared__ int s_next[NMAX];
-  __shared__ int s_wtot[WAVES];
-  __shared__ int s_flag;
-
-  // ---- load the QP record into LDS
-  const double* xr = a.xref + (size_t)q * (N + 1) * NX;
-  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
-  for (int i = tid; i < (N + 1) * NX; i += NTHR) s_xref[i] = xr[i];
-  for (int i = tid; i < (N + 1) * NL * 3; i += NTHR) s_foot[i] = ft[i];
-  for (int i = tid; i < 2 * 16 * NMAX; i += NTHR) (&s_G[0][0][0])[i] = T(0);
-  if (tid < 32) (&s_w[0][0])[tid] = T(0), (&s_q[0][0])[tid] = T(0);
-  if (tid == 0) s_flag = 0;
-  const int ne = N * L;
-  int e = 0;
-  if (tid < ne) {
-    e = a.contact[(size_t)q * ne + tid] ? 1 : 0;
-    s_e[tid] = (uint8_t)e;
-  }
-  // ballot prefix over (k, leg) in k-major order -> triple index of each stance (k, leg)
-  const unsigned long long bal = __ballot(e);
-  const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-  if (lane == 0) s_wtot[wave] = __popcll(bal);
-  __syncthreads();
-  int off = 0;
-  for (int w = 0; w < wave; ++w) off += s_wtot[w];
-  int nt = 0;
-  for (int w = 0; w < WAVES; ++w) nt += s_wtot[w];
-  if (e) {
-    const int t = off + pre;
-    if (t < NTRI) {
-      s_tk[t] = tid / L;
-      s_tleg[t] = tid % L;
-    }
-  }
-  if (tid < N) {
-    int ns = 0;
-    for (int i = 0; i < L; ++i) ns += s_e[tid * L + i];
-    s_ns[tid] = ns;
-    if (ns == 0) atomicOr(&s_flag, 1);
-    // per-step M_k = dt * I_b^{-1} R_z(psi_k)^T  (Theta row of A_k)
-    const double psi = s_xref[tid * NX + 11];
-    double sp, cp;
-    sincos(psi, &sp, &cp);
-    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) {
-        double s = 0.0;
-        for (int t = 0; t < 3; ++t) s += M->inv_inertia[r * 3 + t] * RzT[t * 3 + c];
-        s_M[tid][r * 3 + c] = M->dt * s;
-      }
-  }
-  __syncthreads();
-  const int n = 3 * nt;
-  int st = CMPC_SUCCESS;
-  if (s_flag) st = CMPC_INVALID_CONTACT;
-  else if (n > NMAX) {
-    if (NMAX < CMPC_IPM_MAX_N) {  // a bigger class follows: leave the hint, not the status
-      if (tid == 0) a.nvar[q] = n;
-      return;
-    }
-    st = CMPC_TOO_LARGE;
-  }
-  if (st == CMPC_SUCCESS && n <= a.n_lo) return;  // served by a smaller class
-  if (st != CMPC_SUCCESS) {
-    if (tid == 0) {
-      a.status[q] = st;
-      a.nvar[q] = 0;
-    }
-    return;
-  }
-  if (tid == 0) {
-    int acc = 0;
-    for (int k = 0; k < N; ++k) {
-      s_cb[k] = 3 * acc;
-      s_tbase[k] = acc;
-      acc += s_ns[k];
-    }
-    s_cb[N] = 3 * acc;
-  }
-  __syncthreads();
-
-  // ---- per-column setup (thread c <-> column c)
-  const int c = tid;
-  const bool col = c < n;
-  int kc = 0, d = 0, leg = 0;
-  T gam[NX];
-#pragma unroll
-  for (int s = 0; s < NX; ++s) gam[s] = T(0);
-  T gcol = T(0);
-  double rx = 0, ry = 0, rz = 0;
-  if (col) {
-    const int t = c / 3;
-    d = c % 3;
-    kc = s_tk[t];
-    leg = s_tleg[t];
-    const int j = 3 * leg + d;
-    const int nb = (kc > 0) + (kc < N - 1);
-    s_diagR[c] = T(2.0 * M->Wf[j] + 2.0 * M->Wr[j] * (double)nb);
-    s_offR[c] = T(-2.0 * M->Wr[j]);
-    int nx = -1;
-    if (kc + 1 < N && s_e[(kc + 1) * L + leg]) {
-      int rank = 0;
-      for (int i = 0; i < leg; ++i) rank += s_e[(kc + 1) * L + i];
-      nx = 3 * (s_tbase[kc + 1] + rank) + d;
-    }
-    s_next[c] = nx;
-    if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)s_ns[kc]));
-    double p[3];
-    stance_point(s_foot, N, kc, leg, [&](int k, int l) { return s_e[k * L + l] != 0; }, p);
-    const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : s_xref + kc * NX;
-    rx = p[0] - cb[0];
-    ry = p[1] - cb[1];
-    rz = p[2] - cb[2];
-  }
-  // free response x_hat_k = Aqp x0 (thread 0)
-  double xh[NX];
-  if (tid == 0) {
-    for (int s = 0; s < NX; ++s) xh[s] = a.x0[(size_t)q * NX + s];
-  }
-
-  acc_t acc[TPW];
-#pragma unroll
-  for (int p = 0; p < TPW; ++p) acc[p] = acc_t{T(0), T(0), T(0), T(0)};
-  // this wave's lower tiles (slot p = tile wave + WAVES p, row-major lower order)
-  constexpr int TT = NMAX <= 128 ? TPW : 1;  // tile table (NMAX <= 128 only)
-  int tile_i[TT], tile_j[TT];
-  bool tile_ok[TT];
-#pragma unroll
-  for (int p = 0; p < TT; ++p) {
-    const int idx = wave + p * WAVES;
-    tile_ok[p] = idx < NLT;
-    tile_of(tile_ok[p] ? idx : 0, tile_i[p], tile_j[p]);
-  }
-
-  const T dt = T(M->dt);
-  const T dtm = T(M->dt_over_m);
-  for (int k = 1; k <= N; ++k) {
-    const int buf = k & 1;
-    const int km = k - 1;
-    // (a) gamma <- A_{k-1} gamma + B_{k-1}[:, c]
-    const double* lk = a.lin ? a.lin + ((size_t)q * N + km) * 6 : nullptr;
-    if (col && kc <= km) {
-      T Lx = gam[6], Ly = gam[7], Lz = gam[8];
-      if (lk) {  // L+ += dt F_bar x c (SQP linearisation)
-        const T Fx = T(lk[3]), Fy = T(lk[4]), Fz = T(lk[5]);
-        const T c0 = gam[0], c1 = gam[1], c2 = gam[2];
-        gam[6] += dt * (Fy * c2 - Fz * c1);
-        gam[7] += dt * (Fz * c0 - Fx * c2);
-        gam[8] += dt * (Fx * c1 - Fy * c0);
-      }
-#pragma unroll
-      for (int s = 0; s < 3; ++s) gam[s] += dt * gam[3 + s];
-      gam[9] += T(s_M[km][0]) * Lx + T(s_M[km][1]) * Ly + T(s_M[km][2]) * Lz;
-      gam[10] += T(s_M[km][3]) * Lx + T(s_M[km][4]) * Ly + T(s_M[km][5]) * Lz;
-      gam[11] += T(s_M[km][6]) * Lx + T(s_M[km][7]) * Ly + T(s_M[km][8]) * Lz;
-      gam[5] += dt * gam[12];
-      if (kc == km) {
-        gam[3 + d] += dtm;
-        // dt * [r]x e_d
-        if (d == 0) {
-          gam[7] += dt * T(rz);
-          gam[8] -= dt * T(ry);
-        } else if (d == 1) {
-          gam[6] -= dt * T(rz);
-          gam[8] += dt * T(rx);
-        } else {
-          gam[6] += dt * T(ry);
-          gam[7] -= dt * T(rx);
-        }
-      }
-    }
-    // (b) free response and weighted tracking error w_k = Q_k (x_hat_k - xref_k)
-    if (tid == 0) {
-      double xn[NX];
-      for (int s = 0; s < 3; ++s) xn[s] = xh[s] + M->dt * xh[3 + s];
-      for (int s = 3; s < 9; ++s) xn[s] = xh[s];
-      xn[5] += M->dt * xh[12];
-      for (int r = 0; r < 3; ++r)
-        xn[9 + r] = xh[9 + r] + s_M[km][r * 3 + 0] * xh[6] + s_M[km][r * 3 + 1] * xh[7] + s_M[km][r * 3 + 2] * xh[8];
-      if (lk) {  // dt F_bar x (c - c_bar)
-        const double d0 = xh[0] - lk[0], d1 = xh[1] - lk[1], d2 = xh[2] - lk[2];
-        xn[6] += M->dt * (lk[4] * d2 - lk[5] * d1);
-        xn[7] += M->dt * (lk[5] * d0 - lk[3] * d2);
-        xn[8] += M->dt * (lk[3] * d1 - lk[4] * d0);
-      }
-      xn[12] = xh[12];
-      for (int s = 0; s < NX; ++s) {
-        xh[s] = xn[s];
-        const double qd = M->qdiag[k][s];
-        s_q[buf][s] = T(qd);
-        s_w[buf][s] = T(qd * (xn[s] - s_xref[k * NX + s]));
-      }
-    }
-    // (c) stage block row Bqp_k
-    if (c < NMAX) {
-#pragma unroll
-      for (int s = 0; s < NX; ++s) s_G[buf][s][c] = gam[s];
-    }
-    __syncthreads();
-    // (d) g += Bqp_k' w_k
-    if (col) {
-      T acc_g = T(0);
-#pragma unroll
-      for (int s = 0; s < NX; ++s) acc_g += gam[s] * s_w[buf][s];
-      gcol += acc_g;
-    }
-    // (e) H += Bqp_k' Q_k Bqp_k on the matrix cores; tiles of not-yet-active columns skipped. The wave's tiles are
-    //     in row-major order, so the active ones are a prefix (p < np). NMAX <= 128: K-slab outer, tiles inner, so
-    //     consecutive MFMAs are independent accumulators and pipeline instead of waiting out each chain (the 256
-    //     class keeps tile-outer order: its 17 tiles per wave leave no registers for the tile table)
-    const int ncols = s_cb[k];
-    if constexpr (NMAX <= 128) {
-      int np = 0;
-#pragma unroll
-      for (int p = 0; p < TPW; ++p) np += (tile_ok[p] && 16 * tile_i[p] < ncols) ? 1 : 0;
-      // K = 12: Bqp row 12 (g_z) is identically 0 and unweighted, rows 13..15 are padding
-#pragma unroll
-      for (int s4 = 0; s4 < 3; ++s4) {
-        const int s = 4 * s4 + (lane >> 4);
-        const T qs = s_q[buf][s];
-#pragma unroll
-        for (int p = 0; p < TPW; ++p) {
-          if (p < np) {
-            const T av = qs * s_G[buf][s][16 * tile_i[p] + (lane & 15)];
-            const T bv = s_G[buf][s][16 * tile_j[p] + (lane & 15)];
-            acc[p] = MF::run(av, bv, acc[p]);
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int p = 0; p < TPW; ++p) {
-        const int idx = wave + p * WAVES;
-        if (idx < NLT) {
-          int ti, tj;
-          tile_of(idx, ti, tj);
-          if (16 * ti < ncols) {
-#pragma unroll
-            for (int s4 = 0; s4 < 3; ++s4) {
-              const int s = 4 * s4 + (lane >> 4);
-              const T av = s_q[buf][s] * s_G[buf][s][16 * ti + (lane & 15)];
-              const T bv = s_G[buf][s][16 * tj + (lane & 15)];
-              acc[p] = MF::run(av, bv, acc[p]);
-            }
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- epilogue: Rbar, identity padding, write the class-padded block of H, g and the pyramid data
-  const int npad = ipm_class(n);
-  T* Hq = a.H + (size_t)q * ld * ld;
-#pragma unroll
-  for (int p = 0; p < TPW; ++p) {
-    const int idx = wave + p * WAVES;
-    if (idx < NLT) {
-      int ti, tj;
-      tile_of(idx, ti, tj);
-      if (16 * ti < npad) {
-        const int cc = 16 * tj + (lane & 15);
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const int rr = 16 * ti + MF::row(lane, r4);
-          T v = acc[p][r4];
-          if (rr == cc) {
-            v = rr < n ? v + s_diagR[rr] : T(1);
-          } else {
-            if (rr < n && s_next[rr] == cc) v += s_offR[rr];
-            if (cc < n && s_next[cc] == rr) v += s_offR[cc];
-          }
-          Hq[h_index(npad, rr, cc)] = v;  // class-packed block in the order the IPM of class npad reads
-          if (ti != tj) Hq[h_index(npad, cc, rr)] = v;
-        }
-      }
-    }
-  }
-  if (c < npad) a.g[(size_t)q * ld + c] = col ? gcol : T(0);
-  if (tid < npad / 3) {
-    const int t = tid;
-    const bool on = t < nt;
-    const int lg = on ? s_tleg[t] : 0;
-    a.tri_mu[(size_t)q * (ld / 3) + t] = on ? T(M->mu[lg]) : T(0);
-    for (int r = 0; r < 5; ++r) {
-      a.tri_lo[((size_t)q * (ld / 3) + t) * 5 + r] = T(0);
-      a.tri_hi[((size_t)q * (ld / 3) + t) * 5 + r] = T(M->ub[r]);
-    }
-    a.tri_map[(size_t)q * (ld / 3) + t] = on ? s_tk[t] * L + lg : -1;
-  }
-  if (tid == 0) {
-    a.status[q] = CMPC_SUCCESS;
-    a.nvar[q] = n;
-  }
+  (void)srbd_condense_qp<T, NMAX, WAVES, false>(a, q, nullptr);
 }
 
 template <typename T>

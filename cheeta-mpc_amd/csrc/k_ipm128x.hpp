@@ -26,6 +26,7 @@
 
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
+#include "srbd_condense.hpp"
 #include "step_ratio.hpp"
 #include "wave_dpp.hpp"
 
@@ -158,25 +159,46 @@ struct Lds {
 
 }  // namespace ipm128x
 
-template <typename T, int MINB>  // MINB workgroups per CU: 2 (fp64, 2 waves per SIMD), 4 (fp32)
-__global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
+// LDS of the 128 class; the fused kernel (k_solve128) runs the workgroup condensing first in the same bytes
+template <typename T, bool FUSED>
+struct Shared128 {
+  ipm128x::Lds<T> ipm;
+};
+template <typename T>
+struct Shared128<T, true> {
+  union {
+    ipm128x::Lds<T> ipm;
+    srbd::SrbdLds<T, 128, 4> cond;
+  };
+};
+
+// One QP on one workgroup of four waves. FUSED (k_solve128, cold-start cmpc_solve_batch): the workgroup condenses the
+// QP first (srbd_condense_qp, which writes H, g and the pyramid data to the workspace) and the IPM reads them back
+// after a workgroup barrier (same CU: no round trip through another launch); the LDS is one union of both phases.
+template <typename T, int MINB, bool FUSED>
+__device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const CondenseArgs<T>* C, const int q) {
   using namespace ipm128x;
-  X_STAMP_DECL;
   constexpr int NP = 128;
-  int q = blockIdx.x;
-  if (a.qlist[1]) {  // compacted class list: real QPs first, the surplus workgroups exit
-    if (q >= a.qcount[1]) return;
-    q = a.qlist[1][q];
-    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
+  // declared here, not in the kernel: as a reference from the kernel the LDS accesses lose their constant base
+  __shared__ Shared128<T, FUSED> U;
+  int n;
+  if constexpr (FUSED) {
+    // status and n of this QP come from the condensing itself (a uniform re-read of status / nvar would be a
+    // scalar-cache load, which does not see the vector stores of this launch)
+    n = srbd_condense_qp<T, 128, 4, true>(*C, q, &U.cond);
+    if (n < 0) return;
+    __syncthreads();  // H, g, pyramid data written by the whole workgroup; the IPM reuses the LDS bytes
+  } else {
+    if (a.status[q] != CMPC_SUCCESS) return;
+    n = a.nvar[q];
   }
-  if (a.status[q] != CMPC_SUCCESS) return;
-  const int n = a.nvar[q];
   if (n <= 64 || n > NP) return;  // served by another size class
+  X_STAMP_DECL;
   const int ld = a.ld;
   const int nt = n / 3;
   const int m = 5 * nt;
   const DevSettings S = a.s;
-  __shared__ Lds<T> L;
+  Lds<T>& L = U.ipm;
 
   const int tid = threadIdx.x;
   const int lane0 = tid & 63, wave0 = tid >> 6;
@@ -740,6 +762,28 @@ __global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
     }
   }
   X_STAMP_STORE(a.stamps, q);
+}
+
+template <typename T, int MINB>  // MINB workgroups per CU: 2 (fp64, 2 waves per SIMD), 4 (fp32)
+__global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
+  int q = blockIdx.x;
+  if (a.qlist[1]) {  // compacted class list: real QPs first, the surplus workgroups exit
+    if (q >= a.qcount[1]) return;
+    q = a.qlist[1][q];
+    if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
+  }
+  ipm128x_body<T, MINB, false>(a, nullptr, q);
+}
+
+// Fused condensing + IPM of the 64 < n <= 128 class (cold-start cmpc_solve_batch): one launch over the class list
+// k_class_lists built from k_solve64's nvar hints.
+template <typename T, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_solve128(IpmArgs<T> a, CondenseArgs<T> c) {
+  int q = blockIdx.x;
+  if (q >= a.qcount[1]) return;
+  q = a.qlist[1][q];
+  if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
+  ipm128x_body<T, MINB, true>(a, &c, q);
 }
 
 }  // namespace cmpc

@@ -9,4 +9,11 @@ int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+int launch_solve128(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (!a.qlist[1] || !a.qcount || a.ld < 128) return -1;  // list-driven only
+  hipLaunchKernelGGL((k_solve128<float, 4>), dim3(B), dim3(256), 0, stream, a, c);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 }  // namespace cmpc

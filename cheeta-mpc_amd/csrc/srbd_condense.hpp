@@ -1,0 +1,396 @@
+#pragma once
+// srbd_condense.hpp — one QP's condensing by one workgroup (WAVES wavefronts): SRBD linearisation, horizon
+// propagation, dense condensing and friction-pyramid stacking, for the workgroup size classes (n <= 128 / 256).
+// Called by k_srbd_condense (k_condense.hip) and by the fused 128-class kernel k_solve128 (k_ipm128x.hpp), which
+// runs the IPM on the same workgroup right after it.
+//
+// Reference semantics (paths relative to the reference repo):
+//   dynamics  CentroidalMPC.cpp:85-92 forward Euler, lever arm linearised at r = p_{i,k} - c^ref_k, p the
+//             stance foot position of stance_point (cmpc_device.hpp: :93 pinning, node 0 = current foot :165-167)
+//   horizon   CentroidalMPC.cpp:159-176 multiple shooting -> condensed X = Aqp x0 + Bqp U
+//   cost      CentroidalMPC.cpp:203-231 -> H = Bqp' Qbar Bqp + Rbar, g = Bqp' Qbar (Aqp x0 - Xref) + rbar (A.3)
+//   f^des     CentroidalMPC.cpp:326-335 (m*9.81/n_stance, "mpc table invalid" when a step has no stance leg)
+//   pyramid   CentroidalMPC.cpp:179-201; swing legs (0 <= F f <= 0) eliminated (A.4)
+//
+// MI355X mapping:
+//   - column c of Bqp (one stance force component) lives in thread c: its 13-state image gamma is propagated through
+//     the SRBD transition with the A_k sparsity pattern (13 FMAs/step, not a dense 13x13 product);
+//   - every step k the block row Bqp_k (13 x n) is staged in LDS (double-buffered) and the rank-13 update
+//     H += Bqp_k' Q_k Bqp_k runs on the matrix cores: v_mfma_f64_16x16x4_f64 (fp64) / v_mfma_f32_16x16x4_f32 (fp32),
+//     16x16 lower tiles of H spread round-robin over the workgroup's wavefronts, accumulators in registers;
+//   - tiles whose columns are still all-zero at step k (inputs of later steps) are skipped, so the MFMA work follows
+//     the block-triangular structure of Bqp;
+//   - Rbar (diagonal + force-rate off-diagonals) and the identity padding are folded into the accumulator epilogue.
+#include "cmpc_device.hpp"
+#include "cmpc_kernels.hpp"
+
+namespace cmpc {
+
+namespace srbd {
+
+template <typename T>
+struct Mfma;
+template <>
+struct Mfma<double> {
+  typedef double acc_t __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ acc_t run(double a, double b, acc_t c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  // C/D layout of v_mfma_f64_16x16x4_f64: col = lane&15, row = (lane>>4) + 4*reg
+  static __device__ __forceinline__ int row(int lane, int reg) { return (lane >> 4) + 4 * reg; }
+};
+template <>
+struct Mfma<float> {
+  typedef float acc_t __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ acc_t run(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  // C/D layout of v_mfma_f32_16x16x4_f32: col = lane&15, row = 4*(lane>>4) + reg
+  static __device__ __forceinline__ int row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
+};
+
+__device__ __forceinline__ void tile_of(int idx, int& ti, int& tj) {
+  ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= idx) ++ti;
+  tj = idx - ti * (ti + 1) / 2;
+}
+
+
+template <typename T, int NMAX, int WAVES>
+struct SrbdLds {
+  static constexpr int NTRI = NMAX / 3;
+  T s_G[2][16][NMAX];
+  T s_w[2][16];
+  T s_q[2][16];
+  double s_xref[(MAXN + 1) * NX];
+  double s_foot[(MAXN + 1) * NL * 3];
+  double s_M[MAXN][9];
+  uint8_t s_e[MAXN * NL];
+  int s_ns[MAXN];
+  int s_cb[MAXN + 1];  // 3 * #triples of steps < k
+  int s_tk[NTRI], s_tleg[NTRI], s_tbase[MAXN];
+  T s_diagR[NMAX], s_offR[NMAX];
+  int s_next[NMAX];
+  int s_wtot[WAVES];
+  int s_flag;
+};
+
+}  // namespace srbd
+
+// One QP (workgroup of 64 * WAVES threads). EXT: the LDS block is the caller's (*ext, e.g. a union with the IPM's),
+// else declared here. Writes H (class-packed), g, the pyramid data, tri_map, status and nvar to the workspace.
+// Returns n when the QP was condensed here, -1 otherwise (invalid contact table / too large: status written; a
+// bigger class: nvar hint; a smaller class: nothing).
+template <typename T, int NMAX, int WAVES, bool EXT>
+__device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q, srbd::SrbdLds<T, NMAX, WAVES>* ext) {
+  using namespace srbd;
+  constexpr int NT = NMAX / 16;              // 16x16 tiles per dimension
+  constexpr int NLT = NT * (NT + 1) / 2;     // lower tiles
+  constexpr int TPW = (NLT + WAVES - 1) / WAVES;
+  constexpr int NTRI = NMAX / 3;
+  constexpr int NTHR = 64 * WAVES;
+  static_assert(NMAX <= NTHR, "one thread per column");
+  using MF = Mfma<T>;
+  using acc_t = typename MF::acc_t;
+  const DevModel* __restrict__ M = a.model;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = M->N, L = NL;
+  const int ld = a.ld;
+
+  __shared__ SrbdLds<T, NMAX, WAVES> Sl;  // stand-alone kernel: declared here (constant LDS base)
+  SrbdLds<T, NMAX, WAVES>& S = EXT ? *ext : Sl;
+
+  // ---- load the QP record into LDS
+  const double* xr = a.xref + (size_t)q * (N + 1) * NX;
+  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
+  for (int i = tid; i < (N + 1) * NX; i += NTHR) S.s_xref[i] = xr[i];
+  for (int i = tid; i < (N + 1) * NL * 3; i += NTHR) S.s_foot[i] = ft[i];
+  for (int i = tid; i < 2 * 16 * NMAX; i += NTHR) (&S.s_G[0][0][0])[i] = T(0);
+  if (tid < 32) (&S.s_w[0][0])[tid] = T(0), (&S.s_q[0][0])[tid] = T(0);
+  if (tid == 0) S.s_flag = 0;
+  const int ne = N * L;
+  int e = 0;
+  if (tid < ne) {
+    e = a.contact[(size_t)q * ne + tid] ? 1 : 0;
+    S.s_e[tid] = (uint8_t)e;
+  }
+  // ballot prefix over (k, leg) in k-major order -> triple index of each stance (k, leg)
+  const unsigned long long bal = __ballot(e);
+  const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) S.s_wtot[wave] = __popcll(bal);
+  __syncthreads();
+  int off = 0;
+  for (int w = 0; w < wave; ++w) off += S.s_wtot[w];
+  int nt = 0;
+  for (int w = 0; w < WAVES; ++w) nt += S.s_wtot[w];
+  if (e) {
+    const int t = off + pre;
+    if (t < NTRI) {
+      S.s_tk[t] = tid / L;
+      S.s_tleg[t] = tid % L;
+    }
+  }
+  if (tid < N) {
+    int ns = 0;
+    for (int i = 0; i < L; ++i) ns += S.s_e[tid * L + i];
+    S.s_ns[tid] = ns;
+    if (ns == 0) atomicOr(&S.s_flag, 1);
+    // per-step M_k = dt * I_b^{-1} R_z(psi_k)^T  (Theta row of A_k)
+    const double psi = S.s_xref[tid * NX + 11];
+    double sp, cp;
+    sincos(psi, &sp, &cp);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double s = 0.0;
+        for (int t = 0; t < 3; ++t) s += M->inv_inertia[r * 3 + t] * RzT[t * 3 + c];
+        S.s_M[tid][r * 3 + c] = M->dt * s;
+      }
+  }
+  __syncthreads();
+  const int n = 3 * nt;
+  int st = CMPC_SUCCESS;
+  if (S.s_flag) st = CMPC_INVALID_CONTACT;
+  else if (n > NMAX) {
+    if (NMAX < CMPC_IPM_MAX_N) {  // a bigger class follows: leave the hint, not the status
+      if (tid == 0) a.nvar[q] = n;
+      return -1;
+    }
+    st = CMPC_TOO_LARGE;
+  }
+  if (st == CMPC_SUCCESS && n <= a.n_lo) return -1;  // served by a smaller class
+  if (st != CMPC_SUCCESS) {
+    if (tid == 0) {
+      a.status[q] = st;
+      a.nvar[q] = 0;
+    }
+    return -1;
+  }
+  if (tid == 0) {
+    int acc = 0;
+    for (int k = 0; k < N; ++k) {
+      S.s_cb[k] = 3 * acc;
+      S.s_tbase[k] = acc;
+      acc += S.s_ns[k];
+    }
+    S.s_cb[N] = 3 * acc;
+  }
+  __syncthreads();
+
+  // ---- per-column setup (thread c <-> column c)
+  const int c = tid;
+  const bool col = c < n;
+  int kc = 0, d = 0, leg = 0;
+  T gam[NX];
+#pragma unroll
+  for (int s = 0; s < NX; ++s) gam[s] = T(0);
+  T gcol = T(0);
+  double rx = 0, ry = 0, rz = 0;
+  if (col) {
+    const int t = c / 3;
+    d = c % 3;
+    kc = S.s_tk[t];
+    leg = S.s_tleg[t];
+    const int j = 3 * leg + d;
+    const int nb = (kc > 0) + (kc < N - 1);
+    S.s_diagR[c] = T(2.0 * M->Wf[j] + 2.0 * M->Wr[j] * (double)nb);
+    S.s_offR[c] = T(-2.0 * M->Wr[j]);
+    int nx = -1;
+    if (kc + 1 < N && S.s_e[(kc + 1) * L + leg]) {
+      int rank = 0;
+      for (int i = 0; i < leg; ++i) rank += S.s_e[(kc + 1) * L + i];
+      nx = 3 * (S.s_tbase[kc + 1] + rank) + d;
+    }
+    S.s_next[c] = nx;
+    if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)S.s_ns[kc]));
+    double p[3];
+    stance_point(S.s_foot, N, kc, leg, [&](int k, int l) { return S.s_e[k * L + l] != 0; }, p);
+    const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : S.s_xref + kc * NX;
+    rx = p[0] - cb[0];
+    ry = p[1] - cb[1];
+    rz = p[2] - cb[2];
+  }
+  // free response x_hat_k = Aqp x0 (thread 0)
+  double xh[NX];
+  if (tid == 0) {
+    for (int s = 0; s < NX; ++s) xh[s] = a.x0[(size_t)q * NX + s];
+  }
+
+  acc_t acc[TPW];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) acc[p] = acc_t{T(0), T(0), T(0), T(0)};
+  // this wave's lower tiles (slot p = tile wave + WAVES p, row-major lower order)
+  constexpr int TT = NMAX <= 128 ? TPW : 1;  // tile table (NMAX <= 128 only)
+  int tile_i[TT], tile_j[TT];
+  bool tile_ok[TT];
+#pragma unroll
+  for (int p = 0; p < TT; ++p) {
+    const int idx = wave + p * WAVES;
+    tile_ok[p] = idx < NLT;
+    tile_of(tile_ok[p] ? idx : 0, tile_i[p], tile_j[p]);
+  }
+
+  const T dt = T(M->dt);
+  const T dtm = T(M->dt_over_m);
+  for (int k = 1; k <= N; ++k) {
+    const int buf = k & 1;
+    const int km = k - 1;
+    // (a) gamma <- A_{k-1} gamma + B_{k-1}[:, c]
+    const double* lk = a.lin ? a.lin + ((size_t)q * N + km) * 6 : nullptr;
+    if (col && kc <= km) {
+      T Lx = gam[6], Ly = gam[7], Lz = gam[8];
+      if (lk) {  // L+ += dt F_bar x c (SQP linearisation)
+        const T Fx = T(lk[3]), Fy = T(lk[4]), Fz = T(lk[5]);
+        const T c0 = gam[0], c1 = gam[1], c2 = gam[2];
+        gam[6] += dt * (Fy * c2 - Fz * c1);
+        gam[7] += dt * (Fz * c0 - Fx * c2);
+        gam[8] += dt * (Fx * c1 - Fy * c0);
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) gam[s] += dt * gam[3 + s];
+      gam[9] += T(S.s_M[km][0]) * Lx + T(S.s_M[km][1]) * Ly + T(S.s_M[km][2]) * Lz;
+      gam[10] += T(S.s_M[km][3]) * Lx + T(S.s_M[km][4]) * Ly + T(S.s_M[km][5]) * Lz;
+      gam[11] += T(S.s_M[km][6]) * Lx + T(S.s_M[km][7]) * Ly + T(S.s_M[km][8]) * Lz;
+      gam[5] += dt * gam[12];
+      if (kc == km) {
+        gam[3 + d] += dtm;
+        // dt * [r]x e_d
+        if (d == 0) {
+          gam[7] += dt * T(rz);
+          gam[8] -= dt * T(ry);
+        } else if (d == 1) {
+          gam[6] -= dt * T(rz);
+          gam[8] += dt * T(rx);
+        } else {
+          gam[6] += dt * T(ry);
+          gam[7] -= dt * T(rx);
+        }
+      }
+    }
+    // (b) free response and weighted tracking error w_k = Q_k (x_hat_k - xref_k)
+    if (tid == 0) {
+      double xn[NX];
+      for (int s = 0; s < 3; ++s) xn[s] = xh[s] + M->dt * xh[3 + s];
+      for (int s = 3; s < 9; ++s) xn[s] = xh[s];
+      xn[5] += M->dt * xh[12];
+      for (int r = 0; r < 3; ++r)
+        xn[9 + r] = xh[9 + r] + S.s_M[km][r * 3 + 0] * xh[6] + S.s_M[km][r * 3 + 1] * xh[7] + S.s_M[km][r * 3 + 2] * xh[8];
+      if (lk) {  // dt F_bar x (c - c_bar)
+        const double d0 = xh[0] - lk[0], d1 = xh[1] - lk[1], d2 = xh[2] - lk[2];
+        xn[6] += M->dt * (lk[4] * d2 - lk[5] * d1);
+        xn[7] += M->dt * (lk[5] * d0 - lk[3] * d2);
+        xn[8] += M->dt * (lk[3] * d1 - lk[4] * d0);
+      }
+      xn[12] = xh[12];
+      for (int s = 0; s < NX; ++s) {
+        xh[s] = xn[s];
+        const double qd = M->qdiag[k][s];
+        S.s_q[buf][s] = T(qd);
+        S.s_w[buf][s] = T(qd * (xn[s] - S.s_xref[k * NX + s]));
+      }
+    }
+    // (c) stage block row Bqp_k
+    if (c < NMAX) {
+#pragma unroll
+      for (int s = 0; s < NX; ++s) S.s_G[buf][s][c] = gam[s];
+    }
+    __syncthreads();
+    // (d) g += Bqp_k' w_k
+    if (col) {
+      T acc_g = T(0);
+#pragma unroll
+      for (int s = 0; s < NX; ++s) acc_g += gam[s] * S.s_w[buf][s];
+      gcol += acc_g;
+    }
+    // (e) H += Bqp_k' Q_k Bqp_k on the matrix cores; tiles of not-yet-active columns skipped. The wave's tiles are
+    //     in row-major order, so the active ones are a prefix (p < np). NMAX <= 128: K-slab outer, tiles inner, so
+    //     consecutive MFMAs are independent accumulators and pipeline instead of waiting out each chain (the 256
+    //     class keeps tile-outer order: its 17 tiles per wave leave no registers for the tile table)
+    const int ncols = S.s_cb[k];
+    if constexpr (NMAX <= 128) {
+      int np = 0;
+#pragma unroll
+      for (int p = 0; p < TPW; ++p) np += (tile_ok[p] && 16 * tile_i[p] < ncols) ? 1 : 0;
+      // K = 12: Bqp row 12 (g_z) is identically 0 and unweighted, rows 13..15 are padding
+#pragma unroll
+      for (int s4 = 0; s4 < 3; ++s4) {
+        const int s = 4 * s4 + (lane >> 4);
+        const T qs = S.s_q[buf][s];
+#pragma unroll
+        for (int p = 0; p < TPW; ++p) {
+          if (p < np) {
+            const T av = qs * S.s_G[buf][s][16 * tile_i[p] + (lane & 15)];
+            const T bv = S.s_G[buf][s][16 * tile_j[p] + (lane & 15)];
+            acc[p] = MF::run(av, bv, acc[p]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < TPW; ++p) {
+        const int idx = wave + p * WAVES;
+        if (idx < NLT) {
+          int ti, tj;
+          tile_of(idx, ti, tj);
+          if (16 * ti < ncols) {
+#pragma unroll
+            for (int s4 = 0; s4 < 3; ++s4) {
+              const int s = 4 * s4 + (lane >> 4);
+              const T av = S.s_q[buf][s] * S.s_G[buf][s][16 * ti + (lane & 15)];
+              const T bv = S.s_G[buf][s][16 * tj + (lane & 15)];
+              acc[p] = MF::run(av, bv, acc[p]);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue: Rbar, identity padding, write the class-padded block of H, g and the pyramid data
+  const int npad = ipm_class(n);
+  T* Hq = a.H + (size_t)q * ld * ld;
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    const int idx = wave + p * WAVES;
+    if (idx < NLT) {
+      int ti, tj;
+      tile_of(idx, ti, tj);
+      if (16 * ti < npad) {
+        const int cc = 16 * tj + (lane & 15);
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int rr = 16 * ti + MF::row(lane, r4);
+          T v = acc[p][r4];
+          if (rr == cc) {
+            v = rr < n ? v + S.s_diagR[rr] : T(1);
+          } else {
+            if (rr < n && S.s_next[rr] == cc) v += S.s_offR[rr];
+            if (cc < n && S.s_next[cc] == rr) v += S.s_offR[cc];
+          }
+          Hq[h_index(npad, rr, cc)] = v;  // class-packed block in the order the IPM of class npad reads
+          if (ti != tj) Hq[h_index(npad, cc, rr)] = v;
+        }
+      }
+    }
+  }
+  if (c < npad) a.g[(size_t)q * ld + c] = col ? gcol : T(0);
+  if (tid < npad / 3) {
+    const int t = tid;
+    const bool on = t < nt;
+    const int lg = on ? S.s_tleg[t] : 0;
+    a.tri_mu[(size_t)q * (ld / 3) + t] = on ? T(M->mu[lg]) : T(0);
+    for (int r = 0; r < 5; ++r) {
+      a.tri_lo[((size_t)q * (ld / 3) + t) * 5 + r] = T(0);
+      a.tri_hi[((size_t)q * (ld / 3) + t) * 5 + r] = T(M->ub[r]);
+    }
+    a.tri_map[(size_t)q * (ld / 3) + t] = on ? S.s_tk[t] * L + lg : -1;
+  }
+  if (tid == 0) {
+    a.status[q] = CMPC_SUCCESS;
+    a.nvar[q] = n;
+  }
+  return n;
+}
+
+}  // namespace cmpc
