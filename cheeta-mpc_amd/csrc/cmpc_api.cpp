@@ -42,7 +42,8 @@ struct cmpc_ctx {
   int* status;
   int* iters;
   int* qlist;   // [3][max_batch] per-class QP lists (k_class_lists)
-  int* qcount;  // [3]
+  int* qcount;  // [9]: k_class_lists' counts, then the fused path's two alternating append counters
+  int fused_parity = 0;  // fused path: this call appends to qcount[3 + 3 parity] and zeroes the other slice
   // cold-start cmpc_solve_batch runs the fused n <= 64 kernel (k_solve64) when N <= 21; CMPC_FUSED=0 in the
   // environment at cmpc_create selects the separate condensing + IPM launches (A/B measurement)
   bool fused;
@@ -109,7 +110,7 @@ Layout layout(int ld, int precision, int B) {
   L.status = take((size_t)B * sizeof(int));
   L.iters = take((size_t)B * sizeof(int));
   L.qlist = take((size_t)3 * B * sizeof(int));
-  L.qcount = take(3 * sizeof(int));
+  L.qcount = take(9 * sizeof(int));  // [0..2] k_class_lists; [3..5], [6..8] appended by k_solve64 (call parity)
   // SQP (cmpc_sqp_solve_batch): linearisation points, iterate, QP solution, per-QP flags and counters
   L.lin = take((size_t)B * MAXN * 6 * 8);
   L.uj = take((size_t)B * MAXN * NU * 8);
@@ -251,6 +252,10 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.out_iters = nullptr;
   a.tri_map = c->tri_map;
   a.out_nu = c->model.N * 12;
+  a.app_list = nullptr;
+  a.app_count = nullptr;
+  a.app_reset = nullptr;
+  a.app_ld = 0;
   return a;
 }
 
@@ -330,6 +335,15 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   ia.out_u = out_u;
   ia.out_status = out_status;
   ia.out_iters = out_iters;
+  // the bigger classes' lists are appended by the fused kernel itself (no k_class_lists launch); the counters of
+  // this call were zeroed by the previous fused call (or at cmpc_create), this call zeroes the next call's
+  int* cnt = c->qcount + 3 + 3 * c->fused_parity;
+  if (c->ld >= 128) {
+    ia.app_list = c->qlist;
+    ia.app_count = cnt;
+    ia.app_reset = c->qcount + 3 + 3 * (c->fused_parity ^ 1);
+    ia.app_ld = B;
+  }
   if (c->items && c->settings.iter_max < 4000) {  // an item carries its iteration in 12 bits
     // one 8-wave workgroup per CU, each owning qpw consecutive QPs (8 <= qpw <= 256)
     int qpw = (B + c->num_cu - 1) / c->num_cu;
@@ -338,22 +352,24 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   } else if (launch_solve64(ia, ca, B, st) != 0) {
     return -2;
   }
-  if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
   if (c->ld < 128) return 0;
-  if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
+  c->fused_parity ^= 1;
+  if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
   IpmArgs<T> al = ia;
-  for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
-  al.qcount = c->qcount;
+  al.app_list = nullptr;
+  al.app_count = al.app_reset = nullptr;
+  for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;  // list 0 unused here
+  al.qcount = cnt;
   ca.n_lo = 64;
   ca.qlist = c->qlist + (size_t)1 * B;
-  ca.qcount = c->qcount + 1;
+  ca.qcount = cnt + 1;
   // 64 < n <= 128: condensing and IPM in one launch (k_solve128), or (CMPC_FUSED128=0) two
   int r = c->fused128 ? launch_solve128(al, ca, B, st) : launch_srbd_condense<T>(ca, 128, B, st);
   if (r == 0 && !c->fused128) r = launch_ipm128(al, B, st);
   if (r == 0 && c->ld > 128) {
     ca.n_lo = 128;
     ca.qlist = c->qlist + (size_t)2 * B;
-    ca.qcount = c->qcount + 2;
+    ca.qcount = cnt + 2;
     r = launch_srbd_condense<T>(ca, 256, B, st);
     if (r == 0) r = launch_ipm256(al, B, st);
   }
@@ -519,6 +535,11 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->mig = c->ws + L.mig;
   c->qlist = (int*)(c->ws + L.qlist);
   c->qcount = (int*)(c->ws + L.qcount);
+  if (hipMemset(c->qcount, 0, 9 * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (c->own_ws) (void)hipFree(c->ws);
+    delete c;
+    return CMPC_ERR_HIP;
+  }
   if (hipMalloc((void**)&c->d_model, sizeof(DevModel)) != hipSuccess) {
     if (c->own_ws) (void)hipFree(c->ws);
     delete c;

@@ -87,6 +87,13 @@ struct IpmArgs {
   int* out_iters;
   const int* tri_map;
   int out_nu;
+  // fused path (k_solve64 / k_solve64q), or app_list = null: a QP of a bigger class is appended to its class list,
+  // app_list[c * app_ld + atomicAdd(&app_count[c], 1)] = q (c = 1: n <= 128, 2: n <= 256; order not fixed, each QP's
+  // result does not depend on it), and workgroup 0 zeroes app_reset[0..2] (the next call's counters)
+  int* app_list;
+  int* app_count;
+  int* app_reset;
+  int app_ld;
 };
 
 // one size class of the workgroup condensing kernel: npad 128 (64 < n <= 128, or n <= 128 when n_lo = 0) or 256

@@ -81,7 +81,7 @@ struct C64Lds {
 // nvar to the workspace exactly as the stand-alone kernel always did, and also hands the result to a fused caller:
 // K = H in the 4 x 16-cyclic register tile of k_ipm64, g_out = g[lane], mu_out = the friction coefficient of the
 // lane's force triple. Returns n, or < 0 when the IPM has nothing to do here: -2 invalid contact table (status
-// written), -1 n > 64 (left to the bigger classes with the nvar hint).
+// written), -3 - n for n > 64 (left to the bigger classes with the nvar hint).
 template <typename T, bool MASK = false>
 __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int q, c64::C64Lds<T>& S, T (&K)[64],
                                              T& g_out, T& mu_out) {
@@ -123,7 +123,7 @@ __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int
   }
   if (n > 64) {  // a bigger class; the hint lets its condensing kernel skip every QP handled here at once
     if (lane == 0) a.nvar[q] = n;
-    return -1;
+    return -3 - n;
   }
 
   // ---- triples: t-th stance (k, leg) in k-major order

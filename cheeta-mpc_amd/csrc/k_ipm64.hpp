@@ -209,6 +209,11 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
         if (n == -2 && A.out_u)  // the rejected QP's result: zeros, INVALID_CONTACT, no iterations
           scatter_result<T>(A, q, 0, T(0), CMPC_INVALID_CONTACT, 0, SH.ipm.scr, olane<MODE == 2>(), 64,
                             [] { ipm64::cbar(); });
+        if (n <= -3 && A.app_list && olane<MODE == 2>() == 0) {  // append to the bigger class's list
+          const int cls = -3 - n <= 128 ? 1 : 2;
+          const int pos = atomicAdd(&A.app_count[cls], 1);
+          A.app_list[(size_t)cls * A.app_ld + pos] = q;
+        }
         return -1;
       }
       // pyramid rows j = lane + 64 cc: the bounds and friction coefficients the condensing just wrote to the
@@ -838,6 +843,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
 // the 128 / 256 IPM kernels follow).
 template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_solve64(IpmArgs<T> A, CondenseArgs<T> C) {
+  if (A.app_reset && blockIdx.x == 0 && threadIdx.x < 3) A.app_reset[threadIdx.x] = 0;  // next call's counters
   (void)ipm64_body<T, WPE, 1>(A, &C, nullptr, (int)blockIdx.x, 0);
 }
 
@@ -863,6 +869,7 @@ __global__ __launch_bounds__(512, 1) void k_solve64q(IpmArgs<T> A, CondenseArgs<
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
   const int q0 = (int)blockIdx.x * qpw;
   const int qn = min(qpw, B - q0);
+  if (A.app_reset && blockIdx.x == 0 && threadIdx.x < 3) A.app_reset[threadIdx.x] = 0;  // next call's counters
   if (qn <= 0) return;
   const unsigned R = (unsigned)qpw + 8u;
   // every entry is written: positions < qn hold the fresh QPs (iteration 0), the rest sequence 0, which no position

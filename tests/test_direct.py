@@ -41,3 +41,37 @@ def test_direct_results_equal_expand_path(cm, monkeypatch, N, B, gait):
     assert np.all(st1[list(bad)] == 5)  # INVALID_CONTACT
     assert np.all(u1[list(bad)] == 0.0) and np.all(it1[list(bad)] == 0)
     assert np.all(st1[[q for q in range(B) if q not in bad]] == 0)
+
+
+def test_repeated_calls_with_class_lists(cm):
+    """The fused path appends the bigger classes' QPs to lists with two alternating counter sets (each call zeroes
+    the next call's): repeated calls, a warm-start (unfused, k_class_lists) call and a rollout call in between, and
+    a smaller batch must all give the first call's results."""
+    N, B = 20, 96
+    m = cm.default_model(N)
+    eng = cm.Engine(m, precision=cm.F64, max_batch=B)
+    x0, xref, foot, contact = cm.generate_device(m, SEED, B, gait=1)
+
+    def run(Bc=B, u_init=None, x=None):
+        u = cm.DeviceArray((Bc, N, 4, 3), np.float64)
+        st = cm.DeviceArray((Bc,), np.int32)
+        it = cm.DeviceArray((Bc,), np.int32)
+        eng.solve_device(Bc, x0, xref, foot, contact, u, x, st, it, u_init=u_init)
+        cm.hip().hipDeviceSynchronize()
+        return u, st.host(), it.host()
+
+    u_ref, st_ref, it_ref = run()
+    assert np.all(st_ref == 0)
+    uh = u_ref.host()
+    for k in range(3):
+        u, st, it = run()
+        np.testing.assert_array_equal(st, st_ref)
+        np.testing.assert_array_equal(it, it_ref)
+        np.testing.assert_array_equal(u.host(), uh)
+        if k == 0:
+            run(u_init=u_ref)  # warm start: the unfused path with k_class_lists
+        if k == 1:
+            run(x=cm.DeviceArray((B, N + 1, 13), np.float64))  # rollout: k_expand after the fused kernels
+    u, st, it = run(Bc=40)
+    np.testing.assert_array_equal(st, st_ref[:40])
+    np.testing.assert_array_equal(u.host(), uh[:40])
