@@ -53,6 +53,7 @@ struct cmpc_ctx {
   double* res;
   void* mig;
   int num_cu;  // compute units of the device (work-item kernel: one workgroup per CU)
+  int w128;       // waves per QP of the 64 < n <= 128 IPM class: 4, or 2 (fp32 only)
   bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;  // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   bool items;  // fused path as IPM-iteration work items (k_solve64q), opt-in: CMPC_ITEMS=1 at cmpc_create (measured
@@ -306,6 +307,14 @@ int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const
 // other classes' early-exit workgroups (mixed gait, config 5: IPM 2.31 -> 1.85-1.89 ms). Measured against running
 // the bigger classes concurrently on a forked side stream: +1.5 % on the mixed batch, -1.5..-2.5 % on the headline
 // (events and an empty launch on the critical path), so the classes run back to back.
+// the 64 < n <= 128 IPM class on the context's wave count
+inline int launch_ipm128_ctx(const cmpc_ctx* c, const IpmArgs<double>& a, int B, hipStream_t st) {
+  return launch_ipm128(a, B, st);
+}
+inline int launch_ipm128_ctx(const cmpc_ctx* c, const IpmArgs<float>& a, int B, hipStream_t st) {
+  return c->w128 == 2 ? launch_ipm128w2(a, B, st) : launch_ipm128(a, B, st);
+}
+
 template <typename T>
 int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, bool lists_ready) {
   if (B <= 0) return 0;
@@ -315,7 +324,7 @@ int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, boo
   for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
   al.qcount = c->qcount;
   int r = launch_ipm64(al, B, st);
-  if (r == 0) r = launch_ipm128(al, B, st);
+  if (r == 0) r = launch_ipm128_ctx(c, al, B, st);
   if (r == 0 && c->ld >= 256) r = launch_ipm256(al, B, st);
   return r;
 }
@@ -365,7 +374,7 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   ca.qcount = cnt + 1;
   // 64 < n <= 128: condensing and IPM in one launch (k_solve128), or (CMPC_FUSED128=0) two
   int r = c->fused128 ? launch_solve128(al, ca, B, st) : launch_srbd_condense<T>(ca, 128, B, st);
-  if (r == 0 && !c->fused128) r = launch_ipm128(al, B, st);
+  if (r == 0 && !c->fused128) r = launch_ipm128_ctx(c, al, B, st);
   if (r == 0 && c->ld > 128) {
     ca.n_lo = 128;
     ca.qlist = c->qlist + (size_t)2 * B;
@@ -491,6 +500,10 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     // stage 1.615 -> 1.657 ms, all-stance 4.19 -> 4.29 ms). CMPC_FUSED128=0/1 overrides (diagnostics).
     const char* f128 = std::getenv("CMPC_FUSED128");
     c->fused128 = f128 ? f128[0] == '1' : precision == CMPC_F32;
+    // fp32 128 class on two waves per QP (CMPC_W128=2): separate condensing launch (the fused one runs on four)
+    const char* w128 = std::getenv("CMPC_W128");
+    c->w128 = (precision == CMPC_F32 && w128 && w128[0] == '2') ? 2 : 4;
+    if (c->w128 == 2) c->fused128 = false;
     const char* di = std::getenv("CMPC_DIRECT");  // diagnostics: 0 = results through k_expand on the fused path
     c->direct = !(di && di[0] == '0');
   }

@@ -120,6 +120,7 @@ int launch_solve64q(const IpmArgs<double>& a, const CondenseArgs<double>& c, int
 int launch_solve64q(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, int qpw, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
+int launch_ipm128w2(const IpmArgs<float>& a, int B, hipStream_t stream);  // the same on 2 waves per QP
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
 int launch_ipm256(const IpmArgs<float>& a, int B, hipStream_t stream);
 

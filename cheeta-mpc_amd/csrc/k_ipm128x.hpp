@@ -22,6 +22,10 @@
 //     sums and backward column sums over the lower registers (c <= rho), partials reduced through LDS;
 //   * one thread per variable (tid < 128) and per pyramid row (tid < 5 n / 3 <= 210); block reductions are DPP
 //     wave reductions + 4 partials through LDS.
+// Two-wave form (NW = 2, fp32, CMPC_W128=2): the same algorithm with wave w owning the row groups 2 rho + w
+// (rows 8 rho + 4w + a, rho = 0..15: 128 tile registers per lane, 2 waves per SIMD), a chunk's pivot rows in register
+// rows 0 and 1, the tile rotated by two register rows per chunk, and two pyramid rows per thread; half as many waves
+// meet at each pair barrier and each brings twice the bulk FMAs.
 #include <type_traits>
 
 #include "cmpc_device.hpp"
@@ -172,13 +176,27 @@ struct Shared128<T, true> {
   };
 };
 
-// One QP on one workgroup of four waves. FUSED (k_solve128, cold-start cmpc_solve_batch): the workgroup condenses the
-// QP first (srbd_condense_qp, which writes H, g and the pyramid data to the workspace) and the IPM reads them back
-// after a workgroup barrier (same CU: no round trip through another launch); the LDS is one union of both phases.
-template <typename T, int MINB, bool FUSED>
+// One QP on one workgroup of NW waves (NW = 4: the layout of the header; NW = 2, fp32 only: each wave owns every other
+// row group, 128 tile registers per lane, two pyramid rows per thread). FUSED (k_solve128, cold-start
+// cmpc_solve_batch, NW = 4): the workgroup condenses the QP first (srbd_condense_qp, which writes H, g and the pyramid
+// data to the workspace) and the IPM reads them back after a workgroup barrier (same CU: no round trip through another
+// launch); the LDS is one union of both phases.
+//
+// Layout constants: row group R = NW rho + w of wave w holds rows RG rho + 4 w + a (RG = 4 NW), register rho * 8 + c
+// (NR = 32 / NW register rows); a 16-pivot chunk spans CR = 16 / RG register rows; thread tid serves pyramid rows
+// tid + NT s (s < PR = 256 / NT).
+template <typename T, int MINB, bool FUSED, int NW = 4>
 __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const CondenseArgs<T>* C, const int q) {
   using namespace ipm128x;
+  static_assert(NW == 4 || NW == 2, "four or two waves per QP");
+  static_assert(!FUSED || NW == 4, "the fused condensing runs on four waves");
   constexpr int NP = 128;
+  constexpr int NT = 64 * NW;  // threads
+  constexpr int NR = 32 / NW;  // register rows per wave
+  constexpr int RG = 4 * NW;   // row stride of a wave's register rows
+  constexpr int CR = 16 / RG;  // register rows per 16-pivot chunk
+  constexpr int PR = 256 / NT; // pyramid-row slots per thread
+  constexpr int NK = NR * 8;   // tile registers per lane
   // declared here, not in the kernel: as a reference from the kernel the LDS accesses lose their constant base
   __shared__ Shared128<T, FUSED> U;
   int n;
@@ -204,40 +222,51 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
   const int lane0 = tid & 63, wave0 = tid >> 6;
   const int la0 = lane0 >> 4, lb0 = lane0 & 15;
 
-  // ---- variable role (tid < 128) and pyramid-row role (tid < m)
+  // ---- variable role (tid < 128) and pyramid-row role (row tid + NT s < m)
   const bool isv = tid < NP;
   const bool var = tid < n;
   const T g_i = var ? a.g[(size_t)q * ld + tid] : T(0);
   const T mu_i = var ? a.tri_mu[(size_t)q * (ld / 3) + tid / 3] : T(0);
   T u_i = (a.warm && var) ? a.u[(size_t)q * ld + tid] : T(0), rg_i = T(0), du_i = T(0);
-  const bool con = tid < m;
-  const int tj = tid / 5, rj = tid % 5;
-  {
-    L.p_lo[tid] = con ? a.tri_lo[((size_t)q * (ld / 3) + tj) * 5 + rj] : T(0);
-    L.p_hi[tid] = con ? a.tri_hi[((size_t)q * (ld / 3) + tj) * 5 + rj] : T(0);
+  auto rowj = [&](int s) { return tid + NT * s; };
+  auto con = [&](int s) { return rowj(s) < m; };
+#pragma unroll
+  for (int s = 0; s < PR; ++s) {
+    const int j = rowj(s);
+    L.p_lo[j] = con(s) ? a.tri_lo[((size_t)q * (ld / 3) + j / 5) * 5 + j % 5] : T(0);
+    L.p_hi[j] = con(s) ? a.tri_hi[((size_t)q * (ld / 3) + j / 5) * 5 + j % 5] : T(0);
   }
   if (tid < 43) L.mut[tid] = tid < nt ? a.tri_mu[(size_t)q * (ld / 3) + tid] : T(0);
   if (isv) L.v[tid] = u_i;
   __syncthreads();
-  auto C_row = [&]() -> T {
-    return con ? pyr_row<T>(rj, L.mut[tj], L.v[3 * tj], L.v[3 * tj + 1], L.v[3 * tj + 2]) : T(0);
+  auto C_row = [&](int s) -> T {
+    const int j = rowj(s), tj = j / 5;
+    return con(s) ? pyr_row<T>(j % 5, L.mut[tj], L.v[3 * tj], L.v[3 * tj + 1], L.v[3 * tj + 2]) : T(0);
   };
-  T tl, tu, ll, lu;
-  {
-    const T cu0 = C_row();
-    tl = con ? fmax(cu0 - L.p_lo[tid], T(THR0)) : T(1);
-    tu = con ? fmax(L.p_hi[tid] - cu0, T(THR0)) : T(1);
-    ll = con ? T(S.mu0) / tl : T(0);
-    lu = con ? T(S.mu0) / tu : T(0);
+  T tl[PR], tu[PR], ll[PR], lu[PR];
+#pragma unroll
+  for (int s = 0; s < PR; ++s) {
+    const T cu0 = C_row(s);
+    tl[s] = con(s) ? fmax(cu0 - L.p_lo[rowj(s)], T(THR0)) : T(1);
+    tu[s] = con(s) ? fmax(L.p_hi[rowj(s)] - cu0, T(THR0)) : T(1);
+    ll[s] = con(s) ? T(S.mu0) / tl[s] : T(0);
+    lu[s] = con(s) ? T(S.mu0) / tu[s] : T(0);
   }
-  T dtl = T(0), dtu = T(0), dll = T(0), dlu = T(0);
+  T dtl[PR], dtu[PR], dll[PR], dlu[PR];
+#pragma unroll
+  for (int s = 0; s < PR; ++s) dtl[s] = dtu[s] = dll[s] = dlu[s] = T(0);
   __syncthreads();
 
+  // the waves' partials in a fixed association (NW = 4: (0 + 1) + (2 + 3))
+  auto red4 = [&](auto op, int k) -> T {
+    if constexpr (NW == 4) return op(op(L.red[0][k], L.red[1][k]), op(L.red[2][k], L.red[3][k]));
+    else return op(L.red[0][k], L.red[1][k]);
+  };
   auto block_sum = [&](T r) -> T {
     r = wave_sum_dpp(r);
     if (lane0 == 0) L.red[wave0][0] = r;
     __syncthreads();
-    const T o = (L.red[0][0] + L.red[1][0]) + (L.red[2][0] + L.red[3][0]);
+    const T o = red4([](T x, T y) { return x + y; }, 0);
     __syncthreads();
     return o;
   };
@@ -245,7 +274,7 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     r = wave_min_dpp(r);
     if (lane0 == 0) L.red[wave0][0] = r;
     __syncthreads();
-    const T o = fmin(fmin(L.red[0][0], L.red[1][0]), fmin(L.red[2][0], L.red[3][0]));
+    const T o = red4([](T x, T y) { return fmin(x, y); }, 0);
     __syncthreads();
     return o;
   };
@@ -257,27 +286,27 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     return dd == 0 ? (w1 - w0) : (dd == 1 ? (w3 - w2) : (mu_i * (w0 + w1 + w2 + w3) + w4));
   };
 
-  T K[64];
+  T K[NK];
   T invd_i = T(1);
 
   // row partial sums of the lane's rows into L.scr (16 per row, rotated 16-B slots: conflict-free both ways);
-  // FULL = all 8 chunks (H u), else the lower registers c <= rho (forward solve). Input chunk values in xc.
+  // FULL = all 8 chunks (H u), else the lower registers c <= (RG rho) / 16 (forward solve). Input chunk values in xc.
   auto row_partials = [&](const T (&xc)[8], auto full_) {
     constexpr bool full = decltype(full_)::value;
     const int ol = olane(), w = owave();
     const int a = ol >> 4, b = ol & 15;
-    // row i = 16 rho + 4w + a: slot i * 16 + ((b/2 + i) & 7) * 2 + (b & 1); i & 7 = (4w + a) & 7 for every rho
+    // row i = RG rho + 4w + a: slot i * 16 + ((b/2 + i) & 7) * 2 + (b & 1); i & 7 = (4w + a) & 7 for every rho
     const int i0 = 4 * w + a;
     const int base = i0 * 16 + ((((b >> 1) + i0) & 7) << 1) + (b & 1);
-    sfor<0, 8>([&](auto r_) {
+    sfor<0, NR>([&](auto r_) {
       constexpr int rho = decltype(r_)::value;
-      constexpr int ce = full ? 8 : rho + 1;
+      constexpr int ce = full ? 8 : (RG * rho) / 16 + 1;
       T p = K[rho * 8] * xc[0];
       sfor<1, ce>([&](auto c_) {
         constexpr int c = decltype(c_)::value;
         p = fma(K[rho * 8 + c], xc[c], p);
       });
-      L.scr[base + 256 * rho] = p;
+      L.scr[base + 16 * RG * rho] = p;
     });
   };
   auto row_sum = [&]() -> T {  // variable tid's 16 partials (caller synchronised)
@@ -306,18 +335,19 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     }
     __syncthreads();
     const T z = (y - row_sum()) * invd_i;
-    if (isv) L.z[(tid & 15) * 8 + (tid >> 4)] = z;
+    if (isv) L.z[(tid % RG) * NR + tid / RG] = z;
     __syncthreads();
     {
       const int ol = olane(), w = owave();
       const int a = ol >> 4, b = ol & 15;
-      T zr[8];
+      T zr[NR];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) zr[r] = L.z[(4 * w + a) * 8 + r];
+      for (int r = 0; r < NR; ++r) zr[r] = L.z[(4 * w + a) * NR + r];
       sfor<0, 8>([&](auto c_) {
         constexpr int c = decltype(c_)::value;
-        T qv = K[c * 8 + c] * zr[c];
-        sfor<c + 1, 8>([&](auto r_) {
+        constexpr int r0 = c * CR;  // first register row whose diagonal chunk is c
+        T qv = K[r0 * 8 + c] * zr[r0];
+        sfor<r0 + 1, NR>([&](auto r_) {
           constexpr int rho = decltype(r_)::value;
           qv = fma(K[rho * 8 + c], zr[rho], qv);
         });
@@ -328,7 +358,7 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     T qs = T(0);
     if (isv) {
 #pragma unroll
-      for (int k = 0; k < 16; k += 2) qs += L.scr[tid * 16 + k] + L.scr[tid * 16 + k + 1];
+      for (int k = 0; k < RG; k += 2) qs += L.scr[tid * 16 + k] + L.scr[tid * 16 + k + 1];
     }
     y = var ? fma(-invd_i, qs, z) : T(0);
     __syncthreads();  // L.scr / L.v are rewritten next
@@ -339,9 +369,13 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
   int it = 0;
 
   auto direction = [&]() {
-    const T rl = L.p_rl[tid], ru = L.p_ru[tid], itl = L.p_itl[tid], itu = L.p_itu[tid];
-    const T rml = L.p_rml[tid], rmu = L.p_rmu[tid];
-    L.w[tid] = (rml + ll * rl) * itl - (rmu + lu * ru) * itu;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      const int j = rowj(s);
+      const T rl = L.p_rl[j], ru = L.p_ru[j], itl = L.p_itl[j], itu = L.p_itu[j];
+      const T rml = L.p_rml[j], rmu = L.p_rmu[j];
+      L.w[j] = (rml + ll[s] * rl) * itl - (rmu + lu[s] * ru) * itu;
+    }
     __syncthreads();
     const T ctw = CT_var();
     T y = var ? -rg_i - ctw : T(0);
@@ -351,22 +385,30 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     du_i = y;
     if (isv) L.v[tid] = du_i;
     __syncthreads();
-    const T cdu = C_row();
-    dtl = con ? cdu + rl : T(0);
-    dtu = con ? ru - cdu : T(0);
-    dll = -(rml + ll * dtl) * itl;
-    dlu = -(rmu + lu * dtu) * itu;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      const int j = rowj(s);
+      const T rl = L.p_rl[j], ru = L.p_ru[j], itl = L.p_itl[j], itu = L.p_itu[j];
+      const T rml = L.p_rml[j], rmu = L.p_rmu[j];
+      const T cdu = C_row(s);
+      dtl[s] = con(s) ? cdu + rl : T(0);
+      dtu[s] = con(s) ? ru - cdu : T(0);
+      dll[s] = -(rml + ll[s] * dtl[s]) * itl;
+      dlu[s] = -(rmu + lu[s] * dtu[s]) * itu;
+    }
     __syncthreads();  // L.v is rewritten next
   };
-  // fraction-to-boundary ratio: the smallest v / (-d) over the thread's four candidates with d < 0 is selected by
+  // fraction-to-boundary ratio: the smallest v / (-d) over the thread's candidates with d < 0 is selected by
   // cross-multiplication (v, -d > 0) and divided once (k_ipm64: the per-candidate IEEE divisions cost ~3 %)
   auto max_step = [&]() -> T {
     MinRatio<T> mr;
-    auto cand = [&](T v, T d) { mr.cand(v, d); };
-    cand(tl, dtl);
-    cand(tu, dtu);
-    cand(ll, dll);
-    cand(lu, dlu);
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      mr.cand(tl[s], dtl[s]);
+      mr.cand(tu[s], dtu[s]);
+      mr.cand(ll[s], dll[s]);
+      mr.cand(lu[s], dlu[s]);
+    }
     return block_min(mr.value());
   };
 
@@ -389,19 +431,21 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
   };
   for (it = 0;; ++it) {
     progress_prio(it);  // cmpc_device.hpp (lab, n = 120 fp64: 3.94 -> 3.91 ms)
-    // ---- H: 64 loads per lane, 4 rows x 16 consecutive columns per instruction
+    // ---- H: NK loads per lane, 4 rows x 16 consecutive columns per instruction
     {
       const int ol = olane(), w = owave();
       const T* hp = Hq + (size_t)(4 * w + (ol >> 4)) * NP + (ol & 15);
 #pragma unroll
-      for (int rho = 0; rho < 8; ++rho)
+      for (int rho = 0; rho < NR; ++rho)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) K[rho * 8 + c] = hp[16 * rho * NP + 16 * c];
+        for (int c = 0; c < 8; ++c) K[rho * 8 + c] = hp[RG * rho * NP + 16 * c];
     }
     // ---- residuals: C u, H u
     if (isv) L.v[tid] = u_i;
     __syncthreads();
-    const T cu = C_row();
+    T cu[PR];
+#pragma unroll
+    for (int s = 0; s < PR; ++s) cu[s] = C_row(s);
     {
       const int ol = olane();
       const int b = ol & 15;
@@ -412,39 +456,45 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     }
     __syncthreads();
     const T hu = row_sum();
-    const T lo = L.p_lo[tid], hi = L.p_hi[tid];
-    const T rl = con ? cu - lo - tl : T(0);
-    const T ru = con ? hi - cu - tu : T(0);
-    L.p_rl[tid] = rl;
-    L.p_ru[tid] = ru;
-    const T ri = fmax(fabs(rl), fabs(ru));
-    T rc, ms;
-    {
-      const T cl = tl * ll, ch = tu * lu;
-      rc = con ? fmax(cl, ch) : T(0);
-      ms = con ? cl + ch : T(0);
+    T ms = T(0);
+    bool fin_r = true, ok_r = true;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      const int j = rowj(s);
+      const T lo = L.p_lo[j], hi = L.p_hi[j];
+      const T rl = con(s) ? cu[s] - lo - tl[s] : T(0);
+      const T ru = con(s) ? hi - cu[s] - tu[s] : T(0);
+      L.p_rl[j] = rl;
+      L.p_ru[j] = ru;
+      const T ri = fmax(fabs(rl), fabs(ru));
+      const T cl = tl[s] * ll[s], ch = tu[s] * lu[s];
+      const T rc = con(s) ? fmax(cl, ch) : T(0);
+      ms += con(s) ? cl + ch : T(0);
+      L.w[j] = ll[s] - lu[s];
+      L.p_res[1][j] = ri;  // this iteration's residual terms, reduced once at the exit
+      L.p_res[2][j] = rc;
+      fin_r = fin_r && isfinite(ri) && isfinite(rc);
+      ok_r = ok_r && ri <= T(S.tol_ineq) && rc <= T(S.tol_comp);
     }
-    L.w[tid] = ll - lu;
     __syncthreads();
     {
       const T ctw = CT_var();
       rg_i = isv ? hu + g_i - ctw : T(0);
     }
     const T rs = fabs(rg_i);
-    L.p_res[0][tid] = rs;  // this iteration's residual terms, reduced once at the exit
-    L.p_res[1][tid] = ri;
-    L.p_res[2][tid] = rc;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) L.p_res[0][rowj(s)] = s == 0 ? rs : T(0);
     ms = block_sum(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
     const bool st_on = a.stats && it < a.stats_cap;  // statistics row of this iteration (cmpc_enable_stats)
     auto st_row = [&]() { return a.stats + ((size_t)q * a.stats_cap + it) * CMPC_STAT_COLS; };
     if (st_on && tid == 0) L.mu_st = mu;  // the row's residual part is written at the end of the iteration / the exit
     // non-finite residual anywhere -> NAN_SOL; stopping rule as a block vote (max <= tol iff all <= tol)
-    if (__syncthreads_or(!(isfinite(rs) && isfinite(ri) && isfinite(rc)))) {
+    if (__syncthreads_or(!(isfinite(rs) && fin_r))) {
       status = CMPC_NAN_SOL;
       break;
     }
-    if (__syncthreads_and(rs <= T(S.tol_stat) && ri <= T(S.tol_ineq) && rc <= T(S.tol_comp))) {
+    if (__syncthreads_and(rs <= T(S.tol_stat) && ok_r)) {
       status = CMPC_SUCCESS;
       break;
     }
@@ -460,12 +510,14 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
 
     // ---- Newton matrix K = H + C' diag(lam_l/t_l + lam_u/t_u) C + reg I: thread j < 128 writes the 3x3 block
     //      column of variable j (rows t3 .. t3 + 2 of its triple), the tile adds it where entry (i, j) falls there
-    {
-      const T itl = con ? T(1) / tl : T(0);
-      const T itu = con ? T(1) / tu : T(0);
-      L.p_itl[tid] = itl;
-      L.p_itu[tid] = itu;
-      L.w[tid] = ll * itl + lu * itu;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      const int j = rowj(s);
+      const T itl = con(s) ? T(1) / tl[s] : T(0);
+      const T itu = con(s) ? T(1) / tu[s] : T(0);
+      L.p_itl[j] = itl;
+      L.p_itu[j] = itu;
+      L.w[j] = ll[s] * itl + lu[s] * itu;
     }
     __syncthreads();
     if (isv) {
@@ -488,14 +540,17 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     {
       const int ol = olane(), w = owave();
       const int a = ol >> 4, b = ol & 15;
-      // entry (i, j) = (16 rho + 4w + a, 16c + b) is in j's triple iff 0 <= i - 3 (j / 3) <= 2: only registers
-      // c = rho - 1 .. rho + 1 can hold such entries
-      sfor<0, 8>([&](auto r_) {
+      // entry (i, j) = (RG rho + 4w + a, 16c + b) is in j's triple iff 0 <= i - 3 (j / 3) <= 2: only registers
+      // c = clo .. chi can hold such entries
+      sfor<0, NR>([&](auto r_) {
         constexpr int rho = decltype(r_)::value;
-        sfor<(rho > 0 ? rho - 1 : 0), (rho < 7 ? rho + 2 : 8)>([&](auto c_) {
+        constexpr int lo_ = RG * rho - 17;
+        constexpr int clo = lo_ <= 0 ? 0 : (lo_ + 15) / 16;
+        constexpr int chi = (RG * rho + RG + 1) / 16 < 7 ? (RG * rho + RG + 1) / 16 : 7;
+        sfor<clo, chi + 1>([&](auto c_) {
           constexpr int c = decltype(c_)::value;
           const int j = 16 * c + b;
-          const int e = 16 * rho + 4 * w + a - 3 * (j / 3);
+          const int e = RG * rho + 4 * w + a - 3 * (j / 3);
           const bool in = e >= 0 && e <= 2;
           const T val = L.blk[in ? e : 0][j];
           K[rho * 8 + c] += in ? val : T(0);
@@ -504,25 +559,29 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     }
     X_STAMP(1);
     // park the per-thread iterate in LDS across the elimination (its registers hold the pivot pairs instead)
-    L.p_tl[tid] = tl;
-    L.p_tu[tid] = tu;
-    L.p_ll[tid] = ll;
-    L.p_lu[tid] = lu;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      const int j = rowj(s);
+      L.p_tl[j] = tl[s];
+      L.p_tu[j] = tu[s];
+      L.p_ll[j] = ll[s];
+      L.p_lu[j] = lu[s];
+    }
     if (isv) {
       L.p_u[tid] = u_i;
       L.p_rg[tid] = rg_i;
     }
-    // ---- elimination with L^-1 in place (see the header), 16-pivot chunks. The register tile is rotated by one
-    //      row group and one column chunk after every chunk (K[rho][c] <- K[rho + 1][c + 1], indices mod 8), so
-    //      the pivot row group is always register row 0 and the pivot column chunk always register column 0:
-    //      compile-time register indices under a run-time chunk loop. Eight rotations restore the order.
+    // ---- elimination with L^-1 in place (see the header), 16-pivot chunks. The register tile is rotated by CR
+    //      register rows and one column chunk after every chunk (K[rho][c] <- K[rho + CR][c + 1], indices mod NR
+    //      and 8), so the chunk's pivot rows are always register rows 0 .. CR - 1 and the pivot column chunk always
+    //      register column 0: compile-time register indices under a run-time chunk loop. Eight rotations restore
+    //      the order.
     const int nch = (n + 15) >> 4;
-    // Pivots in pairs (p = 16 c0 + 2 b, q = p + 1; both rows in the same wave, register row 0): one barrier and one
+    // Pivots in pairs (p = 16 c0 + 2 b, q = p + 1; both rows in the same wave and register row): one barrier and one
     // LDS round trip per pair. Row q gets pivot p from the broadcast copy (xq' = xq + K[q][p] mp, the look-ahead's
     // own FMA), its pivot from uniform LDS reads (d_q = K[q][q] + K[q][p] (-K[p][q] / d_p)): bit-identical to one
     // pivot at a time.
     T mp[8], mq[8];
-    // multipliers of the pair from the two broadcast rows
     // the pair's pivots and their reciprocals: scalar chain, started as soon as the pair's scalars are read so
     // that its latency (two reciprocals in sequence) runs under the bulk FMAs of the previous pair
     auto pair_piv = [&](T dp, T kqp, T kpq, T kqq, int s, T& invp, T& invq) {
@@ -534,6 +593,7 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
         L.dg[s + 1] = dq;
       }
     };
+    // multipliers of the pair from the two broadcast rows
     auto pair_vec = [&](const T (&xp)[8], const T (&xq)[8], T kqp, T invp, T invq, auto tp_) {
       constexpr int tp = decltype(tp_)::value, tq = tp + 1;
 #pragma unroll
@@ -593,25 +653,30 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
         }
         sfor<0, 8>([&](auto b_) {
           constexpr int b = decltype(b_)::value;
-          constexpr int tp = 2 * b;                            // pivots 16 c0 + tp, + tp + 1
-          constexpr int w2 = (tp + 2) / 4, a2 = (tp + 2) % 4;  // owner wave and first row of the next pair (b < 7)
+          constexpr int tp = 2 * b;  // pivots 16 c0 + tp, + tp + 1
+          // next pair (b < 7): chunk row tp + 2 = RG r2 + 4 w2 + a2 (register row r2 of wave w2, rows a2, a2 + 1)
+          constexpr int r2 = (tp + 2) / RG, w2 = ((tp + 2) % RG) / 4, a2 = (tp + 2) % 4;
           constexpr int nb = (b + 1) & 1;
           const int wv = owave();
           if constexpr (b < 7) {
-            // register row 0 (rows 16 c0 + 4 wv + a) below the pair: 4 wv + a > tp + 1; the next pair's owner
-            // first, then its two rows to LDS
+            // the chunk's rows below the pair: the next pair's owner first, then its two rows to LDS
             if (wv == w2) {
               if constexpr (a2 == 2) {
-                if (la0 >= 2) row_update2(std::integral_constant<int, 0>{}, std::integral_constant<int, tp>{});
+                if (la0 >= 2) row_update2(std::integral_constant<int, r2>{}, std::integral_constant<int, tp>{});
               } else {
-                row_update2(std::integral_constant<int, 0>{}, std::integral_constant<int, tp>{});
+                row_update2(std::integral_constant<int, r2>{}, std::integral_constant<int, tp>{});
               }
               if (la0 == a2 || la0 == a2 + 1) {
 #pragma unroll
-                for (int c = 0; c < 8; ++c) L.rowbuf[nb][la0 - a2][16 * c + lb0] = K[c];
+                for (int c = 0; c < 8; ++c) L.rowbuf[nb][la0 - a2][16 * c + lb0] = K[r2 * 8 + c];
               }
             }
-            if (wv > w2) row_update2(std::integral_constant<int, 0>{}, std::integral_constant<int, tp>{});
+            // every other chunk register row whose rows all lie below the pair
+            sfor<0, CR>([&](auto rr_) {
+              constexpr int rr = decltype(rr_)::value;
+              if (RG * rr + 4 * wv >= tp + 2 && !(rr == r2 && wv == w2))
+                row_update2(rr_, std::integral_constant<int, tp>{});
+            });
           }
           // next pair published: its first row and pivot scalars are read here, landing while the bulk runs (the
           // second row after it: registers)
@@ -632,10 +697,10 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
             kqq = L.rowbuf[nb][1][tp + 3];
             pair_piv(dp, kqp, kpq, kqq, 16 * c0 + tp + 2, invp, invq);
           }
-          // bulk: register rows 1 .. 7 - c0 (row groups below the chunk), padding groups skipped
-          sfor<1, 8>([&](auto r_) {
+          // bulk: register rows CR .. NR - 1 - CR c0 (row groups below the chunk), padding groups skipped
+          sfor<CR, NR>([&](auto r_) {
             constexpr int rho = decltype(r_)::value;
-            if (rho <= 7 - c0 && 16 * (c0 + rho) < n) row_update2(r_, std::integral_constant<int, tp>{});
+            if (rho <= NR - 1 - CR * c0 && 16 * c0 + RG * rho < n) row_update2(r_, std::integral_constant<int, tp>{});
           });
           if constexpr (b < 7) {
 #pragma unroll
@@ -645,20 +710,24 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
         });
         __syncthreads();  // rowbuf[0] is rewritten by the next chunk's first pair
       }
-      // rotate: K[rho][c] <- K[rho + 1][c + 1]
-      T K0[64];
+      // rotate: K[rho][c] <- K[rho + CR][c + 1]
+      T K0[NK];
 #pragma unroll
-      for (int e = 0; e < 64; ++e) K0[e] = K[e];
+      for (int e = 0; e < NK; ++e) K0[e] = K[e];
 #pragma unroll
-      for (int r = 0; r < 8; ++r)
+      for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) K[r * 8 + c] = K0[((r + 1) & 7) * 8 + ((c + 1) & 7)];
+        for (int c = 0; c < 8; ++c) K[r * 8 + c] = K0[((r + CR) % NR) * 8 + ((c + 1) & 7)];
     }
     X_STAMP(2);
-    tl = L.p_tl[tid];
-    tu = L.p_tu[tid];
-    ll = L.p_ll[tid];
-    lu = L.p_lu[tid];
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      const int j = rowj(s);
+      tl[s] = L.p_tl[j];
+      tu[s] = L.p_tu[j];
+      ll[s] = L.p_ll[j];
+      lu[s] = L.p_lu[j];
+    }
     if (isv) {
       u_i = L.p_u[tid];
       rg_i = L.p_rg[tid];
@@ -674,23 +743,32 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
         break;
       }
     }
-    // strict lower part only in the diagonal-straddling registers (rho, c = rho): keep j < i  <=>  b < 4w + a
+    // strict lower part only in the diagonal-straddling registers (rho, c = RG rho / 16): keep j < i
     {
       const int w = owave();
-      sfor<0, 8>([&](auto r_) {
+      sfor<0, NR>([&](auto r_) {
         constexpr int rho = decltype(r_)::value;
-        K[rho * 8 + rho] = (lb0 < 4 * w + la0) ? K[rho * 8 + rho] : T(0);
+        constexpr int cd = (RG * rho) / 16, off = RG * rho - 16 * cd;
+        K[rho * 8 + cd] = (lb0 < off + 4 * w + la0) ? K[rho * 8 + cd] : T(0);
       });
     }
 
     X_STAMP(3);
     // ---- predictor (affine scaling direction)
-    L.p_rml[tid] = tl * ll;
-    L.p_rmu[tid] = tu * lu;
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      L.p_rml[rowj(s)] = tl[s] * ll[s];
+      L.p_rmu[rowj(s)] = tu[s] * lu[s];
+    }
     direction();
     T alpha = fmin(T(1), max_step());
     if (m > 0) {
-      T maff = con ? (tl + alpha * dtl) * (ll + alpha * dll) + (tu + alpha * dtu) * (lu + alpha * dlu) : T(0);
+      T maff = T(0);
+#pragma unroll
+      for (int s = 0; s < PR; ++s)
+        maff += con(s) ? (tl[s] + alpha * dtl[s]) * (ll[s] + alpha * dll[s]) +
+                             (tu[s] + alpha * dtu[s]) * (lu[s] + alpha * dlu[s])
+                       : T(0);
       maff = block_sum(maff) / T(2 * m);
       const T ratio = maff / mu;
       const T sigma = ratio * ratio * ratio;
@@ -701,8 +779,11 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
         sr[2] = (double)sigma;
       }
       // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
-      L.p_rml[tid] = con ? tl * ll + dtl * dll - sigma * mu : T(0);
-      L.p_rmu[tid] = con ? tu * lu + dtu * dlu - sigma * mu : T(0);
+#pragma unroll
+      for (int s = 0; s < PR; ++s) {
+        L.p_rml[rowj(s)] = con(s) ? tl[s] * ll[s] + dtl[s] * dll[s] - sigma * mu : T(0);
+        L.p_rmu[rowj(s)] = con(s) ? tu[s] * lu[s] + dtu[s] * dlu[s] - sigma * mu : T(0);
+      }
       direction();
       alpha = fmin(T(1), T(TAU) * max_step());
     }
@@ -717,10 +798,13 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
       break;
     }
     u_i = fma(alpha, du_i, u_i);
-    tl = fma(alpha, dtl, tl);
-    tu = fma(alpha, dtu, tu);
-    ll = fma(alpha, dll, ll);
-    lu = fma(alpha, dlu, lu);
+#pragma unroll
+    for (int s = 0; s < PR; ++s) {
+      tl[s] = fma(alpha, dtl[s], tl[s]);
+      tu[s] = fma(alpha, dtu[s], tu[s]);
+      ll[s] = fma(alpha, dll[s], ll[s]);
+      lu[s] = fma(alpha, dlu[s], lu[s]);
+    }
     if (st_on && wave0 == 0) stats_res(st_row());  // this iteration's residuals, still in L.p_res
     X_STAMP(7);
   }
@@ -734,7 +818,7 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
   }
   if (a.out_u) {  // the pyramid bounds in L.p_lo are dead by now
     __syncthreads();
-    scatter_result<T>(a, q, n, u_i, status, it, L.p_lo, tid, 256, [] { __syncthreads(); });
+    scatter_result<T>(a, q, n, u_i, status, it, L.p_lo, tid, NT, [] { __syncthreads(); });
   }
   if (a.stats && it < a.stats_cap) {  // the stopping iteration's row: residuals and mu, no step
     __syncthreads();
@@ -745,7 +829,14 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     }
   }
   if (a.res) {  // block max of the last residual terms (each thread reads back what it stored)
-    const T r0 = wave_max_dpp(L.p_res[0][tid]), r1 = wave_max_dpp(L.p_res[1][tid]), r2 = wave_max_dpp(L.p_res[2][tid]);
+    T v0 = L.p_res[0][tid], v1 = L.p_res[1][tid], v2 = L.p_res[2][tid];
+#pragma unroll
+    for (int s = 1; s < PR; ++s) {
+      v0 = fmax(v0, L.p_res[0][rowj(s)]);
+      v1 = fmax(v1, L.p_res[1][rowj(s)]);
+      v2 = fmax(v2, L.p_res[2][rowj(s)]);
+    }
+    const T r0 = wave_max_dpp(v0), r1 = wave_max_dpp(v1), r2 = wave_max_dpp(v2);
     __syncthreads();
     if (lane0 == 0) {
       L.red[wave0][0] = r0;
@@ -754,25 +845,26 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     }
     __syncthreads();
     if (tid == 0) {
+      auto mx = [](T x, T y) { return fmax(x, y); };
       double* o = a.res + (size_t)q * 4;
-      o[0] = (double)fmax(fmax(L.red[0][0], L.red[1][0]), fmax(L.red[2][0], L.red[3][0]));
+      o[0] = (double)red4(mx, 0);
       o[1] = 0.0;
-      o[2] = (double)fmax(fmax(L.red[0][1], L.red[1][1]), fmax(L.red[2][1], L.red[3][1]));
-      o[3] = (double)fmax(fmax(L.red[0][2], L.red[1][2]), fmax(L.red[2][2], L.red[3][2]));
+      o[2] = (double)red4(mx, 1);
+      o[3] = (double)red4(mx, 2);
     }
   }
   X_STAMP_STORE(a.stamps, q);
 }
 
-template <typename T, int MINB>  // MINB workgroups per CU: 2 (fp64, 2 waves per SIMD), 4 (fp32)
-__global__ __launch_bounds__(256, MINB) void k_ipm128x(IpmArgs<T> a) {
+template <typename T, int MINB, int NW = 4>  // MINB workgroups per CU: 2 (fp64, 2 waves per SIMD), 4 (fp32)
+__global__ __launch_bounds__(64 * NW, MINB) void k_ipm128x(IpmArgs<T> a) {
   int q = blockIdx.x;
   if (a.qlist[1]) {  // compacted class list: real QPs first, the surplus workgroups exit
     if (q >= a.qcount[1]) return;
     q = a.qlist[1][q];
     if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
-  ipm128x_body<T, MINB, false>(a, nullptr, q);
+  ipm128x_body<T, MINB, false, NW>(a, nullptr, q);
 }
 
 // Fused condensing + IPM of the 64 < n <= 128 class (cold-start cmpc_solve_batch): one launch over the class list
