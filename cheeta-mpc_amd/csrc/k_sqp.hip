@@ -5,14 +5,20 @@
 // with its line search takeStep (:509-619). Here every QP of the batch iterates (cmpc_sqp_solve_batch, cmpc_api.cpp):
 //   lin_j = (c_k, F_k = sum_i e_ik f_ik) of the nonlinear rollout of U_j   (k_sqp_init / k_sqp_step)
 //   U_qp  = the condensed QP linearised at lin_j, warm-started from U_j  (the hot path itself, CondenseArgs::lin)
-//   alpha = the first of 1, 1/2, ..., 1/128 with J(U_j + alpha d) <= J(U_j), d = U_qp - U_j, else 0
-// with J the NLP cost of the nonlinear rollout (single shooting: no defects, so the cost alone is the merit).
-// The restatement is oracle/cmpc_oracle.c:oracle_sqp_solve / oracle_nlp_rollout_cost; the rollout and cost follow
-// its floating-point order with contraction off, so the line-search decisions are the oracle's.
+//   takeStep (:509-619) with zero constraint violation (single shooting: the rollout meets the dynamics, so the
+//   merit is the NLP cost J, :447): alpha = 1, 1/2, ... while alpha >= alpha_min; Armijo J(U_j + alpha du) <
+//   J(U_j) + armijoFactor alpha metric when the descent metric (:287-296) is negative, else J(U_j + alpha du) < J(U_j);
+//   after a rejection the search stops once alpha |dx| and alpha |du| are both below deltaTol (:596-604);
+//   checkConvergence (:620-645): no step, |J_new - J_j| < costTol, or alpha |dx|, alpha |du| < deltaTol
+// with MultipleShootingSettings.h:42-54's defaults and deltaTol = sqp_tol. The restatement is
+// oracle/cmpc_oracle.c:oracle_sqp_solve / oracle_nlp_rollout_cost / oracle_nlp_linstep; rollout, cost, linearised
+// response and norms follow its floating-point order with contraction off, so the line-search decisions are the
+// oracle's.
 //
-// One wave per QP: lanes 0..7 evaluate the eight trial steps, lane 8 the current iterate (alpha = 0), each lane a
-// whole rollout (13 states x N steps, scalar); the step, the convergence test and the next linearisation point are
-// then lane-parallel over the 12 N inputs.
+// One wave per QP: lanes 0..13 evaluate the fourteen trial steps 2^-m (2^-13 >= alpha_min = 1e-4 > 2^-14), lane 14
+// the current iterate, lane 15 the linearised response |dx| and the descent metric, lane 16 |du|, each lane one whole
+// sequential pass (13 states x N steps); the step, the convergence test and the next linearisation point are then
+// lane-parallel over the 12 N inputs.
 #include <hip/hip_runtime.h>
 
 #include "cmpc/cmpc.h"
@@ -22,6 +28,11 @@
 namespace cmpc {
 
 namespace {
+
+// line search / convergence settings of the SQP: MultipleShootingSettings.h:44-54 defaults (oracle/cmpc_oracle.h)
+constexpr double SQP_ALPHA_MIN = 1e-4;  // 2^-13 is the last trial step (lanes 0..13)
+constexpr double SQP_ARMIJO = 1e-4;
+constexpr double SQP_COST_TOL = 1e-4;
 
 #pragma clang fp contract(off)
 
@@ -108,6 +119,96 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
   return J;
 }
 
+// Linearised response of the rollout of u0 to du = u1 - u0 and the descent metric (MultipleShootingSolver.cpp:287-296):
+// mirrors oracle_nlp_linstep operation for operation. Returns |dx| (trajectoryNorm, :492-503) in dxn.
+__device__ double linstep_metric(const DevModel* M, const double* x0, const double* xref, const double* foot,
+                                 const uint8_t* ct, const double* u0, const double* u1, double* dxn) {
+  const int N = M->N;
+  const double dt = M->dt;
+  double xs[NX], xn[NX], dx[NX], dn[NX];
+  for (int s = 0; s < NX; ++s) {
+    xs[s] = x0[s];
+    dx[s] = 0.0;
+  }
+  double ss = 0.0, mt = 0.0;
+  for (int k = 0; k < N; ++k) {
+    const double* uk = u0 + (size_t)k * NU;
+    double duk[NU];
+    for (int j = 0; j < NU; ++j) duk[j] = u1[(size_t)k * NU + j] - uk[j];
+    double F[3] = {0.0, 0.0, 0.0}, Tq[3] = {0.0, 0.0, 0.0}, dF[3] = {0.0, 0.0, 0.0}, dT[3] = {0.0, 0.0, 0.0};
+    int ns = 0;
+    for (int i = 0; i < NL; ++i) {
+      if (!ct[k * NL + i]) continue;
+      ++ns;
+      double p[3];
+      stance_point(foot, ct, N, k, i, p);
+      const double* f = uk + 3 * i;
+      const double* df = duk + 3 * i;
+      const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
+      F[0] += f[0];
+      F[1] += f[1];
+      F[2] += f[2];
+      Tq[0] += ry * f[2] - rz * f[1];
+      Tq[1] += rz * f[0] - rx * f[2];
+      Tq[2] += rx * f[1] - ry * f[0];
+      dF[0] += df[0];
+      dF[1] += df[1];
+      dF[2] += df[2];
+      dT[0] += (ry * df[2] - rz * df[1]) - (dx[1] * f[2] - dx[2] * f[1]);
+      dT[1] += (rz * df[0] - rx * df[2]) - (dx[2] * f[0] - dx[0] * f[2]);
+      dT[2] += (rx * df[1] - ry * df[0]) - (dx[0] * f[1] - dx[1] * f[0]);
+    }
+    for (int j = 0; j < NU; ++j) {
+      const int i = j / 3;
+      const double fd = (j % 3 == 2 && ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
+      double gu = 2.0 * M->Wf[j] * (uk[j] - fd);
+      if (k > 0) gu += 2.0 * M->Wr[j] * (uk[j] - u0[(size_t)(k - 1) * NU + j]);
+      if (k + 1 < N) gu -= 2.0 * M->Wr[j] * (u0[(size_t)(k + 1) * NU + j] - uk[j]);
+      mt += gu * duk[j];
+    }
+    double sp, cp;
+    sincos(xref[k * NX + 11], &sp, &cp);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int d = 0; d < 3; ++d) {
+      xn[d] = xs[d] + dt * xs[3 + d];
+      dn[d] = dx[d] + dt * dx[3 + d];
+    }
+    xn[3] = xs[3] + dt * (F[0] / M->mass);
+    xn[4] = xs[4] + dt * (F[1] / M->mass);
+    xn[5] = xs[5] + dt * (xs[12] + F[2] / M->mass);
+    dn[3] = dx[3] + dt * (dF[0] / M->mass);
+    dn[4] = dx[4] + dt * (dF[1] / M->mass);
+    dn[5] = dx[5] + dt * (dx[12] + dF[2] / M->mass);
+    for (int d = 0; d < 3; ++d) {
+      xn[6 + d] = xs[6 + d] + dt * Tq[d];
+      dn[6 + d] = dx[6 + d] + dt * dT[d];
+    }
+    for (int a = 0; a < 3; ++a) {
+      double m = 0.0, dm = 0.0;
+      for (int b = 0; b < 3; ++b) {
+        double s2 = 0.0;
+        for (int e = 0; e < 3; ++e) s2 += M->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
+        m += dt * s2 * xs[6 + b];
+        dm += dt * s2 * dx[6 + b];
+      }
+      xn[9 + a] = xs[9 + a] + m;
+      dn[9 + a] = dx[9 + a] + dm;
+    }
+    xn[12] = xs[12];
+    dn[12] = dx[12];
+    for (int s = 0; s < NX; ++s) {
+      xs[s] = xn[s];
+      dx[s] = dn[s];
+    }
+    for (int s = 0; s < NX; ++s) {
+      mt += M->qdiag[k + 1][s] * (xs[s] - xref[(k + 1) * NX + s]) * dx[s];
+      ss += dx[s] * dx[s];
+    }
+  }
+  *dxn = sqrt(ss);
+  return mt;
+}
+
 // U_j <- the cold QP's solution, lin <- its rollout; QPs the cold QP rejected are done from the start.
 __global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
   const int q = blockIdx.x;
@@ -150,28 +251,40 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     }
     return;
   }
-  // trial steps: lane m < 8 -> alpha = 2^-m, lane 8 -> the current iterate
-  double J = 0.0;
-  if (lane <= 8) {
-    const double alpha = lane < 8 ? ldexp(1.0, -lane) : 0.0;
-    J = lane < 8 ? rollout_cost(M, x0, xr, ft, ct, uj, uq, alpha, nullptr, nullptr)
-                 : rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, nullptr, nullptr);
+  // lanes m < 14: trial step alpha = 2^-m; lane 14: the current iterate; lane 15: |dx| and the descent metric;
+  // lane 16: |du| (sequential, the oracle's order)
+  double J = 0.0, aux = 0.0;
+  if (lane < 14) {
+    J = rollout_cost(M, x0, xr, ft, ct, uj, uq, ldexp(1.0, -lane), nullptr, nullptr);
+  } else if (lane == 14) {
+    J = rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, nullptr, nullptr);
+  } else if (lane == 15) {
+    J = linstep_metric(M, x0, xr, ft, ct, uj, uq, &aux);
+  } else if (lane == 16) {
+    double s2 = 0.0;
+    for (int i = 0; i < nu; ++i) {
+      const double d = uq[i] - uj[i];
+      s2 += d * d;
+    }
+    aux = sqrt(s2);
   }
-  const double J0 = __shfl(J, 8, 64);
-  const unsigned long long ok = __ballot(lane < 8 && J <= J0);
-  const double alpha = ok ? ldexp(1.0, -(__ffsll((long long)ok) - 1)) : 0.0;
-  // |d|_inf, |U_j|_inf, then the step (lane-parallel over the inputs)
-  double dm = 0.0, um = 0.0;
-  for (int i = lane; i < nu; i += 64) {
-    dm = fmax(dm, fabs(uq[i] - uj[i]));
-    um = fmax(um, fabs(uj[i]));
-  }
-  dm = wave_max(dm);
-  um = wave_max(um);
+  const double J0 = __shfl(J, 14, 64);
+  const double metric = __shfl(J, 15, 64), dxn = __shfl(aux, 15, 64), dun = __shfl(aux, 16, 64);
+  const double tol = a.tol;
+  // lane m: accepted (Armijo / decrease), and the early exit after a rejection at alpha = 2^-m (m >= 1)
+  const double am = ldexp(1.0, -(lane < 14 ? lane : 0));
+  const bool okm = lane < 14 && (metric < 0.0 ? (J < J0 + SQP_ARMIJO * am * metric) : (J < J0));
+  const bool exm = lane >= 1 && lane < 14 && am * dxn < tol && am * dun < tol;
+  const unsigned long long okb = __ballot(okm), exb = __ballot(exm);
+  const int e = exb ? __ffsll((long long)exb) - 1 : 14;  // trials m >= e are never reached
+  const unsigned long long reach = okb & ((1ull << e) - 1ull);
+  const int ma = reach ? __ffsll((long long)reach) - 1 : -1;
+  const double alpha = ma >= 0 ? ldexp(1.0, -ma) : 0.0;
+  const double Jn = ma >= 0 ? __shfl(J, ma, 64) : J0;
   __syncthreads();
   if (alpha > 0.0)
     for (int i = lane; i < nu; i += 64) uj[i] = uj[i] + alpha * (uq[i] - uj[i]);
-  const bool conv = alpha == 0.0 || alpha * dm <= a.tol * fmax(1.0, um);
+  const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
   __syncthreads();
   if (lane == 0) {
     if (conv) a.done[q] = 1;

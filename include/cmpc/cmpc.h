@@ -152,10 +152,14 @@ int cmpc_solve_batch_warm(cmpc_ctx* ctx, int B, const double* d_x0, const double
 /* Batched Gauss-Newton SQP on the bilinear centroidal NLP: the reference's NLP keeps the lever
  * arm (p_i - c) x f_i bilinear (CentroidalMPC.cpp:86). Per QP: U_0 = the QP at the reference linearisation (as
  * cmpc_solve_batch); then up to sqp_iter_max times: linearise at the nonlinear rollout of U_j (lever arm p - c_k,
- * dt F_k x (c - c_k) coupling), solve that QP warm-started from U_j, and take the first step of 1, 1/2, ..., 1/128
- * that does not raise the NLP cost of the nonlinear rollout (MultipleShootingSolver::runImpl / takeStep,
- * MultipleShootingSolver.cpp:146-214, :509-619, play this role in ocs2). A QP stops when its accepted step is
- * <= sqp_tol max(1, |U_j|_inf) or no step is accepted. d_x (optional) receives the nonlinear rollout. d_qp_iters:
+ * dt F_k x (c - c_k) coupling), solve that QP warm-started from U_j, and step by ocs2's filter line search
+ * (MultipleShootingSolver::takeStep, MultipleShootingSolver.cpp:509-619) in its zero-violation form (single shooting:
+ * the rollout meets the dynamics, the merit is the NLP cost): alpha = 1, 1/2, ... >= alpha_min = 1e-4, Armijo
+ * (armijoFactor 1e-4) on the descent metric grad J . [dx; du] (:287-296) when it is negative, else plain decrease;
+ * the search ends early once alpha |dx| and alpha |du| are below deltaTol. A QP stops (checkConvergence, :620-645)
+ * when no step is taken, when |J_new - J_j| < costTol = 1e-4, or when alpha |dx| and alpha |du| (2-norms over the
+ * trajectory) are both below deltaTol = sqp_tol (ocs2 default 1e-6); the other settings are
+ * MultipleShootingSettings.h:44-54's defaults. d_x (optional) receives the nonlinear rollout. d_qp_iters:
  * total IPM iterations, d_sqp_iters: SQP iterations (both optional). Synchronises the stream once per SQP iteration
  * (early exit when every QP has converged). */
 int cmpc_sqp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,

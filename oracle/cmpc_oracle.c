@@ -1322,19 +1322,117 @@ double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const d
   return J;
 }
 
+/* Linearised response of the rollout of u to the step du (the QP's dx, single shooting: no defects) and the descent
+ * metric of MultipleShootingSolver::getOCPSolution (MultipleShootingSolver.cpp:287-296): sum_k dJ/dx_k . dx_k +
+ * dJ/du_k . du_k at u. Returns |dx| (trajectoryNorm, :492-503: the 2-norm over the whole trajectory) and the metric.
+ * Jacobian of the step of oracle_nlp_rollout_cost at (x_k, u_k); floating-point order is the one k_sqp_step follows. */
+void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                        const uint8_t* contact, const double* u, const double* du, double* dxnorm, double* metric) {
+  const int N = c->N, L = c->L;
+  const double dt = c->dt;
+  double xs[NX], xn[NX], dx[NX], dn[NX];
+  memcpy(xs, x0, sizeof(xs));
+  memset(dx, 0, sizeof(dx));
+  double ss = 0.0, mt = 0.0;
+  for (int k = 0; k < N; ++k) {
+    const double* uk = u + (size_t)k * NU;
+    const double* duk = du + (size_t)k * NU;
+    double F[3] = {0.0, 0.0, 0.0}, T[3] = {0.0, 0.0, 0.0}, dF[3] = {0.0, 0.0, 0.0}, dT[3] = {0.0, 0.0, 0.0};
+    int ns = 0;
+    for (int i = 0; i < L; ++i) {
+      if (!contact[k * L + i]) continue;
+      ++ns;
+      double p[3];
+      oracle_stance_point(foot, contact, N, L, k, i, p);
+      const double* f = uk + 3 * i;
+      const double* df = duk + 3 * i;
+      const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
+      F[0] += f[0];
+      F[1] += f[1];
+      F[2] += f[2];
+      T[0] += ry * f[2] - rz * f[1];
+      T[1] += rz * f[0] - rx * f[2];
+      T[2] += rx * f[1] - ry * f[0];
+      dF[0] += df[0];
+      dF[1] += df[1];
+      dF[2] += df[2];
+      /* d[(p - c) x f] = (p - c) x df - dc x f */
+      dT[0] += (ry * df[2] - rz * df[1]) - (dx[1] * f[2] - dx[2] * f[1]);
+      dT[1] += (rz * df[0] - rx * df[2]) - (dx[2] * f[0] - dx[0] * f[2]);
+      dT[2] += (rx * df[1] - ry * df[0]) - (dx[0] * f[1] - dx[1] * f[0]);
+    }
+    (void)T;
+    /* dJ/du_k . du_k: force tracking and both force-rate terms that hold u_k */
+    for (int j = 0; j < NU; ++j) {
+      const int i = j / 3;
+      const double fd = (j % 3 == 2 && contact[k * L + i] && ns > 0) ? c->mass * GRAV / (double)ns : 0.0;
+      double gu = 2.0 * c->Wf[j] * (uk[j] - fd);
+      if (k > 0) gu += 2.0 * c->Wr[j] * (uk[j] - u[(size_t)(k - 1) * NU + j]);
+      if (k + 1 < N) gu -= 2.0 * c->Wr[j] * (u[(size_t)(k + 1) * NU + j] - uk[j]);
+      mt += gu * duk[j];
+    }
+    const double psi = xref[k * NX + 11];
+    const double cp = cos(psi), sp = sin(psi);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int d = 0; d < 3; ++d) {
+      xn[d] = xs[d] + dt * xs[3 + d];
+      dn[d] = dx[d] + dt * dx[3 + d];
+    }
+    xn[3] = xs[3] + dt * (F[0] / c->mass);
+    xn[4] = xs[4] + dt * (F[1] / c->mass);
+    xn[5] = xs[5] + dt * (xs[12] + F[2] / c->mass);
+    dn[3] = dx[3] + dt * (dF[0] / c->mass);
+    dn[4] = dx[4] + dt * (dF[1] / c->mass);
+    dn[5] = dx[5] + dt * (dx[12] + dF[2] / c->mass);
+    for (int d = 0; d < 3; ++d) {
+      xn[6 + d] = xs[6 + d] + dt * T[d];
+      dn[6 + d] = dx[6 + d] + dt * dT[d];
+    }
+    for (int a = 0; a < 3; ++a) {
+      double m = 0.0, dm = 0.0;
+      for (int b = 0; b < 3; ++b) {
+        double s2 = 0.0;
+        for (int e = 0; e < 3; ++e) s2 += c->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
+        m += dt * s2 * xs[6 + b];
+        dm += dt * s2 * dx[6 + b];
+      }
+      xn[9 + a] = xs[9 + a] + m;
+      dn[9 + a] = dx[9 + a] + dm;
+    }
+    xn[12] = xs[12];
+    dn[12] = dx[12];
+    memcpy(xs, xn, sizeof(xs));
+    memcpy(dx, dn, sizeof(dx));
+    /* dJ/dx_{k+1} . dx_{k+1} and |dx|^2 */
+    for (int sI = 0; sI < NX; ++sI) {
+      mt += c->qdiag[k + 1][sI] * (xs[sI] - xref[(k + 1) * NX + sI]) * dx[sI];
+      ss += dx[sI] * dx[sI];
+    }
+  }
+  *dxnorm = sqrt(ss);
+  *metric = mt;
+}
+
 /* Gauss-Newton SQP on the centroidal NLP (the role of MultipleShootingSolver::runImpl, MultipleShootingSolver.cpp:
- * 146-214, for this problem; single shooting, so the merit is the NLP cost of the nonlinear rollout):
+ * 146-214, for this problem; single shooting, so the dynamics are met exactly and the merit is the NLP cost of the
+ * nonlinear rollout, :447):
  *   U_0 = QP at the reference (lin = NULL);
- *   repeat: lin = (c_k, F_k) of the rollout of U_j; U_qp = QP at lin, warm-started from U_j; d = U_qp - U_j;
- *           alpha = the first of 1, 1/2, ..., 1/128 with J(U_j + alpha d) <= J(U_j) (else 0);
- *           U_{j+1} = U_j + alpha d; stop when alpha |d|_inf <= sqp_tol max(1, |U_j|_inf) or alpha = 0.
- * The pyramid constraints are linear in f, so every trial point stays feasible. */
+ *   repeat: lin = (c_k, F_k) of the rollout of U_j; U_qp = QP at lin, warm-started from U_j; du = U_qp - U_j;
+ *           takeStep (:509-619) with zero constraint violation: alpha = 1, 1/2, ... while alpha >= alpha_min; accept
+ *           J(U_j + alpha du) < J(U_j) + armijoFactor alpha metric if metric < 0 (Armijo, :562-566), else
+ *           J(U_j + alpha du) < J(U_j) (:567-571); after a rejection stop early once alpha |dx| and alpha |du| are
+ *           both below deltaTol (:596-604);
+ *           checkConvergence (:620-645): stop when no step was taken, when |J_new - J_j| < costTol, or when
+ *           alpha |dx| and alpha |du| are both below deltaTol.
+ * Settings are MultipleShootingSettings.h:42-54's defaults, deltaTol = sqp_tol. The pyramid constraints are linear in
+ * f, so every trial point stays feasible. */
 int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
                      const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
                      double* x, int* qp_iters, int* sqp_iters) {
   const int N = c->N, nu = N * NU;
   double* uq = (double*)malloc(sizeof(double) * nu);
   double* ut = (double*)malloc(sizeof(double) * nu);
+  double* du = (double*)malloc(sizeof(double) * nu);
   double* lin = (double*)malloc(sizeof(double) * N * 6);
   cmpc_settings sw = *s;
   sw.warm_start = 0;
@@ -1352,22 +1450,30 @@ int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_ite
         st = sq;
         break;
       }
-      double dmax_ = 0.0, umax = 0.0;
+      double dun2 = 0.0;
       for (int i = 0; i < nu; ++i) {
-        dmax_ = dmax(dmax_, fabs(uq[i] - u[i]));
-        umax = dmax(umax, fabs(u[i]));
+        du[i] = uq[i] - u[i];
+        dun2 += du[i] * du[i];
       }
-      double alpha = 0.0, a = 1.0;
-      for (int m = 0; m < 8; ++m, a *= 0.5) {
-        for (int i = 0; i < nu; ++i) ut[i] = u[i] + a * (uq[i] - u[i]);
-        if (oracle_nlp_rollout_cost(c, x0, xref, foot, contact, ut, NULL, NULL) <= J0) {
+      const double dun = sqrt(dun2);
+      double dxn = 0.0, metric = 0.0;
+      oracle_nlp_linstep(c, x0, xref, foot, contact, u, du, &dxn, &metric);
+      double alpha = 0.0, Jn = J0;
+      for (double a = 1.0; a >= SQP_ALPHA_MIN;) {
+        for (int i = 0; i < nu; ++i) ut[i] = u[i] + a * du[i];
+        const double Jt = oracle_nlp_rollout_cost(c, x0, xref, foot, contact, ut, NULL, NULL);
+        const int ok = metric < 0.0 ? (Jt < J0 + SQP_ARMIJO * a * metric) : (Jt < J0);
+        if (ok) {
           alpha = a;
+          Jn = Jt;
           break;
         }
+        a *= SQP_ALPHA_DECAY;
+        if (a * dxn < sqp_tol && a * dun < sqp_tol) break;
       }
       if (alpha > 0.0)
-        for (int i = 0; i < nu; ++i) u[i] = u[i] + alpha * (uq[i] - u[i]);
-      if (alpha == 0.0 || alpha * dmax_ <= sqp_tol * dmax(1.0, umax)) {
+        for (int i = 0; i < nu; ++i) u[i] = u[i] + alpha * du[i];
+      if (alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < sqp_tol && alpha * dun < sqp_tol)) {
         ++its;
         break;
       }
@@ -1378,6 +1484,7 @@ int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_ite
   if (sqp_iters) *sqp_iters = its;
   free(uq);
   free(ut);
+  free(du);
   free(lin);
   return st;
 }

@@ -59,6 +59,13 @@ int oracle_solve_one_lin(const oracle_consts* c, const cmpc_settings* s, const d
 double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
                                const uint8_t* contact, const double* u, double* x, double* lin);
 /* Gauss-Newton SQP on the bilinear NLP; u [N][L][3] out, x [(N+1)][13] nonlinear rollout. */
+/* line search / convergence settings of the SQP: MultipleShootingSettings.h:44-54 defaults */
+#define SQP_ALPHA_DECAY 0.5
+#define SQP_ALPHA_MIN 1e-4
+#define SQP_ARMIJO 1e-4
+#define SQP_COST_TOL 1e-4
+void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                        const uint8_t* contact, const double* u, const double* du, double* dxnorm, double* metric);
 int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
                      const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
                      double* x, int* qp_iters, int* sqp_iters);

@@ -106,6 +106,8 @@ def lib():
         L.oracle_nlp_rollout_cost.argtypes = [C.c_void_p, d, d, d, u8, d, d, d]
         L.oracle_nlp_rollout_cost.restype = C.c_double
         L.oracle_sqp_solve.argtypes = [C.c_void_p, P(Settings), C.c_int, C.c_double, d, d, d, u8, d, d, i, i]
+        L.oracle_nlp_linstep.argtypes = [C.c_void_p, d, d, d, u8, d, d, d, d]
+        L.oracle_nlp_linstep.restype = None
         L.oracle_srbd_dynamics_lin.argtypes = [C.c_void_p, d, d, u8, d, d, d, d]
         L.oracle_srbd_dynamics_lin.restype = None
         L.oracle_policy.argtypes = [C.c_void_p, d, d, u8, d, C.c_double, d, i]
@@ -240,6 +242,17 @@ def nlp_rollout_cost(model, x0, xref, foot, contact, u):
     J = lib().oracle_nlp_rollout_cost(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u), _p(x),
                                       _p(lin))
     return J, x, lin
+
+
+def nlp_linstep(model, x0, xref, foot, contact, u, du):
+    """Linearised response of the rollout of u to du: (|dx| over the trajectory, descent metric grad J . [dx; du])."""
+    c = consts(model)
+    x0, xref, foot, u, du = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, xref, foot, u, du))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    dxn, mt = C.c_double(0.0), C.c_double(0.0)
+    lib().oracle_nlp_linstep(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u), _p(du),
+                             C.byref(dxn), C.byref(mt))
+    return dxn.value, mt.value
 
 
 def sqp_solve(model, settings, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7):

@@ -95,6 +95,45 @@ def test_oracle_sqp_converges_to_nlp_stationary_point(op):
     assert np.all(u[contact[5] == 0] == 0.0)
 
 
+def test_linstep_is_the_directional_derivative(op):
+    """The line search's inputs (MultipleShootingSolver.cpp:287-296, :492-503): the descent metric is grad J . du
+    along the nonlinear rollout and |dx| the norm of the rollout's linear response, both by central differences."""
+    N = 10
+    mo = op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, 4, gait=1)
+    rng = np.random.default_rng(7)
+    for q in range(4):
+        u = op.solve_batch(mo, op.default_settings(), x0[q:q + 1], xref[q:q + 1], foot[q:q + 1], contact[q:q + 1])[0][0]
+        du = rng.standard_normal(u.shape) * 5.0 * contact[q][..., None]
+        dxn, mt = op.nlp_linstep(mo, x0[q], xref[q], foot[q], contact[q], u, du)
+        h = 1e-4
+        Jp, xp, _ = op.nlp_rollout_cost(mo, x0[q], xref[q], foot[q], contact[q], u + h * du)
+        Jm, xm, _ = op.nlp_rollout_cost(mo, x0[q], xref[q], foot[q], contact[q], u - h * du)
+        assert abs(mt - (Jp - Jm) / (2 * h)) < 1e-6 * max(1.0, abs(mt))
+        assert abs(dxn - np.linalg.norm((xp - xm) / (2 * h))) < 1e-7 * max(1.0, dxn)
+
+
+def test_sqp_line_search_rules(op):
+    """Every accepted SQP step satisfies the reference's acceptance test (Armijo with the descent metric when it is
+    negative, plain decrease otherwise; MultipleShootingSolver.cpp:562-571) at a step 2^-m >= alpha_min."""
+    N = 10
+    mo = op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, 6, gait=1)
+    s = op.default_settings()
+    for q in range(6):
+        u_prev = None
+        for its in range(1, 6):
+            u, _, st, _, si = op.sqp_solve(mo, s, x0[q], xref[q], foot[q], contact[q], sqp_iter_max=its, sqp_tol=1e-9)
+            assert st == 0
+            if u_prev is not None and si == its:
+                J0, _, lin = op.nlp_rollout_cost(mo, x0[q], xref[q], foot[q], contact[q], u_prev)
+                J1 = op.nlp_rollout_cost(mo, x0[q], xref[q], foot[q], contact[q], u)[0]
+                assert J1 <= J0
+            u_prev = u
+            if si < its:
+                break
+
+
 def condense_lin(op, mo, x0, xref, foot, contact, lin):
     """Condensed QP at a linearisation point through the oracle's full condensing + elimination."""
     import ctypes as C
