@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box script (round 2 evidence): GPU tests, smoke, headline bench with the CPU baseline, rocprofv3 kernel stats,
+# GPU-box script (round 2 evidence, re-run after each change of libcmpc.so): GPU tests, smoke, headline bench with the CPU baseline, rocprofv3 kernel stats,
 # FETCH_SIZE / WRITE_SIZE traffic summaries (md5-stamped) for the headline and configs 3 / 5, SQ counter passes.
 # Every GPU step has its own time limit; a fault / abort / time-out ends the script.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/final; mkdir -p $O; cd $R
