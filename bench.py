@@ -111,6 +111,23 @@ def pmc_traffic(path, prefix):
     return (tot if tot > 0 else None), os.path.basename(path)
 
 
+def pmc_sq(wkey, prefix):
+    """Per-dispatch SQ counters of the kernel whose name contains `prefix`, from the committed rocprofv3 --pmc summary
+    of this workload (profiles/pmc_sq_<workload key>.json, cheeta-mpc_amd/tools/pmc_summary.py), only when it was
+    taken on this exact build of libcmpc.so (md5)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_sq_{wkey}.json")
+    if not os.path.exists(path):
+        return None, "no SQ PMC summary for this workload"
+    with open(path) as f:
+        doc = json.load(f)
+    if doc.get("lib_md5") != lib_md5():
+        return None, f"SQ PMC summary {os.path.basename(path)} was taken on another build of libcmpc.so"
+    for k, v in doc["kernels"].items():
+        if prefix in k:
+            return v["counters"], os.path.basename(path)
+    return None, f"{prefix} not in {os.path.basename(path)}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -272,6 +289,23 @@ def main():
         extra = {"roofline_other_stage": other,
                  "roofline_solve": roof("whole solve (all classes, condensing + IPM)", f_all, ms_cond + ms_ipm,
                                         "valu", "cmpc::k_", "IPM + condensing FLOPs of every QP")}
+        # the condensing's H = Bqp' Q Bqp contraction inside k_solve64 runs on the matrix cores: its MFMA rate and
+        # busy fraction from the committed SQ counters of this build (executed MFMA FLOPs = MOPS x 512)
+        c, src = pmc_sq(wkey, "k_solve64")
+        mops = c.get("SQ_INSTS_VALU_MFMA_MOPS_F64" if prec == cm.F64 else "SQ_INSTS_VALU_MFMA_MOPS_F32") if c else None
+        if mops is not None and ms_cond > 0:
+            mfl = 512.0 * mops
+            cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0  # GRBM_GUI_ACTIVE sums the 8 XCDs
+            extra["mfma_condensing"] = {
+                "kernel": "k_solve64 condensing phase (H = Bqp' Q Bqp on v_mfma_%s_16x16x4), rate over the fused "
+                          "kernel's duration" % ("f64" if prec == cm.F64 else "f32"),
+                "mfma_flops_per_launch": mfl, "achieved": mfl / (ms_cond * 1e-3) / 1e12, "peak": peak / 1e12,
+                "unit": "TFLOP/s", "frac": mfl / (ms_cond * 1e-3) / peak,
+                "mfma_busy_frac": (c["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024.0)
+                                   if cyc > 0 and "SQ_VALU_MFMA_BUSY_CYCLES" in c else None),
+                "source": src}
+        else:
+            extra["mfma_condensing"] = {"kernel": "k_solve64 condensing phase", "achieved": None, "source": src}
     else:
         roofline = roof("IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)", float(fl_ipm.sum()),
                         ms_ipm, "valu", "k_ipm", "IPM FLOPs")

@@ -4,7 +4,7 @@ derive the utilisation figures DESIGN.md quotes. Units follow MI355X_MICROARCH.m
 SQ_WAIT_* and SQ_ACTIVE_INST_* count quad-cycles (x4 = shader cycles); SQ_VALU_MFMA_BUSY_CYCLES counts cycles;
 SQ_INSTS_* are wave-instructions summed over the dispatch; GRBM_GUI_ACTIVE is summed over the 8 XCDs.
 
-  python pmc_summary.py <dir> [--json out.json]
+  python pmc_summary.py <dir> [--json out.json]     (out.json: {"lib_md5": ..., "kernels": {name: ...}})
 """
 import collections
 import csv
@@ -68,8 +68,14 @@ def main():
         for dn, dv in res[k]["derived"].items():
             print(f"  = {dn:32s} {dv:.4g}")
     if "--json" in sys.argv:
+        # stamped with the libcmpc.so md5 of this tree, so bench.py reports the MFMA figures only for the build the
+        # counters were taken on
+        import hashlib
+        lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lib", "libcmpc.so")
+        with open(lib, "rb") as f:
+            md5 = hashlib.md5(f.read()).hexdigest()
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
-            json.dump(res, f, indent=1)
+            json.dump({"lib_md5": md5, "kernels": res}, f, indent=1)
 
 
 if __name__ == "__main__":

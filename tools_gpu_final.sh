@@ -19,13 +19,13 @@ for W in "N10_B4096_f64_trot|" "N20_B4096_f32_trot|--horizon 20 --precision f32"
   done
   python3 $R/cheeta-mpc_amd/tools/pmc_traffic.py $D $O/traffic_$KEY.json "$BA" > $D/summary.txt || exit 1
 done
-for W in "head|" "c3|--horizon 20 --precision f32" "c5|--gait 1"; do
-  KEY=${W%%|*}; BA=${W#*|}; D=$O/sq_$KEY; mkdir -p $D; i=0
+for W in "head|N10_B4096_f64_trot|" "c3|N20_B4096_f32_trot|--horizon 20 --precision f32" "c5|N10_B4096_f64_mixed|--gait 1"; do
+  KEY=${W%%|*}; R2=${W#*|}; WK=${R2%%|*}; BA=${R2#*|}; D=$O/sq_$KEY; mkdir -p $D; i=0
   for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace --stats -d $D/p$i -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-sample 0 $BA > $D/p$i.log 2>&1; rc=$?
     echo "sq $KEY pass $i rc=$rc"; [ $rc -ne 0 ] && exit 1
   done
-  python3 $R/cheeta-mpc_amd/tools/pmc_summary.py $D --json $O/sq_$KEY.json > $O/sq_$KEY.txt || exit 1
+  python3 $R/cheeta-mpc_amd/tools/pmc_summary.py $D --json $O/pmc_sq_$WK.json > $O/sq_$KEY.txt || exit 1
 done
 echo all_done
