@@ -197,7 +197,7 @@ def main():
     def step(i):
         e, (uo, so, io), sh = engs[i % K], outs[i % K], streams[i % K]
         if args.sqp_iters > 0:
-            cm.lib().cmpc_sqp_solve_batch(e.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, args.sqp_iters, 1e-7,
+            cm.lib().cmpc_sqp_solve_batch(e.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, args.sqp_iters, 1e-6,
                                           uo.ptr, None, so.ptr, sqp_qi.ptr, sqp_si.ptr, sh)
         else:
             e.solve_device(B, x0, xref, foot, contact, uo, None, so, io, sh)

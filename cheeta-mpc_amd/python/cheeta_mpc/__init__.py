@@ -289,8 +289,9 @@ class Engine:
         _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
         return r.host()
 
-    def sqp_solve(self, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7, want_x=True):
-        """Batched SQP on the bilinear NLP (cmpc_sqp_solve_batch): (u, x, status, qp_iters, sqp_iters)."""
+    def sqp_solve(self, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-6, want_x=True):
+        """Batched SQP on the bilinear NLP (cmpc_sqp_solve_batch): (u, x, status, qp_iters, sqp_iters). sqp_tol is
+        ocs2's deltaTol (MultipleShootingSettings.h:43, default 1e-6): the bound on alpha |dx| and alpha |du|."""
         B = x0.shape[0]
         N = self.model.N
         d = {k: DeviceArray.from_host(v) for k, v in
