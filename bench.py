@@ -236,15 +236,19 @@ def main():
     gather = {"what": "U of every rank into rank 0's GPU (cmpc_ipc_open + cmpc_gather_shard), after the timed steps",
               "bytes": world * B * N * 12 * 8, "ms": 0.0 if world == 1 else None}
     if world > 1:
+        # ResultGather's constructor and gather() reach every collective on every rank and raise on all ranks
+        # together, so the collectives below stay matched whatever fails
         try:
             from cheeta_mpc.shard import ResultGather
             row = N * 12 * 8
             rg = ResultGather(dist, world * B * row)
             barrier()
             tg = time.perf_counter()
-            rg.gather(u.ptr, rank * B * row, B * row, stream)
-            gather["ms"] = max_over_ranks(time.perf_counter() - tg) * 1e3
-            rg.close()
+            try:
+                rg.gather(u.ptr, rank * B * row, B * row, stream)
+                gather["ms"] = max_over_ranks(time.perf_counter() - tg) * 1e3
+            finally:
+                rg.close()
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             gather["error"] = repr(e)[:200]
 

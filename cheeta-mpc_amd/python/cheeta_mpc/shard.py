@@ -73,29 +73,51 @@ class ResultGather:
         self.buf = None
         self.dst = C.c_void_p()
         self.mapped = False
-        if dist.rank == 0:
+        if dist.world == 1:
             self.buf = cm.DeviceArray((max(self.total, 1),), "uint8")
             self.dst = self.buf.ptr
-        if dist.world > 1:
-            hb = None
+        else:
+            # every rank reaches each collective whatever fails locally (a rank that raised before a collective
+            # would leave the others blocked in it): errors travel with the handle exchange and are raised after it
+            hb, err = None, None
             if dist.rank == 0:
-                h = cm.IpcHandle()
-                cm._chk(cm.lib().cmpc_ipc_export(self.buf.ptr, C.byref(h)), "cmpc_ipc_export")
-                hb = bytes(h.bytes)
+                try:
+                    self.buf = cm.DeviceArray((max(self.total, 1),), "uint8")
+                    self.dst = self.buf.ptr
+                    h = cm.IpcHandle()
+                    cm._chk(cm.lib().cmpc_ipc_export(self.buf.ptr, C.byref(h)), "cmpc_ipc_export")
+                    hb = bytes(h.bytes)
+                except Exception as e:  # noqa: BLE001 - re-raised below, after the exchange
+                    err = e
             hb = dist.gather_object(hb)[0]
-            if dist.rank != 0:
-                h = cm.IpcHandle()
-                C.memmove(C.addressof(h), hb, len(hb))
-                cm._chk(cm.lib().cmpc_ipc_open(C.byref(h), C.byref(self.dst)), "cmpc_ipc_open")
-                self.mapped = True
+            if dist.rank != 0 and hb is None:
+                err = RuntimeError("rank 0 could not export its result buffer")
+            if dist.rank != 0 and err is None:
+                try:
+                    h = cm.IpcHandle()
+                    C.memmove(C.addressof(h), hb, len(hb))
+                    cm._chk(cm.lib().cmpc_ipc_open(C.byref(h), C.byref(self.dst)), "cmpc_ipc_open")
+                    self.mapped = True
+                except Exception as e:  # noqa: BLE001 - reported after the ranks agree
+                    err = e
+            # all ranks learn whether every rank is mapped; a failure anywhere fails the gather on every rank
+            if dist.max(0.0 if err is None else 1.0) > 0.0:
+                self.close()
+                raise err if err is not None else RuntimeError("result gather unavailable on another rank")
 
     def gather(self, src_ptr, offset_bytes, nbytes, stream=None):
         cm = self.cm
-        if offset_bytes < 0 or offset_bytes + nbytes > self.total:
-            raise ValueError("shard outside the gathered buffer")
-        cm._chk(cm.lib().cmpc_gather_shard(self.dst, int(offset_bytes), src_ptr, int(nbytes), stream), "cmpc_gather_shard")
-        cm._hchk(cm.hip().hipStreamSynchronize(stream), "hipStreamSynchronize")
-        self.dist.barrier()
+        err = None
+        try:
+            if offset_bytes < 0 or offset_bytes + nbytes > self.total:
+                raise ValueError("shard outside the gathered buffer")
+            cm._chk(cm.lib().cmpc_gather_shard(self.dst, int(offset_bytes), src_ptr, int(nbytes), stream),
+                    "cmpc_gather_shard")
+            cm._hchk(cm.hip().hipStreamSynchronize(stream), "hipStreamSynchronize")
+        except Exception as e:  # noqa: BLE001 - raised after the collective, so no rank is left waiting
+            err = e
+        if self.dist.max(0.0 if err is None else 1.0) > 0.0:  # the barrier, and every rank learns of a failure
+            raise err if err is not None else RuntimeError("result gather failed on another rank")
 
     def host(self, dtype, shape):
         """Rank 0: the gathered buffer as a host array."""

@@ -77,3 +77,47 @@ def test_two_rank_gloo_shards_match_single_process(tmp_path):
     ur, _, sr, _ = op.solve_batch(m, op.default_settings(), x0, xref, foot, contact, want_x=False)
     assert np.array_equal(st, sr)
     assert np.array_equal(u, ur)
+
+
+GATHER_FAIL_WORKER = r"""
+import os, sys, pickle
+sys.path[:0] = [os.path.join(ROOT, 'cheeta-mpc_amd', 'python')]
+from cheeta_mpc.shard import Dist, ResultGather
+import cheeta_mpc as cm
+d = Dist()
+if d.rank == 0:  # rank 0 cannot export its buffer (stands for a failed hipIpcGetMemHandle / allocation)
+    class _Fail:
+        def __init__(self, *a, **k):
+            raise RuntimeError("export failed on rank 0")
+    cm.DeviceArray = _Fail
+try:
+    ResultGather(d, 1024)
+    res = 'no error'
+except Exception as e:
+    res = type(e).__name__ + ': ' + str(e)
+d.barrier()  # the ranks' collectives are still matched after the failure
+t = d.max(1.0 + d.rank)
+with open(OUT + str(d.rank), 'wb') as f:
+    pickle.dump({'res': res, 't': t}, f)
+d.close()
+"""
+
+
+def test_result_gather_failure_is_symmetric(tmp_path):
+    """A rank that cannot set up the result gather (ResultGather, the xGMI / IPC gather of SURVEY §8e) makes every rank
+    raise after the handle exchange instead of leaving the other ranks blocked in a collective: both ranks report the
+    failure, and the barrier and the max-reduction that follow still match (no hang)."""
+    import pickle
+    out = tmp_path / "res"
+    script = tmp_path / "worker.py"
+    script.write_text(f"ROOT = {ROOT!r}\nOUT = {str(out)!r}\n" + GATHER_FAIL_WORKER)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    r0 = pickle.load(open(str(out) + "0", "rb"))
+    r1 = pickle.load(open(str(out) + "1", "rb"))
+    assert "export failed on rank 0" in r0["res"]
+    assert "rank 0 could not export" in r1["res"]
+    assert r0["t"] == r1["t"] == 2.0
