@@ -6,6 +6,7 @@ rank writes its shard into rank 0's buffer with one device-to-device copy (xGMI 
 mapping), so no collective and no reduction runs on the data path."""
 import ctypes as C
 import os
+import sys
 
 
 def shard_range(total, world, rank):
@@ -29,7 +30,18 @@ class Dist:
             import torch.distributed as d
             if not d.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-                d.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                # gloo prints "[Gloo] Rank r is connected to ..." on the process's stdout at rendezvous; bench.py's
+                # stdout must carry only its JSON line, so fd 1 points at stderr while the group forms
+                sys.stdout.flush()
+                saved = os.dup(1)
+                os.dup2(2, 1)
+                try:
+                    d.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                    d.barrier()  # every rank connected (and its message written) before stdout comes back
+                finally:
+                    sys.stdout.flush()
+                    os.dup2(saved, 1)
+                    os.close(saved)
             self._d, self._t = d, torch
 
     def barrier(self):

@@ -121,3 +121,29 @@ def test_result_gather_failure_is_symmetric(tmp_path):
     assert "export failed on rank 0" in r0["res"]
     assert "rank 0 could not export" in r1["res"]
     assert r0["t"] == r1["t"] == 2.0
+
+
+STDOUT_WORKER = r"""
+import os, sys
+sys.path[:0] = [os.path.join(ROOT, 'cheeta-mpc_amd', 'python')]
+from cheeta_mpc.shard import Dist
+d = Dist()
+d.barrier()
+if d.rank == 0:
+    print('{"value": 1}')
+d.close()
+"""
+
+
+def test_rank0_stdout_is_only_the_json_line(tmp_path):
+    """bench.py's contract: rank 0 prints one JSON line. gloo's rendezvous message ("[Gloo] Rank r is connected to
+    ...") is routed to stderr while the process group forms, so no rank's stdout carries anything else."""
+    script = tmp_path / "worker.py"
+    script.write_text(f"ROOT = {ROOT!r}\n" + STDOUT_WORKER)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    assert [p.returncode for p in procs] == [0, 0]
+    assert outs[0] == '{"value": 1}\n', outs[0]
+    assert outs[1] == "", outs[1]
