@@ -56,6 +56,11 @@ struct cmpc_ctx {
   int w128;       // waves per QP of the 64 < n <= 128 IPM class: 4, or 2 (fp32 only)
   bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;  // fused path without rollout: the IPM kernels scatter the results (no k_expand)
+  // fused path, forked: the bigger classes run on a side stream beside k_solve64, from class lists built off the
+  // contact tables (k_contact_lists) instead of k_solve64's appends; CMPC_FORK at cmpc_create
+  bool fork = false;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool items;  // fused path as IPM-iteration work items (k_solve64q), opt-in: CMPC_ITEMS=1 at cmpc_create (measured
                // 7-17 % slower than k_solve64 on the headline; DESIGN.md "work items")
   double* stats = nullptr;  // [max_batch][stats_rows][CMPC_STAT_COLS] (cmpc_enable_stats)
@@ -344,6 +349,35 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   ia.out_u = out_u;
   ia.out_status = out_status;
   ia.out_iters = out_iters;
+  if (c->fork && c->ld >= 128 && !c->items) {
+    // forked: side stream = class lists from the contact tables + the bigger classes; caller's stream = k_solve64
+    // (no appends); the caller's stream waits for the side stream at the end
+    IpmArgs<T> al = ia;
+    for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
+    al.qcount = c->qcount;
+    CondenseArgs<T> cb = ca;
+    if (hipEventRecord(c->ev_fork, st) != hipSuccess || hipStreamWaitEvent(c->side, c->ev_fork, 0) != hipSuccess)
+      return -2;
+    int r = launch_contact_lists(contact, c->model.N, B, c->nvar, c->qlist, c->qcount, c->side);
+    cb.n_lo = 64;
+    cb.qlist = c->qlist + (size_t)1 * B;
+    cb.qcount = c->qcount + 1;
+    if (r == 0) r = c->fused128 ? launch_solve128(al, cb, B, c->side) : launch_srbd_condense<T>(cb, 128, B, c->side);
+    if (r == 0 && !c->fused128) r = launch_ipm128_ctx(c, al, B, c->side);
+    if (r == 0 && c->ld > 128) {
+      cb.n_lo = 128;
+      cb.qlist = c->qlist + (size_t)2 * B;
+      cb.qcount = c->qcount + 2;
+      r = launch_srbd_condense<T>(cb, 256, B, c->side);
+      if (r == 0) r = launch_ipm256(al, B, c->side);
+    }
+    if (r != 0) return -2;
+    if (launch_solve64(ia, ca, B, st) != 0) return -2;  // app_list null: no appends
+    if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
+    if (hipEventRecord(c->ev_join, c->side) != hipSuccess || hipStreamWaitEvent(st, c->ev_join, 0) != hipSuccess)
+      return -2;
+    return 0;
+  }
   // the bigger classes' lists are appended by the fused kernel itself (no k_class_lists launch); the counters of
   // this call were zeroed by the previous fused call (or at cmpc_create), this call zeroes the next call's
   int* cnt = c->qcount + 3 + 3 * c->fused_parity;
@@ -506,6 +540,8 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     if (c->w128 == 2) c->fused128 = false;
     const char* di = std::getenv("CMPC_DIRECT");  // diagnostics: 0 = results through k_expand on the fused path
     c->direct = !(di && di[0] == '0');
+    const char* fk = std::getenv("CMPC_FORK");
+    c->fork = fk && fk[0] == '1';
   }
   (void)hipGetDevice(&c->device);
   c->num_cu = 0;
@@ -558,6 +594,16 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     delete c;
     return CMPC_ERR_HIP;
   }
+  if (c->fork) {  // the side stream at the highest priority, so its long bigger-class workgroups dispatch first
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      cmpc_destroy(c);
+      return CMPC_ERR_HIP;
+    }
+  }
   const int r = cmpc_set_model(c, model);
   if (r != CMPC_OK) {
     cmpc_destroy(c);
@@ -575,6 +621,9 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (c->stage) (void)hipFree(c->stage);
   if (c->pol) (void)hipFree(c->pol);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
   return CMPC_OK;
 }

@@ -190,6 +190,9 @@ int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, 
 // per-class QP lists: lists [3][B] (ascending QP ids), counts [3]; one workgroup. by_status != 0: QPs with
 // status == CMPC_SUCCESS, classed by nvar; by_status == 0: QPs with nvar > 0 (the condensing hints, written for every
 // QP by the first condensing kernel)
+// class lists 1 / 2 and their nvar hints from the contact tables alone (forked fused path, k_misc.hip)
+int launch_contact_lists(const uint8_t* contact, int N, int B, int* nvar, int* lists, int* counts,
+                         hipStream_t stream);
 int launch_class_lists(const int* status, const int* nvar, int B, int by_status, int* lists, int* counts,
                        hipStream_t stream);
 

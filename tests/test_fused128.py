@@ -37,3 +37,37 @@ def test_fused128_equals_two_launches(cm, monkeypatch, N, B, gait, prec, all_sta
     np.testing.assert_array_equal(st1, st0)
     np.testing.assert_array_equal(it1, it0)
     np.testing.assert_array_equal(u1, u0)
+
+
+@pytest.mark.parametrize("N,B,gait,prec,all_stance", [(10, 300, 1, "F64", False), (20, 96, 0, "F32", False),
+                                                      (12, 64, 1, "F64", False), (10, 4096, 0, "F64", False)])
+def test_forked_bigger_classes_equal_serial(cm, monkeypatch, N, B, gait, prec, all_stance):
+    """CMPC_FORK=1: the bigger classes run on a side stream beside k_solve64 from class lists built off the contact
+    tables; the same kernels solve the same QPs, so statuses, iteration counts and forces equal the serial path bit for
+    bit (mixed gait with rejected tables, N = 20 fp32, N = 12 with the 256 class, the headline batch)."""
+    p = getattr(cm, prec)
+    m = cm.default_model(N)
+    s = cm.default_settings() if p == cm.F64 else cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3, tol_comp=1e-4)
+    x0, xref, foot, contact = cm.generate_device(m, SEED, B, gait=gait)
+    ct = contact.host()
+    ct[1] = 0  # rejected tables: no stance leg at any step
+    ct[3, 2] = 0
+    contact = cm.DeviceArray.from_host(ct)
+    out = {}
+    for fork in ("0", "1"):
+        monkeypatch.setenv("CMPC_FORK", fork)
+        eng = cm.Engine(m, settings=s, precision=p, max_batch=B)
+        for rep in range(2):  # repeated calls reuse the lists and the side stream
+            u = cm.DeviceArray((B, N, 4, 3), np.float64)
+            st = cm.DeviceArray((B,), np.int32)
+            it = cm.DeviceArray((B,), np.int32)
+            eng.solve_device(B, x0, xref, foot, contact, u, None, st, it)
+            cm.hip().hipDeviceSynchronize()
+            out[(fork, rep)] = (u.host(), st.host(), it.host())
+    u0, st0, it0 = out[("0", 1)]
+    assert st0[1] == 5 and st0[3] == 5
+    for key in (("1", 0), ("1", 1), ("0", 0)):
+        u1, st1, it1 = out[key]
+        np.testing.assert_array_equal(st1, st0)
+        np.testing.assert_array_equal(it1, it0)
+        np.testing.assert_array_equal(u1, u0)
