@@ -311,7 +311,9 @@ int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const
 // first and its surplus workgroups exit at the end of the grid; without the lists a class's QPs sat between the
 // other classes' early-exit workgroups (mixed gait, config 5: IPM 2.31 -> 1.85-1.89 ms). Measured against running
 // the bigger classes concurrently on a forked side stream: +1.5 % on the mixed batch, -1.5..-2.5 % on the headline
-// (events and an empty launch on the critical path), so the classes run back to back.
+// (events and an empty launch on the critical path), so the classes run back to back. (The fused path's fork,
+// CMPC_FORK=1 in run_fused_t, builds its lists off the contact tables instead and starts beside k_solve64: config 5
+// +2 %, headline -2..3 %; opt-in.)
 // the 64 < n <= 128 IPM class on the context's wave count
 inline int launch_ipm128_ctx(const cmpc_ctx* c, const IpmArgs<double>& a, int B, hipStream_t st) {
   return launch_ipm128(a, B, st);
