@@ -16,6 +16,7 @@
 #include "cmpc/cmpc.h"
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
+#include "src_hash.h"
 
 using namespace cmpc;
 
@@ -44,25 +45,14 @@ struct cmpc_ctx {
   int* qlist;   // [3][max_batch] per-class QP lists (k_class_lists)
   int* qcount;  // [9]: k_class_lists' counts, then the fused path's two alternating append counters
   int fused_parity = 0;  // fused path: this call appends to qcount[3 + 3 parity] and zeroes the other slice
-  // cold-start cmpc_solve_batch runs the fused n <= 64 kernel (k_solve64) when N <= 21; CMPC_FUSED=0 in the
-  // environment at cmpc_create selects the separate condensing + IPM launches (A/B measurement)
-  bool fused;
+  // kernel path (cmpc_set_path; every choice gives bit-identical results):
+  bool fused;     // cold-start cmpc_solve_batch runs the fused n <= 64 kernel (k_solve64); possible when N <= 21
+  bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
+  bool direct;    // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   double *lin, *uj, *uq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
   double* res;
-  void* mig;
-  int num_cu;  // compute units of the device (work-item kernel: one workgroup per CU)
-  int w128;       // waves per QP of the 64 < n <= 128 IPM class: 4, or 2 (fp32 only)
-  bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
-  bool direct;  // fused path without rollout: the IPM kernels scatter the results (no k_expand)
-  // fused path, forked: the bigger classes run on a side stream beside k_solve64, from class lists built off the
-  // contact tables (k_contact_lists) instead of k_solve64's appends; CMPC_FORK at cmpc_create
-  bool fork = false;
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool items;  // fused path as IPM-iteration work items (k_solve64q), opt-in: CMPC_ITEMS=1 at cmpc_create (measured
-               // 7-17 % slower than k_solve64 on the headline; DESIGN.md "work items")
   double* stats = nullptr;  // [max_batch][stats_rows][CMPC_STAT_COLS] (cmpc_enable_stats)
   int stats_rows = 0;
   // host-API staging (grown on demand, outside the async path)
@@ -92,7 +82,7 @@ int ld_for(const cmpc_model& m) {
 
 struct Layout {
   size_t H, g, mu, lo, hi, u, map, nvar, status, iters, qlist, qcount, lin, uj, uq, stq, itq, done, sqpi, qpi, cnt, res_scr,
-      res, mig, total;
+      res, total;
 };
 
 Layout layout(int ld, int precision, int B) {
@@ -127,9 +117,8 @@ Layout layout(int ld, int precision, int B) {
   L.sqpi = take((size_t)B * sizeof(int));
   L.qpi = take((size_t)B * sizeof(int));
   L.cnt = take(sizeof(int));
-  L.res_scr = take((size_t)B * 3 * 256 * es);  // per-thread residual terms of the last IPM iteration
+  L.res_scr = take((size_t)B * 3 * 64 * es);   // per-lane residual terms of k_ipm64's last IPM iteration
   L.res = take((size_t)B * 4 * sizeof(double));  // final residuals (cmpc_get_residuals)
-  L.mig = take((size_t)B * 10 * 64 * es);         // parked IPM state of the work-item kernel (k_solve64q)
   L.total = o;
   return L;
 }
@@ -243,12 +232,6 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
   a.stamps = nullptr;
   a.res_scr = (T*)c->res_scr;
   a.res = c->res;
-  a.mig = (T*)c->mig;
-  {
-    const char* e = std::getenv("CMPC_ITEMS_PERIOD");  // diagnostics: iterations per work item
-    a.mig_period = e ? std::atoi(e) : 1;
-    if (a.mig_period < 1) a.mig_period = 1;
-  }
   a.stats = c->stats;
   a.stats_cap = c->stats_rows;
   for (int k = 0; k < 3; ++k) a.qlist[k] = nullptr;
@@ -311,16 +294,9 @@ int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const
 // first and its surplus workgroups exit at the end of the grid; without the lists a class's QPs sat between the
 // other classes' early-exit workgroups (mixed gait, config 5: IPM 2.31 -> 1.85-1.89 ms). Measured against running
 // the bigger classes concurrently on a forked side stream: +1.5 % on the mixed batch, -1.5..-2.5 % on the headline
-// (events and an empty launch on the critical path), so the classes run back to back. (The fused path's fork,
-// CMPC_FORK=1 in run_fused_t, builds its lists off the contact tables instead and starts beside k_solve64: config 5
-// +2 %, headline -2..3 %; opt-in.)
-// the 64 < n <= 128 IPM class on the context's wave count
-inline int launch_ipm128_ctx(const cmpc_ctx* c, const IpmArgs<double>& a, int B, hipStream_t st) {
-  return launch_ipm128(a, B, st);
-}
-inline int launch_ipm128_ctx(const cmpc_ctx* c, const IpmArgs<float>& a, int B, hipStream_t st) {
-  return c->w128 == 2 ? launch_ipm128w2(a, B, st) : launch_ipm128(a, B, st);
-}
+// (events and an empty launch on the critical path), so the classes run back to back. (A fork of the fused path that
+// built its lists off the contact tables and started beside k_solve64 measured config 5 +2 %, headline -2..3 %; it
+// was removed)
 
 template <typename T>
 int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, bool lists_ready) {
@@ -331,7 +307,7 @@ int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, boo
   for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
   al.qcount = c->qcount;
   int r = launch_ipm64(al, B, st);
-  if (r == 0) r = launch_ipm128_ctx(c, al, B, st);
+  if (r == 0) r = launch_ipm128(al, B, st);
   if (r == 0 && c->ld >= 256) r = launch_ipm256(al, B, st);
   return r;
 }
@@ -351,35 +327,6 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   ia.out_u = out_u;
   ia.out_status = out_status;
   ia.out_iters = out_iters;
-  if (c->fork && c->ld >= 128 && !c->items) {
-    // forked: side stream = class lists from the contact tables + the bigger classes; caller's stream = k_solve64
-    // (no appends); the caller's stream waits for the side stream at the end
-    IpmArgs<T> al = ia;
-    for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
-    al.qcount = c->qcount;
-    CondenseArgs<T> cb = ca;
-    if (hipEventRecord(c->ev_fork, st) != hipSuccess || hipStreamWaitEvent(c->side, c->ev_fork, 0) != hipSuccess)
-      return -2;
-    int r = launch_contact_lists(contact, c->model.N, B, c->nvar, c->qlist, c->qcount, c->side);
-    cb.n_lo = 64;
-    cb.qlist = c->qlist + (size_t)1 * B;
-    cb.qcount = c->qcount + 1;
-    if (r == 0) r = c->fused128 ? launch_solve128(al, cb, B, c->side) : launch_srbd_condense<T>(cb, 128, B, c->side);
-    if (r == 0 && !c->fused128) r = launch_ipm128_ctx(c, al, B, c->side);
-    if (r == 0 && c->ld > 128) {
-      cb.n_lo = 128;
-      cb.qlist = c->qlist + (size_t)2 * B;
-      cb.qcount = c->qcount + 2;
-      r = launch_srbd_condense<T>(cb, 256, B, c->side);
-      if (r == 0) r = launch_ipm256(al, B, c->side);
-    }
-    if (r != 0) return -2;
-    if (launch_solve64(ia, ca, B, st) != 0) return -2;  // app_list null: no appends
-    if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
-    if (hipEventRecord(c->ev_join, c->side) != hipSuccess || hipStreamWaitEvent(st, c->ev_join, 0) != hipSuccess)
-      return -2;
-    return 0;
-  }
   // the bigger classes' lists are appended by the fused kernel itself (no k_class_lists launch); the counters of
   // this call were zeroed by the previous fused call (or at cmpc_create), this call zeroes the next call's
   int* cnt = c->qcount + 3 + 3 * c->fused_parity;
@@ -389,14 +336,7 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
     ia.app_reset = c->qcount + 3 + 3 * (c->fused_parity ^ 1);
     ia.app_ld = B;
   }
-  if (c->items && c->settings.iter_max < 4000) {  // an item carries its iteration in 12 bits
-    // one 8-wave workgroup per CU, each owning qpw consecutive QPs (8 <= qpw <= 256)
-    int qpw = (B + c->num_cu - 1) / c->num_cu;
-    qpw = qpw < 8 ? 8 : (qpw > 256 ? 256 : qpw);
-    if (launch_solve64q(ia, ca, B, qpw, st) != 0) return -2;
-  } else if (launch_solve64(ia, ca, B, st) != 0) {
-    return -2;
-  }
+  if (launch_solve64(ia, ca, B, st) != 0) return -2;
   if (c->ld < 128) return 0;
   c->fused_parity ^= 1;
   if (ev1 && hipEventRecord(ev1, st) != hipSuccess) return -2;
@@ -410,7 +350,7 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   ca.qcount = cnt + 1;
   // 64 < n <= 128: condensing and IPM in one launch (k_solve128), or (CMPC_FUSED128=0) two
   int r = c->fused128 ? launch_solve128(al, ca, B, st) : launch_srbd_condense<T>(ca, 128, B, st);
-  if (r == 0 && !c->fused128) r = launch_ipm128_ctx(c, al, B, st);
+  if (r == 0 && !c->fused128) r = launch_ipm128(al, B, st);
   if (r == 0 && c->ld > 128) {
     ca.n_lo = 128;
     ca.qlist = c->qlist + (size_t)2 * B;
@@ -527,29 +467,13 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->precision = precision;
   c->max_batch = max_batch;
   c->ld = ld_for(*model);
-  {
-    const char* f = std::getenv("CMPC_FUSED");
-    c->fused = model->N <= CMPC_C64_MAXN && !(f && f[0] == '0');
-    const char* it = std::getenv("CMPC_ITEMS");
-    c->items = it && it[0] == '1';
-    // 128 class fused for fp32 only (config 3: 2.267 -> 2.243 ms); fp64 measured slower fused (config 5 class
-    // stage 1.615 -> 1.657 ms, all-stance 4.19 -> 4.29 ms). CMPC_FUSED128=0/1 overrides (diagnostics).
-    const char* f128 = std::getenv("CMPC_FUSED128");
-    c->fused128 = f128 ? f128[0] == '1' : precision == CMPC_F32;
-    // fp32 128 class on two waves per QP (CMPC_W128=2): separate condensing launch (the fused one runs on four)
-    const char* w128 = std::getenv("CMPC_W128");
-    c->w128 = (precision == CMPC_F32 && w128 && w128[0] == '2') ? 2 : 4;
-    if (c->w128 == 2) c->fused128 = false;
-    const char* di = std::getenv("CMPC_DIRECT");  // diagnostics: 0 = results through k_expand on the fused path
-    c->direct = !(di && di[0] == '0');
-    const char* fk = std::getenv("CMPC_FORK");
-    c->fork = fk && fk[0] == '1';
-  }
+  // default kernel path (cmpc_set_path): the fused n <= 64 kernel whenever it can serve the horizon; the fused 128
+  // class for fp32 only (config 3: 2.267 -> 2.243 ms; fp64 measured slower fused: config 5 class stage 1.615 ->
+  // 1.657 ms, all-stance 4.19 -> 4.29 ms); results scattered by the IPM kernels
+  c->fused = model->N <= CMPC_C64_MAXN;
+  c->fused128 = precision == CMPC_F32;
+  c->direct = true;
   (void)hipGetDevice(&c->device);
-  c->num_cu = 0;
-  if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
-      c->num_cu <= 0)
-    c->num_cu = 256;
   const Layout L = layout(c->ld, precision, max_batch);
   c->ws_bytes = L.total;
   if (dev_mem) {
@@ -583,7 +507,6 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->cnt = (int*)(c->ws + L.cnt);
   c->res_scr = c->ws + L.res_scr;
   c->res = (double*)(c->ws + L.res);
-  c->mig = c->ws + L.mig;
   c->qlist = (int*)(c->ws + L.qlist);
   c->qcount = (int*)(c->ws + L.qcount);
   if (hipMemset(c->qcount, 0, 9 * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
@@ -595,16 +518,6 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
     if (c->own_ws) (void)hipFree(c->ws);
     delete c;
     return CMPC_ERR_HIP;
-  }
-  if (c->fork) {  // the side stream at the highest priority, so its long bigger-class workgroups dispatch first
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
-      cmpc_destroy(c);
-      return CMPC_ERR_HIP;
-    }
   }
   const int r = cmpc_set_model(c, model);
   if (r != CMPC_OK) {
@@ -623,9 +536,6 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (c->stage) (void)hipFree(c->stage);
   if (c->pol) (void)hipFree(c->pol);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
   return CMPC_OK;
 }
@@ -653,6 +563,34 @@ int cmpc_get_model(const cmpc_ctx* c, cmpc_model* out) {
 
 int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
 int cmpc_ctx_fused(const cmpc_ctx* c) { return c && c->fused ? 1 : 0; }
+
+int cmpc_set_path(cmpc_ctx* c, int option, int value) {
+  if (!c || (value != 0 && value != 1)) return CMPC_ERR_ARG;
+  switch (option) {
+    case CMPC_PATH_FUSED64:
+      if (value && c->model.N > CMPC_C64_MAXN) return CMPC_ERR_ARG;  // the one-wave condensing holds N <= 21
+      c->fused = value != 0;
+      return CMPC_OK;
+    case CMPC_PATH_FUSED128:
+      c->fused128 = value != 0;
+      return CMPC_OK;
+    case CMPC_PATH_DIRECT:
+      c->direct = value != 0;
+      return CMPC_OK;
+    default:
+      return CMPC_ERR_ARG;
+  }
+}
+
+int cmpc_get_path(const cmpc_ctx* c, int option) {
+  if (!c) return CMPC_ERR_ARG;
+  switch (option) {
+    case CMPC_PATH_FUSED64: return c->fused ? 1 : 0;
+    case CMPC_PATH_FUSED128: return c->fused128 ? 1 : 0;
+    case CMPC_PATH_DIRECT: return c->direct ? 1 : 0;
+    default: return CMPC_ERR_ARG;
+  }
+}
 
 int cmpc_enable_stats(cmpc_ctx* c, int rows) {
   if (!c || rows < 0 || rows > 4096) return CMPC_ERR_ARG;
@@ -1262,6 +1200,8 @@ int cmpc_device_info(int* num_cu, int* clock_khz, char* arch, int arch_len) {
   return CMPC_OK;
 }
 
-const char* cmpc_version(void) { return "cheeta-mpc-amd 0.1.0 (gfx950)"; }
+// CMPC_SRC_HASH: sha256 prefix of every source, header and build file of libcmpc.so, written by the Makefile
+// (build/src_hash.h), so a bench line or test log names the exact source it ran
+const char* cmpc_version(void) { return "cheeta-mpc-amd 0.3.0 (gfx950) src " CMPC_SRC_HASH; }
 
 }  // extern "C"

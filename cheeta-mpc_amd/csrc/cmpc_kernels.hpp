@@ -66,12 +66,10 @@ struct IpmArgs {
   DevSettings s;
   unsigned long long* stamps;  // diagnostic builds only (-DCMPC_IPM_STAMPS): per-QP phase cycles, else null
   // final residuals (cmpc_get_residuals), or null: res[q][4] = (stat, eq = 0, ineq, comp) at the iterate where the
-  // IPM stopped; res_scr [B][3][256] holds each thread's last (stat, ineq, comp) terms until the exit reduction
+  // IPM stopped; res_scr [B][3][64] holds each lane's last (stat, ineq, comp) terms until the exit reduction
+  // (k_ipm64 only: the 128 / 256 classes reduce in LDS)
   T* res_scr;
   double* res;
-  // parked IPM state of the work-item kernel k_solve64q: [B][10][64] (u, H u, t_lo, t_hi, lam_lo, lam_hi)
-  T* mig;
-  int mig_period;  // k_solve64q: IPM iterations per work item (1)
   // per-iteration statistics (cmpc_enable_stats), or null: stats[q][it][CMPC_STAT_COLS] for it < stats_cap
   double* stats;
   int stats_cap;
@@ -87,7 +85,7 @@ struct IpmArgs {
   int* out_iters;
   const int* tri_map;
   int out_nu;
-  // fused path (k_solve64 / k_solve64q), or app_list = null: a QP of a bigger class is appended to its class list,
+  // fused path (k_solve64), or app_list = null: a QP of a bigger class is appended to its class list,
   // app_list[c * app_ld + atomicAdd(&app_count[c], 1)] = q (c = 1: n <= 128, 2: n <= 256; order not fixed, each QP's
   // result does not depend on it), and workgroup 0 zeroes app_reset[0..2] (the next call's counters)
   int* app_list;
@@ -115,12 +113,8 @@ int launch_solve64(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B,
 // fused workgroup condensing + IPM of the 64 < n <= 128 class over its class list (k_solve128, k_ipm128x.hpp)
 int launch_solve128(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream);
 int launch_solve128(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream);
-// work-item form (k_solve64q): one 8-wave workgroup per qpw consecutive QPs, IPM iterations as items (a.mig)
-int launch_solve64q(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, int qpw, hipStream_t stream);
-int launch_solve64q(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, int qpw, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
-int launch_ipm128w2(const IpmArgs<float>& a, int B, hipStream_t stream);  // the same on 2 waves per QP
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
 int launch_ipm256(const IpmArgs<float>& a, int B, hipStream_t stream);
 
@@ -190,9 +184,6 @@ int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, 
 // per-class QP lists: lists [3][B] (ascending QP ids), counts [3]; one workgroup. by_status != 0: QPs with
 // status == CMPC_SUCCESS, classed by nvar; by_status == 0: QPs with nvar > 0 (the condensing hints, written for every
 // QP by the first condensing kernel)
-// class lists 1 / 2 and their nvar hints from the contact tables alone (forked fused path, k_misc.hip)
-int launch_contact_lists(const uint8_t* contact, int N, int B, int* nvar, int* lists, int* counts,
-                         hipStream_t stream);
 int launch_class_lists(const int* status, const int* nvar, int B, int by_status, int* lists, int* counts,
                        hipStream_t stream);
 

@@ -82,7 +82,7 @@ struct C64Lds {
 // K = H in the 4 x 16-cyclic register tile of k_ipm64, g_out = g[lane], mu_out = the friction coefficient of the
 // lane's force triple. Returns n, or < 0 when the IPM has nothing to do here: -2 invalid contact table (status
 // written), -3 - n for n > 64 (left to the bigger classes with the nvar hint).
-template <typename T, bool MASK = false>
+template <typename T>
 __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int q, c64::C64Lds<T>& S, T (&K)[64],
                                              T& g_out, T& mu_out) {
   using namespace c64;
@@ -90,10 +90,7 @@ __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int
   using MF = Mf64<T>;
   using acc_t = typename MF::acc_t;
   const DevModel* __restrict__ M = a.model;
-  // one wave per QP; MASK (k_solve64q: eight waves per workgroup): the lane is read opaquely so that lane-derived
-  // values are computed per QP, not hoisted out of the enclosing work-item loop
-  int lane = MASK ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
-  if constexpr (MASK) asm volatile("" : "+v"(lane));
+  const int lane = (int)threadIdx.x;  // one wave per QP
   const int g4 = lane >> 4, col = lane & 15;
   const int N = M->N;
   constexpr int L = NL;

@@ -9,12 +9,6 @@ int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// two waves per QP (each wave owns every other row group: 128 tile registers per lane, 2 waves per SIMD)
-int launch_ipm128w2(const IpmArgs<float>& a, int B, hipStream_t stream) {
-  hipLaunchKernelGGL((k_ipm128x<float, 2, 2>), dim3(B), dim3(128), 0, stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
 int launch_solve128(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   if (!a.qlist[1] || !a.qcount || a.ld < 128) return -1;  // list-driven only

@@ -130,10 +130,8 @@ __device__ __forceinline__ void sfor_down(F&& f) {  // E-1 down to B
 // Compiler-only ordering of LDS accesses: one wave's DS instructions execute in order, so a read issued after a
 // write (or a write after a read) in program order sees the right data without s_waitcnt.
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
-// MASK: the wave's lane inside a multi-wave workgroup (k_solve64q); the one-wave kernels take threadIdx.x as is
-template <bool MASK = false>
 __device__ __forceinline__ int olane() {
-  int l = MASK ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
+  int l = (int)threadIdx.x;
   asm volatile("" : "+v"(l));
   return l;
 }
@@ -181,45 +179,39 @@ struct IpmShared<T, true> {
 // Body of one QP on one wavefront. MODE 0 (k_ipm64): everything is read from the workspace a separate condensing
 // launch filled. MODE 1 (k_solve64): the QP is condensed first by the same wave (condense64_qp, which also writes H
 // and the QP data to the workspace for the later iterations and the other stages) and the first Newton matrix starts
-// from the H the condensing leaves in registers. MODE 2 (k_solve64q, one work item): as MODE 1 when it0 == 0 (the
-// item condenses the QP), else the QP resumes at iteration it0 from the state an earlier item parked in A.mig; the
-// item runs ONE iteration and parks the state again. Returns the next iteration to run (MODE 2) or -1 when the QP
-// is finished (or not of this class).
+// from the H the condensing leaves in registers. (An iteration-work-item form, k_solve64q, measured 7-17 % slower
+// and was moved out of the library)
 template <typename T, int WPE, int MODE>
-__device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArgs<T>* C,
-                                          IpmShared<T, (MODE > 0)>* SHp, int q, int it0, int n_in = 0) {
-  // one-wave kernels: the LDS block is declared here, so its accesses keep a constant base (as a reference from the
-  // kernel, ds_write2 / ds_read2 pairing is lost: +640 instructions, +3 % time); item mode: the wave's block
-  // (item mode: the wave's block of the kernel's array; the pairing is lost there either way, by the wave's base)
-  __shared__ IpmShared<T, (MODE > 0)> SHl;
-  IpmShared<T, (MODE > 0)>& SH = MODE == 2 ? *SHp : SHl;
+__device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseArgs<T>* C, int q) {
+  // the LDS block is declared here, so its accesses keep a constant base (as a reference from the kernel,
+  // ds_write2 / ds_read2 pairing is lost: +640 instructions, +3 % time)
+  __shared__ IpmShared<T, (MODE > 0)> SH;
   constexpr bool FUSED = MODE > 0;
   using namespace ipm64;
   IPM_STAMP_DECL;
-  const bool fresh = MODE < 2 || it0 == 0;
   Lds<T>& L = SH.ipm;
   T K[64];
   T g_v, mu_v;
   T lo[2], hi[2], muc[2];
   int n;
   if constexpr (FUSED) {
-    if (fresh) {
-      n = condense64_qp<T, MODE == 2>(*C, q, SH.cond, K, g_v, mu_v);
+    {
+      n = condense64_qp<T>(*C, q, SH.cond, K, g_v, mu_v);
       if (n < 0) {  // invalid contact table (status written) or a bigger class (nvar hint written)
         if (n == -2 && A.out_u)  // the rejected QP's result: zeros, INVALID_CONTACT, no iterations
-          scatter_result<T>(A, q, 0, T(0), CMPC_INVALID_CONTACT, 0, SH.ipm.scr, olane<MODE == 2>(), 64,
+          scatter_result<T>(A, q, 0, T(0), CMPC_INVALID_CONTACT, 0, SH.ipm.scr, olane(), 64,
                             [] { ipm64::cbar(); });
-        if (n <= -3 && A.app_list && olane<MODE == 2>() == 0) {  // append to the bigger class's list
+        if (n <= -3 && A.app_list && olane() == 0) {  // append to the bigger class's list
           const int cls = -3 - n <= 128 ? 1 : 2;
           const int pos = atomicAdd(&A.app_count[cls], 1);
           A.app_list[(size_t)cls * A.app_ld + pos] = q;
         }
-        return -1;
+        return;
       }
       // pyramid rows j = lane + 64 cc: the bounds and friction coefficients the condensing just wrote to the
       // workspace, taken from the model and its triple table in LDS before the IPM reuses those bytes
       const DevModel* M = C->model;
-      const int lane_ = MODE == 2 ? ipm64::olane<true>() : (int)threadIdx.x;
+      const int lane_ = (int)threadIdx.x;
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
         const int j = lane_ + 64 * cc;
@@ -231,31 +223,23 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    } else {
-      // resumed item: n travels with the item. (Reading nvar[q] here would be a uniform load, i.e. a scalar-cache
-      // load, and the scalar cache does not see the vector store of another wave of this launch.)
-      n = n_in;
     }
   } else {
-    if (A.status[q] != CMPC_SUCCESS) return -1;  // invalid contact table / too large: status already set
+    if (A.status[q] != CMPC_SUCCESS) return;  // invalid contact table / too large: status already set
     n = A.nvar[q];
-    if (n > 64) return -1;  // served by the 128 class
+    if (n > 64) return;  // served by the 128 class
   }
   const int ld = A.ld;
   const int nt = n / 3;
   const int m = 5 * nt;
   const DevSettings S = A.s;
-  int lane = MODE == 2 ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;  // re-read opaquely at every iteration
-  // plain lane id: lane masks only (hoisted into SGPR pairs); in item mode read opaquely per item, so that the masks
-  // are not hoisted out of the scheduler's loop (they would stay live across it and spill)
-  const int lane0 = MODE == 2 ? ipm64::olane<true>() : (int)threadIdx.x;
+  int lane = (int)threadIdx.x;  // re-read opaquely at every iteration
+  const int lane0 = (int)threadIdx.x;  // plain lane id: lane masks only (hoisted into SGPR pairs)
 
   // ---- lane-per-variable data
   const bool vin = lane < n;
-  // item mode: data another wave of this workgroup wrote is visible after the ring's workgroup-scope acquire (one
-  // CU, one vector L1, no threadgroup split), so plain loads serve; nontemporal loads here cost 36 VGPR spills
   auto ldx = [&](const T* p) -> T { return *p; };
-  if (!(FUSED && fresh)) {
+  if (!FUSED) {
     g_v = vin ? ldx(A.g + (size_t)q * ld + lane) : T(0);
     mu_v = vin ? ldx(A.tri_mu + (size_t)q * (ld / 3) + lane / 3) : T(0);
   }
@@ -270,7 +254,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     const int j = lane + 64 * cc;
     const bool on = j < m;
     const int t = j / 5;
-    if (!(FUSED && fresh)) {
+    if (!FUSED) {
       lo[cc] = on ? ldx(A.tri_lo + ((size_t)q * (ld / 3) + t) * 5 + j % 5) : T(0);
       hi[cc] = on ? ldx(A.tri_hi + ((size_t)q * (ld / 3) + t) * 5 + j % 5) : T(0);
       muc[cc] = on ? ldx(A.tri_mu + (size_t)q * (ld / 3) + t) : T(0);
@@ -313,20 +297,6 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   T invd_v = T(1);
   T hu_v = T(0), rhs_v = T(0);
   T rg_v = T(0), du_v = T(0);
-  // parked state of a resumed item (MODE 2): [u, H u, t_lo, t_hi, lam_lo, lam_hi (2 slots each)] x 64 lanes
-  auto mig_at = [&]() { return A.mig + (size_t)q * 10 * 64 + olane<MODE == 2>(); };  // recomputed where used (no live VGPR pair)
-  if (MODE == 2 && !fresh) {
-    const T* mig = mig_at();
-    u_v = ldx(mig);
-    hu_v = ldx(mig + 64);
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      tl[cc] = ldx(mig + (2 + cc) * 64);
-      tu[cc] = ldx(mig + (4 + cc) * 64);
-      ll[cc] = ldx(mig + (6 + cc) * 64);
-      lu[cc] = ldx(mig + (8 + cc) * 64);
-    }
-  }
   T dtl[2], dtu[2], dll[2], dlu[2];
 
   // Solve K x = y with the eliminated tile (see the factorisation): strictly lower part S (X = L^-1 with
@@ -335,7 +305,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   //   forward  t = D^-1 y;  z = D^-1 (y - S t)            row sums: 16 partials per lane, reduced through LDS
   //   backward x = z - D^-1 (S' z)                         column sums: 4 partials per lane, reduced through LDS
   auto solve = [&](T& y) {
-    const int ol = olane<MODE == 2>();
+    const int ol = olane();
     const int ola = ol >> 4, olb = ol & 15;
     L.v[ol] = y * invd_v;
     cbar();
@@ -389,7 +359,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   const T* Hq = A.H + (size_t)q * ld * ld;
   // H in tile order (64 coalesced 512-B rows) into the registers of the factor
   auto load_H = [&]() {
-    const int ln = olane<MODE == 2>();
+    const int ln = olane();
 #pragma unroll
     for (int e = 0; e < 64; ++e) K[e] = Hq[e * 64 + ln];
   };
@@ -443,12 +413,11 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
 
   int status = CMPC_MAX_ITER;
   int it = 0;
-  for (it = (MODE == 2 ? it0 : 0);; ++it) {
-    if constexpr (MODE < 2) progress_prio(it);  // cmpc_device.hpp (item mode: items, not waves, balance the SIMD)
-    if (!(FUSED && fresh && it == 0)) {
+  for (it = 0;; ++it) {
+    progress_prio(it);  // cmpc_device.hpp
+    if (!(FUSED && it == 0)) {
       // fused: iteration 0 starts from the condensing's registers; the rows it stored are re-read from iteration 1
-      // on by the same lanes (the wait drains the stores before the first re-read; in item mode the hand-off's
-      // release fence does)
+      // on by the same lanes (the wait drains the stores before the first re-read)
       if (MODE == 1 && it == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       load_H();  // consumed first by Hu below: the pyramid residuals run while the 64 rows are in flight
     }
@@ -457,7 +426,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     IPM_STAMP(3);
 #endif
-    lane = olane<MODE == 2>();
+    lane = olane();
     const int la = lane >> 4, lb = lane & 15;
 
     // ---- residuals that do not need H: C u, slack/complementarity residuals, C' lam
@@ -513,10 +482,10 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     rg_v = vin ? hu + g_v - ctw : T(0);
     rs = fabs(rg_v);
     if (A.res_scr) {  // this iteration's residual terms, reduced once at the exit
-      T* rp = A.res_scr + (size_t)q * 3 * 256 + lane;
+      T* rp = A.res_scr + (size_t)q * 3 * 64 + lane;
       rp[0] = rs;
-      rp[256] = ri;
-      rp[512] = rc;
+      rp[64] = ri;
+      rp[128] = rc;
     }
     ms = wave_sum_dpp(ms);
     const T mu = m > 0 ? ms / T(2 * m) : T(0);
@@ -771,7 +740,7 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     u_v = fma(alpha, du_v, u_v);
     // H du = K du - (C' Sigma C + reg I) du = rhs - D du (D: the 3x3 blocks of this iteration, du still in L.v)
     {
-      const int ln = olane<MODE == 2>();
+      const int ln = olane();
       const int t3 = 3 * (ln / 3), e = ln - t3;
       T ddu = T(0);
       if (vin) {
@@ -788,22 +757,9 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
       lu[cc] = fma(alpha, dlu[cc], lu[cc]);
     }
     IPM_STAMP(7);
-    if (MODE == 2 && it + 1 - it0 >= A.mig_period) {  // park the state; the next iteration is a new work item
-      T* mig = mig_at();
-      mig[0] = u_v;
-      mig[64] = hu_v;
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        mig[(2 + cc) * 64] = tl[cc];
-        mig[(4 + cc) * 64] = tu[cc];
-        mig[(6 + cc) * 64] = ll[cc];
-        mig[(8 + cc) * 64] = lu[cc];
-      }
-      return (it + 1) | (n << 16);  // next iteration and the QP's size (k_solve64q item)
-    }
   }
 
-  lane = olane<MODE == 2>();
+  lane = olane();
   const bool fin = isfinite(u_v);
   if (lane < ld) A.u[(size_t)q * ld + lane] = vin ? u_v : T(0);
   if (uflag(__any(!fin))) status = CMPC_NAN_SOL;
@@ -813,8 +769,8 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
   }
   if (A.out_u) scatter_result<T>(A, q, n, u_v, status, it, L.scr, lane, 64, [] { cbar(); });
   if (A.res) {  // max over the lanes of the last residual terms (the same lanes stored them)
-    const T* rp = A.res_scr + (size_t)q * 3 * 256 + lane;
-    const T r0 = wave_max_dpp(rp[0]), r1 = wave_max_dpp(rp[256]), r2 = wave_max_dpp(rp[512]);
+    const T* rp = A.res_scr + (size_t)q * 3 * 64 + lane;
+    const T r0 = wave_max_dpp(rp[0]), r1 = wave_max_dpp(rp[64]), r2 = wave_max_dpp(rp[128]);
     if (lane == 0) {
       double* o = A.res + (size_t)q * 4;
       o[0] = (double)r0;
@@ -824,7 +780,6 @@ __device__ __forceinline__ int ipm64_body(const IpmArgs<T>& A, const CondenseArg
     }
   }
   IPM_STAMP_STORE(A.stamps, q);
-  return -1;
 }
 
 template <typename T, int WPE>
@@ -835,7 +790,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
     q = A.qlist[0][q];
     if ((unsigned)q >= gridDim.x) return;  // grid = batch: a corrupt list entry cannot address past it
   }
-  (void)ipm64_body<T, WPE, 0>(A, nullptr, nullptr, q, 0);
+  ipm64_body<T, WPE, 0>(A, nullptr, q);
 }
 
 // Fused stage 1 + stage 2 for the n <= 64 class (cmpc_solve_batch, cold start): one launch condenses and solves
@@ -844,103 +799,7 @@ __global__ __launch_bounds__(64, WPE) void k_ipm64(IpmArgs<T> A) {
 template <typename T, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_solve64(IpmArgs<T> A, CondenseArgs<T> C) {
   if (A.app_reset && blockIdx.x == 0 && threadIdx.x < 3) A.app_reset[threadIdx.x] = 0;  // next call's counters
-  (void)ipm64_body<T, WPE, 1>(A, &C, nullptr, (int)blockIdx.x, 0);
-}
-
-// Work-item form of k_solve64 (cmpc_solve_batch, cold start, n <= 64 class): one workgroup of 8 waves per CU owns
-// qpw consecutive QPs and hands their IPM iterations to its waves one at a time from a FIFO in LDS; a wave runs one
-// iteration of one QP (the first item of a QP also condenses it), parks the QP's state in A.mig (≈ 5 KB) and takes
-// the next item. Why: with one QP per wave, the batch runs in rounds of whole QPs and the two waves of a SIMD finish
-// theirs at different times (the older wave wins arbitration; lab timeline: 145 vs 190-230 us), so a 4096-QP launch
-// ends with one wave per SIMD for ~60 us; with iteration items every wave stays busy until the last few items.
-// The hand-off stays inside the CU: state stores, a workgroup-scope release, the FIFO entry (LDS); the consumer's
-// workgroup-scope acquire, then the loads (HIP's workgroup scope: every wave of the workgroup is on this CU).
-// FIFO: ring of R = qpw + 8 entries {sequence (position + 1), item (QP index | iteration << 16)}; a wave reserves
-// a position with an LDS atomic and waits for that position's sequence; pushes go to the tail position. At most qpw
-// items are queued and at most 8 positions are reserved and unread, so R never wraps onto an unread entry. Waves
-// leave when every QP of the workgroup is finished; waits are bounded (no hang if an item is ever lost).
-constexpr int kSolve64qMaxQpw = 256;
-template <typename T>
-__global__ __launch_bounds__(512, 1) void k_solve64q(IpmArgs<T> A, CondenseArgs<T> C, int B, int qpw,
-                                                      unsigned spin_max) {
-  __shared__ unsigned long long ring[kSolve64qMaxQpw + 8];
-  __shared__ int qhead, qtail, qdone;
-  __shared__ IpmShared<T, true> SH[8];
-  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
-  const int q0 = (int)blockIdx.x * qpw;
-  const int qn = min(qpw, B - q0);
-  if (A.app_reset && blockIdx.x == 0 && threadIdx.x < 3) A.app_reset[threadIdx.x] = 0;  // next call's counters
-  if (qn <= 0) return;
-  const unsigned R = (unsigned)qpw + 8u;
-  // every entry is written: positions < qn hold the fresh QPs (iteration 0), the rest sequence 0, which no position
-  // waits for (LDS keeps the previous launch's FIFO, whose sequences would otherwise match)
-  for (int p = (int)threadIdx.x; p < (int)R; p += (int)blockDim.x)
-    ring[p] = p < qn ? (((unsigned long long)(p + 1) << 32) | (unsigned)p) : 0ull;
-  if (threadIdx.x == 0) {
-    qhead = 0;
-    qtail = qn;
-    qdone = 0;
-  }
-  __syncthreads();
-  // FIFO words are read and written by LDS atomics (ds_*: the shared arrays keep their address space); every
-  // decision is taken on wave-uniform values (readfirstlane), so the waits are scalar loops
-  auto ld_entry = [&](unsigned slot) -> unsigned long long {
-    return __hip_atomic_load(&ring[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  // every wave handles at most qn * (iter_max + 1) items (a guard: the FIFO never holds more)
-  const int item_max = qn * (A.s.iter_max + 1);
-  for (int items = 0; items < item_max; ++items) {
-    int pos = 0;
-    if (lane == 0) pos = atomicAdd(&qhead, 1);
-    pos = __builtin_amdgcn_readfirstlane(pos);
-    const unsigned slot = (unsigned)pos % R;
-    unsigned item = 0;
-    bool got = false;
-    for (unsigned spins = 0; spins < spin_max; ++spins) {
-      const unsigned long long e = ld_entry(slot);
-      const unsigned seq = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(e >> 32));
-      if (seq == (unsigned)(pos + 1)) {
-        item = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)e);
-        got = true;
-        break;
-      }
-      const int d = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&qdone, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_WORKGROUP));
-      if (d >= qn) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (!got) {
-#ifdef CMPC_ITEMS_DEBUG
-      if (lane == 0 && qdone < qn) printf("k_solve64q wg %d wave %d: gave up at pos %d (head %d tail %d done %d/%d)\n",
-                                          (int)blockIdx.x, w, pos, qhead, qtail, qdone, qn);
-#endif
-      break;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // item: QP index (8 bits) | iteration (12 bits) << 8 | n (7 bits) << 20
-    const int ql = (int)(item & 0xffu), it = (int)((item >> 8) & 0xfffu), n_item = (int)(item >> 20);
-    if (ql >= qn || n_item > 64) break;  // not an item of this launch (cannot happen; never touch memory for it)
-    // the item's result is wave-uniform by construction; readfirstlane makes that explicit to the compiler (the
-    // scheduler's branches then stay scalar), and a result outside [1, iter_max + 1] ends the QP
-    const int r = __builtin_amdgcn_readfirstlane(ipm64_body<T, 2, 2>(A, &C, &SH[w], q0 + ql, it, n_item));
-    int next = r < 0 ? -1 : (r & 0xffff);
-    const int n_next = r < 0 ? 0 : (r >> 16);
-    if (next <= it || next > A.s.iter_max + 1 || next > 0xfff) next = -1;
-    if (next < 0) {
-      if (lane == 0) atomicAdd(&qdone, 1);
-    } else {
-      // the parked state (and H, g, the pyramid data of a first item) must be written before the FIFO entry: the
-      // workgroup-scope release alone lowers to an LDS wait only (no vmcnt) on gfx950, hence the explicit drain
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) {
-        const int p = atomicAdd(&qtail, 1);
-        __hip_atomic_store(&ring[(unsigned)p % R],
-                           ((unsigned long long)(p + 1) << 32) | (unsigned)(ql | (next << 8) | (n_next << 20)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-  }
+  ipm64_body<T, WPE, 1>(A, &C, (int)blockIdx.x);
 }
 
 }  // namespace cmpc

@@ -265,68 +265,6 @@ int launch_class_lists(const int* status, const int* nvar, int B, int by_status,
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// Class lists straight from the contact tables (forked fused path): n = 3 * (#stance leg-steps) of each QP with a
-// valid table (every step has a stance leg; the fused n <= 64 kernel reports the others), QPs with 64 < n <= 128 into
-// list 1 and 128 < n <= 256 into list 2 in ascending order, and their nvar hint for the bigger classes' condensing. It
-// runs beside the fused kernel, which writes the same nvar for these QPs and nothing else they read.
-__global__ __launch_bounds__(1024) void k_contact_lists(const uint8_t* contact, int N, int B, int* nvar, int* lists,
-                                                        int* counts) {
-  __shared__ int s_wtot[3][16];
-  __shared__ int s_base[3];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid < 3) s_base[tid] = 0;
-  __syncthreads();
-  for (int q0 = 0; q0 < B; q0 += 1024) {
-    const int q = q0 + tid;
-    int cls = -1;
-    if (q < B) {
-      const uint8_t* ct = contact + (size_t)q * N * NL;
-      int ns = 0;
-      bool valid = true;
-      for (int k = 0; k < N; ++k) {
-        int sk = 0;
-        for (int i = 0; i < NL; ++i) sk += ct[k * NL + i] ? 1 : 0;
-        valid = valid && sk > 0;
-        ns += sk;
-      }
-      const int n = 3 * ns;
-      if (valid && n > 64 && n <= 256) {
-        cls = n <= 128 ? 1 : 2;
-        nvar[q] = n;
-      }
-    }
-    int pre = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int c = 1; c < 3; ++c) {
-      const unsigned long long mask = __ballot(cls == c);
-      if (cls == c) pre = __popcll(mask & below);
-      if (lane == 0) s_wtot[c][w] = __popcll(mask);
-    }
-    __syncthreads();
-    if (cls >= 1) {
-      int off = s_base[cls];
-      for (int v = 0; v < w; ++v) off += s_wtot[cls][v];
-      lists[(size_t)cls * B + off + pre] = q;
-    }
-    __syncthreads();
-    if (tid >= 1 && tid < 3) {
-      int t = 0;
-      for (int v = 0; v < 16; ++v) t += s_wtot[tid][v];
-      s_base[tid] += t;
-    }
-    __syncthreads();
-  }
-  if (tid < 3) counts[tid] = tid == 0 ? 0 : s_base[tid];
-}
-
-int launch_contact_lists(const uint8_t* contact, int N, int B, int* nvar, int* lists, int* counts,
-                         hipStream_t stream) {
-  if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_contact_lists, dim3(1), dim3(1024), 0, stream, contact, N, B, nvar, lists, counts);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
 // ------------------------------------------------------------------------------------------ solver statistics
 // cmpc_get_residuals: the IPM kernels' final residuals, NaN for QPs they did not run (status 5 / 6 or unset)
 __global__ void k_residuals(const double* res, const int* status, int B, double* out) {

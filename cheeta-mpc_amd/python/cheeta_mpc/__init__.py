@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("CMPC_LIB") or os.path.join(PKG_ROOT, "lib", "libcmpc.
 
 NX, NU, NL = 13, 12, 4
 F64, F32 = 0, 1
+# kernel-path options of a context (cmpc_set_path; bit-identical results for every choice)
+PATH_FUSED64, PATH_FUSED128, PATH_DIRECT = 0, 1, 2
 STATUS = {0: "SUCCESS", 1: "MAX_ITER", 2: "MIN_STEP", 3: "NAN_SOL", 4: "INCONS_EQ", 5: "INVALID_CONTACT",
           6: "TOO_LARGE"}
 
@@ -81,6 +83,8 @@ def lib():
     L.cmpc_get_model.argtypes = [vp, P(Model)]
     L.cmpc_ctx_ld.argtypes = [vp]
     L.cmpc_ctx_fused.argtypes = [vp]
+    L.cmpc_set_path.argtypes = [vp, C.c_int, C.c_int]
+    L.cmpc_get_path.argtypes = [vp, C.c_int]
     L.cmpc_get_residuals.argtypes = [vp, C.c_int, d, vp]
     L.cmpc_enable_stats.argtypes = [vp, C.c_int]
     L.cmpc_get_stats.argtypes = [vp, C.c_int, d, vp]
@@ -217,7 +221,8 @@ def default_settings(**kw):
 class Engine:
     """One cmpc context (device workspace for max_batch QPs of horizon model.N)."""
 
-    def __init__(self, model, settings=None, precision=F64, max_batch=4096):
+    def __init__(self, model, settings=None, precision=F64, max_batch=4096, path=None):
+        """path: {PATH_* option: 0 / 1} applied with cmpc_set_path after creation (A/B tests; default path if None)."""
         self.model = model
         self.settings = settings or default_settings()
         self.precision = precision
@@ -226,6 +231,14 @@ class Engine:
         _chk(lib().cmpc_create(C.byref(model), C.byref(self.settings), precision, max_batch, None,
                                C.byref(self.ctx)), "cmpc_create")
         self.ld = lib().cmpc_ctx_ld(self.ctx)
+        for k, v in (path or {}).items():
+            self.set_path(k, v)
+
+    def set_path(self, option, value):
+        _chk(lib().cmpc_set_path(self.ctx, option, int(value)), "cmpc_set_path")
+
+    def get_path(self, option):
+        return lib().cmpc_get_path(self.ctx, option)
 
     def close(self):
         if self.ctx:

@@ -131,9 +131,21 @@ int cmpc_set_model(cmpc_ctx* ctx, const cmpc_model* model); /* horizon N must no
 int cmpc_get_model(const cmpc_ctx* ctx, cmpc_model* out);
 /* Leading dimension (padded max condensed size) of the context's H workspace. */
 int cmpc_ctx_ld(const cmpc_ctx* ctx);
-/* 1 when a cold-start cmpc_solve_batch runs the fused condensing + IPM kernel for the n <= 64 class (N <= 21; the
- * environment variable CMPC_FUSED=0 at cmpc_create selects the two separate launches instead), else 0. */
+/* 1 when a cold-start cmpc_solve_batch runs the fused condensing + IPM kernel for the n <= 64 class, else 0
+ * (= cmpc_get_path(ctx, CMPC_PATH_FUSED64)). */
 int cmpc_ctx_fused(const cmpc_ctx* ctx);
+/* Kernel path of a context, for A/B measurement and tests; every choice gives bit-identical results:
+ *   CMPC_PATH_FUSED64   1 (default when N <= 21): cold-start solves condense and solve the n <= 64 class in one
+ *                       launch; 0: a condensing launch, then the IPM launch. 1 is CMPC_ERR_ARG when N > 21.
+ *   CMPC_PATH_FUSED128  1: the 64 < n <= 128 class condensed and solved in one launch on the fused path (default for
+ *                       fp32 contexts); 0: two launches (default for fp64, where the fused form measured slower).
+ *   CMPC_PATH_DIRECT    1 (default): on the fused path without a rollout the IPM kernels write u / status / iters;
+ *                       0: through the scatter kernel.
+ * cmpc_set_path returns CMPC_ERR_ARG for an unknown option or a value other than 0 / 1; cmpc_get_path returns the
+ * current value or CMPC_ERR_ARG. */
+enum cmpc_path_option { CMPC_PATH_FUSED64 = 0, CMPC_PATH_FUSED128 = 1, CMPC_PATH_DIRECT = 2 };
+int cmpc_set_path(cmpc_ctx* ctx, int option, int value);
+int cmpc_get_path(const cmpc_ctx* ctx, int option);
 
 /* Full hot path: SRBD linearisation -> condensing (H, g) -> friction/force-bound stacking -> batched IPM ->
  * scatter to [N][L][3] (zeros for swing legs) and optional rollout. Device pointers, async on stream.
@@ -319,7 +331,7 @@ const char* cmpc_status_string(int status);
 const char* cmpc_error_string(int err);
 /* Device properties used by the bench roofline (peak fp64 FLOP/s from the datasheet unless measured). */
 int cmpc_device_info(int* num_cu, int* clock_khz, char* arch_name, int arch_len);
-/* Version string of the build. */
+/* Version string of the build, ending in the sha256 prefix of the library's sources ("... src <16 hex>"). */
 const char* cmpc_version(void);
 
 #ifdef __cplusplus

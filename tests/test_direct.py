@@ -1,6 +1,6 @@
 """Result scatter in the IPM kernels' epilogues (fused cold-start path without rollout: k_solve64, k_ipm128x and
 k_ipm_tiled write u[N][4][3], status and iterations themselves; no k_expand launch) against the k_expand path
-(CMPC_DIRECT=0 at cmpc_create): identical outputs, bit for bit, on batches that reach every size class (N = 10 and
+(cmpc_set_path(CMPC_PATH_DIRECT, 0)): identical outputs, bit for bit, on batches that reach every size class (N = 10 and
 N = 20 mixed gaits: n <= 64, 64 < n <= 128, 128 < n <= 256) and carry rejected QPs (a step without a stance leg:
 INVALID_CONTACT, zero forces, zero iterations)."""
 import numpy as np
@@ -11,10 +11,9 @@ pytestmark = pytest.mark.gpu
 SEED = 20221125
 
 
-def _solve(cm, N, B, gait, monkeypatch, direct, invalid=()):
-    monkeypatch.setenv("CMPC_DIRECT", "1" if direct else "0")
+def _solve(cm, N, B, gait, direct, invalid=()):
     m = cm.default_model(N)
-    eng = cm.Engine(m, precision=cm.F64, max_batch=B)
+    eng = cm.Engine(m, precision=cm.F64, max_batch=B, path={cm.PATH_DIRECT: direct})
     x0, xref, foot, contact = cm.generate_device(m, SEED, B, gait=gait)
     if invalid:
         c = contact.host()
@@ -31,10 +30,10 @@ def _solve(cm, N, B, gait, monkeypatch, direct, invalid=()):
 
 
 @pytest.mark.parametrize("N,B,gait", [(10, 300, 1), (20, 96, 1), (10, 64, 0)])
-def test_direct_results_equal_expand_path(cm, monkeypatch, N, B, gait):
+def test_direct_results_equal_expand_path(cm, N, B, gait):
     bad = (3, 17, B - 1)
-    u0, st0, it0 = _solve(cm, N, B, gait, monkeypatch, direct=False, invalid=bad)
-    u1, st1, it1 = _solve(cm, N, B, gait, monkeypatch, direct=True, invalid=bad)
+    u0, st0, it0 = _solve(cm, N, B, gait, direct=False, invalid=bad)
+    u1, st1, it1 = _solve(cm, N, B, gait, direct=True, invalid=bad)
     np.testing.assert_array_equal(st1, st0)
     np.testing.assert_array_equal(it1, it0)
     np.testing.assert_array_equal(u1, u0)

@@ -4,7 +4,6 @@ kernel (fused k_solve64 n <= 64, k_ipm128x, k_ipm_tiled n <= 256) is checked aga
 IPM (oracle/cmpc_oracle.c:qp_ipm_run, res[4]) reports for the same condensed QP, plus the stopping-rule semantics
 (SUCCESS => every residual within its tolerance; MAX_ITER at a tiny iter_max => not) and NaN for QPs the IPM skipped.
 Parity note: the oracle is this repo's restatement; HPIPM's own statistics are unpinned."""
-import os
 
 import numpy as np
 import pytest
@@ -67,15 +66,7 @@ def test_residuals_fused_equals_separate_launches(cm, op):
     mo = op.default_model(N)
     x0, xref, foot, contact = op.generate(mo, SEED, B, gait=1)  # mixed gait: n <= 64 and 64 < n <= 128 QPs
     eng_f = cm.Engine(cm.default_model(N), precision=cm.F64, max_batch=B)
-    old = os.environ.get("CMPC_FUSED")
-    os.environ["CMPC_FUSED"] = "0"
-    try:
-        eng_s = cm.Engine(cm.default_model(N), precision=cm.F64, max_batch=B)
-    finally:
-        if old is None:
-            del os.environ["CMPC_FUSED"]
-        else:
-            os.environ["CMPC_FUSED"] = old
+    eng_s = cm.Engine(cm.default_model(N), precision=cm.F64, max_batch=B, path={cm.PATH_FUSED64: 0})
     assert cm.lib().cmpc_ctx_fused(eng_f.ctx) == 1 and cm.lib().cmpc_ctx_fused(eng_s.ctx) == 0
     uf, _, sf, itf = eng_f.solve(x0, xref, foot, contact, want_x=False)
     rf = eng_f.residuals(B)

@@ -2,7 +2,7 @@
 # GPU-box script: rocprofv3 counter passes over one bench.py command (one pass per argument, counters space-separated
 # inside the argument; each pass within the per-block slot limits of MI355X_MICROARCH.md). BENCH_ARGS picks the
 # workload (default: the headline). Every pass has its own hard time limit; a failed pass ends the script.
-#   bash tools_gpu_pmc.sh "SQ_WAVES SQ_INSTS_VALU" "FETCH_SIZE" ...
+#   bash tools/gpu_pmc.sh "SQ_WAVES SQ_INSTS_VALU" "FETCH_SIZE" ...
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/pmc; mkdir -p $O
 BA=${BENCH_ARGS:-"--steps 3 --warmup 1 --cpu-sample 0"}
 cd /tmp && export TMPDIR=/tmp
