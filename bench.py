@@ -10,11 +10,16 @@ condensing + pyramid stacking + batched IPM + scatter/rollout (the whole hot pat
 
 Multi-GPU: the QP batch shards with no data-path collective (weak scaling, B per GPU, QP ids offset by rank so every
 QP's inputs are the same whatever the sharding); gloo is used only for the start/stop barriers and the max-over-ranks
-time. Rank 0 prints one JSON line.
+time. Rank 0 prints one JSON line. `bench.py --gpus N` (N > 1) without a launcher starts its N ranks itself, one
+child process per GPU, before anything touches the GPU. `value` is the solve throughput; `value_end_to_end` repeats the
+timed steps with every step's U shard copied into rank 0's GPU (the xGMI result gather of SURVEY section 8e) inside the
+timed window.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -96,7 +101,7 @@ def lib_md5():
 
 
 def pmc_traffic(path, prefix):
-    """HBM bytes per launch of the kernels whose name contains `prefix`, from the committed rocprofv3 --pmc summary
+    """HBM bytes per launch of the kernels whose name contains `prefix` (a string or a tuple of strings), from the committed rocprofv3 --pmc summary
     of this workload (profiles/traffic_<workload key>.json, written by cheeta-mpc_amd/tools/pmc_traffic.py from
     separate FETCH_SIZE / WRITE_SIZE passes of this same bench command). PMC counters cannot be read inside a normal
     run, so the value comes from the profiled run; it is reported only when the summary was taken on this exact
@@ -107,14 +112,16 @@ def pmc_traffic(path, prefix):
         doc = json.load(f)
     if doc.get("lib_md5") and doc["lib_md5"] != lib_md5():
         return None, f"PMC summary {os.path.basename(path)} was taken on another build of libcmpc.so"
-    tot = sum(v["hbm_bytes"] for k, v in doc["kernels"].items() if prefix in k)
+    pre = (prefix,) if isinstance(prefix, str) else tuple(prefix)
+    tot = sum(v["hbm_bytes"] for k, v in doc["kernels"].items() if any(p in k for p in pre))
     return (tot if tot > 0 else None), os.path.basename(path)
 
 
 def pmc_sq(wkey, prefix):
-    """Per-dispatch SQ counters of the kernel whose name contains `prefix`, from the committed rocprofv3 --pmc summary
-    of this workload (profiles/pmc_sq_<workload key>.json, cheeta-mpc_amd/tools/pmc_summary.py), only when it was
-    taken on this exact build of libcmpc.so (md5)."""
+    """Per-dispatch SQ counters of the kernels whose names contain `prefix` (a string or a tuple: the counters of
+    every matching kernel summed, e.g. a two-launch stage), from the committed rocprofv3 --pmc summary of this
+    workload (profiles/pmc_sq_<workload key>.json, cheeta-mpc_amd/tools/pmc_summary.py), only when it was taken on
+    this exact build of libcmpc.so (md5)."""
     path = os.path.join(ROOT, "profiles", f"pmc_sq_{wkey}.json")
     if not os.path.exists(path):
         return None, "no SQ PMC summary for this workload"
@@ -122,17 +129,82 @@ def pmc_sq(wkey, prefix):
         doc = json.load(f)
     if doc.get("lib_md5") != lib_md5():
         return None, f"SQ PMC summary {os.path.basename(path)} was taken on another build of libcmpc.so"
+    pre = (prefix,) if isinstance(prefix, str) else tuple(prefix)
+    acc = {}
     for k, v in doc["kernels"].items():
-        if prefix in k:
-            return v["counters"], os.path.basename(path)
-    return None, f"{prefix} not in {os.path.basename(path)}"
+        if any(p in k for p in pre):
+            for c, x in v["counters"].items():
+                acc[c] = acc.get(c, 0.0) + x
+    if not acc:
+        return None, f"{pre} not in {os.path.basename(path)}"
+    return acc, os.path.basename(path)
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """--gpus n > 1 without a launcher: one child process per rank (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set;
+    each child binds GPU LOCAL_RANK), started before this process touches the GPU; no exec. Rank 0's stdout (the JSON
+    line) is relayed; the other ranks' stdout goes to stderr. Returns the exit code: non-zero if any rank failed."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    # rank 0's stdout is drained by a thread; a rank that fails ends the others (they would otherwise wait in the
+    # rendezvous or a barrier for the gloo timeout)
+    import threading
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    while any(p.poll() is None for p in procs):
+        if any(p.poll() not in (None, 0) for p in procs):
+            time.sleep(2.0)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            break
+        time.sleep(0.1)
+    codes = [p.wait() for p in procs]
+    reader.join()
+    sys.stdout.write(b"".join(chunks).decode())
+    sys.stdout.flush()
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    if bad:
+        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr)
+        return 1
+    return 0
+
+
+def stub_rank(args):
+    """--stub (CPU tests of the launcher): the rank set-up, barriers and max-over-ranks of a real run over gloo, no
+    HIP call; rank 0 prints a JSON line carrying n_gpus like the real one. --stub-fail-rank r makes rank r exit 3."""
+    sys.path.insert(0, os.path.join(ROOT, "cheeta-mpc_amd", "python"))
+    from cheeta_mpc.shard import Dist
+    dist = Dist()
+    if dist.rank == args.stub_fail_rank:
+        sys.exit(3)
+    dist.barrier()
+    t = dist.max(float(dist.rank))
+    if dist.rank == 0:
+        print(json.dumps({"metric": "stub", "n_gpus": dist.world, "max_rank": t, "stub": True}), flush=True)
+    dist.close()
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults: 200 timed steps (~0.1 s at the headline) after 50 warm-up steps; with only 3 warm-up steps the first
+    # timed steps still ran at the idle clock (headline 7.93-8.10 M QPs/s at 3 / 20 against 8.38-8.45 M at 3 / 100,
+    # profiles/r03_warmup_ab.txt)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=4096, help="QPs per GPU per step")
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
@@ -153,7 +225,19 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's CPU share (cpu_share())")
     ap.add_argument("--traffic-json", default="",
                     help="PMC summary giving roofline.traffic (default: profiles/traffic_<workload key>.json)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pass (solve + result gather timed)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if ws is not None and int(ws) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (the launcher started a different rank count)")
+    if args.stub:
+        stub_rank(args)
+        return
 
     import cheeta_mpc as cm
     from cheeta_mpc.shard import Dist
@@ -231,22 +315,46 @@ def main():
     # stage 1 / 2 / 3 (cmpc.h): condensing / IPM / expand, or on the fused path fused n<=64 / bigger classes / expand
     ms_cond, ms_ipm, ms_exp = (m.value / max(ncalls.value, 1) for m in ms)
 
-    # result gather beside the timed region ("xGMI only for result gather"): every rank writes its U
-    # shard into rank 0's buffer (IPC-mapped device-to-device copy; no collective). A failure is reported, not fatal.
-    gather = {"what": "U of every rank into rank 0's GPU (cmpc_ipc_open + cmpc_gather_shard), after the timed steps",
-              "bytes": world * B * N * 12 * 8, "ms": 0.0 if world == 1 else None}
-    if world > 1:
-        # ResultGather's constructor and gather() reach every collective on every rank and raise on all ranks
-        # together, so the collectives below stay matched whatever fails
+    # end-to-end pass ("xGMI only for result gather"): the same K steps with every step's U shard
+    # written into rank 0's GPU right after its solve (IPC-mapped device-to-device copy on the step's stream: a peer
+    # write over xGMI between GPUs; no collective), all inside the timed window. A failure is reported, not fatal.
+    row = N * 12 * 8
+    gather = {"what": "every step: solve, then U of the rank's shard into rank 0's GPU (cmpc_ipc_open + "
+                      "cmpc_gather_shard on the step's stream), inside the timed window",
+              "bytes_per_step": world * B * row, "ms_per_step": None}
+    value_e2e = None
+    if not args.no_e2e and args.sqp_iters <= 0:
+        # ResultGather's constructor and the checks below reach every collective on every rank and raise on all ranks
+        # together, so the collectives stay matched whatever fails
         try:
             from cheeta_mpc.shard import ResultGather
-            row = N * 12 * 8
             rg = ResultGather(dist, world * B * row)
-            barrier()
-            tg = time.perf_counter()
             try:
-                rg.gather(u.ptr, rank * B * row, B * row, stream)
-                gather["ms"] = max_over_ranks(time.perf_counter() - tg) * 1e3
+                for i in range(args.warmup):
+                    step(i)
+                    cm._chk(cm.lib().cmpc_gather_shard(rg.dst, rank * B * row, outs[i % K][0].ptr, B * row,
+                                                       streams[i % K]), "cmpc_gather_shard")
+                H.hipDeviceSynchronize()
+                barrier()
+                H.hipDeviceSynchronize()
+                t0 = time.perf_counter()
+                for i in range(args.steps):
+                    step(i)
+                    cm._chk(cm.lib().cmpc_gather_shard(rg.dst, rank * B * row, outs[i % K][0].ptr, B * row,
+                                                       streams[i % K]), "cmpc_gather_shard")
+                for sh in streams:
+                    H.hipStreamSynchronize(sh)
+                H.hipDeviceSynchronize()
+                t1 = time.perf_counter()
+                barrier()
+                e2e = max_over_ranks(t1 - t0)
+                value_e2e = world * B * args.steps / e2e
+                gather["ms_per_step"] = e2e / args.steps * 1e3
+                gather["gather_ms_per_step"] = (e2e - elapsed) / args.steps * 1e3
+                # rank 0's buffer now holds every rank's U of the last step: its own slice must equal its solve
+                if rank == 0:
+                    got = rg.host(np.float64, (world * B, N, 4, 3))[:B]
+                    gather["rank0_slice_exact"] = bool(np.array_equal(got, outs[(args.steps - 1) % K][0].host()))
             finally:
                 rg.close()
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
@@ -285,31 +393,38 @@ def main():
         f_big = float(fl_ipm[~small].sum() + fl_cond[~small].sum())
         r_small = roof("k_solve64 (fused condensing + IPM, n<=64)", f_small, ms_cond, "valu", "k_solve64",
                        "IPM + condensing FLOPs of the n<=64 QPs")
-        r_big = roof("bigger classes (k_srbd_condense + k_ipm128x n<=128 / k_ipm_tiled n<=256)", f_big, ms_ipm,
-                     "valu", "k_ipm1", "IPM + condensing FLOPs of the n>64 QPs")
+        big_kernels = ("k_solve128", "k_srbd_condense", "k_ipm128x", "k_ipm_tiled", "k_class_lists")
+        r_big = roof("bigger classes (k_solve128 or k_srbd_condense + k_ipm128x n<=128; k_srbd_condense + "
+                     "k_ipm_tiled n<=256)", f_big, ms_ipm, "valu", big_kernels,
+                     "IPM + condensing FLOPs of the n>64 QPs")
         roofline, other = (r_small, r_big) if ms_cond >= ms_ipm else (r_big, r_small)
         stages = {"solve64_fused": ms_cond, "bigger_classes": ms_ipm, "expand": ms_exp}
         f_all = f_small + f_big
         extra = {"roofline_other_stage": other,
                  "roofline_solve": roof("whole solve (all classes, condensing + IPM)", f_all, ms_cond + ms_ipm,
                                         "valu", "cmpc::k_", "IPM + condensing FLOPs of every QP")}
-        # the condensing's H = Bqp' Q Bqp contraction inside k_solve64 runs on the matrix cores: its MFMA rate and
-        # busy fraction from the committed SQ counters of this build (executed MFMA FLOPs = MOPS x 512)
-        c, src = pmc_sq(wkey, "k_solve64")
+        # the condensing's H = Bqp' Q Bqp contraction runs on the matrix cores: its MFMA rate and busy fraction, for
+        # the dominant stage's kernels, from the committed SQ counters of this build (executed MFMA FLOPs = MOPS x 512)
+        if ms_cond >= ms_ipm:
+            mk, mms, what = ("k_solve64",), ms_cond, "k_solve64 condensing phase"
+        else:
+            mk, mms, what = (("k_solve128",) if cm.lib().cmpc_get_path(eng.ctx, cm.PATH_FUSED128) == 1 else
+                             ("k_srbd_condense",)), ms_ipm, "bigger-class condensing"
+        c, src = pmc_sq(wkey, mk)
         mops = c.get("SQ_INSTS_VALU_MFMA_MOPS_F64" if prec == cm.F64 else "SQ_INSTS_VALU_MFMA_MOPS_F32") if c else None
-        if mops is not None and ms_cond > 0:
+        if mops is not None and mms > 0:
             mfl = 512.0 * mops
             cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0  # GRBM_GUI_ACTIVE sums the 8 XCDs
             extra["mfma_condensing"] = {
-                "kernel": "k_solve64 condensing phase (H = Bqp' Q Bqp on v_mfma_%s_16x16x4), rate over the fused "
-                          "kernel's duration" % ("f64" if prec == cm.F64 else "f32"),
-                "mfma_flops_per_launch": mfl, "achieved": mfl / (ms_cond * 1e-3) / 1e12, "peak": peak / 1e12,
-                "unit": "TFLOP/s", "frac": mfl / (ms_cond * 1e-3) / peak,
+                "kernel": "%s (H = Bqp' Q Bqp on v_mfma_%s_16x16x4 in %s), rate over the stage's duration"
+                          % (what, "f64" if prec == cm.F64 else "f32", "+".join(mk)),
+                "mfma_flops_per_launch": mfl, "achieved": mfl / (mms * 1e-3) / 1e12, "peak": peak / 1e12,
+                "unit": "TFLOP/s", "frac": mfl / (mms * 1e-3) / peak,
                 "mfma_busy_frac": (c["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024.0)
                                    if cyc > 0 and "SQ_VALU_MFMA_BUSY_CYCLES" in c else None),
                 "source": src}
         else:
-            extra["mfma_condensing"] = {"kernel": "k_solve64 condensing phase", "achieved": None, "source": src}
+            extra["mfma_condensing"] = {"kernel": what, "achieved": None, "source": src}
     else:
         roofline = roof("IPM stage (k_ipm64 n<=64, k_ipm128x n<=128, k_ipm_tiled<16> n<=256)", float(fl_ipm.sum()),
                         ms_ipm, "valu", "k_ipm", "IPM FLOPs")
@@ -350,7 +465,9 @@ def main():
         "fused_n64": fused,
         "inflight": K,
         "stage_events": args.stage_events,
-        "gather_ms": gather["ms"], "gather": gather,
+        "value_end_to_end": value_e2e,
+        "gather_ms": gather.get("gather_ms_per_step"), "gather": gather,
+        "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,
                    "mean_n": float(nvar.mean())},
     }
