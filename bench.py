@@ -221,6 +221,8 @@ def main():
                     help="timed: HIP events around every stage of every timed step (the roofline's kernel times come "
                          "from the timed region itself); after: the timed steps run without events and the stage times "
                          "come from as many profiled steps run right after them")
+    ap.add_argument("--ric", type=int, choices=[0, 1, 2], default=0,
+                    help="CMPC_PATH_RICCATI: 0 condensed, 1 stage-wise kernel for the n > 64 classes, 2 for every QP")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="QPs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's CPU share (cpu_share())")
     ap.add_argument("--traffic-json", default="",
@@ -258,7 +260,8 @@ def main():
     else:
         settings = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3, tol_comp=1e-4)
     K = max(1, args.inflight)
-    engs = [cm.Engine(model, settings, precision=prec, max_batch=B) for _ in range(K)]
+    path = {cm.PATH_RICCATI: args.ric} if args.ric else None
+    engs = [cm.Engine(model, settings, precision=prec, max_batch=B, path=path) for _ in range(K)]
     eng = engs[0]
     x0, xref, foot, contact = cm.generate_device(model, SEED, B, gait=args.gait, offset=rank * B)
     if args.all_stance:

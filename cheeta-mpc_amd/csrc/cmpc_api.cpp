@@ -49,6 +49,9 @@ struct cmpc_ctx {
   bool fused;     // cold-start cmpc_solve_batch runs the fused n <= 64 kernel (k_solve64); possible when N <= 21
   bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;    // fused path without rollout: the IPM kernels scatter the results (no k_expand)
+  int ric = 0;    // stage-wise (Riccati) kernel k_ric: 0 off, 1 the n > 64 classes of the fused path, 2 every QP
+  void* ric_scr = nullptr;  // its per-QP stage factors [max_batch][ric_scratch_elems(N)]
+  size_t ric_scr_bytes = 0;
   double *lin, *uj, *uq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
@@ -312,6 +315,47 @@ int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, boo
   return r;
 }
 
+template <typename T>
+RicArgs<T> ric_args(cmpc_ctx* c, const double* x0, const double* xref, const double* foot, const uint8_t* contact,
+                    double* out_u, int* out_status, int* out_iters) {
+  RicArgs<T> a;
+  a.model = c->d_model;
+  a.N = c->model.N;
+  a.ld = c->ld;
+  a.x0 = x0;
+  a.xref = xref;
+  a.foot = foot;
+  a.contact = contact;
+  a.lin = nullptr;
+  a.s = dev_settings(c->settings);
+  a.scratch = (T*)c->ric_scr;
+  a.scr_stride = ric_scratch_elems(c->model.N);
+  a.u_ws = (T*)c->u;
+  a.tri_map = c->tri_map;
+  a.nvar = c->nvar;
+  a.status = c->status;
+  a.iters = c->iters;
+  a.out_u = out_u;
+  a.out_status = out_status;
+  a.out_iters = out_iters;
+  a.out_nu = c->model.N * 12;
+  a.res = c->res;
+  a.stats = c->stats;
+  a.stats_cap = c->stats_rows;
+  a.qlist = nullptr;
+  a.qlist2 = nullptr;
+  a.qcount = nullptr;
+  return a;
+}
+
+// Stage-wise path for every QP (CMPC_PATH_RICCATI = 2): one k_ric launch, no condensing.
+template <typename T>
+int run_ric_all_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                  const uint8_t* contact, hipStream_t st, double* out_u, int* out_status, int* out_iters) {
+  RicArgs<T> ra = ric_args<T>(c, x0, xref, foot, contact, out_u, out_status, out_iters);
+  return launch_ric<T>(ra, c->model.N <= 16 ? 1 : 2, B, st);
+}
+
 // Fused path (cold-start cmpc_solve_batch, N <= 21): k_solve64 condenses and solves the whole n <= 64 class in one
 // launch (the condensing's MFMA/latency-bound phase overlaps the IPM of the co-resident wave, and the first Newton
 // matrix starts from the condensing's registers instead of an H round trip); the bigger classes follow as before:
@@ -345,6 +389,20 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
   al.app_count = al.app_reset = nullptr;
   for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;  // list 0 unused here
   al.qcount = cnt;
+  if (c->ric == 1) {  // stage-wise kernel over the appended lists (n <= 128 first, then n > 128)
+    RicArgs<T> ra = ric_args<T>(c, x0, xref, foot, contact, out_u, out_status, out_iters);
+    ra.qlist = c->qlist + (size_t)1 * B;
+    ra.qcount = cnt + 1;
+    if (c->model.N <= 16) {  // nt <= 64 for every QP: one launch over both lists
+      ra.qlist2 = c->qlist + (size_t)2 * B;
+      return launch_ric<T>(ra, 1, B, st);
+    }
+    ra.qlist2 = nullptr;
+    if (launch_ric<T>(ra, 1, B, st) != 0) return -2;
+    ra.qlist = c->qlist + (size_t)2 * B;
+    ra.qcount = cnt + 2;
+    return launch_ric<T>(ra, 2, B, st);
+  }
   ca.n_lo = 64;
   ca.qlist = c->qlist + (size_t)1 * B;
   ca.qcount = cnt + 1;
@@ -535,6 +593,7 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (c->stats) (void)hipFree(c->stats);
   if (c->stage) (void)hipFree(c->stage);
   if (c->pol) (void)hipFree(c->pol);
+  if (c->ric_scr) (void)hipFree(c->ric_scr);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   delete c;
   return CMPC_OK;
@@ -564,7 +623,9 @@ int cmpc_get_model(const cmpc_ctx* c, cmpc_model* out) {
 int cmpc_ctx_ld(const cmpc_ctx* c) { return c ? c->ld : 0; }
 int cmpc_ctx_fused(const cmpc_ctx* c) { return c && c->fused ? 1 : 0; }
 
+static int set_ric_path(cmpc_ctx* c, int value);
 int cmpc_set_path(cmpc_ctx* c, int option, int value) {
+  if (c && option == CMPC_PATH_RICCATI) return set_ric_path(c, value);
   if (!c || (value != 0 && value != 1)) return CMPC_ERR_ARG;
   switch (option) {
     case CMPC_PATH_FUSED64:
@@ -582,12 +643,34 @@ int cmpc_set_path(cmpc_ctx* c, int option, int value) {
   }
 }
 
+// CMPC_PATH_RICCATI takes 0 / 1 / 2 (cmpc.h); the stage factors' scratch is allocated on first use (outside the
+// solve path)
+static int set_ric_path(cmpc_ctx* c, int value) {
+  if (value < 0 || value > 2) return CMPC_ERR_ARG;
+  if (value > 0) {
+    if (c->model.N > CMPC_RIC_MAXN) return CMPC_ERR_ARG;
+    if (value == 1 && !c->fused) return CMPC_ERR_ARG;
+    const size_t es = c->precision == CMPC_F64 ? 8 : 4;
+    const size_t bytes = (size_t)c->max_batch * ric_scratch_elems(c->model.N) * es;
+    if (c->ric_scr_bytes < bytes) {
+      if (c->ric_scr) (void)hipFree(c->ric_scr);
+      c->ric_scr = nullptr;
+      c->ric_scr_bytes = 0;
+      HIP_OK(hipMalloc(&c->ric_scr, bytes));
+      c->ric_scr_bytes = bytes;
+    }
+  }
+  c->ric = value;
+  return CMPC_OK;
+}
+
 int cmpc_get_path(const cmpc_ctx* c, int option) {
   if (!c) return CMPC_ERR_ARG;
   switch (option) {
     case CMPC_PATH_FUSED64: return c->fused ? 1 : 0;
     case CMPC_PATH_FUSED128: return c->fused128 ? 1 : 0;
     case CMPC_PATH_DIRECT: return c->direct ? 1 : 0;
+    case CMPC_PATH_RICCATI: return c->ric;
     default: return CMPC_ERR_ARG;
   }
 }
@@ -636,8 +719,16 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   const int warm = (u_init && c->settings.warm_start != 0) ? 1 : 0;
   // fused path without rollout: the IPM kernels write u / status / iters themselves (no k_expand)
-  const bool direct = c->direct && !warm && c->fused && x == nullptr && c->model.N * 12 <= 256;
-  if (!warm && c->fused) {
+  const bool direct = c->direct && !warm && (c->fused || c->ric == 2) && x == nullptr && c->model.N * 12 <= 256;
+  if (!warm && c->ric == 2) {
+    double* du = direct ? u : nullptr;
+    int* ds = direct ? status : nullptr;
+    int* di = direct ? iters : nullptr;
+    const int rr = c->precision == CMPC_F64 ? run_ric_all_t<double>(c, B, x0, xref, foot, contact, st, du, ds, di)
+                                            : run_ric_all_t<float>(c, B, x0, xref, foot, contact, st, du, ds, di);
+    if (rr != 0) return CMPC_ERR_HIP;
+    if (ev) HIP_OK(hipEventRecord(ev[1], st));
+  } else if (!warm && c->fused) {
     double* du = direct ? u : nullptr;
     int* ds = direct ? status : nullptr;
     int* di = direct ? iters : nullptr;

@@ -118,6 +118,48 @@ int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 <
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
 int launch_ipm256(const IpmArgs<float>& a, int B, hipStream_t stream);
 
+// Stage-wise (Riccati) form of the whole hot path, one wavefront per QP (k_ric.hpp): SRBD linearisation, pyramid
+// stacking and the Mehrotra IPM with Riccati Newton solves; no condensing, no H in the workspace. Writes the same
+// per-QP outputs as condensing + IPM (u [B][ld] in condensed order, tri_map, nvar, status, iters, res, stats) and,
+// when out_u is set, the caller's [N][4][3] forces directly.
+template <typename T>
+struct RicArgs {
+  const DevModel* model;
+  int N;               // horizon (host copy of model->N: picks the instantiation)
+  int ld;
+  const double* x0;
+  const double* xref;
+  const double* foot;
+  const uint8_t* contact;
+  const double* lin;   // SQP linearisation point [B][N][6] or null (CondenseArgs::lin)
+  DevSettings s;
+  T* scratch;          // per-QP stage factors: [B][N][ric::RS]
+  size_t scr_stride;   // elements per QP
+  T* u_ws;             // [B][ld] condensed-order solution, or null
+  int* tri_map;        // [B][ld / 3] or null
+  int* nvar;
+  int* status;
+  int* iters;
+  double* out_u;       // direct scatter, or null
+  int* out_status;
+  int* out_iters;
+  int out_nu;
+  double* res;         // [B][4] or null
+  double* stats;       // [B][stats_cap][CMPC_STAT_COLS] or null
+  int stats_cap;
+  // QP selection: null = workgroup b serves QP b; else QP qlist[b] for b < qcount[0], then qlist2[b - qcount[0]]
+  // for b < qcount[0] + qcount[1] (qlist2 may be null)
+  const int* qlist;
+  const int* qlist2;
+  const int* qcount;
+};
+#define CMPC_RIC_MAXN 21
+// per-QP scratch elements of the stage factors at horizon N
+__host__ __device__ inline size_t ric_scratch_elems(int N) { return (size_t)N * (12 * 12 + 12 * 24); }
+// tpl: force triples per lane (1: nt <= 64, i.e. every QP when N <= 16; 2: nt <= 128)
+template <typename T>
+int launch_ric(const RicArgs<T>& a, int tpl, int grid, hipStream_t stream);
+
 // res[q][4] of the QPs the IPM ran; NaN for the others (status 5 / 6)
 int launch_residuals(const double* res_ws, const int* status, int B, double* out, hipStream_t stream);
 

@@ -12,14 +12,15 @@ void check(int r, const char* what) {
 }
 }  // namespace
 
-CentroidalMPC::CentroidalMPC(double mass, int num_legs, int predict_horizon, double time_step, const VectorXd& weights,
-                             const VectorXd& mu, IPOPT_SOLVER /*ipopt_solver*/, int precision, int max_batch)
+CentroidalMPC::CentroidalMPC(double mass, int num_legs, int predict_horizon, double time_step, const double* weights,
+                             size_t n_weights, const double* mu, size_t n_mu, IPOPT_SOLVER /*ipopt_solver*/,
+                             int precision, int max_batch)
     : precision_(precision), max_batch_(max_batch) {
   // CentroidalMPC.cpp:24-25
   if (!(mass > 0 && num_legs > 0 && predict_horizon > 0)) throw std::invalid_argument("[CentroidalMPC] bad arguments");
-  if ((int)mu.size() != num_legs) throw std::invalid_argument("[CentroidalMPC] mu.size() != num_legs");
+  if ((int)n_mu != num_legs) throw std::invalid_argument("[CentroidalMPC] mu.size() != num_legs");
   if (num_legs != CMPC_MAX_LEGS) throw std::invalid_argument("[CentroidalMPC] this build supports num_legs == 4");
-  if ((int)weights.size() != (num_legs + 1) * 9) throw std::invalid_argument("[CentroidalMPC] weights size");
+  if ((int)n_weights != (num_legs + 1) * 9) throw std::invalid_argument("[CentroidalMPC] weights size");
   cmpc_model_default(&model_, predict_horizon);
   model_.mass = mass;
   model_.dt = time_step;
@@ -41,8 +42,8 @@ void CentroidalMPC::SetupMPC() {
   check(cmpc_create(&model_, &settings_, precision_, max_batch_, nullptr, &ctx_), "cmpc_create");
 }
 
-void CentroidalMPC::UpdateWeights(const VectorXd& weights) {
-  if ((int)weights.size() != CMPC_NUM_WEIGHTS) throw std::invalid_argument("[CentroidalMPC] weights size");
+void CentroidalMPC::UpdateWeightsRaw(const double* weights, size_t n) {
+  if ((int)n != CMPC_NUM_WEIGHTS) throw std::invalid_argument("[CentroidalMPC] weights size");
   for (int i = 0; i < CMPC_NUM_WEIGHTS; ++i) model_.weights[i] = weights[(size_t)i];
   if (ctx_) check(cmpc_set_model(ctx_, &model_), "cmpc_set_model");
 }
@@ -52,10 +53,12 @@ void CentroidalMPC::setSettings(const cmpc_settings& s) {
   if (ctx_) check(cmpc_set_settings(ctx_, &settings_), "cmpc_set_settings");
 }
 
-void CentroidalMPC::PackRecord(const VectorXd& state, const VectorXd& des_state, const VectorXd& des_inputs,
-                               VectorXd& x0, VectorXd& xref, VectorXd& foot, std::vector<uint8_t>& contact) const {
+void CentroidalMPC::PackRecordRaw(const double* state, size_t n_state, const double* des_state, size_t n_des_state,
+                                  const double* des_inputs, size_t n_des_inputs, std::vector<double>& x0,
+                                  std::vector<double>& xref, std::vector<double>& foot,
+                                  std::vector<uint8_t>& contact) const {
   const int N = model_.N, L = model_.n_legs;
-  if ((int)state.size() < 9 + 3 * L || (int)des_state.size() < 9 * (N + 1) || (int)des_inputs.size() < L * (4 * N + 3))
+  if ((int)n_state < 9 + 3 * L || (int)n_des_state < 9 * (N + 1) || (int)n_des_inputs < L * (4 * N + 3))
     throw std::invalid_argument("[CentroidalMPC] input vector sizes");
   x0.assign(CMPC_NX, 0.0);
   for (int j = 0; j < 9; ++j) x0[(size_t)j] = state[(size_t)j];  // c, v, L (CentroidalMPC.cpp:284-286)
@@ -79,19 +82,19 @@ void CentroidalMPC::PackRecord(const VectorXd& state, const VectorXd& des_state,
   }
 }
 
-CentroidalMPC::VectorXd CentroidalMPC::UpdateMPC(const VectorXd& state, const VectorXd& des_state,
-                                                 const VectorXd& des_inputs) {
+void CentroidalMPC::UpdateMPCRaw(const double* state, size_t n_state, const double* des_state, size_t n_des_state,
+                                 const double* des_inputs, size_t n_des_inputs, double* out) {
   if (!ctx_) throw std::runtime_error("[CentroidalMPC] SetupMPC() not called");
   const int N = model_.N, L = model_.n_legs;
-  VectorXd x0, xref, foot;
+  std::vector<double> x0, xref, foot;
   std::vector<uint8_t> contact;
-  PackRecord(state, des_state, des_inputs, x0, xref, foot, contact);
+  PackRecordRaw(state, n_state, des_state, n_des_state, des_inputs, n_des_inputs, x0, xref, foot, contact);
   for (int k = 0; k < N; ++k) {  // CentroidalMPC.cpp:326-330
     int ns = 0;
     for (int i = 0; i < L; ++i) ns += contact[(size_t)k * L + i];
     if (ns <= 0) throw std::runtime_error("mpc table invalid");
   }
-  VectorXd u((size_t)N * CMPC_NU);
+  std::vector<double> u((size_t)N * CMPC_NU);
   int status = -1, iters = 0;
   check(cmpc_solve_batch_host(ctx_, 1, x0.data(), xref.data(), foot.data(), contact.data(), u.data(), nullptr, &status,
                               &iters),
@@ -100,11 +103,9 @@ CentroidalMPC::VectorXd CentroidalMPC::UpdateMPC(const VectorXd& state, const Ve
   last_iters_ = iters;
   current_time_ += model_.dt;  // CentroidalMPC.cpp:368
   // per leg: contact_force_i as 3 x N column-major (controller_ output order)
-  VectorXd out((size_t)L * 3 * N);
   for (int i = 0; i < L; ++i)
     for (int k = 0; k < N; ++k)
       for (int d = 0; d < 3; ++d) out[(size_t)i * 3 * N + 3 * k + d] = u[((size_t)k * L + i) * 3 + d];
-  return out;
 }
 
 int CentroidalMPC::FeedbackPolicyBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,

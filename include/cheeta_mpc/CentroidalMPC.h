@@ -1,9 +1,13 @@
 /*
- * CentroidalMPC.h — Eigen-free mirror of the reference's public MPC class (reference CentroidalMPC.h:15-33,
+ * CentroidalMPC.h — mirror of the reference's public MPC class (reference CentroidalMPC.h:15-33,
  * NonlinearMPC.h:50-154), backed by the MI355X batched QP engine through the C ABI (cmpc/cmpc.h).
  *
  * Same constructor arguments, SetupMPC(), UpdateMPC(state, des_state, des_inputs) with the reference's flat
- * layouts (CentroidalMPC.cpp:284-323) and the same "mpc table invalid" std::runtime_error (:328-330). Differences:
+ * layouts (CentroidalMPC.cpp:284-323) and the same "mpc table invalid" std::runtime_error (:328-330). The vector
+ * arguments are templates over any contiguous double vector with data() / size() / resize() (Eigen::VectorXd, which
+ * the reference takes, or std::vector<double>): the reference's caller (CentoidMPCTest.cpp) compiles against this
+ * header with only the include swapped, and the library behind it (libcmpc.so, host/CentroidalMPC.cpp) sees raw
+ * pointers only. Differences:
  *   - UpdateMPC returns the contact forces (the reference returns an empty vector, :369): per leg i a 3 x N
  *     column-major block, legs concatenated — the order of the reference controller's contact_force_i outputs;
  *   - the IPOPT_SOLVER argument is accepted and ignored (the solver is the batched GPU interior point method);
@@ -12,32 +16,66 @@
  */
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 #include <stdexcept>
 #include <vector>
 
 #include "cmpc/cmpc.h"
 
+#if !defined(CMPC_EIGEN_STANDIN) && __has_include(<Eigen/Dense>)
+#include <Eigen/Dense>
+#define CMPC_HAVE_EIGEN 1
+#endif
+
 enum class IPOPT_SOLVER : unsigned int { MUMPS = 0, WSMP = 1, PARDISO = 2, MA27 = 3, MA57 = 4, MA77 = 5, MA86 = 6, MA97 = 7 };
 
 namespace cheeta_mpc {
+#ifdef CMPC_HAVE_EIGEN
+using VectorXd = Eigen::VectorXd;  // the reference's argument type (CentroidalMPC.h:26-32)
+#else
 using VectorXd = std::vector<double>;
-}
+#endif
+}  // namespace cheeta_mpc
 
 class CentroidalMPC {
  public:
   using VectorXd = cheeta_mpc::VectorXd;
 
-  CentroidalMPC(double mass, int num_legs, int predict_horizon, double time_step, const VectorXd& weights,
-                const VectorXd& mu, IPOPT_SOLVER ipopt_solver = IPOPT_SOLVER::MA97, int precision = CMPC_F64,
-                int max_batch = 1);
+  template <class Vec>
+  CentroidalMPC(double mass, int num_legs, int predict_horizon, double time_step, const Vec& weights, const Vec& mu,
+                IPOPT_SOLVER ipopt_solver = IPOPT_SOLVER::MA97, int precision = CMPC_F64, int max_batch = 1)
+      : CentroidalMPC(mass, num_legs, predict_horizon, time_step, weights.data(), (size_t)weights.size(), mu.data(),
+                      (size_t)mu.size(), ipopt_solver, precision, max_batch) {}
+  /* the constructor proper: raw arrays (weights[(num_legs + 1) * 9], mu[num_legs]) */
+  CentroidalMPC(double mass, int num_legs, int predict_horizon, double time_step, const double* weights,
+                size_t n_weights, const double* mu, size_t n_mu, IPOPT_SOLVER ipopt_solver, int precision,
+                int max_batch);
   ~CentroidalMPC();
   CentroidalMPC(const CentroidalMPC&) = delete;
   CentroidalMPC& operator=(const CentroidalMPC&) = delete;
 
   void SetupMPC();
-  VectorXd UpdateMPC(const VectorXd& state, const VectorXd& des_state, const VectorXd& des_inputs);
-  void UpdateWeights(const VectorXd& weights);
+
+  /* Returns the forces in the caller's vector type (per leg a 3 x N column-major block). */
+  template <class Vec>
+  Vec UpdateMPC(const Vec& state, const Vec& des_state, const Vec& des_inputs) {
+    Vec out;
+    out.resize((decltype(out.size()))OutputSize());
+    UpdateMPCRaw(state.data(), (size_t)state.size(), des_state.data(), (size_t)des_state.size(), des_inputs.data(),
+                 (size_t)des_inputs.size(), out.data());
+    return out;
+  }
+  template <class Vec>
+  void UpdateWeights(const Vec& weights) {
+    UpdateWeightsRaw(weights.data(), (size_t)weights.size());
+  }
+
+  /* raw-array forms: out[OutputSize()] */
+  int OutputSize() const { return model_.n_legs * 3 * model_.N; }
+  void UpdateMPCRaw(const double* state, size_t n_state, const double* des_state, size_t n_des_state,
+                    const double* des_inputs, size_t n_des_inputs, double* out);
+  void UpdateWeightsRaw(const double* weights, size_t n);
 
   /* Batched extension: device pointers in cmpc_solve_batch's record layout, async on stream. */
   int UpdateMPCBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot, const uint8_t* d_contact,
@@ -50,8 +88,15 @@ class CentroidalMPC {
                           int* d_status, void* stream);
 
   /* The 13-state record UpdateMPC builds from the reference's flat layouts (exposed for tests). */
-  void PackRecord(const VectorXd& state, const VectorXd& des_state, const VectorXd& des_inputs, VectorXd& x0,
-                  VectorXd& xref, VectorXd& foot, std::vector<uint8_t>& contact) const;
+  template <class Vec>
+  void PackRecord(const Vec& state, const Vec& des_state, const Vec& des_inputs, std::vector<double>& x0,
+                  std::vector<double>& xref, std::vector<double>& foot, std::vector<uint8_t>& contact) const {
+    PackRecordRaw(state.data(), (size_t)state.size(), des_state.data(), (size_t)des_state.size(), des_inputs.data(),
+                  (size_t)des_inputs.size(), x0, xref, foot, contact);
+  }
+  void PackRecordRaw(const double* state, size_t n_state, const double* des_state, size_t n_des_state,
+                     const double* des_inputs, size_t n_des_inputs, std::vector<double>& x0, std::vector<double>& xref,
+                     std::vector<double>& foot, std::vector<uint8_t>& contact) const;
 
   int lastStatus() const { return last_status_; }
   int lastIterations() const { return last_iters_; }

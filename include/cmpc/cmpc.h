@@ -134,16 +134,21 @@ int cmpc_ctx_ld(const cmpc_ctx* ctx);
 /* 1 when a cold-start cmpc_solve_batch runs the fused condensing + IPM kernel for the n <= 64 class, else 0
  * (= cmpc_get_path(ctx, CMPC_PATH_FUSED64)). */
 int cmpc_ctx_fused(const cmpc_ctx* ctx);
-/* Kernel path of a context, for A/B measurement and tests; every choice gives bit-identical results:
+/* Kernel path of a context, for A/B measurement and tests; the first three options give bit-identical results:
  *   CMPC_PATH_FUSED64   1 (default when N <= 21): cold-start solves condense and solve the n <= 64 class in one
  *                       launch; 0: a condensing launch, then the IPM launch. 1 is CMPC_ERR_ARG when N > 21.
  *   CMPC_PATH_FUSED128  1: the 64 < n <= 128 class condensed and solved in one launch on the fused path (default for
  *                       fp32 contexts); 0: two launches (default for fp64, where the fused form measured slower).
  *   CMPC_PATH_DIRECT    1 (default): on the fused path without a rollout the IPM kernels write u / status / iters;
  *                       0: through the scatter kernel.
- * cmpc_set_path returns CMPC_ERR_ARG for an unknown option or a value other than 0 / 1; cmpc_get_path returns the
- * current value or CMPC_ERR_ARG. */
-enum cmpc_path_option { CMPC_PATH_FUSED64 = 0, CMPC_PATH_FUSED128 = 1, CMPC_PATH_DIRECT = 2 };
+ *   CMPC_PATH_RICCATI   0 (default): the condensed path above. 1: on the fused path, the n > 64 QPs are solved by the
+ *                       stage-wise kernel (Riccati Newton solves over the horizon, no condensing, HPIPM's method);
+ *                       2: every cold-start QP is (one launch). Results agree with the condensed path to rounding,
+ *                       not bit for bit (a different factorisation of the same Newton systems). Needs N <= 21; 1 needs
+ *                       CMPC_PATH_FUSED64 = 1. The first non-zero value allocates the stage-factor scratch.
+ * cmpc_set_path returns CMPC_ERR_ARG for an unknown option or a value out of range (0 / 1; 0 / 1 / 2 for
+ * CMPC_PATH_RICCATI); cmpc_get_path returns the current value or CMPC_ERR_ARG. */
+enum cmpc_path_option { CMPC_PATH_FUSED64 = 0, CMPC_PATH_FUSED128 = 1, CMPC_PATH_DIRECT = 2, CMPC_PATH_RICCATI = 3 };
 int cmpc_set_path(cmpc_ctx* ctx, int option, int value);
 int cmpc_get_path(const cmpc_ctx* ctx, int option);
 

@@ -1,3 +1,5 @@
+// Built twice (tests/cpp/Makefile): against the hpipm_catkin stand-in types and against Eigen / ocs2_core-shaped
+// types (mock_eigen, mock_ocs2), so it uses only the API both share (no zero-initialising constructors either).
 // C++ mirror of the reference gtests ocs2_sqp/hpipm_catkin/test/testHpipmInterface.cpp (solve_and_check_dynamic
 // :37-69, solve_after_resize :71-110, knownSolution :112-152, with_constraints :154-206, noInputs :208-256,
 // retrieveRiccati :258-340) against the
@@ -16,6 +18,12 @@ using namespace ocs2;
 static std::mt19937_64 rng(20221125);
 static double U() { return std::uniform_real_distribution<double>(-1.0, 1.0)(rng); }
 
+static matrix_t zeros(int r, int c) {
+  matrix_t m(r, c);
+  for (int j = 0; j < c; ++j)
+    for (int i = 0; i < r; ++i) m(i, j) = 0.0;
+  return m;
+}
 static matrix_t randm(int r, int c) {
   matrix_t m(r, c);
   for (int j = 0; j < c; ++j)
@@ -258,7 +266,8 @@ static matrix_t tr(const matrix_t& A) {
 }
 static matrix_t add(const matrix_t& A, const matrix_t& B, double sb = 1.0) {
   matrix_t C = A;
-  for (size_t e = 0; e < C.a.size(); ++e) C.a[e] += sb * B.a[e];
+  for (int j = 0; j < C.cols(); ++j)
+    for (int i = 0; i < C.rows(); ++i) C(i, j) += sb * B(i, j);
   return C;
 }
 static vector_t addv(const vector_t& a, const vector_t& b, double sb = 1.0) {
@@ -268,7 +277,7 @@ static vector_t addv(const vector_t& a, const vector_t& b, double sb = 1.0) {
 }
 static matrix_t inv(const matrix_t& A) {  // Gauss-Jordan with partial pivoting (small, well conditioned)
   const int n = A.rows();
-  matrix_t M = A, I(n, n);
+  matrix_t M = A, I = zeros(n, n);
   for (int i = 0; i < n; ++i) I(i, i) = 1.0;
   for (int c = 0; c < n; ++c) {
     int p = c;
@@ -297,7 +306,8 @@ static matrix_t inv(const matrix_t& A) {  // Gauss-Jordan with partial pivoting 
 static double maxdiffm(const matrix_t& a, const matrix_t& b) {
   if (a.rows() != b.rows() || a.cols() != b.cols()) return 1e300;
   double m = 0.0;
-  for (size_t e = 0; e < a.a.size(); ++e) m = std::fmax(m, std::fabs(a.a[e] - b.a[e]));
+  for (int j = 0; j < a.cols(); ++j)
+    for (int i = 0; i < a.rows(); ++i) m = std::fmax(m, std::fabs(a(i, j) - b(i, j)));
   return m;
 }
 
@@ -328,10 +338,9 @@ static void retrieve_riccati() {
     const vector_t rr = addv(addv(c.dfdu, mtv(B, sv)), mtv(B, mv(Sm, b)));
     SmG[(size_t)k] = add(add(c.dfdxx, mm(tr(A), mm(Sm, A))), mm(tr(P_BTSmA), mm(invR, P_BTSmA)), -1.0);
     svG[(size_t)k] = addv(addv(addv(c.dfdx, mtv(A, sv)), mtv(A, mv(Sm, b))), mv(tr(P_BTSmA), mv(invR, rr)), -1.0);
-    KG[(size_t)k] = mm(invR, P_BTSmA);
-    for (auto& v : KG[(size_t)k].a) v = -v;
+    KG[(size_t)k] = add(zeros(nu, nx), mm(invR, P_BTSmA), -1.0);
     kG[(size_t)k] = mv(invR, rr);
-    for (auto& v : kG[(size_t)k].v) v = -v;
+    for (int i = 0; i < kG[(size_t)k].size(); ++i) kG[(size_t)k][i] = -kG[(size_t)k][i];
   }
   HpipmInterface hpipm(HpipmInterface::OcpSize(N, nx, nu));
   vector_array_t xs, us;
@@ -356,6 +365,76 @@ static void retrieve_riccati() {
   CHECK(e < 1e-9, "retrieveRiccati 1e-9");
 }
 
+// total cost of a trajectory: sum_k 1/2 x'Q x + u'S x + 1/2 u'R u + q'x + r'u (+ terminal)
+static double total_cost(const std::vector<ScalarFunctionQuadraticApproximation>& cost, const vector_array_t& xs,
+                         const vector_array_t& us) {
+  double J = 0.0;
+  for (size_t k = 0; k < cost.size(); ++k) {
+    const auto& c = cost[k];
+    const vector_t& x = xs[k];
+    const vector_t qx = mv(c.dfdxx, x);
+    for (int i = 0; i < x.size(); ++i) J += 0.5 * x[i] * qx[i] + c.dfdx[i] * x[i];
+    if (k < us.size() && us[k].size() > 0) {
+      const vector_t& u = us[k];
+      const vector_t ru = mv(c.dfduu, u), sx = mv(c.dfdux, x);
+      for (int i = 0; i < u.size(); ++i) J += 0.5 * u[i] * ru[i] + u[i] * sx[i] + c.dfdu[i] * u[i];
+    }
+  }
+  return J;
+}
+
+// Riccati quantities after an equality-constrained solve (the non-projection branch of getOCPSolution followed by
+// setPrimalSolution's getRiccatiFeedback, MultipleShootingSolver.cpp:275-277, :334-340): u_k = K_k x_k + k_k on the
+// solution, K_0 = d u_0 / d x0 by finite differences of the constrained solution map, and the cost-to-go of node 0
+// reproduces the change of the optimal cost under a perturbation of x0.
+static void constrained_riccati() {
+  const int nx = 3, nu = 2, N = 5;
+  const vector_t x0 = randv(nx);
+  std::vector<VectorFunctionLinearApproximation> sys, con;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+    con.push_back(randomConstraints(nx, nu, 1));
+  }
+  cost.push_back(randomCost(nx, 0));
+  con.push_back(randomConstraints(nx, 0, 1));
+  con[2] = VectorFunctionLinearApproximation();
+  HpipmInterface hpipm(hpipm_interface::extractSizesFromProblem(sys, cost, &con));
+  vector_array_t xs, us;
+  CHECK(hpipm.solve(x0, sys, cost, &con, xs, us, false) == SUCCESS, "constrained riccati status");
+  const auto K = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  const auto kf = hpipm.getRiccatiFeedforward(sys[0], cost[0]);
+  const auto ctg = hpipm.getRiccatiCostToGo(sys[0], cost[0]);
+  double e_pol = 0.0, e_fd = 0.0, e_ctg = 0.0;
+  for (int k = 0; k < N; ++k) e_pol = std::fmax(e_pol, maxdiff(us[(size_t)k], addv(mv(K[(size_t)k], xs[(size_t)k]), kf[(size_t)k])));
+  const double J0 = total_cost(cost, xs, us);
+  const double eps = 1e-3;
+  for (int i = 0; i < nx; ++i) {
+    vector_t x1 = x0;
+    x1[i] += eps;
+    vector_array_t x1s, u1s;
+    hpipm.solve(x1, sys, cost, &con, x1s, u1s, false);
+    for (int a = 0; a < nu; ++a) e_fd = std::fmax(e_fd, std::fabs((u1s[0][a] - us[0][a]) / eps - K[0](a, i)));
+    // V(x0 + d) - V(x0) = s'd + x0'S d + 1/2 d'S d
+    const double dJ = total_cost(cost, x1s, u1s) - J0;
+    double pred = ctg[0].dfdx[i] * eps + 0.5 * ctg[0].dfdxx(i, i) * eps * eps;
+    for (int c = 0; c < nx; ++c) pred += x0[c] * ctg[0].dfdxx(c, i) * eps;
+    e_ctg = std::fmax(e_ctg, std::fabs(dJ - pred) / std::fmax(1.0, std::fabs(dJ)));
+  }
+  // the later stages' feedback acts on the state of that stage: perturb the tail through u_0 is not needed — the
+  // policy identity above covers k >= 1; K symmetric pieces: cost-to-go Hessians are symmetric
+  double e_sym = 0.0;
+  for (int k = 0; k <= N; ++k)
+    for (int i = 0; i < nx; ++i)
+      for (int j = 0; j < nx; ++j) e_sym = std::fmax(e_sym, std::fabs(ctg[(size_t)k].dfdxx(i, j) - ctg[(size_t)k].dfdxx(j, i)));
+  std::printf("constrained riccati: policy %.2e, fd K0 %.2e, cost-to-go %.2e, symmetry %.2e\n", e_pol, e_fd, e_ctg, e_sym);
+  CHECK(e_pol < 1e-9, "constrained riccati u = K x + k");
+  CHECK(e_fd < 1e-7, "constrained riccati K0 by finite differences");
+  CHECK(e_ctg < 1e-7, "constrained riccati cost-to-go");
+  CHECK(e_sym < 1e-9, "constrained riccati S symmetric");
+}
+
 int main() {
   dynamics_feasible(false);
   dynamics_feasible(true);
@@ -363,6 +442,7 @@ int main() {
   known_solution(true);
   with_constraints();
   retrieve_riccati();
+  constrained_riccati();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;
 }

@@ -375,6 +375,24 @@ def test_cpp_hpipm_interface_mirror(cpp_bins):
     assert "PASSED" in r.stdout
 
 
+def test_cpp_hpipm_interface_mirror_ocs2_types(cpp_bins):
+    """The same gtest mirror compiled against Eigen / ocs2_core-shaped value types (tests/cpp/mock_eigen, mock_ocs2:
+    private storage, uninitialised sizing constructors): the include swap a real ocs2 build makes (reference
+    HpipmInterface.h:38); includes the Riccati quantities after an equality-constrained solve."""
+    r = subprocess.run([str(cpp_bins / "test_hpipm_interface_ocs2")], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASSED" in r.stdout and "constrained riccati" in r.stdout
+
+
+def test_cpp_centroidal_mpc_eigen_driver_equals_vector_driver(cpp_bins):
+    """CentoidMPCTest.cpp's calls written with Eigen::VectorXd, comma initializers and make_shared (the reference's
+    own style) against cheeta_mpc/CentroidalMPC.h print exactly what the std::vector build prints."""
+    a = subprocess.run([str(cpp_bins / "centroid_mpc_test")], capture_output=True, text=True, timeout=120)
+    b = subprocess.run([str(cpp_bins / "centroid_mpc_test_eigen")], capture_output=True, text=True, timeout=120)
+    assert a.returncode == 0 and b.returncode == 0, a.stdout + a.stderr + b.stdout + b.stderr
+    assert a.stdout == b.stdout
+
+
 def test_cpp_centroidal_mpc_driver(cpp_bins, op):
     """CentoidMPCTest.cpp equivalent through the C++ CentroidalMPC mirror vs the numpy golden (literal quirk)."""
     r = subprocess.run([str(cpp_bins / "centroid_mpc_test")], capture_output=True, text=True, timeout=120)
