@@ -50,8 +50,6 @@ struct cmpc_ctx {
   bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;    // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   int ric = 0;    // stage-wise (Riccati) kernel k_ric: 0 off, 1 the n > 64 classes of the fused path, 2 every QP
-  void* ric_scr = nullptr;  // its per-QP stage factors [max_batch][ric_scratch_elems(N)]
-  size_t ric_scr_bytes = 0;
   double *lin, *uj, *uq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
@@ -328,8 +326,6 @@ RicArgs<T> ric_args(cmpc_ctx* c, const double* x0, const double* xref, const dou
   a.contact = contact;
   a.lin = nullptr;
   a.s = dev_settings(c->settings);
-  a.scratch = (T*)c->ric_scr;
-  a.scr_stride = ric_scratch_elems(c->model.N);
   a.u_ws = (T*)c->u;
   a.tri_map = c->tri_map;
   a.nvar = c->nvar;
@@ -353,7 +349,7 @@ template <typename T>
 int run_ric_all_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                   const uint8_t* contact, hipStream_t st, double* out_u, int* out_status, int* out_iters) {
   RicArgs<T> ra = ric_args<T>(c, x0, xref, foot, contact, out_u, out_status, out_iters);
-  return launch_ric<T>(ra, c->model.N <= 16 ? 1 : 2, B, st);
+  return launch_ric<T>(ra, 12 * c->model.N, B, st);
 }
 
 // Fused path (cold-start cmpc_solve_batch, N <= 21): k_solve64 condenses and solves the whole n <= 64 class in one
@@ -393,15 +389,16 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
     RicArgs<T> ra = ric_args<T>(c, x0, xref, foot, contact, out_u, out_status, out_iters);
     ra.qlist = c->qlist + (size_t)1 * B;
     ra.qcount = cnt + 1;
-    if (c->model.N <= 16) {  // nt <= 64 for every QP: one launch over both lists
+    const int nfull = 12 * c->model.N;
+    if (nfull <= 128) {  // one launch over both lists
       ra.qlist2 = c->qlist + (size_t)2 * B;
-      return launch_ric<T>(ra, 1, B, st);
+      return launch_ric<T>(ra, nfull, B, st);
     }
     ra.qlist2 = nullptr;
-    if (launch_ric<T>(ra, 1, B, st) != 0) return -2;
+    if (launch_ric<T>(ra, 128, B, st) != 0) return -2;
     ra.qlist = c->qlist + (size_t)2 * B;
     ra.qcount = cnt + 2;
-    return launch_ric<T>(ra, 2, B, st);
+    return launch_ric<T>(ra, nfull, B, st);
   }
   ca.n_lo = 64;
   ca.qlist = c->qlist + (size_t)1 * B;
@@ -593,7 +590,6 @@ int cmpc_destroy(cmpc_ctx* c) {
   if (c->stats) (void)hipFree(c->stats);
   if (c->stage) (void)hipFree(c->stage);
   if (c->pol) (void)hipFree(c->pol);
-  if (c->ric_scr) (void)hipFree(c->ric_scr);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   delete c;
   return CMPC_OK;
@@ -643,22 +639,12 @@ int cmpc_set_path(cmpc_ctx* c, int option, int value) {
   }
 }
 
-// CMPC_PATH_RICCATI takes 0 / 1 / 2 (cmpc.h); the stage factors' scratch is allocated on first use (outside the
-// solve path)
+// CMPC_PATH_RICCATI takes 0 / 1 / 2 (cmpc.h)
 static int set_ric_path(cmpc_ctx* c, int value) {
   if (value < 0 || value > 2) return CMPC_ERR_ARG;
   if (value > 0) {
     if (c->model.N > CMPC_RIC_MAXN) return CMPC_ERR_ARG;
     if (value == 1 && !c->fused) return CMPC_ERR_ARG;
-    const size_t es = c->precision == CMPC_F64 ? 8 : 4;
-    const size_t bytes = (size_t)c->max_batch * ric_scratch_elems(c->model.N) * es;
-    if (c->ric_scr_bytes < bytes) {
-      if (c->ric_scr) (void)hipFree(c->ric_scr);
-      c->ric_scr = nullptr;
-      c->ric_scr_bytes = 0;
-      HIP_OK(hipMalloc(&c->ric_scr, bytes));
-      c->ric_scr_bytes = bytes;
-    }
   }
   c->ric = value;
   return CMPC_OK;

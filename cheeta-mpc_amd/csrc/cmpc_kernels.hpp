@@ -133,8 +133,6 @@ struct RicArgs {
   const uint8_t* contact;
   const double* lin;   // SQP linearisation point [B][N][6] or null (CondenseArgs::lin)
   DevSettings s;
-  T* scratch;          // per-QP stage factors: [B][N][ric::RS]
-  size_t scr_stride;   // elements per QP
   T* u_ws;             // [B][ld] condensed-order solution, or null
   int* tri_map;        // [B][ld / 3] or null
   int* nvar;
@@ -154,11 +152,9 @@ struct RicArgs {
   const int* qcount;
 };
 #define CMPC_RIC_MAXN 21
-// per-QP scratch elements of the stage factors at horizon N
-__host__ __device__ inline size_t ric_scratch_elems(int N) { return (size_t)N * (12 * 12 + 12 * 24); }
-// tpl: force triples per lane (1: nt <= 64, i.e. every QP when N <= 16; 2: nt <= 128)
+// nmax: the largest condensed size of the QPs the launch can see (picks the LDS factor store and triples per lane)
 template <typename T>
-int launch_ric(const RicArgs<T>& a, int tpl, int grid, hipStream_t stream);
+int launch_ric(const RicArgs<T>& a, int nmax, int grid, hipStream_t stream);
 
 // res[q][4] of the QPs the IPM ran; NaN for the others (status 5 / 6)
 int launch_residuals(const double* res_ws, const int* status, int B, double* out, hipStream_t stream);

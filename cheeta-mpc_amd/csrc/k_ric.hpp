@@ -35,9 +35,36 @@
 #include "step_ratio.hpp"
 #include "wave_dpp.hpp"
 
+// Diagnostic builds only (-DCMPC_RIC_STAMPS, lab): s_memtime cycles per phase of each QP, written over row 0 of the
+// statistics buffer (cmpc_enable_stats): [0] setup, [1] gradient, [2] factorisations, [3] solves, [4] the rest of the
+// iterations, [5] total, [6] iterations.
+#ifdef CMPC_RIC_STAMPS
+#define RIC_STAMP_DECL                                 \
+  unsigned long long rst_[6] = {0, 0, 0, 0, 0, 0};    \
+  const unsigned long long rst0_ = ric::memtime();    \
+  unsigned long long rprev_ = rst0_
+#define RIC_STAMP(k)                             \
+  do {                                           \
+    const unsigned long long t_ = ric::memtime(); \
+    rst_[k] += t_ - rprev_;                      \
+    rprev_ = t_;                                 \
+  } while (0)
+#else
+#define RIC_STAMP_DECL (void)0
+#define RIC_STAMP(k) (void)0
+#endif
+
 namespace cmpc {
 
 namespace ric {
+
+__device__ __forceinline__ unsigned long long memtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 constexpr int ZS = 24;           // z slots: 12 state rows + 12 previous-force slots
 constexpr int RS = 12 * 12 + 12 * ZS;  // scratch per stage: Li [12][12], Y [12][24]
@@ -55,8 +82,11 @@ struct Lim<float> {
   static constexpr float mu_min = 1e-35f;
 };
 
-template <typename T, int NR, int TPL>
+template <typename T, int NR, int TPL, int FS>
 struct Lds {
+  T fac[FS];             // stage factors (compact): per stage Li packed lower, then the state columns of Y
+  int foff[NR + 1];      // offset of stage k's factors in fac
+  T wf2[12], wr2[12];    // 2 Wf, 2 Wr per force slot
   int sb[NR];            // stance mask of step k
   int cb[NR + 1];        // 3 * #triples before step k
   int tk[4 * NR], tleg[4 * NR];
@@ -74,8 +104,6 @@ struct Lds {
     struct {
       T G[12][ZS];
       T Rt[12][12];
-      T Li[12][12];
-      T Y[12][ZS];
       T Pcol[6][12];
     } f;
     struct {
@@ -85,12 +113,22 @@ struct Lds {
   };
 };
 
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// Ordering of LDS traffic between the lanes of the one wave (the workgroup is one wave): LDS writes drained
+// (lgkmcnt) before the other lanes read them. The factor store and every exchange live in LDS, so the fence has no
+// outstanding global stores to wait for inside the iteration.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 template <typename T>
 __device__ __forceinline__ T shfl_x32(T v) {
   return __shfl_xor(v, 32, 64);
 }
+
+// compact index of force slot a (3 leg + d) among the stance slots of mask sk
+__device__ __forceinline__ int cslot(int sk, int a) { return 3 * __popc(sk & ((1 << (a / 3)) - 1)) + a % 3; }
 
 template <typename T>
 __device__ __forceinline__ T pinv_sqrt(T d) {
@@ -100,15 +138,16 @@ __device__ __forceinline__ T pinv_sqrt(T d) {
 }  // namespace ric
 
 // Body of one QP. TPL: force triples per lane (nt <= 64 TPL); NR: longest horizon the LDS block holds.
-template <typename T, int TPL, int NR>
+template <typename T, int TPL, int NR, int FS>
 __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
   using namespace ric;
-  __shared__ Lds<T, NR, TPL> S;
+  __shared__ Lds<T, NR, TPL, FS> S;
   const DevModel* __restrict__ M = A.model;
   const int N = M->N;
   const int lane = (int)threadIdx.x;
   const DevSettings st = A.s;
   const T dt = T(M->dt), dtm = T(M->dt_over_m);
+  RIC_STAMP_DECL;
 
   // ---- contact table: stance masks, triple offsets (k-major, legs ascending: the condensed variable order)
   int sbl = 0;
@@ -150,11 +189,30 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     finish_rejected(CMPC_TOO_LARGE);
     return;
   }
+  // factor storage per stage: m (m + 1) / 2 + 12 m (m = 3 n_stance)
+  const int msl = 3 * nsl;
+  int fsz = lane < N ? msl * (msl + 1) / 2 + 12 * msl : 0;
+  int fpre = fsz;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(fpre, o, 64);
+    if (lane >= o) fpre += v;
+  }
+  const int ftot = __shfl(fpre, N - 1, 64);
+  if (ftot > FS) {
+    finish_rejected(CMPC_TOO_LARGE);
+    return;
+  }
   if (lane < N) {
     S.sb[lane] = sbl;
     S.cb[lane] = 3 * (incl - nsl);
+    S.foff[lane] = fpre - fsz;
   }
   if (lane == 0) S.cb[N] = 3 * nt;
+  if (lane < 12) {
+    S.wf2[lane] = T(2.0 * M->Wf[lane]);
+    S.wr2[lane] = T(2.0 * M->Wr[lane]);
+  }
   wsync();
   // triple table, lever arms (stance_point, cmpc_device.hpp) and the Theta rows of A_k
   for (int e = lane; e < NL * N; e += 64) {
@@ -223,6 +281,7 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) u[c][d] = T(0);
 
+  RIC_STAMP(0);
   // ---- H u + g at the start point (u = 0): rollout of the 13 states and the adjoint sweep (oracle ric_grad)
   T hug[TPL][3];
   {
@@ -335,6 +394,7 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     wsync();
   }
 
+  RIC_STAMP(1);
   // ---- IPM state: pyramid rows of each triple, slacks clipped at THR0, lam = mu0 / t
   T tl[TPL][5], tu[TPL][5], ll[TPL][5], lu[TPL][5];
 #pragma unroll
@@ -350,11 +410,13 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     }
   }
   const int m = 5 * nt;
-  T* scr = A.scratch + (size_t)q * A.scr_stride;
   const int hh = lane >> 5, jj = lane & 31;
   const bool colv = jj < ZS;
 
-  // ---- Riccati factorisation of the Newton matrix (blocks in S.blk); returns false on a NaN pivot
+  // ---- Riccati factorisation of the Newton matrix (blocks in S.blk); returns false on a NaN pivot. The factors of
+  //      stage k stay in LDS (S.fac + S.foff[k], compact slot order): Li packed lower [m (m + 1) / 2], then the state
+  //      columns of Y [m][12]. The previous-force columns of Y are not stored: St has one entry -2 Wr there (same
+  //      slot, leg in stance at k - 1 and k), so Y[.][12 + c] = -2 Wr_c Li[.][c].
   auto factor = [&]() -> bool {
     T Pc[12];
 #pragma unroll
@@ -363,8 +425,10 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     for (int k = N - 1; k >= 0; --k) {
       const int Sk = S.sb[k];
       const int Sp = k > 0 ? S.sb[k - 1] : 0;
-      T* Lik = scr + (size_t)k * RS;
-      T* Yk = Lik + 144;
+      const int Sc = Sk & Sp;
+      const int m = 3 * __popc(Sk);
+      T* F = S.fac + S.foff[k];
+      T* Yx = F + m * (m + 1) / 2;
       // columns c (0..2) and Theta (9..11) of P, rows 0..11, for A~'P A~
       if (hh == 0 && (jj < 3 || (jj >= 9 && jj < 12))) {
         const int pc = jj < 3 ? jj : jj - 6;
@@ -372,7 +436,6 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
         for (int r = 0; r < 12; ++r) S.f.Pcol[pc][r] = Pc[r];
       }
       // 1. G = B~' P, column jj, rows = stance slots
-      T Gc[12];
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         if ((Sk >> l) & 1) {
@@ -384,17 +447,10 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
             const T wz = d == 0 ? -ry : (d == 1 ? rx : T(0));
             const T xp = dtm * Pc[3 + d] + dt * (wx * Pc[6] + wy * Pc[7] + wz * Pc[8]);
             const T part = hh ? Pc[3 * l + d] : xp;
-            Gc[3 * l + d] = part + shfl_x32(part);
+            const T gv = part + shfl_x32(part);
+            if (hh == 0 && colv) S.f.G[3 * l + d][jj] = gv;
           }
-        } else {
-#pragma unroll
-          for (int d = 0; d < 3; ++d) Gc[3 * l + d] = T(0);
         }
-      }
-      if (hh == 0 && colv) {
-#pragma unroll
-        for (int s = 0; s < 12; ++s)
-          if ((Sk >> (s / 3)) & 1) S.f.G[s][jj] = Gc[s];
       }
       wsync();
       // 2. Rt = R_k + G B~: lane (slot a, leg b) forms Rt[a][3b .. 3b + 2]
@@ -416,7 +472,7 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
               // block (da, db): xx yy zz on the diagonal, xz / yz off it, xy = 0
               const T bv = da == db ? bk[da] : ((da + db == 2 && da != 1) ? bk[3] : ((da + db == 3) ? bk[4] : T(0)));
               v += bv;
-              if (da == db) v += T(2.0 * M->Wf[a] + (k >= 1 ? 2.0 * M->Wr[a] : 0.0));
+              if (da == db) v += S.wf2[a] + (k >= 1 ? S.wr2[a] : T(0));
             }
             S.f.Rt[a][3 * lb + db] = v;
           }
@@ -424,36 +480,35 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
       }
       wsync();
       // 3. Cholesky Rt = L L' and Li = L^-1, lane a < 12 holds row a
-      T R[12], Iv[12];
+      {
+        T R[12], Iv[12];
 #pragma unroll
-      for (int b = 0; b < 12; ++b) {
-        R[b] = (lane < 12 && ((Sk >> (b / 3)) & 1)) ? S.f.Rt[lane < 12 ? lane : 0][b] : T(0);
-        Iv[b] = lane == b ? T(1) : T(0);
-      }
-#pragma unroll
-      for (int p = 0; p < 12; ++p) {
-        if ((Sk >> (p / 3)) & 1) {
-          const T dp = readlane(R[p], p);
-          nanp |= dp != dp;
-          const T invs = pinv_sqrt(dp);
-          const T lap = lane > p ? R[p] * invs : T(0);
-#pragma unroll
-          for (int c = 0; c <= p; ++c) Iv[c] = lane == p ? Iv[c] * invs : Iv[c];
-#pragma unroll
-          for (int b = p + 1; b < 12; ++b)
-            if ((Sk >> (b / 3)) & 1) R[b] = fma(-lap, readlane(R[p], b) * invs, R[b]);
-#pragma unroll
-          for (int c = 0; c <= p; ++c)
-            if ((Sk >> (c / 3)) & 1) Iv[c] = fma(-lap, readlane(Iv[c], p), Iv[c]);
+        for (int b = 0; b < 12; ++b) {
+          R[b] = (lane < 12 && ((Sk >> (b / 3)) & 1)) ? S.f.Rt[lane < 12 ? lane : 0][b] : T(0);
+          Iv[b] = lane == b ? T(1) : T(0);
         }
-      }
-      if (lane < 12 && ((Sk >> (lane / 3)) & 1)) {
 #pragma unroll
-        for (int c = 0; c < 12; ++c) {
-          if ((Sk >> (c / 3)) & 1) {
-            S.f.Li[lane][c] = Iv[c];
-            Lik[lane * 12 + c] = Iv[c];
+        for (int p = 0; p < 12; ++p) {
+          if ((Sk >> (p / 3)) & 1) {
+            const T dp = readlane(R[p], p);
+            nanp |= dp != dp;
+            const T invs = pinv_sqrt(dp);
+            const T lap = lane > p ? R[p] * invs : T(0);
+#pragma unroll
+            for (int c = 0; c <= p; ++c) Iv[c] = lane == p ? Iv[c] * invs : Iv[c];
+#pragma unroll
+            for (int b = p + 1; b < 12; ++b)
+              if ((Sk >> (b / 3)) & 1) R[b] = fma(-lap, readlane(R[p], b) * invs, R[b]);
+#pragma unroll
+            for (int c = 0; c <= p; ++c)
+              if ((Sk >> (c / 3)) & 1) Iv[c] = fma(-lap, readlane(Iv[c], p), Iv[c]);
           }
+        }
+        if (lane < 12 && ((Sk >> (lane / 3)) & 1)) {
+          const int ap = cslot(Sk, lane);
+#pragma unroll
+          for (int c = 0; c < 12; ++c)
+            if (c <= lane && ((Sk >> (c / 3)) & 1)) F[ap * (ap + 1) / 2 + cslot(Sk, c)] = Iv[c];
         }
       }
       if (k == 0) break;
@@ -476,7 +531,7 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
               }
             } else if (jj < ZS) {
               const int sj = jj - 12;
-              if (sj == a && ((Sp >> (sj / 3)) & 1)) v = T(-2.0 * M->Wr[a]);
+              if (sj == a && ((Sp >> (sj / 3)) & 1)) v = -S.wr2[a];
             }
           }
           stc[a] = v;
@@ -485,20 +540,19 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
         for (int a = 0; a < 12; ++a) {
           T y = T(0);
           if ((Sk >> (a / 3)) & 1) {
+            const int ap = cslot(Sk, a);
+            const T* Lr = F + ap * (ap + 1) / 2;
 #pragma unroll
             for (int c = 0; c <= a; ++c)
-              if ((Sk >> (c / 3)) & 1) y = fma(S.f.Li[a][c], stc[c], y);
+              if ((Sk >> (c / 3)) & 1) y = fma(Lr[cslot(Sk, c)], stc[c], y);
           }
           Yc[a] = y;
         }
       }
-      if (hh == 0 && colv) {
+      if (hh == 0 && jj < 12) {
 #pragma unroll
         for (int a = 0; a < 12; ++a)
-          if ((Sk >> (a / 3)) & 1) {
-            S.f.Y[a][jj] = Yc[a];
-            Yk[a * ZS + jj] = Yc[a];
-          }
+          if ((Sk >> (a / 3)) & 1) Yx[cslot(Sk, a) * 12 + jj] = Yc[a];
       }
       wsync();
       // 5. P_k = Q_k + A~' P A~ - Y' Y (+ 2 Wr on the previous-force slots of the legs of step k - 1)
@@ -530,26 +584,32 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
       } else {
 #pragma unroll
         for (int r = 0; r < 12; ++r)
-          nc[r] = (hh == 1 && jj >= 12 && jj < ZS && r == jj - 12 && ((Sp >> (r / 3)) & 1)) ? T(2.0 * M->Wr[r]) : T(0);
+          nc[r] = (hh == 1 && jj >= 12 && jj < ZS && r == jj - 12 && ((Sp >> (r / 3)) & 1)) ? S.wr2[r] : T(0);
       }
+      // rows of Y: state rows from Yx (hh = 0), previous-force rows -2 Wr_r Li[.][r] (hh = 1, legs of S_k and S_k-1)
 #pragma unroll
       for (int a = 0; a < 12; ++a) {
         if ((Sk >> (a / 3)) & 1) {
           const T ya = Yc[a];
+          const int ap = cslot(Sk, a);
 #pragma unroll
-          for (int r = 0; r < 12; ++r) nc[r] = fma(-S.f.Y[a][12 * hh + r], ya, nc[r]);
+          for (int r = 0; r < 12; ++r) {
+            const bool upv = ((Sc >> (r / 3)) & 1) && r <= a;
+            const int ad = hh == 0 ? m * (m + 1) / 2 + ap * 12 + r : ap * (ap + 1) / 2 + (upv ? cslot(Sk, r) : 0);
+            const T sc = hh == 0 ? T(1) : (upv ? -S.wr2[r] : T(0));
+            nc[r] = fma(-(F[ad] * sc), ya, nc[r]);
+          }
         }
       }
 #pragma unroll
       for (int r = 0; r < 12; ++r) Pc[r] = colv ? nc[r] : T(0);
       wsync();
     }
-    __threadfence_block();
     wsync();
     return !__any(nanp);
   };
 
-  // ---- solve (H + C' Sigma C + reg I) x = b, b and x in the triple lanes' registers
+  // ---- solve (H + C' Sigma C + reg I) x = b, b and x in the triple lanes' registers, with the stage factors in LDS
   auto solve = [&](T (&bx)[TPL][3]) {
 #pragma unroll
     for (int c = 0; c < TPL; ++c)
@@ -562,12 +622,15 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     for (int k = N - 1; k >= 0; --k) {
       const int Sk = S.sb[k];
       const int Sp = k > 0 ? S.sb[k - 1] : 0;
-      const T* Lik = scr + (size_t)k * RS;
-      const T* Yk = Lik + 144;
+      const int Sc = Sk & Sp;
+      const int m = 3 * __popc(Sk);
+      const T* F = S.fac + S.foff[k];
+      const T* Yx = F + m * (m + 1) / 2;
       if (lane < ZS) S.vec[lane] = pv;
       wsync();
       T hva = T(0);
       const bool sa = lane < 12 && ((Sk >> (lane / 3)) & 1);
+      const int ap = sa ? cslot(Sk, lane) : 0;
       if (sa) {
         const int l = lane / 3, d = lane % 3;
         const T rx = T(S.lev[k][l][0]), ry = T(S.lev[k][l][1]), rz = T(S.lev[k][l][2]);
@@ -582,16 +645,17 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
       wsync();
       T wa = T(0);
       if (sa) {
+        const T* Lr = F + ap * (ap + 1) / 2;
 #pragma unroll
         for (int c = 0; c < 12; ++c)
-          if (c <= lane && ((Sk >> (c / 3)) & 1)) wa = fma(Lik[lane * 12 + c], S.hv[c], wa);
+          if (((Sk >> (c / 3)) & 1) && c <= lane) wa = fma(Lr[cslot(Sk, c)], S.hv[c], wa);
         S.wk[k][lane] = wa;
       }
       if (k == 0) break;
       if (lane < 12) S.hv2[lane] = wa;
       wsync();
       if (lane < ZS) {
-        T v;
+        T v = T(0);
         if (lane < 12) {
           v = S.vec[lane];
           if (lane >= 3 && lane < 6) v = fma(dt, S.vec[lane - 3], v);
@@ -600,13 +664,23 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
             const int cc = lane - 6;
             v += T(Mk[cc]) * S.vec[9] + T(Mk[3 + cc]) * S.vec[10] + T(Mk[6 + cc]) * S.vec[11];
           }
-        } else {
-          v = T(0);
-        }
 #pragma unroll
-        for (int a = 0; a < 12; ++a)
-          if ((Sk >> (a / 3)) & 1) v = fma(-Yk[a * ZS + lane], S.hv2[a], v);
-        if (lane >= 12 && !((Sp >> ((lane - 12) / 3)) & 1)) v = T(0);
+          for (int a = 0; a < 12; ++a)
+            if ((Sk >> (a / 3)) & 1) v = fma(-Yx[cslot(Sk, a) * 12 + lane], S.hv2[a], v);
+        } else {
+          const int c = lane - 12;
+          if ((Sc >> (c / 3)) & 1) {  // -(Y'w)[12 + c] = 2 Wr_c sum_a Li[a][c] w_a
+            const int cp = cslot(Sk, c);
+            T acc = T(0);
+#pragma unroll
+            for (int a = 0; a < 12; ++a)
+              if (((Sk >> (a / 3)) & 1) && a >= c) {
+                const int apa = cslot(Sk, a);
+                acc = fma(F[apa * (apa + 1) / 2 + cp], S.hv2[a], acc);
+              }
+            v = S.wr2[c] * acc;
+          }
+        }
         pv = v;
       }
       wsync();
@@ -616,17 +690,26 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     T zv = T(0);
     for (int k = 0; k < N; ++k) {
       const int Sk = S.sb[k];
-      const T* Lik = scr + (size_t)k * RS;
-      const T* Yk = Lik + 144;
+      const int Sp = k > 0 ? S.sb[k - 1] : 0;
+      const int Sc = Sk & Sp;
+      const int m = 3 * __popc(Sk);
+      const T* F = S.fac + S.foff[k];
+      const T* Yx = F + m * (m + 1) / 2;
       if (lane < ZS) S.vec[lane] = zv;
       wsync();
       const bool sa = lane < 12 && ((Sk >> (lane / 3)) & 1);
+      const int ap = sa ? cslot(Sk, lane) : 0;
       T ya = T(0);
       if (sa) {
         ya = S.wk[k][lane];
         if (k > 0) {
+          const T* Yr = Yx + ap * 12;
 #pragma unroll
-          for (int j = 0; j < ZS; ++j) ya = fma(Yk[lane * ZS + j], S.vec[j], ya);
+          for (int j = 0; j < 12; ++j) ya = fma(Yr[j], S.vec[j], ya);
+          const T* Lr = F + ap * (ap + 1) / 2;
+#pragma unroll
+          for (int c = 0; c < 12; ++c)
+            if (((Sc >> (c / 3)) & 1) && c <= lane) ya = fma(-S.wr2[c] * Lr[cslot(Sk, c)], S.vec[12 + c], ya);
         }
       }
       if (lane < 12) S.hv[lane] = ya;
@@ -635,7 +718,10 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
       if (sa) {
 #pragma unroll
         for (int p = 0; p < 12; ++p)
-          if (p >= lane && ((Sk >> (p / 3)) & 1)) va = fma(-Lik[p * 12 + lane], S.hv[p], va);
+          if (((Sk >> (p / 3)) & 1) && p >= lane) {
+            const int pp = cslot(Sk, p);
+            va = fma(-F[pp * (pp + 1) / 2 + ap], S.hv[p], va);
+          }
         const int l = lane / 3, d = lane % 3;
         const int t = S.cb[k] / 3 + __popc(Sk & ((1 << l) - 1));
         S.bs[3 * t + d] = va;
@@ -709,7 +795,9 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
         du[c][d] = rhs[c][d];
       }
     }
+    RIC_STAMP(4);
     solve(du);
+    RIC_STAMP(3);
 #pragma unroll
     for (int c = 0; c < TPL; ++c) {
       T cdu[5];
@@ -824,10 +912,12 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
       }
     }
     wsync();
+    RIC_STAMP(4);
     if (!factor()) {
       status = CMPC_NAN_SOL;
       break;
     }
+    RIC_STAMP(2);
     // slack residuals again (not kept across the factorisation: registers)
 #pragma unroll
     for (int c = 0; c < TPL; ++c) {
@@ -914,6 +1004,15 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
     }
   }
 
+  RIC_STAMP(4);
+#ifdef CMPC_RIC_STAMPS
+  if (A.stats && lane == 0) {
+    double* o = A.stats + (size_t)q * A.stats_cap * CMPC_STAT_COLS;
+    for (int k = 0; k < 5; ++k) o[k] = (double)rst_[k];
+    o[5] = (double)(ric::memtime() - rst0_);
+    o[6] = (double)it;
+  }
+#endif
   // ---- outputs: condensed u, status, iterations, residuals, (direct) the caller's [N][4][3] forces
   bool fin = true;
 #pragma unroll
@@ -961,7 +1060,7 @@ __device__ __forceinline__ void ric_body(const RicArgs<T>& A, const int q) {
   }
 }
 
-template <typename T, int TPL, int NR, int WPE>
+template <typename T, int TPL, int NR, int FS, int WPE>
 __global__ __launch_bounds__(64, WPE) void k_ric(RicArgs<T> A) {
   int q = (int)blockIdx.x;
   if (A.qlist) {  // class lists of the fused path: list 1 then list 2; the surplus workgroups exit
@@ -971,7 +1070,7 @@ __global__ __launch_bounds__(64, WPE) void k_ric(RicArgs<T> A) {
     else return;
     if ((unsigned)q >= gridDim.x) return;
   }
-  ric_body<T, TPL, NR>(A, q);
+  ric_body<T, TPL, NR, FS>(A, q);
 }
 
 }  // namespace cmpc

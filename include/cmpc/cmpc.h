@@ -145,7 +145,7 @@ int cmpc_ctx_fused(const cmpc_ctx* ctx);
  *                       stage-wise kernel (Riccati Newton solves over the horizon, no condensing, HPIPM's method);
  *                       2: every cold-start QP is (one launch). Results agree with the condensed path to rounding,
  *                       not bit for bit (a different factorisation of the same Newton systems). Needs N <= 21; 1 needs
- *                       CMPC_PATH_FUSED64 = 1. The first non-zero value allocates the stage-factor scratch.
+ *                       CMPC_PATH_FUSED64 = 1.
  * cmpc_set_path returns CMPC_ERR_ARG for an unknown option or a value out of range (0 / 1; 0 / 1 / 2 for
  * CMPC_PATH_RICCATI); cmpc_get_path returns the current value or CMPC_ERR_ARG. */
 enum cmpc_path_option { CMPC_PATH_FUSED64 = 0, CMPC_PATH_FUSED128 = 1, CMPC_PATH_DIRECT = 2, CMPC_PATH_RICCATI = 3 };
@@ -243,7 +243,10 @@ int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double*
  * on the device by condensing the cost and the constraint rows to U-space and a range-space KKT solve (Cholesky of H
  * and of the Schur complement E H^-1 E'). Redundant consistent rows are dropped; status CMPC_INCONS_EQ when the rows
  * cannot all be met (|E U - f| > 1e-8 of the data scale), CMPC_NAN_SOL when H is not positive definite or the
- * solution is non-finite. nc == NULL is CMPC_ERR_ARG (use cmpc_ocp_solve_batch_host). */
+ * solution is non-finite. nc == NULL is CMPC_ERR_ARG (use cmpc_ocp_solve_batch_host).
+ * Status parity: HPIPM's OCP IPM treats lg = ug rows as two-sided inequalities and, given inconsistent rows, stops
+ * at MAX_ITER or MIN_STEP rather than INCONS_EQ; this direct solve detects the inconsistency and says so (parity of
+ * that status unpinned: HPIPM is not available here). */
 size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* nc);
 int cmpc_ocp_solve_batch_eq_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0,
                                  const double* rec, const double* crec, double* x, double* u, int* status);
