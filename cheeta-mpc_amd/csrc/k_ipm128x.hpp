@@ -62,8 +62,14 @@
 #define X_STAMP_STORE(ptr, q) (void)0
 #endif
 
+// fp32 elimination bulk on packed FMAs (row_update2); 0 selects the DPP-FMA form (lab A/B builds only)
+#ifndef CMPC_PK128
+#define CMPC_PK128 1
+#endif
+
 namespace cmpc {
 namespace ipm128x {
+constexpr bool PACKED = CMPC_PK128 != 0;
 
 __device__ __forceinline__ unsigned long long memtime() {
   unsigned long long t;
@@ -613,6 +619,30 @@ __device__ __forceinline__ void ipm128x_body(const IpmArgs<T>& a, const Condense
     // register row rho by the pair (source columns tp, tq of register chunk 0): pass p then pass q
     auto row_update2 = [&](auto rho_, auto tp_) {
       constexpr int rho = decltype(rho_)::value, tp = decltype(tp_)::value, tq = tp + 1;
+      if constexpr (sizeof(T) == 4 && PACKED) {
+        // fp32: the row multiplier K[i][p] is broadcast once into a register (v_mov_b32_dpp row_newbcast) and the 8
+        // column chunks are updated as 4 packed pairs (v_pk_fma_f32, multiplier in both halves): 2 + 8 instructions
+        // per register row and pair instead of 16 DPP FMAs (lab/micro/f32_issue.hip: 23.8 vs 10.9-15.3 FMA/clk per
+        // SIMD at 4 waves). Column p itself carries mp[0] = 0 in lane p, as in the DPP form.
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        auto pass = [&](auto tb_, const T (&mv)[8]) {
+          constexpr int tb = decltype(tb_)::value;
+          const float t = __builtin_bit_cast(
+              float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, K[rho * 8]), 0x150 + tb, 0xf, 0xf, false));
+          const f2 tt = {t, t};
+#pragma unroll
+          for (int cp = 0; cp < 4; ++cp) {
+            f2 k = {K[rho * 8 + 2 * cp], K[rho * 8 + 2 * cp + 1]};
+            const f2 mm = {mv[2 * cp], mv[2 * cp + 1]};
+            k = __builtin_elementwise_fma(tt, mm, k);
+            K[rho * 8 + 2 * cp] = k.x;
+            K[rho * 8 + 2 * cp + 1] = k.y;
+          }
+        };
+        pass(std::integral_constant<int, tp>{}, mp);
+        pass(std::integral_constant<int, tq>{}, mq);
+        return;
+      }
       dfma<tp, T>(K[rho * 8 + 1], K[rho * 8], mp[1]);
       sfor<2, 8>([&](auto c_) {
         constexpr int c = decltype(c_)::value;
