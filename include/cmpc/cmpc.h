@@ -67,8 +67,17 @@ enum cmpc_qp_status {
   CMPC_INCONS_EQ = 4,        /* inconsistent equality constraints (HpipmInterface path with constraints) */
   CMPC_INVALID_CONTACT = 5,  /* a horizon step has no stance leg: reference throws "mpc table invalid"
                                 (CentroidalMPC.cpp:328-330) */
-  CMPC_TOO_LARGE = 6         /* condensed size exceeds what this build's kernels support */
+  CMPC_TOO_LARGE = 6,        /* condensed size exceeds what this build's kernels support */
+  CMPC_INFEASIBLE_STEP = 7   /* cmpc_nlp_solve_batch: the step box of a later stance run's foothold is empty
+                                (des_foot_pos varies over the run by more than the box, CentroidalMPC.cpp:196-198) */
 };
+
+/* Foothold step box of the NLP (CentroidalMPC.cpp:30-31): step_lb <= foot_pos - des_foot_pos <= step_ub at every node
+ * 1..N (CentroidalMPC.cpp:196-198). */
+#define CMPC_STEP_LB_XY (-0.2)
+#define CMPC_STEP_LB_Z (-0.1)
+#define CMPC_STEP_UB_XY 0.2
+#define CMPC_STEP_UB_Z 0.1
 
 enum cmpc_precision { CMPC_F64 = 0, CMPC_F32 = 1 };
 

@@ -47,6 +47,7 @@ void oracle_consts_init(const cmpc_model* m, oracle_consts* c) {
     for (int d = 0; d < 3; ++d) {
       c->Wf[3 * i + d] = w[9 + 3 * L + 3 * i + d];
       c->Wr[3 * i + d] = w[9 + 6 * L + 3 * i + d];
+      c->Wp[3 * i + d] = w[9 + 3 * i + d];
     }
   }
   for (int k = 0; k <= m->N && k < 64; ++k) {
@@ -1253,6 +1254,56 @@ void oracle_gait_contact(const cmpc_gait* g, const int* leg_map, double t_start,
  * may be NULL. Returns the cost. Floating-point order is the one k_sqp_step follows. */
 double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
                                const uint8_t* contact, const double* u, double* x, double* lin) {
+  return oracle_nlp_rollout_cost_feet(c, x0, xref, foot, contact, u, NULL, x, lin);
+}
+
+/* Lever-arm point of stance leg i at step k: oracle_stance_point, plus the foothold offset D [N][L][3] of its run
+ * when the run is a later one (D indexed by the run's first step; D = NULL: frozen footholds). */
+static void lever_point(const double* foot, const uint8_t* contact, const double* D, int N, int L, int k, int i,
+                        double p[3]) {
+  oracle_stance_point(foot, contact, N, L, k, i, p);
+  if (!D) return;
+  int s = k;
+  while (s > 0 && contact[(s - 1) * L + i]) --s;
+  if (s == 0) return;
+  const double* dl = D + ((size_t)s * L + i) * 3;
+  p[0] = p[0] + dl[0];
+  p[1] = p[1] + dl[1];
+  p[2] = p[2] + dl[2];
+}
+
+/* Foot tracking cost of the later stance runs (CentroidalMPC.cpp:218-221 over the run's nodes s..e+1; nodes of the
+ * first run are pinned to the current foot and free swing nodes track exactly, so neither depends on a decision
+ * variable): sum_i sum_runs sum_j sum_d Wp (pbar + D - des_j)^2, legs outer, runs by first step, nodes, components.
+ * With dD != NULL returns instead the directional derivative sum 2 Wp (pbar + D - des_j) dD. */
+static double foot_cost(const oracle_consts* c, const double* foot, const uint8_t* contact, const double* D,
+                        const double* dD) {
+  const int N = c->N, L = c->L;
+  double J = 0.0;
+  for (int i = 0; i < L; ++i)
+    for (int s = 1; s < N; ++s) {
+      if (!contact[s * L + i] || contact[(s - 1) * L + i]) continue;
+      int e = s;
+      while (e + 1 < N && contact[(e + 1) * L + i]) ++e;
+      double pb[3];
+      oracle_stance_point(foot, contact, N, L, s, i, pb);
+      const double* dl = D + ((size_t)s * L + i) * 3;
+      for (int j = s; j <= e + 1; ++j)
+        for (int d = 0; d < 3; ++d) {
+          const double ed = (pb[d] + dl[d]) - foot[((size_t)j * L + i) * 3 + d];
+          if (dD)
+            J += 2.0 * c->Wp[3 * i + d] * ed * dD[((size_t)s * L + i) * 3 + d];
+          else
+            J += c->Wp[3 * i + d] * ed * ed;
+        }
+    }
+  return J;
+}
+
+/* Same, with the later runs' footholds as decision variables: pbar + D (D [N][L][3] by run start, NULL: frozen) in
+ * the lever arm and the foot tracking cost of the later runs added after the rollout. */
+double oracle_nlp_rollout_cost_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                                    const uint8_t* contact, const double* u, const double* D, double* x, double* lin) {
   const int N = c->N, L = c->L;
   const double dt = c->dt;
   double xs[NX], xn[NX];
@@ -1267,7 +1318,7 @@ double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const d
       if (!contact[k * L + i]) continue;
       ++ns;
       double p[3];
-      oracle_stance_point(foot, contact, N, L, k, i, p);
+      lever_point(foot, contact, D, N, L, k, i, p);
       const double* f = uk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
       F[0] += f[0];
@@ -1319,6 +1370,7 @@ double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const d
       J += 0.5 * c->qdiag[k + 1][sI] * e * e;
     }
   }
+  if (D) J += foot_cost(c, foot, contact, D, NULL);
   return J;
 }
 
@@ -1328,6 +1380,14 @@ double oracle_nlp_rollout_cost(const oracle_consts* c, const double* x0, const d
  * Jacobian of the step of oracle_nlp_rollout_cost at (x_k, u_k); floating-point order is the one k_sqp_step follows. */
 void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
                         const uint8_t* contact, const double* u, const double* du, double* dxnorm, double* metric) {
+  oracle_nlp_linstep_feet(c, x0, xref, foot, contact, u, NULL, du, NULL, dxnorm, metric);
+}
+
+/* Same at the iterate (u, D) along (du, dD): d[(p - c) x f] = (p - c) x df - (dc - dp) x f, and the foot tracking
+ * cost's derivative added to the metric after the rollout (D, dD NULL: frozen footholds). */
+void oracle_nlp_linstep_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                             const uint8_t* contact, const double* u, const double* D, const double* du,
+                             const double* dD, double* dxnorm, double* metric) {
   const int N = c->N, L = c->L;
   const double dt = c->dt;
   double xs[NX], xn[NX], dx[NX], dn[NX];
@@ -1342,8 +1402,14 @@ void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* 
     for (int i = 0; i < L; ++i) {
       if (!contact[k * L + i]) continue;
       ++ns;
-      double p[3];
-      oracle_stance_point(foot, contact, N, L, k, i, p);
+      double p[3], dp[3] = {0.0, 0.0, 0.0};
+      lever_point(foot, contact, D, N, L, k, i, p);
+      if (dD) {
+        int s = k;
+        while (s > 0 && contact[(s - 1) * L + i]) --s;
+        if (s > 0)
+          for (int d = 0; d < 3; ++d) dp[d] = dD[((size_t)s * L + i) * 3 + d];
+      }
       const double* f = uk + 3 * i;
       const double* df = duk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
@@ -1356,10 +1422,11 @@ void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* 
       dF[0] += df[0];
       dF[1] += df[1];
       dF[2] += df[2];
-      /* d[(p - c) x f] = (p - c) x df - dc x f */
-      dT[0] += (ry * df[2] - rz * df[1]) - (dx[1] * f[2] - dx[2] * f[1]);
-      dT[1] += (rz * df[0] - rx * df[2]) - (dx[2] * f[0] - dx[0] * f[2]);
-      dT[2] += (rx * df[1] - ry * df[0]) - (dx[0] * f[1] - dx[1] * f[0]);
+      /* d[(p - c) x f] = (p - c) x df - (dc - dp) x f */
+      const double q0 = dx[0] - dp[0], q1 = dx[1] - dp[1], q2 = dx[2] - dp[2];
+      dT[0] += (ry * df[2] - rz * df[1]) - (q1 * f[2] - q2 * f[1]);
+      dT[1] += (rz * df[0] - rx * df[2]) - (q2 * f[0] - q0 * f[2]);
+      dT[2] += (rx * df[1] - ry * df[0]) - (q0 * f[1] - q1 * f[0]);
     }
     (void)T;
     /* dJ/du_k . du_k: force tracking and both force-rate terms that hold u_k */
@@ -1409,6 +1476,7 @@ void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* 
       ss += dx[sI] * dx[sI];
     }
   }
+  if (D && dD) mt += foot_cost(c, foot, contact, D, dD);
   *dxnorm = sqrt(ss);
   *metric = mt;
 }
@@ -1485,6 +1553,397 @@ int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_ite
   free(uq);
   free(ut);
   free(du);
+  free(lin);
+  return st;
+}
+
+/* ------------------------------------------------------------------------------ footholds as variables (§8 a5/f3) */
+/* The reference's NLP optimises foot_pos[i] at every node (CentroidalMPC.cpp:132-133) under the swing dynamics
+ * foot_pos+ = foot_pos + (1 - e) foot_vel dt (:93, :174-176), the pinning foot_pos(:,0) = current (:165-167), the step
+ * box step_lb <= foot_pos - des_foot_pos <= step_ub at nodes 1..N (:196-198, :30-31) and the tracking cost (:218-221).
+ * foot_vel is free and uncosted, so a swing node that starts no stance run tracks des exactly, a run that starts at
+ * step 0 stays at the current foot, and each LATER stance run (first step s >= 1 after a swing step, last stance step
+ * e) holds one free foothold p over its nodes s..e+1. It is parametrised as p = pbar + delta, pbar =
+ * oracle_stance_point (the mean of des over the nodes), so the tracking cost is sum_j Wp (pbar + delta - des_j)^2 and
+ * the box reads lo <= delta <= hi with lo_d = max_j (des_jd - pbar_d) + step_lb_d, hi_d = min_j (...) + step_ub_d.
+ * D [N][L][3] holds delta at index (s, i) of each later run (other entries unused, kept 0). */
+
+static const double STEP_LB[3] = {CMPC_STEP_LB_XY, CMPC_STEP_LB_XY, CMPC_STEP_LB_Z};
+static const double STEP_UB[3] = {CMPC_STEP_UB_XY, CMPC_STEP_UB_XY, CMPC_STEP_UB_Z};
+
+/* 1 when step s starts a later stance run of leg i; *e = its last stance step. */
+static int later_start(const uint8_t* contact, int N, int L, int s, int i, int* e) {
+  if (s < 1 || s >= N || !contact[s * L + i] || contact[(s - 1) * L + i]) return 0;
+  int ee = s;
+  while (ee + 1 < N && contact[(ee + 1) * L + i]) ++ee;
+  if (e) *e = ee;
+  return 1;
+}
+
+int oracle_foot_box(const double* foot, const uint8_t* contact, int N, int L, int s, int i, double pbar[3],
+                    double lo[3], double hi[3], int* cnt) {
+  int e = 0;
+  if (!later_start(contact, N, L, s, i, &e)) return 0;
+  oracle_stance_point(foot, contact, N, L, s, i, pbar);
+  for (int d = 0; d < 3; ++d) {
+    double mx = -INFINITY, mn = INFINITY;
+    for (int j = s; j <= e + 1; ++j) {
+      const double v = foot[((size_t)j * L + i) * 3 + d] - pbar[d];
+      mx = v > mx ? v : mx;
+      mn = v < mn ? v : mn;
+    }
+    lo[d] = mx + STEP_LB[d];
+    hi[d] = mn + STEP_UB[d];
+  }
+  if (cnt) *cnt = e + 2 - s;
+  return 1;
+}
+
+/* Feasible start of the footholds: delta = clamp(0, lo, hi) for every later run (D [N][L][3], zeros elsewhere). */
+void oracle_feet_init(const oracle_consts* c, const double* foot, const uint8_t* contact, double* D) {
+  const int N = c->N, L = c->L;
+  memset(D, 0, sizeof(double) * (size_t)N * L * 3);
+  for (int s = 1; s < N; ++s)
+    for (int i = 0; i < L; ++i) {
+      double pb[3], lo[3], hi[3];
+      if (!oracle_foot_box(foot, contact, N, L, s, i, pb, lo, hi, NULL)) continue;
+      for (int d = 0; d < 3; ++d) D[((size_t)s * L + i) * 3 + d] = fmin(fmax(0.0, lo[d]), hi[d]);
+    }
+}
+
+/* The reference controller's foot_pos output [(N+1)][L][3] (:269-273) from D: node 0 and the first run's nodes the
+ * current foot, a later run's nodes pbar + delta, a free swing node des. */
+void oracle_feet_table(const oracle_consts* c, const double* foot, const uint8_t* contact, const double* D,
+                       double* out) {
+  const int N = c->N, L = c->L;
+  for (int j = 0; j <= N; ++j)
+    for (int i = 0; i < L; ++i) {
+      double* o = out + ((size_t)j * L + i) * 3;
+      const double* des = foot + ((size_t)j * L + i) * 3;
+      const int k = (j < N && contact[j * L + i]) ? j : ((j > 0 && contact[(j - 1) * L + i]) ? j - 1 : -1);
+      if (j == 0) {
+        o[0] = des[0], o[1] = des[1], o[2] = des[2];
+      } else if (k < 0) {
+        o[0] = des[0], o[1] = des[1], o[2] = des[2];
+      } else {
+        lever_point(foot, contact, D, N, L, k, i, o);
+      }
+    }
+}
+
+/* Condensed QP of the SQP with footholds, linearised at lin = (c_bar_k, F_bar_k) and at the iterate's per-leg forces
+ * ubar [N][L][3] and footholds D: variables in the device's order, for each step k and leg i the force triple of a
+ * stance (k, i) (tri_map k L + i) and then, when (k, i) starts a later run, its foothold triple (tri_map N L + k L + i,
+ * mu = 0, rows [-x, x, -y, y, z] bounded by the step box). Torque (p - c) x f linearised at (pbar + D, c_bar, f_bar):
+ * (pbar + D - c_bar) x f + delta x f_bar - D x f_bar - c x F_bar + c_bar x F_bar, so a foothold column acts at each
+ * step k of its run on the L rows with dt e_d x f_bar_ik, and b_k gains -dt sum D x f_bar_ik. Cost: the condensed
+ * state and force terms as oracle_condense_full_lin, plus 2 Wp cnt on the foothold diagonal and
+ * 2 Wp sum_j (pbar - des_j) in g. Status INVALID_CONTACT / TOO_LARGE as oracle_condense_lin, INFEASIBLE_STEP when a
+ * run's box is empty. */
+int oracle_condense_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, const double* lin, const double* ubar, const double* D, int ld,
+                         int* n_out, double* H, double* g, double* tri_mu, double* tri_lo, double* tri_hi,
+                         int* tri_map) {
+  const int N = c->N, L = c->L;
+  const double dt = c->dt;
+  *n_out = 0;
+  for (int k = 0; k < N; ++k) {
+    int ns = 0;
+    for (int i = 0; i < L; ++i) ns += contact[k * L + i] ? 1 : 0;
+    if (ns == 0) return CMPC_INVALID_CONTACT;
+  }
+  /* triple list */
+  int nt = 0;
+  int* code = (int*)malloc(sizeof(int) * (size_t)2 * N * L);
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < L; ++i) {
+      if (contact[k * L + i]) code[nt++] = k * L + i;
+      if (later_start(contact, N, L, k, i, NULL)) code[nt++] = N * L + k * L + i;
+    }
+  const int n = 3 * nt;
+  if (n > ld) {
+    free(code);
+    return CMPC_TOO_LARGE;
+  }
+  double flo[3 * 4 * 64], fhi[3 * 4 * 64];
+  for (int t = 0; t < nt; ++t) {
+    if (code[t] < N * L) continue;
+    const int s = (code[t] - N * L) / L, i = (code[t] - N * L) % L;
+    double pb[3];
+    oracle_foot_box(foot, contact, N, L, s, i, pb, flo + 3 * t, fhi + 3 * t, NULL);
+    for (int d = 0; d < 3; ++d)
+      if (!(flo[3 * t + d] <= fhi[3 * t + d])) {
+        free(code);
+        return CMPC_INFEASIBLE_STEP;
+      }
+  }
+  /* dynamics at the iterate: the force columns' lever arm pbar + D (a foot table whose later-run nodes hold it) */
+  double* ft = (double*)malloc(sizeof(double) * (size_t)(N + 1) * L * 3);
+  oracle_feet_table(c, foot, contact, D, ft);
+  double* A = (double*)malloc(sizeof(double) * N * NX * NX);
+  double* B = (double*)malloc(sizeof(double) * N * NX * NU);
+  double* bb = (double*)malloc(sizeof(double) * N * NX);
+  oracle_srbd_dynamics_lin(c, xref, ft, contact, lin, A, B, bb);
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < L; ++i) {
+      if (!contact[k * L + i]) continue;
+      int s = k;
+      while (s > 0 && contact[(s - 1) * L + i]) --s;
+      if (s == 0) continue;
+      const double* dl = D + ((size_t)s * L + i) * 3;
+      const double* f = ubar + (size_t)k * NU + 3 * i;
+      bb[k * NX + 6] -= dt * (dl[1] * f[2] - dl[2] * f[1]);
+      bb[k * NX + 7] -= dt * (dl[2] * f[0] - dl[0] * f[2]);
+      bb[k * NX + 8] -= dt * (dl[0] * f[1] - dl[1] * f[0]);
+    }
+  double* G = (double*)calloc((size_t)NX * n, sizeof(double));
+  double* G2 = (double*)malloc(sizeof(double) * NX * (n > 0 ? n : 1));
+  double xh[NX], xh2[NX], e[NX];
+  memcpy(xh, x0, sizeof(xh));
+  for (int a = 0; a < ld; ++a) {
+    for (int b = 0; b < ld; ++b) H[(size_t)a * ld + b] = 0.0;
+    g[a] = 0.0;
+  }
+  for (int k = 0; k < N; ++k) {
+    const double* Ak = A + (size_t)k * NX * NX;
+    const double* Bk = B + (size_t)k * NX * NU;
+    for (int r = 0; r < NX; ++r) {
+      for (int j = 0; j < n; ++j) {
+        double sacc = 0.0;
+        for (int t = 0; t < NX; ++t) sacc += Ak[r * NX + t] * G[t * n + j];
+        G2[r * n + j] = sacc;
+      }
+      double sacc = 0.0;
+      for (int t = 0; t < NX; ++t) sacc += Ak[r * NX + t] * xh[t];
+      xh2[r] = sacc + bb[k * NX + r];
+    }
+    /* input columns acting at step k */
+    for (int t = 0; t < nt; ++t) {
+      if (code[t] < N * L) {
+        if (code[t] / L != k) continue;
+        const int i = code[t] % L;
+        for (int r = 0; r < NX; ++r)
+          for (int d = 0; d < 3; ++d) G2[r * n + 3 * t + d] += Bk[r * NU + 3 * i + d];
+      } else {
+        const int s = (code[t] - N * L) / L, i = (code[t] - N * L) % L;
+        int ee = 0;
+        later_start(contact, N, L, s, i, &ee);
+        if (k < s || k > ee) continue;
+        const double* f = ubar + (size_t)k * NU + 3 * i;
+        /* dt e_d x f_bar: e_0 x f = (0, -fz, fy), e_1 x f = (fz, 0, -fx), e_2 x f = (-fy, fx, 0) */
+        G2[7 * n + 3 * t + 0] += dt * -f[2];
+        G2[8 * n + 3 * t + 0] += dt * f[1];
+        G2[6 * n + 3 * t + 1] += dt * f[2];
+        G2[8 * n + 3 * t + 1] += dt * -f[0];
+        G2[6 * n + 3 * t + 2] += dt * -f[1];
+        G2[7 * n + 3 * t + 2] += dt * f[0];
+      }
+    }
+    memcpy(G, G2, sizeof(double) * NX * n);
+    memcpy(xh, xh2, sizeof(xh));
+    const double* q = c->qdiag[k + 1];
+    for (int r = 0; r < NX; ++r) e[r] = q[r] * (xh[r] - xref[(k + 1) * NX + r]);
+    for (int a = 0; a < n; ++a) {
+      double ga = 0.0;
+      for (int r = 0; r < NX; ++r) ga += G[r * n + a] * e[r];
+      g[a] += ga;
+      for (int b = 0; b <= a; ++b) {
+        double sacc = 0.0;
+        for (int r = 0; r < NX; ++r) sacc += G[r * n + a] * q[r] * G[r * n + b];
+        H[(size_t)a * ld + b] += sacc;
+      }
+    }
+  }
+  /* force terms (R-bar, r-bar) and foothold tracking */
+  for (int t = 0; t < nt; ++t) {
+    if (code[t] < N * L) {
+      const int k = code[t] / L, i = code[t] % L;
+      int ns = 0;
+      for (int l = 0; l < L; ++l) ns += contact[k * L + l] ? 1 : 0;
+      const int nb = (k > 0) + (k < N - 1);
+      int tn = -1; /* triple of (k + 1, i) */
+      if (k + 1 < N && contact[(k + 1) * L + i])
+        for (int u2 = t + 1; u2 < nt; ++u2)
+          if (code[u2] == (k + 1) * L + i) tn = u2;
+      for (int d = 0; d < 3; ++d) {
+        const int j = 3 * i + d, a = 3 * t + d;
+        H[(size_t)a * ld + a] += 2.0 * c->Wf[j] + 2.0 * c->Wr[j] * (double)nb;
+        if (tn >= 0) H[(size_t)(3 * tn + d) * ld + a] += -2.0 * c->Wr[j];
+        if (d == 2) g[a] += -2.0 * c->Wf[j] * (c->mass * GRAV / (double)ns);
+      }
+    } else {
+      const int s = (code[t] - N * L) / L, i = (code[t] - N * L) % L;
+      double pb[3], lo[3], hi[3];
+      int cnt = 0, ee = 0;
+      oracle_foot_box(foot, contact, N, L, s, i, pb, lo, hi, &cnt);
+      later_start(contact, N, L, s, i, &ee);
+      for (int d = 0; d < 3; ++d) {
+        const int a = 3 * t + d;
+        double gs = 0.0;
+        for (int j = s; j <= ee + 1; ++j) gs += pb[d] - foot[((size_t)j * L + i) * 3 + d];
+        H[(size_t)a * ld + a] += 2.0 * c->Wp[3 * i + d] * (double)cnt;
+        g[a] += 2.0 * c->Wp[3 * i + d] * gs;
+      }
+    }
+  }
+  for (int a = 0; a < ld; ++a)
+    for (int b = a + 1; b < ld; ++b) H[(size_t)a * ld + b] = H[(size_t)b * ld + a];
+  for (int a = n; a < ld; ++a) H[(size_t)a * ld + a] = 1.0;
+  for (int t = 0; t < ld / 3; ++t) {
+    const int on = t < nt, foot_t = on && code[t] >= N * L;
+    if (tri_map) tri_map[t] = on ? code[t] : -1;
+    if (tri_mu) tri_mu[t] = (on && !foot_t) ? c->mu[code[t] % L] : 0.0;
+    for (int r = 0; r < 5; ++r) {
+      double lo = 0.0, hi = c->force_ub[r];
+      if (foot_t) {
+        const int d = r / 2 < 2 ? r / 2 : 2;
+        const int neg = (r == 0 || r == 2);
+        lo = neg ? -fhi[3 * t + d] : flo[3 * t + d];
+        hi = neg ? -flo[3 * t + d] : fhi[3 * t + d];
+      }
+      if (tri_lo) tri_lo[t * 5 + r] = lo;
+      if (tri_hi) tri_hi[t * 5 + r] = hi;
+    }
+  }
+  *n_out = n;
+  free(code);
+  free(ft);
+  free(A);
+  free(B);
+  free(bb);
+  free(G);
+  free(G2);
+  return CMPC_SUCCESS;
+}
+
+/* One QP of the SQP with footholds: oracle_condense_feet at (lin, u, D), IPM warm-started from (u, D) when
+ * s->warm_start, solution scattered back: u [N][L][3] (swing 0) and D (later-run entries). */
+int oracle_solve_one_feet(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                          const double* foot, const uint8_t* contact, const double* lin, double* u, double* D,
+                          int* iters) {
+  const int N = c->N, L = c->L, ld = NU * N;
+  double* H = (double*)malloc(sizeof(double) * ld * ld);
+  double* g = (double*)malloc(sizeof(double) * ld);
+  double* mu = (double*)malloc(sizeof(double) * ld);
+  double* lo = (double*)malloc(sizeof(double) * 5 * ld);
+  double* hi = (double*)malloc(sizeof(double) * 5 * ld);
+  double* uc = (double*)malloc(sizeof(double) * ld);
+  int* map = (int*)malloc(sizeof(int) * ld);
+  double* ub = (double*)malloc(sizeof(double) * N * NU);
+  double* Db = (double*)malloc(sizeof(double) * N * NU);
+  memcpy(ub, u, sizeof(double) * N * NU);
+  memcpy(Db, D, sizeof(double) * N * NU);
+  int n = 0, it = 0;
+  int st = oracle_condense_feet(c, x0, xref, foot, contact, lin, ub, Db, ld, &n, H, g, mu, lo, hi, map);
+  if (st == CMPC_SUCCESS) {
+    for (int t = 0; t < n / 3; ++t) {
+      const double* src = map[t] < N * L ? ub + map[t] * 3 : Db + (map[t] - N * L) * 3;
+      for (int d = 0; d < 3; ++d) uc[3 * t + d] = s->warm_start ? src[d] : 0.0;
+    }
+    st = oracle_qp_ipm(n, ld, H, g, mu, lo, hi, s, uc, NULL, NULL, &it, NULL);
+    memset(u, 0, sizeof(double) * N * NU);
+    memset(D, 0, sizeof(double) * N * NU);
+    for (int t = 0; t < n / 3; ++t) {
+      double* dst = map[t] < N * L ? u + map[t] * 3 : D + (map[t] - N * L) * 3;
+      for (int d = 0; d < 3; ++d) dst[d] = uc[3 * t + d];
+    }
+  }
+  if (iters) *iters = it;
+  free(H);
+  free(g);
+  free(mu);
+  free(lo);
+  free(hi);
+  free(uc);
+  free(map);
+  free(ub);
+  free(Db);
+  return st;
+}
+
+/* oracle_sqp_solve with the later runs' footholds as decision variables (the reference's NLP, CentroidalMPC.cpp:
+ * 132-133, 196-198, 218-221): U_0 = the QP at the reference linearisation (frozen footholds, where the foothold
+ * columns vanish: F_bar = 0), D_0 = oracle_feet_init; each iteration solves oracle_solve_one_feet at the iterate and
+ * line-searches (U, D) jointly, |du| over forces and footholds. feet [(N+1)][L][3] (may be NULL): oracle_feet_table of
+ * the final D. */
+int oracle_sqp_solve_feet(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
+                          const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
+                          double* D, double* feet, double* x, int* qp_iters, int* sqp_iters) {
+  const int N = c->N, nu = N * NU;
+  double* uq = (double*)malloc(sizeof(double) * nu);
+  double* ut = (double*)malloc(sizeof(double) * nu);
+  double* du = (double*)malloc(sizeof(double) * nu);
+  double* Dq = (double*)malloc(sizeof(double) * nu);
+  double* Dt = (double*)malloc(sizeof(double) * nu);
+  double* dD = (double*)malloc(sizeof(double) * nu);
+  double* lin = (double*)malloc(sizeof(double) * N * 6);
+  cmpc_settings sw = *s;
+  sw.warm_start = 0;
+  int it = 0, its = 0;
+  int st = oracle_solve_one_lin(c, &sw, x0, xref, foot, contact, NULL, u, NULL, &it);
+  oracle_feet_init(c, foot, contact, D);
+  int tot = it;
+  if (st == CMPC_SUCCESS) {
+    sw.warm_start = 1;
+    for (its = 0; its < sqp_iter_max; ++its) {
+      const double J0 = oracle_nlp_rollout_cost_feet(c, x0, xref, foot, contact, u, D, NULL, lin);
+      memcpy(uq, u, sizeof(double) * nu);
+      memcpy(Dq, D, sizeof(double) * nu);
+      const int sq = oracle_solve_one_feet(c, &sw, x0, xref, foot, contact, lin, uq, Dq, &it);
+      tot += it;
+      if (sq != CMPC_SUCCESS) {
+        st = sq;
+        break;
+      }
+      double dun2 = 0.0;
+      for (int i = 0; i < nu; ++i) {
+        du[i] = uq[i] - u[i];
+        dun2 += du[i] * du[i];
+      }
+      for (int i = 0; i < nu; ++i) {
+        dD[i] = Dq[i] - D[i];
+        dun2 += dD[i] * dD[i];
+      }
+      const double dun = sqrt(dun2);
+      double dxn = 0.0, metric = 0.0;
+      oracle_nlp_linstep_feet(c, x0, xref, foot, contact, u, D, du, dD, &dxn, &metric);
+      double alpha = 0.0, Jn = J0;
+      for (double a = 1.0; a >= SQP_ALPHA_MIN;) {
+        for (int i = 0; i < nu; ++i) {
+          ut[i] = u[i] + a * du[i];
+          Dt[i] = D[i] + a * dD[i];
+        }
+        const double Jt = oracle_nlp_rollout_cost_feet(c, x0, xref, foot, contact, ut, Dt, NULL, NULL);
+        const int ok = metric < 0.0 ? (Jt < J0 + SQP_ARMIJO * a * metric) : (Jt < J0);
+        if (ok) {
+          alpha = a;
+          Jn = Jt;
+          break;
+        }
+        a *= SQP_ALPHA_DECAY;
+        if (a * dxn < sqp_tol && a * dun < sqp_tol) break;
+      }
+      if (alpha > 0.0)
+        for (int i = 0; i < nu; ++i) {
+          u[i] = u[i] + alpha * du[i];
+          D[i] = D[i] + alpha * dD[i];
+        }
+      if (alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < sqp_tol && alpha * dun < sqp_tol)) {
+        ++its;
+        break;
+      }
+    }
+  }
+  if (x) oracle_nlp_rollout_cost_feet(c, x0, xref, foot, contact, u, D, x, NULL);
+  if (feet) oracle_feet_table(c, foot, contact, D, feet);
+  if (qp_iters) *qp_iters = tot;
+  if (sqp_iters) *sqp_iters = its;
+  free(uq);
+  free(ut);
+  free(du);
+  free(Dq);
+  free(Dt);
+  free(dD);
   free(lin);
   return st;
 }

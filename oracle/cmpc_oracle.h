@@ -29,6 +29,7 @@ typedef struct oracle_consts {
   double mu[CMPC_MAX_LEGS];
   double Wf[CMPC_NU]; /* force tracking weight per (leg, comp) */
   double Wr[CMPC_NU]; /* force-rate weight per (leg, comp) */
+  double Wp[CMPC_NU]; /* foot position tracking weight per (leg, comp), w[9 + 3i + c] (CentroidalMPC.cpp:218-221) */
   double qdiag[64][CMPC_NX]; /* 2*diag(Q_k), k = 0..N (k = 0 unused) */
   double force_ub[5];
 } oracle_consts;
@@ -69,6 +70,28 @@ void oracle_nlp_linstep(const oracle_consts* c, const double* x0, const double* 
 int oracle_sqp_solve(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
                      const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
                      double* x, int* qp_iters, int* sqp_iters);
+/* Footholds of the later stance runs as decision variables (CentroidalMPC.cpp:132-133, 196-198, 218-221; see
+ * cmpc_oracle.c): D [N][L][3] = foothold offsets from the run's mean des position, indexed by the run's first step. */
+double oracle_nlp_rollout_cost_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                                    const uint8_t* contact, const double* u, const double* D, double* x, double* lin);
+void oracle_nlp_linstep_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                             const uint8_t* contact, const double* u, const double* D, const double* du,
+                             const double* dD, double* dxnorm, double* metric);
+int oracle_foot_box(const double* foot, const uint8_t* contact, int N, int L, int s, int i, double pbar[3],
+                    double lo[3], double hi[3], int* cnt);
+void oracle_feet_init(const oracle_consts* c, const double* foot, const uint8_t* contact, double* D);
+void oracle_feet_table(const oracle_consts* c, const double* foot, const uint8_t* contact, const double* D,
+                       double* out);
+int oracle_condense_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, const double* lin, const double* ubar, const double* D, int ld,
+                         int* n_out, double* H, double* g, double* tri_mu, double* tri_lo, double* tri_hi,
+                         int* tri_map);
+int oracle_solve_one_feet(const oracle_consts* c, const cmpc_settings* s, const double* x0, const double* xref,
+                          const double* foot, const uint8_t* contact, const double* lin, double* u, double* D,
+                          int* iters);
+int oracle_sqp_solve_feet(const oracle_consts* c, const cmpc_settings* s, int sqp_iter_max, double sqp_tol,
+                          const double* x0, const double* xref, const double* foot, const uint8_t* contact, double* u,
+                          double* D, double* feet, double* x, int* qp_iters, int* sqp_iters);
 
 /* Full condensing over all 12N inputs (no elimination): Hfull [12N][12N], gfull [12N]. Returns 0 or
  * CMPC_INVALID_CONTACT. */

@@ -117,6 +117,19 @@ def lib():
         L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         L.oracle_stance_feet.argtypes = [C.c_int, C.c_int, d, u8, d]
         L.oracle_stance_feet.restype = None
+        L.oracle_nlp_rollout_cost_feet.argtypes = [C.c_void_p, d, d, d, u8, d, d, d, d]
+        L.oracle_nlp_rollout_cost_feet.restype = C.c_double
+        L.oracle_nlp_linstep_feet.argtypes = [C.c_void_p, d, d, d, u8, d, d, d, d, d, d]
+        L.oracle_nlp_linstep_feet.restype = None
+        L.oracle_foot_box.argtypes = [d, u8, C.c_int, C.c_int, C.c_int, C.c_int, d, d, d, i]
+        L.oracle_feet_init.argtypes = [C.c_void_p, d, u8, d]
+        L.oracle_feet_init.restype = None
+        L.oracle_feet_table.argtypes = [C.c_void_p, d, u8, d, d]
+        L.oracle_feet_table.restype = None
+        L.oracle_condense_feet.argtypes = [C.c_void_p, d, d, d, u8, d, d, d, C.c_int, i, d, d, d, d, d, i]
+        L.oracle_solve_one_feet.argtypes = [C.c_void_p, P(Settings), d, d, d, u8, d, d, d, i]
+        L.oracle_sqp_solve_feet.argtypes = [C.c_void_p, P(Settings), C.c_int, C.c_double, d, d, d, u8, d, d, d, d,
+                                            i, i]
         _lib = L
     return _lib
 
@@ -124,7 +137,8 @@ def lib():
 class _Consts(C.Structure):
     _fields_ = [("N", C.c_int), ("L", C.c_int), ("mass", C.c_double), ("dt", C.c_double),
                 ("inv_inertia", C.c_double * 9), ("mu", C.c_double * 4), ("Wf", C.c_double * 12),
-                ("Wr", C.c_double * 12), ("qdiag", (C.c_double * 13) * 64), ("force_ub", C.c_double * 5)]
+                ("Wr", C.c_double * 12), ("Wp", C.c_double * 12), ("qdiag", (C.c_double * 13) * 64),
+                ("force_ub", C.c_double * 5)]
 
 
 def _p(a, t=C.c_double):
@@ -267,6 +281,105 @@ def sqp_solve(model, settings, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol
     st = lib().oracle_sqp_solve(C.byref(c), C.byref(settings), sqp_iter_max, sqp_tol, _p(x0), _p(xref), _p(foot),
                                 _p(contact, C.c_uint8), _p(u), _p(x), C.byref(qi), C.byref(si))
     return u, x, st, qi.value, si.value
+
+
+def _f64(*a):
+    return tuple(np.ascontiguousarray(v, dtype=np.float64) for v in a)
+
+
+def nlp_rollout_cost_feet(model, x0, xref, foot, contact, u, D):
+    """nlp_rollout_cost with the later runs' footholds pbar + D (D [N,L,3] by run start): (J, x, lin)."""
+    N = model.N
+    c = consts(model)
+    x = np.zeros((N + 1, NX))
+    lin = np.zeros((N, 6))
+    x0, xref, foot, u, D = _f64(x0, xref, foot, u, D)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    J = lib().oracle_nlp_rollout_cost_feet(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u),
+                                           _p(D), _p(x), _p(lin))
+    return J, x, lin
+
+
+def nlp_linstep_feet(model, x0, xref, foot, contact, u, D, du, dD):
+    c = consts(model)
+    x0, xref, foot, u, D, du, dD = _f64(x0, xref, foot, u, D, du, dD)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    dxn, mt = C.c_double(0.0), C.c_double(0.0)
+    lib().oracle_nlp_linstep_feet(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u), _p(D),
+                                  _p(du), _p(dD), C.byref(dxn), C.byref(mt))
+    return dxn.value, mt.value
+
+
+def foot_box(foot, contact, s, i):
+    """(pbar, lo, hi, cnt) of the later run of leg i starting at step s, or None."""
+    N, L = contact.shape
+    foot = np.ascontiguousarray(foot, dtype=np.float64)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    pb, lo, hi, cnt = np.zeros(3), np.zeros(3), np.zeros(3), C.c_int(0)
+    ok = lib().oracle_foot_box(_p(foot), _p(contact, C.c_uint8), N, L, s, i, _p(pb), _p(lo), _p(hi), C.byref(cnt))
+    return (pb, lo, hi, cnt.value) if ok else None
+
+
+def feet_init(model, foot, contact):
+    c = consts(model)
+    foot = np.ascontiguousarray(foot, dtype=np.float64)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    D = np.zeros((model.N, NL, 3))
+    lib().oracle_feet_init(C.byref(c), _p(foot), _p(contact, C.c_uint8), _p(D))
+    return D
+
+
+def feet_table(model, foot, contact, D):
+    c = consts(model)
+    foot, D = _f64(foot, D)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    out = np.zeros((model.N + 1, NL, 3))
+    lib().oracle_feet_table(C.byref(c), _p(foot), _p(contact, C.c_uint8), _p(D), _p(out))
+    return out
+
+
+def condense_feet(model, x0, xref, foot, contact, lin, ubar, D, ld=None):
+    """Condensed QP of the SQP with footholds: (n, H, g, mu, lo, hi, tri_map, status), H [ld, ld]."""
+    N = model.N
+    ld = ld or 12 * N
+    c = consts(model)
+    H, g = np.zeros((ld, ld)), np.zeros(ld)
+    mu, lo, hi = np.zeros(ld // 3), np.zeros((ld // 3, 5)), np.zeros((ld // 3, 5))
+    mp = np.zeros(ld // 3, np.int32)
+    n = C.c_int(0)
+    x0, xref, foot, lin, ubar, D = _f64(x0, xref, foot, lin, ubar, D)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    st = lib().oracle_condense_feet(C.byref(c), _p(x0), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(lin),
+                                    _p(ubar), _p(D), ld, C.byref(n), _p(H), _p(g), _p(mu), _p(lo), _p(hi),
+                                    _p(mp, C.c_int))
+    return n.value, H, g, mu, lo, hi, mp, st
+
+
+def solve_one_feet(model, settings, x0, xref, foot, contact, lin, u, D):
+    """One foothold QP at (lin, u, D), warm-started from (u, D) when settings.warm_start: (u, D, status, iters)."""
+    c = consts(model)
+    x0, xref, foot, lin = _f64(x0, xref, foot, lin)
+    u, D = (np.array(v, dtype=np.float64) for v in (u, D))
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    it = C.c_int(0)
+    st = lib().oracle_solve_one_feet(C.byref(c), C.byref(settings), _p(x0), _p(xref), _p(foot),
+                                     _p(contact, C.c_uint8), _p(lin), _p(u), _p(D), C.byref(it))
+    return u, D, st, it.value
+
+
+def sqp_solve_feet(model, settings, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7):
+    """SQP with the later runs' footholds as variables: (u, D, feet [N+1,L,3], x, status, qp_iters, sqp_iters)."""
+    N = model.N
+    c = consts(model)
+    u, D = np.zeros((N, NL, 3)), np.zeros((N, NL, 3))
+    feet, x = np.zeros((N + 1, NL, 3)), np.zeros((N + 1, NX))
+    x0, xref, foot = _f64(x0, xref, foot)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    qi, si = C.c_int(0), C.c_int(0)
+    st = lib().oracle_sqp_solve_feet(C.byref(c), C.byref(settings), sqp_iter_max, sqp_tol, _p(x0), _p(xref),
+                                     _p(foot), _p(contact, C.c_uint8), _p(u), _p(D), _p(feet), _p(x), C.byref(qi),
+                                     C.byref(si))
+    return u, D, feet, x, st, qi.value, si.value
 
 
 def qp_ipm_stats(n, H, g, mu, lo, hi, settings, rows):
