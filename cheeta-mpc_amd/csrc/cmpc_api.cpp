@@ -50,7 +50,7 @@ struct cmpc_ctx {
   bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;    // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   int ric = 0;    // stage-wise (Riccati) kernel k_ric: 0 off, 1 the n > 64 classes of the fused path, 2 every QP
-  double *lin, *uj, *uq;
+  double *lin, *uj, *uq, *dj, *dq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
   double* res;
@@ -82,11 +82,11 @@ int ld_for(const cmpc_model& m) {
 }
 
 struct Layout {
-  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, qlist, qcount, lin, uj, uq, stq, itq, done, sqpi, qpi, cnt, res_scr,
-      res, total;
+  size_t H, g, mu, lo, hi, u, map, nvar, status, iters, qlist, qcount, lin, uj, uq, dj, dq, stq, itq, done, sqpi, qpi,
+      cnt, res_scr, res, total;
 };
 
-Layout layout(int ld, int precision, int B) {
+Layout layout(int ld, int precision, int B, int N) {
   const size_t es = precision == CMPC_F64 ? 8 : 4;
   const size_t nt = (size_t)(ld / 3);
   Layout L;
@@ -112,6 +112,8 @@ Layout layout(int ld, int precision, int B) {
   L.lin = take((size_t)B * MAXN * 6 * 8);
   L.uj = take((size_t)B * MAXN * NU * 8);
   L.uq = take((size_t)B * MAXN * NU * 8);
+  L.dj = take((size_t)B * N * NU * 8);  // cmpc_nlp_solve_batch: foothold offsets of the iterate and of the QP
+  L.dq = take((size_t)B * N * NU * 8);
   L.stq = take((size_t)B * sizeof(int));
   L.itq = take((size_t)B * sizeof(int));
   L.done = take((size_t)B * sizeof(int));
@@ -139,6 +141,7 @@ void derive_model(const cmpc_model& m, DevModel& d) {
     for (int c = 0; c < 3; ++c) {
       d.Wf[3 * i + c] = w[9 + 3 * L + 3 * i + c];
       d.Wr[3 * i + c] = w[9 + 6 * L + 3 * i + c];
+      d.Wp[3 * i + c] = w[9 + 3 * i + c];
     }
   }
   for (int k = 0; k <= m.N && k <= MAXN; ++k) {
@@ -201,6 +204,8 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.foot = foot;
   a.contact = contact;
   a.lin = nullptr;
+  a.ubar = nullptr;
+  a.dbar = nullptr;
   a.H = (T*)c->H;
   a.g = (T*)c->g;
   a.tri_mu = (T*)c->tri_mu;
@@ -255,13 +260,17 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
 // class's kernel dispatches only its own QPs first, and the IPM reuses the same lists (*lists = true).
 template <typename T>
 int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                   const uint8_t* contact, hipStream_t st, const double* lin, bool* lists) {
+                   const uint8_t* contact, hipStream_t st, const double* lin, bool* lists, const double* ubar,
+                   const double* dbar) {
   CondenseArgs<T> a = condense_args<T>(c, x0, xref, foot, contact);
   a.lin = lin;
+  a.ubar = ubar;
+  a.dbar = dbar;
   *lists = false;
-  const bool small = c->model.N <= CMPC_C64_MAXN;
+  // the one-wave condensing has no foothold columns: with footholds every QP goes through the workgroup kernel
+  const bool small = c->model.N <= CMPC_C64_MAXN && !dbar;
   int r = small ? launch_condense64<T>(a, B, st) : 0;
-  if (r == 0 && !small) r = launch_srbd_condense<T>(a, 128, B, st);  // n_lo = 0: classes 64 and 128
+  if (r == 0 && !small) r = launch_srbd_condense<T>(a, c->ld < 128 ? 64 : 128, B, st);  // n_lo = 0: classes 64, 128
   if (r != 0 || c->ld < 128) return r;
   if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
   *lists = true;
@@ -281,12 +290,13 @@ int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, con
 }
 
 int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                 const uint8_t* contact, hipStream_t st, const double* lin = nullptr, bool* lists = nullptr) {
+                 const uint8_t* contact, hipStream_t st, const double* lin = nullptr, bool* lists = nullptr,
+                 const double* ubar = nullptr, const double* dbar = nullptr) {
   bool dummy = false;
   if (!lists) lists = &dummy;
   int r;
-  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin, lists);
-  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin, lists);
+  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin, lists, ubar, dbar);
+  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin, lists, ubar, dbar);
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 
@@ -503,7 +513,7 @@ void cmpc_model_default(cmpc_model* m, int N) {
 
 size_t cmpc_memsize(const cmpc_model* model, int precision, int max_batch) {
   if (!model_ok(model) || max_batch <= 0) return 0;
-  return layout(ld_for(*model), precision, max_batch).total;
+  return layout(ld_for(*model), precision, max_batch, model->N).total;
 }
 
 int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int precision, int max_batch, void* dev_mem,
@@ -529,7 +539,7 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->fused128 = precision == CMPC_F32;
   c->direct = true;
   (void)hipGetDevice(&c->device);
-  const Layout L = layout(c->ld, precision, max_batch);
+  const Layout L = layout(c->ld, precision, max_batch, c->model.N);
   c->ws_bytes = L.total;
   if (dev_mem) {
     c->ws = (char*)dev_mem;
@@ -552,6 +562,8 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->status = (int*)(c->ws + L.status);
   c->iters = (int*)(c->ws + L.iters);
   c->lin = (double*)(c->ws + L.lin);
+  c->dj = (double*)(c->ws + L.dj);
+  c->dq = (double*)(c->ws + L.dq);
   c->uj = (double*)(c->ws + L.uj);
   c->uq = (double*)(c->ws + L.uq);
   c->stq = (int*)(c->ws + L.stq);
@@ -755,14 +767,21 @@ int cmpc_solve_batch_warm(cmpc_ctx* c, int B, const double* x0, const double* xr
   e.status_out = status;
   e.iters_ws = c->iters;
   e.iters_out = iters;
+  e.dq = nullptr;
   if (launch_expand(e, B, st) != 0) return CMPC_ERR_HIP;
   if (ev) HIP_OK(hipEventRecord(ev[3], st));
   return CMPC_OK;
 }
 
-int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                         const uint8_t* contact, int sqp_iter_max, double sqp_tol, double* u, double* x, int* status,
-                         int* qp_iters, int* sqp_iters, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// Shared SQP driver of cmpc_sqp_solve_batch (feet false) and cmpc_nlp_solve_batch (feet true: the later runs'
+// footholds are decision variables, dj/dq carry them, feet_out the foot_pos table).
+int sqp_run(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot, const uint8_t* contact,
+            int sqp_iter_max, double sqp_tol, double* u, double* x, int* status, int* qp_iters, int* sqp_iters,
+            void* stream, bool feet, double* feet_out) {
   if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !status || sqp_iter_max < 0 ||
       !(sqp_tol >= 0.0))
     return CMPC_ERR_ARG;
@@ -791,12 +810,17 @@ int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xre
   a.sqp_iters = c->sqpi;
   a.count = c->cnt;
   a.tol = sqp_tol;
+  a.dj = feet ? c->dj : nullptr;
+  a.dq = feet ? c->dq : nullptr;
+  a.feet = feet ? feet_out : nullptr;
   if (launch_sqp(0, a, B, st) != 0) return CMPC_ERR_HIP;
   for (int it = 0; it < sqp_iter_max; ++it) {
     bool lists = false;
-    r = run_condense(c, B, x0, xref, foot, contact, st, c->lin, &lists);
+    r = run_condense(c, B, x0, xref, foot, contact, st, c->lin, &lists, feet ? c->uj : nullptr,
+                     feet ? c->dj : nullptr);
     if (r != CMPC_OK) return r;
-    if (launch_pack_warm(c->uj, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B, st) != 0)
+    if (launch_pack_warm(c->uj, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B, st,
+                         feet ? c->dj : nullptr) != 0)
       return CMPC_ERR_HIP;
     r = run_ipm(c, B, st, 1, lists);
     if (r != CMPC_OK) return r;
@@ -817,6 +841,7 @@ int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xre
     e.status_out = c->stq;
     e.iters_ws = c->iters;
     e.iters_out = c->itq;
+    e.dq = feet ? c->dq : nullptr;
     if (launch_expand(e, B, st) != 0) return CMPC_ERR_HIP;
     if (launch_sqp(1, a, B, st) != 0) return CMPC_ERR_HIP;
     // early exit once every QP has converged (one 4-byte read-back per SQP iteration)
@@ -830,6 +855,25 @@ int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xre
   if (qp_iters) HIP_OK(hipMemcpyAsync(qp_iters, c->qpi, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
   if (sqp_iters) HIP_OK(hipMemcpyAsync(sqp_iters, c->sqpi, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
   return CMPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpc_sqp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, int sqp_iter_max, double sqp_tol, double* u, double* x, int* status,
+                         int* qp_iters, int* sqp_iters, void* stream) {
+  return sqp_run(c, B, x0, xref, foot, contact, sqp_iter_max, sqp_tol, u, x, status, qp_iters, sqp_iters, stream,
+                 false, nullptr);
+}
+
+int cmpc_nlp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                         const uint8_t* contact, int sqp_iter_max, double sqp_tol, double* u, double* feet,
+                         double* x, int* status, int* qp_iters, int* sqp_iters, void* stream) {
+  if (!feet) return CMPC_ERR_ARG;
+  return sqp_run(c, B, x0, xref, foot, contact, sqp_iter_max, sqp_tol, u, x, status, qp_iters, sqp_iters, stream,
+                 true, feet);
 }
 
 int cmpc_policy_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
@@ -985,6 +1029,33 @@ int cmpc_condense_batch(cmpc_ctx* c, int B, const double* x0, const double* xref
   if (launch_unpack_qp(c->H, c->g, c->nvar, c->precision, c->ld, H, g, B, st) != 0) return CMPC_ERR_HIP;
   HIP_OK(hipMemcpyAsync(n, c->nvar, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
   HIP_OK(hipMemcpyAsync(status, c->status, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  return CMPC_OK;
+}
+
+int cmpc_condense_lin_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                            const uint8_t* contact, const double* lin, const double* ubar, const double* dbar,
+                            double* H, double* g, int* n, int* status, int* tri_map, double* tri_lo, double* tri_hi,
+                            void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !H || !g || !n || !status || (dbar && (!ubar || !lin))) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int r = run_condense(c, B, x0, xref, foot, contact, st, lin, nullptr, ubar, dbar);
+  if (r != CMPC_OK) return r;
+  if (launch_unpack_qp(c->H, c->g, c->nvar, c->precision, c->ld, H, g, B, st) != 0) return CMPC_ERR_HIP;
+  HIP_OK(hipMemcpyAsync(n, c->nvar, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  HIP_OK(hipMemcpyAsync(status, c->status, (size_t)B * sizeof(int), hipMemcpyDeviceToDevice, st));
+  const size_t nt = (size_t)B * (c->ld / 3);
+  if (tri_map) HIP_OK(hipMemcpyAsync(tri_map, c->tri_map, nt * sizeof(int), hipMemcpyDeviceToDevice, st));
+  const void* src[2] = {c->tri_lo, c->tri_hi};
+  double* dst[2] = {tri_lo, tri_hi};
+  for (int k = 0; k < 2; ++k) {
+    if (!dst[k]) continue;
+    if (c->precision == CMPC_F64) {
+      HIP_OK(hipMemcpyAsync(dst[k], src[k], nt * 5 * 8, hipMemcpyDeviceToDevice, st));
+    } else if (launch_convert_f32_to_f64((const float*)src[k], dst[k], nt * 5, st) != 0) {
+      return CMPC_ERR_HIP;
+    }
+  }
   return CMPC_OK;
 }
 

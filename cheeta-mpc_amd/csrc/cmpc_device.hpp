@@ -25,6 +25,7 @@ struct DevModel {
   double mu[NL];
   double Wf[NU];             // force tracking weights   w[9+3L+3i+c]  (CentroidalMPC.cpp:223-225)
   double Wr[NU];             // force-rate weights       w[9+6L+3i+c]  (CentroidalMPC.cpp:227-231)
+  double Wp[NU];             // foot position weights    w[9+3i+c]     (CentroidalMPC.cpp:218-221)
   double qdiag[MAXN + 1][NX];// 2*diag(Q_k) incl. squared CoM-z weight (CentroidalMPC.cpp:203-210)
   double ub[5];              // pyramid row upper bounds (CentroidalMPC.cpp:182-183)
 };
@@ -120,6 +121,56 @@ __device__ __forceinline__ void stance_point(const double* foot, int N, int k, i
 __device__ __forceinline__ void stance_point(const double* foot, const uint8_t* ct, int N, int k, int leg,
                                              double p[3]) {
   stance_point(foot, N, k, leg, [ct](int kk, int l) { return ct[kk * NL + l] != 0; }, p);
+}
+
+// Footholds as decision variables (cmpc_nlp_solve_batch; oracle/cmpc_oracle.c oracle_foot_box & co.): a LATER stance
+// run of leg `leg` (first step s >= 1 after a swing step, last stance step e) holds one free foothold over its nodes
+// s..e+1, p = pbar + delta with pbar = stance_point (the mean of des over the nodes); D [N][NL][3] holds delta at
+// (s, leg). Step box of the NLP (CentroidalMPC.cpp:30-31, :196-198): lo_d = max_j (des_jd - pbar_d) + step_lb_d,
+// hi_d = min_j (des_jd - pbar_d) + step_ub_d over j = s..e+1.
+__device__ __forceinline__ double step_lb(int d) { return d < 2 ? CMPC_STEP_LB_XY : CMPC_STEP_LB_Z; }
+__device__ __forceinline__ double step_ub(int d) { return d < 2 ? CMPC_STEP_UB_XY : CMPC_STEP_UB_Z; }
+
+// First step of the stance run holding stance step k of leg (0: the pinned first run).
+template <typename StanceFn>
+__device__ __forceinline__ int run_start(int k, int leg, StanceFn st) {
+  int s = k;
+  while (s > 0 && st(s - 1, leg)) --s;
+  return s;
+}
+// 1 when step s starts a later run of leg; *e = its last stance step.
+template <typename StanceFn>
+__device__ __forceinline__ bool later_start(int N, int s, int leg, StanceFn st, int* e) {
+  if (s < 1 || s >= N || !st(s, leg) || st(s - 1, leg)) return false;
+  int ee = s;
+  while (ee + 1 < N && st(ee + 1, leg)) ++ee;
+  *e = ee;
+  return true;
+}
+// Box component d of the later run (s, leg) ending at e; pbar from stance_point.
+__device__ __forceinline__ void foot_box_d(const double* des, int s, int e, int leg, int d, const double* pbar,
+                                           double* lo, double* hi) {
+  double mx = -__builtin_inf(), mn = __builtin_inf();
+  for (int j = s; j <= e + 1; ++j) {
+    const double v = des[(j * NL + leg) * 3 + d] - pbar[d];
+    mx = v > mx ? v : mx;
+    mn = v < mn ? v : mn;
+  }
+  *lo = mx + step_lb(d);
+  *hi = mn + step_ub(d);
+}
+// Lever-arm point with the run's foothold offset: stance_point + D[s][leg] for a later run (D null: frozen).
+template <typename StanceFn>
+__device__ __forceinline__ void lever_point(const double* foot, const double* D, int N, int k, int leg, StanceFn st,
+                                            double p[3]) {
+  stance_point(foot, N, k, leg, st, p);
+  if (!D) return;
+  const int s = run_start(k, leg, st);
+  if (s == 0) return;
+  const double* dl = D + (s * NL + leg) * 3;
+  p[0] = p[0] + dl[0];
+  p[1] = p[1] + dl[1];
+  p[2] = p[2] + dl[2];
 }
 
 // Friction pyramid row rho of F(mu) applied to (fx, fy, fz)  (CentroidalMPC.cpp:186-190)

@@ -36,6 +36,13 @@ struct CondenseArgs {
   // lever arm becomes p_ik - c_bar_k and L+ gains dt F_bar_k x (c_k - c_bar_k) (Taylor expansion of the bilinear
   // dt sum_i e_ik (p_ik - c_k) x f_ik of CentroidalMPC.cpp:86)
   const double* lin;
+  // footholds as decision variables (cmpc_nlp_solve_batch; workgroup condensing only): dbar [B][N][NL][3] = the
+  // iterate's foothold offsets by run start (cmpc_device.hpp lever_point), ubar [B][N][12] = the iterate's forces.
+  // dbar != null adds one foothold triple per later stance run after the force triple of its first (step, leg):
+  // columns dt e_d x f_bar_ik on the L rows at each step of the run, mu 0, rows [-x, x, -y, y, z] in the step box,
+  // tri_map N L + s L + leg (oracle_condense_feet)
+  const double* ubar;
+  const double* dbar;
   T* H;
   T* g;
   T* tri_mu;
@@ -176,6 +183,7 @@ struct ExpandArgs {
   int* status_out;
   const int* iters_ws;
   int* iters_out;
+  double* dq;  // [B][N][L][3] foothold offsets of the foothold triples (tri_map >= N L), or null
 };
 int launch_expand(const ExpandArgs& a, int B, hipStream_t stream);
 
@@ -210,12 +218,17 @@ struct SqpArgs {
   int* sqp_iters;      // [B]
   int* count;          // [1] QPs not done (k_sqp_count)
   double tol;
+  // footholds as decision variables (cmpc_nlp_solve_batch), all null for cmpc_sqp_solve_batch
+  double* dj;          // [B][N][L][3] iterate's foothold offsets by run start (k_sqp_init: clamp(0, lo, hi))
+  const double* dq;    // [B][N][L][3] the QP's foothold offsets (k_expand ExpandArgs::dq)
+  double* feet;        // [B][N+1][L][3] foot_pos output (k_sqp_final) or null
 };
 int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream);  // 0 init, 1 step, 2 final, 3 count
 
 // warm start: scatter a previous solution u_init [B][N][L][3] into the condensed order of each QP (tri_map)
+// d_init [B][N][L][3] (or null): the foothold offsets for the foothold triples (tri_map >= N L)
 int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, const int* status, int precision,
-                     int ld, int N, void* u_ws, int B, hipStream_t stream);
+                     int ld, int N, void* u_ws, int B, hipStream_t stream, const double* d_init = nullptr);
 // receding-horizon shift of a solution: out[k] = in[min(k + shift, N - 1)] per QP
 int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, hipStream_t stream);
 

@@ -4,7 +4,7 @@
 
 namespace cmpc {
 
-template <typename T, int NMAX, int WAVES>
+template <typename T, int NMAX, int WAVES, bool FEET>
 __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a) {
   int q = blockIdx.x;
   if (a.qlist) {  // class list: this class's QPs first, the surplus workgroups exit
@@ -13,22 +13,26 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     if ((unsigned)q >= gridDim.x) return;  // grid = batch
   }
   if (a.n_lo > 0 && a.nvar[q] <= a.n_lo) return;  // finished (or rejected) by a smaller class
-  (void)srbd_condense_qp<T, NMAX, WAVES, false>(a, q, nullptr);
+  (void)srbd_condense_qp<T, NMAX, WAVES, false, FEET>(a, q, nullptr);
 }
 
 template <typename T>
 int launch_srbd_condense(const CondenseArgs<T>& a, int npad, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   if (npad > a.ld) return -1;
+  const bool feet = a.dbar != nullptr;  // foothold columns (cmpc_nlp_solve_batch): the FEET instantiations
   switch (npad) {
     case 64:
-      hipLaunchKernelGGL((k_srbd_condense<T, 64, 4>), dim3(B), dim3(256), 0, stream, a);
+      if (feet) hipLaunchKernelGGL((k_srbd_condense<T, 64, 4, true>), dim3(B), dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((k_srbd_condense<T, 64, 4, false>), dim3(B), dim3(256), 0, stream, a);
       break;
     case 128:
-      hipLaunchKernelGGL((k_srbd_condense<T, 128, 4>), dim3(B), dim3(256), 0, stream, a);
+      if (feet) hipLaunchKernelGGL((k_srbd_condense<T, 128, 4, true>), dim3(B), dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((k_srbd_condense<T, 128, 4, false>), dim3(B), dim3(256), 0, stream, a);
       break;
     case 256:  // 17 lower 16x16 tiles per wave; one thread per Bqp column in waves 0-3
-      hipLaunchKernelGGL((k_srbd_condense<T, 256, 8>), dim3(B), dim3(512), 0, stream, a);
+      if (feet) hipLaunchKernelGGL((k_srbd_condense<T, 256, 8, true>), dim3(B), dim3(512), 0, stream, a);
+      else hipLaunchKernelGGL((k_srbd_condense<T, 256, 8, false>), dim3(B), dim3(512), 0, stream, a);
       break;
     default:
       return -1;

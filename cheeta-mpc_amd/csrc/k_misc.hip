@@ -146,11 +146,16 @@ __device__ void expand_one(const ExpandArgs& a, int q) {
   const int n = st == CMPC_TOO_LARGE || st == CMPC_INVALID_CONTACT ? 0 : a.nvar[q];
   const T* uw = reinterpret_cast<const T*>(a.u_ws) + (size_t)q * ld;
   double* uo = a.u + (size_t)q * N * NU;
-  for (int i = tid; i < N * NU; i += blockDim.x) uo[i] = 0.0;
+  double* dqo = a.dq ? a.dq + (size_t)q * N * NU : nullptr;
+  for (int i = tid; i < N * NU; i += blockDim.x) {
+    uo[i] = 0.0;
+    if (dqo) dqo[i] = 0.0;
+  }
   __syncthreads();
   for (int t = tid; t < n / 3; t += blockDim.x) {
     const int kl = a.tri_map[(size_t)q * (ld / 3) + t];
-    for (int d = 0; d < 3; ++d) uo[kl * 3 + d] = (double)uw[3 * t + d];
+    double* dst = kl < N * L ? uo + kl * 3 : dqo + (kl - N * L) * 3;  // foothold triples only with a.dq
+    for (int d = 0; d < 3; ++d) dst[d] = (double)uw[3 * t + d];
   }
   if (tid == 0) {
     a.status_out[q] = st;
@@ -869,7 +874,8 @@ namespace cmpc {
 // thread per condensed variable slot; QPs rejected by the condensing (status != SUCCESS) are left alone.
 template <typename T>
 __global__ __launch_bounds__(256) void k_pack_warm(const double* u_init, const int* tri_map, const int* nvar,
-                                                   const int* status, int ld, int N, T* u_ws, int B) {
+                                                   const int* status, int ld, int N, T* u_ws, int B,
+                                                   const double* d_init) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long)B * ld) return;
   const int q = (int)(e / ld), i = (int)(e % ld);
@@ -877,23 +883,24 @@ __global__ __launch_bounds__(256) void k_pack_warm(const double* u_init, const i
   const int n = nvar[q];
   T v = T(0);
   if (i < n) {
-    const int km = tri_map[(size_t)q * (ld / 3) + i / 3];  // k * L + leg
-    v = (T)u_init[(size_t)q * N * NU + (size_t)km * 3 + i % 3];
+    const int km = tri_map[(size_t)q * (ld / 3) + i / 3];  // k * L + leg (N L + s L + leg: foothold)
+    v = km < N * NL ? (T)u_init[(size_t)q * N * NU + (size_t)km * 3 + i % 3]
+                    : (T)d_init[(size_t)q * N * NU + (size_t)(km - N * NL) * 3 + i % 3];
   }
   u_ws[e] = v;
 }
 
 int launch_pack_warm(const double* u_init, const int* tri_map, const int* nvar, const int* status, int precision,
-                     int ld, int N, void* u_ws, int B, hipStream_t stream) {
+                     int ld, int N, void* u_ws, int B, hipStream_t stream, const double* d_init) {
   if (B <= 0) return 0;
   const long total = (long)B * ld;
   const dim3 grid((unsigned)((total + 255) / 256));
   if (precision == CMPC_F64)
     hipLaunchKernelGGL((k_pack_warm<double>), grid, dim3(256), 0, stream, u_init, tri_map, nvar, status, ld, N,
-                       (double*)u_ws, B);
+                       (double*)u_ws, B, d_init);
   else
     hipLaunchKernelGGL((k_pack_warm<float>), grid, dim3(256), 0, stream, u_init, tri_map, nvar, status, ld, N,
-                       (float*)u_ws, B);
+                       (float*)u_ws, B, d_init);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

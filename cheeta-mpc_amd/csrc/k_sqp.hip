@@ -36,11 +36,47 @@ constexpr double SQP_COST_TOL = 1e-4;
 
 #pragma clang fp contract(off)
 
-// Nonlinear rollout + NLP cost of the inputs u0 + alpha (u1 - u0) (u1 may be null: alpha unused). Writes
-// lin [N][6] and x [(N+1)][13] when non-null. Mirrors oracle_nlp_rollout_cost operation for operation.
+// Foothold offset of the later run (s, leg) at the trial point D0 + alpha (D1 - D0) (D1 null: D0).
+__device__ __forceinline__ void trial_offset(const double* D0, const double* D1, double alpha, int s, int leg,
+                                             double o[3]) {
+  for (int d = 0; d < 3; ++d) {
+    const double a = D0[(s * NL + leg) * 3 + d];
+    o[d] = D1 ? a + alpha * (D1[(s * NL + leg) * 3 + d] - a) : a;
+  }
+}
+
+// Foot tracking cost of the later runs at the trial footholds D0 + alpha (D1 - D0), or (deriv) its derivative at D0
+// along dD = D1 - D0: oracle foot_cost, same loop order (legs, runs by first step, nodes, components).
+__device__ double foot_cost(const DevModel* M, const double* foot, const uint8_t* ct, const double* D0,
+                            const double* D1, double alpha, bool deriv) {
+  const int N = M->N;
+  auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
+  double J = 0.0;
+  for (int i = 0; i < NL; ++i)
+    for (int s = 1; s < N; ++s) {
+      int e = 0;
+      if (!later_start(N, s, i, st, &e)) continue;
+      double pb[3], dl[3];
+      stance_point(foot, N, s, i, st, pb);
+      trial_offset(D0, deriv ? nullptr : D1, alpha, s, i, dl);
+      for (int j = s; j <= e + 1; ++j)
+        for (int d = 0; d < 3; ++d) {
+          const double ed = (pb[d] + dl[d]) - foot[(j * NL + i) * 3 + d];
+          if (deriv)
+            J += 2.0 * M->Wp[3 * i + d] * ed * (D1[(s * NL + i) * 3 + d] - dl[d]);
+          else
+            J += M->Wp[3 * i + d] * ed * ed;
+        }
+    }
+  return J;
+}
+
+// Nonlinear rollout + NLP cost of the inputs u0 + alpha (u1 - u0) (u1 may be null: alpha unused) and, with footholds
+// (D0 non-null), the later runs' footholds D0 + alpha (D1 - D0) in the lever arm plus their tracking cost. Writes
+// lin [N][6] and x [(N+1)][13] when non-null. Mirrors oracle_nlp_rollout_cost_feet operation for operation.
 __device__ double rollout_cost(const DevModel* M, const double* x0, const double* xref, const double* foot,
                                const uint8_t* ct, const double* u0, const double* u1, double alpha, double* lin,
-                               double* xo) {
+                               double* xo, const double* D0 = nullptr, const double* D1 = nullptr) {
   const int N = M->N;
   const double dt = M->dt;
   double xs[NX], xn[NX];
@@ -66,6 +102,16 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
       ++ns;
       double p[3];
       stance_point(foot, ct, N, k, i, p);
+      if (D0) {
+        const int s0 = run_start(k, i, [ct](int kk, int l) { return ct[kk * NL + l] != 0; });
+        if (s0 > 0) {
+          double dl[3];
+          trial_offset(D0, D1, alpha, s0, i, dl);
+          p[0] = p[0] + dl[0];
+          p[1] = p[1] + dl[1];
+          p[2] = p[2] + dl[2];
+        }
+      }
       const double* f = uk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
       F[0] += f[0];
@@ -116,13 +162,16 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
       J += 0.5 * M->qdiag[k + 1][s] * e * e;
     }
   }
+  if (D0) J += foot_cost(M, foot, ct, D0, D1, alpha, false);
   return J;
 }
 
-// Linearised response of the rollout of u0 to du = u1 - u0 and the descent metric (MultipleShootingSolver.cpp:287-296):
-// mirrors oracle_nlp_linstep operation for operation. Returns |dx| (trajectoryNorm, :492-503) in dxn.
+// Linearised response of the rollout of u0 to du = u1 - u0 (and, with footholds, dD = D1 - D0) and the descent metric
+// (MultipleShootingSolver.cpp:287-296): mirrors oracle_nlp_linstep_feet operation for operation. Returns |dx|
+// (trajectoryNorm, :492-503) in dxn.
 __device__ double linstep_metric(const DevModel* M, const double* x0, const double* xref, const double* foot,
-                                 const uint8_t* ct, const double* u0, const double* u1, double* dxn) {
+                                 const uint8_t* ct, const double* u0, const double* u1, double* dxn,
+                                 const double* D0 = nullptr, const double* D1 = nullptr) {
   const int N = M->N;
   const double dt = M->dt;
   double xs[NX], xn[NX], dx[NX], dn[NX];
@@ -140,8 +189,17 @@ __device__ double linstep_metric(const DevModel* M, const double* x0, const doub
     for (int i = 0; i < NL; ++i) {
       if (!ct[k * NL + i]) continue;
       ++ns;
-      double p[3];
+      double p[3], dp[3] = {0.0, 0.0, 0.0};
       stance_point(foot, ct, N, k, i, p);
+      if (D0) {
+        const int s0 = run_start(k, i, [ct](int kk, int l) { return ct[kk * NL + l] != 0; });
+        if (s0 > 0)
+          for (int d = 0; d < 3; ++d) {
+            const double a = D0[(s0 * NL + i) * 3 + d];
+            p[d] = p[d] + a;
+            dp[d] = D1[(s0 * NL + i) * 3 + d] - a;
+          }
+      }
       const double* f = uk + 3 * i;
       const double* df = duk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
@@ -154,9 +212,10 @@ __device__ double linstep_metric(const DevModel* M, const double* x0, const doub
       dF[0] += df[0];
       dF[1] += df[1];
       dF[2] += df[2];
-      dT[0] += (ry * df[2] - rz * df[1]) - (dx[1] * f[2] - dx[2] * f[1]);
-      dT[1] += (rz * df[0] - rx * df[2]) - (dx[2] * f[0] - dx[0] * f[2]);
-      dT[2] += (rx * df[1] - ry * df[0]) - (dx[0] * f[1] - dx[1] * f[0]);
+      const double q0 = dx[0] - dp[0], q1 = dx[1] - dp[1], q2 = dx[2] - dp[2];
+      dT[0] += (ry * df[2] - rz * df[1]) - (q1 * f[2] - q2 * f[1]);
+      dT[1] += (rz * df[0] - rx * df[2]) - (q2 * f[0] - q0 * f[2]);
+      dT[2] += (rx * df[1] - ry * df[0]) - (q0 * f[1] - q1 * f[0]);
     }
     for (int j = 0; j < NU; ++j) {
       const int i = j / 3;
@@ -205,6 +264,7 @@ __device__ double linstep_metric(const DevModel* M, const double* x0, const doub
       ss += dx[s] * dx[s];
     }
   }
+  if (D0) mt += foot_cost(M, foot, ct, D0, D1, 0.0, true);
   *dxn = sqrt(ss);
   return mt;
 }
@@ -216,13 +276,34 @@ __global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
   const int N = M->N;
   const int nu = N * NU;
   for (int i = threadIdx.x; i < nu; i += 64) a.uj[(size_t)q * nu + i] = a.u[(size_t)q * nu + i];
+  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
+  const uint8_t* ct = a.contact + (size_t)q * N * NL;
+  double* dj = a.dj ? a.dj + (size_t)q * nu : nullptr;
+  if (dj)  // footholds start at clamp(0, lo, hi) (oracle_feet_init)
+    for (int sl = threadIdx.x; sl < N * NL; sl += 64) {
+      const int s0 = sl / NL, leg = sl % NL;
+      auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
+      int e = 0;
+      double pb[3];
+      const bool run = later_start(N, s0, leg, st, &e);
+      if (run) stance_point(ft, N, s0, leg, st, pb);
+      for (int d = 0; d < 3; ++d) {
+        double v = 0.0;
+        if (run) {
+          double lo, hi;
+          foot_box_d(ft, s0, e, leg, d, pb, &lo, &hi);
+          v = fmin(fmax(0.0, lo), hi);
+        }
+        dj[sl * 3 + d] = v;
+      }
+    }
+  __syncthreads();
   if (threadIdx.x == 0) {
     a.done[q] = a.status[q] != CMPC_SUCCESS ? 1 : 0;
     a.sqp_iters[q] = 0;
     a.qp_iters[q] = a.iters ? a.iters[q] : 0;
-    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, a.foot + (size_t)q * (N + 1) * NL * 3,
-                 a.contact + (size_t)q * N * NL, a.u + (size_t)q * nu, nullptr, 0.0, a.lin + (size_t)q * N * 6,
-                 nullptr);
+    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, ft, ct, a.u + (size_t)q * nu, nullptr,
+                 0.0, a.lin + (size_t)q * N * 6, nullptr, dj);
   }
 }
 
@@ -236,6 +317,8 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   const int nu = N * NU;
   double* uj = a.uj + (size_t)q * nu;
   const double* uq = a.uq + (size_t)q * nu;
+  double* dj = a.dj ? a.dj + (size_t)q * nu : nullptr;  // footholds (cmpc_nlp_solve_batch)
+  const double* dq = a.dj ? a.dq + (size_t)q * nu : nullptr;
   const double* x0 = a.x0 + (size_t)q * NX;
   const double* xr = a.xref + (size_t)q * (N + 1) * NX;
   const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
@@ -255,17 +338,22 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   // lane 16: |du| (sequential, the oracle's order)
   double J = 0.0, aux = 0.0;
   if (lane < 14) {
-    J = rollout_cost(M, x0, xr, ft, ct, uj, uq, ldexp(1.0, -lane), nullptr, nullptr);
+    J = rollout_cost(M, x0, xr, ft, ct, uj, uq, ldexp(1.0, -lane), nullptr, nullptr, dj, dq);
   } else if (lane == 14) {
-    J = rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, nullptr, nullptr);
+    J = rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, nullptr, nullptr, dj, nullptr);
   } else if (lane == 15) {
-    J = linstep_metric(M, x0, xr, ft, ct, uj, uq, &aux);
+    J = linstep_metric(M, x0, xr, ft, ct, uj, uq, &aux, dj, dq);
   } else if (lane == 16) {
     double s2 = 0.0;
     for (int i = 0; i < nu; ++i) {
       const double d = uq[i] - uj[i];
       s2 += d * d;
     }
+    if (dj)
+      for (int i = 0; i < nu; ++i) {
+        const double d = dq[i] - dj[i];
+        s2 += d * d;
+      }
     aux = sqrt(s2);
   }
   const double J0 = __shfl(J, 14, 64);
@@ -283,12 +371,15 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   const double Jn = ma >= 0 ? __shfl(J, ma, 64) : J0;
   __syncthreads();
   if (alpha > 0.0)
-    for (int i = lane; i < nu; i += 64) uj[i] = uj[i] + alpha * (uq[i] - uj[i]);
+    for (int i = lane; i < nu; i += 64) {
+      uj[i] = uj[i] + alpha * (uq[i] - uj[i]);
+      if (dj) dj[i] = dj[i] + alpha * (dq[i] - dj[i]);
+    }
   const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
   __syncthreads();
   if (lane == 0) {
     if (conv) a.done[q] = 1;
-    rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, a.lin + (size_t)q * N * 6, nullptr);
+    rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, a.lin + (size_t)q * N * 6, nullptr, dj);
   }
 }
 
@@ -299,11 +390,27 @@ __global__ __launch_bounds__(64) void k_sqp_final(SqpArgs a) {
   const int N = M->N;
   const int nu = N * NU;
   for (int i = threadIdx.x; i < nu; i += 64) a.u[(size_t)q * nu + i] = a.uj[(size_t)q * nu + i];
+  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
+  const uint8_t* ct = a.contact + (size_t)q * N * NL;
+  const double* dj = a.dj ? a.dj + (size_t)q * nu : nullptr;
+  if (dj && a.feet)  // the controller's foot_pos output (oracle_feet_table)
+    for (int sl = threadIdx.x; sl < (N + 1) * NL; sl += 64) {
+      const int j = sl / NL, i = sl % NL;
+      auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
+      const int k = (j < N && ct[j * NL + i]) ? j : ((j > 0 && ct[(j - 1) * NL + i]) ? j - 1 : -1);
+      double p[3];
+      if (j == 0 || k < 0) {
+        for (int d = 0; d < 3; ++d) p[d] = ft[sl * 3 + d];
+      } else {
+        lever_point(ft, dj, N, k, i, st, p);
+      }
+      double* o = a.feet + ((size_t)q * (N + 1) * NL + sl) * 3;
+      for (int d = 0; d < 3; ++d) o[d] = p[d];
+    }
   __syncthreads();
   if (threadIdx.x == 0 && a.x)
-    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, a.foot + (size_t)q * (N + 1) * NL * 3,
-                 a.contact + (size_t)q * N * NL, a.u + (size_t)q * nu, nullptr, 0.0, nullptr,
-                 a.x + (size_t)q * (N + 1) * NX);
+    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, ft, ct, a.u + (size_t)q * nu, nullptr,
+                 0.0, nullptr, a.x + (size_t)q * (N + 1) * NX, dj);
 }
 
 // number of QPs not yet done -> count[0]

@@ -56,9 +56,10 @@ __device__ __forceinline__ void tile_of(int idx, int& ti, int& tj) {
 }
 
 
-template <typename T, int NMAX, int WAVES>
+template <typename T, int NMAX, int WAVES, bool FEET = false>
 struct SrbdLds {
   static constexpr int NTRI = NMAX / 3;
+  static constexpr int FT = FEET ? NTRI : 1;  // foothold arrays only in the FEET instantiation (LDS of k_solve128)
   T s_G[2][16][NMAX];
   T s_w[2][16];
   T s_q[2][16];
@@ -68,7 +69,14 @@ struct SrbdLds {
   uint8_t s_e[MAXN * NL];
   int s_ns[MAXN];
   int s_cb[MAXN + 1];  // 3 * #triples of steps < k
-  int s_tk[NTRI], s_tleg[NTRI], s_tbase[MAXN];
+  int s_tk[NTRI], s_tleg[NTRI];
+  int s_nt[MAXN];  // triples acting first at step k (stance legs + later runs starting at k)
+  // foothold triples (CondenseArgs::dbar): force triple of each stance (k, leg), foothold flag, run end, box (delta)
+  // and the run's mean des position
+  int s_slot[FEET ? MAXN * NL : 1];
+  uint8_t s_tf[FT];
+  int s_te[FT];
+  double s_blo[FT][3], s_bhi[FT][3], s_pbar[FT][3];
   T s_diagR[NMAX], s_offR[NMAX];
   int s_next[NMAX];
   int s_wtot[WAVES];
@@ -81,8 +89,10 @@ struct SrbdLds {
 // else declared here. Writes H (class-packed), g, the pyramid data, tri_map, status and nvar to the workspace.
 // Returns n when the QP was condensed here, -1 otherwise (invalid contact table / too large: status written; a
 // bigger class: nvar hint; a smaller class: nothing).
-template <typename T, int NMAX, int WAVES, bool EXT>
-__device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q, srbd::SrbdLds<T, NMAX, WAVES>* ext) {
+// FEET: the instantiation that also serves CondenseArgs::dbar (foothold columns); without it dbar is ignored.
+template <typename T, int NMAX, int WAVES, bool EXT, bool FEET = false>
+__device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
+                                                srbd::SrbdLds<T, NMAX, WAVES, FEET>* ext) {
   using namespace srbd;
   constexpr int NT = NMAX / 16;              // 16x16 tiles per dimension
   constexpr int NLT = NT * (NT + 1) / 2;     // lower tiles
@@ -97,8 +107,8 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   const int N = M->N, L = NL;
   const int ld = a.ld;
 
-  __shared__ SrbdLds<T, NMAX, WAVES> Sl;  // stand-alone kernel: declared here (constant LDS base)
-  SrbdLds<T, NMAX, WAVES>& S = EXT ? *ext : Sl;
+  __shared__ SrbdLds<T, NMAX, WAVES, FEET> Sl;  // stand-alone kernel: declared here (constant LDS base)
+  SrbdLds<T, NMAX, WAVES, FEET>& S = EXT ? *ext : Sl;
 
   // ---- load the QP record into LDS
   const double* xr = a.xref + (size_t)q * (N + 1) * NX;
@@ -109,15 +119,21 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   if (tid < 32) (&S.s_w[0][0])[tid] = T(0), (&S.s_q[0][0])[tid] = T(0);
   if (tid == 0) S.s_flag = 0;
   const int ne = N * L;
-  int e = 0;
+  const bool feet = FEET && a.dbar != nullptr;
+  const double* Dq = feet ? a.dbar + (size_t)q * N * NU : nullptr;
+  int e = 0, fs = 0;
   if (tid < ne) {
-    e = a.contact[(size_t)q * ne + tid] ? 1 : 0;
+    const uint8_t* ctq = a.contact + (size_t)q * ne;
+    e = ctq[tid] ? 1 : 0;
     S.s_e[tid] = (uint8_t)e;
+    fs = (feet && e && tid >= L && !ctq[tid - L]) ? 1 : 0;  // (k, leg) starts a later run
   }
-  // ballot prefix over (k, leg) in k-major order -> triple index of each stance (k, leg)
-  const unsigned long long bal = __ballot(e);
-  const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-  if (lane == 0) S.s_wtot[wave] = __popcll(bal);
+  // ballot prefix over (k, leg) in k-major order -> triple index of each stance (k, leg); a later run's foothold
+  // triple follows the force triple of its first (k, leg)
+  const unsigned long long bal = __ballot(e), balf = __ballot(fs);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const int pre = __popcll(bal & below) + __popcll(balf & below);
+  if (lane == 0) S.s_wtot[wave] = __popcll(bal) + __popcll(balf);
   __syncthreads();
   int off = 0;
   for (int w = 0; w < wave; ++w) off += S.s_wtot[w];
@@ -125,15 +141,43 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   for (int w = 0; w < WAVES; ++w) nt += S.s_wtot[w];
   if (e) {
     const int t = off + pre;
+    if (FEET) S.s_slot[tid] = t;
     if (t < NTRI) {
       S.s_tk[t] = tid / L;
       S.s_tleg[t] = tid % L;
+      if (FEET) S.s_tf[t] = 0;
+    }
+    if (FEET && fs && t + 1 < NTRI) {
+      const int k = tid / L, leg = tid % L;
+      auto st = [&](int kk, int l) { return S.s_e[kk * L + l] != 0; };
+      int ee = k;
+      later_start(N, k, leg, st, &ee);
+      S.s_tk[t + 1] = k;
+      S.s_tleg[t + 1] = leg;
+      S.s_tf[t + 1] = 1;
+      S.s_te[t + 1] = ee;
+      double pb[3];
+      stance_point(S.s_foot, N, k, leg, st, pb);
+      bool empty = false;
+      for (int d = 0; d < 3; ++d) {
+        double lo, hi;
+        foot_box_d(S.s_foot, k, ee, leg, d, pb, &lo, &hi);
+        S.s_pbar[t + 1][d] = pb[d];
+        S.s_blo[t + 1][d] = lo;
+        S.s_bhi[t + 1][d] = hi;
+        empty = empty || !(lo <= hi);
+      }
+      if (empty) atomicOr(&S.s_flag, 2);
     }
   }
   if (tid < N) {
-    int ns = 0;
-    for (int i = 0; i < L; ++i) ns += S.s_e[tid * L + i];
+    int ns = 0, nf = 0;
+    for (int i = 0; i < L; ++i) {
+      ns += S.s_e[tid * L + i];
+      nf += (feet && tid > 0 && S.s_e[tid * L + i] && !S.s_e[(tid - 1) * L + i]) ? 1 : 0;
+    }
     S.s_ns[tid] = ns;
+    S.s_nt[tid] = ns + nf;
     if (ns == 0) atomicOr(&S.s_flag, 1);
     // per-step M_k = dt * I_b^{-1} R_z(psi_k)^T  (Theta row of A_k)
     const double psi = S.s_xref[tid * NX + 11];
@@ -150,7 +194,8 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   __syncthreads();
   const int n = 3 * nt;
   int st = CMPC_SUCCESS;
-  if (S.s_flag) st = CMPC_INVALID_CONTACT;
+  if (S.s_flag & 1) st = CMPC_INVALID_CONTACT;
+  else if (S.s_flag & 2) st = CMPC_INFEASIBLE_STEP;
   else if (n > NMAX) {
     if (NMAX < CMPC_IPM_MAX_N) {  // a bigger class follows: leave the hint, not the status
       if (tid == 0) a.nvar[q] = n;
@@ -170,8 +215,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
     int acc = 0;
     for (int k = 0; k < N; ++k) {
       S.s_cb[k] = 3 * acc;
-      S.s_tbase[k] = acc;
-      acc += S.s_ns[k];
+      acc += S.s_nt[k];
     }
     S.s_cb[N] = 3 * acc;
   }
@@ -181,6 +225,8 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   const int c = tid;
   const bool col = c < n;
   int kc = 0, d = 0, leg = 0;
+  bool fcol = false;  // a foothold column (acts at steps kc..ke)
+  int ke = 0;
   T gam[NX];
 #pragma unroll
   for (int s = 0; s < NX; ++s) gam[s] = T(0);
@@ -192,23 +238,39 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
     kc = S.s_tk[t];
     leg = S.s_tleg[t];
     const int j = 3 * leg + d;
-    const int nb = (kc > 0) + (kc < N - 1);
-    S.s_diagR[c] = T(2.0 * M->Wf[j] + 2.0 * M->Wr[j] * (double)nb);
-    S.s_offR[c] = T(-2.0 * M->Wr[j]);
-    int nx = -1;
-    if (kc + 1 < N && S.s_e[(kc + 1) * L + leg]) {
-      int rank = 0;
-      for (int i = 0; i < leg; ++i) rank += S.s_e[(kc + 1) * L + i];
-      nx = 3 * (S.s_tbase[kc + 1] + rank) + d;
+    auto stf = [&](int k, int l) { return S.s_e[k * L + l] != 0; };
+    fcol = FEET && feet && S.s_tf[t];
+    if (fcol) {  // foothold: 2 Wp cnt on the diagonal, 2 Wp sum_j (pbar - des_j) in g (oracle_condense_feet)
+      ke = S.s_te[t];
+      double gs = 0.0;
+      for (int jn = kc; jn <= ke + 1; ++jn) gs += S.s_pbar[t][d] - S.s_foot[(jn * L + leg) * 3 + d];
+      S.s_diagR[c] = T(2.0 * M->Wp[j] * (double)(ke + 2 - kc));
+      S.s_offR[c] = T(0);
+      S.s_next[c] = -1;
+      gcol = T(2.0 * M->Wp[j] * gs);
+    } else {
+      const int nb = (kc > 0) + (kc < N - 1);
+      S.s_diagR[c] = T(2.0 * M->Wf[j] + 2.0 * M->Wr[j] * (double)nb);
+      S.s_offR[c] = T(-2.0 * M->Wr[j]);
+      int nx = -1;
+      if (kc + 1 < N && S.s_e[(kc + 1) * L + leg]) {
+        if (FEET) {
+          nx = 3 * S.s_slot[(kc + 1) * L + leg] + d;
+        } else {
+          int rank = 0;
+          for (int i = 0; i < leg; ++i) rank += S.s_e[(kc + 1) * L + i];
+          nx = S.s_cb[kc + 1] + 3 * rank + d;
+        }
+      }
+      S.s_next[c] = nx;
+      if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)S.s_ns[kc]));
+      double p[3];
+      lever_point(S.s_foot, Dq, N, kc, leg, stf, p);
+      const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : S.s_xref + kc * NX;
+      rx = p[0] - cb[0];
+      ry = p[1] - cb[1];
+      rz = p[2] - cb[2];
     }
-    S.s_next[c] = nx;
-    if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)S.s_ns[kc]));
-    double p[3];
-    stance_point(S.s_foot, N, kc, leg, [&](int k, int l) { return S.s_e[k * L + l] != 0; }, p);
-    const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : S.s_xref + kc * NX;
-    rx = p[0] - cb[0];
-    ry = p[1] - cb[1];
-    rz = p[2] - cb[2];
   }
   // free response x_hat_k = Aqp x0 (thread 0)
   double xh[NX];
@@ -252,7 +314,21 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
       gam[10] += T(S.s_M[km][3]) * Lx + T(S.s_M[km][4]) * Ly + T(S.s_M[km][5]) * Lz;
       gam[11] += T(S.s_M[km][6]) * Lx + T(S.s_M[km][7]) * Ly + T(S.s_M[km][8]) * Lz;
       gam[5] += dt * gam[12];
-      if (kc == km) {
+      if (fcol) {
+        if (km <= ke) {  // dt e_d x f_bar_{leg, km}
+          const double* fb = a.ubar + ((size_t)q * N + km) * NU + 3 * leg;
+          if (d == 0) {
+            gam[7] += dt * T(-fb[2]);
+            gam[8] += dt * T(fb[1]);
+          } else if (d == 1) {
+            gam[6] += dt * T(fb[2]);
+            gam[8] += dt * T(-fb[0]);
+          } else {
+            gam[6] += dt * T(-fb[1]);
+            gam[7] += dt * T(fb[0]);
+          }
+        }
+      } else if (kc == km) {
         gam[3 + d] += dtm;
         // dt * [r]x e_d
         if (d == 0) {
@@ -281,6 +357,17 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
         xn[7] += M->dt * (lk[5] * d0 - lk[3] * d2);
         xn[8] += M->dt * (lk[3] * d1 - lk[4] * d0);
       }
+      if (feet)  // -dt D x f_bar of the later runs' stance legs
+        for (int i = 0; i < L; ++i) {
+          if (!S.s_e[km * L + i]) continue;
+          const int s0 = run_start(km, i, [&](int k2, int l) { return S.s_e[k2 * L + l] != 0; });
+          if (s0 == 0) continue;
+          const double* dl = Dq + (s0 * NL + i) * 3;
+          const double* fb = a.ubar + ((size_t)q * N + km) * NU + 3 * i;
+          xn[6] -= M->dt * (dl[1] * fb[2] - dl[2] * fb[1]);
+          xn[7] -= M->dt * (dl[2] * fb[0] - dl[0] * fb[2]);
+          xn[8] -= M->dt * (dl[0] * fb[1] - dl[1] * fb[0]);
+        }
       xn[12] = xh[12];
       for (int s = 0; s < NX; ++s) {
         xh[s] = xn[s];
@@ -378,13 +465,21 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   if (tid < npad / 3) {
     const int t = tid;
     const bool on = t < nt;
+    const bool ft = FEET && on && feet && S.s_tf[t];
     const int lg = on ? S.s_tleg[t] : 0;
-    a.tri_mu[(size_t)q * (ld / 3) + t] = on ? T(M->mu[lg]) : T(0);
+    a.tri_mu[(size_t)q * (ld / 3) + t] = (on && !ft) ? T(M->mu[lg]) : T(0);
     for (int r = 0; r < 5; ++r) {
-      a.tri_lo[((size_t)q * (ld / 3) + t) * 5 + r] = T(0);
-      a.tri_hi[((size_t)q * (ld / 3) + t) * 5 + r] = T(M->ub[r]);
+      double lo = 0.0, hi = M->ub[r];
+      if (ft) {  // rows [-x, x, -y, y, z] of the step box
+        const int dd = r < 4 ? r / 2 : 2;
+        const bool neg = r == 0 || r == 2;
+        lo = neg ? -S.s_bhi[t][dd] : S.s_blo[t][dd];
+        hi = neg ? -S.s_blo[t][dd] : S.s_bhi[t][dd];
+      }
+      a.tri_lo[((size_t)q * (ld / 3) + t) * 5 + r] = T(lo);
+      a.tri_hi[((size_t)q * (ld / 3) + t) * 5 + r] = T(hi);
     }
-    a.tri_map[(size_t)q * (ld / 3) + t] = on ? S.s_tk[t] * L + lg : -1;
+    a.tri_map[(size_t)q * (ld / 3) + t] = on ? (ft ? N * L : 0) + S.s_tk[t] * L + lg : -1;
   }
   if (tid == 0) {
     a.status[q] = CMPC_SUCCESS;

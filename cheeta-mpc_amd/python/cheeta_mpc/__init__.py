@@ -92,6 +92,8 @@ def lib():
     L.cmpc_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
     L.cmpc_solve_batch_warm.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, i, i, vp]
     L.cmpc_sqp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, i, i, i, vp]
+    L.cmpc_nlp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, d, i, i, i, vp]
+    L.cmpc_condense_lin_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, d, d, i, i, i, d, d, vp]
     L.cmpc_policy_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, C.c_double, d, i, i, vp]
     L.cmpc_shift_inputs.argtypes = [C.c_int, C.c_int, d, C.c_int, d, vp]
     L.cmpc_solve_batch_host.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i]
@@ -321,6 +323,46 @@ class Engine:
                                         si.ptr, None), "cmpc_sqp_solve_batch")
         _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
         return u.host(), (x.host() if want_x else None), st.host(), qi.host(), si.host()
+
+    def nlp_solve(self, x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-6, want_x=True):
+        """The NLP with the later runs' footholds as decision variables (cmpc_nlp_solve_batch):
+        (u, feet [B,N+1,L,3], x, status, qp_iters, sqp_iters)."""
+        B = x0.shape[0]
+        N = self.model.N
+        d = {k: DeviceArray.from_host(v) for k, v in
+             dict(x0=np.asarray(x0, np.float64), xref=np.asarray(xref, np.float64),
+                  foot=np.asarray(foot, np.float64), contact=np.asarray(contact, np.uint8)).items()}
+        u = DeviceArray((B, N, NL, 3), np.float64)
+        feet = DeviceArray((B, N + 1, NL, 3), np.float64)
+        x = DeviceArray((B, N + 1, NX), np.float64) if want_x else None
+        st = DeviceArray((B,), np.int32)
+        qi = DeviceArray((B,), np.int32)
+        si = DeviceArray((B,), np.int32)
+        _chk(lib().cmpc_nlp_solve_batch(self.ctx, B, d["x0"].ptr, d["xref"].ptr, d["foot"].ptr, d["contact"].ptr,
+                                        sqp_iter_max, sqp_tol, u.ptr, feet.ptr, x.ptr if want_x else None, st.ptr,
+                                        qi.ptr, si.ptr, None), "cmpc_nlp_solve_batch")
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return u.host(), feet.host(), (x.host() if want_x else None), st.host(), qi.host(), si.host()
+
+    def condense_lin(self, x0, xref, foot, contact, lin=None, ubar=None, dbar=None):
+        """Condensed QP at a linearisation point (cmpc_condense_lin_batch): (H, g, n, status, tri_map, lo, hi)."""
+        B = x0.shape[0]
+        nt = self.ld // 3
+        d = [DeviceArray.from_host(np.asarray(a, t)) if a is not None else None for a, t in
+             ((x0, np.float64), (xref, np.float64), (foot, np.float64), (contact, np.uint8), (lin, np.float64),
+              (ubar, np.float64), (dbar, np.float64))]
+        H = DeviceArray((B, self.ld, self.ld), np.float64)
+        g = DeviceArray((B, self.ld), np.float64)
+        n = DeviceArray((B,), np.int32)
+        st = DeviceArray((B,), np.int32)
+        mp = DeviceArray((B, nt), np.int32)
+        lo = DeviceArray((B, nt, 5), np.float64)
+        hi = DeviceArray((B, nt, 5), np.float64)
+        p = [a.ptr if a is not None else None for a in d]
+        _chk(lib().cmpc_condense_lin_batch(self.ctx, B, *p, H.ptr, g.ptr, n.ptr, st.ptr, mp.ptr, lo.ptr, hi.ptr,
+                                           None), "cmpc_condense_lin_batch")
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return H.host(), g.host(), n.host(), st.host(), mp.host(), lo.host(), hi.host()
 
     def policy(self, x0, xref, foot, contact, u, act_tol=0.0):
         """Feedback policy dU/dx0 at the solution u [B,N,L,3] (cmpc_policy_batch): (K [B,N,L,3,13], nfree, status).

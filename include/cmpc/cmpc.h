@@ -191,6 +191,22 @@ int cmpc_solve_batch_warm(cmpc_ctx* ctx, int B, const double* d_x0, const double
 int cmpc_sqp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                          const uint8_t* d_contact, int sqp_iter_max, double sqp_tol, double* d_u, double* d_x,
                          int* d_status, int* d_qp_iters, int* d_sqp_iters, void* stream);
+/* The reference's NLP with its foothold variables (CentroidalMPC.cpp:132-133: foot_pos[i] at every node, swing
+ * dynamics :93 / :174-176, pinned node 0 :165-167, step box :196-198 with CMPC_STEP_LB/UB, tracking cost :218-221):
+ * cmpc_sqp_solve_batch over the forces AND the footholds. foot_vel is free and uncosted, so a swing node that starts
+ * no stance run tracks des_foot_pos exactly and a stance run from step 0 stays at the current foot; each later stance
+ * run (first stance step s >= 1) holds one free foothold, a decision variable of every QP of the SQP (a foothold
+ * triple with mu = 0 whose rows [-x, x, -y, y, z] carry the step box; its lever-arm columns dt e_d x f_bar act on
+ * the angular momentum at each step of the run). The footholds start at the box-projected mean of des_foot_pos over
+ * the run's nodes (the frozen footholds of cmpc_solve_batch), the forces at the cold QP's solution; the line search
+ * and the convergence test cover both (|du| over forces and footholds). d_feet [B][N+1][L][3] (required): the
+ * reference controller's foot_pos outputs (:269-273) — node 0 and the first run's nodes the current foot, a later
+ * run's nodes its foothold, free swing nodes des_foot_pos. Status CMPC_INFEASIBLE_STEP when a run's box is empty
+ * (the forces then stay at the last iterate). Condensing runs on the workgroup kernels (n grows by 3 per later run).
+ * Oracle: oracle_sqp_solve_feet. */
+int cmpc_nlp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                         const uint8_t* d_contact, int sqp_iter_max, double sqp_tol, double* d_u, double* d_feet,
+                         double* d_x, int* d_status, int* d_qp_iters, int* d_sqp_iters, void* stream);
 /* Feedback policy of each QP at its solution d_u [B][N][L][3] (e.g. from cmpc_solve_batch): d_K [B][N][L][3][13]
  * = dU/dx0, the condensed counterpart of HpipmInterface::getRiccatiFeedback (HpipmInterface.cpp:330-455; ocs2 uses
  * it as the linear feedback policy, MultipleShootingSolver.cpp:334-362). K = -Z (Z'HZ)^{-1} Z' Bqp'Q Aqp, where Z
@@ -215,6 +231,14 @@ int cmpc_solve_batch_host(cmpc_ctx* ctx, int B, const double* x0, const double* 
  *   d_status [B] (CMPC_SUCCESS, or CMPC_INVALID_CONTACT / CMPC_TOO_LARGE). */
 int cmpc_condense_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                         const uint8_t* d_contact, double* d_H, double* d_g, int* d_n, int* d_status, void* stream);
+/* Same at an SQP linearisation point (test hook of the SQP / NLP subproblems): d_lin [B][N][6] (c_bar_k, F_bar_k) or
+ * NULL; with d_dbar [B][N][L][3] (foothold offsets by run start) and d_ubar [B][N][L][3] (forces) the foothold
+ * triples of cmpc_nlp_solve_batch are added (oracle_condense_feet). Optional outputs: d_tri_map [B][ld/3] (k L + leg,
+ * N L + s L + leg for a foothold triple, -1 padding), d_tri_lo / d_tri_hi [B][ld/3][5]. */
+int cmpc_condense_lin_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                            const uint8_t* d_contact, const double* d_lin, const double* d_ubar, const double* d_dbar,
+                            double* d_H, double* d_g, int* d_n, int* d_status, int* d_tri_map, double* d_tri_lo,
+                            double* d_tri_hi, void* stream);
 
 /* Generic batched dense friction-pyramid QP (stage 2 alone):
  *   min 1/2 u'Hu + g'u  s.t.  lo_j <= F(mu_a) u_{3a..3a+2} <= hi_j   (F as CentroidalMPC.cpp:186-190)

@@ -21,7 +21,7 @@ _FIRST = ("test_gpu_parity.py::test_cpp_centroidal_mpc_driver", "test_full_size.
           "test_multi_rank_gpu.py::test_config4_full_batch_one_gpu",
           "test_multi_rank_gpu.py::test_two_rank_hip_shards_gather_bit_exact",
           "test_gpu_parity.py::test_device_matches_golden_fp64", "test_gpu_parity.py::test_device_foot_semantics",
-          "test_ocp_eq.py::", "test_hpipm_eq_riccati.py::", "test_sqp.py::")
+          "test_ocp_eq.py::", "test_hpipm_eq_riccati.py::", "test_sqp.py::", "test_feet.py::")
 
 
 def pytest_collection_modifyitems(session, config, items):

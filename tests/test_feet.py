@@ -187,3 +187,99 @@ def test_empty_step_box_is_reported(op):
     assert st == 7  # CMPC_INFEASIBLE_STEP
     n, *_, stc = op.condense_feet(mo, x0[0], xref[0], foot2, contact[0], np.zeros((N, 6)), u, D)
     assert stc == 7
+
+
+# ------------------------------------------------------------------------------------------------ device (gpu)
+
+def rel_err(u, ur):
+    return float(np.max(np.abs(u - ur)) / max(1.0, float(np.max(np.abs(ur)))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,gait", [(10, 1), (10, 2), (20, 1), (5, 1)])
+def test_device_foothold_condensing_matches_oracle(cm, op, N, gait):
+    """cmpc_condense_lin_batch with foothold columns vs oracle_condense_feet (classes 64 / 128 / 256 and the
+    one-class context N = 5): same triple order and boxes, H and g to 1e-11."""
+    B = 8
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=gait)
+    rng = np.random.default_rng(N + gait)
+    u = rng.uniform(0, 40, (B, N, NL, 3)) * contact[..., None]
+    D = np.zeros((B, N, NL, 3))
+    lin = np.zeros((B, N, 6))
+    for q in range(B):
+        for (s, i, e) in later_runs(contact[q]):
+            D[q, s, i] = rng.uniform(-0.05, 0.05, 3)
+        lin[q] = op.nlp_rollout_cost_feet(mo, x0[q], xref[q], foot[q], contact[q], u[q], D[q])[2]
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    H, g, n, st, mp, lo, hi = eng.condense_lin(x0, xref, foot, contact, lin, u, D)
+    for q in range(B):
+        nr, Hr, gr, mur, lor, hir, mpr, sr = op.condense_feet(mo, x0[q], xref[q], foot[q], contact[q], lin[q], u[q],
+                                                               D[q], ld=eng.ld)
+        assert st[q] == sr == 0 and n[q] == nr
+        t = nr // 3
+        assert np.array_equal(mp[q, :t], mpr[:t])
+        assert np.allclose(lo[q, :t], lor[:t], rtol=0, atol=1e-15) and np.allclose(hi[q, :t], hir[:t], rtol=0,
+                                                                                  atol=1e-15)
+        sc = max(1.0, np.abs(Hr[:nr, :nr]).max())
+        assert np.abs(H[q, :nr, :nr] - Hr[:nr, :nr]).max() < 1e-11 * sc
+        assert np.abs(g[q, :nr] - gr[:nr]).max() < 1e-11 * max(1.0, np.abs(gr[:nr]).max())
+    # frozen footholds (no dbar): the hook reproduces cmpc_condense_batch
+    H0, g0, n0, st0, *_ = eng.condense_lin(x0, xref, foot, contact)
+    H1, g1, n1, st1 = eng.condense(x0, xref, foot, contact)
+    assert np.array_equal(H0, H1) and np.array_equal(g0, g1) and np.array_equal(n0, n1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,gait,prec", [(10, 1, 0), (10, 2, 0), (20, 1, 0), (10, 1, 1), (20, 1, 1)])
+def test_device_nlp_matches_oracle(cm, op, N, gait, prec):
+    B = 16
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=gait)
+    # fp32: the IPM tolerances fp32 reaches (as test_full_size's fp32 configs)
+    settings = cm.default_settings() if prec == 0 else cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3,
+                                                                           tol_comp=1e-4)
+    eng = cm.Engine(m, settings, precision=prec, max_batch=B)
+    u, feet, x, st, qi, si = eng.nlp_solve(x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7)
+    s = op.default_settings()
+    for q in range(B):
+        ur, Dr, feetr, xr, sr, qir, sir = op.sqp_solve_feet(mo, s, x0[q], xref[q], foot[q], contact[q],
+                                                            sqp_iter_max=10, sqp_tol=1e-7)
+        assert st[q] == sr == 0
+        if prec == 0:
+            assert rel_err(u[q], ur) < 1e-6, q
+            assert np.abs(feet[q] - feetr).max() < 1e-8, q
+            assert abs(int(si[q]) - sir) <= 1 and si[q] < 10
+            assert np.abs(x[q] - xr).max() < 1e-6 * max(1.0, np.abs(xr).max())
+        else:  # fp32 QPs inside an fp64 line search: the NLP cost matches the fp64 oracle's to 1e-3
+            J = op.nlp_rollout_cost_feet(mo, x0[q], xref[q], foot[q], contact[q], u[q],
+                                         feet_offsets(op, mo, foot[q], contact[q], feet[q]))[0]
+            Jr = op.nlp_rollout_cost_feet(mo, x0[q], xref[q], foot[q], contact[q], ur, Dr)[0]
+            assert abs(J - Jr) < 1e-3 * abs(Jr)
+        # feet table semantics: node 0 current, free swing nodes des, boxes respected
+        assert np.array_equal(feet[q][0], foot[q][0])
+        for (s0, i, e) in later_runs(contact[q]):
+            pb, blo, bhi, cnt = op.foot_box(foot[q], contact[q], s0, i)
+            dl = feet[q][s0, i] - pb
+            assert np.all(dl >= blo - 1e-6) and np.all(dl <= bhi + 1e-6)
+    assert np.all(u[contact == 0] == 0.0)
+
+
+def feet_offsets(op, mo, foot, contact, feet):
+    D = np.zeros((mo.N, NL, 3))
+    for (s, i, e) in later_runs(contact):
+        D[s, i] = feet[s, i] - op.foot_box(foot, contact, s, i)[0]
+    return D
+
+
+@pytest.mark.gpu
+def test_device_nlp_empty_step_box(cm, op):
+    N, B = 10, 4
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=1)
+    runs = later_runs(contact[1])
+    s0, i, e = runs[0]
+    foot[1, e + 1, i, 0] += 0.5
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    u, feet, x, st, qi, si = eng.nlp_solve(x0, xref, foot, contact)
+    assert st[1] == 7 and all(st[q] == 0 for q in (0, 2, 3))
