@@ -1032,6 +1032,49 @@ int cmpc_condense_batch(cmpc_ctx* c, int B, const double* x0, const double* xref
   return CMPC_OK;
 }
 
+int cmpc_nlp_solve_batch_host(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                              const uint8_t* contact, int sqp_iter_max, double sqp_tol, double* u, double* feet,
+                              double* x, int* status, int* qp_iters, int* sqp_iters) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !feet || !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  const int N = c->model.N;
+  const size_t n_x0 = (size_t)B * CMPC_NX, n_xr = (size_t)B * (N + 1) * CMPC_NX,
+               n_ft = (size_t)B * (N + 1) * CMPC_MAX_LEGS * 3, n_ct = (size_t)B * N * CMPC_MAX_LEGS,
+               n_u = (size_t)B * N * CMPC_NU, n_xo = x ? n_xr : 0;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bytes = al(n_x0 * 8) + al(n_xr * 8) + 2 * al(n_ft * 8) + al(n_ct) + al(n_u * 8) + al(n_xo * 8) +
+                       3 * al((size_t)B * sizeof(int));
+  int r = ensure_stage(c, bytes);
+  if (r != CMPC_OK) return r;
+  char* p = c->stage;
+  double* d_x0 = (double*)p; p += al(n_x0 * 8);
+  double* d_xr = (double*)p; p += al(n_xr * 8);
+  double* d_ft = (double*)p; p += al(n_ft * 8);
+  double* d_fo = (double*)p; p += al(n_ft * 8);
+  uint8_t* d_ct = (uint8_t*)p; p += al(n_ct);
+  double* d_u = (double*)p; p += al(n_u * 8);
+  double* d_xo = x ? (double*)p : nullptr; p += al(n_xo * 8);
+  int* d_st = (int*)p; p += al((size_t)B * sizeof(int));
+  int* d_qi = (int*)p; p += al((size_t)B * sizeof(int));
+  int* d_si = (int*)p;
+  HIP_OK(hipMemcpy(d_x0, x0, n_x0 * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_xr, xref, n_xr * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_ft, foot, n_ft * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_ct, contact, n_ct, hipMemcpyHostToDevice));
+  r = cmpc_nlp_solve_batch(c, B, d_x0, d_xr, d_ft, d_ct, sqp_iter_max, sqp_tol, d_u, d_fo, d_xo, d_st, d_qi, d_si,
+                           nullptr);
+  if (r != CMPC_OK) return r;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(u, d_u, n_u * 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(feet, d_fo, n_ft * 8, hipMemcpyDeviceToHost));
+  if (x) HIP_OK(hipMemcpy(x, d_xo, n_xo * 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(status, d_st, (size_t)B * sizeof(int), hipMemcpyDeviceToHost));
+  if (qp_iters) HIP_OK(hipMemcpy(qp_iters, d_qi, (size_t)B * sizeof(int), hipMemcpyDeviceToHost));
+  if (sqp_iters) HIP_OK(hipMemcpy(sqp_iters, d_si, (size_t)B * sizeof(int), hipMemcpyDeviceToHost));
+  return CMPC_OK;
+}
+
 int cmpc_condense_lin_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                             const uint8_t* contact, const double* lin, const double* ubar, const double* dbar,
                             double* H, double* g, int* n, int* status, int* tri_map, double* tri_lo, double* tri_hi,

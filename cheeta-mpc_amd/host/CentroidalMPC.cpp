@@ -95,17 +95,59 @@ void CentroidalMPC::UpdateMPCRaw(const double* state, size_t n_state, const doub
     if (ns <= 0) throw std::runtime_error("mpc table invalid");
   }
   std::vector<double> u((size_t)N * CMPC_NU);
-  int status = -1, iters = 0;
-  check(cmpc_solve_batch_host(ctx_, 1, x0.data(), xref.data(), foot.data(), contact.data(), u.data(), nullptr, &status,
-                              &iters),
-        "cmpc_solve_batch_host");
+  std::vector<double> feet((size_t)(N + 1) * L * 3);
+  int status = -1, iters = 0, sqp_iters = 0;
+  if (nonlinear_) {
+    check(cmpc_nlp_solve_batch_host(ctx_, 1, x0.data(), xref.data(), foot.data(), contact.data(), sqp_iter_max_,
+                                    sqp_tol_, u.data(), feet.data(), nullptr, &status, &iters, &sqp_iters),
+          "cmpc_nlp_solve_batch_host");
+  } else {
+    check(cmpc_solve_batch_host(ctx_, 1, x0.data(), xref.data(), foot.data(), contact.data(), u.data(), nullptr,
+                                &status, &iters),
+          "cmpc_solve_batch_host");
+    FrozenFeet(foot, contact, feet);
+  }
   last_status_ = status;
   last_iters_ = iters;
+  last_sqp_iters_ = sqp_iters;
+  foot_pos_.assign((size_t)L * 3 * (N + 1), 0.0);  // per leg 3 x (N+1) column-major (controller_ output order)
+  for (int i = 0; i < L; ++i)
+    for (int j = 0; j <= N; ++j)
+      for (int d = 0; d < 3; ++d) foot_pos_[(size_t)i * 3 * (N + 1) + 3 * j + d] = feet[((size_t)j * L + i) * 3 + d];
   current_time_ += model_.dt;  // CentroidalMPC.cpp:368
   // per leg: contact_force_i as 3 x N column-major (controller_ output order)
   for (int i = 0; i < L; ++i)
     for (int k = 0; k < N; ++k)
       for (int d = 0; d < 3; ++d) out[(size_t)i * 3 * N + 3 * k + d] = u[((size_t)k * L + i) * 3 + d];
+}
+
+// foot_pos of the QP mode (cmpc.h cmpc_nlp_solve_batch semantics with the footholds frozen): node 0 and a run from
+// step 0 at the current foot, a later run's nodes at p_s + sum_j (p_j - p_s) / cnt over its nodes s..e+1 (the
+// lever-arm point the QP uses), free swing nodes at des_foot_pos.
+void CentroidalMPC::FrozenFeet(const std::vector<double>& foot, const std::vector<uint8_t>& contact,
+                               std::vector<double>& feet) const {
+  const int N = model_.N, L = model_.n_legs;
+  auto ct = [&](int k, int i) { return contact[(size_t)k * L + i] != 0; };
+  for (int j = 0; j <= N; ++j)
+    for (int i = 0; i < L; ++i) {
+      const int k = (j < N && ct(j, i)) ? j : ((j > 0 && ct(j - 1, i)) ? j - 1 : -1);
+      double* o = &feet[((size_t)j * L + i) * 3];
+      const double* des = &foot[((size_t)j * L + i) * 3];
+      for (int d = 0; d < 3; ++d) o[d] = des[d];
+      if (j == 0 || k < 0) continue;
+      int s = k;
+      while (s > 0 && ct(s - 1, i)) --s;
+      int e = k;
+      while (e + 1 < N && ct(e + 1, i)) ++e;
+      const double* ps = &foot[((size_t)s * L + i) * 3];
+      for (int d = 0; d < 3; ++d) o[d] = ps[d];
+      if (s == 0) continue;
+      for (int d = 0; d < 3; ++d) {
+        double acc = 0.0;
+        for (int jj = s + 1; jj <= e + 1; ++jj) acc += foot[((size_t)jj * L + i) * 3 + d] - ps[d];
+        o[d] = ps[d] + acc / (double)(e + 2 - s);
+      }
+    }
 }
 
 int CentroidalMPC::FeedbackPolicyBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,

@@ -11,6 +11,10 @@
  *   - UpdateMPC returns the contact forces (the reference returns an empty vector, :369): per leg i a 3 x N
  *     column-major block, legs concatenated — the order of the reference controller's contact_force_i outputs;
  *   - the IPOPT_SOLVER argument is accepted and ignored (the solver is the batched GPU interior point method);
+ *   - by default UpdateMPC solves the condensed QP of the hot path (lever arm at the reference CoM, later stance runs
+ *     at the mean des foothold); setNonlinear(true) solves the reference's NLP instead (cmpc_nlp_solve_batch: SQP on
+ *     the bilinear lever arm with the later runs' footholds as decision variables, CentroidalMPC.cpp:132-133,
+ *     196-198, 218-221); FootPositions() returns the foot_pos output (:269-273) of the last call in both modes;
  *   - nothing is printed (the reference prints the table and every output, :325, :357-362);
  *   - UpdateMPCBatch solves many robots' problems in one call (device-resident records, see cmpc_solve_batch).
  */
@@ -98,13 +102,29 @@ class CentroidalMPC {
                      const double* des_inputs, size_t n_des_inputs, std::vector<double>& x0, std::vector<double>& xref,
                      std::vector<double>& foot, std::vector<uint8_t>& contact) const;
 
+  /* Nonlinear mode: UpdateMPC solves the NLP with foothold variables (SQP: at most sqp_iter_max iterations,
+   * ocs2's deltaTol = sqp_tol). */
+  void setNonlinear(bool on, int sqp_iter_max = 10, double sqp_tol = 1e-6) {
+    nonlinear_ = on;
+    sqp_iter_max_ = sqp_iter_max;
+    sqp_tol_ = sqp_tol;
+  }
+  bool nonlinear() const { return nonlinear_; }
+  /* The controller's foot_pos outputs of the last UpdateMPC (CentroidalMPC.cpp:269-273): per leg a 3 x (N+1)
+   * column-major block, legs concatenated. Node 0 and a stance run from step 0 at the current foot, free swing nodes
+   * at des_foot_pos, a later stance run at its foothold (QP mode: the frozen mean of des_foot_pos over the run). */
+  const std::vector<double>& FootPositions() const { return foot_pos_; }
+
   int lastStatus() const { return last_status_; }
-  int lastIterations() const { return last_iters_; }
+  int lastIterations() const { return last_iters_; }  // IPM iterations (all SQP subproblems in nonlinear mode)
+  int lastSqpIterations() const { return last_sqp_iters_; }
   double currentTime() const { return current_time_; }
   const cmpc_model& model() const { return model_; }
   void setSettings(const cmpc_settings& s);
 
  private:
+  void FrozenFeet(const std::vector<double>& foot, const std::vector<uint8_t>& contact,
+                  std::vector<double>& feet) const;
   cmpc_model model_;
   cmpc_settings settings_;
   int precision_;
@@ -113,4 +133,9 @@ class CentroidalMPC {
   double current_time_ = 0.0;
   int last_status_ = -1;
   int last_iters_ = 0;
+  int last_sqp_iters_ = 0;
+  bool nonlinear_ = false;
+  int sqp_iter_max_ = 10;
+  double sqp_tol_ = 1e-6;
+  std::vector<double> foot_pos_;
 };

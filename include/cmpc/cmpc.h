@@ -207,6 +207,10 @@ int cmpc_sqp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double*
 int cmpc_nlp_solve_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                          const uint8_t* d_contact, int sqp_iter_max, double sqp_tol, double* d_u, double* d_feet,
                          double* d_x, int* d_status, int* d_qp_iters, int* d_sqp_iters, void* stream);
+/* Same, host pointers; synchronous (the CentroidalMPC mirror's nonlinear UpdateMPC). */
+int cmpc_nlp_solve_batch_host(cmpc_ctx* ctx, int B, const double* x0, const double* xref, const double* foot,
+                              const uint8_t* contact, int sqp_iter_max, double sqp_tol, double* u, double* feet,
+                              double* x, int* status, int* qp_iters, int* sqp_iters);
 /* Feedback policy of each QP at its solution d_u [B][N][L][3] (e.g. from cmpc_solve_batch): d_K [B][N][L][3][13]
  * = dU/dx0, the condensed counterpart of HpipmInterface::getRiccatiFeedback (HpipmInterface.cpp:330-455; ocs2 uses
  * it as the linear feedback policy, MultipleShootingSolver.cpp:334-362). K = -Z (Z'HZ)^{-1} Z' Bqp'Q Aqp, where Z

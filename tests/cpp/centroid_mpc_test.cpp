@@ -55,6 +55,30 @@ int main() {
     for (int k = 0; k < horizon; ++k)
       std::printf("force2 %d %d %.17g %.17g %.17g\n", i, k, f2[(size_t)i * 3 * horizon + 3 * k],
                   f2[(size_t)i * 3 * horizon + 3 * k + 1], f2[(size_t)i * 3 * horizon + 3 * k + 2]);
+  // foot_pos output of the QP mode (frozen later-run footholds), then the reference's NLP with the later runs'
+  // footholds as decision variables (setNonlinear, cmpc_nlp_solve_batch)
+  {
+    const std::vector<double>& fp = mpc.FootPositions();
+    for (int i = 0; i < num_legs; ++i)
+      for (int j = 0; j <= horizon; ++j)
+        std::printf("foot2 %d %d %.17g %.17g %.17g\n", i, j, fp[(size_t)i * 3 * (horizon + 1) + 3 * j],
+                    fp[(size_t)i * 3 * (horizon + 1) + 3 * j + 1], fp[(size_t)i * 3 * (horizon + 1) + 3 * j + 2]);
+  }
+  mpc.setNonlinear(true, 10, 1e-7);
+  const std::vector<double> f3 = mpc.UpdateMPC(state, des_state, des_input);
+  std::printf("status3 %d sqp %d\n", mpc.lastStatus(), mpc.lastSqpIterations());
+  for (int i = 0; i < num_legs; ++i)
+    for (int k = 0; k < horizon; ++k)
+      std::printf("force3 %d %d %.17g %.17g %.17g\n", i, k, f3[(size_t)(i * 3 * horizon + 3 * k)],
+                  f3[(size_t)(i * 3 * horizon + 3 * k + 1)], f3[(size_t)(i * 3 * horizon + 3 * k + 2)]);
+  {
+    const std::vector<double>& fp = mpc.FootPositions();
+    for (int i = 0; i < num_legs; ++i)
+      for (int j = 0; j <= horizon; ++j)
+        std::printf("foot3 %d %d %.17g %.17g %.17g\n", i, j, fp[(size_t)i * 3 * (horizon + 1) + 3 * j],
+                    fp[(size_t)i * 3 * (horizon + 1) + 3 * j + 1], fp[(size_t)i * 3 * (horizon + 1) + 3 * j + 2]);
+  }
+  mpc.setNonlinear(false);
   // "mpc table invalid" (CentroidalMPC.cpp:328-330)
   std::vector<double> bad = des_input;
   for (int i = 0; i < num_legs; ++i) bad[(size_t)i * (4 * horizon + 3) + 2] = 0;

@@ -399,14 +399,18 @@ def test_cpp_centroidal_mpc_driver(cpp_bins, op):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "caught mpc table invalid" in r.stdout
     z = _load("centoid_mpc_test_N6")
-    u = np.zeros((6, 4, 3))
-    u2 = np.zeros((6, 4, 3))
+    u, u2, u3 = np.zeros((6, 4, 3)), np.zeros((6, 4, 3)), np.zeros((6, 4, 3))
+    feet2, feet3 = np.zeros((7, 4, 3)), np.zeros((7, 4, 3))
     for line in r.stdout.splitlines():
         if line.startswith("status"):
             assert line.split()[1] == "0"
         if line.startswith("force"):
             tag, i, k, fx, fy, fz = line.split()
-            (u if tag == "force" else u2)[int(k), int(i)] = [float(fx), float(fy), float(fz)]
+            {"force": u, "force2": u2, "force3": u3}[tag][int(k), int(i)] = [float(fx), float(fy), float(fz)]
+        if line.startswith("foot"):
+            tag, i, j, px, py, pz = line.split()
+            {"foot2": feet2, "foot3": feet3}[tag][int(j), int(i)] = [float(px), float(py), float(pz)]
+    assert "status3 0" in r.stdout
     assert rel_err(u, z["u"][0]) < 1e-6
     # second call: state[9+6] (rh foot x) moved 2 cm -> the record's node 0 moves, U changes, oracle agrees
     foot2 = z["foot"].copy()
@@ -416,6 +420,14 @@ def test_cpp_centroidal_mpc_driver(cpp_bins, op):
     assert sr2[0] == 0
     assert rel_err(u2, ur2[0]) < 1e-6
     assert rel_err(u2, u) > 1e-4
+    # QP mode's foot_pos output: the frozen footholds (node 0 current, later runs at the mean des, swing des)
+    assert np.array_equal(feet2, op.feet_table(mo, foot2[0], z["contact"][0], np.zeros((6, 4, 3))))
+    # setNonlinear(true): the reference's NLP with the later runs' footholds as variables (oracle_sqp_solve_feet)
+    ur3, Dr3, feetr3, _, sr3, _, _ = op.sqp_solve_feet(mo, op.default_settings(), z["x0"][0], z["xref"][0],
+                                                       z["foot"][0], z["contact"][0], sqp_iter_max=10, sqp_tol=1e-7)
+    assert sr3 == 0 and np.abs(Dr3).max() > 1e-4  # the footholds move
+    assert rel_err(u3, ur3) < 1e-6
+    assert np.abs(feet3 - feetr3).max() < 1e-8
 
 
 @pytest.mark.gpu
