@@ -68,7 +68,8 @@ namespace {
 // one problem in the engine's packed forms (cmpc.h: OCP record [A,B,b] per stage then [Q,S,R,q,r] per node;
 // constraint record [C,D,e] per node with rows), column-major blocks as Eigen stores them
 struct Packed {
-  int N = 0, nx = 0;
+  int N = 0, nx = 0;        // nx: the padded state dimension, max over the nodes
+  std::vector<int> nxk;     // the problem's own state dimension per node (OcpSize::numStates)
   std::vector<int> nu, nc;
   std::vector<double> rec, crec;
   std::vector<size_t> coff;  // start of node k's [C, D, e] in crec
@@ -103,40 +104,59 @@ class HpipmInterface::Impl {
                                std::to_string(constraints->size()) + " with " + std::to_string(N + 1) + " nodes.");
     Packed p;
     p.N = N;
-    p.nx = (int)x0.size();
-    const int nx = p.nx;
+    // per-node state dimensions (OcpSize::numStates, HPIPM's nx[k]): node k's state is embedded in the first
+    // nxk[k] components of a padded state of dimension nx = max_k nxk[k]; the padding rows and columns of A, B, b,
+    // Q, S, q and C are 0, so padding states stay 0 and never couple (the device path takes one nx per problem)
+    p.nxk.assign((size_t)N + 1, 0);
+    p.nxk[0] = (int)x0.size();
     p.nu.assign((size_t)N, 0);
     for (int k = 0; k < N; ++k) {
-      p.nu[(size_t)k] = (int)dyn[(size_t)k].dfdu.cols();
-      if ((int)dyn[(size_t)k].dfdx.rows() != nx || (int)dyn[(size_t)k].dfdx.cols() != nx)
-        throw std::runtime_error("[HpipmInterface] constant state dimension required");
+      const auto& d = dyn[(size_t)k];
+      p.nu[(size_t)k] = (int)d.dfdu.cols();
+      p.nxk[(size_t)k + 1] = (int)d.dfdx.rows();
+      if ((int)d.dfdx.cols() != p.nxk[(size_t)k] || (int)d.f.size() != p.nxk[(size_t)k + 1] ||
+          (p.nu[(size_t)k] > 0 && (int)d.dfdu.rows() != p.nxk[(size_t)k + 1]))
+        throw std::runtime_error("[HpipmInterface] dynamics " + std::to_string(k) + " has inconsistent sizes");
     }
+    for (int k = 0; k <= N; ++k) {
+      const auto& c = cost[(size_t)k];
+      const int m = k < N ? p.nu[(size_t)k] : 0;
+      if ((int)c.dfdxx.rows() != p.nxk[(size_t)k] || (int)c.dfdxx.cols() != p.nxk[(size_t)k] ||
+          (int)c.dfdx.size() != p.nxk[(size_t)k] ||
+          (m > 0 && ((int)c.dfduu.rows() != m || (int)c.dfdux.rows() != m || (int)c.dfdux.cols() != p.nxk[(size_t)k])))
+        throw std::runtime_error("[HpipmInterface] cost " + std::to_string(k) + " has inconsistent sizes");
+    }
+    p.nx = *std::max_element(p.nxk.begin(), p.nxk.end());
+    const int nx = p.nx;
     p.rec.assign(cmpc_ocp_record_size(N, nx, p.nu.data()), 0.0);
     size_t o = 0;
-    auto put = [&](const double* src, size_t n) {
-      for (size_t i = 0; i < n; ++i) p.rec[o + i] = src ? src[i] : 0.0;
-      o += n;
+    // column-major r x c block (src may be null) into an R x C slot, zero padded
+    auto put = [&](const double* src, int r, int c, int R, int Cc) {
+      for (int j = 0; j < Cc; ++j)
+        for (int i = 0; i < R; ++i) p.rec[o + (size_t)j * R + i] = (src && i < r && j < c) ? src[(size_t)j * r + i] : 0.0;
+      o += (size_t)R * Cc;
     };
     for (int k = 0; k < N; ++k) {
       const auto& d = dyn[(size_t)k];
-      put(d.dfdx.data(), (size_t)nx * nx);
-      put(d.dfdu.data(), (size_t)nx * p.nu[(size_t)k]);
-      put(d.f.data(), (size_t)nx);
+      const int r = p.nxk[(size_t)k + 1], c = p.nxk[(size_t)k], m = p.nu[(size_t)k];
+      put(d.dfdx.data(), r, c, nx, nx);
+      put(m ? d.dfdu.data() : nullptr, r, m, nx, m);
+      put(d.f.data(), r, 1, nx, 1);
     }
     const double reg = settings_.reg_prim;
     for (int k = 0; k <= N; ++k) {
       const auto& c = cost[(size_t)k];
-      const size_t m = k < N ? (size_t)p.nu[(size_t)k] : 0;
+      const int m = k < N ? p.nu[(size_t)k] : 0, xk = p.nxk[(size_t)k];
       const size_t oq = o;
-      put(c.dfdxx.data(), (size_t)nx * nx);
+      put(c.dfdxx.data(), xk, xk, nx, nx);
       if (k > 0)  // HPIPM's primal regularisation; node 0's state is eliminated
-        for (int i = 0; i < nx; ++i) p.rec[oq + (size_t)i * nx + i] += reg;
-      put(m ? c.dfdux.data() : nullptr, m * nx);
+        for (int i = 0; i < xk; ++i) p.rec[oq + (size_t)i * nx + i] += reg;
+      put(m ? c.dfdux.data() : nullptr, m, xk, m, nx);
       const size_t orr = o;
-      put(m ? c.dfduu.data() : nullptr, m * m);
-      for (size_t i = 0; i < m; ++i) p.rec[orr + i * m + i] += reg;
-      put(c.dfdx.data(), (size_t)nx);
-      put(m ? c.dfdu.data() : nullptr, m);
+      put(m ? c.dfduu.data() : nullptr, m, m, m, m);
+      for (int i = 0; i < m; ++i) p.rec[orr + (size_t)i * m + i] += reg;
+      put(c.dfdx.data(), xk, 1, nx, 1);
+      put(m ? c.dfdu.data() : nullptr, m, 1, m, 1);
     }
     int nU = 0;
     for (int v : p.nu) nU += v;
@@ -153,24 +173,29 @@ class HpipmInterface::Impl {
         const int m = k < N ? p.nu[(size_t)k] : 0;
         p.coff[(size_t)k] = p.crec.size();
         if (rows == 0) continue;
-        if ((int)c.dfdx.rows() != rows || (int)c.dfdx.cols() != nx ||
+        const int xk = p.nxk[(size_t)k];
+        if ((int)c.dfdx.rows() != rows || (int)c.dfdx.cols() != xk ||
             (m > 0 && ((int)c.dfdu.rows() != rows || (int)c.dfdu.cols() != m)))
           throw std::runtime_error("[HpipmInterface] constraint " + std::to_string(k) + " has inconsistent sizes");
         p.nc[(size_t)k] = rows;
         nE += rows;
-        p.crec.insert(p.crec.end(), c.dfdx.data(), c.dfdx.data() + (size_t)rows * nx);
+        p.crec.insert(p.crec.end(), c.dfdx.data(), c.dfdx.data() + (size_t)rows * xk);
+        p.crec.insert(p.crec.end(), (size_t)rows * (nx - xk), 0.0);  // padding state columns
         if (m > 0) p.crec.insert(p.crec.end(), c.dfdu.data(), c.dfdu.data() + (size_t)rows * m);
         p.crec.insert(p.crec.end(), c.f.data(), c.f.data() + rows);
       }
       p.coff[(size_t)N + 1] = p.crec.size();
     }
     std::vector<double> x((size_t)(N + 1) * nx), u((size_t)(nU > 0 ? nU : 1));
+    std::vector<double> x0p((size_t)nx, 0.0);
+    for (int i = 0; i < p.nxk[0]; ++i) x0p[(size_t)i] = x0(i);
     int status = -1;
-    deviceSolve(p, nE > 0, 1, x0.data(), x.data(), u.data(), &status);
+    deviceSolve(p, nE > 0, 1, x0p.data(), x.data(), u.data(), &status);
     xs.assign((size_t)N + 1, vector_t());
     for (int k = 0; k <= N; ++k) {
-      xs[(size_t)k].resize(nx);
-      for (int i = 0; i < nx; ++i) xs[(size_t)k](i) = k == 0 ? x0(i) : x[(size_t)k * nx + i];
+      const int xk = p.nxk[(size_t)k];
+      xs[(size_t)k].resize(xk);
+      for (int i = 0; i < xk; ++i) xs[(size_t)k](i) = k == 0 ? x0(i) : x[(size_t)k * nx + i];
     }
     us.assign((size_t)N, vector_t());
     int off = 0;
@@ -179,7 +204,7 @@ class HpipmInterface::Impl {
       for (int i = 0; i < p.nu[(size_t)k]; ++i) us[(size_t)k](i) = u[(size_t)off + i];
       off += p.nu[(size_t)k];
     }
-    if (verbose) printStatus(p, nE > 0, x0.data(), x, u, status);
+    if (verbose) printStatus(p, nE > 0, x0p.data(), x, u, status);
     last_ = std::move(p);
     lastConstrained_ = nE > 0;
     riccatiValid_ = false;
@@ -190,7 +215,8 @@ class HpipmInterface::Impl {
   void riccati(const VectorFunctionLinearApproximation& dyn0, const ScalarFunctionQuadraticApproximation& cost0) {
     const int N = last_.N;
     if (N == 0) throw std::runtime_error("[HpipmInterface] no solved problem to take Riccati quantities from");
-    if ((int)dyn0.dfdx.rows() != last_.nx || (int)dyn0.dfdu.cols() != last_.nu[0] || (int)cost0.dfdxx.rows() != last_.nx)
+    if ((int)dyn0.dfdx.rows() != last_.nxk[1] || (int)dyn0.dfdx.cols() != last_.nxk[0] ||
+        (int)dyn0.dfdu.cols() != last_.nu[0] || (int)cost0.dfdxx.rows() != last_.nxk[0])
       throw std::runtime_error("[HpipmInterface] dynamics0 / cost0 do not match the last solved problem");
     if (riccatiValid_) return;
     const int nx = last_.nx;
@@ -217,11 +243,13 @@ class HpipmInterface::Impl {
     riccati(d0, c0);
     const int N = last_.N, nx = last_.nx;
     std::vector<ScalarFunctionQuadraticApproximation> out((size_t)N + 1);
-    for (int k = 0; k <= N; ++k) {
-      out[(size_t)k].dfdxx.resize(nx, nx);
-      out[(size_t)k].dfdx.resize(nx);
-      std::copy(Sm_.begin() + (long)k * nx * nx, Sm_.begin() + (long)(k + 1) * nx * nx, out[(size_t)k].dfdxx.data());
-      std::copy(sv_.begin() + (long)k * nx, sv_.begin() + (long)(k + 1) * nx, out[(size_t)k].dfdx.data());
+    for (int k = 0; k <= N; ++k) {  // node k's own nxk x nxk block of the padded S_k
+      const int xk = last_.nxk[(size_t)k];
+      out[(size_t)k].dfdxx.resize(xk, xk);
+      out[(size_t)k].dfdx.resize(xk);
+      for (int j = 0; j < xk; ++j)
+        for (int i = 0; i < xk; ++i) out[(size_t)k].dfdxx(i, j) = Sm_[(size_t)k * nx * nx + (size_t)j * nx + i];
+      for (int i = 0; i < xk; ++i) out[(size_t)k].dfdx(i) = sv_[(size_t)k * nx + i];
       out[(size_t)k].f = 0.0;
     }
     return out;
@@ -232,9 +260,9 @@ class HpipmInterface::Impl {
     matrix_array_t out((size_t)N);
     size_t o = 0;
     for (int k = 0; k < N; ++k) {
-      const int m = last_.nu[(size_t)k];
-      out[(size_t)k].resize(m, nx);
-      std::copy(K_.begin() + (long)o, K_.begin() + (long)(o + (size_t)m * nx), out[(size_t)k].data());
+      const int m = last_.nu[(size_t)k], xk = last_.nxk[(size_t)k];
+      out[(size_t)k].resize(m, xk);  // the first nxk columns of the padded m x nx gain (column-major)
+      std::copy(K_.begin() + (long)o, K_.begin() + (long)(o + (size_t)m * xk), out[(size_t)k].data());
       o += (size_t)m * nx;
     }
     return out;

@@ -34,6 +34,9 @@ class HpipmInterface {
    * rows C dx + D du + e = 0 are imposed as the reference's lg = ug rows (HpipmInterface.cpp:223-264) by
    * cmpc_ocp_solve_batch_eq_host (x0-eliminated stage 0, redundant rows dropped, inconsistent rows -> INCONS_EQ,
    * where HPIPM's interior point method would stop at MAX_ITER or MIN_STEP instead: status parity unpinned).
+   * The state dimension may change along the horizon (OcpSize::numStates[k], OcpSize.cpp:55-60): each node's state is
+   * embedded in a zero-padded state of the largest dimension, whose padding never couples, and every output (state
+   * trajectory, S_k, K_k) comes back in the node's own dimension.
    * Settings::reg_prim is added to the input Hessians (and the state Hessians of nodes 1..N); the other settings
    * parametrise an interior point method this direct solve does not run (HpipmInterfaceSettings.h).
    * verbose: the reference's status line, iteration count, max residuals and statistics table (one row: the

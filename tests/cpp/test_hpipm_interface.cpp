@@ -435,6 +435,110 @@ static void constrained_riccati() {
   CHECK(e_sym < 1e-9, "constrained riccati S symmetric");
 }
 
+// Per-node state dimensions (OcpSize::numStates[k], OcpSize.cpp:55-60; HPIPM takes nx[k] per node): a known
+// solution (the knownSolution construction with nx changing along the horizon), the Riccati quantities against the
+// closed-form recursion (retrieveRiccati's, with rectangular A_k), and an equality row at a node whose state is
+// smaller than the largest.
+static void varying_state_dims() {
+  const int N = 5, nu = 2;
+  const int nxk[N + 1] = {3, 4, 2, 3, 4, 3};
+  std::vector<vector_t> xg{randv(nxk[0])}, ug;
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    ug.push_back(randv(nu));
+    VectorFunctionLinearApproximation d;
+    d.dfdx = randm(nxk[k + 1], nxk[k]);
+    d.dfdu = randm(nxk[k + 1], nu);
+    d.f = randv(nxk[k + 1]);
+    sys.push_back(d);
+    vector_t xn = d.f;
+    const vector_t ax = mv(d.dfdx, xg[(size_t)k]), bu = mv(d.dfdu, ug[(size_t)k]);
+    for (int i = 0; i < nxk[k + 1]; ++i) xn[i] += ax[i] + bu[i];
+    xg.push_back(xn);
+    cost.push_back(randomCost(nxk[k], nu));
+    const vector_t qx = mv(cost[(size_t)k].dfdxx, xg[(size_t)k]), su = mtv(cost[(size_t)k].dfdux, ug[(size_t)k]);
+    for (int i = 0; i < nxk[k]; ++i) cost[(size_t)k].dfdx[i] = -(qx[i] + su[i]);
+    const vector_t ru = mv(cost[(size_t)k].dfduu, ug[(size_t)k]), sx = mv(cost[(size_t)k].dfdux, xg[(size_t)k]);
+    for (int i = 0; i < nu; ++i) cost[(size_t)k].dfdu[i] = -(ru[i] + sx[i]);
+  }
+  cost.push_back(randomCost(nxk[N], 0));
+  const vector_t qN = mv(cost[(size_t)N].dfdxx, xg[(size_t)N]);
+  for (int i = 0; i < nxk[N]; ++i) cost[(size_t)N].dfdx[i] = -qN[i];
+  const auto size = hpipm_interface::extractSizesFromProblem(sys, cost, nullptr);
+  CHECK(size.numStates[2] == 2 && size.numStates[4] == 4, "varying nx: extractSizesFromProblem");
+  HpipmInterface hpipm(size);
+  vector_array_t xs, us;
+  auto st = hpipm.solve(xg[0], sys, cost, nullptr, xs, us, false);
+  CHECK(st == SUCCESS, "varying nx status");
+  double e = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    CHECK(xs[(size_t)k].size() == nxk[k], "varying nx: x size");
+    e = std::fmax(e, maxdiff(xs[(size_t)k], xg[(size_t)k]));
+  }
+  for (int k = 0; k < N; ++k) e = std::fmax(e, maxdiff(us[(size_t)k], ug[(size_t)k]));
+  // Riccati quantities vs the closed-form recursion over rectangular A_k
+  std::vector<matrix_t> SmG((size_t)N + 1), KG((size_t)N);
+  std::vector<vector_t> svG((size_t)N + 1), kG((size_t)N);
+  SmG[(size_t)N] = cost[(size_t)N].dfdxx;
+  svG[(size_t)N] = cost[(size_t)N].dfdx;
+  for (int k = N - 1; k >= 0; --k) {
+    const matrix_t& Sm = SmG[(size_t)k + 1];
+    const vector_t& sv = svG[(size_t)k + 1];
+    const auto& A = sys[(size_t)k].dfdx;
+    const auto& B = sys[(size_t)k].dfdu;
+    const auto& b = sys[(size_t)k].f;
+    const auto& c = cost[(size_t)k];
+    const matrix_t P = add(c.dfdux, mm(tr(B), mm(Sm, A)));
+    const matrix_t invR = inv(add(c.dfduu, mm(tr(B), mm(Sm, B))));
+    const vector_t rr = addv(addv(c.dfdu, mtv(B, sv)), mtv(B, mv(Sm, b)));
+    SmG[(size_t)k] = add(add(c.dfdxx, mm(tr(A), mm(Sm, A))), mm(tr(P), mm(invR, P)), -1.0);
+    svG[(size_t)k] = addv(addv(addv(c.dfdx, mtv(A, sv)), mtv(A, mv(Sm, b))), mv(tr(P), mv(invR, rr)), -1.0);
+    KG[(size_t)k] = add(zeros(nu, nxk[k]), mm(invR, P), -1.0);
+    kG[(size_t)k] = mv(invR, rr);
+    for (int i = 0; i < kG[(size_t)k].size(); ++i) kG[(size_t)k][i] = -kG[(size_t)k][i];
+  }
+  const auto K = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  const auto kf = hpipm.getRiccatiFeedforward(sys[0], cost[0]);
+  const auto ctg = hpipm.getRiccatiCostToGo(sys[0], cost[0]);
+  double er = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    CHECK(ctg[(size_t)k].dfdxx.rows() == nxk[k] && ctg[(size_t)k].dfdx.size() == nxk[k], "varying nx: S size");
+    er = std::fmax(er, maxdiffm(ctg[(size_t)k].dfdxx, SmG[(size_t)k]));
+    er = std::fmax(er, maxdiff(ctg[(size_t)k].dfdx, svG[(size_t)k]));
+  }
+  for (int k = 0; k < N; ++k) {
+    CHECK(K[(size_t)k].rows() == nu && K[(size_t)k].cols() == nxk[k], "varying nx: K size");
+    er = std::fmax(er, maxdiffm(K[(size_t)k], KG[(size_t)k]));
+    er = std::fmax(er, maxdiff(kf[(size_t)k], kG[(size_t)k]));
+  }
+  // one equality row at node 2 (nx = 2): C dx + D du + e = 0 holds at the solution, u = K x + k
+  std::vector<VectorFunctionLinearApproximation> cons((size_t)N + 1);
+  for (int k = 0; k <= N; ++k) {
+    cons[(size_t)k].dfdx = zeros(0, nxk[k]);
+    cons[(size_t)k].dfdu = zeros(0, k < N ? nu : 0);
+    cons[(size_t)k].f = vector_t(0);
+  }
+  cons[2] = randomConstraints(nxk[2], nu, 1);
+  HpipmInterface hc(hpipm_interface::extractSizesFromProblem(sys, cost, &cons));
+  vector_array_t xc, uc;
+  st = hc.solve(xg[0], sys, cost, &cons, xc, uc, false);
+  CHECK(st == SUCCESS, "varying nx constrained status");
+  const vector_t cr = addv(addv(mv(cons[2].dfdx, xc[2]), mv(cons[2].dfdu, uc[2])), cons[2].f);
+  double ec = std::fabs(cr[0]);
+  for (int k = 0; k < N; ++k) {
+    vector_t xn = sys[(size_t)k].f;
+    const vector_t ax = mv(sys[(size_t)k].dfdx, xc[(size_t)k]), bu = mv(sys[(size_t)k].dfdu, uc[(size_t)k]);
+    for (int i = 0; i < nxk[k + 1]; ++i) xn[i] += ax[i] + bu[i];
+    ec = std::fmax(ec, maxdiff(xc[(size_t)k + 1], xn));
+  }
+  const auto Kc = hc.getRiccatiFeedback(sys[0], cost[0]);
+  const auto kc = hc.getRiccatiFeedforward(sys[0], cost[0]);
+  for (int k = 0; k < N; ++k) ec = std::fmax(ec, maxdiff(uc[(size_t)k], addv(mv(Kc[(size_t)k], xc[(size_t)k]), kc[(size_t)k])));
+  std::printf("varying state dims: solution %.3e riccati %.3e constrained %.3e\n", e, er, ec);
+  CHECK(e < 1e-9 && er < 1e-9 && ec < 1e-8, "varying state dims");
+}
+
 int main() {
   dynamics_feasible(false);
   dynamics_feasible(true);
@@ -443,6 +547,7 @@ int main() {
   with_constraints();
   retrieve_riccati();
   constrained_riccati();
+  varying_state_dims();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;
 }

@@ -373,6 +373,7 @@ def test_cpp_hpipm_interface_mirror(cpp_bins):
     r = subprocess.run([str(cpp_bins / "test_hpipm_interface")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASSED" in r.stdout
+    assert "varying state dims" in r.stdout  # OcpSize::numStates per node (OcpSize.cpp:55-60)
 
 
 def test_cpp_hpipm_interface_mirror_ocs2_types(cpp_bins):
