@@ -214,6 +214,9 @@ def main():
     ap.add_argument("--sqp-iters", type=int, default=0,
                     help="> 0: one step = the batched SQP on the bilinear NLP (cmpc_sqp_solve_batch), this many "
                          "SQP iterations at most; not the headline metric")
+    ap.add_argument("--nlp", action="store_true",
+                    help="with --sqp-iters: the reference's NLP with the later runs' footholds as decision variables "
+                         "(cmpc_nlp_solve_batch) instead of frozen footholds")
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent batches in flight: step i runs on context / stream i %% K (a serving pattern; "
                          "each step is still one full batch through the whole hot path). Default 1: the headline")
@@ -280,10 +283,14 @@ def main():
 
     sqp_qi = cm.DeviceArray((B,), np.int32)
     sqp_si = cm.DeviceArray((B,), np.int32)
+    feet_out = cm.DeviceArray((B, N + 1, 4, 3), np.float64) if args.nlp else None
 
     def step(i):
         e, (uo, so, io), sh = engs[i % K], outs[i % K], streams[i % K]
-        if args.sqp_iters > 0:
+        if args.sqp_iters > 0 and args.nlp:
+            cm.lib().cmpc_nlp_solve_batch(e.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, args.sqp_iters, 1e-6,
+                                          uo.ptr, feet_out.ptr, None, so.ptr, sqp_qi.ptr, sqp_si.ptr, sh)
+        elif args.sqp_iters > 0:
             cm.lib().cmpc_sqp_solve_batch(e.ctx, B, x0.ptr, xref.ptr, foot.ptr, contact.ptr, args.sqp_iters, 1e-6,
                                           uo.ptr, None, so.ptr, sqp_qi.ptr, sqp_si.ptr, sh)
         else:
@@ -476,7 +483,8 @@ def main():
     }
     if args.sqp_iters > 0:
         si = sqp_si.host()
-        result["metric"] = "centroidal NLP solves/sec by batched SQP (bilinear lever arm), not the headline metric"
+        result["metric"] = ("centroidal NLP solves/sec by batched SQP (bilinear lever arm"
+                            + (", footholds as variables" if args.nlp else "") + "), not the headline metric")
         result["unit"] = "NLPs/s"
         result["solver"]["mean_sqp_iters"] = float(si.mean())
         result["solver"]["mean_iters"] = float(iters[ok].mean()) if ok.any() else 0.0
