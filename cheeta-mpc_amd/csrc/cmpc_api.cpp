@@ -206,6 +206,7 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.lin = nullptr;
   a.ubar = nullptr;
   a.dbar = nullptr;
+  a.skip = nullptr;
   a.H = (T*)c->H;
   a.g = (T*)c->g;
   a.tri_mu = (T*)c->tri_mu;
@@ -261,11 +262,12 @@ IpmArgs<T> ipm_args(cmpc_ctx* c) {
 template <typename T>
 int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                    const uint8_t* contact, hipStream_t st, const double* lin, bool* lists, const double* ubar,
-                   const double* dbar) {
+                   const double* dbar, const int* skip) {
   CondenseArgs<T> a = condense_args<T>(c, x0, xref, foot, contact);
   a.lin = lin;
   a.ubar = ubar;
   a.dbar = dbar;
+  a.skip = skip;
   *lists = false;
   // the one-wave condensing has no foothold columns: with footholds every QP goes through the workgroup kernel
   const bool small = c->model.N <= CMPC_C64_MAXN && !dbar;
@@ -291,12 +293,14 @@ int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, con
 
 int run_condense(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
                  const uint8_t* contact, hipStream_t st, const double* lin = nullptr, bool* lists = nullptr,
-                 const double* ubar = nullptr, const double* dbar = nullptr) {
+                 const double* ubar = nullptr, const double* dbar = nullptr, const int* skip = nullptr) {
   bool dummy = false;
   if (!lists) lists = &dummy;
   int r;
-  if (c->precision == CMPC_F64) r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin, lists, ubar, dbar);
-  else r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin, lists, ubar, dbar);
+  if (c->precision == CMPC_F64)
+    r = run_condense_t<double>(c, B, x0, xref, foot, contact, st, lin, lists, ubar, dbar, skip);
+  else
+    r = run_condense_t<float>(c, B, x0, xref, foot, contact, st, lin, lists, ubar, dbar, skip);
   return r == 0 ? CMPC_OK : (r == -1 ? CMPC_ERR_ARG : CMPC_ERR_HIP);
 }
 
@@ -792,6 +796,7 @@ int sqp_run(cmpc_ctx* c, int B, const double* x0, const double* xref, const doub
   if (r != CMPC_OK) return r;
   SqpArgs a;
   a.model = c->d_model;
+  a.N = c->model.N;
   a.x0 = x0;
   a.xref = xref;
   a.foot = foot;
@@ -816,8 +821,9 @@ int sqp_run(cmpc_ctx* c, int B, const double* x0, const double* xref, const doub
   if (launch_sqp(0, a, B, st) != 0) return CMPC_ERR_HIP;
   for (int it = 0; it < sqp_iter_max; ++it) {
     bool lists = false;
+    // QPs whose SQP has converged are not condensed or solved again (CondenseArgs::skip = done)
     r = run_condense(c, B, x0, xref, foot, contact, st, c->lin, &lists, feet ? c->uj : nullptr,
-                     feet ? c->dj : nullptr);
+                     feet ? c->dj : nullptr, c->done);
     if (r != CMPC_OK) return r;
     if (launch_pack_warm(c->uj, c->tri_map, c->nvar, c->status, c->precision, c->ld, c->model.N, c->u, B, st,
                          feet ? c->dj : nullptr) != 0)

@@ -12,6 +12,9 @@ namespace cmpc {
 #define CMPC_IPM_MAX_N 256
 
 // class-padded size of a condensed problem
+// internal per-QP status of a QP the SQP no longer solves (CondenseArgs::skip); never returned to the caller
+#define CMPC_STATUS_SKIPPED 100
+
 __host__ __device__ inline int ipm_class(int n) { return n <= 64 ? 64 : (n <= 128 ? 128 : 256); }
 
 // Position of H[i][j] inside a QP's class-packed block. Class 64 is stored in the 4 x 16-cyclic register order of
@@ -43,6 +46,9 @@ struct CondenseArgs {
   // tri_map N L + s L + leg (oracle_condense_feet)
   const double* ubar;
   const double* dbar;
+  // SQP: skip[q] != 0 marks a QP whose SQP has converged; it is not condensed (nvar 0 and, if it was SUCCESS, status
+  // CMPC_STATUS_SKIPPED, so no IPM class, warm pack or list takes it). Null: every QP.
+  const int* skip;
   T* H;
   T* g;
   T* tri_mu;
@@ -200,6 +206,7 @@ int launch_pack_qp(const double* H, const double* g, const double* tri_mu, const
 // batched SQP on the bilinear NLP (k_sqp.hip)
 struct SqpArgs {
   const DevModel* model;
+  int N;               // horizon (host copy of model->N: sizes the kernels' LDS)
   const double* x0;
   const double* xref;
   const double* foot;

@@ -13,6 +13,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     if ((unsigned)q >= gridDim.x) return;  // grid = batch
   }
   if (a.n_lo > 0 && a.nvar[q] <= a.n_lo) return;  // finished (or rejected) by a smaller class
+  if (a.skip && a.skip[q]) {                       // converged SQP (CondenseArgs::skip)
+    if (threadIdx.x == 0) {  // a rejected / failed QP keeps its status; a solved one keeps its residuals
+      if (a.status[q] == CMPC_SUCCESS) a.status[q] = CMPC_STATUS_SKIPPED;
+      a.nvar[q] = 0;
+    }
+    return;
+  }
   (void)srbd_condense_qp<T, NMAX, WAVES, false, FEET>(a, q, nullptr);
 }
 

@@ -30,6 +30,13 @@ namespace cmpc {
 
 template <typename T>
 __global__ __launch_bounds__(64) void k_condense64(CondenseArgs<T> a) {
+  if (a.skip && a.skip[blockIdx.x]) {  // converged SQP (CondenseArgs::skip)
+    if (threadIdx.x == 0) {  // a rejected / failed QP keeps its status; a solved one keeps its residuals
+      if (a.status[blockIdx.x] == CMPC_SUCCESS) a.status[blockIdx.x] = CMPC_STATUS_SKIPPED;
+      a.nvar[blockIdx.x] = 0;
+    }
+    return;
+  }
   __shared__ c64::C64Lds<T> S;
   T K[64], g, mu;
   (void)condense64_qp<T>(a, (int)blockIdx.x, S, K, g, mu);

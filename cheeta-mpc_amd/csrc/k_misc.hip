@@ -276,7 +276,8 @@ __global__ void k_residuals(const double* res, const int* status, int B, double*
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 4 * B) return;
   const int st = status[i / 4];
-  out[i] = (st >= CMPC_SUCCESS && st <= CMPC_NAN_SOL) ? res[i] : __builtin_nan("");
+  // CMPC_STATUS_SKIPPED: a converged SQP's QP, whose residuals are those of its last IPM run
+  out[i] = ((st >= CMPC_SUCCESS && st <= CMPC_NAN_SOL) || st == CMPC_STATUS_SKIPPED) ? res[i] : __builtin_nan("");
 }
 int launch_residuals(const double* res_ws, const int* status, int B, double* out, hipStream_t stream) {
   if (B <= 0) return 0;

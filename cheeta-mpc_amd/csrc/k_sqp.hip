@@ -17,8 +17,9 @@
 //
 // One wave per QP: lanes 0..13 evaluate the fourteen trial steps 2^-m (2^-13 >= alpha_min = 1e-4 > 2^-14), lane 14
 // the current iterate, lane 15 the linearised response |dx| and the descent metric, lane 16 |du|, each lane one whole
-// sequential pass (13 states x N steps); the step, the convergence test and the next linearisation point are then
-// lane-parallel over the 12 N inputs.
+// sequential pass (13 states x N steps) over the QP's data staged in LDS by the whole wave first (View: the lever-arm
+// points and Theta blocks precomputed once instead of per pass); the step, the convergence test and the next
+// linearisation point are then lane-parallel over the 12 N inputs.
 #include <hip/hip_runtime.h>
 
 #include "cmpc/cmpc.h"
@@ -36,6 +37,85 @@ constexpr double SQP_COST_TOL = 1e-4;
 
 #pragma clang fp contract(off)
 
+// One QP's read-only data, staged in LDS by the whole wave before the sequential per-lane passes (each lane's rollout
+// is a long dependent chain; from LDS its operands arrive in tens of cycles instead of a global-load latency each):
+// x0, xref, des foot table, contact flags, the lever-arm point of every stance (k, leg) (stance_point), the first step
+// of its run, dt-free Theta blocks s2 = I_b^-1 R_z(psi_k)^T per step (the oracle's s2, same operations), and the
+// iterate / QP solution forces and foothold offsets. Dynamic LDS, sqp_lds_bytes(N).
+struct View {
+  double *x0, *xr, *des, *pb, *S2, *u0, *u1, *D0, *D1;
+  uint8_t* ct;
+  int* rs;
+};
+
+__host__ __device__ inline size_t sqp_lds_doubles(int N) { return 16 + (size_t)(N + 1) * (NX + NL * 3) + (size_t)N * (NL * 3 + 9 + 4 * NU); }
+__host__ __device__ inline size_t sqp_lds_bytes(int N) {
+  return sqp_lds_doubles(N) * 8 + (size_t)N * NL * (sizeof(int) + 1);
+}
+
+__device__ View carve(unsigned char* sm, int N) {
+  View V;
+  double* p = reinterpret_cast<double*>(sm);
+  V.x0 = p; p += 16;
+  V.xr = p; p += (N + 1) * NX;
+  V.des = p; p += (N + 1) * NL * 3;
+  V.pb = p; p += N * NL * 3;
+  V.S2 = p; p += N * 9;
+  V.u0 = p; p += N * NU;
+  V.u1 = p; p += N * NU;
+  V.D0 = p; p += N * NU;
+  V.D1 = p; p += N * NU;
+  V.rs = reinterpret_cast<int*>(p);
+  V.ct = reinterpret_cast<uint8_t*>(V.rs + N * NL);
+  return V;
+}
+
+// Stage QP q (every lane calls; u1 / D0 / D1 may be null: not staged). The caller syncs before reading.
+__device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* u0, const double* u1, const double* D0,
+                      const double* D1) {
+  const DevModel* M = a.model;
+  const int N = M->N, lane = threadIdx.x;
+  View V = carve(sm, N);
+  const double* xr = a.xref + (size_t)q * (N + 1) * NX;
+  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
+  const uint8_t* ct = a.contact + (size_t)q * N * NL;
+  for (int i = lane; i < NX; i += 64) V.x0[i] = a.x0[(size_t)q * NX + i];
+  for (int i = lane; i < (N + 1) * NX; i += 64) V.xr[i] = xr[i];
+  for (int i = lane; i < (N + 1) * NL * 3; i += 64) V.des[i] = ft[i];
+  for (int i = lane; i < N * NL; i += 64) V.ct[i] = ct[i];
+  for (int i = lane; i < N * NU; i += 64) {
+    V.u0[i] = u0[i];
+    if (u1) V.u1[i] = u1[i];
+    if (D0) V.D0[i] = D0[i];
+    if (D1) V.D1[i] = D1[i];
+  }
+  // lever-arm points and run starts from the global record (the LDS copies are not visible before the sync)
+  auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
+  for (int sl = lane; sl < N * NL; sl += 64) {
+    const int k = sl / NL, i = sl % NL;
+    double p[3] = {0.0, 0.0, 0.0};
+    int s0 = 0;
+    if (ct[sl]) {
+      stance_point(ft, N, k, i, st, p);
+      s0 = run_start(k, i, st);
+    }
+    for (int d = 0; d < 3; ++d) V.pb[sl * 3 + d] = p[d];
+    V.rs[sl] = s0;
+  }
+  for (int k = lane; k < N; k += 64) {
+    double sp, cp;
+    sincos(xr[k * NX + 11], &sp, &cp);
+    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
+    for (int r = 0; r < 3; ++r)
+      for (int b = 0; b < 3; ++b) {
+        double s2 = 0.0;
+        for (int e = 0; e < 3; ++e) s2 += M->inv_inertia[r * 3 + e] * RzT[e * 3 + b];
+        V.S2[k * 9 + r * 3 + b] = s2;
+      }
+  }
+  return V;
+}
+
 // Foothold offset of the later run (s, leg) at the trial point D0 + alpha (D1 - D0) (D1 null: D0).
 __device__ __forceinline__ void trial_offset(const double* D0, const double* D1, double alpha, int s, int leg,
                                              double o[3]) {
@@ -47,21 +127,21 @@ __device__ __forceinline__ void trial_offset(const double* D0, const double* D1,
 
 // Foot tracking cost of the later runs at the trial footholds D0 + alpha (D1 - D0), or (deriv) its derivative at D0
 // along dD = D1 - D0: oracle foot_cost, same loop order (legs, runs by first step, nodes, components).
-__device__ double foot_cost(const DevModel* M, const double* foot, const uint8_t* ct, const double* D0,
-                            const double* D1, double alpha, bool deriv) {
+__device__ double foot_cost(const DevModel* M, const View& V, const double* D1, double alpha, bool deriv) {
   const int N = M->N;
+  const uint8_t* ct = V.ct;
   auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
   double J = 0.0;
   for (int i = 0; i < NL; ++i)
     for (int s = 1; s < N; ++s) {
       int e = 0;
       if (!later_start(N, s, i, st, &e)) continue;
-      double pb[3], dl[3];
-      stance_point(foot, N, s, i, st, pb);
-      trial_offset(D0, deriv ? nullptr : D1, alpha, s, i, dl);
+      const double* pb = V.pb + (s * NL + i) * 3;  // stance_point of the run
+      double dl[3];
+      trial_offset(V.D0, deriv ? nullptr : D1, alpha, s, i, dl);
       for (int j = s; j <= e + 1; ++j)
         for (int d = 0; d < 3; ++d) {
-          const double ed = (pb[d] + dl[d]) - foot[(j * NL + i) * 3 + d];
+          const double ed = (pb[d] + dl[d]) - V.des[(j * NL + i) * 3 + d];
           if (deriv)
             J += 2.0 * M->Wp[3 * i + d] * ed * (D1[(s * NL + i) * 3 + d] - dl[d]);
           else
@@ -71,23 +151,25 @@ __device__ double foot_cost(const DevModel* M, const double* foot, const uint8_t
   return J;
 }
 
-// Nonlinear rollout + NLP cost of the inputs u0 + alpha (u1 - u0) (u1 may be null: alpha unused) and, with footholds
-// (D0 non-null), the later runs' footholds D0 + alpha (D1 - D0) in the lever arm plus their tracking cost. Writes
+// Nonlinear rollout + NLP cost of the inputs u0 + alpha (u1 - u0) (has_u1 false: u0) and, with footholds (feet), the
+// later runs' footholds D0 + alpha (D1 - D0) (has_u1 false: D0) in the lever arm plus their tracking cost. Writes
 // lin [N][6] and x [(N+1)][13] when non-null. Mirrors oracle_nlp_rollout_cost_feet operation for operation.
-__device__ double rollout_cost(const DevModel* M, const double* x0, const double* xref, const double* foot,
-                               const uint8_t* ct, const double* u0, const double* u1, double alpha, double* lin,
-                               double* xo, const double* D0 = nullptr, const double* D1 = nullptr) {
+__device__ double rollout_cost(const DevModel* M, const View& V, bool has_u1, double alpha, double* lin, double* xo,
+                               bool feet) {
   const int N = M->N;
   const double dt = M->dt;
+  const double* u0 = V.u0;
+  const double* u1 = has_u1 ? V.u1 : nullptr;
+  const double* D1 = has_u1 ? V.D1 : nullptr;
   double xs[NX], xn[NX];
-  for (int s = 0; s < NX; ++s) xs[s] = x0[s];
+  for (int s = 0; s < NX; ++s) xs[s] = V.x0[s];
   if (xo)
     for (int s = 0; s < NX; ++s) xo[s] = xs[s];
   double J = 0.0;
   double unext[NU];
   auto input = [&](int k, int j) -> double {
-    const double a = u0[(size_t)k * NU + j];
-    return u1 ? a + alpha * (u1[(size_t)k * NU + j] - a) : a;
+    const double a = u0[k * NU + j];
+    return u1 ? a + alpha * (u1[k * NU + j] - a) : a;
   };
   for (int j = 0; j < NU; ++j) unext[j] = input(0, j);
   for (int k = 0; k < N; ++k) {
@@ -98,19 +180,17 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
     double F[3] = {0.0, 0.0, 0.0}, Tq[3] = {0.0, 0.0, 0.0};
     int ns = 0;
     for (int i = 0; i < NL; ++i) {
-      if (!ct[k * NL + i]) continue;
+      if (!V.ct[k * NL + i]) continue;
       ++ns;
       double p[3];
-      stance_point(foot, ct, N, k, i, p);
-      if (D0) {
-        const int s0 = run_start(k, i, [ct](int kk, int l) { return ct[kk * NL + l] != 0; });
-        if (s0 > 0) {
-          double dl[3];
-          trial_offset(D0, D1, alpha, s0, i, dl);
-          p[0] = p[0] + dl[0];
-          p[1] = p[1] + dl[1];
-          p[2] = p[2] + dl[2];
-        }
+      for (int d = 0; d < 3; ++d) p[d] = V.pb[(k * NL + i) * 3 + d];
+      const int s0 = V.rs[k * NL + i];
+      if (feet && s0 > 0) {
+        double dl[3];
+        trial_offset(V.D0, D1, alpha, s0, i, dl);
+        p[0] = p[0] + dl[0];
+        p[1] = p[1] + dl[1];
+        p[2] = p[2] + dl[2];
       }
       const double* f = uk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
@@ -128,7 +208,7 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
       }
     for (int j = 0; j < NU; ++j) {
       const int i = j / 3;
-      const double fd = (j % 3 == 2 && ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
+      const double fd = (j % 3 == 2 && V.ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
       const double e = uk[j] - fd;
       J += M->Wf[j] * e * e;
       if (k + 1 < N) {
@@ -136,70 +216,61 @@ __device__ double rollout_cost(const DevModel* M, const double* x0, const double
         J += M->Wr[j] * r * r;
       }
     }
-    double sp, cp;
-    sincos(xref[k * NX + 11], &sp, &cp);
-    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
     for (int d = 0; d < 3; ++d) xn[d] = xs[d] + dt * xs[3 + d];
     xn[3] = xs[3] + dt * (F[0] / M->mass);
     xn[4] = xs[4] + dt * (F[1] / M->mass);
     xn[5] = xs[5] + dt * (xs[12] + F[2] / M->mass);
     for (int d = 0; d < 3; ++d) xn[6 + d] = xs[6 + d] + dt * Tq[d];
-    for (int a = 0; a < 3; ++a) {
+    for (int r = 0; r < 3; ++r) {
       double m = 0.0;
-      for (int b = 0; b < 3; ++b) {
-        double s2 = 0.0;
-        for (int e = 0; e < 3; ++e) s2 += M->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
-        m += dt * s2 * xs[6 + b];
-      }
-      xn[9 + a] = xs[9 + a] + m;
+      for (int b = 0; b < 3; ++b) m += dt * V.S2[k * 9 + r * 3 + b] * xs[6 + b];
+      xn[9 + r] = xs[9 + r] + m;
     }
     xn[12] = xs[12];
     for (int s = 0; s < NX; ++s) xs[s] = xn[s];
     if (xo)
       for (int s = 0; s < NX; ++s) xo[(size_t)(k + 1) * NX + s] = xs[s];
     for (int s = 0; s < NX; ++s) {
-      const double e = xs[s] - xref[(k + 1) * NX + s];
+      const double e = xs[s] - V.xr[(k + 1) * NX + s];
       J += 0.5 * M->qdiag[k + 1][s] * e * e;
     }
   }
-  if (D0) J += foot_cost(M, foot, ct, D0, D1, alpha, false);
+  if (feet) J += foot_cost(M, V, D1, alpha, false);
   return J;
 }
 
 // Linearised response of the rollout of u0 to du = u1 - u0 (and, with footholds, dD = D1 - D0) and the descent metric
 // (MultipleShootingSolver.cpp:287-296): mirrors oracle_nlp_linstep_feet operation for operation. Returns |dx|
 // (trajectoryNorm, :492-503) in dxn.
-__device__ double linstep_metric(const DevModel* M, const double* x0, const double* xref, const double* foot,
-                                 const uint8_t* ct, const double* u0, const double* u1, double* dxn,
-                                 const double* D0 = nullptr, const double* D1 = nullptr) {
+__device__ double linstep_metric(const DevModel* M, const View& V, double* dxn, bool feet) {
   const int N = M->N;
   const double dt = M->dt;
+  const double* u0 = V.u0;
+  const double* u1 = V.u1;
   double xs[NX], xn[NX], dx[NX], dn[NX];
   for (int s = 0; s < NX; ++s) {
-    xs[s] = x0[s];
+    xs[s] = V.x0[s];
     dx[s] = 0.0;
   }
   double ss = 0.0, mt = 0.0;
   for (int k = 0; k < N; ++k) {
-    const double* uk = u0 + (size_t)k * NU;
+    const double* uk = u0 + k * NU;
     double duk[NU];
-    for (int j = 0; j < NU; ++j) duk[j] = u1[(size_t)k * NU + j] - uk[j];
+    for (int j = 0; j < NU; ++j) duk[j] = u1[k * NU + j] - uk[j];
     double F[3] = {0.0, 0.0, 0.0}, Tq[3] = {0.0, 0.0, 0.0}, dF[3] = {0.0, 0.0, 0.0}, dT[3] = {0.0, 0.0, 0.0};
     int ns = 0;
     for (int i = 0; i < NL; ++i) {
-      if (!ct[k * NL + i]) continue;
+      if (!V.ct[k * NL + i]) continue;
       ++ns;
       double p[3], dp[3] = {0.0, 0.0, 0.0};
-      stance_point(foot, ct, N, k, i, p);
-      if (D0) {
-        const int s0 = run_start(k, i, [ct](int kk, int l) { return ct[kk * NL + l] != 0; });
-        if (s0 > 0)
-          for (int d = 0; d < 3; ++d) {
-            const double a = D0[(s0 * NL + i) * 3 + d];
-            p[d] = p[d] + a;
-            dp[d] = D1[(s0 * NL + i) * 3 + d] - a;
-          }
-      }
+      for (int d = 0; d < 3; ++d) p[d] = V.pb[(k * NL + i) * 3 + d];
+      const int s0 = V.rs[k * NL + i];
+      if (feet && s0 > 0)
+        for (int d = 0; d < 3; ++d) {
+          const double a = V.D0[(s0 * NL + i) * 3 + d];
+          p[d] = p[d] + a;
+          dp[d] = V.D1[(s0 * NL + i) * 3 + d] - a;
+        }
       const double* f = uk + 3 * i;
       const double* df = duk + 3 * i;
       const double rx = p[0] - xs[0], ry = p[1] - xs[1], rz = p[2] - xs[2];
@@ -219,15 +290,12 @@ __device__ double linstep_metric(const DevModel* M, const double* x0, const doub
     }
     for (int j = 0; j < NU; ++j) {
       const int i = j / 3;
-      const double fd = (j % 3 == 2 && ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
+      const double fd = (j % 3 == 2 && V.ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
       double gu = 2.0 * M->Wf[j] * (uk[j] - fd);
-      if (k > 0) gu += 2.0 * M->Wr[j] * (uk[j] - u0[(size_t)(k - 1) * NU + j]);
-      if (k + 1 < N) gu -= 2.0 * M->Wr[j] * (u0[(size_t)(k + 1) * NU + j] - uk[j]);
+      if (k > 0) gu += 2.0 * M->Wr[j] * (uk[j] - u0[(k - 1) * NU + j]);
+      if (k + 1 < N) gu -= 2.0 * M->Wr[j] * (u0[(k + 1) * NU + j] - uk[j]);
       mt += gu * duk[j];
     }
-    double sp, cp;
-    sincos(xref[k * NX + 11], &sp, &cp);
-    const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
     for (int d = 0; d < 3; ++d) {
       xn[d] = xs[d] + dt * xs[3 + d];
       dn[d] = dx[d] + dt * dx[3 + d];
@@ -242,16 +310,15 @@ __device__ double linstep_metric(const DevModel* M, const double* x0, const doub
       xn[6 + d] = xs[6 + d] + dt * Tq[d];
       dn[6 + d] = dx[6 + d] + dt * dT[d];
     }
-    for (int a = 0; a < 3; ++a) {
+    for (int r = 0; r < 3; ++r) {
       double m = 0.0, dm = 0.0;
       for (int b = 0; b < 3; ++b) {
-        double s2 = 0.0;
-        for (int e = 0; e < 3; ++e) s2 += M->inv_inertia[a * 3 + e] * RzT[e * 3 + b];
+        const double s2 = V.S2[k * 9 + r * 3 + b];
         m += dt * s2 * xs[6 + b];
         dm += dt * s2 * dx[6 + b];
       }
-      xn[9 + a] = xs[9 + a] + m;
-      dn[9 + a] = dx[9 + a] + dm;
+      xn[9 + r] = xs[9 + r] + m;
+      dn[9 + r] = dx[9 + r] + dm;
     }
     xn[12] = xs[12];
     dn[12] = dx[12];
@@ -260,26 +327,32 @@ __device__ double linstep_metric(const DevModel* M, const double* x0, const doub
       dx[s] = dn[s];
     }
     for (int s = 0; s < NX; ++s) {
-      mt += M->qdiag[k + 1][s] * (xs[s] - xref[(k + 1) * NX + s]) * dx[s];
+      mt += M->qdiag[k + 1][s] * (xs[s] - V.xr[(k + 1) * NX + s]) * dx[s];
       ss += dx[s] * dx[s];
     }
   }
-  if (D0) mt += foot_cost(M, foot, ct, D0, D1, 0.0, true);
+  if (feet) mt += foot_cost(M, V, V.D1, 0.0, true);
   *dxn = sqrt(ss);
   return mt;
 }
 
-// U_j <- the cold QP's solution, lin <- its rollout; QPs the cold QP rejected are done from the start.
+extern __shared__ __attribute__((aligned(16))) unsigned char sqp_lds[];
+
+// U_j <- the cold QP's solution, lin <- its rollout; QPs the cold QP rejected are done from the start. With footholds
+// the offsets start at clamp(0, lo, hi) (oracle_feet_init).
 __global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
   const int q = blockIdx.x;
   const DevModel* M = a.model;
   const int N = M->N;
   const int nu = N * NU;
-  for (int i = threadIdx.x; i < nu; i += 64) a.uj[(size_t)q * nu + i] = a.u[(size_t)q * nu + i];
-  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
-  const uint8_t* ct = a.contact + (size_t)q * N * NL;
-  double* dj = a.dj ? a.dj + (size_t)q * nu : nullptr;
-  if (dj)  // footholds start at clamp(0, lo, hi) (oracle_feet_init)
+  const double* uc = a.u + (size_t)q * nu;
+  for (int i = threadIdx.x; i < nu; i += 64) a.uj[(size_t)q * nu + i] = uc[i];
+  View V = stage(a, q, sqp_lds, uc, nullptr, nullptr, nullptr);
+  const bool feet = a.dj != nullptr;
+  if (feet) {
+    const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
+    const uint8_t* ct = a.contact + (size_t)q * N * NL;
+    double* dj = a.dj + (size_t)q * nu;
     for (int sl = threadIdx.x; sl < N * NL; sl += 64) {
       const int s0 = sl / NL, leg = sl % NL;
       auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
@@ -295,15 +368,16 @@ __global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
           v = fmin(fmax(0.0, lo), hi);
         }
         dj[sl * 3 + d] = v;
+        V.D0[sl * 3 + d] = v;
       }
     }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     a.done[q] = a.status[q] != CMPC_SUCCESS ? 1 : 0;
     a.sqp_iters[q] = 0;
     a.qp_iters[q] = a.iters ? a.iters[q] : 0;
-    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, ft, ct, a.u + (size_t)q * nu, nullptr,
-                 0.0, a.lin + (size_t)q * N * 6, nullptr, dj);
+    rollout_cost(M, V, false, 0.0, a.lin + (size_t)q * N * 6, nullptr, feet);
   }
 }
 
@@ -317,12 +391,9 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   const int nu = N * NU;
   double* uj = a.uj + (size_t)q * nu;
   const double* uq = a.uq + (size_t)q * nu;
-  double* dj = a.dj ? a.dj + (size_t)q * nu : nullptr;  // footholds (cmpc_nlp_solve_batch)
-  const double* dq = a.dj ? a.dq + (size_t)q * nu : nullptr;
-  const double* x0 = a.x0 + (size_t)q * NX;
-  const double* xr = a.xref + (size_t)q * (N + 1) * NX;
-  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
-  const uint8_t* ct = a.contact + (size_t)q * N * NL;
+  const bool feet = a.dj != nullptr;  // footholds (cmpc_nlp_solve_batch)
+  double* dj = feet ? a.dj + (size_t)q * nu : nullptr;
+  const double* dq = feet ? a.dq + (size_t)q * nu : nullptr;
   if (lane == 0) {
     a.sqp_iters[q] += 1;
     a.qp_iters[q] += a.iters_q[q];
@@ -334,24 +405,26 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     }
     return;
   }
+  View V = stage(a, q, sqp_lds, uj, uq, dj, dq);
+  __syncthreads();
   // lanes m < 14: trial step alpha = 2^-m; lane 14: the current iterate; lane 15: |dx| and the descent metric;
   // lane 16: |du| (sequential, the oracle's order)
   double J = 0.0, aux = 0.0;
   if (lane < 14) {
-    J = rollout_cost(M, x0, xr, ft, ct, uj, uq, ldexp(1.0, -lane), nullptr, nullptr, dj, dq);
+    J = rollout_cost(M, V, true, ldexp(1.0, -lane), nullptr, nullptr, feet);
   } else if (lane == 14) {
-    J = rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, nullptr, nullptr, dj, nullptr);
+    J = rollout_cost(M, V, false, 0.0, nullptr, nullptr, feet);
   } else if (lane == 15) {
-    J = linstep_metric(M, x0, xr, ft, ct, uj, uq, &aux, dj, dq);
+    J = linstep_metric(M, V, &aux, feet);
   } else if (lane == 16) {
     double s2 = 0.0;
     for (int i = 0; i < nu; ++i) {
-      const double d = uq[i] - uj[i];
+      const double d = V.u1[i] - V.u0[i];
       s2 += d * d;
     }
-    if (dj)
+    if (feet)
       for (int i = 0; i < nu; ++i) {
-        const double d = dq[i] - dj[i];
+        const double d = V.D1[i] - V.D0[i];
         s2 += d * d;
       }
     aux = sqrt(s2);
@@ -372,45 +445,51 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   __syncthreads();
   if (alpha > 0.0)
     for (int i = lane; i < nu; i += 64) {
-      uj[i] = uj[i] + alpha * (uq[i] - uj[i]);
-      if (dj) dj[i] = dj[i] + alpha * (dq[i] - dj[i]);
+      const double un = V.u0[i] + alpha * (V.u1[i] - V.u0[i]);
+      uj[i] = un;
+      V.u0[i] = un;
+      if (feet) {
+        const double dn = V.D0[i] + alpha * (V.D1[i] - V.D0[i]);
+        dj[i] = dn;
+        V.D0[i] = dn;
+      }
     }
   const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
   __syncthreads();
   if (lane == 0) {
     if (conv) a.done[q] = 1;
-    rollout_cost(M, x0, xr, ft, ct, uj, nullptr, 0.0, a.lin + (size_t)q * N * 6, nullptr, dj);
+    rollout_cost(M, V, false, 0.0, a.lin + (size_t)q * N * 6, nullptr, feet);
   }
 }
 
-// Final outputs: u <- U_j, x <- its nonlinear rollout, status stays, iteration counts reported.
+// Final outputs: u <- U_j, x <- its nonlinear rollout, the foot_pos table (footholds), status stays.
 __global__ __launch_bounds__(64) void k_sqp_final(SqpArgs a) {
   const int q = blockIdx.x;
   const DevModel* M = a.model;
   const int N = M->N;
   const int nu = N * NU;
-  for (int i = threadIdx.x; i < nu; i += 64) a.u[(size_t)q * nu + i] = a.uj[(size_t)q * nu + i];
-  const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
-  const uint8_t* ct = a.contact + (size_t)q * N * NL;
-  const double* dj = a.dj ? a.dj + (size_t)q * nu : nullptr;
-  if (dj && a.feet)  // the controller's foot_pos output (oracle_feet_table)
+  const double* ujq = a.uj + (size_t)q * nu;
+  for (int i = threadIdx.x; i < nu; i += 64) a.u[(size_t)q * nu + i] = ujq[i];
+  const bool feet = a.dj != nullptr;
+  View V = stage(a, q, sqp_lds, ujq, nullptr, feet ? a.dj + (size_t)q * nu : nullptr, nullptr);
+  __syncthreads();
+  if (feet && a.feet)  // the controller's foot_pos output (oracle_feet_table)
     for (int sl = threadIdx.x; sl < (N + 1) * NL; sl += 64) {
       const int j = sl / NL, i = sl % NL;
-      auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
-      const int k = (j < N && ct[j * NL + i]) ? j : ((j > 0 && ct[(j - 1) * NL + i]) ? j - 1 : -1);
+      const int k = (j < N && V.ct[j * NL + i]) ? j : ((j > 0 && V.ct[(j - 1) * NL + i]) ? j - 1 : -1);
       double p[3];
       if (j == 0 || k < 0) {
-        for (int d = 0; d < 3; ++d) p[d] = ft[sl * 3 + d];
+        for (int d = 0; d < 3; ++d) p[d] = V.des[sl * 3 + d];
       } else {
-        lever_point(ft, dj, N, k, i, st, p);
+        for (int d = 0; d < 3; ++d) p[d] = V.pb[(k * NL + i) * 3 + d];
+        const int s0 = V.rs[k * NL + i];
+        if (s0 > 0)
+          for (int d = 0; d < 3; ++d) p[d] = p[d] + V.D0[(s0 * NL + i) * 3 + d];
       }
       double* o = a.feet + ((size_t)q * (N + 1) * NL + sl) * 3;
       for (int d = 0; d < 3; ++d) o[d] = p[d];
     }
-  __syncthreads();
-  if (threadIdx.x == 0 && a.x)
-    rollout_cost(M, a.x0 + (size_t)q * NX, a.xref + (size_t)q * (N + 1) * NX, ft, ct, a.u + (size_t)q * nu, nullptr,
-                 0.0, nullptr, a.x + (size_t)q * (N + 1) * NX, dj);
+  if (threadIdx.x == 0 && a.x) rollout_cost(M, V, false, 0.0, nullptr, a.x + (size_t)q * (N + 1) * NX, feet);
 }
 
 // number of QPs not yet done -> count[0]
@@ -428,10 +507,12 @@ __global__ __launch_bounds__(256) void k_sqp_count(const int* done, int B, int* 
 
 int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream) {
   if (B <= 0) return 0;
+  if (a.N < 1 || a.N > MAXN) return -1;
+  const size_t lds = sqp_lds_bytes(a.N);
   switch (which) {
-    case 0: hipLaunchKernelGGL(k_sqp_init, dim3(B), dim3(64), 0, stream, a); break;
-    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), 0, stream, a); break;
-    case 2: hipLaunchKernelGGL(k_sqp_final, dim3(B), dim3(64), 0, stream, a); break;
+    case 0: hipLaunchKernelGGL(k_sqp_init, dim3(B), dim3(64), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL(k_sqp_final, dim3(B), dim3(64), lds, stream, a); break;
     case 3: hipLaunchKernelGGL(k_sqp_count, dim3(1), dim3(256), 0, stream, a.done, B, a.count); break;
     default: return -1;
   }
