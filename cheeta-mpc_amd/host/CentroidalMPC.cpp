@@ -163,3 +163,11 @@ int CentroidalMPC::UpdateMPCBatch(int B, const double* d_x0, const double* d_xre
   if (!ctx_) return CMPC_ERR_ARG;
   return cmpc_solve_batch(ctx_, B, d_x0, d_xref, d_foot, d_contact, d_u, d_x, d_status, d_iters, stream);
 }
+
+int CentroidalMPC::UpdateNLPBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                                  const uint8_t* d_contact, double* d_u, double* d_feet, double* d_x, int* d_status,
+                                  int* d_qp_iters, int* d_sqp_iters, void* stream) {
+  if (!ctx_) return CMPC_ERR_ARG;
+  return cmpc_nlp_solve_batch(ctx_, B, d_x0, d_xref, d_foot, d_contact, sqp_iter_max_, sqp_tol_, d_u, d_feet, d_x,
+                              d_status, d_qp_iters, d_sqp_iters, stream);
+}

@@ -85,6 +85,12 @@ class CentroidalMPC {
   int UpdateMPCBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot, const uint8_t* d_contact,
                      double* d_u, double* d_x, int* d_status, int* d_iters, void* stream);
 
+  /* Batched NLP with the later runs' footholds as decision variables (cmpc_nlp_solve_batch): device pointers in
+   * cmpc_solve_batch's record layout plus d_feet [B][N+1][L][3]; the SQP limits of setNonlinear. */
+  int UpdateNLPBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot, const uint8_t* d_contact,
+                     double* d_u, double* d_feet, double* d_x, int* d_status, int* d_qp_iters, int* d_sqp_iters,
+                     void* stream);
+
   /* Feedback policy dU/dx0 of each QP at its solution d_u (cmpc_policy_batch; the condensed counterpart of
    * HpipmInterface::getRiccatiFeedback, HpipmInterface.cpp:330-455): d_K [B][N][L][3][13]. */
   int FeedbackPolicyBatch(int B, const double* d_x0, const double* d_xref, const double* d_foot,

@@ -122,6 +122,46 @@ def test_invalid_contact_table(op):
     assert np.all(u[2] == 0)
 
 
+def test_known_solution_recovered_with_pyramid_rows(op):
+    """SURVEY §8c known-solution construction on the condensed QP: pick U* strictly inside every friction pyramid,
+    set g = -H U*, and the IPM (pyramid rows present, all inactive at U*) returns U*."""
+    m = op.default_model(10)
+    x0, xref, foot, contact = op.generate(m, 17, 4, gait=1)
+    rng = np.random.default_rng(4)
+    for q in range(4):
+        n, H, g, mu, lo, hi, mp, st = op.condense(m, x0[q], xref[q], foot[q], contact[q])
+        assert st == 0
+        t = n // 3
+        fz = rng.uniform(10.0, 60.0, t)
+        fx = rng.uniform(-0.3, 0.3, t) * mu[:t] * fz
+        fy = rng.uniform(-0.3, 0.3, t) * mu[:t] * fz
+        us = np.stack([fx, fy, fz], axis=1).reshape(-1)
+        g2 = g.copy()
+        g2[:n] = -H[:n, :n] @ us
+        u, ll, lu, st2, it, res = op.qp_ipm(n, H, g2, mu, lo, hi, op.tight_settings())
+        assert st2 == 0
+        assert np.abs(u - us).max() < 1e-8 * max(1.0, np.abs(us).max())
+
+
+def test_fdes_sums_to_weight(op):
+    """f^des_z = m 9.81 / n_stance per stance leg (CentroidalMPC.cpp:326-335) sums to m g per step. With
+    every state weight 0 the condensed gradient is r-bar = -2 W_f f^des alone."""
+    m = op.default_model(10)
+    for j in range(9):
+        m.weights[j] = 0.0
+    x0, xref, foot, contact = op.generate(m, 23, 3, gait=1)
+    L = 4
+    for q in range(3):
+        H, g, st = op.condense_full(m, x0[q], xref[q], foot[q], contact[q])
+        assert st == 0
+        N = m.N
+        for k in range(N):
+            fz = [-g[12 * k + 3 * i + 2] / (2.0 * m.weights[9 + 3 * L + 3 * i + 2]) for i in range(L)]
+            assert abs(sum(fz) - m.mass * 9.81) < 1e-9
+            for i in range(L):
+                assert (fz[i] == 0.0) == (contact[q][k, i] == 0)
+
+
 def test_unconstrained_is_newton_step(op):
     # with no inequality rows the IPM is one Newton step: H u = -g
     rng = np.random.default_rng(0)
