@@ -74,6 +74,9 @@ struct SrbdLds {
   // foothold triples (CondenseArgs::dbar): force triple of each stance (k, leg), foothold flag, run end, box (delta)
   // and the run's mean des position
   int s_slot[FEET ? MAXN * NL : 1];
+  int s_rs[FEET ? MAXN * NL : 1];            // first step of the run of each stance (k, leg)
+  double s_fb[FEET ? MAXN * NU : 1];         // the iterate's forces f_bar [N][12] (CondenseArgs::ubar)
+  double s_D[FEET ? MAXN * NU : 1];          // the iterate's foothold offsets [N][4][3] (CondenseArgs::dbar)
   uint8_t s_tf[FT];
   int s_te[FT];
   double s_blo[FT][3], s_bhi[FT][3], s_pbar[FT][3];
@@ -115,12 +118,18 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
   for (int i = tid; i < (N + 1) * NX; i += NTHR) S.s_xref[i] = xr[i];
   for (int i = tid; i < (N + 1) * NL * 3; i += NTHR) S.s_foot[i] = ft[i];
+  if constexpr (FEET) {  // the iterate's forces and foothold offsets, read once (the per-step passes use LDS)
+    if (a.dbar)
+      for (int i = tid; i < N * NU; i += NTHR) {
+        S.s_fb[i] = a.ubar[(size_t)q * N * NU + i];
+        S.s_D[i] = a.dbar[(size_t)q * N * NU + i];
+      }
+  }
   for (int i = tid; i < 2 * 16 * NMAX; i += NTHR) (&S.s_G[0][0][0])[i] = T(0);
   if (tid < 32) (&S.s_w[0][0])[tid] = T(0), (&S.s_q[0][0])[tid] = T(0);
   if (tid == 0) S.s_flag = 0;
   const int ne = N * L;
   const bool feet = FEET && a.dbar != nullptr;
-  const double* Dq = feet ? a.dbar + (size_t)q * N * NU : nullptr;
   int e = 0, fs = 0;
   if (tid < ne) {
     const uint8_t* ctq = a.contact + (size_t)q * ne;
@@ -141,7 +150,10 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   for (int w = 0; w < WAVES; ++w) nt += S.s_wtot[w];
   if (e) {
     const int t = off + pre;
-    if (FEET) S.s_slot[tid] = t;
+    if (FEET) {
+      S.s_slot[tid] = t;
+      S.s_rs[tid] = run_start(tid / L, tid % L, [&](int kk, int l) { return S.s_e[kk * L + l] != 0; });
+    }
     if (t < NTRI) {
       S.s_tk[t] = tid / L;
       S.s_tleg[t] = tid % L;
@@ -265,7 +277,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
       S.s_next[c] = nx;
       if (d == 2) gcol = T(-2.0 * M->Wf[j] * (M->mass * GRAV / (double)S.s_ns[kc]));
       double p[3];
-      lever_point(S.s_foot, Dq, N, kc, leg, stf, p);
+      lever_point(S.s_foot, feet ? S.s_D : nullptr, N, kc, leg, stf, p);
       const double* cb = a.lin ? a.lin + ((size_t)q * N + kc) * 6 : S.s_xref + kc * NX;
       rx = p[0] - cb[0];
       ry = p[1] - cb[1];
@@ -316,7 +328,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
       gam[5] += dt * gam[12];
       if (fcol) {
         if (km <= ke) {  // dt e_d x f_bar_{leg, km}
-          const double* fb = a.ubar + ((size_t)q * N + km) * NU + 3 * leg;
+          const double* fb = S.s_fb + km * NU + 3 * leg;
           if (d == 0) {
             gam[7] += dt * T(-fb[2]);
             gam[8] += dt * T(fb[1]);
@@ -360,10 +372,10 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
       if (feet)  // -dt D x f_bar of the later runs' stance legs
         for (int i = 0; i < L; ++i) {
           if (!S.s_e[km * L + i]) continue;
-          const int s0 = run_start(km, i, [&](int k2, int l) { return S.s_e[k2 * L + l] != 0; });
+          const int s0 = S.s_rs[km * L + i];
           if (s0 == 0) continue;
-          const double* dl = Dq + (s0 * NL + i) * 3;
-          const double* fb = a.ubar + ((size_t)q * N + km) * NU + 3 * i;
+          const double* dl = S.s_D + (s0 * NL + i) * 3;
+          const double* fb = S.s_fb + km * NU + 3 * i;
           xn[6] -= M->dt * (dl[1] * fb[2] - dl[2] * fb[1]);
           xn[7] -= M->dt * (dl[2] * fb[0] - dl[0] * fb[2]);
           xn[8] -= M->dt * (dl[0] * fb[1] - dl[1] * fb[0]);
