@@ -283,3 +283,28 @@ def test_device_nlp_empty_step_box(cm, op):
     eng = cm.Engine(m, precision=0, max_batch=B)
     u, feet, x, st, qi, si = eng.nlp_solve(x0, xref, foot, contact)
     assert st[1] == 7 and all(st[q] == 0 for q in (0, 2, 3))
+
+
+@pytest.mark.gpu
+def test_device_nlp_short_horizon_and_invalid_table(cm, op):
+    """N = 5 (a one-class context, ld = 64, so the foothold QPs run in the workgroup condensing's 64 class) against
+    the oracle, with one QP whose contact table has a flight step: INVALID_CONTACT ("mpc table invalid",
+    CentroidalMPC.cpp:328-330), zero forces, the others unaffected."""
+    N, B = 5, 12
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=1)
+    contact[3, 2, :] = 0
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    assert eng.ld == 64
+    u, feet, x, st, qi, si = eng.nlp_solve(x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7)
+    s = op.default_settings()
+    for q in range(B):
+        ur, Dr, feetr, xr, sr, qir, sir = op.sqp_solve_feet(mo, s, x0[q], xref[q], foot[q], contact[q],
+                                                            sqp_iter_max=10, sqp_tol=1e-7)
+        assert st[q] == sr
+        if q == 3:
+            assert sr == 5 and not u[q].any()
+            continue
+        assert sr == 0
+        assert rel_err(u[q], ur) < 1e-6, q
+        assert np.abs(feet[q] - feetr).max() < 1e-8, q
