@@ -13,9 +13,10 @@ NL = 4
 G = 9.81
 
 
-def ref_nlp(mo, x0, xref, foot, contact):
+def ref_nlp(mo, x0, xref, foot, contact, fix_feet=None):
     """Objective / constraints of the reference NLP over z = [c, v, L (3 x (N+1) each), per leg: p (3 x (N+1)),
-    pv (3 x N), f (3 x N)]; returns (f, df, eq constraints list, ineq constraints list, unpack)."""
+    pv (3 x N), f (3 x N)]; returns (f, df, eq constraints list, ineq constraints list, unpack). fix_feet
+    [(N+1)][L][3]: foot_pos additionally pinned at every node (the frozen-foothold problem of cmpc_sqp_solve_batch)."""
     torch = pytest.importorskip("torch")
     N, dt, m = mo.N, mo.dt, mo.mass
     w = np.array(mo.weights[:45])
@@ -75,6 +76,10 @@ def ref_nlp(mo, x0, xref, foot, contact):
         out.append((c[1:] - (c[:-1] + v[:-1] * dt)).reshape(-1))
         out.append((v[1:] - (v[:-1] + acc * dt)).reshape(-1))
         out.append((L[1:] - (L[:-1] + tq * dt)).reshape(-1))
+        if fix_feet is not None:  # foot_vel pinned so that the swing integrator lands on the fixed positions
+            FF = T(fix_feet)
+            for i, (p, pv, f) in enumerate(legs):
+                out.append((pv - (FF[1:, i, :] - FF[:-1, i, :]) / dt).reshape(-1))
         return torch.cat([o.reshape(-1) for o in out])
 
     Fm = [torch.tensor([[-1, 0, mu[i]], [1, 0, mu[i]], [0, -1, mu[i]], [0, 1, mu[i]], [0, 0, 1]],
@@ -171,3 +176,23 @@ def test_reference_nlp_matches_oracle_sqp_with_footholds(op, case):
                 assert np.abs(p_ref[j, i] - foot[j, i]).max() < 2e-5, (i, j)
     # the states: the oracle's nonlinear rollout is the reference's trajectory
     assert np.abs(x[:, 0:3] - c.numpy()).max() < 1e-5 and np.abs(x[:, 6:9] - L.numpy()).max() < 1e-4
+
+
+def test_reference_nlp_with_frozen_footholds_matches_oracle_sqp(op):
+    """The same literal problem with foot_pos pinned at the frozen footholds (current foot / the run's mean des / des
+    on swing nodes) is what cmpc_sqp_solve_batch solves: SLSQP's optimum vs oracle_sqp_solve."""
+    from scipy.optimize import minimize
+    N = 6
+    mo = op.default_model(N)
+    x0, xref, foot, contact = (a[0] for a in op.generate(mo, SEED + 11, 1, gait=1))
+    fixed = op.feet_table(mo, foot, contact, np.zeros((N, NL, 3)))
+    nz, (fv, fj), (ev, ej), (iv, ij), unpack = ref_nlp(mo, x0, xref, foot, contact, fix_feet=fixed)
+    z0 = initial_guess(op, mo, x0, xref, foot, contact, nz, unpack)
+    res = minimize(fv, z0, jac=fj, method="SLSQP",
+                   constraints=[{"type": "eq", "fun": ev, "jac": ej}, {"type": "ineq", "fun": iv, "jac": ij}],
+                   options={"ftol": 1e-12, "maxiter": 500})
+    assert res.success, res.message
+    f_ref = np.stack([unpack(res.x)[3][i][2].numpy() for i in range(NL)], axis=1)
+    u, x, st, qi, si = op.sqp_solve(mo, op.default_settings(), x0, xref, foot, contact, sqp_iter_max=50, sqp_tol=1e-10)
+    assert st == 0
+    assert np.abs(u - f_ref).max() < 2e-5 * max(1.0, np.abs(f_ref).max()), np.abs(u - f_ref).max()
