@@ -95,3 +95,24 @@ def test_residuals_max_iter_and_skipped(cm, op):
     d = cm.default_settings()
     above = (res[run, 0] > d.tol_stat) | (res[run, 2] > d.tol_ineq) | (res[run, 3] > d.tol_comp)
     assert above.all(), res[run]
+
+
+@pytest.mark.parametrize("feet", [False, True])
+def test_residuals_after_sqp(cm, op, feet):
+    """After cmpc_sqp_solve_batch / cmpc_nlp_solve_batch the residuals are those of each QP's last subproblem, also
+    for QPs whose SQP converged early and were skipped by later iterations; NaN for a rejected contact table."""
+    N, B = 10, 32
+    m, mo = cm.default_model(N), op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, B, gait=1)
+    contact[5, 3, :] = 0  # "mpc table invalid"
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    if feet:
+        u, _, _, st, qi, si = eng.nlp_solve(x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7)
+    else:
+        u, _, st, qi, si = eng.sqp_solve(x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7)
+    res = eng.residuals(B)
+    s = cm.default_settings()
+    assert st[5] == 5 and np.all(np.isnan(res[5]))
+    ok = np.arange(B) != 5
+    assert np.all(st[ok] == 0) and len(set(si[ok].tolist())) > 1  # QPs converge after different SQP iterations
+    assert np.all(res[ok, 0] <= s.tol_stat) and np.all(res[ok, 2] <= s.tol_ineq) and np.all(res[ok, 3] <= s.tol_comp)
