@@ -882,14 +882,16 @@ int cmpc_nlp_solve_batch(cmpc_ctx* c, int B, const double* x0, const double* xre
                  true, feet);
 }
 
-int cmpc_policy_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
-                      const uint8_t* contact, const double* u, double act_tol, double* K, int* nfree, int* status,
-                      void* stream) {
-  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !K || !status)
-    return CMPC_ERR_ARG;
-  if (B == 0) return CMPC_OK;
+}  // extern "C"
+
+namespace {
+
+// Feedback policy of the QPs linearised at lin ([B][N][6] in the context workspace, or null: the reference
+// linearisation) at their solutions u.
+int policy_run(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot, const uint8_t* contact,
+               const double* u, double act_tol, double* K, int* nfree, int* status, void* stream, const double* lin) {
   hipStream_t st = (hipStream_t)stream;
-  int r = run_condense(c, B, x0, xref, foot, contact, st);
+  int r = run_condense(c, B, x0, xref, foot, contact, st, lin);
   if (r != CMPC_OK) return r;
   // scratch for at most `chunk` QPs per launch; launches on one stream reuse it in order
   const size_t stride = policy_scratch_doubles(c->model.N, c->ld);
@@ -909,16 +911,48 @@ int cmpc_policy_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, 
     int rr;
     if (c->precision == CMPC_F64) {
       PolicyArgs<double> a{c->d_model, c->ld, q0, xref, foot, contact, u, (const double*)c->H, c->tri_map, c->nvar,
-                           c->status, act_tol, K, nfree, status, c->pol, stride};
+                           c->status, act_tol, K, nfree, status, c->pol, stride, lin};
       rr = launch_policy<double>(a, nq, st);
     } else {
       PolicyArgs<float> a{c->d_model, c->ld, q0, xref, foot, contact, u, (const float*)c->H, c->tri_map, c->nvar,
-                          c->status, act_tol, K, nfree, status, c->pol, stride};
+                          c->status, act_tol, K, nfree, status, c->pol, stride, lin};
       rr = launch_policy<float>(a, nq, st);
     }
     if (rr != 0) return CMPC_ERR_HIP;
   }
   return CMPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cmpc_policy_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                      const uint8_t* contact, const double* u, double act_tol, double* K, int* nfree, int* status,
+                      void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !K || !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  return policy_run(c, B, x0, xref, foot, contact, u, act_tol, K, nfree, status, stream, nullptr);
+}
+
+int cmpc_sqp_policy_batch(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot,
+                          const uint8_t* contact, const double* u, double act_tol, double* K, int* nfree, int* status,
+                          void* stream) {
+  if (!c || B < 0 || B > c->max_batch || !x0 || !xref || !foot || !contact || !u || !K || !status)
+    return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  SqpArgs a{};
+  a.model = c->d_model;
+  a.N = c->model.N;
+  a.x0 = x0;
+  a.xref = xref;
+  a.foot = foot;
+  a.contact = contact;
+  a.u = const_cast<double*>(u);  // read only by k_sqp_lin
+  a.lin = c->lin;
+  if (launch_sqp(4, a, B, (hipStream_t)stream) != 0) return CMPC_ERR_HIP;
+  return policy_run(c, B, x0, xref, foot, contact, u, act_tol, K, nfree, status, stream, c->lin);
 }
 
 int cmpc_shift_inputs(int B, int N, const double* d_u, int shift, double* d_u_out, void* stream) {

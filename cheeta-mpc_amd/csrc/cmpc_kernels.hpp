@@ -230,7 +230,8 @@ struct SqpArgs {
   const double* dq;    // [B][N][L][3] the QP's foothold offsets (k_expand ExpandArgs::dq)
   double* feet;        // [B][N+1][L][3] foot_pos output (k_sqp_final) or null
 };
-int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream);  // 0 init, 1 step, 2 final, 3 count
+// 0 init, 1 step, 2 final, 3 count, 4 lin <- the linearisation point (c_k, F_k) of the nonlinear rollout of u
+int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream);
 
 // warm start: scatter a previous solution u_init [B][N][L][3] into the condensed order of each QP (tri_map)
 // d_init [B][N][L][3] (or null): the foothold offsets for the foothold triples (tri_map >= N L)
@@ -269,6 +270,7 @@ struct PolicyArgs {
   int* status_out;      // [B]
   double* scratch;      // [launch QPs][stride]
   size_t stride;
+  const double* lin;    // [B][N][6] linearisation point of the QP (CondenseArgs::lin) or null: the reference one
 };
 size_t policy_scratch_doubles(int N, int ld);
 template <typename T>

@@ -26,11 +26,12 @@ namespace {
 
 constexpr int PT = 256;  // threads per QP
 
-// Row-major A_k (13 x 13) into ab[0..168] and B_k (13 x 12) into ab[169..324] (no SQP linearisation term): the
-// forward-Euler SRBD map of CentroidalMPC.cpp:85-92 with the lever arm frozen at p_{k,i} - c^ref_k (p: stance_point)
-// (oracle_srbd_dynamics). Entry-parallel over the workgroup.
+// Row-major A_k (13 x 13) into ab[0..168] and B_k (13 x 12) into ab[169..324]: the forward-Euler SRBD map of
+// CentroidalMPC.cpp:85-92 with the lever arm frozen at p_{k,i} - c^ref_k (p: stance_point), or, with the SQP
+// linearisation lk = (c_bar_k, F_bar_k), at p_{k,i} - c_bar_k plus dt [F_bar_k]x in the L rows / c columns
+// (oracle_srbd_dynamics_lin). Entry-parallel over the workgroup.
 __device__ void build_ab(const DevModel* M, const double* xr, const double* ft, const uint8_t* ct, int k,
-                         double* ab) {
+                         const double* lk, double* ab) {
   const double dt = M->dt;
   const double psi = xr[k * NX + 11];
   const double cp = cos(psi), sp = sin(psi);
@@ -39,7 +40,11 @@ __device__ void build_ab(const DevModel* M, const double* xr, const double* ft, 
     if (e < NX * NX) {
       const int r = e / NX, c = e % NX;
       if (r == c) v = 1.0;
-      else if (r < 3 && c == r + 3) v = dt;
+      else if (lk && r >= 6 && r < 9 && c < 3) {  // L+ += dt F_bar x c
+        const double* F = lk + 3;
+        const double SF[9] = {0.0, -F[2], F[1], F[2], 0.0, -F[0], -F[1], F[0], 0.0};
+        v = dt * SF[(r - 6) * 3 + c];
+      } else if (r < 3 && c == r + 3) v = dt;
       else if (r == 5 && c == 12) v = dt;
       else if (r >= 9 && r < 12 && c >= 6 && c < 9) {
         const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
@@ -56,7 +61,7 @@ __device__ void build_ab(const DevModel* M, const double* xr, const double* ft, 
         if (r >= 6 && r < 9) {
           double p[3];
           stance_point(ft, ct, M->N, k, i, p);
-          const double* cb = xr + (size_t)k * NX;
+          const double* cb = lk ? lk : xr + (size_t)k * NX;
           const double rx = p[0] - cb[0], ry = p[1] - cb[1], rz = p[2] - cb[2];
           const double S[9] = {0.0, -rz, ry, rz, 0.0, -rx, -ry, rx, 0.0};
           v = dt * S[(r - 6) * 3 + b];
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(PT) void k_policy(PolicyArgs<T> a) {
   // forward: Aqp block rows P_k
   for (int e = tid; e < NX * NX; e += PT) P[e] = (e / NX == e % NX) ? 1.0 : 0.0;
   for (int k = 0; k < N; ++k) {
-    build_ab(M, xr, ft, ct, k, ab);
+    build_ab(M, xr, ft, ct, k, a.lin ? a.lin + ((size_t)q * N + k) * 6 : nullptr, ab);
     __syncthreads();
     const double* Pk = P + (size_t)k * NX * NX;
     double* Pn = P + (size_t)(k + 1) * NX * NX;
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(PT) void k_policy(PolicyArgs<T> a) {
   double* lc = lam0;
   double* ln = lam1;
   for (int j = N - 1; j >= 0; --j) {
-    build_ab(M, xr, ft, ct, j, ab);
+    build_ab(M, xr, ft, ct, j, a.lin ? a.lin + ((size_t)q * N + j) * 6 : nullptr, ab);
     __syncthreads();
     const double* Bj = ab + NX * NX;
     for (int e = tid; e < NU * NX; e += PT) {

@@ -492,6 +492,16 @@ __global__ __launch_bounds__(64) void k_sqp_final(SqpArgs a) {
   if (threadIdx.x == 0 && a.x) rollout_cost(M, V, false, 0.0, nullptr, a.x + (size_t)q * (N + 1) * NX, feet);
 }
 
+// lin <- (c_k, F_k) of the nonlinear rollout of u (the point cmpc_sqp_policy_batch linearises the QP at).
+__global__ __launch_bounds__(64) void k_sqp_lin(SqpArgs a) {
+  const int q = blockIdx.x;
+  const DevModel* M = a.model;
+  const int N = M->N;
+  View V = stage(a, q, sqp_lds, a.u + (size_t)q * N * NU, nullptr, nullptr, nullptr);
+  __syncthreads();
+  if (threadIdx.x == 0) rollout_cost(M, V, false, 0.0, a.lin + (size_t)q * N * 6, nullptr, false);
+}
+
 // number of QPs not yet done -> count[0]
 __global__ __launch_bounds__(256) void k_sqp_count(const int* done, int B, int* count) {
   int c = 0;
@@ -514,6 +524,7 @@ int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream) {
     case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), lds, stream, a); break;
     case 2: hipLaunchKernelGGL(k_sqp_final, dim3(B), dim3(64), lds, stream, a); break;
     case 3: hipLaunchKernelGGL(k_sqp_count, dim3(1), dim3(256), 0, stream, a.done, B, a.count); break;
+    case 4: hipLaunchKernelGGL(k_sqp_lin, dim3(B), dim3(64), lds, stream, a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

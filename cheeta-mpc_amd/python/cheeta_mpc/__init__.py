@@ -95,6 +95,7 @@ def lib():
     L.cmpc_nlp_solve_batch.argtypes = [vp, C.c_int, d, d, d, u8, C.c_int, C.c_double, d, d, d, i, i, i, vp]
     L.cmpc_condense_lin_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, d, d, d, i, i, i, d, d, vp]
     L.cmpc_policy_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, C.c_double, d, i, i, vp]
+    L.cmpc_sqp_policy_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, C.c_double, d, i, i, vp]
     L.cmpc_shift_inputs.argtypes = [C.c_int, C.c_int, d, C.c_int, d, vp]
     L.cmpc_solve_batch_host.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i]
     L.cmpc_condense_batch.argtypes = [vp, C.c_int, d, d, d, u8, d, d, i, i, vp]
@@ -377,6 +378,21 @@ class Engine:
         st = DeviceArray((B,), np.int32)
         _chk(lib().cmpc_policy_batch(self.ctx, B, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr, act_tol, K.ptr,
                                      nf.ptr, st.ptr, None), "cmpc_policy_batch")
+        _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        return K.host(), nf.host(), st.host()
+
+    def sqp_policy(self, x0, xref, foot, contact, u, act_tol=0.0):
+        """Feedback policy of the QP linearised at the nonlinear rollout of u (cmpc_sqp_policy_batch)."""
+        B = x0.shape[0]
+        N = self.model.N
+        d = [DeviceArray.from_host(np.asarray(a, t)) for a, t in
+             ((x0, np.float64), (xref, np.float64), (foot, np.float64), (contact, np.uint8),
+              (np.asarray(u, np.float64).reshape(B, N, NL, 3), np.float64))]
+        K = DeviceArray((B, N, NL, 3, NX), np.float64)
+        nf = DeviceArray((B,), np.int32)
+        st = DeviceArray((B,), np.int32)
+        _chk(lib().cmpc_sqp_policy_batch(self.ctx, B, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr, act_tol,
+                                         K.ptr, nf.ptr, st.ptr, None), "cmpc_sqp_policy_batch")
         _hchk(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
         return K.host(), nf.host(), st.host()
 

@@ -223,6 +223,13 @@ int cmpc_nlp_solve_batch_host(cmpc_ctx* ctx, int B, const double* x0, const doub
 int cmpc_policy_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
                       const uint8_t* d_contact, const double* d_u, double act_tol, double* d_K, int* d_nfree,
                       int* d_status, void* stream);
+/* Same for the QP linearised at the nonlinear rollout of u (the SQP's subproblem at its solution: lever arm p - c_k,
+ * dt F_k x c coupling; e.g. u from cmpc_sqp_solve_batch, which ends on a fixed point of that QP): the feedback ocs2
+ * reads off the last QP of its SQP (MultipleShootingSolver.cpp:334-362), with the linearisation point held fixed.
+ * Oracle: oracle_policy_lin. */
+int cmpc_sqp_policy_batch(cmpc_ctx* ctx, int B, const double* d_x0, const double* d_xref, const double* d_foot,
+                          const uint8_t* d_contact, const double* d_u, double act_tol, double* d_K, int* d_nfree,
+                          int* d_status, void* stream);
 /* Receding-horizon shift of a batch of solutions on the device: out[q][k] = u[q][min(k + shift, N - 1)] (the role of
  * MultipleShootingSolver::initializeStateInputTrajectories, MultipleShootingSolver.cpp:220-266, on a fixed grid).
  * d_u_out must not alias d_u. */

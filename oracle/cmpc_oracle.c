@@ -2008,13 +2008,21 @@ int oracle_policy_triple(double mu, const double* ub, const double* f, double to
  * Returns CMPC_SUCCESS, CMPC_INVALID_CONTACT, or CMPC_NAN_SOL when Z' H Z is not positive definite. */
 int oracle_policy(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                   const double* u, double act_tol, double* K, int* n_free) {
+  return oracle_policy_lin(c, xref, foot, contact, NULL, u, act_tol, K, n_free);
+}
+
+/* Same for the QP linearised at lin [N][6] (oracle_srbd_dynamics_lin; NULL: the reference linearisation): the
+ * feedback of the SQP's subproblem at its solution (ocs2 reads the Riccati gains of the last QP,
+ * MultipleShootingSolver.cpp:334-362). The linearisation point is held fixed, as HPIPM's factorisation is. */
+int oracle_policy_lin(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                      const double* lin, const double* u, double act_tol, double* K, int* n_free) {
   const int N = c->N, L = c->L, nf = NU * N;
   *n_free = 0;
   memset(K, 0, sizeof(double) * nf * NX);
   double* Hf = (double*)malloc(sizeof(double) * nf * nf);
   double* gf = (double*)malloc(sizeof(double) * nf);
   double x0z[NX] = {0};
-  int st = oracle_condense_full(c, x0z, xref, foot, contact, Hf, gf);
+  int st = oracle_condense_full_lin(c, x0z, xref, foot, contact, lin, Hf, gf);
   if (st != CMPC_SUCCESS) {
     free(Hf);
     free(gf);
@@ -2023,7 +2031,7 @@ int oracle_policy(const oracle_consts* c, const double* xref, const double* foot
   /* F = sum_k G_k' Q_{k+1} P_{k+1}, P_{k+1} = A_k P_k (P_0 = I), G_{k+1} = A_k G_k + [B_k at step k] */
   double* A = (double*)malloc(sizeof(double) * N * NX * NX);
   double* Bm = (double*)malloc(sizeof(double) * N * NX * NU);
-  oracle_srbd_dynamics(c, xref, foot, contact, A, Bm);
+  oracle_srbd_dynamics_lin(c, xref, foot, contact, lin, A, Bm, NULL);
   double* G = (double*)calloc((size_t)NX * nf, sizeof(double));
   double* G2 = (double*)malloc(sizeof(double) * NX * nf);
   double* F = (double*)calloc((size_t)nf * NX, sizeof(double));

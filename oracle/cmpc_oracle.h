@@ -163,6 +163,8 @@ void oracle_chol_solve(int n, const double* L, int lda, double* b);   /* solves 
 int oracle_policy_triple(double mu, const double* ub, const double* f, double tol, double* Z);
 int oracle_policy(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
                   const double* u, double act_tol, double* K, int* n_free);
+int oracle_policy_lin(const oracle_consts* c, const double* xref, const double* foot, const uint8_t* contact,
+                      const double* lin, const double* u, double act_tol, double* K, int* n_free);
 
 
 /* The same QP solved without condensing, HPIPM-style: the shared Mehrotra IPM with its Newton systems solved by a

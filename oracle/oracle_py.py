@@ -111,6 +111,8 @@ def lib():
         L.oracle_srbd_dynamics_lin.argtypes = [C.c_void_p, d, d, u8, d, d, d, d]
         L.oracle_srbd_dynamics_lin.restype = None
         L.oracle_policy.argtypes = [C.c_void_p, d, d, u8, d, C.c_double, d, i]
+        L.oracle_policy_lin.argtypes = [C.c_void_p, d, d, u8, d, d, C.c_double, d, i]
+        L.oracle_solve_one_lin.argtypes = [C.c_void_p, P(Settings), d, d, d, u8, d, d, d, i]
         L.oracle_policy_triple.argtypes = [C.c_double, d, d, C.c_double, d]
         L.oracle_riccati_solve_batch.argtypes = [P(Model), P(Settings), C.c_int, d, d, d, u8, d, i, i, C.c_int]
         L.oracle_riccati_gain0.argtypes = [C.c_void_p, d, d, u8, d]
@@ -520,17 +522,32 @@ def riccati_gain0(model, xref, foot, contact):
     return K0, st
 
 
-def policy(model, xref, foot, contact, u, act_tol=1e-5):
-    """Feedback policy dU/dx0 of one QP at its solution u [N,L,3] (oracle_policy): (K [N,L,3,13], n_free, status)."""
+def policy(model, xref, foot, contact, u, act_tol=1e-5, lin=None):
+    """Feedback policy dU/dx0 of one QP at its solution u [N,L,3] (oracle_policy; lin [N,6]: the QP linearised
+    there, oracle_policy_lin): (K [N,L,3,13], n_free, status)."""
     N = model.N
     c = consts(model)
     K = np.zeros((N, NL, 3, NX))
     nfree = C.c_int(0)
     xref, foot, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (xref, foot, u))
     contact = np.ascontiguousarray(contact, dtype=np.uint8)
-    st = lib().oracle_policy(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8), _p(u), act_tol, _p(K),
-                             C.byref(nfree))
+    ln = None if lin is None else np.ascontiguousarray(lin, dtype=np.float64)
+    st = lib().oracle_policy_lin(C.byref(c), _p(xref), _p(foot), _p(contact, C.c_uint8),
+                                 _p(ln) if ln is not None else None, _p(u), act_tol, _p(K), C.byref(nfree))
     return K, nfree.value, st
+
+
+def solve_one_lin(model, settings, x0, xref, foot, contact, lin, u_init=None):
+    """One QP linearised at lin [N,6] (oracle_solve_one_lin): (u [N,L,3], status, iters)."""
+    N = model.N
+    c = consts(model)
+    u = np.zeros((N, NL, 3)) if u_init is None else np.array(u_init, dtype=np.float64).reshape(N, NL, 3)
+    x0, xref, foot, lin = _f64(x0, xref, foot, lin)
+    contact = np.ascontiguousarray(contact, dtype=np.uint8)
+    it = C.c_int(0)
+    st = lib().oracle_solve_one_lin(C.byref(c), C.byref(settings), _p(x0), _p(xref), _p(foot),
+                                    _p(contact, C.c_uint8), _p(lin), _p(u), None, C.byref(it))
+    return u, st, it.value
 
 
 def policy_triple(mu, ub, f, tol):

@@ -149,3 +149,56 @@ def test_oracle_policy_equals_riccati_feedback_when_unconstrained(op, N, gait):
         K0, rst = op.riccati_gain0(m, xref[q], foot[q], contact[q])
         assert rst == 0
         assert np.abs(K[0] - K0).max() / max(1.0, np.abs(K0).max()) < 1e-9
+
+
+@pytest.mark.parametrize("ub4", [None, 15.0])
+def test_oracle_policy_at_sqp_linearisation_matches_finite_differences(op, ub4):
+    """The feedback of the QP linearised at the SQP solution (oracle_policy_lin): central differences of that QP's
+    solution map in x0 with the linearisation point held fixed, as HPIPM's factorisation of the last QP is."""
+    N = 10
+    m = _model(op, N, ub4)
+    s = op.tight_settings()
+    x0, xref, foot, contact = op.generate(m, SEED + 3, 2, gait=1)
+    for q in range(2):
+        u = op.sqp_solve(m, s, x0[q], xref[q], foot[q], contact[q], sqp_iter_max=20, sqp_tol=1e-10)[0]
+        lin = op.nlp_rollout_cost(m, x0[q], xref[q], foot[q], contact[q], u)[2]
+        uq, st, _ = op.solve_one_lin(m, s, x0[q], xref[q], foot[q], contact[q], lin)
+        assert st == 0
+        K, nfree, pst = op.policy(m, xref[q], foot[q], contact[q], uq, lin=lin)
+        assert pst == 0
+        h = 1e-4
+        fd = np.zeros_like(K)
+        for j in range(12):
+            dp, dm = x0[q].copy(), x0[q].copy()
+            dp[j] += h
+            dm[j] -= h
+            up = op.solve_one_lin(m, s, dp, xref[q], foot[q], contact[q], lin)[0]
+            um = op.solve_one_lin(m, s, dm, xref[q], foot[q], contact[q], lin)[0]
+            fd[..., j] = (up - um) / (2 * h)
+        assert np.abs(fd[..., :12] - K[..., :12]).max() / max(1.0, np.abs(K).max()) < 1e-6
+        # differs from the policy of the reference-linearised QP
+        K0 = op.policy(m, xref[q], foot[q], contact[q], uq)[0]
+        assert np.abs(K - K0).max() > 1e-6 * max(1.0, np.abs(K).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,gait,ub4", [(10, 1, 15.0), (20, 0, None)])
+def test_device_sqp_policy_matches_oracle(cm, op, N, gait, ub4):
+    """cmpc_sqp_policy_batch at the device SQP's solution against oracle_policy_lin at the same u, linearised at its
+    nonlinear rollout (classes 64 / 128 at N = 10 mixed, 128 at N = 20)."""
+    B = 16
+    m, mo = cm.default_model(N), _model(op, N, ub4)
+    if ub4 is not None:
+        m.force_ub[4] = ub4
+    x0, xref, foot, contact = op.generate(mo, SEED + 5, B, gait=gait)
+    eng = cm.Engine(m, precision=0, max_batch=B)
+    u, _, st, _, _ = eng.sqp_solve(x0, xref, foot, contact, sqp_iter_max=10, sqp_tol=1e-7, want_x=False)
+    assert np.all(st == 0)
+    K, nfree, pst = eng.sqp_policy(x0, xref, foot, contact, u)
+    K0 = eng.policy(x0, xref, foot, contact, u)[0]
+    for q in range(B):
+        lin = op.nlp_rollout_cost(mo, x0[q], xref[q], foot[q], contact[q], u[q])[2]
+        Kr, nfr, sr = op.policy(mo, xref[q], foot[q], contact[q], u[q], lin=lin)
+        assert pst[q] == sr == 0 and nfree[q] == nfr
+        assert np.abs(K[q] - Kr).max() / max(1.0, np.abs(Kr).max()) < 1e-9, q
+    assert np.abs(K - K0).max() > 1e-6  # not the reference-linearised QP's policy
