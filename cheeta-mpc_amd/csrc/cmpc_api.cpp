@@ -390,6 +390,14 @@ int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const 
     ia.app_reset = c->qcount + 3 + 3 * (c->fused_parity ^ 1);
     ia.app_ld = B;
   }
+  if (c->ld >= 128) {
+    // Under stream capture the graph is replayed with this call's parity frozen, so nothing would re-zero this
+    // slice between replays: the captured call zeroes it itself (a memset node); uncaptured calls keep relying on
+    // the previous call's reset (no extra launch on the hot path).
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return -2;
+    if (cs == hipStreamCaptureStatusActive && hipMemsetAsync(cnt, 0, 3 * sizeof(int), st) != hipSuccess) return -2;
+  }
   if (launch_solve64(ia, ca, B, st) != 0) return -2;
   if (c->ld < 128) return 0;
   c->fused_parity ^= 1;
