@@ -226,6 +226,9 @@ def main():
                          "come from as many profiled steps run right after them")
     ap.add_argument("--ric", type=int, choices=[0, 1, 2], default=0,
                     help="CMPC_PATH_RICCATI: 0 condensed, 1 stage-wise kernel for the n > 64 classes, 2 for every QP")
+    ap.add_argument("--path", action="append", default=[], metavar="OPTION=VALUE",
+                    help="kernel-path option of the context (cmpc_set_path; A/B runs): FUSED64, FUSED128, DIRECT or "
+                         "RICCATI, e.g. --path FUSED128=1; repeatable")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="QPs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's CPU share (cpu_share())")
     ap.add_argument("--traffic-json", default="",
@@ -263,7 +266,11 @@ def main():
     else:
         settings = cm.default_settings(tol_stat=1e-3, tol_ineq=1e-3, tol_comp=1e-4)
     K = max(1, args.inflight)
-    path = {cm.PATH_RICCATI: args.ric} if args.ric else None
+    path = {cm.PATH_RICCATI: args.ric} if args.ric else {}
+    for kv in args.path:
+        k, v = kv.split("=")
+        path[getattr(cm, "PATH_" + k.upper())] = int(v)
+    path = path or None
     engs = [cm.Engine(model, settings, precision=prec, max_batch=B, path=path) for _ in range(K)]
     eng = engs[0]
     x0, xref, foot, contact = cm.generate_device(model, SEED, B, gait=args.gait, offset=rank * B)
@@ -474,6 +481,7 @@ def main():
         "stages_ms": stages,
         "fused_n64": fused,
         "inflight": K,
+        "path": {k: eng.get_path(getattr(cm, "PATH_" + k)) for k in ("FUSED64", "FUSED128", "DIRECT", "RICCATI")},
         "stage_events": args.stage_events,
         "value_end_to_end": value_e2e,
         "gather_ms": gather.get("gather_ms_per_step"), "gather": gather,

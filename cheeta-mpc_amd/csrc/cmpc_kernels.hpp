@@ -23,6 +23,16 @@ __host__ __device__ inline int ipm_class(int n) { return n <= 64 ? 64 : (n <= 12
 __host__ __device__ inline int h_index(int npad, int i, int j) {
   return npad == 64 ? (((i >> 2) * 4 + (j >> 4)) * 64 + (i & 3) * 16 + (j & 15)) : i * npad + j;
 }
+// Classes 64 and 256 store only the lower-or-diagonal 16 x 16 tiles of H (h_stored: tile column <= tile row). The
+// strictly upper tiles are exact transposes of the lower ones (the condensing builds them that way): k_ipm64 reads
+// them as the mirrored elements of the 40 stored rows it loads anyway (20 KB instead of 32 KB of H per QP and
+// iteration from MALL: headline PMC traffic 1.30 -> 0.73 GB per launch), k_ipm_tiled reads lower tiles only. Class
+// 128 stays full: k_ipm128x's mirrored loads (16 rows per instruction) cost more time than the traffic they saved
+// (configs 3 / 5: +5 % / +2.5 %, profiles/r03_hsym_ab.txt). Readers of an arbitrary element go through h_index_sym.
+__host__ __device__ inline bool h_stored(int i, int j) { return (j >> 4) <= (i >> 4); }
+__host__ __device__ inline int h_index_sym(int npad, int i, int j) {
+  return (npad == 128 || h_stored(i, j)) ? h_index(npad, i, j) : h_index(npad, j, i);
+}
 
 // Per-QP workspace of one context (precision T), QP-major:
 //   H [B][ld][ld], g [B][ld], tri_mu [B][ld/3], tri_lo/tri_hi [B][ld/3][5], tri_map [B][ld/3], nvar [B],

@@ -366,10 +366,11 @@ __device__ __forceinline__ int condense64_qp(const CondenseArgs<T>& a, const int
     }
   }
 
-  // ---- outputs: H (class 64, tile order), g, pyramid data, status
+  // ---- outputs: H (class 64, tile order, the 40 lower-or-diagonal register rows: h_stored), g, pyramid data, status
   T* Hq = a.H + (size_t)q * ld * ld;
 #pragma unroll
-  for (int e = 0; e < 64; ++e) Hq[e * 64 + lane] = K[e];
+  for (int e = 0; e < 64; ++e)
+    if ((e & 3) <= (e >> 4)) Hq[e * 64 + lane] = K[e];
   if (lane < ld) a.g[(size_t)q * ld + lane] = colv ? gcol : T(0);
   if (lane < ld / 3 && lane < 64 / 3) {
     const int t = lane;

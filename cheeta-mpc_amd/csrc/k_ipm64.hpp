@@ -357,11 +357,20 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
   };
 
   const T* Hq = A.H + (size_t)q * ld * ld;
-  // H in tile order (64 coalesced 512-B rows) into the registers of the factor
+  // H in tile order into the registers of the factor: the 40 stored rows (coalesced 512 B each), then the 24 strictly
+  // upper registers as the mirrored elements of those rows (h_stored): register (r, c), c > r / 4, of lane
+  // (a, b) is H[b + 16c][a + 4r] = stored register 16c + 4 (b >> 2) + (r >> 2), lane 16 (b & 3) + a + 4 (r & 3)
   auto load_H = [&]() {
     const int ln = olane();
-#pragma unroll
-    for (int e = 0; e < 64; ++e) K[e] = Hq[e * 64 + ln];
+    sfor<0, 64>([&](auto e_) {
+      constexpr int e = decltype(e_)::value;
+      if constexpr ((e & 3) <= (e >> 4)) K[e] = Hq[e * 64 + ln];
+    });
+    const int mt = ((ln & 15) >> 2) * 256 + (ln & 3) * 16 + (ln >> 4);
+    sfor<0, 64>([&](auto e_) {
+      constexpr int e = decltype(e_)::value, r = e >> 2, c = e & 3;
+      if constexpr (c > (r >> 2)) K[e] = Hq[(16 * c + (r >> 2)) * 64 + 4 * (r & 3) + mt];
+    });
   };
 
   // Newton direction for the complementarity targets in L.rml / L.rmu. After the iteration's last solve the factor

@@ -801,7 +801,7 @@ __global__ __launch_bounds__(256) void k_unpack_qp(const T* H_ws, const T* g_ws,
   double* ho = H + (size_t)q * ld * ld;
   for (int e = threadIdx.x; e < ld * ld; e += blockDim.x) {
     const int r = e / ld, c = e % ld;
-    ho[e] = (r < np && c < np) ? (double)hq[h_index(np, r, c)] : (r == c ? 1.0 : 0.0);
+    ho[e] = (r < np && c < np) ? (double)hq[h_index_sym(np, r, c)] : (r == c ? 1.0 : 0.0);
   }
   for (int i = threadIdx.x; i < ld; i += blockDim.x) g[(size_t)q * ld + i] = i < np ? (double)g_ws[(size_t)q * ld + i] : 0.0;
 }

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(PT) void k_policy(PolicyArgs<T> a) {
     double s = 0.0;
     for (int x = 0; x < 3; ++x) {
       double hz = 0.0;
-      for (int y = 0; y < 3; ++y) hz += (double)Hq[h_index(npad, 3 * t1 + x, 3 * t2 + y)] * Z[t2 * 9 + y * 3 + c2];
+      for (int y = 0; y < 3; ++y) hz += (double)Hq[h_index_sym(npad, 3 * t1 + x, 3 * t2 + y)] * Z[t2 * 9 + y * 3 + c2];
       s += Z[t1 * 9 + x * 3 + c1] * hz;
     }
     Hr[r1 * m + r2] = s;

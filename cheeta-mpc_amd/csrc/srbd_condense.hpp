@@ -468,7 +468,9 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
             if (cc < n && S.s_next[cc] == rr) v += S.s_offR[cc];
           }
           Hq[h_index(npad, rr, cc)] = v;  // class-packed block in the order the IPM of class npad reads
-          if (ti != tj) Hq[h_index(npad, cc, rr)] = v;
+          // classes 64 / 256: lower tiles only (h_stored); the NMAX = 128 kernels keep the unconditional mirror
+          // (the run-time class test alone made k_solve128<float> 1.4 % slower)
+          if (ti != tj && (NMAX == 128 || npad == 128)) Hq[h_index(npad, cc, rr)] = v;
         }
       }
     }
