@@ -481,7 +481,7 @@ def main():
         "stages_ms": stages,
         "fused_n64": fused,
         "inflight": K,
-        "path": {k: eng.get_path(getattr(cm, "PATH_" + k)) for k in ("FUSED64", "FUSED128", "DIRECT", "RICCATI")},
+        "path": {k: eng.get_path(getattr(cm, "PATH_" + k)) for k in ("FUSED64", "FUSED128", "DIRECT", "RICCATI", "IPM72")},
         "stage_events": args.stage_events,
         "value_end_to_end": value_e2e,
         "gather_ms": gather.get("gather_ms_per_step"), "gather": gather,

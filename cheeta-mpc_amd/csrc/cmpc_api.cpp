@@ -42,14 +42,15 @@ struct cmpc_ctx {
   int* nvar;
   int* status;
   int* iters;
-  int* qlist;   // [3][max_batch] per-class QP lists (k_class_lists)
-  int* qcount;  // [9]: k_class_lists' counts, then the fused path's two alternating append counters
+  int* qlist;   // [4][max_batch] per-class QP lists (k_class_lists; the fourth: 64 < n <= 72 for k_ipm72)
+  int* qcount;  // [10]: k_class_lists' counts, the fused path's two alternating append counters, the fourth list's
   int fused_parity = 0;  // fused path: this call appends to qcount[3 + 3 parity] and zeroes the other slice
   // kernel path (cmpc_set_path; every choice gives bit-identical results):
   bool fused;     // cold-start cmpc_solve_batch runs the fused n <= 64 kernel (k_solve64); possible when N <= 21
   bool fused128;  // fused path: the 64 < n <= 128 class as one condensing + IPM launch (k_solve128)
   bool direct;    // fused path without rollout: the IPM kernels scatter the results (no k_expand)
   int ric = 0;    // stage-wise (Riccati) kernel k_ric: 0 off, 1 the n > 64 classes of the fused path, 2 every QP
+  bool ipm72 = true;  // separate IPM launches: 64 < n <= 72 on the bordered one-wave kernel (k_ipm72)
   double *lin, *uj, *uq, *dj, *dq;
   int *stq, *itq, *done, *sqpi, *qpi, *cnt;
   void* res_scr;
@@ -106,8 +107,8 @@ Layout layout(int ld, int precision, int B, int N) {
   L.nvar = take((size_t)B * sizeof(int));
   L.status = take((size_t)B * sizeof(int));
   L.iters = take((size_t)B * sizeof(int));
-  L.qlist = take((size_t)3 * B * sizeof(int));
-  L.qcount = take(9 * sizeof(int));  // [0..2] k_class_lists; [3..5], [6..8] appended by k_solve64 (call parity)
+  L.qlist = take((size_t)4 * B * sizeof(int));  // [3]: k_ipm72's part of the 128 class (run_ipm_classes)
+  L.qcount = take(10 * sizeof(int));  // [0..2] k_class_lists; [3..5], [6..8] appended by k_solve64 (call parity); [9]
   // SQP (cmpc_sqp_solve_batch): linearisation points, iterate, QP solution, per-QP flags and counters
   L.lin = take((size_t)B * MAXN * 6 * 8);
   L.uj = take((size_t)B * MAXN * NU * 8);
@@ -317,11 +318,20 @@ template <typename T>
 int run_ipm_classes(cmpc_ctx* c, const IpmArgs<T>& a, int B, hipStream_t st, bool lists_ready) {
   if (B <= 0) return 0;
   if (c->ld < 128) return launch_ipm<T>(a, B, st);  // one class
-  if (!lists_ready && launch_class_lists(a.status, a.nvar, B, 1, c->qlist, c->qcount, st) != 0) return -2;
+  // with k_ipm72 the lists are always rebuilt here, the 128 class split at n = 72 (list 3, count qcount[9])
+  if ((c->ipm72 || !lists_ready) &&
+      launch_class_lists(a.status, a.nvar, B, 1, c->qlist, c->qcount, st, c->ipm72 ? 72 : 0) != 0)
+    return -2;
   IpmArgs<T> al = a;
   for (int k = 0; k < 3; ++k) al.qlist[k] = c->qlist + (size_t)k * B;
   al.qcount = c->qcount;
   int r = launch_ipm64(al, B, st);
+  if (r == 0 && c->ipm72) {  // 64 < n <= 72 on one wave (the NLP's trot subproblems); list 1 holds n > 72 now
+    IpmArgs<T> a72 = al;
+    a72.qlist[1] = c->qlist + (size_t)3 * B;
+    a72.qcount = c->qcount + 8;  // k_ipm72 reads qcount[1] = the fourth list's count, qcount[9]
+    r = launch_ipm72(a72, B, st);
+  }
   if (r == 0) r = launch_ipm128(al, B, st);
   if (r == 0 && c->ld >= 256) r = launch_ipm256(al, B, st);
   return r;
@@ -588,7 +598,7 @@ int cmpc_create(const cmpc_model* model, const cmpc_settings* settings, int prec
   c->res = (double*)(c->ws + L.res);
   c->qlist = (int*)(c->ws + L.qlist);
   c->qcount = (int*)(c->ws + L.qcount);
-  if (hipMemset(c->qcount, 0, 9 * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+  if (hipMemset(c->qcount, 0, 10 * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     if (c->own_ws) (void)hipFree(c->ws);
     delete c;
     return CMPC_ERR_HIP;
@@ -658,6 +668,9 @@ int cmpc_set_path(cmpc_ctx* c, int option, int value) {
     case CMPC_PATH_DIRECT:
       c->direct = value != 0;
       return CMPC_OK;
+    case CMPC_PATH_IPM72:
+      c->ipm72 = value != 0;
+      return CMPC_OK;
     default:
       return CMPC_ERR_ARG;
   }
@@ -681,6 +694,7 @@ int cmpc_get_path(const cmpc_ctx* c, int option) {
     case CMPC_PATH_FUSED128: return c->fused128 ? 1 : 0;
     case CMPC_PATH_DIRECT: return c->direct ? 1 : 0;
     case CMPC_PATH_RICCATI: return c->ric;
+    case CMPC_PATH_IPM72: return c->ipm72 ? 1 : 0;
     default: return CMPC_ERR_ARG;
   }
 }

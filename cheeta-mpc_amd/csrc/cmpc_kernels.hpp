@@ -136,6 +136,8 @@ int launch_solve64(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B,
 // fused workgroup condensing + IPM of the 64 < n <= 128 class over its class list (k_solve128, k_ipm128x.hpp)
 int launch_solve128(const IpmArgs<double>& a, const CondenseArgs<double>& c, int B, hipStream_t stream);
 int launch_solve128(const IpmArgs<float>& a, const CondenseArgs<float>& c, int B, hipStream_t stream);
+int launch_ipm72(const IpmArgs<double>& a, int B, hipStream_t stream);   // 64 < n <= 72 (k_ipm72.hpp, one wave)
+int launch_ipm72(const IpmArgs<float>& a, int B, hipStream_t stream);
 int launch_ipm128(const IpmArgs<double>& a, int B, hipStream_t stream);  // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm128(const IpmArgs<float>& a, int B, hipStream_t stream);   // 64 < n <= 128 (k_ipm128x.hpp, 4 waves)
 int launch_ipm256(const IpmArgs<double>& a, int B, hipStream_t stream);  // 128 < n <= 256 (k_ipm256.hpp)
@@ -252,9 +254,10 @@ int launch_shift_inputs(const double* in, int N, int shift, double* out, int B, 
 
 // per-class QP lists: lists [3][B] (ascending QP ids), counts [3]; one workgroup. by_status != 0: QPs with
 // status == CMPC_SUCCESS, classed by nvar; by_status == 0: QPs with nvar > 0 (the condensing hints, written for every
-// QP by the first condensing kernel)
+// QP by the first condensing kernel). n_mid > 64: the 128 class is split, list 1 = n_mid < n <= 128 and a fourth
+// list (lists + 3 B, count in counts[9]) = 64 < n <= n_mid (k_ipm72's QPs)
 int launch_class_lists(const int* status, const int* nvar, int B, int by_status, int* lists, int* counts,
-                       hipStream_t stream);
+                       hipStream_t stream, int n_mid = 0);
 
 // widen/narrow helpers used by the test hooks
 int launch_convert_f32_to_f64(const float* in, double* out, size_t n, hipStream_t stream);

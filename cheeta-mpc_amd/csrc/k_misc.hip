@@ -220,11 +220,12 @@ int launch_expand(const ExpandArgs& a, int B, hipStream_t stream) {
 // One workgroup of 16 waves walks the batch in 1024-QP tiles: per class a wave ballot gives each QP its rank inside
 // the wave, wave totals through LDS give the tile offsets, so every list is in ascending QP order (deterministic).
 __global__ __launch_bounds__(1024) void k_class_lists(const int* status, const int* nvar, int B, int by_status,
-                                                      int* lists, int* counts) {
-  __shared__ int s_wtot[3][16];
-  __shared__ int s_base[3];
+                                                      int n_mid, int* lists, int* counts) {
+  __shared__ int s_wtot[4][16];
+  __shared__ int s_base[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid < 3) s_base[tid] = 0;
+  const int ncls = n_mid > 64 ? 4 : 3;
+  if (tid < 4) s_base[tid] = 0;
   // the next tile's hints are requested before this tile's scans, so the loads overlap the barriers
   int nv_next = tid < B ? nvar[tid] : 0;
   int st_next = (by_status && tid < B) ? status[tid] : CMPC_SUCCESS;
@@ -237,11 +238,13 @@ __global__ __launch_bounds__(1024) void k_class_lists(const int* status, const i
       if (by_status) st_next = status[q + 1024];
     }
     int cls = -1;
-    if (q < B && stv == CMPC_SUCCESS && (by_status || nv > 0)) cls = nv <= 64 ? 0 : (nv <= 128 ? 1 : 2);
+    if (q < B && stv == CMPC_SUCCESS && (by_status || nv > 0)) {
+      cls = nv <= 64 ? 0 : (nv <= 128 ? 1 : 2);
+      if (cls == 1 && nv <= n_mid) cls = 3;
+    }
     int pre = 0;
     const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < ncls; ++c) {
       const unsigned long long mask = __ballot(cls == c);
       if (cls == c) pre = __popcll(mask & below);
       if (lane == 0) s_wtot[c][w] = __popcll(mask);
@@ -253,20 +256,20 @@ __global__ __launch_bounds__(1024) void k_class_lists(const int* status, const i
       lists[(size_t)cls * B + off + pre] = q;
     }
     __syncthreads();
-    if (tid < 3) {
+    if (tid < ncls) {
       int t = 0;
       for (int v = 0; v < 16; ++v) t += s_wtot[tid][v];
       s_base[tid] += t;
     }
     __syncthreads();
   }
-  if (tid < 3) counts[tid] = s_base[tid];
+  if (tid < ncls) counts[tid < 3 ? tid : 9] = s_base[tid];
 }
 
 int launch_class_lists(const int* status, const int* nvar, int B, int by_status, int* lists, int* counts,
-                       hipStream_t stream) {
+                       hipStream_t stream, int n_mid) {
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_class_lists, dim3(1), dim3(1024), 0, stream, status, nvar, B, by_status, lists, counts);
+  hipLaunchKernelGGL(k_class_lists, dim3(1), dim3(1024), 0, stream, status, nvar, B, by_status, n_mid, lists, counts);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

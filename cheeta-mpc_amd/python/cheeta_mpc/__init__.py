@@ -17,8 +17,9 @@ LIB_PATH = os.environ.get("CMPC_LIB") or os.path.join(PKG_ROOT, "lib", "libcmpc.
 NX, NU, NL = 13, 12, 4
 F64, F32 = 0, 1
 # kernel-path options of a context (cmpc_set_path; the first three give bit-identical results; PATH_RICCATI: 0 off,
-# 1 the n > 64 classes of the fused path, 2 every QP through the stage-wise kernel)
-PATH_FUSED64, PATH_FUSED128, PATH_DIRECT, PATH_RICCATI = 0, 1, 2, 3
+# 1 the n > 64 classes of the fused path, 2 every QP through the stage-wise kernel; PATH_IPM72: 64 < n <= 72 on the bordered
+# one-wave kernel where the IPM runs as its own launch)
+PATH_FUSED64, PATH_FUSED128, PATH_DIRECT, PATH_RICCATI, PATH_IPM72 = 0, 1, 2, 3, 4
 STATUS = {0: "SUCCESS", 1: "MAX_ITER", 2: "MIN_STEP", 3: "NAN_SOL", 4: "INCONS_EQ", 5: "INVALID_CONTACT",
           6: "TOO_LARGE"}
 

@@ -155,9 +155,19 @@ int cmpc_ctx_fused(const cmpc_ctx* ctx);
  *                       2: every cold-start QP is (one launch). Results agree with the condensed path to rounding,
  *                       not bit for bit (a different factorisation of the same Newton systems). Needs N <= 21; 1 needs
  *                       CMPC_PATH_FUSED64 = 1.
+ *   CMPC_PATH_IPM72     1 (default): where the IPM runs as its own launch (warm starts, the SQP / NLP subproblems,
+ *                       CMPC_PATH_FUSED64 = 0), QPs with 64 < n <= 72 (the NLP's trot subproblems at N = 10: 60 forces
+ *                       and two to four foothold triples) are solved by a one-wave kernel on the bordered Newton system (Schur
+ *                       complement of the 64 x 64 block); 0: by the four-wave 128 class. Results agree to rounding.
  * cmpc_set_path returns CMPC_ERR_ARG for an unknown option or a value out of range (0 / 1; 0 / 1 / 2 for
  * CMPC_PATH_RICCATI); cmpc_get_path returns the current value or CMPC_ERR_ARG. */
-enum cmpc_path_option { CMPC_PATH_FUSED64 = 0, CMPC_PATH_FUSED128 = 1, CMPC_PATH_DIRECT = 2, CMPC_PATH_RICCATI = 3 };
+enum cmpc_path_option {
+  CMPC_PATH_FUSED64 = 0,
+  CMPC_PATH_FUSED128 = 1,
+  CMPC_PATH_DIRECT = 2,
+  CMPC_PATH_RICCATI = 3,
+  CMPC_PATH_IPM72 = 4
+};
 int cmpc_set_path(cmpc_ctx* ctx, int option, int value);
 int cmpc_get_path(const cmpc_ctx* ctx, int option);
 
