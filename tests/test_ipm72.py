@@ -16,11 +16,13 @@ def rel_err(u, ur):
 
 
 def contact_with(N, B, n_triples, rng):
-    """Contact tables with exactly n_triples stance legs (the swing ones at random later steps)."""
-    c = np.ones((B, N, 4), np.uint8)
+    """Contact tables with exactly n_triples stance legs, at least one per step (a step without one is
+    INVALID_CONTACT, CentroidalMPC.cpp:328-330)."""
+    c = np.zeros((B, N, 4), np.uint8)
     for q in range(B):
-        off = rng.choice(np.arange(4, 4 * N), size=4 * N - n_triples[q], replace=False)
-        c[q].reshape(-1)[off] = 0
+        c[q, np.arange(N), rng.integers(0, 4, size=N)] = 1
+        free = np.flatnonzero(c[q].reshape(-1) == 0)
+        c[q].reshape(-1)[rng.choice(free, size=n_triples[q] - N, replace=False)] = 1
     return c
 
 
@@ -95,3 +97,23 @@ def test_nlp_bordered_class_matches_128_class(cm, op, prec):
     if prec == 0:
         assert np.array_equal(i1, i0)
         assert np.abs(q1.astype(int) - q0.astype(int)).max() <= 1
+
+
+def test_every_class_in_one_batch(cm, op):
+    """One N = 20 batch with n = 60 / 66 / 69 / 72 / 120 / 240 through the separate IPM launches (k_class_lists with
+    the 128 class split at 72: lists 0..3 at once, k_ipm64 / k_ipm72 / k_ipm128x / k_ipm_tiled), against the oracle."""
+    N = 20
+    m, mo = cm.default_model(N), op.default_model(N)
+    rng = np.random.default_rng(5)
+    sizes = [20, 22, 23, 24, 40, 80] * 3
+    B = len(sizes)
+    x0, xref, foot, _ = op.generate(mo, SEED, B, gait=0)
+    contact = contact_with(N, B, sizes, rng)
+    ur, _, st_r, it_r = op.solve_batch(mo, op.default_settings(), x0, xref, foot, contact, want_x=False)
+    eng = cm.Engine(m, precision=0, max_batch=B, path={cm.PATH_FUSED64: 0})
+    assert eng.ld == 256
+    u, _, st, it = eng.solve(x0, xref, foot, contact, want_x=False)
+    assert np.array_equal(st, st_r) and np.all(st == 0), (st, st_r)
+    assert np.array_equal(it, it_r), (it, it_r)
+    for q in range(B):
+        assert rel_err(u[q], ur[q]) < 1e-8, q
