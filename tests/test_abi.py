@@ -125,3 +125,14 @@ def test_step_ratio_extreme_fp32_values():
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp"), "bin/test_step_ratio"])
     out = subprocess.check_output([os.path.join(ROOT, "tests", "cpp", "bin", "test_step_ratio")], text=True)
     assert "step_ratio: ok" in out, out
+
+
+def test_path_option_constants_match_header():
+    """cheeta_mpc.PATH_* mirror enum cmpc_path_option of include/cmpc/cmpc.h (cmpc_set_path / cmpc_get_path)."""
+    import cheeta_mpc
+    txt = open(os.path.join(ROOT, "include", "cmpc", "cmpc.h")).read()
+    body = re.search(r"enum cmpc_path_option\s*\{(.*?)\}", txt, flags=re.S).group(1)
+    enum = {k: int(v) for k, v in re.findall(r"CMPC_PATH_([A-Z0-9]+)\s*=\s*(\d+)", body)}
+    assert set(enum) == {"FUSED64", "FUSED128", "DIRECT", "RICCATI", "IPM72"}
+    for k, v in enum.items():
+        assert getattr(cheeta_mpc, "PATH_" + k) == v, k
