@@ -117,3 +117,29 @@ def test_every_class_in_one_batch(cm, op):
     assert np.array_equal(it, it_r), (it, it_r)
     for q in range(B):
         assert rel_err(u[q], ur[q]) < 1e-8, q
+
+
+def test_bordered_class_non_finite_input(cm, op):
+    """A NaN in the gradient of an n = 66 / 72 QP gives the oracle's status (NAN_SOL) on both kernels; its neighbours
+    in the batch are unaffected."""
+    N, B = 6, 6
+    m, mo = cm.default_model(N), op.default_model(N)
+    rng = np.random.default_rng(3)
+    x0, xref, foot, _ = op.generate(mo, SEED, B, gait=0)
+    contact = contact_with(N, B, [22, 24] * 3, rng)
+    Hs, gs, ns, mus, los, his = [], [], [], [], [], []
+    for q in range(B):
+        n, H, g, mu, lo, hi, mp, st = op.condense(mo, x0[q], xref[q], foot[q], contact[q], ld=128)
+        Hs.append(H); gs.append(g); ns.append(n); mus.append(mu); los.append(lo); his.append(hi)
+    gs[1][5] = np.nan   # tile variable (n = 72)
+    gs[2][65] = np.nan  # border variable (n = 66)
+    ref = [op.qp_ipm(ns[q], Hs[q], gs[q], mus[q], los[q], his[q], op.default_settings()) for q in range(B)]
+    st_r = np.array([r[3] for r in ref])
+    assert st_r[1] == st_r[2] == 3 and np.all(np.delete(st_r, [1, 2]) == 0)
+    for v in (1, 0):
+        eng = cm.Engine(m, precision=0, max_batch=B, path={cm.PATH_IPM72: v})
+        u, st, it = eng.qp_solve(np.array(Hs), np.array(gs), np.array(ns, np.int32), np.array(mus), np.array(los),
+                                 np.array(his))
+        assert np.array_equal(st, st_r), (v, st, st_r)
+        for q in np.nonzero(st_r == 0)[0]:
+            assert rel_err(u[q, :ns[q]], ref[q][0]) < 1e-9, (v, q)
