@@ -69,14 +69,29 @@ def cpu_share():
     return n, why
 
 
+def oracle_fast_build():
+    """The -O3 oracle build for this host: liboracle_fast_v4.so (x86-64-v4, AVX-512) when /proc/cpuinfo lists the v4
+    feature set, else liboracle_fast.so (x86-64-v3). Returns (file name, ISA level)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            flags = next((ln.split(":", 1)[1].split() for ln in f if ln.startswith("flags")), [])
+    except OSError:
+        flags = []
+    v4 = {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"}
+    if v4.issubset(flags) and os.path.exists(os.path.join(ROOT, "oracle", "liboracle_fast_v4.so")):
+        return "liboracle_fast_v4.so", "x86-64-v4"
+    return "liboracle_fast.so", "x86-64-v3"
+
+
 def cpu_baseline(model_n, x0, xref, foot, contact, threads, min_cpu_s=10.0, max_wall_s=5.0, riccati=False):
-    """The CPU oracle (same algorithm, fp64; the -O3 liboracle_fast.so build) on a bounded sample of the same batch,
+    """The CPU oracle (same algorithm, fp64; the -O3 build for this host's ISA level, oracle_fast_build) on a bounded
+    sample of the same batch,
     repeated until it has done about min_cpu_s of thread-time (capped at max_wall_s wall): QPs/s = QPs solved / wall
     time. riccati=True times the HPIPM-style restatement instead (no condensing; Riccati Newton steps over the stages,
     same iterates)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as op  # test infrastructure: the CPU restatement, timed as the baseline
-    op.select_build("liboracle_fast.so")
+    op.select_build(oracle_fast_build()[0])
     mo = op.default_model(model_n)
     s = op.default_settings()
     done, wall, u, st = 0, 0.0, None, None
@@ -511,7 +526,8 @@ def main():
         result["cpu_baseline"] = {"value": done / dtc, "unit": "QPs/s", "cores": threads, "kind": "port",
                                   "host_cpus": os.cpu_count(), "cpu_share": f"{share} ({share_why})",
                                   "sample": f"first {S} QPs of the same batch x{done // S}, oracle/cmpc_oracle.c "
-                                            f"fp64 (same algorithm) built -O3 -march=x86-64-v3 (liboracle_fast.so), "
+                                            f"fp64 (same algorithm) built -O3 -march={oracle_fast_build()[1]} "
+                                            f"({oracle_fast_build()[0]}), "
                                             f"{threads} pthreads, {dtc:.2f} s wall"}
         result["max_rel_du_vs_cpu_fp64"] = float(rel[both].max()) if both.any() else None
         ur, str_, dtr, doner = cpu_baseline(N, hx0, hxr, hft, ct[:S], threads, riccati=True)
