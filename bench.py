@@ -235,6 +235,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent batches in flight: step i runs on context / stream i %% K (a serving pattern; "
                          "each step is still one full batch through the whole hot path). Default 1: the headline")
+    ap.add_argument("--graph", type=int, choices=[0, 1], default=0,
+                    help="1: each context's step is captured once into a hipGraph (stream capture of cmpc_solve_batch) "
+                         "and the timed steps replay it (the stage times then come from direct steps after them)")
     ap.add_argument("--stage-events", choices=["timed", "after"], default="timed",
                     help="timed: HIP events around every stage of every timed step (the roofline's kernel times come "
                          "from the timed region itself); after: the timed steps run without events and the stage times "
@@ -322,7 +325,31 @@ def main():
         step(i)
     H.hipDeviceSynchronize()
 
-    timed_events = args.stage_events == "timed"
+    direct_step = step
+    if args.graph and args.sqp_iters > 0:
+        sys.exit("bench.py: --graph captures cmpc_solve_batch only (the SQP reads a convergence flag back per iteration)")
+    if args.graph:  # one captured step per context / stream; the timed loop replays them
+        for fn, at in (("hipStreamBeginCapture", [C.c_void_p, C.c_int]),
+                       ("hipStreamEndCapture", [C.c_void_p, C.POINTER(C.c_void_p)]),
+                       ("hipGraphInstantiate", [C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t]),
+                       ("hipGraphLaunch", [C.c_void_p, C.c_void_p])):
+            getattr(H, fn).argtypes = at
+        exes = []
+        for k in range(K):
+            g, ex = C.c_void_p(), C.c_void_p()
+            cm._hchk(H.hipStreamBeginCapture(streams[k], 0), "hipStreamBeginCapture")
+            direct_step(k)
+            cm._hchk(H.hipStreamEndCapture(streams[k], C.byref(g)), "hipStreamEndCapture")
+            cm._hchk(H.hipGraphInstantiate(C.byref(ex), g, None, None, 0), "hipGraphInstantiate")
+            exes.append(ex)
+
+        def step(i):
+            cm._hchk(H.hipGraphLaunch(exes[i % K], streams[i % K]), "hipGraphLaunch")
+        for i in range(args.warmup):
+            step(i)
+        H.hipDeviceSynchronize()
+
+    timed_events = args.stage_events == "timed" and not args.graph
     if timed_events:
         cm.lib().cmpc_profile_begin(eng.ctx, (args.steps + K - 1) // K)
     barrier()
@@ -339,7 +366,7 @@ def main():
     if not timed_events:  # stage times from the same number of profiled steps right after the timed ones
         cm.lib().cmpc_profile_begin(eng.ctx, (args.steps + K - 1) // K)
         for i in range(args.steps):
-            step(i)
+            direct_step(i)
         H.hipDeviceSynchronize()
     ms = [C.c_double(0), C.c_double(0), C.c_double(0)]
     ncalls = C.c_int(0)
@@ -496,6 +523,7 @@ def main():
         "stages_ms": stages,
         "fused_n64": fused,
         "inflight": K,
+        "graph": bool(args.graph),
         "path": {k: eng.get_path(getattr(cm, "PATH_" + k)) for k in ("FUSED64", "FUSED128", "DIRECT", "RICCATI", "IPM72")},
         "stage_events": args.stage_events,
         "value_end_to_end": value_e2e,
