@@ -242,6 +242,10 @@ def main():
                     help="timed: HIP events around every stage of every timed step (the roofline's kernel times come "
                          "from the timed region itself); after: the timed steps run without events and the stage times "
                          "come from as many profiled steps run right after them")
+    ap.add_argument("--event-frac", type=float, default=0.25,
+                    help="with --stage-events timed: the events bracket the stages of the last this fraction of the "
+                         "timed steps (each timed event costs ~1 %% of a headline step: 4 per call, 3-4 %% with "
+                         "every step profiled, profiles/r03d_events_ab.txt); 1 = every timed step")
     ap.add_argument("--ric", type=int, choices=[0, 1, 2], default=0,
                     help="CMPC_PATH_RICCATI: 0 condensed, 1 stage-wise kernel for the n > 64 classes, 2 for every QP")
     ap.add_argument("--path", action="append", default=[], metavar="OPTION=VALUE",
@@ -350,12 +354,16 @@ def main():
         H.hipDeviceSynchronize()
 
     timed_events = args.stage_events == "timed" and not args.graph
-    if timed_events:
-        cm.lib().cmpc_profile_begin(eng.ctx, (args.steps + K - 1) // K)
+    # context 0's calls in the timed loop are steps 0, K, 2K, ...; the last n_prof of them carry the stage events
+    n_ctx0 = (args.steps + K - 1) // K
+    n_prof = min(n_ctx0, max(1, int(np.ceil(n_ctx0 * min(max(args.event_frac, 0.0), 1.0)))))
+    i_prof = (n_ctx0 - n_prof) * K
     barrier()
     H.hipDeviceSynchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if timed_events and i == i_prof:
+            cm.lib().cmpc_profile_begin(eng.ctx, n_prof)
         step(i)
     for sh in streams:
         H.hipStreamSynchronize(sh)
@@ -526,6 +534,7 @@ def main():
         "graph": bool(args.graph),
         "path": {k: eng.get_path(getattr(cm, "PATH_" + k)) for k in ("FUSED64", "FUSED128", "DIRECT", "RICCATI", "IPM72")},
         "stage_events": args.stage_events,
+        "stage_event_steps": n_prof if timed_events else None,
         "value_end_to_end": value_e2e,
         "gather_ms": gather.get("gather_ms_per_step"), "gather": gather,
         "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
