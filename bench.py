@@ -197,18 +197,37 @@ def launch_ranks(n, argv):
     return 0
 
 
+def device_census(dist, my_id, allow_shared):
+    """The distinct physical GPUs (PCI identities) the ranks serve. Every rank gets the same answer; a run whose ranks
+    share a GPU is refused (exit 2, reason on stderr) unless --allow-shared, which labels the line shared_gpu.
+    Returns (n_distinct, ids)."""
+    ids = dist.gather_object(my_id)
+    n = len(set(ids))
+    if n < dist.world and not allow_shared:
+        if dist.rank == 0:
+            print(f"bench.py: --gpus {dist.world} but the ranks serve only {n} distinct GPU(s) {sorted(set(ids))}; "
+                  f"refused (pass --allow-shared to measure ranks sharing a GPU, labelled shared_gpu)", file=sys.stderr)
+        dist.close()
+        sys.exit(2)
+    return n, ids
+
+
 def stub_rank(args):
-    """--stub (CPU tests of the launcher): the rank set-up, barriers and max-over-ranks of a real run over gloo, no
-    HIP call; rank 0 prints a JSON line carrying n_gpus like the real one. --stub-fail-rank r makes rank r exit 3."""
+    """--stub (CPU tests of the launcher): the rank set-up, device census, barriers and max-over-ranks of a real run
+    over gloo, no HIP call; rank 0 prints a JSON line carrying n_gpus like the real one. --stub-fail-rank r makes rank
+    r exit 3; --stub-devices a,b,.. gives rank r the PCI identity entry r (default: one distinct device per rank)."""
     sys.path.insert(0, os.path.join(ROOT, "cheeta-mpc_amd", "python"))
     from cheeta_mpc.shard import Dist
     dist = Dist()
     if dist.rank == args.stub_fail_rank:
         sys.exit(3)
+    devs = args.stub_devices.split(",") if args.stub_devices else [f"0000:{r:02x}:00.0" for r in range(dist.world)]
+    n_dev, ids = device_census(dist, devs[dist.rank % len(devs)], args.allow_shared)
     dist.barrier()
     t = dist.max(float(dist.rank))
     if dist.rank == 0:
-        print(json.dumps({"metric": "stub", "n_gpus": dist.world, "max_rank": t, "stub": True}), flush=True)
+        print(json.dumps({"metric": "stub", "n_gpus": n_dev, "n_ranks": dist.world, "shared_gpu": n_dev < dist.world,
+                          "devices": ids, "max_rank": t, "stub": True}), flush=True)
     dist.close()
 
 
@@ -256,8 +275,12 @@ def main():
     ap.add_argument("--traffic-json", default="",
                     help="PMC summary giving roofline.traffic (default: profiles/traffic_<workload key>.json)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pass (solve + result gather timed)")
+    ap.add_argument("--allow-shared", action="store_true",
+                    help="let ranks share a GPU (rehearsal on a one-GPU box); the line then says shared_gpu and n_gpus "
+                         "counts distinct devices")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-devices", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     ws = os.environ.get("WORLD_SIZE")
@@ -276,8 +299,10 @@ def main():
     ndev = cm.device_count()
     if ndev <= 0:
         raise RuntimeError("bench.py: no HIP device visible")
-    # one GPU per rank; the modulo covers launchers that expose only the rank's own GPU (HIP_VISIBLE_DEVICES)
+    # one GPU per rank; the modulo covers launchers that expose only the rank's own GPU (HIP_VISIBLE_DEVICES); the
+    # census refuses ranks that would share a device (one visible GPU for --gpus N > 1) unless --allow-shared
     cm._hchk(cm.hip().hipSetDevice(dist.local_rank % ndev), "hipSetDevice")
+    n_dev, dev_ids = device_census(dist, cm.device_pci_id(dist.local_rank % ndev), args.allow_shared)
     barrier, max_over_ranks = dist.barrier, dist.max
 
     B, N = args.batch, args.horizon
@@ -417,7 +442,6 @@ def main():
                 e2e = max_over_ranks(t1 - t0)
                 value_e2e = world * B * args.steps / e2e
                 gather["ms_per_step"] = e2e / args.steps * 1e3
-                gather["gather_ms_per_step"] = (e2e - elapsed) / args.steps * 1e3
                 # rank 0's buffer now holds every rank's U of the last step: its own slice must equal its solve
                 if rank == 0:
                     got = rg.host(np.float64, (world * B, N, 4, 3))[:B]
@@ -501,6 +525,12 @@ def main():
                                            ms_cond, "mfma", "condense", "condensing FLOPs")}
 
     value = world * B * args.steps / elapsed
+    # the gather's cost: end-to-end minus compute, both measured on this run; only where there is a gather to other
+    # ranks (world > 1), and never negative (the two passes differ by run-to-run noise where the copy is cheap)
+    gather_ms = None
+    if world > 1 and gather.get("ms_per_step") is not None:
+        gather_ms = max(0.0, gather["ms_per_step"] - elapsed / args.steps * 1e3)
+        gather["gather_ms_per_step"] = gather_ms
     result = {
         # BASELINE.json's metric for the headline configuration; other workloads name their own N and batch.
         # "vs HPIPM" is the metric's name: HPIPM cannot be built offline, so max_rel_du_vs_cpu_fp64 below is
@@ -511,7 +541,10 @@ def main():
                    f"{'' if K == 1 else f', {K} batches in flight'}; max|du| vs fp64 CPU oracle"),
         "value": value,
         "unit": "QPs/s",
-        "n_gpus": world,
+        "n_gpus": n_dev,
+        "n_ranks": world,
+        "shared_gpu": n_dev < world,
+        "devices": dev_ids,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -536,7 +569,7 @@ def main():
         "stage_events": args.stage_events,
         "stage_event_steps": n_prof if timed_events else None,
         "value_end_to_end": value_e2e,
-        "gather_ms": gather.get("gather_ms_per_step"), "gather": gather,
+        "gather_ms": gather_ms, "gather": gather,
         "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,
                    "mean_n": float(nvar.mean())},

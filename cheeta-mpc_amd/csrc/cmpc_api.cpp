@@ -473,25 +473,6 @@ int ensure_stage(cmpc_ctx* c, size_t bytes) {
   return CMPC_OK;
 }
 
-// Offsets of A, B, b (k < N) and Q, S, R, q, r (k <= N) inside one packed OCP record ([8][N+1], cmpc.h layout).
-std::vector<size_t> ocp_offsets(int N, int nx, const int* nu) {
-  std::vector<size_t> offs(8 * (size_t)(N + 1), 0);
-  size_t o = 0;
-  for (int k = 0; k < N; ++k) {
-    offs[0 * (N + 1) + k] = o; o += (size_t)nx * nx;
-    offs[1 * (N + 1) + k] = o; o += (size_t)nx * nu[k];
-    offs[2 * (N + 1) + k] = o; o += (size_t)nx;
-  }
-  for (int k = 0; k <= N; ++k) {
-    const size_t m = k < N ? (size_t)nu[k] : 0;
-    offs[3 * (N + 1) + k] = o; o += (size_t)nx * nx;
-    offs[4 * (N + 1) + k] = o; o += m * nx;
-    offs[5 * (N + 1) + k] = o; o += m * m;
-    offs[6 * (N + 1) + k] = o; o += (size_t)nx;
-    offs[7 * (N + 1) + k] = o; o += m;
-  }
-  return offs;
-}
 
 }  // namespace
 
@@ -1195,226 +1176,9 @@ int cmpc_generate_batch(const cmpc_model* m, uint64_t seed, int64_t qp_offset, i
              : CMPC_ERR_HIP;
 }
 
-size_t cmpc_ocp_record_size(int N, int nx, const int* nu) {
-  if (N <= 0 || nx <= 0 || !nu) return 0;
-  size_t o = 0;
-  for (int k = 0; k < N; ++k) o += (size_t)nx * nx + (size_t)nx * nu[k] + nx;
-  for (int k = 0; k <= N; ++k) {
-    const size_t m = k < N ? (size_t)nu[k] : 0;
-    o += (size_t)nx * nx + m * nx + m * m + nx + m;
-  }
-  return o;
-}
-
-size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* nc) {
-  if (N <= 0 || nx <= 0 || !nu || !nc) return 0;
-  size_t o = 0;
-  for (int k = 0; k <= N; ++k) {
-    const size_t m = k < N ? (size_t)nu[k] : 0;
-    o += (size_t)nc[k] * (nx + m + 1);
-  }
-  return o;
-}
-
 }  // extern "C"
 
-namespace {
-
-// Shared host path of cmpc_ocp_solve_batch_host / cmpc_ocp_solve_batch_eq_host (nc == nullptr: no constraints).
-int ocp_solve_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
-                   const double* crec, double* x, double* u, int* status) {
-  if (B < 0 || N <= 0 || N > CMPC_OCP_MAX_N || nx <= 0 || nx > 64 || !nu || !x0 || !rec || !x || !u || !status)
-    return CMPC_ERR_ARG;
-  if (nc && !crec) return CMPC_ERR_ARG;
-  if (B == 0) return CMPC_OK;
-  int nU = 0, nE = 0;
-  for (int k = 0; k < N; ++k) {
-    if (nu[k] < 0) return CMPC_ERR_ARG;
-    nU += nu[k];
-  }
-  if (nc)
-    for (int k = 0; k <= N; ++k) {
-      if (nc[k] < 0) return CMPC_ERR_ARG;
-      nE += nc[k];
-    }
-  const int ldo = nU > 0 ? nU : 1;
-  const size_t rs = cmpc_ocp_record_size(N, nx, nu);
-  const size_t crs = nE ? cmpc_ocp_constraint_record_size(N, nx, nu, nc) : 0;
-  std::vector<size_t> offs = ocp_offsets(N, nx, nu);
-  std::vector<size_t> coffs(3 * (size_t)(N + 1), 0);
-  {
-    size_t o = 0;
-    for (int k = 0; k <= N && nE; ++k) {
-      const size_t m = k < N ? (size_t)nu[k] : 0;
-      coffs[(size_t)k] = o; o += (size_t)nc[k] * nx;
-      coffs[(size_t)(N + 1) + k] = o; o += (size_t)nc[k] * m;
-      coffs[2 * (size_t)(N + 1) + k] = o; o += (size_t)nc[k];
-    }
-  }
-  std::vector<int> nuv(nu, nu + N);
-  nuv.push_back(0);
-  int *d_nu = nullptr, *d_st = nullptr, *d_nc = nullptr;
-  size_t *d_offs = nullptr, *d_coffs = nullptr;
-  double *d_x0 = nullptr, *d_rec = nullptr, *d_H = nullptr, *d_g = nullptr, *d_sc = nullptr, *d_x = nullptr,
-         *d_u = nullptr, *d_crec = nullptr, *d_esc = nullptr;
-  int r = CMPC_OK;
-  auto ck = [&r](hipError_t e) { if (e != hipSuccess) r = CMPC_ERR_HIP; };
-  const size_t scr = 2 * (size_t)nx * ldo + 4 * (size_t)nx;
-  ck(hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)));
-  ck(hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()));
-  ck(hipMalloc((void**)&d_x0, sizeof(double) * B * nx));
-  ck(hipMalloc((void**)&d_rec, sizeof(double) * B * rs));
-  ck(hipMalloc((void**)&d_H, sizeof(double) * B * ldo * ldo));
-  ck(hipMalloc((void**)&d_g, sizeof(double) * B * ldo));
-  ck(hipMalloc((void**)&d_sc, sizeof(double) * B * scr));
-  ck(hipMalloc((void**)&d_x, sizeof(double) * B * (N + 1) * nx));
-  ck(hipMalloc((void**)&d_u, sizeof(double) * B * ldo));
-  ck(hipMalloc((void**)&d_st, sizeof(int) * B));
-  if (nE) {
-    ck(hipMalloc((void**)&d_nc, sizeof(int) * (N + 1)));
-    ck(hipMalloc((void**)&d_coffs, sizeof(size_t) * coffs.size()));
-    ck(hipMalloc((void**)&d_crec, sizeof(double) * B * crs));
-    ck(hipMalloc((void**)&d_esc, sizeof(double) * B * ocp_eq_scratch(nE, ldo)));
-  }
-  if (r == CMPC_OK) {
-    ck(hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice));
-    ck(hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice));
-    ck(hipMemcpy(d_x0, x0, sizeof(double) * B * nx, hipMemcpyHostToDevice));
-    ck(hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice));
-    if (nE) {
-      ck(hipMemcpy(d_nc, nc, sizeof(int) * (N + 1), hipMemcpyHostToDevice));
-      ck(hipMemcpy(d_coffs, coffs.data(), sizeof(size_t) * coffs.size(), hipMemcpyHostToDevice));
-      ck(hipMemcpy(d_crec, crec, sizeof(double) * B * crs, hipMemcpyHostToDevice));
-    }
-    OcpArgs a;
-    a.N = N;
-    a.nx = nx;
-    a.nU = nU;
-    a.nu = d_nu;
-    a.offs = d_offs;
-    a.rec_size = rs;
-    a.x0 = d_x0;
-    a.rec = d_rec;
-    a.H = d_H;
-    a.g = d_g;
-    a.ldo = ldo;
-    a.scratch = d_sc;
-    a.x = d_x;
-    a.u = d_u;
-    a.status = d_st;
-    if (nE) {
-      a.nc = d_nc;
-      a.coffs = d_coffs;
-      a.crec_size = crs;
-      a.crec = d_crec;
-      a.nE = nE;
-      a.escratch = d_esc;
-    }
-    if (r == CMPC_OK && (launch_ocp_solve(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess)) r = CMPC_ERR_HIP;
-    if (r == CMPC_OK) {
-      ck(hipMemcpy(x, d_x, sizeof(double) * B * (N + 1) * nx, hipMemcpyDeviceToHost));
-      if (nU > 0)
-        for (int b = 0; b < B; ++b)
-          ck(hipMemcpy(u + (size_t)b * nU, d_u + (size_t)b * nU, sizeof(double) * nU, hipMemcpyDeviceToHost));
-      ck(hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost));
-    }
-  }
-  for (void* pfree : {(void*)d_nu, (void*)d_offs, (void*)d_x0, (void*)d_rec, (void*)d_H, (void*)d_g, (void*)d_sc,
-                      (void*)d_x, (void*)d_u, (void*)d_st, (void*)d_nc, (void*)d_coffs, (void*)d_crec, (void*)d_esc})
-    if (pfree) (void)hipFree(pfree);
-  return r;
-}
-
-}  // namespace
-
 extern "C" {
-
-int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
-                              double* u, int* status) {
-  return ocp_solve_host(B, N, nx, nu, nullptr, x0, rec, nullptr, x, u, status);
-}
-
-int cmpc_ocp_solve_batch_eq_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0,
-                                 const double* rec, const double* crec, double* x, double* u, int* status) {
-  if (!nc) return CMPC_ERR_ARG;
-  return ocp_solve_host(B, N, nx, nu, nc, x0, rec, crec, x, u, status);
-}
-
-int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const double* rec, double* Sm, double* sv,
-                                double* K, double* kff, int* status) {
-  if (B < 0 || N <= 0 || N > CMPC_OCP_MAX_N || nx <= 0 || nx > CMPC_RIC_MAX_DIM || !nu || !rec || !Sm || !sv ||
-      !status)
-    return CMPC_ERR_ARG;
-  if (B == 0) return CMPC_OK;
-  int nU = 0;
-  for (int k = 0; k < N; ++k) {
-    if (nu[k] < 0 || nu[k] > CMPC_RIC_MAX_DIM) return CMPC_ERR_ARG;
-    nU += nu[k];
-  }
-  if (nU > 0 && (!K || !kff)) return CMPC_ERR_ARG;
-  const size_t rs = cmpc_ocp_record_size(N, nx, nu);
-  std::vector<size_t> offs = ocp_offsets(N, nx, nu);
-  std::vector<int> nuv(nu, nu + N);
-  nuv.push_back(0);
-  const size_t nK = (size_t)nU * nx, nSm = (size_t)(N + 1) * nx * nx, nsv = (size_t)(N + 1) * nx;
-  int* d_nu = nullptr;
-  int* d_st = nullptr;
-  size_t* d_offs = nullptr;
-  double *d_rec = nullptr, *d_Sm = nullptr, *d_sv = nullptr, *d_K = nullptr, *d_k = nullptr, *d_sc = nullptr;
-  int r = CMPC_OK;
-  auto ck = [&r](hipError_t e) { if (e != hipSuccess) r = CMPC_ERR_HIP; };
-  if (hipMalloc((void**)&d_nu, sizeof(int) * (N + 1)) != hipSuccess ||
-      hipMalloc((void**)&d_offs, sizeof(size_t) * offs.size()) != hipSuccess ||
-      hipMalloc((void**)&d_rec, sizeof(double) * B * rs) != hipSuccess ||
-      hipMalloc((void**)&d_Sm, sizeof(double) * B * nSm) != hipSuccess ||
-      hipMalloc((void**)&d_sv, sizeof(double) * B * nsv) != hipSuccess ||
-      hipMalloc((void**)&d_K, sizeof(double) * B * (nK > 0 ? nK : 1)) != hipSuccess ||
-      hipMalloc((void**)&d_k, sizeof(double) * B * (nU > 0 ? nU : 1)) != hipSuccess ||
-      hipMalloc((void**)&d_sc, sizeof(double) * B * ric_scratch(nx)) != hipSuccess ||
-      hipMalloc((void**)&d_st, sizeof(int) * B) != hipSuccess)
-    r = CMPC_ERR_HIP;
-  if (r == CMPC_OK) {
-    ck(hipMemcpy(d_nu, nuv.data(), sizeof(int) * (N + 1), hipMemcpyHostToDevice));
-    ck(hipMemcpy(d_offs, offs.data(), sizeof(size_t) * offs.size(), hipMemcpyHostToDevice));
-    ck(hipMemcpy(d_rec, rec, sizeof(double) * B * rs, hipMemcpyHostToDevice));
-    RiccatiArgs a;
-    a.N = N;
-    a.nx = nx;
-    a.nu = d_nu;
-    a.offs = d_offs;
-    a.rec_size = rs;
-    a.rec = d_rec;
-    a.Sm = d_Sm;
-    a.sv = d_sv;
-    a.K = d_K;
-    a.kff = d_k;
-    a.scratch = d_sc;
-    a.nK = (int)nK;
-    a.nU = nU;
-    a.status = d_st;
-    if (r == CMPC_OK && (launch_ocp_riccati(a, B, nullptr) != 0 || hipDeviceSynchronize() != hipSuccess))
-      r = CMPC_ERR_HIP;
-    if (r == CMPC_OK) {
-      ck(hipMemcpy(Sm, d_Sm, sizeof(double) * B * nSm, hipMemcpyDeviceToHost));
-      ck(hipMemcpy(sv, d_sv, sizeof(double) * B * nsv, hipMemcpyDeviceToHost));
-      if (nU > 0) {
-        ck(hipMemcpy(K, d_K, sizeof(double) * B * nK, hipMemcpyDeviceToHost));
-        ck(hipMemcpy(kff, d_k, sizeof(double) * B * nU, hipMemcpyDeviceToHost));
-      }
-      ck(hipMemcpy(status, d_st, sizeof(int) * B, hipMemcpyDeviceToHost));
-    }
-  }
-  (void)hipFree(d_nu);
-  (void)hipFree(d_offs);
-  (void)hipFree(d_rec);
-  (void)hipFree(d_Sm);
-  (void)hipFree(d_sv);
-  (void)hipFree(d_K);
-  (void)hipFree(d_k);
-  (void)hipFree(d_sc);
-  (void)hipFree(d_st);
-  return r;
-}
 
 const char* cmpc_status_string(int s) {
   switch (s) {
@@ -1425,6 +1189,7 @@ const char* cmpc_status_string(int s) {
     case CMPC_INCONS_EQ: return "INCONS_EQ";
     case CMPC_INVALID_CONTACT: return "INVALID_CONTACT";
     case CMPC_TOO_LARGE: return "TOO_LARGE";
+    case CMPC_INFEASIBLE_STEP: return "INFEASIBLE_STEP";
     default: return "UNKNOWN";
   }
 }

@@ -289,56 +289,4 @@ size_t policy_scratch_doubles(int N, int ld);
 template <typename T>
 int launch_policy(const PolicyArgs<T>& a, int nq, hipStream_t stream);
 
-// generic OCP (HpipmInterface::solve semantics)
-struct OcpArgs {
-  int N, nx, nU;
-  const int* nu;       // device [N+1]
-  const size_t* offs;  // device [8][N+1] record offsets (A,B,b,Q,S,R,q,r)
-  size_t rec_size;
-  const double* x0;    // [B][nx]
-  const double* rec;   // [B][rec_size]
-  double* H;           // [B][ldo][ldo] workspace
-  double* g;           // [B][ldo]
-  int ldo;
-  double* scratch;     // [B][2*nx*ldo + 4*nx]
-  double* x;           // [B][N+1][nx]
-  double* u;           // [B][nU]
-  int* status;
-  // equality constraints C_k x_k + D_k u_k + e_k = 0 (cmpc_ocp_solve_batch_eq_host); crec == nullptr: none
-  const int* nc = nullptr;        // device [N+1] rows per node
-  const size_t* coffs = nullptr;  // device [3][N+1] constraint-record offsets (C, D, e)
-  size_t crec_size = 0;
-  const double* crec = nullptr;   // [B][crec_size]
-  int nE = 0;                     // sum_k nc_k
-  double* escratch = nullptr;     // [B][ocp_eq_scratch(nE, ldo)]
-};
-#define CMPC_OCP_MAX_N 256
-// per-problem scratch of the equality-constrained solve: E [nE][ldo], W [ldo][nE+1], S [nE][nE], f, lam, drop [nE]
-__host__ __device__ inline size_t ocp_eq_scratch(int nE, int ldo) {
-  return (size_t)nE * ldo + (size_t)ldo * (nE + 1) + (size_t)nE * nE + 3 * (size_t)nE;
-}
-int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream);
-
-// Riccati recursion of the same OCP (HpipmInterface::getRiccati*, HpipmInterface.cpp:330-455)
-struct RiccatiArgs {
-  int N, nx;
-  const int* nu;       // device [N+1]
-  const size_t* offs;  // device [8][N+1] record offsets
-  size_t rec_size;
-  const double* rec;   // [B][rec_size]
-  double* Sm;          // [B][N+1][nx*nx] column-major
-  double* sv;          // [B][N+1][nx]
-  double* K;           // [B][sum nu_k * nx] stage blocks nu_k x nx column-major
-  double* kff;         // [B][sum nu_k]
-  double* scratch;     // [B][RIC_SCRATCH(nx)]
-  int nK, nU;          // sum nu_k * nx, sum nu_k (per problem)
-  int* status;
-};
-#define CMPC_RIC_MAX_DIM 64
-__host__ __device__ inline size_t ric_scratch(int nx) {
-  const size_t m = CMPC_RIC_MAX_DIM;
-  return (size_t)nx * nx + nx * m + nx + m * nx + m * m + m + m * (nx + 1);
-}
-int launch_ocp_riccati(const RiccatiArgs& a, int B, hipStream_t stream);
-
 }  // namespace cmpc

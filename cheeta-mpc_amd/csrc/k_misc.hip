@@ -1,5 +1,5 @@
 // k_misc.hip — the small kernels around the hot path: synthetic input generation, result scatter/rollout,
-// precision conversion, and the generic OCP-QP path behind HpipmInterface::solve.
+// precision conversion, class lists, warm-start packing (the HpipmInterface::solve path is k_ocp.hip).
 #include "cmpc_device.hpp"
 #include "cmpc_kernels.hpp"
 
@@ -310,484 +310,6 @@ int launch_convert_f64_to_f32(const double* in, float* out, size_t n, hipStream_
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// ------------------------------------------------------------------------------------------ generic OCP-QP
-// HpipmInterface::Impl::solve semantics (HpipmInterface.cpp:166-301): x0 eliminated (b0 = f0 + A0 x0, r0 += S0 x0,
-// :177-208), condensed to U-space, Cholesky-solved, states rolled out, non-finite solution -> NAN_SOL (:290-295).
-// Equality constraints C_k x_k + D_k u_k + e_k = 0 (the reference hands them to HPIPM as lg = ug = -e, :223-264, with
-// the stage-0 rows bounded by -e_0 - C_0 x0, :236-244) are condensed alongside the cost, row by row at their node:
-// E U = f with E = C_k dx_k/dU + D_k, f = -e_k - C_k x_k(U = 0). The KKT system [H E'; E 0] is solved by the
-// range-space method: H = L L', W = L^-1 E', S = W'W = M M' (pivots at or below 1e-12 of the largest diagonal drop
-// their row: redundant rows), lam from S lam = W'(-L^-1 g) - f, U = -L^-T (L^-1 g + W lam). Rows that stay violated
-// (|E U - f| above 1e-8 of the data scale: inconsistent constraints) -> INCONS_EQ. One 256-thread workgroup per
-// problem; column-major stage matrices.
-
-#define OCP_CM(M, ld, r, c) ((M)[(size_t)(c) * (ld) + (r)])
-
-__global__ __launch_bounds__(256) void k_ocp_solve(OcpArgs a) {
-  const int q = blockIdx.x;
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int N = a.N, nx = a.nx, nU = a.nU, ldo = a.ldo;
-  const double* rec = a.rec + (size_t)q * a.rec_size;
-  const size_t* oA = a.offs;
-  const size_t* oB = a.offs + (N + 1);
-  const size_t* ob = a.offs + 2 * (N + 1);
-  const size_t* oQ = a.offs + 3 * (N + 1);
-  const size_t* oS = a.offs + 4 * (N + 1);
-  const size_t* oR = a.offs + 5 * (N + 1);
-  const size_t* oq = a.offs + 6 * (N + 1);
-  const size_t* orr = a.offs + 7 * (N + 1);
-  double* H = a.H + (size_t)q * ldo * ldo;
-  double* g = a.g + (size_t)q * ldo;
-  double* G = a.scratch + (size_t)q * (2 * (size_t)nx * ldo + 4 * nx);
-  double* QG = G + (size_t)nx * ldo;
-  double* xb = QG + (size_t)nx * ldo;
-  double* tmp = xb + nx;
-  double* xb2 = tmp + nx;
-  double* u = a.u + (size_t)q * nU;
-  double* x = a.x + (size_t)q * (N + 1) * nx;
-  __shared__ int s_cu[CMPC_OCP_MAX_N + 2];
-  __shared__ int s_ro[CMPC_OCP_MAX_N + 2];
-  __shared__ int s_flag;
-  __shared__ double s_l;
-  const int nE = a.crec ? a.nE : 0;
-  const double* crec = a.crec ? a.crec + (size_t)q * a.crec_size : nullptr;
-  double* E = nE ? a.escratch + (size_t)q * ocp_eq_scratch(nE, ldo) : nullptr;
-  double* W = nE ? E + (size_t)nE * ldo : nullptr;       // [ldo][nE + 1]: L^-1 E' and, in column nE, L^-1 g
-  double* Sm = nE ? W + (size_t)ldo * (nE + 1) : nullptr;  // [nE][nE]
-  double* fe = nE ? Sm + (size_t)nE * nE : nullptr;        // [nE]
-  double* lam = nE ? fe + nE : nullptr;                    // [nE]
-  double* drop = nE ? lam + nE : nullptr;                  // [nE] 1 for a dropped (redundant) row
-  if (tid == 0) {
-    int c = 0, r = 0;
-    for (int k = 0; k < N; ++k) {
-      s_cu[k] = c;
-      c += a.nu[k];
-    }
-    s_cu[N] = c;
-    for (int k = 0; k <= N; ++k) {
-      s_ro[k] = r;
-      r += nE ? a.nc[k] : 0;
-    }
-    s_flag = 0;
-  }
-  for (int i = tid; i < nU * nU; i += nth) H[(size_t)(i / nU) * ldo + i % nU] = 0.0;
-  for (int i = tid; i < nU; i += nth) g[i] = 0.0;
-  for (int i = tid; i < nx * nU; i += nth) G[(size_t)(i / nU) * ldo + i % nU] = 0.0;
-  for (int i = tid; i < nx; i += nth) xb[i] = a.x0[(size_t)q * nx + i];
-  __syncthreads();
-  for (int k = 0; k <= N; ++k) {
-    const int m = k < N ? a.nu[k] : 0;
-    const int c0 = s_cu[k];
-    const double* Q = rec + oQ[k];
-    const double* S = rec + oS[k];
-    const double* R = rec + oR[k];
-    const double* qv = rec + oq[k];
-    const double* rv = rec + orr[k];
-    if (nE && a.nc[k] > 0) {  // constraint rows of node k against x_k = G U + xb (G, xb not modified until below)
-      const int nck = a.nc[k], r0 = s_ro[k];
-      const double* Ck = crec + a.coffs[k];
-      const double* Dk = crec + a.coffs[(N + 1) + k];
-      const double* ek = crec + a.coffs[2 * (N + 1) + k];
-      for (int e = tid; e < nck * nU; e += nth) {
-        const int rr = e / nU, b = e % nU;
-        double v = 0.0;
-        if (b < c0) {
-          for (int j = 0; j < nx; ++j) v += OCP_CM(Ck, nck, rr, j) * G[(size_t)j * ldo + b];
-        } else if (b < c0 + m) {
-          v = OCP_CM(Dk, nck, rr, b - c0);
-        }
-        E[(size_t)(r0 + rr) * ldo + b] = v;
-      }
-      for (int rr = tid; rr < nck; rr += nth) {
-        double v = -ek[rr];
-        for (int j = 0; j < nx; ++j) v -= OCP_CM(Ck, nck, rr, j) * xb[j];
-        fe[r0 + rr] = v;
-      }
-    }
-    if (k >= 1) {
-      for (int i = tid; i < nx; i += nth) {
-        double s = qv[i];
-        for (int j = 0; j < nx; ++j) s += OCP_CM(Q, nx, i, j) * xb[j];
-        tmp[i] = s;
-      }
-      for (int e = tid; e < nx * c0; e += nth) {
-        const int i = e / c0, b = e % c0;
-        double s = 0.0;
-        for (int j = 0; j < nx; ++j) s += OCP_CM(Q, nx, i, j) * G[(size_t)j * ldo + b];
-        QG[(size_t)i * ldo + b] = s;
-      }
-      __syncthreads();
-      for (int aa = tid; aa < c0; aa += nth) {
-        double s = 0.0;
-        for (int i = 0; i < nx; ++i) s += G[(size_t)i * ldo + aa] * tmp[i];
-        g[aa] += s;
-      }
-      for (int e = tid; e < c0 * c0; e += nth) {
-        const int aa = e / c0, b = e % c0;
-        double s = 0.0;
-        for (int i = 0; i < nx; ++i) s += G[(size_t)i * ldo + aa] * QG[(size_t)i * ldo + b];
-        H[(size_t)aa * ldo + b] += s;
-      }
-      __syncthreads();
-    }
-    if (m > 0) {
-      for (int aa = tid; aa < m; aa += nth) {
-        double s = rv[aa];
-        for (int j = 0; j < nx; ++j) s += OCP_CM(S, m, aa, j) * xb[j];
-        g[c0 + aa] += s;
-      }
-      for (int e = tid; e < m * m; e += nth) {
-        const int aa = e / m, b = e % m;
-        H[(size_t)(c0 + aa) * ldo + c0 + b] += OCP_CM(R, m, aa, b);
-      }
-      if (k >= 1)
-        for (int e = tid; e < m * c0; e += nth) {
-          const int aa = e / c0, b = e % c0;
-          double s = 0.0;
-          for (int j = 0; j < nx; ++j) s += OCP_CM(S, m, aa, j) * G[(size_t)j * ldo + b];
-          H[(size_t)(c0 + aa) * ldo + b] += s;
-          H[(size_t)b * ldo + c0 + aa] += s;
-        }
-      __syncthreads();
-    }
-    if (k < N) {
-      const double* A = rec + oA[k];
-      const double* Bm = rec + oB[k];
-      const double* bv = rec + ob[k];
-      const int cn = c0 + m;
-      for (int e = tid; e < nx * cn; e += nth) {
-        const int i = e / cn, b = e % cn;
-        double s = b >= c0 ? OCP_CM(Bm, nx, i, b - c0) : 0.0;
-        for (int j = 0; j < nx; ++j) s += OCP_CM(A, nx, i, j) * G[(size_t)j * ldo + b];
-        QG[(size_t)i * ldo + b] = s;
-      }
-      for (int i = tid; i < nx; i += nth) {
-        double s = bv[i];
-        for (int j = 0; j < nx; ++j) s += OCP_CM(A, nx, i, j) * xb[j];
-        xb2[i] = s;
-      }
-      __syncthreads();
-      for (int e = tid; e < nx * cn; e += nth) G[(size_t)(e / cn) * ldo + e % cn] = QG[(size_t)(e / cn) * ldo + e % cn];
-      for (int i = tid; i < nx; i += nth) xb[i] = xb2[i];
-      __syncthreads();
-    }
-  }
-  // Cholesky (right-looking, lower) + triangular solves for u = -H^{-1} g
-  for (int k = 0; k < nU; ++k) {
-    if (tid == 0) {
-      const double d = H[(size_t)k * ldo + k];
-      if (!(d > 0.0)) s_flag = 1;
-      s_l = sqrt(d);
-      H[(size_t)k * ldo + k] = s_l;
-    }
-    __syncthreads();
-    const double l = s_l;
-    for (int i = k + 1 + tid; i < nU; i += nth) H[(size_t)i * ldo + k] /= l;
-    __syncthreads();
-    const int rem = nU - k - 1;
-    for (int e = tid; e < rem * rem; e += nth) {
-      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-      if (j <= i) H[(size_t)i * ldo + j] -= H[(size_t)i * ldo + k] * H[(size_t)j * ldo + k];
-    }
-    __syncthreads();
-  }
-  for (int i = tid; i < nU; i += nth) u[i] = -g[i];
-  __syncthreads();
-  for (int k = 0; k < nU; ++k) {
-    if (tid == 0) u[k] /= H[(size_t)k * ldo + k];
-    __syncthreads();
-    for (int i = k + 1 + tid; i < nU; i += nth) u[i] -= H[(size_t)i * ldo + k] * u[k];
-    __syncthreads();
-  }
-  if (nE) {
-    // W = L^-1 E' (one thread per constraint row); column nE is L^-1 (-g) = the forward-solved u above
-    for (int rr = tid; rr < nE; rr += nth) {
-      for (int i = 0; i < nU; ++i) {
-        double v = E[(size_t)rr * ldo + i];
-        for (int j = 0; j < i; ++j) v -= H[(size_t)i * ldo + j] * W[(size_t)j * (nE + 1) + rr];
-        W[(size_t)i * (nE + 1) + rr] = v / H[(size_t)i * ldo + i];
-      }
-    }
-    for (int i = tid; i < nU; i += nth) W[(size_t)i * (nE + 1) + nE] = u[i];
-    __syncthreads();
-    // S = W'W, rhs = W'(-L^-1 g) - f
-    for (int e = tid; e < nE * nE; e += nth) {
-      const int r1 = e / nE, r2 = e % nE;
-      double v = 0.0;
-      for (int i = 0; i < nU; ++i) v += W[(size_t)i * (nE + 1) + r1] * W[(size_t)i * (nE + 1) + r2];
-      Sm[e] = v;
-    }
-    for (int rr = tid; rr < nE; rr += nth) {
-      double v = -fe[rr];
-      for (int i = 0; i < nU; ++i) v += W[(size_t)i * (nE + 1) + rr] * W[(size_t)i * (nE + 1) + nE];
-      lam[rr] = v;
-      drop[rr] = 0.0;
-    }
-    __syncthreads();
-    // S = M M' (right-looking, lower); a pivot at or below 1e-12 of the largest diagonal drops its row (lam = 0)
-    if (tid == 0) {
-      double dmax = 0.0;
-      for (int r = 0; r < nE; ++r) dmax = fmax(dmax, Sm[(size_t)r * nE + r]);
-      s_l = dmax;
-    }
-    __syncthreads();
-    const double smin = 1e-12 * s_l;
-    for (int k = 0; k < nE; ++k) {
-      const double d = Sm[(size_t)k * nE + k];
-      const bool dr = !(d > smin);
-      if (tid == 0) {
-        drop[k] = dr ? 1.0 : 0.0;
-        Sm[(size_t)k * nE + k] = dr ? 1.0 : sqrt(d);
-      }
-      __syncthreads();
-      const double l = Sm[(size_t)k * nE + k];
-      for (int i = k + 1 + tid; i < nE; i += nth) Sm[(size_t)i * nE + k] = dr ? 0.0 : Sm[(size_t)i * nE + k] / l;
-      __syncthreads();
-      const int rem = nE - k - 1;
-      for (int e = tid; e < rem * rem; e += nth) {
-        const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-        if (j <= i) Sm[(size_t)i * nE + j] -= Sm[(size_t)i * nE + k] * Sm[(size_t)j * nE + k];
-      }
-      __syncthreads();
-    }
-    // lam = S^-1 rhs with the dropped rows held at 0 (serial sweeps; nE is small on this path)
-    if (tid == 0) {
-      for (int k = 0; k < nE; ++k) {
-        double v = drop[k] != 0.0 ? 0.0 : lam[k];
-        for (int j = 0; j < k; ++j) v -= Sm[(size_t)k * nE + j] * lam[j];
-        lam[k] = drop[k] != 0.0 ? 0.0 : v / Sm[(size_t)k * nE + k];
-      }
-      for (int k = nE - 1; k >= 0; --k) {
-        double v = lam[k];
-        for (int j = k + 1; j < nE; ++j) v -= Sm[(size_t)j * nE + k] * lam[j];
-        lam[k] = drop[k] != 0.0 ? 0.0 : v / Sm[(size_t)k * nE + k];
-      }
-    }
-    __syncthreads();
-    // forward part of U: -L^-1 g - W lam
-    for (int i = tid; i < nU; i += nth) {
-      double v = u[i];
-      for (int rr = 0; rr < nE; ++rr) v -= W[(size_t)i * (nE + 1) + rr] * lam[rr];
-      u[i] = v;
-    }
-    __syncthreads();
-  }
-  for (int k = nU - 1; k >= 0; --k) {
-    if (tid == 0) u[k] /= H[(size_t)k * ldo + k];
-    __syncthreads();
-    for (int i = tid; i < k; i += nth) u[i] -= H[(size_t)k * ldo + i] * u[k];
-    __syncthreads();
-  }
-  if (nE) {  // consistency: E U = f to 1e-8 of the data scale, else the rows are inconsistent (HPIPM's INCONS_EQ)
-    if (tid == 0) {
-      double worst = 0.0;
-      for (int rr = 0; rr < nE; ++rr) {
-        double v = -fe[rr], sc = fabs(fe[rr]);
-        for (int i = 0; i < nU; ++i) {
-          v += E[(size_t)rr * ldo + i] * u[i];
-          sc = fmax(sc, fabs(E[(size_t)rr * ldo + i] * u[i]));
-        }
-        worst = fmax(worst, fabs(v) / (1.0 + sc));
-      }
-      if (!(worst <= 1e-8) && s_flag == 0) s_flag = 2;
-    }
-    __syncthreads();
-  }
-  // rollout x_{k+1} = A_k x_k + B_k u_k + b_k (x_0 = x0, HpipmInterface.cpp:303-315)
-  for (int i = tid; i < nx; i += nth) x[i] = a.x0[(size_t)q * nx + i];
-  __syncthreads();
-  for (int k = 0; k < N; ++k) {
-    const double* A = rec + oA[k];
-    const double* Bm = rec + oB[k];
-    const double* bv = rec + ob[k];
-    const int c0 = s_cu[k], m = a.nu[k];
-    for (int i = tid; i < nx; i += nth) {
-      double s = bv[i];
-      for (int j = 0; j < nx; ++j) s += OCP_CM(A, nx, i, j) * x[k * nx + j];
-      for (int b = 0; b < m; ++b) s += OCP_CM(Bm, nx, i, b) * u[c0 + b];
-      x[(k + 1) * nx + i] = s;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    int st = s_flag == 1 ? CMPC_NAN_SOL : (s_flag == 2 ? CMPC_INCONS_EQ : CMPC_SUCCESS);
-    for (int i = 0; i < nU; ++i)
-      if (!isfinite(u[i])) st = CMPC_NAN_SOL;
-    for (int i = 0; i < (N + 1) * nx; ++i)
-      if (!isfinite(x[i])) st = CMPC_NAN_SOL;
-    a.status[q] = st;
-  }
-}
-
-int launch_ocp_solve(const OcpArgs& a, int B, hipStream_t stream) {
-  if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_ocp_solve, dim3(B), dim3(256), 0, stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// ------------------------------------------------------------------------------------------ Riccati recursion
-// Cost-to-go (Sm, sv) and affine policy u_k = K_k x_k + k_k of the equality-free OCP, backward from Sm_N = Q_N,
-// sv_N = q_N (testHpipmInterface.cpp:280-304; the quantities HpipmInterface::getRiccati* rebuild from HPIPM's
-// ric_P / ric_p / ric_Lr / ric_Ls / ric_k, HpipmInterface.cpp:330-455):
-//   P = S + B'Sm A,  Rt = R + B'Sm B = Lr Lr',  rr = r + B'(sv + Sm b)
-//   K = -Rt^-1 P,  k = -Rt^-1 rr,  Sm_k = Q + A'Sm A - P'Rt^-1 P,  sv_k = q + A'(sv + Sm b) - P'Rt^-1 rr
-// One 256-thread workgroup per problem, stage products thread-parallel, Rt factored in place (Cholesky; a
-// non-positive pivot -> NAN_SOL), one thread per right-hand-side column for the two triangular solves.
-__global__ __launch_bounds__(256) void k_ocp_riccati(RiccatiArgs a) {
-  const int q = blockIdx.x;
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int N = a.N, nx = a.nx;
-  constexpr int M = CMPC_RIC_MAX_DIM;
-  const double* rec = a.rec + (size_t)q * a.rec_size;
-  const size_t* oA = a.offs;
-  const size_t* oB = a.offs + (N + 1);
-  const size_t* ob = a.offs + 2 * (N + 1);
-  const size_t* oQ = a.offs + 3 * (N + 1);
-  const size_t* oS = a.offs + 4 * (N + 1);
-  const size_t* oR = a.offs + 5 * (N + 1);
-  const size_t* oq = a.offs + 6 * (N + 1);
-  const size_t* orr = a.offs + 7 * (N + 1);
-  double* Sm = a.Sm + (size_t)q * (N + 1) * nx * nx;
-  double* sv = a.sv + (size_t)q * (N + 1) * nx;
-  double* Kq = a.K + (size_t)q * a.nK;
-  double* kq = a.kff + (size_t)q * a.nU;
-  double* SmA = a.scratch + (size_t)q * ric_scratch(nx);  // nx x nx
-  double* SmB = SmA + (size_t)nx * nx;                     // nx x m   (ld nx)
-  double* w = SmB + (size_t)nx * M;                        // nx: sv + Sm b
-  double* P = w + nx;                                      // m x nx   (ld m)
-  double* Rt = P + (size_t)M * nx;                         // m x m    (ld m)
-  double* rr = Rt + (size_t)M * M;                         // m
-  double* X = rr + M;                                      // m x (nx + 1) (ld m)
-  __shared__ int s_koff[CMPC_OCP_MAX_N + 1], s_uoff[CMPC_OCP_MAX_N + 1];
-  __shared__ int s_bad;
-  if (tid == 0) {
-    int ok = 0, ou = 0;
-    for (int k = 0; k < N; ++k) {
-      s_koff[k] = ok;
-      s_uoff[k] = ou;
-      ok += a.nu[k] * nx;
-      ou += a.nu[k];
-    }
-    s_bad = 0;
-  }
-  for (int i = tid; i < nx * nx; i += nth) Sm[(size_t)N * nx * nx + i] = rec[oQ[N] + i];
-  for (int i = tid; i < nx; i += nth) sv[(size_t)N * nx + i] = rec[oq[N] + i];
-  __syncthreads();
-  for (int k = N - 1; k >= 0; --k) {
-    const int m = a.nu[k];
-    const double* A = rec + oA[k];
-    const double* Bm = rec + oB[k];
-    const double* b = rec + ob[k];
-    const double* Q = rec + oQ[k];
-    const double* S = rec + oS[k];
-    const double* R = rec + oR[k];
-    const double* qv = rec + oq[k];
-    const double* r = rec + orr[k];
-    const double* Sn = Sm + (size_t)(k + 1) * nx * nx;
-    const double* sn = sv + (size_t)(k + 1) * nx;
-    double* Sk = Sm + (size_t)k * nx * nx;
-    double* sk = sv + (size_t)k * nx;
-    // Sm A, Sm B, sv + Sm b
-    for (int e = tid; e < nx * nx; e += nth) {
-      const int i = e % nx, j = e / nx;
-      double acc = 0.0;
-      for (int t = 0; t < nx; ++t) acc += OCP_CM(Sn, nx, i, t) * OCP_CM(A, nx, t, j);
-      SmA[e] = acc;
-    }
-    for (int e = tid; e < nx * m; e += nth) {
-      const int i = e % nx, c = e / nx;
-      double acc = 0.0;
-      for (int t = 0; t < nx; ++t) acc += OCP_CM(Sn, nx, i, t) * OCP_CM(Bm, nx, t, c);
-      SmB[e] = acc;
-    }
-    for (int i = tid; i < nx; i += nth) {
-      double acc = sn[i];
-      for (int t = 0; t < nx; ++t) acc += OCP_CM(Sn, nx, i, t) * b[t];
-      w[i] = acc;
-    }
-    __syncthreads();
-    if (m > 0) {
-      for (int e = tid; e < m * nx; e += nth) {
-        const int c = e % m, j = e / m;
-        double acc = OCP_CM(S, m, c, j);
-        for (int t = 0; t < nx; ++t) acc += OCP_CM(Bm, nx, t, c) * OCP_CM(SmA, nx, t, j);
-        P[e] = acc;
-      }
-      for (int e = tid; e < m * m; e += nth) {
-        const int c = e % m, d = e / m;
-        double acc = OCP_CM(R, m, c, d);
-        for (int t = 0; t < nx; ++t) acc += OCP_CM(Bm, nx, t, c) * OCP_CM(SmB, nx, t, d);
-        Rt[e] = acc;
-      }
-      for (int c = tid; c < m; c += nth) {
-        double acc = r[c];
-        for (int t = 0; t < nx; ++t) acc += OCP_CM(Bm, nx, t, c) * w[t];
-        rr[c] = acc;
-      }
-      __syncthreads();
-      // Rt = Lr Lr' in place (lower)
-      for (int s2 = 0; s2 < m; ++s2) {
-        if (tid == 0) {
-          const double d = OCP_CM(Rt, m, s2, s2);
-          if (!(d > 0.0)) s_bad = 1;
-          OCP_CM(Rt, m, s2, s2) = d > 0.0 ? sqrt(d) : 1.0;
-        }
-        __syncthreads();
-        const double piv = OCP_CM(Rt, m, s2, s2);
-        for (int i = s2 + 1 + tid; i < m; i += nth) OCP_CM(Rt, m, i, s2) /= piv;
-        __syncthreads();
-        const int rem = m - s2 - 1;
-        for (int e = tid; e < rem * rem; e += nth) {
-          const int i = s2 + 1 + e % rem, j = s2 + 1 + e / rem;
-          if (j <= i) OCP_CM(Rt, m, i, j) -= OCP_CM(Rt, m, i, s2) * OCP_CM(Rt, m, j, s2);
-        }
-        __syncthreads();
-      }
-      // X = Rt^-1 [P | rr], one column per thread
-      for (int c = tid; c <= nx; c += nth) {
-        double* xc = X + (size_t)c * m;
-        for (int i = 0; i < m; ++i) xc[i] = c < nx ? OCP_CM(P, m, i, c) : rr[i];
-        for (int i = 0; i < m; ++i) {
-          double v = xc[i];
-          for (int t = 0; t < i; ++t) v -= OCP_CM(Rt, m, i, t) * xc[t];
-          xc[i] = v / OCP_CM(Rt, m, i, i);
-        }
-        for (int i = m - 1; i >= 0; --i) {
-          double v = xc[i];
-          for (int t = i + 1; t < m; ++t) v -= OCP_CM(Rt, m, t, i) * xc[t];
-          xc[i] = v / OCP_CM(Rt, m, i, i);
-        }
-      }
-      __syncthreads();
-      for (int e = tid; e < m * nx; e += nth) Kq[s_koff[k] + e] = -X[e];  // column-major m x nx, same as X
-      for (int c = tid; c < m; c += nth) kq[s_uoff[k] + c] = -X[(size_t)nx * m + c];
-    }
-    // Sm_k = Q + A'Sm A - P'X,  sv_k = q + A'w - P'x_rr
-    for (int e = tid; e < nx * nx; e += nth) {
-      const int i = e % nx, j = e / nx;
-      double acc = OCP_CM(Q, nx, i, j);
-      for (int t = 0; t < nx; ++t) acc += OCP_CM(A, nx, t, i) * OCP_CM(SmA, nx, t, j);
-      for (int c = 0; c < m; ++c) acc -= OCP_CM(P, m, c, i) * OCP_CM(X, m, c, j);
-      if (!isfinite(acc)) s_bad = 1;
-      Sk[e] = acc;
-    }
-    for (int i = tid; i < nx; i += nth) {
-      double acc = qv[i];
-      for (int t = 0; t < nx; ++t) acc += OCP_CM(A, nx, t, i) * w[t];
-      for (int c = 0; c < m; ++c) acc -= OCP_CM(P, m, c, i) * X[(size_t)nx * m + c];
-      if (!isfinite(acc)) s_bad = 1;
-      sk[i] = acc;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) a.status[q] = s_bad ? CMPC_NAN_SOL : CMPC_SUCCESS;
-}
-
-int launch_ocp_riccati(const RiccatiArgs& a, int B, hipStream_t stream) {
-  if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_ocp_riccati, dim3(B), dim3(256), 0, stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
 
 }  // namespace cmpc
 

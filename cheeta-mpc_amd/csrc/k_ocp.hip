@@ -1,0 +1,1160 @@
+// k_ocp.hip — stage-wise OCP-QP interior-point solver on the device: the HpipmInterface::solve path (reference
+// ocs2_sqp/hpipm_catkin/src/HpipmInterface.cpp:166-301) for problems of the ocs2_legged_robot size (nx = 24,
+// nu_k <= 24, N ~ 70; ocs2_legged_robot/config/mpc/task.info:33, :102), batched.
+//
+// Algorithm: HPIPM's OCP IPM as restated by oracle/ocp_ipm.c (x0 eliminated, HpipmInterface.cpp:177-208; the
+// constraint rows C x + D u + e = 0 as two-sided general constraints lg = ug = -e, :223-264; Mehrotra predictor-
+// corrector, one step length, tau = 0.995, the Settings of HpipmInterfaceSettings.h:44-57 honoured). Every Newton
+// system is solved stage-wise:
+//   - factorisation (backward over the stages, the only heavy serial chain): per stage the augmented symmetric matrix
+//       M = [B A rb; 0 0 1]' [P p; p' 0] [B A rb; 0 0 1] + [R~ S~' g_u; S~ Q~ g_x; g_u' g_x' 0] + Gc' Sigma Gc
+//     (rows/columns u | x | rhs) is formed in a register tile (16 x 16 threads, each an R x R cyclic tile) and the
+//     u block is eliminated by nu_k Gauss-Jordan sweep steps (one workgroup barrier each): the swept matrix holds
+//     -Minv = -(R~ + B'PB)^-1, -K = Minv M_ux, P_k = M_xx - M_xu Minv M_ux, -kff and p_k at once; P_k, p_k stay in
+//     LDS for the next stage, whose data was prefetched into registers during the sweep;
+//   - everything else is stage-parallel (residuals, right-hand sides, A + B K, the row directions) except two cheap
+//     serial nx x nx matrix-vector chains (forward dx_{k+1} = (A + BK) dx_k + bcl_k; backward
+//     p_k = (A + BK)' p_{k+1} + h_k for the corrector's right-hand side).
+// One workgroup of 256 threads per problem; problem-major workspace allocated once per cmpc_ocp handle.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "k_ocp.hpp"
+
+namespace cmpc {
+namespace {
+
+constexpr int NT = OCP_NT;
+constexpr double TAU_OCP = 0.995;  // fraction-to-boundary, as oracle/ocp_ipm.c
+
+// Lab instrumentation (-DCMPC_OCP_STAMPS, lab/ocp_stamps.sh only, never in libcmpc.so): thread 0 of problem 0
+// accumulates shader-clock cycles per phase (s_memtime) into a device array read by cmpc_ocp_debug_stamps.
+#ifdef CMPC_OCP_STAMPS
+__device__ unsigned long long ocp_stamp_acc[32];
+__device__ unsigned long long ocp_stamp_prev;
+#define OCP_STAMP(id)                                                         \
+  do {                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();           \
+      ocp_stamp_acc[id] += now_ - ocp_stamp_prev;                             \
+      ocp_stamp_prev = now_;                                                  \
+    }                                                                         \
+  } while (0)
+#else
+#define OCP_STAMP(id) \
+  do {                \
+  } while (0)
+#endif
+
+__device__ __forceinline__ double nmax(double a, double b) {
+  return (a != a || b != b) ? __builtin_nan("") : (a > b ? a : b);
+}
+struct OpMax {
+  __device__ double operator()(double a, double b) const { return nmax(a, b); }
+};
+struct OpMin {
+  __device__ double operator()(double a, double b) const { return a < b ? a : b; }
+};
+struct OpSum {
+  __device__ double operator()(double a, double b) const { return a + b; }
+};
+
+template <class Op>
+__device__ __forceinline__ double block_reduce(double v, double* red, Op op) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = red[0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; ++w) r = op(r, red[w]);
+  return r;
+}
+
+// Per-problem view: record blocks, constraint blocks and workspace arrays of problem q
+struct View {
+  const OcpLayout& L;
+  const double* rec;
+  const double* crec;
+  double* ws;
+  int NP;
+  __device__ __forceinline__ View(const OcpSolveArgs& a, int q)
+      : L(a.L),
+        rec(a.rec + (long long)q * a.L.rec_size),
+        crec(a.crec ? a.crec + (long long)q * a.L.crec_size : nullptr),
+        ws(a.ws + (long long)q * a.L.ws_stride),
+        NP(a.L.N + 1) {}
+  __device__ const double* A(int k) const { return rec + L.orec[8 * k + 0]; }
+  __device__ const double* Bm(int k) const { return rec + L.orec[8 * k + 1]; }
+  __device__ const double* b(int k) const { return rec + L.orec[8 * k + 2]; }
+  __device__ const double* Q(int k) const { return rec + L.orec[8 * k + 3]; }
+  __device__ const double* S(int k) const { return rec + L.orec[8 * k + 4]; }
+  __device__ const double* R(int k) const { return rec + L.orec[8 * k + 5]; }
+  __device__ const double* q(int k) const { return rec + L.orec[8 * k + 6]; }
+  __device__ const double* r(int k) const { return rec + L.orec[8 * k + 7]; }
+  __device__ const double* C(int k) const { return crec + L.ocon[4 * k + 0]; }
+  __device__ const double* D(int k) const { return crec + L.ocon[4 * k + 1]; }
+  __device__ const double* e(int k) const { return crec + L.ocon[4 * k + 2]; }
+  __device__ double* row(int i) const { return ws + L.o_rows + (long long)i * L.m; }
+  __device__ double* x() const { return ws + L.o_x; }
+  __device__ double* u() const { return ws + L.o_u; }
+  __device__ double* pi() const { return ws + L.o_pi; }
+  __device__ double* rgu() const { return ws + L.o_rgu; }
+  __device__ double* rgx() const { return ws + L.o_rgx; }
+  __device__ double* rb() const { return ws + L.o_rb; }
+  __device__ double* gu() const { return ws + L.o_gu; }
+  __device__ double* gx() const { return ws + L.o_gx; }
+  __device__ double* du() const { return ws + L.o_du; }
+  __device__ double* dx() const { return ws + L.o_dx; }
+  __device__ double* dpi() const { return ws + L.o_dpi; }
+  __device__ double* P(int k) const { return ws + L.o_P + (long long)k * L.nx * L.nx; }
+  __device__ double* pv() const { return ws + L.o_pv; }
+  __device__ double* K(int k) const { return ws + L.o_K + L.cK[k]; }
+  __device__ double* Mi(int k) const { return ws + L.o_Mi + L.cM[k]; }
+  __device__ double* kf() const { return ws + L.o_kf; }
+  __device__ double* Acl(int k) const { return ws + L.o_Acl + (long long)k * L.nx * L.nx; }
+  __device__ double* h() const { return ws + L.o_h; }
+  __device__ double* y() const { return ws + L.o_y; }
+  __device__ double* bcl() const { return ws + L.o_bcl; }
+};
+
+// LDS carve
+struct Lds {
+  double *Paug, *ABx, *Tx, *col, *vec, *red, *sgn;
+  int np1, nrm, nzp;
+};
+__device__ __forceinline__ Lds carve(double* smem, const OcpLayout& L, int NZP) {
+  Lds s;
+  s.np1 = L.nx + 1;
+  s.nrm = L.nx + 1 + L.ngmax;
+  s.nzp = NZP;
+  const int pa = (s.np1 * s.np1 + 1) & ~1;
+  s.Paug = smem;
+  s.ABx = s.Paug + pa;
+  s.Tx = s.ABx + s.nrm * NZP;
+  s.col = s.Tx + s.nrm * NZP;
+  s.vec = s.col + 2 * NZP;
+  s.red = s.vec + 128;
+  s.sgn = s.red + 64;
+  return s;
+}
+
+// c = C x + D u for every row (node 0's x is x0; the step's dx node 0 is 0)
+__device__ __forceinline__ void rows_value(const View& V, const double* xs, const double* us, double* out) {
+  const OcpLayout& L = V.L;
+  for (int j = threadIdx.x; j < L.m; j += NT) {
+    const int k = L.rstage[j], jl = j - L.cr[k], g = L.ng[k], mk = L.nu[k];
+    const double* C = V.C(k);
+    const double* D = V.D(k);
+    double s = 0.0;
+    for (int i = 0; i < L.nx; ++i) s = fma(C[(long long)i * g + jl], xs[(long long)k * L.nx + i], s);
+    for (int a = 0; a < mk; ++a) s = fma(D[(long long)a * g + jl], us[L.cu[k] + a], s);
+    out[j] = s;
+  }
+}
+
+// out_u += D' v, out_x += C' v (x part for nodes >= 1), per entry over the node's rows
+__device__ __forceinline__ double gct_u(const View& V, int k, int a, const double* v) {
+  const int g = V.L.ng[k];
+  const double* D = V.D(k);
+  const double* vk = v + V.L.cr[k];
+  double s = 0.0;
+  for (int j = 0; j < g; ++j) s = fma(D[(long long)a * g + j], vk[j], s);
+  return s;
+}
+__device__ __forceinline__ double gct_x(const View& V, int k, int i, const double* v) {
+  const int g = V.L.ng[k];
+  const double* C = V.C(k);
+  const double* vk = v + V.L.cr[k];
+  double s = 0.0;
+  for (int j = 0; j < g; ++j) s = fma(C[(long long)i * g + j], vk[j], s);
+  return s;
+}
+
+// Stationarity and dynamics residuals at (x, u, pi, l_l - l_u); returns the local max of |r_g| (rs) and |r_b| (re)
+__device__ __forceinline__ void residuals(const View& V, double& rs, double& re) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx, N = L.N;
+  const double* x = V.x();
+  const double* u = V.u();
+  const double* pi = V.pi();
+  double* wl = V.row(R_W);  // l_l - l_u, prepared by the caller
+  const int nU = L.nU, nXr = N * nx;
+  for (int it = threadIdx.x; it < nU + 2 * nXr; it += NT) {
+    if (it < nU) {
+      const int k = L.ustage[it], a = it - L.cu[k], mk = L.nu[k];
+      const double* R = V.R(k);
+      const double* S = V.S(k);
+      const double* Bm = V.Bm(k);
+      double s = V.r(k)[a];
+      for (int c = 0; c < mk; ++c) s = fma(R[(long long)c * mk + a], u[L.cu[k] + c], s);
+      for (int j = 0; j < nx; ++j) s = fma(S[(long long)j * mk + a], x[(long long)k * nx + j], s);
+      for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a * nx + t], pi[(long long)k * nx + t], s);
+      s -= gct_u(V, k, a, wl);
+      V.rgu()[it] = s;
+      rs = nmax(rs, fabs(s));
+    } else if (it < nU + nXr) {
+      const int e = it - nU, k = 1 + e / nx, i = e % nx, mk = L.nu[k];
+      const double* Q = V.Q(k);
+      const double* S = V.S(k);
+      double s = V.q(k)[i] - pi[(long long)(k - 1) * nx + i];
+      for (int j = 0; j < nx; ++j) s = fma(Q[(long long)j * nx + i], x[(long long)k * nx + j], s);
+      for (int a = 0; a < mk; ++a) s = fma(S[(long long)i * mk + a], u[L.cu[k] + a], s);
+      if (k < N) {
+        const double* A = V.A(k);
+        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], pi[(long long)k * nx + t], s);
+      }
+      s -= gct_x(V, k, i, wl);
+      V.rgx()[(long long)k * nx + i] = s;
+      rs = nmax(rs, fabs(s));
+    } else {
+      const int e = it - nU - nXr, k = e / nx, i = e % nx, mk = L.nu[k];
+      const double* A = V.A(k);
+      const double* Bm = V.Bm(k);
+      double s = V.b(k)[i] - x[(long long)(k + 1) * nx + i];
+      for (int j = 0; j < nx; ++j) s = fma(A[(long long)j * nx + i], x[(long long)k * nx + j], s);
+      for (int a = 0; a < mk; ++a) s = fma(Bm[(long long)a * nx + i], u[L.cu[k] + a], s);
+      V.rb()[(long long)k * nx + i] = s;
+      re = nmax(re, fabs(s));
+    }
+  }
+}
+
+// Step right-hand side g = r_g + Gc' w (node 0 has no state entries)
+__device__ __forceinline__ void step_rhs(const View& V) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx, nXr = L.N * nx;
+  const double* w = V.row(R_W);
+  for (int it = threadIdx.x; it < L.nU + nXr; it += NT) {
+    if (it < L.nU) {
+      const int k = L.ustage[it], a = it - L.cu[k];
+      V.gu()[it] = V.rgu()[it] + gct_u(V, k, a, w);
+    } else {
+      const int e = it - L.nU, k = 1 + e / nx, i = e % nx;
+      V.gx()[(long long)k * nx + i] = V.rgx()[(long long)k * nx + i] + gct_x(V, k, i, w);
+    }
+  }
+}
+
+// Stage k's augmented data rows (LDS image [nrk][NZP]): rows 0..nx-1 = [B A rb], row nx = [0 0 1],
+// rows nx+1.. = [D C 0] (their T rows are Sigma times them). Element loads are branch-light: one address selected,
+// one unconditional load (from a valid dummy address for the constant entries), then a select.
+struct StagePtrs {
+  const double *A, *B, *rb, *C, *D;
+  int mk, nz, g;
+};
+__device__ __forceinline__ StagePtrs stage_ptrs(const View& V, int k) {
+  StagePtrs P;
+  const int nx = V.L.nx;
+  P.mk = V.L.nu[k];
+  P.nz = P.mk + nx;
+  P.g = V.L.ng[k];
+  P.A = V.A(k);
+  P.B = V.Bm(k);
+  P.rb = V.rb() + (long long)k * nx;
+  P.C = P.g ? V.C(k) : P.rb;
+  P.D = P.g ? V.D(k) : P.rb;
+  return P;
+}
+__device__ __forceinline__ double stage_load(const StagePtrs& P, int nx, int r, int l) {
+  const double* p = P.rb;
+  double cst = 0.0;
+  bool use = false;
+  if (l <= P.nz) {
+    if (r < nx) {
+      use = true;
+      p = l < P.mk ? P.B + (long long)l * nx + r : (l < P.nz ? P.A + (long long)(l - P.mk) * nx + r : P.rb + r);
+    } else if (r == nx) {
+      cst = l == P.nz ? 1.0 : 0.0;
+    } else if (l < P.nz) {
+      const int j = r - nx - 1;
+      use = true;
+      p = l < P.mk ? P.D + (long long)l * P.g + j : P.C + (long long)(l - P.mk) * P.g + j;
+    }
+  }
+  const double v = *p;
+  return use ? v : cst;
+}
+
+// Stage k's Hessian / right-hand-side block [R~ S~' g_u; S~ Q~ g_x; g_u' g_x' 0] (reg on the R and Q diagonals)
+struct HPtrs {
+  const double *R, *S, *Q, *gu, *gx;
+  int mk, nz;
+};
+__device__ __forceinline__ HPtrs h_ptrs(const View& V, int k) {
+  HPtrs H;
+  H.mk = V.L.nu[k];
+  H.nz = H.mk + V.L.nx;
+  H.R = V.R(k);
+  H.S = V.S(k);
+  H.Q = V.Q(k);
+  H.gu = V.gu() + V.L.cu[k];
+  H.gx = V.gx() + (long long)k * V.L.nx;
+  return H;
+}
+__device__ __forceinline__ double h_load(const HPtrs& H, int nx, int i, int l, double reg) {
+  const double* p = H.gx;
+  bool use = false;
+  double add = 0.0;
+  if (i <= H.nz && l <= H.nz && !(i == H.nz && l == H.nz)) {
+    use = true;
+    if (l == H.nz) {
+      p = i < H.mk ? H.gu + i : H.gx + (i - H.mk);
+    } else if (i == H.nz) {
+      p = l < H.mk ? H.gu + l : H.gx + (l - H.mk);
+    } else if (i < H.mk && l < H.mk) {
+      p = H.R + (long long)l * H.mk + i;
+      add = i == l ? reg : 0.0;
+    } else if (i < H.mk) {
+      p = H.S + (long long)(l - H.mk) * H.mk + i;
+    } else if (l < H.mk) {
+      p = H.S + (long long)(i - H.mk) * H.mk + l;
+    } else {
+      p = H.Q + (long long)(l - H.mk) * nx + (i - H.mk);
+      add = i == l ? reg : 0.0;
+    }
+  }
+  const double v = *p;
+  return use ? v + add : 0.0;
+}
+
+template <int NZP>
+struct StagePrefetch {
+  static constexpr int EPT = NZP == 64 ? (64 * 64) / NT : 1;  // register prefetch for the 64 class only
+  double v[EPT];
+};
+
+// Backward factorisation of the barrier-weighted Newton matrix with the right-hand side (gu, gx, rb) of ws.
+// Writes P_k, pv_k (k = 0..N), K_k, Minv_k, kf_k (k = 0..N-1). Returns false on a NaN pivot.
+template <int NZP>
+__device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double reg) {
+  constexpr int R = NZP / 16;
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, ti = tid & 15, tj = tid >> 4;
+  const int N = L.N, nx = L.nx, np1 = nx + 1;
+  bool bad = false;
+  // P_N = Q_N + reg I + C_N' Sigma C_N, p_N = g_x,N
+  {
+    const int g = L.ng[N];
+    const double* Q = V.Q(N);
+    const double* sig = V.row(R_SIG) + L.cr[N];
+    for (int e = tid; e < np1 * np1; e += NT) {
+      const int r = e / np1, c = e % np1;
+      double val;
+      if (r < nx && c < nx) {
+        val = Q[(long long)c * nx + r] + (r == c ? reg : 0.0);
+        const double* C = g ? V.C(N) : nullptr;
+        for (int j = 0; j < g; ++j) val = fma(C[(long long)r * g + j] * sig[j], C[(long long)c * g + j], val);
+        V.P(N)[(long long)c * nx + r] = val;
+      } else if (r < nx) {
+        val = V.gx()[(long long)N * nx + r];
+        V.pv()[(long long)N * nx + r] = val;
+      } else if (c < nx) {
+        val = V.gx()[(long long)N * nx + c];
+      } else {
+        val = 0.0;
+      }
+      S.Paug[r * np1 + c] = val;
+    }
+    // stage N-1 data into LDS
+    const StagePtrs P = stage_ptrs(V, N - 1);
+    const int nrk = np1 + P.g;
+    const double* sg = V.row(R_SIG) + L.cr[N - 1];
+    for (int e = tid; e < nrk * NZP; e += NT) {
+      const int r = e / NZP, l = e % NZP;
+      const double v = stage_load(P, nx, r, l);
+      S.ABx[e] = v;
+      if (r > nx) S.Tx[e] = sg[r - nx - 1] * v;
+    }
+  }
+  double hm[R][R];
+  {
+    const HPtrs H = h_ptrs(V, N - 1);
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = 0; b < R; ++b) hm[a][b] = h_load(H, nx, ti + 16 * a, tj + 16 * b, reg);
+  }
+  __syncthreads();
+  OCP_STAMP(10);
+  for (int k = N - 1; k >= 0; --k) {
+    const int mk = L.nu[k], nz = mk + nx, nrk = np1 + L.ng[k];
+    // --- T = Paug [B A rb; 0 0 1] (rows 0..nx), eight accumulators per pass ---
+    for (int l = tid & 63; l < NZP; l += 64) {
+#pragma unroll 1
+      for (int half = 0; half < 2; ++half) {
+        const int rbase = (tid >> 6) + 32 * half;
+        if (rbase >= np1) break;
+        double acc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+        for (int s2 = 0; s2 < np1; ++s2) {
+          const double abv = S.ABx[s2 * NZP + l];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int r = rbase + 4 * t;
+            if (r < np1) acc[t] = fma(S.Paug[r * np1 + s2], abv, acc[t]);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int r = rbase + 4 * t;
+          if (r < np1) S.Tx[r * NZP + l] = acc[t];
+        }
+      }
+    }
+    __syncthreads();
+    OCP_STAMP(11);
+    // --- M = H + ABx' Tx over the stage's nrk rows (register tile) ---
+    double m[R][R];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = 0; b < R; ++b) m[a][b] = hm[a][b];
+    for (int r = 0; r < nrk; ++r) {
+      double ai[R], tl[R];
+#pragma unroll
+      for (int a = 0; a < R; ++a) ai[a] = S.ABx[r * NZP + ti + 16 * a];
+#pragma unroll
+      for (int b = 0; b < R; ++b) tl[b] = S.Tx[r * NZP + tj + 16 * b];
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < R; ++b) m[a][b] = fma(ai[a], tl[b], m[a][b]);
+    }
+    __syncthreads();  // ABx / Tx are free: the next stage's data goes there
+    OCP_STAMP(12);
+    // --- prefetch stage k-1 (its data rows, its H tile, its rows' Sigma) ---
+    StagePrefetch<NZP> pf;
+    const int kn = k - 1;
+    if (kn >= 0) {
+      const StagePtrs P = stage_ptrs(V, kn);
+      const int nrn = np1 + P.g;
+      if constexpr (NZP == 64) {
+#pragma unroll
+        for (int s2 = 0; s2 < StagePrefetch<NZP>::EPT; ++s2) {
+          const int e = tid + NT * s2;
+          pf.v[s2] = e < nrn * NZP ? stage_load(P, nx, e / NZP, e % NZP) : 0.0;
+        }
+      }
+      if (tid < P.g) S.sgn[tid] = V.row(R_SIG)[L.cr[kn] + tid];
+      const HPtrs H = h_ptrs(V, kn);
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < R; ++b) hm[a][b] = h_load(H, nx, ti + 16 * a, tj + 16 * b, reg);
+    }
+    OCP_STAMP(13);
+    // --- Gauss-Jordan sweep of the u block ---
+    if (mk > 0) {
+      if (tj == 0) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) S.col[ti + 16 * a] = m[a][0];
+      }
+      __syncthreads();
+      for (int j = 0; j < mk; ++j) {
+        const double* cb = S.col + (j & 1) * NZP;
+        const double d = cb[j];
+        bad = bad || (d != d);
+        const double dinv = d > 1e-200 ? 1.0 / d : 0.0;
+        double ci[R], cl[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          const int i = ti + 16 * a;
+          ci[a] = i == j ? -1.0 : cb[i];
+        }
+#pragma unroll
+        for (int b = 0; b < R; ++b) {
+          const int l = tj + 16 * b;
+          cl[b] = l == j ? -1.0 : cb[l];
+        }
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          const int i = ti + 16 * a;
+          const double f = -ci[a] * dinv;
+#pragma unroll
+          for (int b = 0; b < R; ++b) {
+            const int l = tj + 16 * b;
+            const double base = (i == j || l == j) ? 0.0 : m[a][b];
+            m[a][b] = fma(f, cl[b], base);
+          }
+        }
+        const int jn = j + 1;
+        if (jn < mk && tj == (jn & 15)) {
+          double* nb = S.col + (jn & 1) * NZP;
+#pragma unroll
+          for (int b = 0; b < R; ++b)
+            if (b == (jn >> 4)) {
+#pragma unroll
+              for (int a = 0; a < R; ++a) nb[ti + 16 * a] = m[a][b];
+            }
+        }
+        __syncthreads();
+      }
+    } else {
+      __syncthreads();  // S.sgn visible to the stores below
+    }
+    OCP_STAMP(14);
+    // --- next stage's data into LDS ---
+    if (kn >= 0) {
+      const int nrn = np1 + L.ng[kn];
+      if constexpr (NZP == 64) {
+#pragma unroll
+        for (int s2 = 0; s2 < StagePrefetch<NZP>::EPT; ++s2) {
+          const int e = tid + NT * s2;
+          if (e < nrn * NZP) {
+            S.ABx[e] = pf.v[s2];
+            if (e / NZP > nx) S.Tx[e] = S.sgn[e / NZP - nx - 1] * pf.v[s2];
+          }
+        }
+      } else {
+        const StagePtrs P = stage_ptrs(V, kn);
+        for (int e = tid; e < nrn * NZP; e += NT) {
+          const int r = e / NZP;
+          const double v = stage_load(P, nx, r, e % NZP);
+          S.ABx[e] = v;
+          if (r > nx) S.Tx[e] = S.sgn[r - nx - 1] * v;
+        }
+      }
+    }
+    OCP_STAMP(15);
+    // --- outputs ---
+    {
+      double* Kk = V.K(k);
+      double* Mk = V.Mi(k);
+      double* kf = V.kf() + L.cu[k];
+      double* Pk = V.P(k);
+      double* pk = V.pv() + (long long)k * nx;
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < R; ++b) {
+          const int i = ti + 16 * a, l = tj + 16 * b;
+          const double v = m[a][b];
+          if (i < mk) {
+            if (l < mk) Mk[(long long)l * mk + i] = -v;
+            else if (l < nz) Kk[(long long)(l - mk) * mk + i] = -v;
+            else if (l == nz) kf[i] = -v;
+          } else if (i < nz) {
+            if (l >= mk && l < nz) {
+              Pk[(long long)(l - mk) * nx + (i - mk)] = v;
+              S.Paug[(i - mk) * np1 + (l - mk)] = v;
+            } else if (l == nz) {
+              pk[i - mk] = v;
+              S.Paug[(i - mk) * np1 + nx] = v;
+            }
+          } else if (i == nz) {
+            if (l >= mk && l < nz) S.Paug[nx * np1 + (l - mk)] = v;
+            else if (l == nz) S.Paug[nx * np1 + nx] = 0.0;
+          }
+        }
+    }
+    __syncthreads();
+    OCP_STAMP(16);
+  }
+  return __syncthreads_or(bad) == 0;
+}
+
+// Closed-loop matrices Acl_k = A_k + B_k K_k (column-major, k = 1..N-1) and bcl_k = rb_k + B_k kf_k (k = 0..N-1)
+__device__ __forceinline__ void acl_pass(const View& V, bool with_acl) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx, N = L.N, nxx = nx * nx;
+  const int nA = with_acl ? (N - 1) * nxx : 0;
+  for (int it = threadIdx.x; it < nA + N * nx; it += NT) {
+    if (it < nA) {
+      const int k = 1 + it / nxx, e = it % nxx, c = e / nx, i = e % nx, mk = L.nu[k];
+      const double* Bm = V.Bm(k);
+      const double* Kk = V.K(k);
+      double s = V.A(k)[(long long)c * nx + i];
+      for (int a = 0; a < mk; ++a) s = fma(Bm[(long long)a * nx + i], Kk[(long long)c * mk + a], s);
+      V.Acl(k)[e] = s;
+    } else {
+      const int e = it - nA, k = e / nx, i = e % nx, mk = L.nu[k];
+      const double* Bm = V.Bm(k);
+      const double* kf = V.kf() + L.cu[k];
+      double s = V.rb()[(long long)k * nx + i];
+      for (int a = 0; a < mk; ++a) s = fma(Bm[(long long)a * nx + i], kf[a], s);
+      V.bcl()[(long long)k * nx + i] = s;
+    }
+  }
+}
+
+// Serial forward sweep: dx_1 = bcl_0, dx_{k+1} = Acl_k dx_k + bcl_k (dx node 0 stays 0)
+__device__ __forceinline__ void forward_pass(const View& V, const Lds& S) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
+  double* dx = V.dx();
+  double* v0 = S.vec;
+  double* v1 = S.vec + 64;
+  if (tid < nx) {
+    const double d = V.bcl()[tid];
+    v0[tid] = d;
+    dx[nx + tid] = d;
+  }
+  if (N > 1)
+    for (int e = tid; e < nxx; e += NT) S.ABx[e] = V.Acl(1)[e];
+  __syncthreads();
+  for (int k = 1; k < N; ++k) {
+    double* cur = (k & 1) ? S.ABx : S.Tx;
+    double* nxt = (k & 1) ? S.Tx : S.ABx;
+    const double* vin = (k & 1) ? v0 : v1;
+    double* vout = (k & 1) ? v1 : v0;
+    double pre[16];
+    const bool more = k + 1 < N;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int e = tid + NT * s2;
+      pre[s2] = (more && e < nxx) ? V.Acl(k + 1)[e] : 0.0;
+    }
+    if (tid < nx) {
+      double acc = V.bcl()[(long long)k * nx + tid];
+      for (int c = 0; c < nx; ++c) acc = fma(cur[c * nx + tid], vin[c], acc);
+      vout[tid] = acc;
+      dx[(long long)(k + 1) * nx + tid] = acc;
+    }
+    if (more) {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int e = tid + NT * s2;
+        if (e < nxx) nxt[e] = pre[s2];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// du_k = K_k dx_k + kf_k, dpi_k = P_{k+1} dx_{k+1} + p_{k+1}; then the row directions and the largest step
+// (returns the local min over rows of the fraction-to-boundary step, 1e300 if none)
+__device__ __forceinline__ double post_pass(const View& V) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx, N = L.N;
+  const double* dx = V.dx();
+  for (int it = threadIdx.x; it < L.nU + N * nx; it += NT) {
+    if (it < L.nU) {
+      const int k = L.ustage[it], a = it - L.cu[k], mk = L.nu[k];
+      double s = V.kf()[it];
+      if (k > 0) {
+        const double* Kk = V.K(k);
+        for (int c = 0; c < nx; ++c) s = fma(Kk[(long long)c * mk + a], dx[(long long)k * nx + c], s);
+      }
+      V.du()[it] = s;
+    } else {
+      const int e = it - L.nU, k = e / nx, i = e % nx;
+      const double* Pn = V.P(k + 1);
+      double s = V.pv()[(long long)(k + 1) * nx + i];
+      for (int t = 0; t < nx; ++t) s = fma(Pn[(long long)t * nx + i], dx[(long long)(k + 1) * nx + t], s);
+      V.dpi()[(long long)k * nx + i] = s;
+    }
+  }
+  __syncthreads();
+  double amax = 1e300;
+  if (L.m > 0) {
+    double* dc = V.row(R_DTL);
+    rows_value(V, dx, V.du(), dc);  // each thread reads back only its own rows below
+    const double *rl = V.row(R_RL), *ru = V.row(R_RU), *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL),
+                 *lu = V.row(R_LU), *rml = V.row(R_RML), *rmu = V.row(R_RMU);
+    double *dtl = V.row(R_DTL), *dtu = V.row(R_DTU), *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
+    for (int j = threadIdx.x; j < L.m; j += NT) {
+      const double c = dtl[j];
+      const double a1 = c + rl[j], a2 = ru[j] - c;
+      const double b1 = -(rml[j] + ll[j] * a1) / tl[j], b2 = -(rmu[j] + lu[j] * a2) / tu[j];
+      dtl[j] = a1;
+      dtu[j] = a2;
+      dll[j] = b1;
+      dlu[j] = b2;
+      if (a1 < 0.0) amax = fmin(amax, -tl[j] / a1);
+      if (a2 < 0.0) amax = fmin(amax, -tu[j] / a2);
+      if (b1 < 0.0) amax = fmin(amax, -ll[j] / b1);
+      if (b2 < 0.0) amax = fmin(amax, -lu[j] / b2);
+    }
+  }
+  return amax;
+}
+
+// Corrector's backward vector pass with the factorisation kept: y_k = P_{k+1} rb_k; h_k = g_x,k + K_k' g_u,k +
+// Acl_k' y_k; p_N = g_x,N, p_k = Acl_k' p_{k+1} + h_k (serial, k = N-1..1); kf_k = -Minv_k (g_u,k + B_k'(y_k + p_{k+1}))
+__device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
+  double* y = V.y();
+  double* h = V.h();
+  double* pv = V.pv();
+  for (int it = tid; it < N * nx; it += NT) {
+    const int k = it / nx, i = it % nx;
+    const double* Pn = V.P(k + 1);
+    double s = 0.0;
+    for (int t = 0; t < nx; ++t) s = fma(Pn[(long long)t * nx + i], V.rb()[(long long)k * nx + t], s);
+    y[it] = s;
+  }
+  for (int it = tid; it < nx; it += NT) pv[(long long)N * nx + it] = V.gx()[(long long)N * nx + it];
+  __syncthreads();
+  for (int it = tid; it < (N - 1) * nx; it += NT) {
+    const int k = 1 + it / nx, i = it % nx, mk = L.nu[k];
+    const double* Kk = V.K(k);
+    const double* Ac = V.Acl(k);
+    double s = V.gx()[(long long)k * nx + i];
+    for (int a = 0; a < mk; ++a) s = fma(Kk[(long long)i * mk + a], V.gu()[L.cu[k] + a], s);
+    for (int t = 0; t < nx; ++t) s = fma(Ac[(long long)i * nx + t], y[(long long)k * nx + t], s);
+    h[(long long)k * nx + i] = s;
+  }
+  // serial p recursion; Acl_k' staged transposed in LDS (double buffer in ABx / Tx)
+  double* v0 = S.vec;
+  double* v1 = S.vec + 64;
+  if (tid < nx) v0[tid] = V.gx()[(long long)N * nx + tid];
+  if (N > 1)
+    for (int e = tid; e < nxx; e += NT) {
+      const int c = e / nx, r = e % nx;  // Acl col-major: e = c nx + r holds Acl(r, c); LDS [r][c]
+      S.ABx[r * nx + c] = V.Acl(N - 1)[e];
+    }
+  __syncthreads();
+  for (int k = N - 1, t2 = 0; k >= 1; --k, ++t2) {
+    double* cur = (t2 & 1) ? S.Tx : S.ABx;
+    double* nxt = (t2 & 1) ? S.ABx : S.Tx;
+    const double* vin = (t2 & 1) ? v1 : v0;
+    double* vout = (t2 & 1) ? v0 : v1;
+    double pre[16];
+    const bool more = k - 1 >= 1;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int e = tid + NT * s2;
+      pre[s2] = (more && e < nxx) ? V.Acl(k - 1)[e] : 0.0;
+    }
+    if (tid < nx) {  // p_k[i] = sum_t Acl(t, i) p_{k+1}[t] + h_k[i]; cur[t * nx + i] = Acl(t, i)
+      double acc = h[(long long)k * nx + tid];
+      for (int t = 0; t < nx; ++t) acc = fma(cur[t * nx + tid], vin[t], acc);
+      vout[tid] = acc;
+      pv[(long long)k * nx + tid] = acc;
+    }
+    if (more) {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int e = tid + NT * s2;
+        if (e < nxx) {
+          const int c = e / nx, r = e % nx;
+          nxt[r * nx + c] = pre[s2];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // z_k = g_u + B'(y_k + p_{k+1}) into du (scratch), then kf = -Minv z
+  double* z = V.du();
+  for (int it = tid; it < L.nU; it += NT) {
+    const int k = L.ustage[it], a = it - L.cu[k];
+    const double* Bm = V.Bm(k);
+    double s = V.gu()[it];
+    for (int t = 0; t < nx; ++t)
+      s = fma(Bm[(long long)a * nx + t], y[(long long)k * nx + t] + pv[(long long)(k + 1) * nx + t], s);
+    z[it] = s;
+  }
+  __syncthreads();
+  for (int it = tid; it < L.nU; it += NT) {
+    const int k = L.ustage[it], a = it - L.cu[k], mk = L.nu[k];
+    const double* Mk = V.Mi(k);
+    double s = 0.0;
+    for (int b = 0; b < mk; ++b) s = fma(Mk[(long long)b * mk + a], z[L.cu[k] + b], s);
+    V.kf()[it] = -s;
+  }
+}
+
+// (l_l - l_u) into R_W
+__device__ __forceinline__ void load_lamdiff(const View& V) {
+  double* w = V.row(R_W);
+  const double *ll = V.row(R_LL), *lu = V.row(R_LU);
+  for (int j = threadIdx.x; j < V.L.m; j += NT) w[j] = ll[j] - lu[j];
+}
+
+template <int NZP>
+__device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds& S) {
+  const View V(a, q);
+  const OcpLayout& L = a.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, m = L.m;
+  double* x = V.x();
+  double* u = V.u();
+  // --- cold start ---
+  for (int i = tid; i < (N + 1) * nx; i += NT) {
+    x[i] = i < nx ? a.x0[(long long)q * nx + i] : 0.0;
+    V.dx()[i] = 0.0;
+    V.gx()[i] = 0.0;
+    V.rgx()[i] = 0.0;
+  }
+  for (int i = tid; i < L.nU; i += NT) u[i] = 0.0;
+  for (int i = tid; i < N * nx; i += NT) V.pi()[i] = 0.0;
+  __syncthreads();
+  {
+    double* c = V.row(R_C);
+    rows_value(V, x, u, c);
+    double *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL),
+           *lu = V.row(R_LU);
+    for (int j = tid; j < m; j += NT) {
+      const int k = L.rstage[j];
+      const double bnd = -V.e(k)[j - L.cr[k]];
+      lg[j] = bnd;
+      ug[j] = bnd;
+      tl[j] = fmax(c[j] - bnd, 1.0);
+      tu[j] = fmax(bnd - c[j], 1.0);
+      ll[j] = a.mu0 / tl[j];
+      lu[j] = a.mu0 / tu[j];
+    }
+  }
+  __syncthreads();
+  int status = 1, it = 0;
+  double rs = 0, re = 0, ri = 0, rc = 0;
+  OCP_STAMP(0);
+  for (it = 0;; ++it) {
+    // --- residuals ---
+    rows_value(V, x, u, V.row(R_C));
+    load_lamdiff(V);
+    __syncthreads();
+    double lrs = 0.0, lre = 0.0, lri = 0.0, lrc = 0.0, lmu = 0.0;
+    residuals(V, lrs, lre);
+    {
+      const double *c = V.row(R_C), *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU),
+                   *ll = V.row(R_LL), *lu = V.row(R_LU);
+      double *rl = V.row(R_RL), *ru = V.row(R_RU);
+      for (int j = tid; j < m; j += NT) {
+        const double a1 = c[j] - lg[j] - tl[j], a2 = ug[j] - c[j] - tu[j];
+        rl[j] = a1;
+        ru[j] = a2;
+        lri = nmax(lri, nmax(fabs(a1), fabs(a2)));
+        const double c1 = tl[j] * ll[j], c2 = tu[j] * lu[j];
+        lrc = nmax(lrc, nmax(c1, c2));
+        lmu += c1 + c2;
+      }
+    }
+    rs = block_reduce(lrs, S.red, OpMax());
+    re = block_reduce(lre, S.red, OpMax());
+    ri = block_reduce(lri, S.red, OpMax());
+    rc = block_reduce(lrc, S.red, OpMax());
+    const double musum = block_reduce(lmu, S.red, OpSum());
+    const double mu = m > 0 ? musum / (2.0 * m) : 0.0;
+    OCP_STAMP(1);
+    double* sr = (a.stats && it < a.stat_rows) ? a.stats + ((long long)q * a.stat_rows + it) * 10 : nullptr;
+    if (sr && tid == 0) {
+      for (int c = 0; c < 5; ++c) sr[c] = __builtin_nan("");
+      sr[5] = mu;
+      sr[6] = rs;
+      sr[7] = re;
+      sr[8] = ri;
+      sr[9] = rc;
+    }
+    if (!(isfinite(rs) && isfinite(re) && isfinite(ri) && isfinite(rc))) {
+      status = 3;
+      break;
+    }
+    if (rs <= a.tol_stat && re <= a.tol_eq && ri <= a.tol_ineq && rc <= a.tol_comp) {
+      status = 0;
+      break;
+    }
+    if (it >= a.iter_max) {
+      status = 1;
+      break;
+    }
+    if (m > 0 && !(mu > 1e-300)) {
+      status = 2;
+      break;
+    }
+    // --- predictor right-hand side and factorisation ---
+    {
+      const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
+                   *ru = V.row(R_RU);
+      double *sig = V.row(R_SIG), *rml = V.row(R_RML), *rmu = V.row(R_RMU), *w = V.row(R_W);
+      for (int j = tid; j < m; j += NT) {
+        sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
+        rml[j] = tl[j] * ll[j];
+        rmu[j] = tu[j] * lu[j];
+        w[j] = (rml[j] + ll[j] * rl[j]) / tl[j] - (rmu[j] + lu[j] * ru[j]) / tu[j];
+      }
+    }
+    __syncthreads();
+    step_rhs(V);
+    __syncthreads();
+    OCP_STAMP(2);
+    if (!factor_pass<NZP>(V, S, a.reg)) {
+      status = 3;
+      break;
+    }
+    OCP_STAMP(17);
+    acl_pass(V, true);
+    __syncthreads();
+    OCP_STAMP(3);
+    forward_pass(V, S);
+    OCP_STAMP(4);
+    double amax = block_reduce(post_pass(V), S.red, OpMin());
+    OCP_STAMP(5);
+    double alpha = fmin(1.0, amax);
+    if (m > 0) {
+      // mu_aff and the corrector
+      double lm = 0.0;
+      const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *dtl = V.row(R_DTL),
+                   *dtu = V.row(R_DTU), *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
+      for (int j = tid; j < m; j += NT)
+        lm += (tl[j] + alpha * dtl[j]) * (ll[j] + alpha * dll[j]) + (tu[j] + alpha * dtu[j]) * (lu[j] + alpha * dlu[j]);
+      const double maff = block_reduce(lm, S.red, OpSum()) / (2.0 * m);
+      const double ratio = maff / mu;
+      const double sigma = ratio * ratio * ratio;
+      if (sr && tid == 0) {
+        sr[0] = alpha;
+        sr[1] = maff;
+        sr[2] = sigma;
+      }
+      {
+        const double *rl = V.row(R_RL), *ru = V.row(R_RU);
+        double *rml = V.row(R_RML), *rmu = V.row(R_RMU), *w = V.row(R_W);
+        for (int j = tid; j < m; j += NT) {
+          rml[j] = tl[j] * ll[j] + dtl[j] * dll[j] - sigma * mu;
+          rmu[j] = tu[j] * lu[j] + dtu[j] * dlu[j] - sigma * mu;
+          w[j] = (rml[j] + ll[j] * rl[j]) / tl[j] - (rmu[j] + lu[j] * ru[j]) / tu[j];
+        }
+      }
+      __syncthreads();
+      step_rhs(V);
+      __syncthreads();
+      OCP_STAMP(6);
+      backward_vec_pass(V, S);
+      __syncthreads();
+      OCP_STAMP(7);
+      acl_pass(V, false);
+      __syncthreads();
+      forward_pass(V, S);
+      OCP_STAMP(8);
+      amax = block_reduce(post_pass(V), S.red, OpMin());
+      OCP_STAMP(5);
+      alpha = fmin(1.0, TAU_OCP * amax);
+    }
+    if (sr && tid == 0) sr[3] = sr[4] = alpha;
+    if (alpha < a.alpha_min) {
+      status = 2;
+      break;
+    }
+    // --- update ---
+    for (int i = tid + nx; i < (N + 1) * nx; i += NT) x[i] = fma(alpha, V.dx()[i], x[i]);
+    for (int i = tid; i < L.nU; i += NT) u[i] = fma(alpha, V.du()[i], u[i]);
+    for (int i = tid; i < N * nx; i += NT) V.pi()[i] = fma(alpha, V.dpi()[i], V.pi()[i]);
+    {
+      double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU);
+      const double *dtl = V.row(R_DTL), *dtu = V.row(R_DTU), *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
+      for (int j = tid; j < m; j += NT) {
+        tl[j] = fma(alpha, dtl[j], tl[j]);
+        tu[j] = fma(alpha, dtu[j], tu[j]);
+        ll[j] = fma(alpha, dll[j], ll[j]);
+        lu[j] = fma(alpha, dlu[j], lu[j]);
+      }
+    }
+    __syncthreads();
+    OCP_STAMP(9);
+  }
+  // --- outputs ---
+  bool fin = true;
+  for (int i = tid; i < (N + 1) * nx; i += NT) {
+    const double v = x[i];
+    fin = fin && isfinite(v);
+    a.x[(long long)q * (N + 1) * nx + i] = v;
+  }
+  for (int i = tid; i < L.nU; i += NT) {
+    const double v = u[i];
+    fin = fin && isfinite(v);
+    a.u[(long long)q * L.nU + i] = v;
+  }
+  const bool allfin = __syncthreads_and(fin) != 0;
+  if (tid == 0) {
+    if (!allfin) status = 3;
+    a.status[q] = status;
+    if (a.iters) a.iters[q] = it;
+    if (a.res) {
+      a.res[(long long)q * 4 + 0] = rs;
+      a.res[(long long)q * 4 + 1] = re;
+      a.res[(long long)q * 4 + 2] = ri;
+      a.res[(long long)q * 4 + 3] = rc;
+    }
+  }
+}
+
+template <int NZP>
+__global__ __launch_bounds__(NT) void k_ocp_ipm(OcpSolveArgs a) {
+  extern __shared__ double smem[];
+  const Lds S = carve(smem, a.L, NZP);
+  OCP_STAMP(31);
+  ipm_body<NZP>(a, blockIdx.x, S);
+}
+
+// Riccati quantities at the exit point (see k_ocp.hpp / cmpc.h cmpc_ocp_riccati)
+template <int NZP>
+__global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
+  extern __shared__ double smem[];
+  const OcpSolveArgs& a = r.S;
+  const OcpLayout& L = a.L;
+  const Lds S = carve(smem, L, NZP);
+  const int q = blockIdx.x, tid = threadIdx.x, nx = L.nx, N = L.N, m = L.m;
+  const View V(a, q);
+  if (a.status[q] == 3) {
+    if (tid == 0) r.rstatus[q] = 3;
+    return;
+  }
+  {
+    const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
+                 *ru = V.row(R_RU);
+    double *sig = V.row(R_SIG), *w = V.row(R_W);
+    for (int j = tid; j < m; j += NT) {
+      sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
+      w[j] = ll[j] * rl[j] / tl[j] - lu[j] * ru[j] / tu[j];
+    }
+  }
+  __syncthreads();
+  step_rhs(V);
+  __syncthreads();
+  const bool ok = factor_pass<NZP>(V, S, a.reg);
+  const long long oP = (long long)q * (N + 1) * nx * nx, op = (long long)q * (N + 1) * nx;
+  const long long oK = (long long)q * (L.nK > 0 ? L.nK : 1), ok2 = (long long)q * (L.nU > 0 ? L.nU : 1),
+                  oM = (long long)q * (L.nM > 0 ? L.nM : 1);
+  const double* x = V.x();
+  const double* u = V.u();
+  // stages k >= 1: K, Minv, k = u - K x + kf, P, p = pi_{k-1} - P x + pv
+  for (int it = tid; it < L.nK; it += NT) r.K[oK + it] = V.ws[L.o_K + it];
+  for (int it = tid; it < L.nM; it += NT) r.Minv[oM + it] = V.ws[L.o_Mi + it];
+  for (int it = tid; it < L.nU; it += NT) {
+    const int k = L.ustage[it], a2 = it - L.cu[k], mk = L.nu[k];
+    if (k == 0) continue;
+    const double* Kk = V.K(k);
+    double s = u[it] + V.kf()[it];
+    for (int c = 0; c < nx; ++c) s = fma(-Kk[(long long)c * mk + a2], x[(long long)k * nx + c], s);
+    r.k[ok2 + it] = s;
+  }
+  for (int it = tid; it < N * nx * nx; it += NT) r.P[oP + (long long)nx * nx + it] = V.ws[L.o_P + (long long)nx * nx + it];
+  for (int it = tid; it < N * nx; it += NT) {
+    const int k = 1 + it / nx, i = it % nx;
+    const double* Pk = V.P(k);
+    double s = V.pi()[(long long)(k - 1) * nx + i] + V.pv()[(long long)k * nx + i];
+    for (int j = 0; j < nx; ++j) s = fma(-Pk[(long long)j * nx + i], x[(long long)k * nx + j], s);
+    r.p[op + (long long)k * nx + i] = s;
+  }
+  __syncthreads();
+  // stage 0, the reference's reconstruction (HpipmInterface.cpp:330-455) from P_1, p_1, Minv_0 and the stage-0 record:
+  // PA = P_1 A_0, v = p_1 + P_1 b_0, Mux = S_0 + B_0'PA, gr = r_0 + B_0'v, K_0 = -Minv_0 Mux, k_0 = -Minv_0 gr,
+  // P_0 = Q_0 + A_0'PA + Mux'K_0, p_0 = q_0 + A_0'v + K_0'gr. LDS: PA [nx][nx] in ABx, Mux [m0][nx] in Tx, v, gr.
+  {
+    const int m0 = L.nu[0];
+    const double* P1 = r.P + oP + (long long)nx * nx;
+    const double* p1 = r.p + op + nx;
+    const double* A = V.A(0);
+    const double* Bm = V.Bm(0);
+    double* PA = S.ABx;
+    double* Mux = S.Tx;
+    double* v = S.vec;
+    double* gr = S.vec + 64;
+    for (int e = tid; e < nx * nx; e += NT) {
+      const int i = e / nx, j = e % nx;  // PA[i][j]
+      double s = 0.0;
+      for (int t = 0; t < nx; ++t) s = fma(P1[(long long)t * nx + i], A[(long long)j * nx + t], s);
+      PA[i * nx + j] = s;
+    }
+    for (int i = tid; i < nx; i += NT) {
+      double s = p1[i];
+      for (int t = 0; t < nx; ++t) s = fma(P1[(long long)t * nx + i], V.b(0)[t], s);
+      v[i] = s;
+    }
+    __syncthreads();
+    for (int e = tid; e < m0 * nx + m0; e += NT) {
+      if (e < m0 * nx) {
+        const int a2 = e / nx, j = e % nx;
+        double s = V.S(0)[(long long)j * m0 + a2];
+        for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a2 * nx + t], PA[t * nx + j], s);
+        Mux[a2 * nx + j] = s;
+      } else {
+        const int a2 = e - m0 * nx;
+        double s = V.r(0)[a2];
+        for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a2 * nx + t], v[t], s);
+        gr[a2] = s;
+      }
+    }
+    __syncthreads();
+    const double* Mi0 = V.Mi(0);
+    for (int e = tid; e < m0 * nx + m0; e += NT) {
+      if (e < m0 * nx) {
+        const int j = e / m0, a2 = e % m0;  // K_0 (a2, j) column-major
+        double s = 0.0;
+        for (int b = 0; b < m0; ++b) s = fma(-Mi0[(long long)b * m0 + a2], Mux[b * nx + j], s);
+        r.K[oK + (long long)j * m0 + a2] = s;
+      } else {
+        const int a2 = e - m0 * nx;
+        double s = 0.0;
+        for (int b = 0; b < m0; ++b) s = fma(-Mi0[(long long)b * m0 + a2], gr[b], s);
+        r.k[ok2 + a2] = s;
+      }
+    }
+    __syncthreads();  // K_0 (global, this workgroup's writes) read back below
+    const double* K0 = r.K + oK;
+    for (int e = tid; e < nx * nx + nx; e += NT) {
+      if (e < nx * nx) {
+        const int j = e / nx, i = e % nx;  // P_0 (i, j)
+        double s = V.Q(0)[(long long)j * nx + i];
+        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], PA[t * nx + j], s);
+        for (int a2 = 0; a2 < m0; ++a2) s = fma(Mux[a2 * nx + i], K0[(long long)j * m0 + a2], s);
+        r.P[oP + e] = s;
+      } else {
+        const int i = e - nx * nx;
+        double s = V.q(0)[i];
+        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], v[t], s);
+        for (int a2 = 0; a2 < m0; ++a2) s = fma(K0[(long long)i * m0 + a2], gr[a2], s);
+        r.p[op + i] = s;
+      }
+    }
+  }
+  if (tid == 0) r.rstatus[q] = ok ? 0 : 3;
+}
+
+}  // namespace
+
+#ifdef CMPC_OCP_STAMPS
+extern "C" int cmpc_ocp_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ocp_stamp_acc), sizeof(unsigned long long) * 32) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ocp_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
+
+size_t ocp_lds_bytes(const OcpLayout& L) {
+  const int np1 = L.nx + 1, nrm = L.nx + 1 + L.ngmax;
+  const size_t pa = (size_t)((np1 * np1 + 1) & ~1);
+  return sizeof(double) * (pa + 2 * (size_t)nrm * L.nzp + 2 * (size_t)L.nzp + 128 + 64 + 64);
+}
+
+int launch_ocp_ipm(const OcpSolveArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  const size_t lds = ocp_lds_bytes(a.L);
+  if (a.L.nzp == 64) {
+    if (hipFuncSetAttribute((const void*)k_ocp_ipm<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_ocp_ipm<64>, dim3(B), dim3(NT), lds, stream, a);
+  } else {
+    if (hipFuncSetAttribute((const void*)k_ocp_ipm<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_ocp_ipm<128>, dim3(B), dim3(NT), lds, stream, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_ocp_ric(const OcpRicArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  const size_t lds = ocp_lds_bytes(a.S.L);
+  if (a.S.L.nzp == 64) {
+    if (hipFuncSetAttribute((const void*)k_ocp_ric<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_ocp_ric<64>, dim3(B), dim3(NT), lds, stream, a);
+  } else {
+    if (hipFuncSetAttribute((const void*)k_ocp_ric<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_ocp_ric<128>, dim3(B), dim3(NT), lds, stream, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cmpc

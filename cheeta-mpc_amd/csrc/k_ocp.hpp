@@ -1,0 +1,73 @@
+// k_ocp.hpp — stage-wise OCP-QP interior-point solver (the HpipmInterface::solve path, reference
+// ocs2_sqp/hpipm_catkin/src/HpipmInterface.cpp:166-301): shared layout of the device kernels (k_ocp.hip) and the
+// host API (ocp_api.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace cmpc {
+
+constexpr int OCP_NT = 256;       // threads per problem (one workgroup)
+constexpr int OCP_ROWS = 17;      // per-row workspace arrays (see OcpLayout::row)
+constexpr int OCP_MAX_NX = 63;    // nx + 1 <= 64
+constexpr int OCP_MAX_NG = 64;    // general-constraint rows per node
+constexpr int OCP_MAX_N = 4096;   // stages
+
+// Per-row arrays, in order, each [m] per problem (m = sum_k ng_k)
+enum OcpRow { R_C = 0, R_LG, R_UG, R_TL, R_TU, R_LL, R_LU, R_RL, R_RU, R_RML, R_RMU, R_W, R_DTL, R_DTU, R_DLL, R_DLU, R_SIG };
+
+// Problem dimensions (shared by every problem of a batch, HPIPM's d_ocp_qp_dim) and the per-problem workspace map.
+// Device arrays are owned by the cmpc_ocp handle (allocated once in cmpc_ocp_create, as HpipmInterface::resize
+// reserves HPIPM's memory, HpipmInterface.cpp:92-129).
+struct OcpLayout {
+  int N, nx, nU, m, nzp, ngmax;
+  int nK, nM;                    // sum nu_k nx, sum nu_k^2
+  const int* nu;                 // [N+1], nu[N] = 0
+  const int* ng;                 // [N+1]
+  const int* cu;                 // [N+2] offsets of u_k in u
+  const int* cr;                 // [N+2] offsets of node k's rows
+  const int* cK;                 // [N+1] offsets of K_k (nu_k x nx, column-major)
+  const int* cM;                 // [N+1] offsets of Minv_k (nu_k x nu_k, column-major)
+  const long long* orec;         // [N+1][8] record offsets: A, B, b (k < N), Q, S, R, q, r (k <= N)
+  const long long* ocon;         // [N+1][4] constraint-record offsets: C, D, e, (pad)
+  const int* ustage;             // [nU] stage of each input entry
+  const int* rstage;             // [m] node of each row
+  long long rec_size, crec_size;
+  // workspace (doubles) per problem: stride and array offsets
+  long long ws_stride;
+  long long o_x, o_u, o_pi, o_rgu, o_rgx, o_rb, o_gu, o_gx, o_du, o_dx, o_dpi, o_rows, o_P, o_pv, o_K, o_Mi, o_kf,
+      o_Acl, o_h, o_y, o_bcl;
+};
+
+struct OcpSolveArgs {
+  OcpLayout L;
+  const double* x0;    // [B][nx]
+  const double* rec;   // [B][rec_size]
+  const double* crec;  // [B][crec_size] or nullptr (m == 0)
+  double* ws;          // [B][ws_stride]
+  double* x;           // [B][(N+1) nx]
+  double* u;           // [B][nU]
+  int* status;         // [B]
+  int* iters;          // [B]
+  double* res;         // [B][4]
+  double* stats;       // [B][stat_rows][10] or nullptr
+  int stat_rows;
+  int iter_max;
+  double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp, reg;
+};
+
+// Riccati quantities at the exit point of the last solve (cmpc_ocp_riccati): P [(N+1)][nx][nx], p [(N+1)][nx],
+// K [nK], k [nU], Minv [nM] per problem (column-major blocks), status [B].
+struct OcpRicArgs {
+  OcpSolveArgs S;
+  double *P, *p, *K, *k, *Minv;
+  int* rstatus;
+};
+
+// LDS bytes of the kernels for a layout
+size_t ocp_lds_bytes(const OcpLayout& L);
+int launch_ocp_ipm(const OcpSolveArgs& a, int B, hipStream_t stream);
+int launch_ocp_ric(const OcpRicArgs& a, int B, hipStream_t stream);
+
+}  // namespace cmpc

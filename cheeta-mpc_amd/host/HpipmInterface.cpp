@@ -1,4 +1,7 @@
-// HpipmInterface.cpp — ocs2::HpipmInterface mirror (reference HpipmInterface.cpp:86-554) on the MI355X engine.
+// HpipmInterface.cpp — ocs2::HpipmInterface mirror (reference HpipmInterface.cpp:86-554) on the MI355X engine: the
+// Impl owns a cmpc_ocp handle (device dimensions, settings and memory, created in initializeMemory / resize as the
+// reference reserves HPIPM's memory, :92-129) and solves through cmpc_ocp_solve_host (one copy in, the stage-wise
+// interior-point kernel, one copy back).
 //
 // Written against the API the real ocs2 / Eigen types and the stand-ins of ocs2_types.h share (rows(), cols(),
 // size(), data(), resize(), operator()), so an ocs2 build compiles this file inside its hpipm_catkin target against
@@ -72,19 +75,28 @@ struct Packed {
   std::vector<int> nxk;     // the problem's own state dimension per node (OcpSize::numStates)
   std::vector<int> nu, nc;
   std::vector<double> rec, crec;
-  std::vector<size_t> coff;  // start of node k's [C, D, e] in crec
 };
-
-double maxabs(double a, double b) { return std::fmax(a, std::fabs(b)); }
 
 }  // namespace
 
 class HpipmInterface::Impl {
  public:
-  Impl(OcpSize s, Settings st) : settings_(st) { initializeMemory(std::move(s)); }
-  void initializeMemory(OcpSize s) {
-    s.numStates[0] = 0;  // x0 eliminated (HpipmInterface.cpp:93-95)
+  Impl(OcpSize s, Settings st) : settings_(st) { initializeMemory(std::move(s), true); }
+  ~Impl() { release(); }
+
+  // HpipmInterface.cpp:92-129: x0 is eliminated (numStates[0] = 0); the device handle (dimensions, settings and all
+  // device memory, cmpc_ocp_create) is re-created only when the size changes (:97-100)
+  void initializeMemory(OcpSize s, bool force = false) {
+    s.numStates[0] = 0;
+    if (!force && s == size_) return;
     size_ = std::move(s);
+    release();
+    const int N = size_.numStages;
+    if (N <= 0) return;
+    int nx = 0;
+    for (int k = 1; k <= N; ++k) nx = std::max(nx, size_.numStates[(size_t)k]);
+    std::vector<int> nc(size_.numIneqConstraints.begin(), size_.numIneqConstraints.end());
+    create(N, nx, std::vector<int>(size_.numInputs.begin(), size_.numInputs.begin() + N), nc);
   }
 
   hpipm_status solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dyn,
@@ -102,11 +114,169 @@ class HpipmInterface::Impl {
     if (constraints != nullptr && (int)constraints->size() != N + 1)
       throw std::runtime_error("[HpipmInterface] Inconsistent size of constraints: " +
                                std::to_string(constraints->size()) + " with " + std::to_string(N + 1) + " nodes.");
-    Packed p;
+    Packed& p = last_;
+    pack(p, x0, dyn, cost, constraints);
+    // the handle must have the problem's dimensions: node 0's state (x0.size()) may exceed numStates[1..N], and rows
+    // passed for nodes the size has none for (or without rows where it has some) re-create it, as a resize would
+    std::vector<int> nc = p.nc;
+    if (!ocp_ || ocpN_ != N || ocpNx_ != p.nx || ocpNu_ != p.nu || ocpNc_ != nc) create(N, p.nx, p.nu, nc);
+    const int nx = p.nx;
+    int nU = 0;
+    for (int v : p.nu) nU += v;
+    xbuf_.assign((size_t)(N + 1) * nx, 0.0);
+    ubuf_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
+    std::vector<double> x0p((size_t)nx, 0.0);
+    for (int i = 0; i < p.nxk[0]; ++i) x0p[(size_t)i] = x0(i);
+    int status = -1, iters = 0;
+    const int r = cmpc_ocp_solve_host(ocp_, 1, x0p.data(), p.rec.data(), p.crec.empty() ? nullptr : p.crec.data(),
+                                      xbuf_.data(), ubuf_.data(), &status, &iters);
+    if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device solve failed: ") + cmpc_error_string(r));
+    // getStateSolution / getInputSolution (:303-328): x[0] = x0, each node in its own dimension; non-finite -> NAN_SOL
+    bool finite = true;
+    xs.assign((size_t)N + 1, vector_t());
+    for (int k = 0; k <= N; ++k) {
+      const int xk = p.nxk[(size_t)k];
+      xs[(size_t)k].resize(xk);
+      for (int i = 0; i < xk; ++i) {
+        xs[(size_t)k](i) = k == 0 ? x0(i) : xbuf_[(size_t)k * nx + i];
+        finite = finite && std::isfinite(xs[(size_t)k](i));
+      }
+    }
+    us.assign((size_t)N, vector_t());
+    int off = 0;
+    for (int k = 0; k < N; ++k) {
+      us[(size_t)k].resize(p.nu[(size_t)k]);
+      for (int i = 0; i < p.nu[(size_t)k]; ++i) {
+        us[(size_t)k](i) = ubuf_[(size_t)off + i];
+        finite = finite && std::isfinite(us[(size_t)k](i));
+      }
+      off += p.nu[(size_t)k];
+    }
+    if (verbose) printStatus(status, iters);
+    riccatiValid_ = false;
+    if (!finite) return hpipm_status::NAN_SOL;
+    return (hpipm_status)status;
+  }
+
+  // Riccati quantities of the last solve (cmpc_ocp_riccati: factorisation at the returned point), fetched once per
+  // solve; stage 0 rebuilt from (dynamics0, cost0) as the reference does (HpipmInterface.cpp:334-347, 376-389, 416-453)
+  void riccati(const VectorFunctionLinearApproximation& dyn0, const ScalarFunctionQuadraticApproximation& cost0) {
+    const Packed& p = last_;
+    const int N = p.N;
+    if (N == 0 || !ocp_) throw std::runtime_error("[HpipmInterface] no solved problem to take Riccati quantities from");
+    if ((int)dyn0.dfdx.rows() != p.nxk[1] || (int)dyn0.dfdx.cols() != p.nxk[0] || (int)dyn0.dfdu.cols() != p.nu[0] ||
+        (int)cost0.dfdxx.rows() != p.nxk[0])
+      throw std::runtime_error("[HpipmInterface] dynamics0 / cost0 do not match the last solved problem");
+    if (!riccatiValid_) {
+      const int nx = p.nx;
+      int nU = 0, nK = 0, nM = 0;
+      for (int v : p.nu) {
+        nU += v;
+        nK += v * nx;
+        nM += v * v;
+      }
+      Pm_.assign((size_t)(N + 1) * nx * nx, 0.0);
+      pv_.assign((size_t)(N + 1) * nx, 0.0);
+      K_.assign((size_t)(nK > 0 ? nK : 1), 0.0);
+      k_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
+      Mi_.assign((size_t)(nM > 0 ? nM : 1), 0.0);
+      int st = -1;
+      const int r = cmpc_ocp_riccati_host(ocp_, 1, Pm_.data(), pv_.data(), K_.data(), k_.data(), Mi_.data(), &st);
+      if (r != CMPC_OK)
+        throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
+      if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati factorisation: NaN pivot");
+      riccatiValid_ = true;
+    }
+    stage0(dyn0, cost0);
+  }
+
+  std::vector<ScalarFunctionQuadraticApproximation> costToGo(const VectorFunctionLinearApproximation& d0,
+                                                              const ScalarFunctionQuadraticApproximation& c0) {
+    riccati(d0, c0);
+    const int N = last_.N, nx = last_.nx;
+    std::vector<ScalarFunctionQuadraticApproximation> out((size_t)N + 1);
+    for (int k = 0; k <= N; ++k) {  // node k's own nxk x nxk block of the padded P_k
+      const int xk = last_.nxk[(size_t)k];
+      out[(size_t)k].dfdxx.resize(xk, xk);
+      out[(size_t)k].dfdx.resize(xk);
+      for (int j = 0; j < xk; ++j)
+        for (int i = 0; i < xk; ++i)
+          out[(size_t)k].dfdxx(i, j) = k == 0 ? S0_[(size_t)j * xk + i] : Pm_[(size_t)k * nx * nx + (size_t)j * nx + i];
+      for (int i = 0; i < xk; ++i) out[(size_t)k].dfdx(i) = k == 0 ? s0_[(size_t)i] : pv_[(size_t)k * nx + i];
+      out[(size_t)k].f = 0.0;
+    }
+    return out;
+  }
+  matrix_array_t feedback(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
+    riccati(d0, c0);
+    const int N = last_.N, nx = last_.nx;
+    matrix_array_t out((size_t)N);
+    size_t o = 0;
+    for (int k = 0; k < N; ++k) {
+      const int m = last_.nu[(size_t)k], xk = last_.nxk[(size_t)k];
+      out[(size_t)k].resize(m, xk);  // the first nxk columns of the padded m x nx gain (column-major)
+      if (k == 0) std::copy(K0_.begin(), K0_.end(), out[0].data());
+      else std::copy(K_.begin() + (long)o, K_.begin() + (long)(o + (size_t)m * xk), out[(size_t)k].data());
+      o += (size_t)m * nx;
+    }
+    return out;
+  }
+  vector_array_t feedforward(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
+    riccati(d0, c0);
+    const int N = last_.N;
+    vector_array_t out((size_t)N);
+    size_t o = 0;
+    for (int k = 0; k < N; ++k) {
+      const int m = last_.nu[(size_t)k];
+      out[(size_t)k].resize(m);
+      if (k == 0) std::copy(k0_.begin(), k0_.end(), out[0].data());
+      else std::copy(k_.begin() + (long)o, k_.begin() + (long)(o + (size_t)m), out[(size_t)k].data());
+      o += (size_t)m;
+    }
+    return out;
+  }
+
+ private:
+  void release() {
+    if (ocp_) cmpc_ocp_destroy(ocp_);
+    ocp_ = nullptr;
+  }
+  void create(int N, int nx, const std::vector<int>& nu, const std::vector<int>& nc) {
+    release();
+    cmpc_settings s;
+    cmpc_settings_default(&s);
+    s.hpipm_mode = (int)settings_.hpipmMode;
+    s.iter_max = settings_.iter_max;
+    s.alpha_min = settings_.alpha_min;
+    s.mu0 = settings_.mu0;
+    s.tol_stat = settings_.tol_stat;
+    s.tol_eq = settings_.tol_eq;
+    s.tol_ineq = settings_.tol_ineq;
+    s.tol_comp = settings_.tol_comp;
+    s.reg_prim = settings_.reg_prim;
+    s.warm_start = settings_.warm_start;
+    s.pred_corr = settings_.pred_corr;
+    s.ric_alg = settings_.ric_alg;
+    bool rows = false;
+    for (int v : nc) rows = rows || v > 0;
+    const int r = cmpc_ocp_create(N, nx, nu.data(), rows ? nc.data() : nullptr, &s, 1, &ocp_);
+    if (r != CMPC_OK) {
+      ocp_ = nullptr;
+      throw std::runtime_error(std::string("[HpipmInterface] cannot create the device solver: ") + cmpc_error_string(r));
+    }
+    ocpN_ = N;
+    ocpNx_ = nx;
+    ocpNu_ = nu;
+    ocpNc_ = nc;
+  }
+
+  // The problem in the engine's packed forms, nodes embedded in the padded state dimension (per-node nx, HPIPM's
+  // nx[k]: the padding rows and columns of A, B, b, Q, S, q and C are 0, so padding states stay 0 and never couple)
+  static void pack(Packed& p, const vector_t& x0, const std::vector<VectorFunctionLinearApproximation>& dyn,
+                   const std::vector<ScalarFunctionQuadraticApproximation>& cost,
+                   const std::vector<VectorFunctionLinearApproximation>* constraints) {
+    const int N = (int)dyn.size();
     p.N = N;
-    // per-node state dimensions (OcpSize::numStates, HPIPM's nx[k]): node k's state is embedded in the first
-    // nxk[k] components of a padded state of dimension nx = max_k nxk[k]; the padding rows and columns of A, B, b,
-    // Q, S, q and C are 0, so padding states stay 0 and never couple (the device path takes one nx per problem)
     p.nxk.assign((size_t)N + 1, 0);
     p.nxk[0] = (int)x0.size();
     p.nu.assign((size_t)N, 0);
@@ -130,8 +300,7 @@ class HpipmInterface::Impl {
     const int nx = p.nx;
     p.rec.assign(cmpc_ocp_record_size(N, nx, p.nu.data()), 0.0);
     size_t o = 0;
-    // column-major r x c block (src may be null) into an R x C slot, zero padded
-    auto put = [&](const double* src, int r, int c, int R, int Cc) {
+    auto put = [&](const double* src, int r, int c, int R, int Cc) {  // column-major r x c block into an R x C slot
       for (int j = 0; j < Cc; ++j)
         for (int i = 0; i < R; ++i) p.rec[o + (size_t)j * R + i] = (src && i < r && j < c) ? src[(size_t)j * r + i] : 0.0;
       o += (size_t)R * Cc;
@@ -143,402 +312,112 @@ class HpipmInterface::Impl {
       put(m ? d.dfdu.data() : nullptr, r, m, nx, m);
       put(d.f.data(), r, 1, nx, 1);
     }
-    const double reg = settings_.reg_prim;
-    for (int k = 0; k <= N; ++k) {
+    for (int k = 0; k <= N; ++k) {  // raw cost blocks: reg_prim enters the device factorisation only
       const auto& c = cost[(size_t)k];
       const int m = k < N ? p.nu[(size_t)k] : 0, xk = p.nxk[(size_t)k];
-      const size_t oq = o;
       put(c.dfdxx.data(), xk, xk, nx, nx);
-      if (k > 0)  // HPIPM's primal regularisation; node 0's state is eliminated
-        for (int i = 0; i < xk; ++i) p.rec[oq + (size_t)i * nx + i] += reg;
       put(m ? c.dfdux.data() : nullptr, m, xk, m, nx);
-      const size_t orr = o;
       put(m ? c.dfduu.data() : nullptr, m, m, m, m);
-      for (int i = 0; i < m; ++i) p.rec[orr + (size_t)i * m + i] += reg;
       put(c.dfdx.data(), xk, 1, nx, 1);
       put(m ? c.dfdu.data() : nullptr, m, 1, m, 1);
     }
-    int nU = 0;
-    for (int v : p.nu) nU += v;
-    // === Constraints === C dx + D du + e = 0 per node, handed to the device as they come (the reference maps them to
-    // HPIPM's lg = ug = -e, with the stage-0 rows bounded through x0, HpipmInterface.cpp:223-264); an empty node
-    // (f.size() == 0) has no rows
+    // === Constraints === C dx + D du + e = 0 per node, the reference's lg = ug = -e rows (HpipmInterface.cpp:223-264,
+    // stage 0 bounded through x0 on the device); an empty node (f.size() == 0) has none
     p.nc.assign((size_t)N + 1, 0);
-    p.coff.assign((size_t)N + 2, 0);
-    int nE = 0;
+    p.crec.clear();
     if (constraints != nullptr) {
       for (int k = 0; k <= N; ++k) {
         const auto& c = (*constraints)[(size_t)k];
         const int rows = (int)c.f.size();
         const int m = k < N ? p.nu[(size_t)k] : 0;
-        p.coff[(size_t)k] = p.crec.size();
         if (rows == 0) continue;
         const int xk = p.nxk[(size_t)k];
         if ((int)c.dfdx.rows() != rows || (int)c.dfdx.cols() != xk ||
             (m > 0 && ((int)c.dfdu.rows() != rows || (int)c.dfdu.cols() != m)))
           throw std::runtime_error("[HpipmInterface] constraint " + std::to_string(k) + " has inconsistent sizes");
         p.nc[(size_t)k] = rows;
-        nE += rows;
         p.crec.insert(p.crec.end(), c.dfdx.data(), c.dfdx.data() + (size_t)rows * xk);
         p.crec.insert(p.crec.end(), (size_t)rows * (nx - xk), 0.0);  // padding state columns
         if (m > 0) p.crec.insert(p.crec.end(), c.dfdu.data(), c.dfdu.data() + (size_t)rows * m);
         p.crec.insert(p.crec.end(), c.f.data(), c.f.data() + rows);
       }
-      p.coff[(size_t)N + 1] = p.crec.size();
     }
-    std::vector<double> x((size_t)(N + 1) * nx), u((size_t)(nU > 0 ? nU : 1));
-    std::vector<double> x0p((size_t)nx, 0.0);
-    for (int i = 0; i < p.nxk[0]; ++i) x0p[(size_t)i] = x0(i);
-    int status = -1;
-    deviceSolve(p, nE > 0, 1, x0p.data(), x.data(), u.data(), &status);
-    xs.assign((size_t)N + 1, vector_t());
-    for (int k = 0; k <= N; ++k) {
-      const int xk = p.nxk[(size_t)k];
-      xs[(size_t)k].resize(xk);
-      for (int i = 0; i < xk; ++i) xs[(size_t)k](i) = k == 0 ? x0(i) : x[(size_t)k * nx + i];
-    }
-    us.assign((size_t)N, vector_t());
-    int off = 0;
-    for (int k = 0; k < N; ++k) {
-      us[(size_t)k].resize(p.nu[(size_t)k]);
-      for (int i = 0; i < p.nu[(size_t)k]; ++i) us[(size_t)k](i) = u[(size_t)off + i];
-      off += p.nu[(size_t)k];
-    }
-    if (verbose) printStatus(p, nE > 0, x0p.data(), x, u, status);
-    last_ = std::move(p);
-    lastConstrained_ = nE > 0;
-    riccatiValid_ = false;
-    return (hpipm_status)status;
   }
 
-  // Device Riccati quantities of the last problem, computed once per solve on first use.
-  void riccati(const VectorFunctionLinearApproximation& dyn0, const ScalarFunctionQuadraticApproximation& cost0) {
-    const int N = last_.N;
-    if (N == 0) throw std::runtime_error("[HpipmInterface] no solved problem to take Riccati quantities from");
-    if ((int)dyn0.dfdx.rows() != last_.nxk[1] || (int)dyn0.dfdx.cols() != last_.nxk[0] ||
-        (int)dyn0.dfdu.cols() != last_.nu[0] || (int)cost0.dfdxx.rows() != last_.nxk[0])
-      throw std::runtime_error("[HpipmInterface] dynamics0 / cost0 do not match the last solved problem");
-    if (riccatiValid_) return;
-    const int nx = last_.nx;
-    int nU = 0;
-    for (int v : last_.nu) nU += v;
-    Sm_.assign((size_t)(N + 1) * nx * nx, 0.0);
-    sv_.assign((size_t)(N + 1) * nx, 0.0);
-    K_.assign((size_t)(nU > 0 ? nU : 1) * nx, 0.0);
-    k_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
-    if (lastConstrained_) {
-      constrainedRiccati();
-    } else {
-      int st = -1;
-      const int r = cmpc_ocp_riccati_batch_host(1, N, nx, last_.nu.data(), last_.rec.data(), Sm_.data(), sv_.data(),
-                                                K_.data(), k_.data(), &st);
-      if (r != CMPC_OK)
-        throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
-      if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati recursion: R + B'PB not positive definite");
-    }
-    riccatiValid_ = true;
-  }
-  std::vector<ScalarFunctionQuadraticApproximation> costToGo(const VectorFunctionLinearApproximation& d0,
-                                                              const ScalarFunctionQuadraticApproximation& c0) {
-    riccati(d0, c0);
-    const int N = last_.N, nx = last_.nx;
-    std::vector<ScalarFunctionQuadraticApproximation> out((size_t)N + 1);
-    for (int k = 0; k <= N; ++k) {  // node k's own nxk x nxk block of the padded S_k
-      const int xk = last_.nxk[(size_t)k];
-      out[(size_t)k].dfdxx.resize(xk, xk);
-      out[(size_t)k].dfdx.resize(xk);
-      for (int j = 0; j < xk; ++j)
-        for (int i = 0; i < xk; ++i) out[(size_t)k].dfdxx(i, j) = Sm_[(size_t)k * nx * nx + (size_t)j * nx + i];
-      for (int i = 0; i < xk; ++i) out[(size_t)k].dfdx(i) = sv_[(size_t)k * nx + i];
-      out[(size_t)k].f = 0.0;
-    }
-    return out;
-  }
-  matrix_array_t feedback(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
-    riccati(d0, c0);
-    const int N = last_.N, nx = last_.nx;
-    matrix_array_t out((size_t)N);
-    size_t o = 0;
-    for (int k = 0; k < N; ++k) {
-      const int m = last_.nu[(size_t)k], xk = last_.nxk[(size_t)k];
-      out[(size_t)k].resize(m, xk);  // the first nxk columns of the padded m x nx gain (column-major)
-      std::copy(K_.begin() + (long)o, K_.begin() + (long)(o + (size_t)m * xk), out[(size_t)k].data());
-      o += (size_t)m * nx;
-    }
-    return out;
-  }
-  vector_array_t feedforward(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
-    riccati(d0, c0);
-    const int N = last_.N;
-    vector_array_t out((size_t)N);
-    size_t o = 0;
-    for (int k = 0; k < N; ++k) {
-      const int m = last_.nu[(size_t)k];
-      out[(size_t)k].resize(m);
-      std::copy(k_.begin() + (long)o, k_.begin() + (long)(o + (size_t)m), out[(size_t)k].data());
-      o += (size_t)m;
-    }
-    return out;
-  }
-
- private:
-  // B problems of the packed form p sharing its records but with their own x0 [B][nx]
-  static void deviceSolve(const Packed& p, bool eq, int B, const double* x0, double* x, double* u, int* status) {
-    std::vector<double> rec, crec;
-    const double* rp = p.rec.data();
-    const double* cp = p.crec.data();
-    if (B > 1) {
-      for (int b = 0; b < B; ++b) rec.insert(rec.end(), p.rec.begin(), p.rec.end());
-      rp = rec.data();
-      if (eq) {
-        for (int b = 0; b < B; ++b) crec.insert(crec.end(), p.crec.begin(), p.crec.end());
-        cp = crec.data();
-      }
-    }
-    const int r = eq ? cmpc_ocp_solve_batch_eq_host(B, p.N, p.nx, p.nu.data(), p.nc.data(), x0, rp, cp, x, u, status)
-                     : cmpc_ocp_solve_batch_host(B, p.N, p.nx, p.nu.data(), x0, rp, x, u, status);
-    if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device solve failed: ") + cmpc_error_string(r));
-  }
-
-  // offsets of node k's blocks inside the OCP record (cmpc.h layout)
-  static void recOffsets(const Packed& p, std::vector<size_t>& dynOff, std::vector<size_t>& costOff) {
-    dynOff.assign((size_t)p.N + 1, 0);
-    costOff.assign((size_t)p.N + 2, 0);
-    size_t o = 0;
-    for (int k = 0; k < p.N; ++k) {
-      dynOff[(size_t)k] = o;
-      o += (size_t)p.nx * p.nx + (size_t)p.nx * p.nu[(size_t)k] + (size_t)p.nx;
-    }
-    dynOff[(size_t)p.N] = o;
-    for (int k = 0; k <= p.N; ++k) {
-      costOff[(size_t)k] = o;
-      const size_t m = k < p.N ? (size_t)p.nu[(size_t)k] : 0;
-      o += (size_t)p.nx * p.nx + m * p.nx + m * m + (size_t)p.nx + m;
-    }
-    costOff[(size_t)p.N + 1] = o;
-  }
-
-  // The tail problem of stages k..N-1 of the last problem (records and constraint rows copied; the state-only rows of
-  // its first node dropped: that state is given).
-  Packed tail(int k) const {
+  // Stage 0 as the reference rebuilds it (HpipmInterface.cpp:334-347, :376-389, :416-453; x0 is not an HPIPM variable):
+  // with Minv_0 = (Lr_0 Lr_0')^-1 of the device factorisation (HPIPM's ric_Lr(0)), P_1, p_1 of node 1,
+  //   K_0 = -Minv_0 (S_0 + B_0'P_1 A_0), k_0 = -Minv_0 (r_0 + B_0'(p_1 + P_1 b_0)),
+  //   S_0 = Q_0 + A_0'P_1 A_0 - (S_0 + B_0'P_1 A_0)'Minv_0 (..), s_0 = q_0 + A_0'(p_1 + P_1 b_0) - (..)'Minv_0 (r_0 + ..).
+  // LinearAlgebra::setTriangularMinimumEigenvalues (ocs2_core, not in the reference tree) is not applied: Lr_0 is used
+  // only through Minv_0, whose pivots the device factorisation already guarded.
+  void stage0(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
     const Packed& p = last_;
-    std::vector<size_t> dynOff, costOff;
-    recOffsets(p, dynOff, costOff);
-    Packed t;
-    t.N = p.N - k;
-    t.nx = p.nx;
-    t.nu.assign(p.nu.begin() + k, p.nu.end());
-    t.rec.assign(p.rec.begin() + (long)dynOff[(size_t)k], p.rec.begin() + (long)dynOff[(size_t)p.N]);
-    t.rec.insert(t.rec.end(), p.rec.begin() + (long)costOff[(size_t)k], p.rec.begin() + (long)costOff[(size_t)p.N + 1]);
-    t.nc.assign((size_t)t.N + 1, 0);
-    t.coff.assign((size_t)t.N + 2, 0);
-    for (int j = k; j <= p.N; ++j) {
-      const int rows = p.nc[(size_t)j];
-      t.coff[(size_t)(j - k)] = t.crec.size();
-      if (rows == 0) continue;
-      const int m = j < p.N ? p.nu[(size_t)j] : 0;
-      const double* C = p.crec.data() + p.coff[(size_t)j];
-      const double* D = C + (size_t)rows * p.nx;
-      const double* e = D + (size_t)rows * m;
-      std::vector<int> keep;
-      for (int i = 0; i < rows; ++i) {
-        bool hasInput = false;
-        for (int c = 0; c < m; ++c) hasInput = hasInput || D[(size_t)c * rows + i] != 0.0;
-        if (j > k || hasInput) keep.push_back(i);
+    const int nx = p.nx, x0n = p.nxk[0], x1n = p.nxk[1], m = p.nu[0];
+    const double* P1 = Pm_.data() + (size_t)nx * nx;  // padded, column-major
+    const double* p1 = pv_.data() + nx;
+    const double* Mi = Mi_.data();                   // m x m column-major
+    auto A = [&](int i, int j) { return d0.dfdx.data()[(size_t)j * x1n + i]; };
+    auto B = [&](int i, int a) { return d0.dfdu.data()[(size_t)a * x1n + i]; };
+    std::vector<double> PA((size_t)x1n * x0n), v((size_t)x1n), Mux((size_t)m * x0n), gr((size_t)m);
+    for (int i = 0; i < x1n; ++i) {
+      for (int j = 0; j < x0n; ++j) {
+        double s = 0.0;
+        for (int t = 0; t < x1n; ++t) s += P1[(size_t)t * nx + i] * A(t, j);
+        PA[(size_t)i * x0n + j] = s;
       }
-      const int kr = (int)keep.size();
-      if (kr == 0) continue;
-      t.nc[(size_t)(j - k)] = kr;
-      for (int c = 0; c < p.nx; ++c)
-        for (int i : keep) t.crec.push_back(C[(size_t)c * rows + i]);
-      for (int c = 0; c < m; ++c)
-        for (int i : keep) t.crec.push_back(D[(size_t)c * rows + i]);
-      for (int i : keep) t.crec.push_back(e[i]);
+      double s = p1[i];
+      for (int t = 0; t < x1n; ++t) s += P1[(size_t)t * nx + i] * d0.f.data()[t];
+      v[(size_t)i] = s;
     }
-    t.coff[(size_t)t.N + 1] = t.crec.size();
-    return t;
-  }
-
-  // Feedback, feedforward and cost-to-go of the equality-constrained problem from the affine solution maps of its
-  // tail problems: for stage k, solve the tail from x_k = 0 and x_k = e_i (one device batch of nx + 1 problems);
-  // u_k = K_k x_k + k_k, and V_k(x) = sum_j l_j(Phi_j x + phi_j, K_j x + k_j) over the tail's trajectories gives
-  // S_k = sum [Phi; K]' [Q S'; S R] [Phi; K] and s_k = sum [Phi; K]' ([Q S'; S R] [phi; kk] + [q; r]).
-  void constrainedRiccati() {
-    const Packed& p = last_;
-    const int N = p.N, nx = p.nx;
-    std::vector<size_t> dynOff, costOff;
-    recOffsets(p, dynOff, costOff);
-    size_t kOff = 0;
-    for (int k = 0; k <= N; ++k) {
-      const int Nt = N - k;
-      const int B = nx + 1;
-      std::vector<double> xt, ut;
-      int nUt = 0;
-      if (Nt > 0) {
-        const Packed t = tail(k);
-        for (int v : t.nu) nUt += v;
-        std::vector<double> x0((size_t)B * nx, 0.0);
-        for (int i = 0; i < nx; ++i) x0[(size_t)(i + 1) * nx + i] = 1.0;
-        xt.assign((size_t)B * (Nt + 1) * nx, 0.0);
-        ut.assign((size_t)B * (nUt > 0 ? nUt : 1), 0.0);
-        std::vector<int> st((size_t)B, -1);
-        bool eq = false;
-        for (int v : t.nc) eq = eq || v > 0;
-        deviceSolve(t, eq, B, x0.data(), xt.data(), ut.data(), st.data());
-        for (int b = 0; b < B; ++b)
-          if (st[(size_t)b] != CMPC_SUCCESS)
-            throw std::runtime_error("[HpipmInterface] constrained Riccati: tail problem of stage " + std::to_string(k) +
-                                     " has status " + cmpc_status_string(st[(size_t)b]));
+    for (int a = 0; a < m; ++a) {
+      for (int j = 0; j < x0n; ++j) {
+        double s = c0.dfdux.data()[(size_t)j * m + a];
+        for (int t = 0; t < x1n; ++t) s += B(t, a) * PA[(size_t)t * x0n + j];
+        Mux[(size_t)a * x0n + j] = s;
       }
-      const int ust = nUt > 0 ? nUt : 1;
-      // trajectory maps of the tail: node j (0..Nt) state Phi_j x + phi_j, stage j input Kj x + kj
-      auto xs = [&](int b, int j, int i) { return Nt > 0 ? xt[((size_t)b * (Nt + 1) + j) * nx + i] : (b == 0 ? 0.0 : (b - 1 == i ? 1.0 : 0.0)); };
-      std::vector<int> uoff((size_t)Nt + 1, 0);
-      for (int j = 0; j < Nt; ++j) uoff[(size_t)j + 1] = uoff[(size_t)j] + p.nu[(size_t)(k + j)];
-      auto us = [&](int b, int j, int i) { return ut[(size_t)b * ust + uoff[(size_t)j] + i]; };
-      if (k < N) {  // K_k (m x nx column-major) and k_k
-        const int m = p.nu[(size_t)k];
-        for (int c = 0; c < nx; ++c)
-          for (int i = 0; i < m; ++i) K_[kOff + (size_t)c * m + i] = us(c + 1, 0, i) - us(0, 0, i);
-        for (int i = 0; i < m; ++i) k_[(kOff / nx) + i] = us(0, 0, i);
-        kOff += (size_t)m * nx;
+      double s = c0.dfdu.data()[a];
+      for (int t = 0; t < x1n; ++t) s += B(t, a) * v[(size_t)t];
+      gr[(size_t)a] = s;
+    }
+    K0_.assign((size_t)m * x0n, 0.0);
+    k0_.assign((size_t)m, 0.0);
+    for (int a = 0; a < m; ++a) {
+      for (int j = 0; j < x0n; ++j) {
+        double s = 0.0;
+        for (int b = 0; b < m; ++b) s -= Mi[(size_t)b * m + a] * Mux[(size_t)b * x0n + j];
+        K0_[(size_t)j * m + a] = s;
       }
-      // cost-to-go of node k
-      double* S = Sm_.data() + (size_t)k * nx * nx;
-      double* s = sv_.data() + (size_t)k * nx;
-      for (int j = 0; j <= Nt; ++j) {
-        const int node = k + j;
-        const int m = node < N ? p.nu[(size_t)node] : 0;
-        const double* Q = p.rec.data() + costOff[(size_t)node];
-        const double* Sx = Q + (size_t)nx * nx;  // S: m x nx
-        const double* R = Sx + (size_t)m * nx;
-        const double* q = R + (size_t)m * m;
-        const double* r = q + nx;
-        const int nz = nx + m;
-        // columns of [Phi; K] (c = 0..nx-1) and [phi; kk]
-        std::vector<double> Z((size_t)nz * (nx + 1));
-        for (int c = 0; c <= nx; ++c)
-          for (int i = 0; i < nz; ++i) {
-            const int b = c < nx ? c + 1 : 0;
-            const double v = i < nx ? xs(b, j, i) : us(b, j, i - nx);
-            const double v0 = i < nx ? xs(0, j, i) : us(0, j, i - nx);
-            Z[(size_t)c * nz + i] = c < nx ? v - v0 : v0;
-          }
-        // W = [Q S'; S R] applied to each column
-        auto Wz = [&](const double* z, double* out) {
-          for (int i = 0; i < nx; ++i) {
-            double a = 0.0;
-            for (int c = 0; c < nx; ++c) a += Q[(size_t)c * nx + i] * z[c];
-            for (int c = 0; c < m; ++c) a += Sx[(size_t)i * m + c] * z[nx + c];  // S'(i, c) = S(c, i)
-            out[i] = a;
-          }
-          for (int i = 0; i < m; ++i) {
-            double a = 0.0;
-            for (int c = 0; c < nx; ++c) a += Sx[(size_t)c * m + i] * z[c];
-            for (int c = 0; c < m; ++c) a += R[(size_t)c * m + i] * z[nx + c];
-            out[nx + i] = a;
-          }
-        };
-        std::vector<double> wz((size_t)nz);
-        for (int c = 0; c <= nx; ++c) {
-          Wz(Z.data() + (size_t)c * nz, wz.data());
-          if (c < nx) {
-            for (int a = 0; a < nx; ++a) {
-              double acc = 0.0;
-              for (int i = 0; i < nz; ++i) acc += Z[(size_t)a * nz + i] * wz[(size_t)i];
-              S[(size_t)c * nx + a] += acc;
-            }
-          } else {
-            for (int i = 0; i < nx; ++i) wz[(size_t)i] += q[i];
-            for (int i = 0; i < m; ++i) wz[(size_t)nx + i] += r[i];
-            for (int a = 0; a < nx; ++a) {
-              double acc = 0.0;
-              for (int i = 0; i < nz; ++i) acc += Z[(size_t)a * nz + i] * wz[(size_t)i];
-              s[a] += acc;
-            }
-          }
-        }
+      double s = 0.0;
+      for (int b = 0; b < m; ++b) s -= Mi[(size_t)b * m + a] * gr[(size_t)b];
+      k0_[(size_t)a] = s;
+    }
+    S0_.assign((size_t)x0n * x0n, 0.0);
+    s0_.assign((size_t)x0n, 0.0);
+    for (int i = 0; i < x0n; ++i) {
+      for (int j = 0; j < x0n; ++j) {
+        double s = c0.dfdxx.data()[(size_t)j * x0n + i];
+        for (int t = 0; t < x1n; ++t) s += A(t, i) * PA[(size_t)t * x0n + j];
+        for (int a = 0; a < m; ++a) s += Mux[(size_t)a * x0n + i] * K0_[(size_t)j * m + a];
+        S0_[(size_t)j * x0n + i] = s;
       }
+      double s = c0.dfdx.data()[i];
+      for (int t = 0; t < x1n; ++t) s += A(t, i) * v[(size_t)t];
+      for (int a = 0; a < m; ++a) s += K0_[(size_t)i * m + a] * gr[(size_t)a];
+      s0_[(size_t)i] = s;
     }
   }
 
-  // The reference's verbose printout (HpipmInterface.cpp:457-503). The direct solve is iteration 0; its residuals
-  // are evaluated here from the trajectories: res_b = dynamics and equality rows, res_g = stationarity in u of the
-  // equality-free problem (adjoint sweep; with equality rows their multipliers are not returned, so NaN).
-  void printStatus(const Packed& p, bool eq, const double* x0, const std::vector<double>& x, const std::vector<double>& u,
-                   int status) const {
-    const int N = p.N, nx = p.nx;
-    std::vector<size_t> dynOff, costOff;
-    recOffsets(p, dynOff, costOff);
-    auto X = [&](int k, int i) { return k == 0 ? x0[i] : x[(size_t)k * nx + i]; };
-    std::vector<int> uoff((size_t)N + 1, 0);
-    for (int k = 0; k < N; ++k) uoff[(size_t)k + 1] = uoff[(size_t)k] + p.nu[(size_t)k];
-    double resB = 0.0, resG = 0.0;
-    for (int k = 0; k < N; ++k) {
-      const int m = p.nu[(size_t)k];
-      const double* A = p.rec.data() + dynOff[(size_t)k];
-      const double* Bm = A + (size_t)nx * nx;
-      const double* b = Bm + (size_t)nx * m;
-      for (int i = 0; i < nx; ++i) {
-        double v = b[i] - X(k + 1, i);
-        for (int c = 0; c < nx; ++c) v += A[(size_t)c * nx + i] * X(k, c);
-        for (int c = 0; c < m; ++c) v += Bm[(size_t)c * nx + i] * u[(size_t)uoff[(size_t)k] + c];
-        resB = maxabs(resB, v);
-      }
-    }
-    for (int k = 0; eq && k <= N; ++k) {
-      const int rows = p.nc[(size_t)k];
-      const int m = k < N ? p.nu[(size_t)k] : 0;
-      const double* C = p.crec.data() + p.coff[(size_t)k];
-      const double* D = C + (size_t)rows * nx;
-      const double* e = D + (size_t)rows * m;
-      for (int i = 0; i < rows; ++i) {
-        double v = e[i];
-        for (int c = 0; c < nx; ++c) v += C[(size_t)c * rows + i] * X(k, c);
-        for (int c = 0; c < m; ++c) v += D[(size_t)c * rows + i] * u[(size_t)uoff[(size_t)k] + c];
-        resB = maxabs(resB, v);
-      }
-    }
-    if (eq) {
-      resG = NAN;
-    } else {  // lambda_N = Q x + q; g_u,k = R u + S x + r + B' lambda_{k+1}; lambda_k = Q x + S' u + q + A' lambda_{k+1}
-      std::vector<double> lam((size_t)nx), ln((size_t)nx);
-      {
-        const double* Q = p.rec.data() + costOff[(size_t)N];
-        const double* q = Q + (size_t)nx * nx;
-        for (int i = 0; i < nx; ++i) {
-          double v = q[i];
-          for (int c = 0; c < nx; ++c) v += Q[(size_t)c * nx + i] * X(N, c);
-          lam[(size_t)i] = v;
-        }
-      }
-      for (int k = N - 1; k >= 0; --k) {
-        const int m = p.nu[(size_t)k];
-        const double* A = p.rec.data() + dynOff[(size_t)k];
-        const double* Bm = A + (size_t)nx * nx;
-        const double* Q = p.rec.data() + costOff[(size_t)k];
-        const double* Sx = Q + (size_t)nx * nx;
-        const double* R = Sx + (size_t)m * nx;
-        const double* q = R + (size_t)m * m;
-        const double* r = q + nx;
-        const double* uk = u.data() + uoff[(size_t)k];
-        for (int i = 0; i < m; ++i) {
-          double v = r[i];
-          for (int c = 0; c < m; ++c) v += R[(size_t)c * m + i] * uk[c];
-          for (int c = 0; c < nx; ++c) v += Sx[(size_t)c * m + i] * X(k, c);
-          for (int c = 0; c < nx; ++c) v += Bm[(size_t)i * nx + c] * lam[(size_t)c];
-          resG = maxabs(resG, v);
-        }
-        for (int i = 0; i < nx; ++i) {
-          double v = q[i];
-          for (int c = 0; c < nx; ++c) v += Q[(size_t)c * nx + i] * X(k, c) + A[(size_t)i * nx + c] * lam[(size_t)c];
-          for (int c = 0; c < m; ++c) v += Sx[(size_t)i * m + c] * uk[c];
-          ln[(size_t)i] = v;
-        }
-        lam.swap(ln);
-      }
-    }
-    std::fprintf(stderr, "\n=== HPIPM (MI355X engine, direct KKT solve) ===\n");
+  // The reference's verbose printout (HpipmInterface.cpp:457-503): status line, iteration count, the final max
+  // residuals (d_ocp_qp_ipm_get_max_res_*) and the per-iteration statistics table (d_ocp_qp_ipm_get_stat), from the
+  // device solver's records (cmpc_ocp_get_residuals_host / cmpc_ocp_get_stats_host; the table's columns are
+  // cmpc_enable_stats', the reference's last seven (lq fact, itref, lin res) are not produced)
+  void printStatus(int status, int iters) const {
+    double res[4] = {NAN, NAN, NAN, NAN};
+    const int rows = cmpc_ocp_stat_rows(ocp_);
+    std::vector<double> stats((size_t)(rows > 0 ? rows : 1) * CMPC_STAT_COLS, NAN);
+    cmpc_ocp_get_residuals_host(ocp_, 1, res);
+    if (rows > 0) cmpc_ocp_get_stats_host(ocp_, 1, stats.data());
+    std::fprintf(stderr, "\n=== HPIPM (MI355X engine) ===\n");
     std::fprintf(stderr, "HPIPM returned with flag %i. -> ", status);
     if (status == CMPC_SUCCESS) std::fprintf(stderr, "QP solved!\n");
     else if (status == CMPC_MAX_ITER) std::fprintf(stderr, "Solver failed! Maximum number of iterations reached\n");
@@ -546,19 +425,24 @@ class HpipmInterface::Impl {
     else if (status == CMPC_NAN_SOL) std::fprintf(stderr, "Solver failed! NaN in computations\n");
     else if (status == CMPC_INCONS_EQ) std::fprintf(stderr, "Solver failed! Unconsistent equality constraints\n");
     else std::fprintf(stderr, "Solver failed! Unknown return flag\n");
-    std::fprintf(stderr, "ipm iter = %d\n", 0);
-    std::fprintf(stderr, "ipm residuals max: res_g = %e, res_b = %e, res_d = %e, res_m = %e\n", resG, resB, 0.0, 0.0);
+    std::fprintf(stderr, "ipm iter = %d\n", iters);
+    std::fprintf(stderr, "ipm residuals max: res_g = %e, res_b = %e, res_d = %e, res_m = %e\n", res[0], res[1], res[2],
+                 res[3]);
     std::fprintf(stderr, "\nalpha_aff\tmu_aff\t\tsigma\t\talpha_prim\talpha_dual\tmu\t\tres_stat\tres_eq\t\tres_ineq\tres_comp\n");
-    std::fprintf(stderr, "%e\t%e\t%e\t%e\t%e\t%e\t%e\t%e\t%e\t%e\t\n", (double)NAN, (double)NAN, (double)NAN, 1.0, 1.0, 0.0,
-                 resG, resB, 0.0, 0.0);
+    for (int j = 0; j < iters + 1 && j < rows; ++j) {
+      for (int i = 0; i < CMPC_STAT_COLS; ++i) std::fprintf(stderr, "%e\t", stats[(size_t)j * CMPC_STAT_COLS + i]);
+      std::fprintf(stderr, "\n");
+    }
   }
 
   Settings settings_;
   OcpSize size_;
+  cmpc_ocp* ocp_ = nullptr;  // the device solver (HPIPM's dim / qp / sol / arg / ws memory)
+  int ocpN_ = 0, ocpNx_ = 0;
+  std::vector<int> ocpNu_, ocpNc_;
   Packed last_;
-  bool lastConstrained_ = false;
   bool riccatiValid_ = false;
-  std::vector<double> Sm_, sv_, K_, k_;
+  std::vector<double> xbuf_, ubuf_, Pm_, pv_, K_, k_, Mi_, K0_, k0_, S0_, s0_;
 };
 
 HpipmInterface::HpipmInterface(OcpSize s, const Settings& st) : pImpl_(new Impl(std::move(s), st)) {}

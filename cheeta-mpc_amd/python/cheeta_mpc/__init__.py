@@ -21,7 +21,7 @@ F64, F32 = 0, 1
 # one-wave kernel where the IPM runs as its own launch)
 PATH_FUSED64, PATH_FUSED128, PATH_DIRECT, PATH_RICCATI, PATH_IPM72 = 0, 1, 2, 3, 4
 STATUS = {0: "SUCCESS", 1: "MAX_ITER", 2: "MIN_STEP", 3: "NAN_SOL", 4: "INCONS_EQ", 5: "INVALID_CONTACT",
-          6: "TOO_LARGE"}
+          6: "TOO_LARGE", 7: "INFEASIBLE_STEP"}
 
 # CentoidMPCTest.cpp:19-33
 TEST_WEIGHTS = [1, 1, 100, 0.5, 0.5, 0, 2, 2, 8,
@@ -113,6 +113,18 @@ def lib():
     L.cmpc_gait_table_destroy.argtypes = [vp]
     L.cmpc_gait_contact_batch.argtypes = [vp, C.c_int, i, d, C.c_double, C.c_double, C.c_int, u8, vp]
     L.cmpc_ocp_riccati_batch_host.argtypes = [C.c_int, C.c_int, C.c_int, i, d, d, d, d, d, i]
+    L.cmpc_ocp_memsize.argtypes = [C.c_int, C.c_int, i, i, C.c_int]
+    L.cmpc_ocp_memsize.restype = C.c_size_t
+    L.cmpc_ocp_create.argtypes = [C.c_int, C.c_int, i, i, P(Settings), C.c_int, P(vp)]
+    L.cmpc_ocp_destroy.argtypes = [vp]
+    L.cmpc_ocp_set_settings.argtypes = [vp, P(Settings)]
+    L.cmpc_ocp_solve.argtypes = [vp, C.c_int, d, d, d, d, d, i, i, vp]
+    L.cmpc_ocp_solve_host.argtypes = [vp, C.c_int, d, d, d, d, d, i, i]
+    L.cmpc_ocp_riccati.argtypes = [vp, C.c_int, d, d, d, d, d, i, vp]
+    L.cmpc_ocp_riccati_host.argtypes = [vp, C.c_int, d, d, d, d, d, i]
+    L.cmpc_ocp_get_residuals.argtypes = [vp, C.c_int, d, vp]
+    L.cmpc_ocp_stat_rows.argtypes = [vp]
+    L.cmpc_ocp_get_stats.argtypes = [vp, C.c_int, d, vp]
     L.cmpc_ipc_export.argtypes = [vp, P(IpcHandle)]
     L.cmpc_ipc_open.argtypes = [P(IpcHandle), P(vp)]
     L.cmpc_ipc_close.argtypes = [vp]
@@ -161,6 +173,15 @@ def _chk(r, what):
 def _hchk(r, what):
     if r != 0:
         raise RuntimeError(f"{what} failed: hipError {r} {hip().hipGetErrorString(r).decode()}")
+
+
+def device_pci_id(dev):
+    """PCI identity "domain:bus:device.function" of HIP device dev (distinguishes physical GPUs across ranks)."""
+    H = hip()
+    H.hipDeviceGetPCIBusId.argtypes = [C.c_char_p, C.c_int, C.c_int]
+    buf = C.create_string_buffer(64)
+    _hchk(H.hipDeviceGetPCIBusId(buf, 64, int(dev)), "hipDeviceGetPCIBusId")
+    return buf.value.decode()
 
 
 def device_count():
@@ -467,6 +488,106 @@ def ocp_solve_eq(N, nx, nu, nc, x0, rec, crec):
     _chk(lib().cmpc_ocp_solve_batch_eq_host(B, N, nx, vp(nua), vp(nca), vp(x0), vp(rec), vp(crec), vp(x), vp(u),
                                             vp(st)), "cmpc_ocp_solve_batch_eq_host")
     return x, u[:, :nU], st
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class OcpSolver:
+    """cmpc_ocp handle (the HpipmInterface::solve path, cmpc.h): dimensions N, nx, nu [N], nc [N+1] (None: no rows),
+    settings and device memory for max_batch problems, allocated once."""
+
+    def __init__(self, N, nx, nu, nc=None, settings=None, max_batch=1):
+        self.N, self.nx = int(N), int(nx)
+        self.nu = np.ascontiguousarray(list(nu)[:N], dtype=np.int32)
+        self.nc = None if nc is None else np.ascontiguousarray(list(nc), dtype=np.int32)
+        self.nU = int(self.nu.sum())
+        self.m = 0 if self.nc is None else int(self.nc.sum())
+        self.nK = int(self.nu.sum()) * self.nx
+        self.nM = int((self.nu.astype(np.int64) ** 2).sum())
+        self.settings = settings or default_settings()
+        self.max_batch = int(max_batch)
+        self.h = C.c_void_p()
+        _chk(lib().cmpc_ocp_create(self.N, self.nx, _dp(self.nu), _dp(self.nc), C.byref(self.settings), self.max_batch,
+                                   C.byref(self.h)), "cmpc_ocp_create")
+        self.rec_size = int(lib().cmpc_ocp_record_size(self.N, self.nx, _dp(self.nu)))
+        self.crec_size = (int(lib().cmpc_ocp_constraint_record_size(self.N, self.nx, _dp(self.nu), _dp(self.nc)))
+                          if self.nc is not None else 0)
+        self.stat_rows = lib().cmpc_ocp_stat_rows(self.h)
+
+    def close(self):
+        if self.h:
+            lib().cmpc_ocp_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_settings(self, s):
+        self.settings = s
+        _chk(lib().cmpc_ocp_set_settings(self.h, C.byref(s)), "cmpc_ocp_set_settings")
+        self.stat_rows = lib().cmpc_ocp_stat_rows(self.h)
+
+    def solve(self, x0, rec, crec=None):
+        """Host path (cmpc_ocp_solve_host): x0 [B,nx], rec [B,rec_size], crec [B,crec_size]. Returns x [B,N+1,nx],
+        u [B,nU], status [B], iters [B]."""
+        x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)
+        B = x0.shape[0]
+        rec = np.ascontiguousarray(rec, np.float64).reshape(B, self.rec_size)
+        cr = None if self.m == 0 else np.ascontiguousarray(crec, np.float64).reshape(B, self.crec_size)
+        x = np.zeros((B, self.N + 1, self.nx))
+        u = np.zeros((B, max(self.nU, 1)))
+        st = np.zeros(B, np.int32)
+        it = np.zeros(B, np.int32)
+        _chk(lib().cmpc_ocp_solve_host(self.h, B, _dp(x0), _dp(rec), _dp(cr), _dp(x), _dp(u), _dp(st), _dp(it)),
+             "cmpc_ocp_solve_host")
+        return x, u[:, :self.nU], st, it
+
+    def solve_device(self, B, x0, rec, crec, x, u, status, iters, stream=None):
+        _chk(lib().cmpc_ocp_solve(self.h, B, x0.ptr, rec.ptr, crec.ptr if crec is not None else None, x.ptr, u.ptr,
+                                  status.ptr, iters.ptr if iters is not None else None, stream), "cmpc_ocp_solve")
+
+    def riccati(self, B):
+        """cmpc_ocp_riccati_host of the last solve: P [B,N+1,nx,nx], p [B,N+1,nx], K (B lists of nu_k x nx), k, Minv,
+        status [B]."""
+        N, nx = self.N, self.nx
+        P = np.zeros((B, (N + 1) * nx * nx))
+        p = np.zeros((B, (N + 1) * nx))
+        K = np.zeros((B, max(self.nK, 1)))
+        k = np.zeros((B, max(self.nU, 1)))
+        M = np.zeros((B, max(self.nM, 1)))
+        st = np.zeros(B, np.int32)
+        _chk(lib().cmpc_ocp_riccati_host(self.h, B, _dp(P), _dp(p), _dp(K), _dp(k), _dp(M), _dp(st)),
+             "cmpc_ocp_riccati_host")
+        Ks, ks, Ms = [], [], []
+        for b in range(B):
+            kb, kk, mb, o, ok, om = [], [], [], 0, 0, 0
+            for s in range(N):
+                m = int(self.nu[s])
+                kb.append(K[b, o:o + m * nx].reshape(nx, m).T.copy())
+                kk.append(k[b, ok:ok + m].copy())
+                mb.append(M[b, om:om + m * m].reshape(m, m).T.copy())
+                o += m * nx
+                ok += m
+                om += m * m
+            Ks.append(kb)
+            ks.append(kk)
+            Ms.append(mb)
+        return (P.reshape(B, N + 1, nx, nx).transpose(0, 1, 3, 2).copy(), p.reshape(B, N + 1, nx), Ks, ks, Ms, st)
+
+    def residuals(self, B):
+        d = DeviceArray((B, 4), np.float64)
+        _chk(lib().cmpc_ocp_get_residuals(self.h, B, d.ptr, None), "cmpc_ocp_get_residuals")
+        return d.host()
+
+    def stats(self, B):
+        d = DeviceArray((B, self.stat_rows, 10), np.float64)
+        _chk(lib().cmpc_ocp_get_stats(self.h, B, d.ptr, None), "cmpc_ocp_get_stats")
+        return d.host()
 
 
 def ocp_riccati(N, nx, nu, rec):

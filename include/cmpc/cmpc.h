@@ -5,8 +5,9 @@
  *   - CentroidalMPC::UpdateMPC            (reference CentroidalMPC.cpp:278-370 / CentroidalMPC.h:32)
  *       → cmpc_solve_batch (B = 1 is one UpdateMPC call)
  *   - HpipmInterface::Impl::solve          (reference ocs2_sqp/hpipm_catkin/src/HpipmInterface.cpp:166-301)
- *       → cmpc_ocp_solve_batch_host (condensed OCP-QP, x0 eliminated as :177-208) and, with equality
- *         constraints (:223-264), cmpc_ocp_solve_batch_eq_host
+ *       → cmpc_ocp_create (initializeMemory, :92-129) + cmpc_ocp_solve / cmpc_ocp_solve_host (stage-wise OCP
+ *         interior-point method on the device, x0 eliminated as :177-208, constraint rows as :223-264) and
+ *         cmpc_ocp_riccati (getRiccati*, :330-455)
  *   - hpipm_interface::Settings            (reference hpipm_catkin/include/hpipm_catkin/HpipmInterfaceSettings.h:44-57)
  *       → cmpc_settings
  *   - d_ocp_qp_ipm_get_status codes        (reference HpipmInterface.h:79-85, HpipmInterface.cpp:462-473)
@@ -64,7 +65,8 @@ enum cmpc_qp_status {
   CMPC_MAX_ITER = 1,         /* maximum number of iterations reached */
   CMPC_MIN_STEP = 2,         /* minimum step length reached */
   CMPC_NAN_SOL = 3,          /* NaN in computations / non-finite solution (HpipmInterface.cpp:290-295) */
-  CMPC_INCONS_EQ = 4,        /* inconsistent equality constraints (HpipmInterface path with constraints) */
+  CMPC_INCONS_EQ = 4,        /* inconsistent equality constraints (HPIPM's code; the interior-point solvers here end
+                                inconsistent rows at MAX_ITER / MIN_STEP as HPIPM's OCP IPM does) */
   CMPC_INVALID_CONTACT = 5,  /* a horizon step has no stance leg: reference throws "mpc table invalid"
                                 (CentroidalMPC.cpp:328-330) */
   CMPC_TOO_LARGE = 6,        /* condensed size exceeds what this build's kernels support */
@@ -89,8 +91,8 @@ enum cmpc_precision { CMPC_F64 = 0, CMPC_F32 = 1 };
  *   pred_corr   must be 1 (the only iteration the build restates); 0 is rejected.
  *   ric_alg     0 or 1: HPIPM's classical / square-root Riccati factorisation choice. Both give the same iterates in
  *               exact arithmetic; the build's dense factorisation serves both.
- *   tol_eq      stopping tolerance on equality residuals: the centroidal QP has none; the equality-constrained OCP
- *               path (cmpc_ocp_solve_batch_eq_host) solves its KKT system directly and reports the residual.
+ *   tol_eq      stopping tolerance on equality residuals: the centroidal QP has none; the OCP path (cmpc_ocp_solve)
+ *               applies it to the dynamics residual.
  *   warm_start  0 or 1: 1 makes cmpc_solve_batch_warm start from the given inputs.
  *   iter_max >= 0; alpha_min, mu0, tol_* > 0; reg_prim >= 0. */
 typedef struct cmpc_settings {
@@ -276,41 +278,83 @@ int cmpc_qp_solve_batch(cmpc_ctx* ctx, int B, const double* d_H, const double* d
 int cmpc_generate_batch(const cmpc_model* model, uint64_t seed, int64_t qp_offset, int B, int gait, double* d_x0,
                         double* d_xref, double* d_foot, uint8_t* d_contact, void* stream);
 
-/* Generic OCP-QP (HpipmInterface::solve semantics, HpipmInterface.cpp:166-301), batched, no inequality rows:
+/* ---- Generic OCP-QP: the HpipmInterface::solve path (reference HpipmInterface.cpp:86-554) ----
  *   min sum_k [1/2 x'Q_k x + u'S_k x + 1/2 u'R_k u + q_k'x + r_k'u] + 1/2 x_N'Q_N x_N + q_N'x_N
- *   s.t. x_{k+1} = A_k x_k + B_k u_k + b_k,  x_0 given.
- * Constant nx, per-stage nu_k (nu_N = 0). Matrices COLUMN-major (Eigen default, so ocs2 .data() passes through).
- * Per-QP packed record (offsets computed by cmpc_ocp_record_size):
- *   A_k (nx*nx), B_k (nx*nu_k), b_k (nx)                       k = 0..N-1
- *   Q_k (nx*nx), S_k (nu_k*nx), R_k (nu_k*nu_k), q_k (nx), r_k (nu_k)   k = 0..N (S,R,r empty at N)
- * Outputs x [(N+1)][nx] (x[0] = x0) and u [sum nu_k]. Solved by condensing + dense Cholesky on the device. */
+ *   s.t. x_{k+1} = A_k x_k + B_k u_k + b_k (k = 0..N-1), x_0 given (eliminated, HpipmInterface.cpp:177-208),
+ *        C_k x_k + D_k u_k + e_k = 0 (nc_k rows at node k = 0..N; the reference's lg = ug = -e rows, :223-264).
+ * Constant (padded) nx, per-stage nu_k (nu_N = 0). All blocks COLUMN-major (Eigen's default, so ocs2 .data() passes
+ * through). Per-problem OCP record (size cmpc_ocp_record_size):
+ *   A_k (nx*nx), B_k (nx*nu_k), b_k (nx)                                 k = 0..N-1
+ *   Q_k (nx*nx), S_k (nu_k*nx), R_k (nu_k*nu_k), q_k (nx), r_k (nu_k)    k = 0..N (S, R, r empty at N)
+ * Per-problem constraint record (size cmpc_ocp_constraint_record_size):
+ *   C_k (nc_k*nx), D_k (nc_k*nu_k), e_k (nc_k)                           k = 0..N
+ * Outputs x [(N+1)][nx] (x[0] = x0), u [sum nu_k]. */
 size_t cmpc_ocp_record_size(int N, int nx, const int* nu);
+size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* nc);
+
+/* Solver handle: HPIPM's dim / qp / sol / ipm_arg / ipm_ws memory (HpipmInterface.cpp:92-129), i.e. the problem
+ * dimensions (N, nx, nu[N], nc[N+1]; nc may be NULL = no rows), the settings and all device memory for up to
+ * max_batch problems, allocated once here; a solve allocates nothing and synchronises nothing.
+ * Sizes: nx <= 63, nu_k + nx + 1 <= 128, nc_k <= 64, nx + 1 + max nc_k <= 128, N <= 4096 (CMPC_ERR_ARG otherwise).
+ * Algorithm (csrc/k_ocp.hip; checker oracle/ocp_ipm.c): HPIPM's OCP interior-point method — the rows are two-sided
+ * general constraints lg = ug = -e with slacks and multipliers, Mehrotra predictor-corrector, one step length,
+ * tau = 0.995, cold start (z = 0, pi = 0, t = max(slack, 1), lam = mu0 / t), stopping on the absolute residuals
+ * |r_stat| <= tol_stat, |r_eq| <= tol_eq (dynamics), |r_ineq| <= tol_ineq (rows), max t lam <= tol_comp, iter_max /
+ * alpha_min honoured (an inconsistent set of rows ends at MAX_ITER or MIN_STEP, as HPIPM's IPM does); every Newton
+ * system solved stage-wise by a Riccati recursion on the barrier-weighted Hessian with reg_prim on the diagonal of
+ * the stage Hessians. Without rows the first Newton step is the solution (iters = 1). warm_start is ignored (cold
+ * start: the reference's default, HpipmInterfaceSettings.h:54). */
+typedef struct cmpc_ocp cmpc_ocp;
+size_t cmpc_ocp_memsize(int N, int nx, const int* nu, const int* nc, int max_batch); /* device bytes */
+int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_settings* settings, int max_batch,
+                    cmpc_ocp** out);
+int cmpc_ocp_destroy(cmpc_ocp* ocp);
+int cmpc_ocp_set_settings(cmpc_ocp* ocp, const cmpc_settings* settings);
+/* Device pointers, asynchronous on stream: d_x0 [B][nx], d_rec [B][record], d_crec [B][constraint record] (NULL when
+ * the handle has no rows), d_x [B][(N+1)][nx], d_u [B][sum nu], d_status [B] (HPIPM codes 0..3), d_iters [B] (may be
+ * NULL). The records must stay valid until cmpc_ocp_riccati of this solve has run, if it is called. */
+int cmpc_ocp_solve(cmpc_ocp* ocp, int B, const double* d_x0, const double* d_rec, const double* d_crec, double* d_x,
+                   double* d_u, int* d_status, int* d_iters, void* stream);
+/* Host pointers: one copy in (records into the handle's device buffers), the solve, one copy back; synchronous. */
+int cmpc_ocp_solve_host(cmpc_ocp* ocp, int B, const double* x0, const double* rec, const double* crec, double* x,
+                        double* u, int* status, int* iters);
+/* Riccati quantities of the last solve's B problems (HpipmInterface::getRiccatiCostToGo / Feedback / Feedforward,
+ * HpipmInterface.cpp:330-455), from a barrier-weighted factorisation at the point the solve returned (HPIPM keeps its
+ * last iteration's; equal without rows, where the solve is one Newton step):
+ *   K_k = -(R~ + B'PB)^-1 (S~ + B'PA), P_k the barrier-weighted Riccati matrix (rows of node k weighted by
+ *   Sigma = lam_l / t_l + lam_u / t_u), k_k = u_k - K_k x_k + (Newton feedforward at the returned point, ~0), and
+ *   p_k = pi_{k-1} - P_k x_k + (Newton cost-to-go gradient at the returned point), k >= 1: the absolute-form
+ *   quantities of the Newton iterate, formed without the Sigma-sized cancellations of the absolute recursion;
+ *   stage 0 as the reference rebuilds it from stage-0 data (HpipmInterface.cpp:334-347, :416-453; here the record's
+ *   A_0, B_0, b_0, Q_0, S_0, R_0, q_0, r_0): K_0 = -Minv_0 (S_0 + B_0'P_1 A_0), k_0 = -Minv_0 (r_0 + B_0'(p_1 + P_1 b_0)),
+ *   P_0, p_0 likewise, Minv_0 = (R~_0 + B_0'P_1 B_0)^-1 with the node-0 rows' weight (HPIPM's Lr_0).
+ * Per problem, column-major: d_P [(N+1)][nx*nx], d_p [(N+1)][nx], d_K [sum nu_k*nx] (stage blocks nu_k x nx),
+ * d_k [sum nu_k], d_Minv [sum nu_k^2] (may be NULL); d_status [B]: 0, or 3 (NaN in the factorisation / no solve).
+ * Asynchronous on stream; overwrites the handle's factorisation workspace. */
+int cmpc_ocp_riccati(cmpc_ocp* ocp, int B, double* d_P, double* d_p, double* d_K, double* d_k, double* d_Minv,
+                     int* d_status, void* stream);
+int cmpc_ocp_riccati_host(cmpc_ocp* ocp, int B, double* P, double* p, double* K, double* k, double* Minv,
+                          int* status);
+/* Final residuals of the last solve, d_res [B][4] = (max |r_stat|, |r_eq|, |r_ineq|, max t lam) as
+ * d_ocp_qp_ipm_get_max_res_stat / _eq / _ineq / _comp (HpipmInterface.cpp:478-485); per-iteration statistics
+ * d_stats [B][rows][CMPC_STAT_COLS] (rows = iter_max + 1 of the settings at create / set_settings; the columns of
+ * cmpc_enable_stats, res_eq = the dynamics residual; rows past a problem's last iteration are NaN). Device pointers,
+ * asynchronous. cmpc_ocp_stat_rows returns rows. */
+int cmpc_ocp_get_residuals(cmpc_ocp* ocp, int B, double* d_res, void* stream);
+int cmpc_ocp_stat_rows(const cmpc_ocp* ocp);
+int cmpc_ocp_get_stats(cmpc_ocp* ocp, int B, double* d_stats, void* stream);
+/* Same, host pointers, synchronous (the HpipmInterface mirror's verbose printout). */
+int cmpc_ocp_get_residuals_host(cmpc_ocp* ocp, int B, double* res);
+int cmpc_ocp_get_stats_host(cmpc_ocp* ocp, int B, double* stats);
+
+/* One-shot host entry points (create, solve, destroy; kept from the 0.3 ABI): the equality-free problem
+ * (cmpc_ocp_solve_batch_host), with rows (cmpc_ocp_solve_batch_eq_host; nc == NULL is CMPC_ERR_ARG), and its Riccati
+ * quantities at x0 = 0 (cmpc_ocp_riccati_batch_host: Sm = P, sv = p, K, kff as cmpc_ocp_riccati, the recursion of
+ * testHpipmInterface.cpp:280-304 with reg_prim on the Hessian diagonals; status 0 or 3). */
 int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
                               double* u, int* status);
-
-/* The same OCP with equality constraints at the nodes (HpipmInterface::solve with constraints != nullptr; the
- * reference passes them to HPIPM as lg = ug = -e, HpipmInterface.cpp:223-264):
- *   C_k x_k + D_k u_k + e_k = 0   (nc_k rows at node k = 0..N; D_N empty; nc_k = 0 leaves a node free).
- * Per-problem constraint record (size cmpc_ocp_constraint_record_size), all blocks COLUMN-major:
- *   C_k (nc_k*nx), D_k (nc_k*nu_k), e_k (nc_k)          k = 0..N
- * The stage-0 rows are bounded through x0 exactly as the reference does (D_0 u_0 = -e_0 - C_0 x0, :236-244). Solved
- * on the device by condensing the cost and the constraint rows to U-space and a range-space KKT solve (Cholesky of H
- * and of the Schur complement E H^-1 E'). Redundant consistent rows are dropped; status CMPC_INCONS_EQ when the rows
- * cannot all be met (|E U - f| > 1e-8 of the data scale), CMPC_NAN_SOL when H is not positive definite or the
- * solution is non-finite. nc == NULL is CMPC_ERR_ARG (use cmpc_ocp_solve_batch_host).
- * Status parity: HPIPM's OCP IPM treats lg = ug rows as two-sided inequalities and, given inconsistent rows, stops
- * at MAX_ITER or MIN_STEP rather than INCONS_EQ; this direct solve detects the inconsistency and says so (parity of
- * that status unpinned: HPIPM is not available here). */
-size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* nc);
 int cmpc_ocp_solve_batch_eq_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0,
                                  const double* rec, const double* crec, double* x, double* u, int* status);
-
-/* Discrete Riccati recursion of the same equality-free OCP on the device: the cost-to-go and affine policy that
- * HpipmInterface::getRiccatiCostToGo / getRiccatiFeedback / getRiccatiFeedforward return (reference
- * HpipmInterface.cpp:330-455, from HPIPM's ric_P / ric_p / ric_Lr / ric_Ls / ric_k; recursion as
- * testHpipmInterface.cpp:280-304). Per problem, all blocks COLUMN-major:
- *   Sm [(N+1)][nx*nx], sv [(N+1)][nx], K [sum_k nu_k*nx] (stage blocks nu_k x nx), kff [sum nu_k].
- * status[b]: 0 SUCCESS, 3 NAN_SOL (R + B'Sm B not positive definite, or a non-finite result). */
 int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const double* rec, double* Sm, double* sv,
                                 double* K, double* kff, int* status);
 

@@ -148,6 +148,24 @@ int oracle_ocp_solve(int N, int nx, const int* nu, const double* x0, const doubl
 int oracle_ocp_riccati(int N, int nx, const int* nu, const double* rec, double* Sm, double* sv, double* K,
                        double* kff);
 
+/* ---- Stage-wise OCP IPM (ocp_ipm.c): HPIPM's d_ocp_qp_ipm as HpipmInterface::solve drives it ----
+ * nc [N+1] rows per node (NULL: none), crec as cmpc_ocp_constraint_record_size (C_k, D_k, e_k column-major; the rows
+ * C x + D u + e = 0 are the two-sided general constraints lg = ug = -e, HpipmInterface.cpp:223-264). x [(N+1)][nx]
+ * (node 0 = x0), u [sum nu_k]; res[4] = max |r_stat|, |r_eq|, |r_ineq|, max t lam at exit; stats [rows][10] as
+ * cmpc_enable_stats (res_eq now the dynamics residual). ric (optional): Riccati quantities of the last factorisation
+ * with the vector part in absolute form (see ocp_ipm.c), all column-major: P [(N+1)][nx][nx], p [(N+1)][nx],
+ * K [sum nu_k nx] (stage blocks nu_k x nx), k [sum nu_k], Minv [sum nu_k^2] ((R~ + B'PB)^-1, may be NULL). */
+typedef struct oracle_ocp_ric {
+  double *P, *p, *K, *k, *Minv;
+} oracle_ocp_ric;
+int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
+                   const double* crec, const cmpc_settings* s, double* x, double* u, int* iters, double* res,
+                   oracle_ocp_ric* ric, double* stats, int stats_rows);
+/* The cold start's first (predictor) Newton step, with the system's data for a dense cross-check. */
+int oracle_ocp_first_step(int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
+                          const double* crec, const cmpc_settings* s, double* du, double* dx, double* dpi,
+                          double* sig, double* rhs_u, double* rhs_x, double* rb);
+
 /* Contact table of one QP from a gait template (cmpc.h cmpc_gait semantics): GaitSchedule.cpp:78-127 tiling,
  * MotionPhaseDefinition.h:69-124 stance legs, mode at the start of each interval (left-closed). contact [N][4]. */
 void oracle_gait_contact(const cmpc_gait* g, const int* leg_map, double t_start, double t0, double dt, int N,

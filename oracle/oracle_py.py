@@ -18,7 +18,7 @@ TEST_WEIGHTS = [1, 1, 100, 0.5, 0.5, 0, 2, 2, 8,
                 0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1,
                 0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.1, 0.1, 0.1]
 STATUS = {0: "SUCCESS", 1: "MAX_ITER", 2: "MIN_STEP", 3: "NAN_SOL", 4: "INCONS_EQ", 5: "INVALID_CONTACT",
-          6: "TOO_LARGE"}
+          6: "TOO_LARGE", 7: "INFEASIBLE_STEP"}
 
 
 class Model(C.Structure):
@@ -99,6 +99,9 @@ def lib():
         L.oracle_ocp_condense.argtypes = [C.c_int, C.c_int, i, d, d, d, d]
         L.oracle_ocp_solve.argtypes = [C.c_int, C.c_int, i, d, d, d, d]
         L.oracle_ocp_riccati.argtypes = [C.c_int, C.c_int, i, d, d, d, d, d]
+        L.oracle_ocp_ipm.argtypes = [C.c_int, C.c_int, i, i, d, d, d, P(Settings), d, d, i, d, C.c_void_p, d,
+                                     C.c_int]
+        L.oracle_ocp_first_step.argtypes = [C.c_int, C.c_int, i, i, d, d, d, P(Settings), d, d, d, d, d, d, d]
         L.oracle_gait_contact.argtypes = [C.c_void_p, i, C.c_double, C.c_double, C.c_double, C.c_int,
                                           C.POINTER(C.c_uint8)]
         L.oracle_gait_contact.restype = None
@@ -487,6 +490,75 @@ def ocp_riccati(N, nx, nu, rec):
         o += nu[k] * nx
         ok += nu[k]
     return Sm, sv, Ks, ks, st
+
+
+class OcpRic(C.Structure):
+    _fields_ = [("P", C.POINTER(C.c_double)), ("p", C.POINTER(C.c_double)), ("K", C.POINTER(C.c_double)),
+                ("k", C.POINTER(C.c_double)), ("Minv", C.POINTER(C.c_double))]
+
+
+def ocp_ipm(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, ric=False, stats_rows=0):
+    """Stage-wise OCP IPM (oracle/ocp_ipm.c). Returns dict: x [(N+1),nx], u [nU], status, iters, res [4], and with
+    ric=True P [(N+1),nx,nx], p [(N+1),nx], K (list of nu_k x nx), k (list), Minv (list); stats [rows,10]."""
+    s = settings if settings is not None else default_settings()
+    nua = np.asarray(list(nu) + [0], dtype=np.int32)
+    nU = int(nua[:N].sum())
+    nca = None if nc is None else np.asarray(nc, dtype=np.int32)
+    crec_a = None if crec is None or nca is None or int(nca.sum()) == 0 else np.ascontiguousarray(crec, np.float64)
+    if crec_a is None:
+        nca = None
+    x = np.zeros((N + 1) * nx)
+    u = np.zeros(max(nU, 1))
+    it = C.c_int(0)
+    res = np.zeros(4)
+    st_rows = np.full((max(stats_rows, 1), 10), np.nan)
+    out = {}
+    r = None
+    if ric:
+        nK = max(int(sum(nu[k] * nx for k in range(N))), 1)
+        nM = max(int(sum(nu[k] * nu[k] for k in range(N))), 1)
+        P = np.zeros((N + 1) * nx * nx)
+        pv = np.zeros((N + 1) * nx)
+        K = np.zeros(nK)
+        kk = np.zeros(max(nU, 1))
+        Mi = np.zeros(nM)
+        r = OcpRic(_p(P), _p(pv), _p(K), _p(kk), _p(Mi))
+    status = lib().oracle_ocp_ipm(N, nx, _p(nua, C.c_int), _p(nca, C.c_int) if nca is not None else None,
+                                  _p(np.ascontiguousarray(x0, dtype=np.float64)), _p(np.ascontiguousarray(rec)),
+                                  _p(crec_a) if crec_a is not None else None, C.byref(s), _p(x), _p(u),
+                                  C.byref(it), _p(res), C.byref(r) if r is not None else None,
+                                  _p(st_rows) if stats_rows else None, stats_rows)
+    out.update(x=x.reshape(N + 1, nx), u=u[:nU], status=status, iters=it.value, res=res)
+    if stats_rows:
+        out["stats"] = st_rows
+    if ric:
+        Ks, ks, Ms, o, om, ok = [], [], [], 0, 0, 0
+        for k in range(N):
+            m = nu[k]
+            Ks.append(K[o:o + m * nx].reshape(nx, m).T.copy())
+            ks.append(kk[ok:ok + m].copy())
+            Ms.append(Mi[om:om + m * m].reshape(m, m).T.copy())
+            o += m * nx
+            om += m * m
+            ok += m
+        out.update(P=P.reshape(N + 1, nx, nx).transpose(0, 2, 1).copy(), p=pv.reshape(N + 1, nx), K=Ks, k=ks, Minv=Ms)
+    return out
+
+
+def ocp_first_step(N, nx, nu, x0, rec, nc=None, crec=None, settings=None):
+    s = settings if settings is not None else default_settings()
+    nua = np.asarray(list(nu) + [0], dtype=np.int32)
+    nU = int(nua[:N].sum())
+    nca = None if nc is None else np.asarray(nc, dtype=np.int32)
+    m = 0 if nca is None else int(nca.sum())
+    du, dx, dpi = np.zeros(max(nU, 1)), np.zeros((N + 1) * nx), np.zeros(N * nx)
+    sig, ru, rx, rb = np.zeros(max(m, 1)), np.zeros(max(nU, 1)), np.zeros((N + 1) * nx), np.zeros(N * nx)
+    st = lib().oracle_ocp_first_step(N, nx, _p(nua, C.c_int), _p(nca, C.c_int) if m else None,
+                                     _p(np.ascontiguousarray(x0, dtype=np.float64)), _p(np.ascontiguousarray(rec)),
+                                     _p(np.ascontiguousarray(crec, np.float64)) if m else None, C.byref(s), _p(du),
+                                     _p(dx), _p(dpi), _p(sig), _p(ru), _p(rx), _p(rb))
+    return dict(status=st, du=du[:nU], dx=dx.reshape(N + 1, nx), dpi=dpi.reshape(N, nx), sig=sig[:m], rhs_u=ru[:nU],
+                rhs_x=rx.reshape(N + 1, nx), rb=rb.reshape(N, nx))
 
 
 def gait_contact(gait, t_start, t0, dt, N, leg_map=None):

@@ -6,6 +6,7 @@
 // HpipmInterface
 // mirror, whose solve runs on the MI355X engine. Random problems from a fixed-seed generator (ocs2's
 // getRandomDynamics/getRandomCost are not vendored): uniform [-1,1) matrices, costs made positive definite.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <random>
@@ -87,6 +88,12 @@ static double maxdiff(const vector_t& a, const vector_t& b) {
   double m = a.size() == b.size() ? 0.0 : 1e300;
   for (int i = 0; i < a.size() && i < b.size(); ++i) m = std::fmax(m, std::fabs(a[i] - b[i]));
   return m;
+}
+
+static double norm(const vector_t& v) {
+  double s = 0.0;
+  for (int i = 0; i < v.size(); ++i) s += v[i] * v[i];
+  return std::sqrt(s);
 }
 
 static int failures = 0;
@@ -384,9 +391,12 @@ static double total_cost(const std::vector<ScalarFunctionQuadraticApproximation>
 }
 
 // Riccati quantities after an equality-constrained solve (the non-projection branch of getOCPSolution followed by
-// setPrimalSolution's getRiccatiFeedback, MultipleShootingSolver.cpp:275-277, :334-340): u_k = K_k x_k + k_k on the
-// solution, K_0 = d u_0 / d x0 by finite differences of the constrained solution map, and the cost-to-go of node 0
-// reproduces the change of the optimal cost under a perturbation of x0.
+// setPrimalSolution's getRiccatiFeedback, MultipleShootingSolver.cpp:275-277, :334-340). The device returns the
+// barrier-weighted Riccati quantities of the interior-point solve at the returned point (cmpc_ocp_riccati): u_k =
+// K_k x_k + k_k holds on the solution to the IPM's accuracy, and K_0 / the node-0 cost-to-go approach the exact
+// derivatives of the constrained solution map as the rows' barrier weights grow (agreement ~1e-4 at HPIPM's default
+// tolerances: rows with near-zero multipliers keep moderate weights). Node 0 carries no rows here: the reference
+// rebuilds stage 0 from (dynamics0, cost0) alone (HpipmInterface.cpp:334-347, :376-389), which leaves out node-0 rows.
 static void constrained_riccati() {
   const int nx = 3, nu = 2, N = 5;
   const vector_t x0 = randv(nx);
@@ -399,6 +409,7 @@ static void constrained_riccati() {
   }
   cost.push_back(randomCost(nx, 0));
   con.push_back(randomConstraints(nx, 0, 1));
+  con[0] = VectorFunctionLinearApproximation();
   con[2] = VectorFunctionLinearApproximation();
   HpipmInterface hpipm(hpipm_interface::extractSizesFromProblem(sys, cost, &con));
   vector_array_t xs, us;
@@ -422,17 +433,132 @@ static void constrained_riccati() {
     for (int c = 0; c < nx; ++c) pred += x0[c] * ctg[0].dfdxx(c, i) * eps;
     e_ctg = std::fmax(e_ctg, std::fabs(dJ - pred) / std::fmax(1.0, std::fabs(dJ)));
   }
-  // the later stages' feedback acts on the state of that stage: perturb the tail through u_0 is not needed — the
-  // policy identity above covers k >= 1; K symmetric pieces: cost-to-go Hessians are symmetric
-  double e_sym = 0.0;
+  double e_sym = 0.0, smax = 1.0;
   for (int k = 0; k <= N; ++k)
     for (int i = 0; i < nx; ++i)
-      for (int j = 0; j < nx; ++j) e_sym = std::fmax(e_sym, std::fabs(ctg[(size_t)k].dfdxx(i, j) - ctg[(size_t)k].dfdxx(j, i)));
-  std::printf("constrained riccati: policy %.2e, fd K0 %.2e, cost-to-go %.2e, symmetry %.2e\n", e_pol, e_fd, e_ctg, e_sym);
-  CHECK(e_pol < 1e-9, "constrained riccati u = K x + k");
-  CHECK(e_fd < 1e-7, "constrained riccati K0 by finite differences");
-  CHECK(e_ctg < 1e-7, "constrained riccati cost-to-go");
-  CHECK(e_sym < 1e-9, "constrained riccati S symmetric");
+      for (int j = 0; j < nx; ++j) {
+        e_sym = std::fmax(e_sym, std::fabs(ctg[(size_t)k].dfdxx(i, j) - ctg[(size_t)k].dfdxx(j, i)));
+        smax = std::fmax(smax, std::fabs(ctg[(size_t)k].dfdxx(i, j)));
+      }
+  std::printf("constrained riccati: policy %.2e, fd K0 %.2e, cost-to-go %.2e, symmetry %.2e (of %.2e)\n", e_pol, e_fd,
+              e_ctg, e_sym, smax);
+  CHECK(e_pol < 1e-7, "constrained riccati u = K x + k");
+  CHECK(e_fd < 1e-3, "constrained riccati K0 by finite differences");
+  CHECK(e_ctg < 1e-3, "constrained riccati cost-to-go");
+  CHECK(e_sym < 1e-12 * smax, "constrained riccati S symmetric");
+}
+
+// The legged-robot size (ocs2_legged_robot/config/mpc/task.info: 24 states, 24 inputs, dt 0.015 s over 1 s -> 67
+// stages), the reference's constructions: knownSolution (1e-9), retrieveRiccati (closed-form recursion, 1e-9 relative)
+// and with_constraints (12 rows per node, dynamics and rows isApprox 1e-9), with a solve-latency print.
+static void legged_size() {
+  const int nx = 24, nu = 24, N = 67;
+  auto stable = [&](int r, int c, double dt) {
+    matrix_t m = randm(r, c);
+    for (int j = 0; j < c; ++j)
+      for (int i = 0; i < r; ++i) m(i, j) = (i == j && r == c ? 1.0 : 0.0) + dt * m(i, j);
+    return m;
+  };
+  std::vector<vector_t> xg{randv(nx)}, ug;
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    ug.push_back(randv(nu));
+    VectorFunctionLinearApproximation d;
+    d.dfdx = stable(nx, nx, 0.015);
+    d.dfdu = stable(nx, nu, 0.015);
+    d.f = randv(nx);
+    for (int i = 0; i < nx; ++i) d.f[i] *= 0.015;
+    sys.push_back(d);
+    vector_t xn = d.f;
+    const vector_t ax = mv(d.dfdx, xg[(size_t)k]), bu = mv(d.dfdu, ug[(size_t)k]);
+    for (int i = 0; i < nx; ++i) xn[i] += ax[i] + bu[i];
+    xg.push_back(xn);
+    cost.push_back(randomCost(nx, nu));
+    const vector_t qx = mv(cost[(size_t)k].dfdxx, xg[(size_t)k]), su = mtv(cost[(size_t)k].dfdux, ug[(size_t)k]);
+    for (int i = 0; i < nx; ++i) cost[(size_t)k].dfdx[i] = -(qx[i] + su[i]);
+    const vector_t ru = mv(cost[(size_t)k].dfduu, ug[(size_t)k]), sx = mv(cost[(size_t)k].dfdux, xg[(size_t)k]);
+    for (int i = 0; i < nu; ++i) cost[(size_t)k].dfdu[i] = -(ru[i] + sx[i]);
+  }
+  cost.push_back(randomCost(nx, 0));
+  const vector_t qN = mv(cost[(size_t)N].dfdxx, xg[(size_t)N]);
+  for (int i = 0; i < nx; ++i) cost[(size_t)N].dfdx[i] = -qN[i];
+  HpipmInterface hpipm(HpipmInterface::OcpSize(N, nx, nu));
+  vector_array_t xs, us;
+  auto st = hpipm.solve(xg[0], sys, cost, nullptr, xs, us, false);  // first call: module load / first touch
+  const auto t0 = std::chrono::steady_clock::now();
+  const int reps = 20;
+  for (int r = 0; r < reps; ++r) st = hpipm.solve(xg[0], sys, cost, nullptr, xs, us, false);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / reps;
+  CHECK(st == SUCCESS, "legged size status");
+  double e = 0.0, sc = 1.0;
+  for (int k = 0; k <= N; ++k) e = std::fmax(e, maxdiff(xs[(size_t)k], xg[(size_t)k]));
+  for (int k = 0; k < N; ++k) e = std::fmax(e, maxdiff(us[(size_t)k], ug[(size_t)k]));
+  // retrieveRiccati at this size
+  std::vector<matrix_t> SmG((size_t)N + 1), KG((size_t)N);
+  std::vector<vector_t> svG((size_t)N + 1), kG((size_t)N);
+  SmG[(size_t)N] = cost[(size_t)N].dfdxx;
+  svG[(size_t)N] = cost[(size_t)N].dfdx;
+  for (int k = N - 1; k >= 0; --k) {
+    const matrix_t& Sm = SmG[(size_t)k + 1];
+    const vector_t& sv = svG[(size_t)k + 1];
+    const auto& A = sys[(size_t)k].dfdx;
+    const auto& B = sys[(size_t)k].dfdu;
+    const auto& b = sys[(size_t)k].f;
+    const auto& c = cost[(size_t)k];
+    const matrix_t P = add(c.dfdux, mm(tr(B), mm(Sm, A)));
+    const matrix_t invR = inv(add(c.dfduu, mm(tr(B), mm(Sm, B))));
+    const vector_t rr = addv(addv(c.dfdu, mtv(B, sv)), mtv(B, mv(Sm, b)));
+    SmG[(size_t)k] = add(add(c.dfdxx, mm(tr(A), mm(Sm, A))), mm(tr(P), mm(invR, P)), -1.0);
+    svG[(size_t)k] = addv(addv(addv(c.dfdx, mtv(A, sv)), mtv(A, mv(Sm, b))), mv(tr(P), mv(invR, rr)), -1.0);
+    KG[(size_t)k] = add(zeros(nu, nx), mm(invR, P), -1.0);
+    kG[(size_t)k] = mv(invR, rr);
+    for (int i = 0; i < nu; ++i) kG[(size_t)k][i] = -kG[(size_t)k][i];
+  }
+  const auto K = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  const auto kf = hpipm.getRiccatiFeedforward(sys[0], cost[0]);
+  const auto ctg = hpipm.getRiccatiCostToGo(sys[0], cost[0]);
+  double er = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    for (int i = 0; i < nx; ++i)
+      for (int j = 0; j < nx; ++j) sc = std::fmax(sc, std::fabs(SmG[(size_t)k](i, j)));
+    er = std::fmax(er, maxdiffm(ctg[(size_t)k].dfdxx, SmG[(size_t)k]));
+    er = std::fmax(er, maxdiff(ctg[(size_t)k].dfdx, svG[(size_t)k]));
+  }
+  for (int k = 0; k < N; ++k) {
+    er = std::fmax(er, maxdiffm(K[(size_t)k], KG[(size_t)k]));
+    er = std::fmax(er, maxdiff(kf[(size_t)k], kG[(size_t)k]));
+  }
+  // with_constraints at this size: 12 rows per node (node 1 empty, node N state-only)
+  std::vector<VectorFunctionLinearApproximation> con;
+  for (int k = 0; k < N; ++k) con.push_back(randomConstraints(nx, nu, 12));
+  con.push_back(randomConstraints(nx, 0, 12));
+  con[1] = VectorFunctionLinearApproximation();
+  HpipmInterface hc(hpipm_interface::extractSizesFromProblem(sys, cost, &con));
+  vector_array_t xc, uc;
+  auto stc = hc.solve(xg[0], sys, cost, &con, xc, uc, false);
+  const auto t1 = std::chrono::steady_clock::now();
+  for (int r = 0; r < reps; ++r) stc = hc.solve(xg[0], sys, cost, &con, xc, uc, false);
+  const double msc = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count() / reps;
+  CHECK(stc == SUCCESS, "legged size constrained status");
+  double ec = 0.0;
+  for (int k = 0; k < N; ++k) {
+    vector_t xn = sys[(size_t)k].f;
+    const vector_t ax = mv(sys[(size_t)k].dfdx, xc[(size_t)k]), bu = mv(sys[(size_t)k].dfdu, uc[(size_t)k]);
+    for (int i = 0; i < nx; ++i) xn[i] += ax[i] + bu[i];
+    ec = std::fmax(ec, maxdiff(xc[(size_t)k + 1], xn) / std::fmax(1e-300, norm(xn)));
+    if (con[(size_t)k].f.size() > 0) {
+      const vector_t r = addv(mv(con[(size_t)k].dfdx, xc[(size_t)k]), mv(con[(size_t)k].dfdu, uc[(size_t)k]));
+      vector_t negf = con[(size_t)k].f;
+      for (int i = 0; i < negf.size(); ++i) negf[i] = -negf[i];
+      ec = std::fmax(ec, maxdiff(r, negf) / std::fmax(1e-300, norm(negf)));
+    }
+  }
+  std::printf("legged size (nx %d, nu %d, N %d): known solution %.3e, riccati %.3e (of %.2e), constrained %.3e; "
+              "host-path solve %.3f ms (no rows), %.3f ms (12 rows per node)\n", nx, nu, N, e, er, sc, ec, ms, msc);
+  CHECK(e < 1e-9, "legged size knownSolution 1e-9");
+  CHECK(er < 1e-9 * sc, "legged size retrieveRiccati 1e-9");
+  CHECK(ec < 1e-9, "legged size with_constraints 1e-9");
 }
 
 // Per-node state dimensions (OcpSize::numStates[k], OcpSize.cpp:55-60; HPIPM takes nx[k] per node): a known
@@ -548,6 +674,7 @@ int main() {
   retrieve_riccati();
   constrained_riccati();
   varying_state_dims();
+  legged_size();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;
 }

@@ -37,3 +37,25 @@ def test_world_size_mismatch_is_refused():
     r = _run(["--gpus", "3", "--stub"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_ranks_sharing_one_gpu_are_refused():
+    """two ranks that see the same physical GPU (a one-GPU box) are refused, not labelled as two
+    GPUs."""
+    r = _run(["--gpus", "2", "--stub", "--stub-devices", "0000:05:00.0"])
+    assert r.returncode != 0
+    assert "distinct GPU" in r.stderr and "--allow-shared" in r.stderr
+
+
+def test_ranks_sharing_one_gpu_labelled_with_allow_shared():
+    r = _run(["--gpus", "2", "--stub", "--stub-devices", "0000:05:00.0", "--allow-shared"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert d["n_gpus"] == 1 and d["n_ranks"] == 2 and d["shared_gpu"] is True
+
+
+def test_distinct_gpus_count_as_gpus():
+    r = _run(["--gpus", "2", "--stub", "--stub-devices", "0000:05:00.0,0000:15:00.0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert d["n_gpus"] == 2 and d["shared_gpu"] is False

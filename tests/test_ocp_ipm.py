@@ -1,0 +1,450 @@
+"""HpipmInterface::solve path at the size of its real caller.
+
+The reference's HpipmInterface (ocs2_sqp/hpipm_catkin/src/HpipmInterface.cpp:166-301) hands the OCP to HPIPM's
+interior-point method: x0 eliminated (:177-208), the equality rows as two-sided general constraints lg = ug
+(:223-264), Riccati Newton steps (ric_alg, HpipmInterfaceSettings.h:56), the Settings' iter_max / tol_* honoured.
+Its caller MultipleShootingSolver runs it on the legged robot: nx = 24, nu = 24 (projected: 10-12, 0 at event
+nodes), N ~ 70 (ocs2_legged_robot/config/mpc/task.info:33, :40, :102).
+
+Oracle: oracle/ocp_ipm.c (oracle_ocp_ipm), the builder's restatement of HPIPM's OCP IPM (HPIPM itself is not
+vendored: parity against its binary is unpinned). It is pinned here on the CPU by
+  - its first Newton step against a dense full-space KKT solve of the same system,
+  - the reference's own constructions (testHpipmInterface.cpp: knownSolution :112-152, with_constraints :154-206,
+    noInputs :208-256, retrieveRiccati :258-340 at 1e-9), at the reference's sizes and at the legged-robot size,
+  - the exact constrained solution (np_ref.ocp_eq_fullspace) and the exact constrained feedback of the tail problems.
+The device (cmpc_ocp_solve / cmpc_ocp_riccati, csrc/k_ocp.hip) must match the oracle: statuses and iteration counts
+equal, trajectories and Riccati quantities to 1e-9 relative (rounding of a different factorisation: Gauss-Jordan
+sweeps on the device, Cholesky in the oracle).
+"""
+import numpy as np
+import pytest
+
+import np_ref
+from cheeta_mpc import ocp as ocpgen
+from test_oracle import random_ocp
+
+
+def _small(seed, N=5, nx=3, nu=None, nc=None, rows=True):
+    rng = np.random.default_rng(seed)
+    nu = list(nu or [2] * N)
+    nc = list(nc or ([1, 0] + [1] * (N - 1))[: N + 1]) if rows else None
+    A, B, b, Q, S, R, q, r = random_ocp(rng, N, nx, nu)
+    p = dict(N=N, nx=nx, nu=nu, nc=nc, x0=rng.uniform(-1, 1, nx), A=A, B=B, b=b, Q=Q, S=S, R=R, q=q, r=r)
+    Cc, D, e = [], [], []
+    for k in range(N + 1):
+        m = nu[k] if k < N else 0
+        g = nc[k] if nc else 0
+        Cc.append(rng.uniform(-1, 1, (g, nx)))
+        D.append(rng.uniform(-1, 1, (g, m)))
+        e.append(rng.uniform(-1, 1, g))
+    p.update(Cc=Cc, D=D, e=e)
+    return p
+
+
+def _known(p, rows_hold=True, seed=0):
+    """knownSolution (testHpipmInterface.cpp:112-152): q, r make a random rollout the optimum; with rows_hold the rows
+    are satisfied there (then it is the constrained optimum too)."""
+    rng = np.random.default_rng(seed + 1000)
+    N = p["N"]
+    xs, us = [p["x0"]], []
+    for k in range(N):
+        us.append(rng.uniform(-1, 1, p["nu"][k]))
+        xs.append(p["b"][k] + p["A"][k] @ xs[k] + p["B"][k] @ us[k])
+        p["q"][k] = -(p["Q"][k] @ xs[k] + p["S"][k].T @ us[k])
+        p["r"][k] = -(p["R"][k] @ us[k] + p["S"][k] @ xs[k])
+    p["q"][N] = -p["Q"][N] @ xs[N]
+    if rows_hold and p.get("nc"):
+        for k in range(N + 1):
+            if p["nc"][k]:
+                p["e"][k] = -(p["Cc"][k] @ xs[k] + (p["D"][k] @ us[k] if k < N else 0.0))
+    p["xs"], p["us"] = np.array(xs), us
+    return p
+
+
+def _oracle(op, p, **kw):
+    rec, crec = ocpgen.pack(p)
+    return op.ocp_ipm(p["N"], p["nx"], p["nu"], p["x0"], rec, nc=p.get("nc"), crec=crec, **kw)
+
+
+def _split(p, u):
+    offs = np.cumsum([0] + list(p["nu"]))
+    return [u[offs[k]:offs[k + 1]] for k in range(p["N"])]
+
+
+def _closed_form_riccati(p, reg=0.0):
+    """testHpipmInterface.cpp:280-304 (unconstrained discrete Riccati recursion)."""
+    N = p["N"]
+    Sm, sv, K, kf = [None] * (N + 1), [None] * (N + 1), [None] * N, [None] * N
+    Sm[N], sv[N] = p["Q"][N], p["q"][N]
+    for k in range(N - 1, -1, -1):
+        A, B, b = p["A"][k], p["B"][k], p["b"][k]
+        Q, R, P, q, r = p["Q"][k], p["R"][k], p["S"][k], p["q"][k], p["r"][k]
+        PBSA = P + B.T @ Sm[k + 1] @ A
+        iR = np.linalg.inv(R + reg * np.eye(len(r)) + B.T @ Sm[k + 1] @ B) if len(r) else np.zeros((0, 0))
+        rr = r + B.T @ sv[k + 1] + B.T @ Sm[k + 1] @ b
+        Sm[k] = Q + A.T @ Sm[k + 1] @ A - PBSA.T @ iR @ PBSA
+        sv[k] = q + A.T @ sv[k + 1] + A.T @ Sm[k + 1] @ b - PBSA.T @ iR @ rr
+        K[k] = -iR @ PBSA
+        kf[k] = -iR @ rr
+    return Sm, sv, K, kf
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(1.0, np.abs(b).max())) if a.size else 0.0
+
+
+# ------------------------------------------------------------------------------------------------- oracle (CPU)
+
+def _dense_first_step(p, sig, gu, gx, rb):
+    """The cold start's Newton system [H + Gc'Sigma Gc + reg I, G'; G, 0] [dz; dpi] = [-g; -rb] assembled densely."""
+    N, nx, nu = p["N"], p["nx"], p["nu"]
+    reg = 1e-12
+    xo, uo, n = {}, {}, 0
+    for k in range(N + 1):
+        if k >= 1:
+            xo[k] = n
+            n += nx
+        if k < N:
+            uo[k] = n
+            n += nu[k]
+    H = np.zeros((n, n))
+    g = np.zeros(n)
+    row0 = 0
+    for k in range(N + 1):
+        m = nu[k] if k < N else 0
+        us = slice(uo[k], uo[k] + m) if k < N else None
+        if k >= 1:
+            xs = slice(xo[k], xo[k] + nx)
+            H[xs, xs] += p["Q"][k] + reg * np.eye(nx)
+            g[xs] += gx[k]
+        if m:
+            H[us, us] += p["R"][k] + reg * np.eye(m)
+            g[us] += gu[k]
+            if k >= 1:
+                H[us, xs] += p["S"][k]
+                H[xs, us] += p["S"][k].T
+        gk = p["nc"][k] if p.get("nc") else 0
+        if gk:
+            s = sig[row0:row0 + gk]
+            row0 += gk
+            Gk = np.zeros((gk, n))
+            if k >= 1:
+                Gk[:, xs] = p["Cc"][k]
+            if m:
+                Gk[:, us] = p["D"][k]
+            H += Gk.T @ (s[:, None] * Gk)
+    G = np.zeros((N * nx, n))
+    for k in range(N):
+        G[k * nx:(k + 1) * nx, xo[k + 1]:xo[k + 1] + nx] = -np.eye(nx)
+        if k >= 1:
+            G[k * nx:(k + 1) * nx, xo[k]:xo[k] + nx] = p["A"][k]
+        if nu[k]:
+            G[k * nx:(k + 1) * nx, uo[k]:uo[k] + nu[k]] = p["B"][k]
+    Kkt = np.block([[H, G.T], [G, np.zeros((N * nx, N * nx))]])
+    sol = np.linalg.solve(Kkt, np.concatenate([-g, -np.concatenate(rb)]))
+    du = np.concatenate([sol[uo[k]:uo[k] + nu[k]] for k in range(N)])
+    dx = np.array([np.zeros(nx)] + [sol[xo[k]:xo[k] + nx] for k in range(1, N + 1)])
+    return du, dx, sol[n:].reshape(N, nx)
+
+
+@pytest.mark.parametrize("shape", [dict(N=5, nx=3), dict(N=6, nx=4, nu=[3, 0, 3, 2, 3, 3], nc=[2, 0, 1, 2, 0, 1, 2])])
+def test_oracle_first_step_is_the_dense_newton_step(op, shape):
+    p = _small(3, **shape)
+    rec, crec = ocpgen.pack(p)
+    fs = op.ocp_first_step(p["N"], p["nx"], p["nu"], p["x0"], rec, nc=p["nc"], crec=crec)
+    assert fs["status"] == 0
+    gu = _split(p, fs["rhs_u"])
+    du, dx, dpi = _dense_first_step(p, fs["sig"], gu, fs["rhs_x"], list(fs["rb"]))
+    assert _rel(fs["du"], du) < 1e-10
+    assert _rel(fs["dx"], dx) < 1e-10
+    assert _rel(fs["dpi"], dpi) < 1e-10
+
+
+@pytest.mark.parametrize("nu", [[2] * 5, [2, 0, 2, 2, 2]])
+def test_oracle_unconstrained_is_one_newton_step(op, nu):
+    """solve_and_check_dynamic / noInputs (testHpipmInterface.cpp:37-69, :208-256): without rows the IPM's first
+    Newton step is the solution; equals the condensed solve (oracle_ocp_solve) and the dynamics hold."""
+    p = _small(5, nu=nu, rows=False)
+    rec, _ = ocpgen.pack(p)
+    r = op.ocp_ipm(p["N"], p["nx"], p["nu"], p["x0"], rec)
+    assert r["status"] == 0 and r["iters"] == 1
+    xc, uc, st = op.ocp_solve(p["N"], p["nx"], p["nu"], p["x0"], rec)
+    assert st == 0 and _rel(r["u"], uc) < 1e-10 and _rel(r["x"], xc) < 1e-10
+    for k, uk in enumerate(_split(p, r["u"])):
+        assert np.allclose(r["x"][k + 1], p["A"][k] @ r["x"][k] + p["B"][k] @ uk + p["b"][k], rtol=1e-12, atol=1e-12)
+
+
+def test_oracle_retrieve_riccati(op):
+    """retrieveRiccati (testHpipmInterface.cpp:258-340): S, s, K, k equal the discrete recursion at 1e-9 and
+    u = K x + k along the solution."""
+    p = _small(8, rows=False)
+    r = _oracle(op, p, ric=True)
+    Sm, sv, K, kf = _closed_form_riccati(p)
+    for k in range(p["N"] + 1):
+        assert _rel(r["P"][k], Sm[k]) < 1e-9 and _rel(r["p"][k], sv[k]) < 1e-9
+    us = _split(p, r["u"])
+    for k in range(p["N"]):
+        assert _rel(r["K"][k], K[k]) < 1e-9 and _rel(r["k"][k], kf[k]) < 1e-9
+        assert np.allclose(us[k], r["K"][k] @ r["x"][k] + r["k"][k], atol=1e-9)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_with_constraints(op, seed):
+    """with_constraints (testHpipmInterface.cpp:154-206): nc = 1 per node, node 1 empty, node N state-only; the IPM
+    converges (HPIPM's stopping rule) to the exact constrained solution (np_ref full-space KKT) and the reference's
+    isApprox checks hold at 1e-9."""
+    p = _small(seed)
+    r = _oracle(op, p)
+    assert r["status"] == 0 and 3 <= r["iters"] <= 30
+    x, u, _ = np_ref.ocp_eq_fullspace(p["N"], p["nx"], p["nu"], p["x0"], p["A"], p["B"], p["b"], p["Q"], p["S"],
+                                      p["R"], p["q"], p["r"], Cc=p["Cc"], D=p["D"], e=p["e"])
+    assert _rel(r["x"], x) < 1e-9 and _rel(r["u"], np.concatenate(u)) < 1e-9
+    us = _split(p, r["u"])
+    for k in range(p["N"]):
+        xn = p["A"][k] @ r["x"][k] + p["B"][k] @ us[k] + p["b"][k]
+        assert np.linalg.norm(r["x"][k + 1] - xn) <= 1e-9 * np.linalg.norm(xn)
+        if p["nc"][k]:
+            v = -(p["Cc"][k] @ r["x"][k] + p["D"][k] @ us[k])
+            assert np.linalg.norm(p["e"][k] - v) <= 1e-9 * np.linalg.norm(p["e"][k])
+
+
+def test_oracle_inconsistent_rows_end_at_max_iter_or_min_step(op):
+    """HPIPM's OCP IPM treats lg = ug rows as inequalities: contradictory rows cannot be met, the IPM runs out of
+    iterations (MAX_ITER) or steps (MIN_STEP) within iter_max; a consistent duplicate row changes nothing."""
+    p = _small(21)
+    base = _oracle(op, p)
+    q = dict(p)
+    q["nc"] = list(p["nc"])
+    q["nc"][2] = 2
+    q["Cc"], q["D"], q["e"] = list(p["Cc"]), list(p["D"]), list(p["e"])
+    q["Cc"][2] = np.vstack([p["Cc"][2], p["Cc"][2]])
+    q["D"][2] = np.vstack([p["D"][2], p["D"][2]])
+    q["e"][2] = np.concatenate([p["e"][2], p["e"][2]])
+    dup = _oracle(op, q)
+    assert base["status"] == 0 and dup["status"] == 0
+    assert _rel(dup["u"], base["u"]) < 1e-8
+    q["e"][2] = np.concatenate([p["e"][2], p["e"][2] + 1.0])
+    for it_max in (30, 12):
+        bad = _oracle(op, q, settings=op.default_settings(iter_max=it_max))
+        assert bad["status"] in (1, 2) and bad["iters"] <= it_max
+        assert bad["res"][2] > 1e-3  # the rows stay violated
+
+
+def _tail_feedback(p, k, eps=1.0):
+    """Exact du_k/dx_k of the equality-constrained tail problem k..N (np_ref full-space solve from x_k = 0 and the
+    unit vectors; the state-only rows of node k dropped, x_k being given), the limit of the barrier-weighted K_k."""
+    N, nx = p["N"], p["nx"]
+    sl = lambda a: list(a[k:])  # noqa: E731
+    Cc, D, e = sl(p["Cc"]), sl(p["D"]), sl(p["e"])
+    if p["nc"][k]:
+        keep = np.abs(D[0]).sum(axis=1) > 0
+        Cc[0], D[0], e[0] = Cc[0][keep], D[0][keep], e[0][keep]
+    args = (N - k, nx, p["nu"][k:], None, sl(p["A"]), sl(p["B"]), sl(p["b"]), sl(p["Q"]), sl(p["S"]), sl(p["R"]),
+            sl(p["q"]), sl(p["r"]))
+    u0 = np_ref.ocp_eq_fullspace(*args[:3], np.zeros(nx), *args[4:], Cc=Cc, D=D, e=e)[1][0]
+    K = np.zeros((len(u0), nx))
+    for i in range(nx):
+        xi = np.zeros(nx)
+        xi[i] = eps
+        K[:, i] = (np_ref.ocp_eq_fullspace(*args[:3], xi, *args[4:], Cc=Cc, D=D, e=e)[1][0] - u0) / eps
+    return K
+
+
+def test_oracle_constrained_riccati(op):
+    """After an equality-constrained solve: K_k (k >= 1) is the barrier-weighted feedback at the exit point, which
+    approaches the exact constrained feedback of the tail problem as Sigma -> inf on the rows (a row whose multiplier
+    is ~0 keeps a moderate Sigma = l / t at the exit point, so the agreement is ~1e-4, not 1e-9: a property of the
+    interior-point method, HPIPM's included); u_k = K_k x_k + k_k holds at the returned point to the IPM's accuracy."""
+    p = _small(2)
+    r = _oracle(op, p, ric=True)
+    assert r["status"] == 0
+    us = _split(p, r["u"])
+    for k in range(1, p["N"]):
+        assert np.abs(us[k] - (r["K"][k] @ r["x"][k] + r["k"][k])).max() < 1e-8
+        assert _rel(r["K"][k], _tail_feedback(p, k)) < 1e-3
+
+
+@pytest.mark.parametrize("projected", [True, False])
+def test_oracle_legged_size_known_solution(op, projected):
+    """knownSolution at the ocs2_legged_robot size (nx = 24, N = 70 with three event nodes; projected: nu 10 / 12 / 0
+    and no rows; else nu = 24 and 12-14 equality rows per node, satisfied at the known solution)."""
+    p = ocpgen.legged_problem(7, projected=projected, known_solution=True, rows_hold=True, cost="random")
+    assert p["N"] == 70 and p["nx"] == 24
+    r = _oracle(op, p)
+    assert r["status"] == 0
+    assert r["iters"] == 1 if projected else r["iters"] <= 30
+    assert _rel(r["x"], p["xs"]) < 1e-9
+    assert _rel(r["u"], np.concatenate(p["us"])) < 1e-9
+
+
+def test_oracle_legged_constrained_matches_fullspace(op):
+    """The legged-size problem with binding rows (random e): the IPM's solution equals the exact full-space solve."""
+    p = ocpgen.legged_problem(11, projected=False)
+    r = _oracle(op, p)
+    assert r["status"] == 0
+    x, u, _ = np_ref.ocp_eq_fullspace(p["N"], p["nx"], p["nu"], p["x0"], p["A"], p["B"], p["b"], p["Q"], p["S"],
+                                      p["R"], p["q"], p["r"], Cc=p["Cc"], D=p["D"], e=p["e"])
+    assert _rel(r["x"], x) < 1e-8 and _rel(r["u"], np.concatenate(u)) < 1e-8
+
+
+def test_oracle_stats_table(op):
+    """Per-iteration statistics: rows 0..iters, residual columns equal to the exit residuals on the last row."""
+    p = _small(4)
+    r = _oracle(op, p, stats_rows=31)
+    st = r["stats"]
+    it = r["iters"]
+    assert np.all(np.isnan(st[it + 1:]))
+    assert np.allclose(st[it, 6:], r["res"], rtol=0, atol=0)
+    assert np.all(np.isnan(st[it, :5]))
+    assert np.all(st[:it, 3] > 0) and np.all(st[:it, 3] <= 1)
+
+
+# ------------------------------------------------------------------------------------------------- device (GPU)
+
+def _device_batch(cm, ps, settings=None):
+    p0 = ps[0]
+    recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+    solver = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), settings=settings, max_batch=len(ps))
+    x, u, st, it = solver.solve(np.array([p["x0"] for p in ps]), np.array(recs),
+                                np.array(crecs) if p0.get("nc") else None)
+    return solver, x, u, st, it
+
+
+def _check_vs_oracle(op, ps, x, u, st, it, settings=None, tol=1e-9):
+    for i, p in enumerate(ps):
+        r = _oracle(op, p, settings=settings)
+        assert st[i] == r["status"], (i, st[i], r["status"])
+        assert it[i] == r["iters"], (i, it[i], r["iters"])
+        assert _rel(x[i], r["x"]) < tol, (i, _rel(x[i], r["x"]))
+        assert _rel(u[i], r["u"]) < tol, (i, _rel(u[i], r["u"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [dict(N=5, nx=3), dict(N=6, nx=4, nu=[3, 0, 3, 2, 3, 3], nc=[2, 0, 1, 2, 0, 1, 2]),
+                                   dict(N=5, nx=3, rows=False), dict(N=5, nx=3, nu=[2, 0, 2, 2, 2], rows=False)])
+def test_device_small_shapes_match_oracle(cm, op, shape):
+    ps = [_small(40 + i, **shape) for i in range(6)]
+    _, x, u, st, it = _device_batch(cm, ps)
+    _check_vs_oracle(op, ps, x, u, st, it)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_legged_size_matches_oracle(cm, op, projected):
+    """nx = 24, N = 70 (67 intervals + 3 event nodes), projected (nu 10 / 12 / 0, no rows) or with the 12-14 equality
+    rows per node (nu = 24): a batch of 6 seeded problems, device vs oracle."""
+    ps = [ocpgen.legged_problem(100 + i, projected=projected) for i in range(6)]
+    _, x, u, st, it = _device_batch(cm, ps)
+    assert np.all(st == 0)
+    _check_vs_oracle(op, ps, x, u, st, it, tol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_legged_known_solution(cm, op, projected):
+    ps = [ocpgen.legged_problem(200 + i, projected=projected, known_solution=True, rows_hold=True, cost="random")
+          for i in range(3)]
+    _, x, u, st, it = _device_batch(cm, ps)
+    for i, p in enumerate(ps):
+        assert st[i] == 0
+        assert _rel(x[i], p["xs"]) < 1e-9 and _rel(u[i], np.concatenate(p["us"])) < 1e-9
+
+
+@pytest.mark.gpu
+def test_device_with_constraints_reference_properties(cm, op):
+    ps = [_small(60 + i) for i in range(4)]
+    _, x, u, st, it = _device_batch(cm, ps)
+    for i, p in enumerate(ps):
+        assert st[i] == 0
+        us = _split(p, u[i])
+        for k in range(p["N"]):
+            xn = p["A"][k] @ x[i][k] + p["B"][k] @ us[k] + p["b"][k]
+            assert np.linalg.norm(x[i][k + 1] - xn) <= 1e-9 * np.linalg.norm(xn)
+            if p["nc"][k]:
+                v = -(p["Cc"][k] @ x[i][k] + p["D"][k] @ us[k])
+                assert np.linalg.norm(p["e"][k] - v) <= 1e-9 * np.linalg.norm(p["e"][k])
+
+
+@pytest.mark.gpu
+def test_device_inconsistent_rows_status(cm, op):
+    p = _small(21)
+    q = dict(p)
+    q["nc"] = list(p["nc"])
+    q["nc"][2] = 2
+    q["Cc"], q["D"], q["e"] = list(p["Cc"]), list(p["D"]), list(p["e"])
+    q["Cc"][2] = np.vstack([p["Cc"][2], p["Cc"][2]])
+    q["D"][2] = np.vstack([p["D"][2], p["D"][2]])
+    q["e"][2] = np.concatenate([p["e"][2], p["e"][2] + 1.0])
+    for it_max in (30, 12):
+        s = cm.default_settings(iter_max=it_max)
+        _, x, u, st, it = _device_batch(cm, [q], settings=s)
+        r = _oracle(op, q, settings=op.default_settings(iter_max=it_max))
+        assert st[0] in (1, 2) and st[0] == r["status"] and it[0] == r["iters"] <= it_max
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["small", "legged_projected", "legged_rows"])
+def test_device_riccati_matches_oracle(cm, op, case):
+    """cmpc_ocp_riccati vs the oracle's Riccati quantities (P, p, K, k, Minv per stage) at 1e-9; without rows also vs
+    the closed-form recursion of retrieveRiccati (testHpipmInterface.cpp:280-304) and u = K x + k."""
+    if case == "small":
+        ps = [_small(70 + i, rows=False) for i in range(3)]
+    elif case == "legged_projected":
+        ps = [ocpgen.legged_problem(300 + i, projected=True) for i in range(3)]
+    else:
+        ps = [ocpgen.legged_problem(310 + i, projected=False) for i in range(3)]
+    solver, x, u, st, it = _device_batch(cm, ps)
+    P, pv, K, kf, Mi, rst = solver.riccati(len(ps))
+    assert np.all(rst == 0)
+    for i, p in enumerate(ps):
+        r = _oracle(op, p, ric=True)
+        N = p["N"]
+        for k in range(N + 1):
+            assert _rel(P[i][k], r["P"][k]) < 1e-9, ("P", k)
+            assert _rel(pv[i][k], r["p"][k]) < 1e-8, ("p", k)
+        for k in range(N):
+            assert _rel(K[i][k], r["K"][k]) < 1e-9, ("K", k)
+            assert _rel(kf[i][k], r["k"][k]) < 1e-8, ("k", k)
+            assert _rel(Mi[i][k], r["Minv"][k]) < 1e-9, ("Minv", k)
+        if p.get("nc") is None:
+            Sm, sv, Kc, kc = _closed_form_riccati(p)
+            us = _split(p, u[i])
+            for k in range(N):
+                assert _rel(K[i][k], Kc[k]) < 1e-8 and _rel(kf[i][k], kc[k]) < 1e-7
+                assert np.allclose(us[k], K[i][k] @ x[i][k] + kf[i][k], atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_device_residuals_and_stats_match_oracle(cm, op):
+    ps = [_small(80 + i) for i in range(3)]
+    solver, x, u, st, it = _device_batch(cm, ps)
+    res = solver.residuals(len(ps))
+    stats = solver.stats(len(ps))
+    for i, p in enumerate(ps):
+        r = _oracle(op, p, stats_rows=solver.stat_rows)
+        assert np.allclose(res[i], r["res"], rtol=1e-6, atol=1e-14)
+        n = r["iters"] + 1
+        a, b = stats[i][:n], r["stats"][:n]
+        assert np.array_equal(np.isnan(a), np.isnan(b))
+        fin = ~np.isnan(b)
+        assert np.allclose(a[fin], b[fin], rtol=1e-6, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_device_pointer_entry_equals_host_entry(cm, op):
+    """cmpc_ocp_solve (device pointers, caller's stream) and cmpc_ocp_solve_host give identical results."""
+    ps = [ocpgen.legged_problem(400 + i, projected=False) for i in range(4)]
+    solver, x, u, st, it = _device_batch(cm, ps)
+    recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+    B = len(ps)
+    dx0 = cm.DeviceArray.from_host(np.array([p["x0"] for p in ps]))
+    drec = cm.DeviceArray.from_host(np.array(recs))
+    dcrec = cm.DeviceArray.from_host(np.array(crecs))
+    dx = cm.DeviceArray((B, ps[0]["N"] + 1, 24), np.float64)
+    du = cm.DeviceArray((B, solver.nU), np.float64)
+    dst = cm.DeviceArray((B,), np.int32)
+    dit = cm.DeviceArray((B,), np.int32)
+    solver.solve_device(B, dx0, drec, dcrec, dx, du, dst, dit)
+    assert np.array_equal(dx.host(), x) and np.array_equal(du.host(), u)
+    assert np.array_equal(dst.host(), st) and np.array_equal(dit.host(), it)
