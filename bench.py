@@ -49,6 +49,151 @@ def condense_flops(contact):
     return (2.0 * 12.0 * m ** 2 + 2.0 * 13.0 * 13.0 * m).sum(axis=1)
 
 
+def ocp_flops(nu, nc, nx, iters):
+    """Algorithmic FLOPs of one stage-wise OCP solve: per IPM iteration the Riccati factorisation of
+    every stage k (nu_k = m, nc_k = g rows, n = nx): P [B A] 2 n^2 (n+m), the symmetric [B A]'(P [B A]) and the rows'
+    Gc' Sigma Gc, lower triangles, (n+m)(n+m+1)(n+g), the Cholesky of R~ + B'PB m^3/3, Ls = M_xu Lr^-T m^2 n,
+    P_k = M_xx - Ls Ls' n^2 m; two Newton solves (predictor, corrector; one without rows) of 2 (2 n^2 + 3 n m + m^2
+    + 2 g (n + m)) each; and one residual evaluation per iteration plus the final one,
+    2 ((n+m)^2 + n (n+m) + 2 g (n+m))."""
+    n = float(nx)
+    f_fact = f_solve = f_res = 0.0
+    for k, m in enumerate(nu):
+        m = float(m)
+        g = float(nc[k]) if nc is not None else 0.0
+        f_fact += 2 * n * n * (n + m) + (n + m) * (n + m + 1) * (n + g) + m ** 3 / 3 + m * m * n + n * n * m
+        f_solve += 2 * (2 * n * n + 3 * n * m + m * m + 2 * g * (n + m))
+        f_res += 2 * ((n + m) ** 2 + n * (n + m) + 2 * g * (n + m))
+    rows = nc is not None and sum(nc) > 0
+    return iters * (f_fact + (2 if rows else 1) * f_solve + f_res) + f_res
+
+
+def ocp_main(args):
+    """--ocp projected|rows: the HpipmInterface::solve path at the ocs2_legged_robot size (cheeta_mpc/ocp.py:
+    nx = 24, 67 intervals + 3 event nodes; projected: nu 10 / 12 / 0 and no rows, the robot's own setting
+    projectStateInputEqualityConstraints = true; rows: nu = 24 and 12-14 equality rows per node). One step = one
+    cmpc_ocp_solve of --batch problems already resident in HBM. Reports solves/s, ms per solve at B = 1 (the MPC tick's
+    latency, task.info:108: 50 Hz = 20 ms), the kernel's roofline and the CPU oracle on the host cores."""
+    import ctypes as C
+    import cheeta_mpc as cm
+    from cheeta_mpc import ocp as gen
+    from cheeta_mpc.shard import Dist
+    dist = Dist()
+    world, rank = dist.world, dist.rank
+    ndev = cm.device_count()
+    if ndev <= 0:
+        raise RuntimeError("bench.py: no HIP device visible")
+    cm._hchk(cm.hip().hipSetDevice(dist.local_rank % ndev), "hipSetDevice")
+    n_dev, dev_ids = device_census(dist, cm.device_pci_id(dist.local_rank % ndev), args.allow_shared)
+    projected = args.ocp == "projected"
+    B = args.batch
+    H = cm.hip()
+    distinct = 16
+    ps = [gen.legged_problem(7000 + rank * distinct + i, projected=projected) for i in range(distinct)]
+    p0 = ps[0]
+    packed = [gen.pack(p) for p in ps]
+    idx = np.arange(B) % distinct
+    x0 = np.array([ps[i]["x0"] for i in idx])
+    recs = np.array([packed[i][0] for i in idx])
+    crecs = np.array([packed[i][1] for i in idx]) if not projected else None
+    solver = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=max(B, 1))
+    dx0, drec = cm.DeviceArray.from_host(x0), cm.DeviceArray.from_host(recs)
+    dcrec = cm.DeviceArray.from_host(crecs) if crecs is not None else None
+    dx = cm.DeviceArray((B, p0["N"] + 1, p0["nx"]), np.float64)
+    du = cm.DeviceArray((B, max(solver.nU, 1)), np.float64)
+    dst, dit = cm.DeviceArray((B,), np.int32), cm.DeviceArray((B,), np.int32)
+    stream = C.c_void_p()
+    H.hipStreamCreate(C.byref(stream))
+    ev = [C.c_void_p(), C.c_void_p()]
+    for e in ev:
+        H.hipEventCreate(C.byref(e))
+
+    def solve(nb):
+        solver.solve_device(nb, dx0, drec, dcrec, dx, du, dst, dit, stream)
+
+    for _ in range(args.warmup):
+        solve(B)
+    H.hipStreamSynchronize(stream)
+    dist.barrier()
+    t0 = time.perf_counter()
+    H.hipEventRecord(ev[0], stream)
+    for _ in range(args.steps):
+        solve(B)
+    H.hipEventRecord(ev[1], stream)
+    H.hipStreamSynchronize(stream)
+    t1 = time.perf_counter()
+    dist.barrier()
+    elapsed = dist.max(t1 - t0)
+    ms_ev = C.c_float()
+    H.hipEventElapsedTime(C.byref(ms_ev), ev[0], ev[1])
+    kernel_ms = ms_ev.value / args.steps  # one k_ocp_ipm launch per step on this stream
+    st, it = dst.host(), dit.host()
+    # B = 1: the latency of one HpipmInterface::solve on the device (kernel only, then with the host copies)
+    reps = 50
+    H.hipEventRecord(ev[0], stream)
+    for _ in range(reps):
+        solve(1)
+    H.hipEventRecord(ev[1], stream)
+    H.hipStreamSynchronize(stream)
+    H.hipEventElapsedTime(C.byref(ms_ev), ev[0], ev[1])
+    ms_b1 = ms_ev.value / reps
+    t = time.perf_counter()
+    for _ in range(10):
+        solver.solve(x0[:1], recs[:1], crecs[:1] if crecs is not None else None)
+    ms_b1_host = (time.perf_counter() - t) / 10 * 1e3
+    ok = st == 0
+    iters_mean = float(it[ok].mean()) if ok.any() else 0.0
+    flops = sum(ocp_flops(p0["nu"], p0.get("nc"), p0["nx"], float(it[b])) for b in range(B) if ok[b])
+    ach = flops / (kernel_ms * 1e-3)
+    value = world * B * args.steps / elapsed
+    shape = (f"nx={p0['nx']}, N={p0['N']} (67 intervals + 3 event nodes), "
+             + ("nu 10/12/0 projected, no rows" if projected else "nu 24/0 with 12-14 equality rows per node"))
+    result = {
+        "metric": f"HpipmInterface OCP-QP solves/sec (ocs2_legged_robot size: {shape}) at batch={B}",
+        "value": value, "unit": "solves/s", "n_gpus": n_dev, "n_ranks": world, "shared_gpu": n_dev < world,
+        "devices": dev_ids, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (cheeta_mpc/ocp.py legged_problem, 16 seeded problems tiled over the batch)",
+        "config": {"workload": f"{B} OCP-QPs per GPU, {shape}, stage-wise interior-point (HPIPM's method), fp64",
+                   "batch_per_gpu": B, "parallelism": f"shard{world}"},
+        "ms_per_solve_b1": ms_b1, "ms_per_solve_b1_host_path": ms_b1_host,
+        "roofline": {"bound": "valu", "kernel": "k_ocp_ipm", "achieved": ach / 1e12, "peak": FP64_PEAK / 1e12,
+                     "unit": "TFLOP/s", "frac": ach / FP64_PEAK, "traffic": None, "flops_per_launch": flops,
+                     "ms_per_launch": kernel_ms, "flops_counted": "ocp_flops (bench.py): Riccati factorisation, "
+                                                                  "Newton solves and residuals per IPM iteration"},
+        "solver": {"success_frac": float(ok.mean()), "mean_iters": iters_mean},
+        "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py as op  # test infrastructure: the CPU restatement, timed as the baseline
+        op.select_build(oracle_fast_build()[0])
+        share, share_why = cpu_share()
+        threads = args.cpu_threads or share
+        S = min(max(args.cpu_sample // 64, threads), B)  # problems per pass
+        done, wall = 0, 0.0
+        while True:
+            t = time.perf_counter()
+            xc, uc, stc, itc = op.ocp_ipm_batch(p0["N"], p0["nx"], p0["nu"], x0[:S], recs[:S], nc=p0.get("nc"),
+                                                crec=crecs[:S] if crecs is not None else None, nthreads=threads)
+            wall += time.perf_counter() - t
+            done += S
+            if wall * threads >= 10.0 or wall >= 5.0:
+                break
+        ug = du.host()[:S, :solver.nU]
+        rel = np.abs(ug - uc).max() / max(1.0, np.abs(uc).max())
+        result["cpu_baseline"] = {"value": done / wall, "unit": "solves/s", "cores": threads, "kind": "port",
+                                  "cpu_share": f"{share} ({share_why})",
+                                  "sample": f"first {S} problems of the batch x{done // S}, oracle/ocp_ipm.c "
+                                            f"(oracle_ocp_ipm_batch, same algorithm, Cholesky Riccati) built -O3 "
+                                            f"-march={oracle_fast_build()[1]}, {threads} pthreads, {wall:.2f} s wall"}
+        result["max_rel_du_vs_cpu_fp64"] = float(rel)
+        result["statuses_equal_cpu"] = bool(np.array_equal(stc, st[:S]))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dist.close()
+
+
 def cpu_share():
     """(threads to use, how it was decided): the CPUs this process may run on (affinity), capped by the cgroup CPU
     quota and by OMP_NUM_THREADS when the host declares its CPU share that way (the GPU box sets it to the box's
@@ -275,6 +420,9 @@ def main():
     ap.add_argument("--traffic-json", default="",
                     help="PMC summary giving roofline.traffic (default: profiles/traffic_<workload key>.json)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pass (solve + result gather timed)")
+    ap.add_argument("--ocp", choices=["projected", "rows"], default="",
+                    help="benchmark the HpipmInterface::solve path (cmpc_ocp_solve) on ocs2_legged_robot-size OCP-QPs "
+                         "instead of the centroidal headline; --batch problems per step")
     ap.add_argument("--allow-shared", action="store_true",
                     help="let ranks share a GPU (rehearsal on a one-GPU box); the line then says shared_gpu and n_gpus "
                          "counts distinct devices")
@@ -290,6 +438,9 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (the launcher started a different rank count)")
     if args.stub:
         stub_rank(args)
+        return
+    if args.ocp:
+        ocp_main(args)
         return
 
     import cheeta_mpc as cm

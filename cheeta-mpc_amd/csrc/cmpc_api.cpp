@@ -641,6 +641,7 @@ int cmpc_set_path(cmpc_ctx* c, int option, int value) {
   switch (option) {
     case CMPC_PATH_FUSED64:
       if (value && c->model.N > CMPC_C64_MAXN) return CMPC_ERR_ARG;  // the one-wave condensing holds N <= 21
+      if (!value && c->ric == 1) return CMPC_ERR_ARG;  // RICCATI = 1 runs on the fused path: set RICCATI first
       c->fused = value != 0;
       return CMPC_OK;
     case CMPC_PATH_FUSED128:
@@ -1220,6 +1221,6 @@ int cmpc_device_info(int* num_cu, int* clock_khz, char* arch, int arch_len) {
 
 // CMPC_SRC_HASH: sha256 prefix of every source, header and build file of libcmpc.so, written by the Makefile
 // (build/src_hash.h), so a bench line or test log names the exact source it ran
-const char* cmpc_version(void) { return "cheeta-mpc-amd 0.3.0 (gfx950) src " CMPC_SRC_HASH; }
+const char* cmpc_version(void) { return "cheeta-mpc-amd 0.4.0 (gfx950) src " CMPC_SRC_HASH; }
 
 }  // extern "C"

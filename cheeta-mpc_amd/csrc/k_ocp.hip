@@ -10,8 +10,9 @@
 //       M = [B A rb; 0 0 1]' [P p; p' 0] [B A rb; 0 0 1] + [R~ S~' g_u; S~ Q~ g_x; g_u' g_x' 0] + Gc' Sigma Gc
 //     (rows/columns u | x | rhs) is formed in a register tile (16 x 16 threads, each an R x R cyclic tile) and the
 //     u block is eliminated by nu_k Gauss-Jordan sweep steps (one workgroup barrier each): the swept matrix holds
-//     -Minv = -(R~ + B'PB)^-1, -K = Minv M_ux, P_k = M_xx - M_xu Minv M_ux, -kff and p_k at once; P_k, p_k stay in
-//     LDS for the next stage, whose data was prefetched into registers during the sweep;
+//     K = -M_uu^-1 M_ux, P_k = M_xx - M_xu M_uu^-1 M_ux, kff and p_k at once, and the pivot columns are the LDL'
+//     factor of M_uu (kept: the corrector's feedforward and HPIPM's ric_Lr come from it by triangular solves);
+//     P_k, p_k stay in LDS for the next stage, whose data was prefetched into registers during the sweep;
 //   - everything else is stage-parallel (residuals, right-hand sides, A + B K, the row directions) except two cheap
 //     serial nx x nx matrix-vector chains (forward dx_{k+1} = (A + BK) dx_k + bcl_k; backward
 //     p_k = (A + BK)' p_{k+1} + h_k for the corrector's right-hand side).
@@ -111,8 +112,8 @@ struct View {
   __device__ double* P(int k) const { return ws + L.o_P + (long long)k * L.nx * L.nx; }
   __device__ double* pv() const { return ws + L.o_pv; }
   __device__ double* K(int k) const { return ws + L.o_K + L.cK[k]; }
-  __device__ double* Mi(int k) const { return ws + L.o_Mi + L.cM[k]; }
   __device__ double* kf() const { return ws + L.o_kf; }
+  __device__ double* Lf(int k) const { return ws + L.o_Lf + L.cM[k]; }
   __device__ double* Acl(int k) const { return ws + L.o_Acl + (long long)k * L.nx * L.nx; }
   __device__ double* h() const { return ws + L.o_h; }
   __device__ double* y() const { return ws + L.o_y; }
@@ -326,7 +327,7 @@ struct StagePrefetch {
 };
 
 // Backward factorisation of the barrier-weighted Newton matrix with the right-hand side (gu, gx, rb) of ws.
-// Writes P_k, pv_k (k = 0..N), K_k, Minv_k, kf_k (k = 0..N-1). Returns false on a NaN pivot.
+// Writes P_k, pv_k (k = 0..N), K_k, kf_k and the LDL' columns Lf_k (k = 0..N-1). Returns false on a NaN pivot.
 template <int NZP>
 __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double reg) {
   constexpr int R = NZP / 16;
@@ -453,11 +454,14 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
         for (int a = 0; a < R; ++a) S.col[ti + 16 * a] = m[a][0];
       }
       __syncthreads();
+      double* Lf = V.Lf(k);
       for (int j = 0; j < mk; ++j) {
         const double* cb = S.col + (j & 1) * NZP;
         const double d = cb[j];
         bad = bad || (d != d);
         const double dinv = d > 1e-200 ? 1.0 / d : 0.0;
+        // the pivot column of the Schur complement is column j of L D (the LDL' factor of M_uu) for rows j..mk-1
+        if (tid >= j && tid < mk) Lf[(long long)j * mk + tid] = cb[tid];
         double ci[R], cl[R];
 #pragma unroll
         for (int a = 0; a < R; ++a) {
@@ -522,7 +526,6 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
     // --- outputs ---
     {
       double* Kk = V.K(k);
-      double* Mk = V.Mi(k);
       double* kf = V.kf() + L.cu[k];
       double* Pk = V.P(k);
       double* pk = V.pv() + (long long)k * nx;
@@ -533,8 +536,7 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
           const int i = ti + 16 * a, l = tj + 16 * b;
           const double v = m[a][b];
           if (i < mk) {
-            if (l < mk) Mk[(long long)l * mk + i] = -v;
-            else if (l < nz) Kk[(long long)(l - mk) * mk + i] = -v;
+            if (l >= mk && l < nz) Kk[(long long)(l - mk) * mk + i] = -v;
             else if (l == nz) kf[i] = -v;
           } else if (i < nz) {
             if (l >= mk && l < nz) {
@@ -672,8 +674,31 @@ __device__ __forceinline__ double post_pass(const View& V) {
   return amax;
 }
 
+// x = -M_uu^{-1} z from the sweep's LDL' columns F (column j holds d_j l_j on rows j..m-1; d_j = F[j][j]), with
+// the sweep's guard (1/d -> 0 for d <= 1e-200). Triangular solves keep the IPM's benign ill-conditioning benign:
+// an explicit inverse applied to z does not (its error grows with the barrier's Sigma and stalls the iteration).
+__device__ __forceinline__ void ldl_solve(const double* __restrict__ F, int m, const double* __restrict__ z,
+                                          double* __restrict__ x) {
+  for (int i = 0; i < m; ++i) x[i] = z[i];
+  for (int j = 0; j < m; ++j) {  // L D y = z, then y /= d
+    const double d = F[(long long)j * m + j];
+    const double dinv = d > 1e-200 ? 1.0 / d : 0.0;
+    const double yj = x[j] * dinv;
+    for (int i = j + 1; i < m; ++i) x[i] = fma(-F[(long long)j * m + i], yj, x[i]);
+    x[j] = yj;
+  }
+  for (int j = m - 1; j >= 0; --j) {  // L' x = y
+    const double d = F[(long long)j * m + j];
+    const double dinv = d > 1e-200 ? 1.0 / d : 0.0;
+    double s = x[j];
+    for (int i = j + 1; i < m; ++i) s = fma(-F[(long long)j * m + i] * dinv, x[i], s);
+    x[j] = s;
+  }
+  for (int i = 0; i < m; ++i) x[i] = -x[i];
+}
+
 // Corrector's backward vector pass with the factorisation kept: y_k = P_{k+1} rb_k; h_k = g_x,k + K_k' g_u,k +
-// Acl_k' y_k; p_N = g_x,N, p_k = Acl_k' p_{k+1} + h_k (serial, k = N-1..1); kf_k = -Minv_k (g_u,k + B_k'(y_k + p_{k+1}))
+// Acl_k' y_k; p_N = g_x,N, p_k = Acl_k' p_{k+1} + h_k (serial, k = N-1..1); kf_k = -M_uu,k^{-1} (g_u,k + B_k'(y_k + p_{k+1})) by the LDL' factors
 __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
@@ -738,7 +763,7 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     }
     __syncthreads();
   }
-  // z_k = g_u + B'(y_k + p_{k+1}) into du (scratch), then kf = -Minv z
+  // z_k = g_u + B'(y_k + p_{k+1}) into du (scratch), then kf = -M_uu^{-1} z
   double* z = V.du();
   for (int it = tid; it < L.nU; it += NT) {
     const int k = L.ustage[it], a = it - L.cu[k];
@@ -749,13 +774,7 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     z[it] = s;
   }
   __syncthreads();
-  for (int it = tid; it < L.nU; it += NT) {
-    const int k = L.ustage[it], a = it - L.cu[k], mk = L.nu[k];
-    const double* Mk = V.Mi(k);
-    double s = 0.0;
-    for (int b = 0; b < mk; ++b) s = fma(Mk[(long long)b * mk + a], z[L.cu[k] + b], s);
-    V.kf()[it] = -s;
-  }
+  for (int k = tid; k < N; k += NT) ldl_solve(V.Lf(k), L.nu[k], z + L.cu[k], V.kf() + L.cu[k]);
 }
 
 // (l_l - l_u) into R_W
@@ -1010,9 +1029,20 @@ __global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
                   oM = (long long)q * (L.nM > 0 ? L.nM : 1);
   const double* x = V.x();
   const double* u = V.u();
-  // stages k >= 1: K, Minv, k = u - K x + kf, P, p = pi_{k-1} - P x + pv
+  // stages k >= 1: K, k = u - K x + kf, P, p = pi_{k-1} - P x + pv
   for (int it = tid; it < L.nK; it += NT) r.K[oK + it] = V.ws[L.o_K + it];
-  for (int it = tid; it < L.nM; it += NT) r.Minv[oM + it] = V.ws[L.o_Mi + it];
+  // Lr_k (HPIPM's ric_Lr): from the sweep's LDL' columns F (d_j = F(j, j)), Lr(i, j) = F(i, j) / sqrt(d_j) for i >= j,
+  // 0 above the diagonal and in a guarded pivot's column
+  for (int k = 0; k < N; ++k) {
+    const int mk = L.nu[k];
+    const double* F = V.Lf(k);
+    double* Lo = r.Lr + oM + L.cM[k];
+    for (int e = tid; e < mk * mk; e += NT) {
+      const int j = e / mk, i = e % mk;
+      const double d = F[(long long)j * mk + j];
+      Lo[e] = (i >= j && d > 1e-200) ? F[e] / sqrt(d) : 0.0;
+    }
+  }
   for (int it = tid; it < L.nU; it += NT) {
     const int k = L.ustage[it], a2 = it - L.cu[k], mk = L.nu[k];
     if (k == 0) continue;
@@ -1030,9 +1060,10 @@ __global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
     r.p[op + (long long)k * nx + i] = s;
   }
   __syncthreads();
-  // stage 0, the reference's reconstruction (HpipmInterface.cpp:330-455) from P_1, p_1, Minv_0 and the stage-0 record:
-  // PA = P_1 A_0, v = p_1 + P_1 b_0, Mux = S_0 + B_0'PA, gr = r_0 + B_0'v, K_0 = -Minv_0 Mux, k_0 = -Minv_0 gr,
-  // P_0 = Q_0 + A_0'PA + Mux'K_0, p_0 = q_0 + A_0'v + K_0'gr. LDS: PA [nx][nx] in ABx, Mux [m0][nx] in Tx, v, gr.
+  // stage 0, the reference's reconstruction (HpipmInterface.cpp:334-347, 376-389, 416-453) from P_1, p_1, Lr_0 and the
+  // stage-0 record: PA = P_1 A_0, v = p_1 + P_1 b_0, Mux = S_0 + B_0'PA, gr = r_0 + B_0'v, T1 = Lr_0^-1 Mux,
+  // t2 = Lr_0^-1 gr, K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2, P_0 = Q_0 + A_0'PA - T1'T1, p_0 = q_0 + A_0'v - T1't2.
+  // LDS: PA [nx][nx] in ABx, Mux / T1 [m0][nx] in Tx, v, gr / t2.
   {
     const int m0 = L.nu[0];
     const double* P1 = r.P + oP + (long long)nx * nx;
@@ -1069,34 +1100,40 @@ __global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
       }
     }
     __syncthreads();
-    const double* Mi0 = V.Mi(0);
-    for (int e = tid; e < m0 * nx + m0; e += NT) {
-      if (e < m0 * nx) {
-        const int j = e / m0, a2 = e % m0;  // K_0 (a2, j) column-major
-        double s = 0.0;
-        for (int b = 0; b < m0; ++b) s = fma(-Mi0[(long long)b * m0 + a2], Mux[b * nx + j], s);
-        r.K[oK + (long long)j * m0 + a2] = s;
-      } else {
-        const int a2 = e - m0 * nx;
-        double s = 0.0;
-        for (int b = 0; b < m0; ++b) s = fma(-Mi0[(long long)b * m0 + a2], gr[b], s);
-        r.k[ok2 + a2] = s;
+    // T1 = Lr_0^-1 Mux (in place, Tx), t2 = Lr_0^-1 gr (in place); K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2 (in place in
+    // the outputs); one thread per right-hand side, the factor's guarded pivots (diag 0) contributing 0 as in HPIPM
+    const double* Lr0 = r.Lr + oM;
+    for (int j = tid; j <= nx; j += NT) {
+      double* c = j < nx ? Mux + j : gr;
+      const int cs = j < nx ? nx : 1;
+      double* o = j < nx ? r.K + oK + (long long)j * m0 : r.k + ok2;
+      for (int a2 = 0; a2 < m0; ++a2) {
+        double s = c[a2 * cs];
+        for (int b = 0; b < a2; ++b) s = fma(-Lr0[(long long)b * m0 + a2], c[b * cs], s);
+        const double d = Lr0[(long long)a2 * m0 + a2];
+        c[a2 * cs] = d > 0.0 ? s / d : 0.0;
       }
+      for (int a2 = m0 - 1; a2 >= 0; --a2) {
+        double s = c[a2 * cs];
+        for (int b = a2 + 1; b < m0; ++b) s = fma(-Lr0[(long long)a2 * m0 + b], o[b], s);
+        const double d = Lr0[(long long)a2 * m0 + a2];
+        o[a2] = d > 0.0 ? s / d : 0.0;
+      }
+      for (int a2 = 0; a2 < m0; ++a2) o[a2] = -o[a2];
     }
-    __syncthreads();  // K_0 (global, this workgroup's writes) read back below
-    const double* K0 = r.K + oK;
+    __syncthreads();
     for (int e = tid; e < nx * nx + nx; e += NT) {
       if (e < nx * nx) {
-        const int j = e / nx, i = e % nx;  // P_0 (i, j)
+        const int j = e / nx, i = e % nx;  // P_0 (i, j) = Q_0 + A_0'PA - T1'T1
         double s = V.Q(0)[(long long)j * nx + i];
         for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], PA[t * nx + j], s);
-        for (int a2 = 0; a2 < m0; ++a2) s = fma(Mux[a2 * nx + i], K0[(long long)j * m0 + a2], s);
+        for (int a2 = 0; a2 < m0; ++a2) s = fma(-Mux[a2 * nx + i], Mux[a2 * nx + j], s);
         r.P[oP + e] = s;
       } else {
-        const int i = e - nx * nx;
+        const int i = e - nx * nx;  // p_0 = q_0 + A_0'v - T1't2
         double s = V.q(0)[i];
         for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], v[t], s);
-        for (int a2 = 0; a2 < m0; ++a2) s = fma(K0[(long long)i * m0 + a2], gr[a2], s);
+        for (int a2 = 0; a2 < m0; ++a2) s = fma(-Mux[a2 * nx + i], gr[a2], s);
         r.p[op + i] = s;
       }
     }

@@ -28,7 +28,7 @@ struct OcpLayout {
   const int* cu;                 // [N+2] offsets of u_k in u
   const int* cr;                 // [N+2] offsets of node k's rows
   const int* cK;                 // [N+1] offsets of K_k (nu_k x nx, column-major)
-  const int* cM;                 // [N+1] offsets of Minv_k (nu_k x nu_k, column-major)
+  const int* cM;                 // [N+1] offsets of nu_k x nu_k blocks (Lf_k, Lr_k; column-major)
   const long long* orec;         // [N+1][8] record offsets: A, B, b (k < N), Q, S, R, q, r (k <= N)
   const long long* ocon;         // [N+1][4] constraint-record offsets: C, D, e, (pad)
   const int* ustage;             // [nU] stage of each input entry
@@ -36,8 +36,8 @@ struct OcpLayout {
   long long rec_size, crec_size;
   // workspace (doubles) per problem: stride and array offsets
   long long ws_stride;
-  long long o_x, o_u, o_pi, o_rgu, o_rgx, o_rb, o_gu, o_gx, o_du, o_dx, o_dpi, o_rows, o_P, o_pv, o_K, o_Mi, o_kf,
-      o_Acl, o_h, o_y, o_bcl;
+  long long o_x, o_u, o_pi, o_rgu, o_rgx, o_rb, o_gu, o_gx, o_du, o_dx, o_dpi, o_rows, o_P, o_pv, o_K, o_kf,
+      o_Lf, o_Acl, o_h, o_y, o_bcl;  // o_Lf: the u-block's LDL' columns per stage (nu_k x nu_k, column-major)
 };
 
 struct OcpSolveArgs {
@@ -58,10 +58,10 @@ struct OcpSolveArgs {
 };
 
 // Riccati quantities at the exit point of the last solve (cmpc_ocp_riccati): P [(N+1)][nx][nx], p [(N+1)][nx],
-// K [nK], k [nU], Minv [nM] per problem (column-major blocks), status [B].
+// K [nK], k [nU], Lr [nM] (HPIPM's ric_Lr, lower) per problem (column-major blocks), status [B].
 struct OcpRicArgs {
   OcpSolveArgs S;
-  double *P, *p, *K, *k, *Minv;
+  double *P, *p, *K, *k, *Lr;
   int* rstatus;
 };
 

@@ -26,7 +26,7 @@ struct cmpc_ocp {
   double *d_x0 = nullptr, *d_rec = nullptr, *d_crec = nullptr, *d_x = nullptr, *d_u = nullptr, *d_res = nullptr,
          *d_stats = nullptr;
   int *d_status = nullptr, *d_iters = nullptr, *d_rst = nullptr;
-  double *d_P = nullptr, *d_p = nullptr, *d_K = nullptr, *d_k = nullptr, *d_Mi = nullptr;
+  double *d_P = nullptr, *d_p = nullptr, *d_K = nullptr, *d_k = nullptr, *d_Lr = nullptr;
   hipStream_t stream = nullptr;
   // the last solve (for cmpc_ocp_riccati)
   int last_B = 0;
@@ -149,8 +149,8 @@ Dims build_dims(int N, int nx, const int* nu, const int* nc, OcpLayout& L, size_
   L.o_P = take(NP * nxx);
   L.o_pv = take(nX);
   L.o_K = take(nK);
-  L.o_Mi = take(nM);
   L.o_kf = take(nU);
+  L.o_Lf = take(nM);
   L.o_Acl = take((long long)N * nxx);
   L.o_h = take(nX);
   L.o_y = take(nP);
@@ -167,7 +167,7 @@ size_t vbytes(const std::vector<T>& v) {
 void free_all(cmpc_ocp* o) {
   for (void* p : {(void*)o->d_dims, (void*)o->d_ws, (void*)o->d_x0, (void*)o->d_rec, (void*)o->d_crec, (void*)o->d_x,
                   (void*)o->d_u, (void*)o->d_res, (void*)o->d_stats, (void*)o->d_status, (void*)o->d_iters,
-                  (void*)o->d_rst, (void*)o->d_P, (void*)o->d_p, (void*)o->d_K, (void*)o->d_k, (void*)o->d_Mi})
+                  (void*)o->d_rst, (void*)o->d_P, (void*)o->d_p, (void*)o->d_K, (void*)o->d_k, (void*)o->d_Lr})
     if (p) (void)hipFree(p);
   if (o->stream) (void)hipStreamDestroy(o->stream);
 }
@@ -327,7 +327,7 @@ int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_sett
   ck(hipMalloc((void**)&o->d_p, sizeof(double) * B * NP * nx));
   ck(hipMalloc((void**)&o->d_K, sizeof(double) * B * (size_t)std::max(o->L.nK, 1)));
   ck(hipMalloc((void**)&o->d_k, sizeof(double) * B * (size_t)std::max(o->nU, 1)));
-  ck(hipMalloc((void**)&o->d_Mi, sizeof(double) * B * (size_t)std::max(o->L.nM, 1)));
+  ck(hipMalloc((void**)&o->d_Lr, sizeof(double) * B * (size_t)std::max(o->L.nM, 1)));
   if (r == CMPC_OK) r = alloc_stats(o);
   if (r == CMPC_OK) ck(hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking));
   if (r != CMPC_OK) {
@@ -393,7 +393,7 @@ int cmpc_ocp_solve_host(cmpc_ocp* o, int B, const double* x0, const double* rec,
   return r;
 }
 
-int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, double* d_k, double* d_Minv,
+int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, double* d_k, double* d_Lr_out,
                      int* d_status, void* stream) {
   if (!o || B <= 0 || B > o->last_B || !d_P || !d_p || !d_status || (o->nU > 0 && (!d_K || !d_k)) ||
       !o->last_rec || !o->last_status)
@@ -404,16 +404,16 @@ int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, 
   a.p = d_p;
   a.K = o->nU > 0 ? d_K : o->d_K;
   a.k = o->nU > 0 ? d_k : o->d_k;
-  a.Minv = d_Minv ? d_Minv : o->d_Mi;
+  a.Lr = d_Lr_out ? d_Lr_out : o->d_Lr;
   a.rstatus = d_status;
   return cmpc::launch_ocp_ric(a, B, (hipStream_t)stream) == 0 ? CMPC_OK : CMPC_ERR_HIP;
 }
 
-int cmpc_ocp_riccati_host(cmpc_ocp* o, int B, double* P, double* p, double* K, double* k, double* Minv,
+int cmpc_ocp_riccati_host(cmpc_ocp* o, int B, double* P, double* p, double* K, double* k, double* Lr,
                           int* status) {
   if (!o || B <= 0 || B > o->last_B || !P || !p || !status || (o->nU > 0 && (!K || !k))) return CMPC_ERR_ARG;
   hipStream_t st = o->stream;
-  int r = cmpc_ocp_riccati(o, B, o->d_P, o->d_p, o->d_K, o->d_k, o->d_Mi, o->d_rst, st);
+  int r = cmpc_ocp_riccati(o, B, o->d_P, o->d_p, o->d_K, o->d_k, o->d_Lr, o->d_rst, st);
   if (r != CMPC_OK) return r;
   const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx;
   auto ck = [&r](hipError_t e) {
@@ -425,7 +425,7 @@ int cmpc_ocp_riccati_host(cmpc_ocp* o, int B, double* P, double* p, double* K, d
     ck(hipMemcpyAsync(K, o->d_K, sizeof(double) * B * o->L.nK, hipMemcpyDeviceToHost, st));
     ck(hipMemcpyAsync(k, o->d_k, sizeof(double) * B * o->nU, hipMemcpyDeviceToHost, st));
   }
-  if (Minv && o->L.nM > 0) ck(hipMemcpyAsync(Minv, o->d_Mi, sizeof(double) * B * o->L.nM, hipMemcpyDeviceToHost, st));
+  if (Lr && o->L.nM > 0) ck(hipMemcpyAsync(Lr, o->d_Lr, sizeof(double) * B * o->L.nM, hipMemcpyDeviceToHost, st));
   ck(hipMemcpyAsync(status, o->d_rst, sizeof(int) * B, hipMemcpyDeviceToHost, st));
   ck(hipStreamSynchronize(st));
   return r;

@@ -181,6 +181,19 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
       }
       if (empty) atomicOr(&S.s_flag, 2);
     }
+    if (FEET && feet && tid < L) {  // a run from step 0 keeps the current foot at its nodes 1..e+1, inside the box
+      int ee = 0;
+      while (ee + 1 < N && S.s_e[(ee + 1) * L + tid]) ++ee;
+      const double lb[3] = {CMPC_STEP_LB_XY, CMPC_STEP_LB_XY, CMPC_STEP_LB_Z};
+      const double ub[3] = {CMPC_STEP_UB_XY, CMPC_STEP_UB_XY, CMPC_STEP_UB_Z};
+      bool out = false;
+      for (int j = 1; j <= ee + 1 && j <= N; ++j)
+        for (int d = 0; d < 3; ++d) {
+          const double v = (double)S.s_foot[tid * 3 + d] - (double)S.s_foot[(j * L + tid) * 3 + d];
+          out = out || v < lb[d] || v > ub[d];
+        }
+      if (out) atomicOr(&S.s_flag, 2);
+    }
   }
   if (tid < N) {
     int ns = 0, nf = 0;

@@ -179,9 +179,9 @@ class HpipmInterface::Impl {
       pv_.assign((size_t)(N + 1) * nx, 0.0);
       K_.assign((size_t)(nK > 0 ? nK : 1), 0.0);
       k_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
-      Mi_.assign((size_t)(nM > 0 ? nM : 1), 0.0);
+      Lr_.assign((size_t)(nM > 0 ? nM : 1), 0.0);
       int st = -1;
-      const int r = cmpc_ocp_riccati_host(ocp_, 1, Pm_.data(), pv_.data(), K_.data(), k_.data(), Mi_.data(), &st);
+      const int r = cmpc_ocp_riccati_host(ocp_, 1, Pm_.data(), pv_.data(), K_.data(), k_.data(), Lr_.data(), &st);
       if (r != CMPC_OK)
         throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
       if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati factorisation: NaN pivot");
@@ -344,21 +344,21 @@ class HpipmInterface::Impl {
     }
   }
 
-  // Stage 0 as the reference rebuilds it (HpipmInterface.cpp:334-347, :376-389, :416-453; x0 is not an HPIPM variable):
-  // with Minv_0 = (Lr_0 Lr_0')^-1 of the device factorisation (HPIPM's ric_Lr(0)), P_1, p_1 of node 1,
-  //   K_0 = -Minv_0 (S_0 + B_0'P_1 A_0), k_0 = -Minv_0 (r_0 + B_0'(p_1 + P_1 b_0)),
-  //   S_0 = Q_0 + A_0'P_1 A_0 - (S_0 + B_0'P_1 A_0)'Minv_0 (..), s_0 = q_0 + A_0'(p_1 + P_1 b_0) - (..)'Minv_0 (r_0 + ..).
-  // LinearAlgebra::setTriangularMinimumEigenvalues (ocs2_core, not in the reference tree) is not applied: Lr_0 is used
-  // only through Minv_0, whose pivots the device factorisation already guarded.
+  // Stage 0 as the reference rebuilds it (HpipmInterface.cpp:334-347, :376-389, :416-453; x0 is not an HPIPM
+  // variable), by triangular solves with Lr_0 of the device factorisation (HPIPM's ric_Lr(0)) and P_1, p_1 of node 1:
+  //   T1 = Lr_0^-1 (S_0 + B_0'P_1 A_0), t2 = Lr_0^-1 (r_0 + B_0'(p_1 + P_1 b_0)), K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2,
+  //   S_0 = Q_0 + A_0'P_1 A_0 - T1'T1, s_0 = q_0 + A_0'(p_1 + P_1 b_0) - T1't2.
+  // LinearAlgebra::setTriangularMinimumEigenvalues (ocs2_core, not in the reference tree) is not applied: the device
+  // factorisation already guards its pivots (a pivot <= 1e-200 gives a zero column, whose solves contribute 0).
   void stage0(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
     const Packed& p = last_;
     const int nx = p.nx, x0n = p.nxk[0], x1n = p.nxk[1], m = p.nu[0];
     const double* P1 = Pm_.data() + (size_t)nx * nx;  // padded, column-major
     const double* p1 = pv_.data() + nx;
-    const double* Mi = Mi_.data();                   // m x m column-major
+    const double* Lr = Lr_.data();                   // m x m column-major, lower
     auto A = [&](int i, int j) { return d0.dfdx.data()[(size_t)j * x1n + i]; };
     auto B = [&](int i, int a) { return d0.dfdu.data()[(size_t)a * x1n + i]; };
-    std::vector<double> PA((size_t)x1n * x0n), v((size_t)x1n), Mux((size_t)m * x0n), gr((size_t)m);
+    std::vector<double> PA((size_t)x1n * x0n), v((size_t)x1n), T1((size_t)m * x0n), t2((size_t)m);
     for (int i = 0; i < x1n; ++i) {
       for (int j = 0; j < x0n; ++j) {
         double s = 0.0;
@@ -373,36 +373,52 @@ class HpipmInterface::Impl {
       for (int j = 0; j < x0n; ++j) {
         double s = c0.dfdux.data()[(size_t)j * m + a];
         for (int t = 0; t < x1n; ++t) s += B(t, a) * PA[(size_t)t * x0n + j];
-        Mux[(size_t)a * x0n + j] = s;
+        T1[(size_t)a * x0n + j] = s;
       }
       double s = c0.dfdu.data()[a];
       for (int t = 0; t < x1n; ++t) s += B(t, a) * v[(size_t)t];
-      gr[(size_t)a] = s;
+      t2[(size_t)a] = s;
     }
+    auto L = [&](int i, int j) { return Lr[(size_t)j * m + i]; };
+    auto lsolve = [&](double* c, size_t cs) {  // c <- Lr^-1 c
+      for (int a = 0; a < m; ++a) {
+        double s = c[(size_t)a * cs];
+        for (int b = 0; b < a; ++b) s -= L(a, b) * c[(size_t)b * cs];
+        c[(size_t)a * cs] = L(a, a) > 0.0 ? s / L(a, a) : 0.0;
+      }
+    };
+    auto ltsolve = [&](double* c, size_t cs) {  // c <- Lr^-T c
+      for (int a = m - 1; a >= 0; --a) {
+        double s = c[(size_t)a * cs];
+        for (int b = a + 1; b < m; ++b) s -= L(b, a) * c[(size_t)b * cs];
+        c[(size_t)a * cs] = L(a, a) > 0.0 ? s / L(a, a) : 0.0;
+      }
+    };
     K0_.assign((size_t)m * x0n, 0.0);
     k0_.assign((size_t)m, 0.0);
-    for (int a = 0; a < m; ++a) {
-      for (int j = 0; j < x0n; ++j) {
-        double s = 0.0;
-        for (int b = 0; b < m; ++b) s -= Mi[(size_t)b * m + a] * Mux[(size_t)b * x0n + j];
-        K0_[(size_t)j * m + a] = s;
-      }
-      double s = 0.0;
-      for (int b = 0; b < m; ++b) s -= Mi[(size_t)b * m + a] * gr[(size_t)b];
-      k0_[(size_t)a] = s;
+    std::vector<double> col((size_t)m);
+    for (int j = 0; j < x0n; ++j) {
+      lsolve(T1.data() + j, (size_t)x0n);
+      for (int a = 0; a < m; ++a) col[(size_t)a] = T1[(size_t)a * x0n + j];
+      ltsolve(col.data(), 1);
+      for (int a = 0; a < m; ++a) K0_[(size_t)j * m + a] = -col[(size_t)a];
     }
+    lsolve(t2.data(), 1);
+    for (int a = 0; a < m; ++a) col[(size_t)a] = t2[(size_t)a];
+    ltsolve(col.data(), 1);
+    for (int a = 0; a < m; ++a) k0_[(size_t)a] = -col[(size_t)a];
     S0_.assign((size_t)x0n * x0n, 0.0);
     s0_.assign((size_t)x0n, 0.0);
     for (int i = 0; i < x0n; ++i) {
       for (int j = 0; j < x0n; ++j) {
         double s = c0.dfdxx.data()[(size_t)j * x0n + i];
         for (int t = 0; t < x1n; ++t) s += A(t, i) * PA[(size_t)t * x0n + j];
-        for (int a = 0; a < m; ++a) s += Mux[(size_t)a * x0n + i] * K0_[(size_t)j * m + a];
+        for (int a = 0; a < m; ++a) s -= T1[(size_t)a * x0n + i] * T1[(size_t)a * x0n + j];
         S0_[(size_t)j * x0n + i] = s;
       }
       double s = c0.dfdx.data()[i];
       for (int t = 0; t < x1n; ++t) s += A(t, i) * v[(size_t)t];
-      for (int a = 0; a < m; ++a) s += K0_[(size_t)i * m + a] * gr[(size_t)a];
+      for (int a = 0; a < m; ++a) s -= T1[(size_t)a * x0n + i] * t2[(size_t)a];
       s0_[(size_t)i] = s;
     }
   }
@@ -442,7 +458,7 @@ class HpipmInterface::Impl {
   std::vector<int> ocpNu_, ocpNc_;
   Packed last_;
   bool riccatiValid_ = false;
-  std::vector<double> xbuf_, ubuf_, Pm_, pv_, K_, k_, Mi_, K0_, k0_, S0_, s0_;
+  std::vector<double> xbuf_, ubuf_, Pm_, pv_, K_, k_, Lr_, K0_, k0_, S0_, s0_;
 };
 
 HpipmInterface::HpipmInterface(OcpSize s, const Settings& st) : pImpl_(new Impl(std::move(s), st)) {}

@@ -552,8 +552,8 @@ class OcpSolver:
                                   status.ptr, iters.ptr if iters is not None else None, stream), "cmpc_ocp_solve")
 
     def riccati(self, B):
-        """cmpc_ocp_riccati_host of the last solve: P [B,N+1,nx,nx], p [B,N+1,nx], K (B lists of nu_k x nx), k, Minv,
-        status [B]."""
+        """cmpc_ocp_riccati_host of the last solve: P [B,N+1,nx,nx], p [B,N+1,nx], K (B lists of nu_k x nx), k, Lr (HPIPM's
+        ric_Lr, lower), status [B]."""
         N, nx = self.N, self.nx
         P = np.zeros((B, (N + 1) * nx * nx))
         p = np.zeros((B, (N + 1) * nx))

@@ -70,8 +70,10 @@ enum cmpc_qp_status {
   CMPC_INVALID_CONTACT = 5,  /* a horizon step has no stance leg: reference throws "mpc table invalid"
                                 (CentroidalMPC.cpp:328-330) */
   CMPC_TOO_LARGE = 6,        /* condensed size exceeds what this build's kernels support */
-  CMPC_INFEASIBLE_STEP = 7   /* cmpc_nlp_solve_batch: the step box of a later stance run's foothold is empty
-                                (des_foot_pos varies over the run by more than the box, CentroidalMPC.cpp:196-198) */
+  CMPC_INFEASIBLE_STEP = 7   /* cmpc_nlp_solve_batch: the step box of CentroidalMPC.cpp:196-198 cannot be met: a
+                                later stance run's foothold box is empty (des_foot_pos varies over the run by more
+                                than the box), or a run from step 0 keeps the current foot (:165-167) outside the box
+                                around des_foot_pos at one of its nodes */
 };
 
 /* Foothold step box of the NLP (CentroidalMPC.cpp:30-31): step_lb <= foot_pos - des_foot_pos <= step_ub at every node
@@ -156,7 +158,7 @@ int cmpc_ctx_fused(const cmpc_ctx* ctx);
  *                       stage-wise kernel (Riccati Newton solves over the horizon, no condensing, HPIPM's method);
  *                       2: every cold-start QP is (one launch). Results agree with the condensed path to rounding,
  *                       not bit for bit (a different factorisation of the same Newton systems). Needs N <= 21; 1 needs
- *                       CMPC_PATH_FUSED64 = 1.
+ *                       CMPC_PATH_FUSED64 = 1, and CMPC_PATH_FUSED64 = 0 is refused while RICCATI is 1.
  *   CMPC_PATH_IPM72     1 (default): where the IPM runs as its own launch (warm starts, the SQP / NLP subproblems,
  *                       CMPC_PATH_FUSED64 = 0), QPs with 64 < n <= 72 (the NLP's trot subproblems at N = 10: 60 forces
  *                       and two to four foothold triples) are solved by a one-wave kernel on the bordered Newton system (Schur
@@ -325,15 +327,18 @@ int cmpc_ocp_solve_host(cmpc_ocp* ocp, int B, const double* x0, const double* re
  *   Sigma = lam_l / t_l + lam_u / t_u), k_k = u_k - K_k x_k + (Newton feedforward at the returned point, ~0), and
  *   p_k = pi_{k-1} - P_k x_k + (Newton cost-to-go gradient at the returned point), k >= 1: the absolute-form
  *   quantities of the Newton iterate, formed without the Sigma-sized cancellations of the absolute recursion;
- *   stage 0 as the reference rebuilds it from stage-0 data (HpipmInterface.cpp:334-347, :416-453; here the record's
- *   A_0, B_0, b_0, Q_0, S_0, R_0, q_0, r_0): K_0 = -Minv_0 (S_0 + B_0'P_1 A_0), k_0 = -Minv_0 (r_0 + B_0'(p_1 + P_1 b_0)),
- *   P_0, p_0 likewise, Minv_0 = (R~_0 + B_0'P_1 B_0)^-1 with the node-0 rows' weight (HPIPM's Lr_0).
+ *   stage 0 as the reference rebuilds it from stage-0 data by triangular solves with Lr_0 (HpipmInterface.cpp:334-347,
+ *   :376-389, :416-453; here the record's A_0, B_0, b_0, Q_0, S_0, R_0, q_0, r_0): T1 = Lr_0^-1 (S_0 + B_0'P_1 A_0),
+ *   t2 = Lr_0^-1 (r_0 + B_0'(p_1 + P_1 b_0)), K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2, P_0 = Q_0 + A_0'P_1 A_0 - T1'T1,
+ *   p_0 = q_0 + A_0'(p_1 + P_1 b_0) - T1't2.
  * Per problem, column-major: d_P [(N+1)][nx*nx], d_p [(N+1)][nx], d_K [sum nu_k*nx] (stage blocks nu_k x nx),
- * d_k [sum nu_k], d_Minv [sum nu_k^2] (may be NULL); d_status [B]: 0, or 3 (NaN in the factorisation / no solve).
+ * d_k [sum nu_k], d_Lr [sum nu_k^2] (HPIPM's ric_Lr, d_ocp_qp_ipm_get_ric_Lr: the lower Cholesky factor of
+ * R~ + B'PB + D'Sigma D, zero above the diagonal; may be NULL); d_status [B]: 0, or 3 (NaN in the factorisation / no
+ * solve).
  * Asynchronous on stream; overwrites the handle's factorisation workspace. */
-int cmpc_ocp_riccati(cmpc_ocp* ocp, int B, double* d_P, double* d_p, double* d_K, double* d_k, double* d_Minv,
+int cmpc_ocp_riccati(cmpc_ocp* ocp, int B, double* d_P, double* d_p, double* d_K, double* d_k, double* d_Lr,
                      int* d_status, void* stream);
-int cmpc_ocp_riccati_host(cmpc_ocp* ocp, int B, double* P, double* p, double* K, double* k, double* Minv,
+int cmpc_ocp_riccati_host(cmpc_ocp* ocp, int B, double* P, double* p, double* K, double* k, double* Lr,
                           int* status);
 /* Final residuals of the last solve, d_res [B][4] = (max |r_stat|, |r_eq|, |r_ineq|, max t lam) as
  * d_ocp_qp_ipm_get_max_res_stat / _eq / _ineq / _comp (HpipmInterface.cpp:478-485); per-iteration statistics

@@ -30,30 +30,25 @@ class HpipmInterface {
   explicit HpipmInterface(OcpSize ocpSize = OcpSize(), const Settings& settings = Settings());
   ~HpipmInterface();
   void resize(OcpSize ocpSize);
-  /* Solved on the device. constraints == nullptr: equality-free stages (cmpc_ocp_solve_batch_host); otherwise the
-   * rows C dx + D du + e = 0 are imposed as the reference's lg = ug rows (HpipmInterface.cpp:223-264) by
-   * cmpc_ocp_solve_batch_eq_host (x0-eliminated stage 0, redundant rows dropped, inconsistent rows -> INCONS_EQ,
-   * where HPIPM's interior point method would stop at MAX_ITER or MIN_STEP instead: status parity unpinned).
+  /* Solved on the device by the stage-wise OCP interior point method (cmpc_ocp_solve_host on the handle resize()
+   * created): HPIPM's Mehrotra predictor-corrector over a Riccati factorisation per iteration (x0 eliminated, the
+   * rows C dx + D du + e = 0 imposed as the reference's lg = ug rows, HpipmInterface.cpp:223-264). Settings are
+   * HPIPM's (iter_max, alpha_min, mu0, tol_*, reg_prim; HpipmInterfaceSettings.h); statuses follow it: SUCCESS,
+   * MAX_ITER, MIN_STEP (inconsistent rows end there, as in HPIPM), NAN_SOL.
    * The state dimension may change along the horizon (OcpSize::numStates[k], OcpSize.cpp:55-60): each node's state is
    * embedded in a zero-padded state of the largest dimension, whose padding never couples, and every output (state
    * trajectory, S_k, K_k) comes back in the node's own dimension.
-   * Settings::reg_prim is added to the input Hessians (and the state Hessians of nodes 1..N); the other settings
-   * parametrise an interior point method this direct solve does not run (HpipmInterfaceSettings.h).
-   * verbose: the reference's status line, iteration count, max residuals and statistics table (one row: the
-   * direct solve is iteration 0), residuals evaluated on the host from the returned trajectories. */
+   * verbose: the reference's status line, iteration count, max residuals and the per-iteration statistics table
+   * (cmpc_ocp_get_residuals / cmpc_ocp_get_stats). */
   hpipm_status solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dynamics,
                      std::vector<ScalarFunctionQuadraticApproximation>& cost,
                      std::vector<VectorFunctionLinearApproximation>* constraints, vector_array_t& stateTrajectory,
                      vector_array_t& inputTrajectory, bool verbose = false);
 
-  /* Riccati quantities of the previously solved problem (reference HpipmInterface.h:93-123, .cpp:330-455).
-   * Unconstrained solve: the device recursion cmpc_ocp_riccati_batch_host. Equality-constrained solve: the exact
-   * feedback of the constrained problem, which HPIPM's barrier-weighted recursion approaches at convergence: for
-   * every stage k the tail problem k..N is solved on the device as a batch of nx + 1 problems (x_k = 0 and the unit
-   * vectors; state-only rows of node k dropped, x_k being given there), so u_k = K_k x_k + k_k and the cost-to-go
-   * 1/2 x' S_k x + s_k' x follows from the tail trajectories' affine maps. The reference rebuilds stage 0 from
-   * (dynamics0, cost0) because HPIPM eliminates x0; here the recursion runs over stage 0 directly, so the arguments
-   * must equal the stage-0 data of the last solve (size-checked). Cost-to-go f is 0, as in the reference. */
+  /* Riccati quantities of the previously solved problem (reference HpipmInterface.h:93-123, .cpp:330-455):
+   * cmpc_ocp_riccati_host refactors at the returned point (HPIPM's barrier-weighted recursion at its exit) and gives
+   * S_k, s_k, K_k, k_k for k >= 1 and Minv_0; stage 0 is rebuilt from (dynamics0, cost0) with the reference's formulas,
+   * as HPIPM eliminates x0. Cost-to-go f is 0, as in the reference. */
   std::vector<ScalarFunctionQuadraticApproximation> getRiccatiCostToGo(const VectorFunctionLinearApproximation& dynamics0,
                                                                        const ScalarFunctionQuadraticApproximation& cost0);
   matrix_array_t getRiccatiFeedback(const VectorFunctionLinearApproximation& dynamics0,

@@ -1639,7 +1639,7 @@ void oracle_feet_table(const oracle_consts* c, const double* foot, const uint8_t
  * step k of its run on the L rows with dt e_d x f_bar_ik, and b_k gains -dt sum D x f_bar_ik. Cost: the condensed
  * state and force terms as oracle_condense_full_lin, plus 2 Wp cnt on the foothold diagonal and
  * 2 Wp sum_j (pbar - des_j) in g. Status INVALID_CONTACT / TOO_LARGE as oracle_condense_lin, INFEASIBLE_STEP when a
- * run's box is empty. */
+ * later run's box is empty or the current foot of a run from step 0 lies outside the box at one of its nodes. */
 int oracle_condense_feet(const oracle_consts* c, const double* x0, const double* xref, const double* foot,
                          const uint8_t* contact, const double* lin, const double* ubar, const double* D, int ld,
                          int* n_out, double* H, double* g, double* tri_mu, double* tri_lo, double* tri_hi,
@@ -1675,6 +1675,21 @@ int oracle_condense_feet(const oracle_consts* c, const double* x0, const double*
       if (!(flo[3 * t + d] <= fhi[3 * t + d])) {
         free(code);
         return CMPC_INFEASIBLE_STEP;
+      }
+  }
+  /* a run from step 0 keeps the current foot (node 0, pinned :165-167) at its nodes 1..e+1, each of which the step box
+   * of :196-198 also bounds: a current foot outside it makes the reference NLP infeasible */
+  for (int i = 0; i < L; ++i) {
+    if (!contact[i]) continue;
+    int e = 0;
+    while (e + 1 < N && contact[(e + 1) * L + i]) ++e;
+    for (int j = 1; j <= e + 1 && j <= N; ++j)
+      for (int d = 0; d < 3; ++d) {
+        const double v = foot[(size_t)i * 3 + d] - foot[((size_t)j * L + i) * 3 + d];
+        if (v < STEP_LB[d] || v > STEP_UB[d]) {
+          free(code);
+          return CMPC_INFEASIBLE_STEP;
+        }
       }
   }
   /* dynamics at the iterate: the force columns' lever arm pbar + D (a foot table whose later-run nodes hold it) */

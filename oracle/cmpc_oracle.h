@@ -154,13 +154,18 @@ int oracle_ocp_riccati(int N, int nx, const int* nu, const double* rec, double* 
  * (node 0 = x0), u [sum nu_k]; res[4] = max |r_stat|, |r_eq|, |r_ineq|, max t lam at exit; stats [rows][10] as
  * cmpc_enable_stats (res_eq now the dynamics residual). ric (optional): Riccati quantities of the last factorisation
  * with the vector part in absolute form (see ocp_ipm.c), all column-major: P [(N+1)][nx][nx], p [(N+1)][nx],
- * K [sum nu_k nx] (stage blocks nu_k x nx), k [sum nu_k], Minv [sum nu_k^2] ((R~ + B'PB)^-1, may be NULL). */
+ * K [sum nu_k nx] (stage blocks nu_k x nx), k [sum nu_k], Lr [sum nu_k^2] (HPIPM's ric_Lr: the lower
+ * Cholesky factor of R~ + B'PB + D'Sigma D, column-major, may be NULL). */
 typedef struct oracle_ocp_ric {
-  double *P, *p, *K, *k, *Minv;
+  double *P, *p, *K, *k, *Lr;
 } oracle_ocp_ric;
 int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
                    const double* crec, const cmpc_settings* s, double* x, double* u, int* iters, double* res,
                    oracle_ocp_ric* ric, double* stats, int stats_rows);
+/* Batch of B problems of the same dimensions over nthreads pthreads (bench.py's cpu_baseline for the OCP path). */
+int oracle_ocp_ipm_batch(int B, int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
+                         size_t rec_size, const double* crec, size_t crec_size, const cmpc_settings* s, double* x,
+                         double* u, int* status, int* iters, int nthreads);
 /* The cold start's first (predictor) Newton step, with the system's data for a dense cross-check. */
 int oracle_ocp_first_step(int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
                           const double* crec, const cmpc_settings* s, double* du, double* dx, double* dpi,

@@ -591,9 +591,10 @@ int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0
    *   K_k = -Lr^-T Ls',  k_k = u_k - K_k x_k + kff_k(step),  p_k = pi_{k-1} - P_k x_k + p_k(step)   (k >= 1),
    * the absolute-form feedforward and cost-to-go gradient of the Newton iterate evaluated without the Sigma-sized
    * cancellations of the absolute recursion (for equality rows Sigma reaches 1e10+). Stage 0 follows the reference's
-   * own reconstruction from the stage-0 data (record's A_0, B_0, b_0, Q_0, S_0, R_0, q_0, r_0) and Minv_0:
-   *   K_0 = -Minv_0 (S_0 + B_0'P_1 A_0), v = p_1 + P_1 b_0, k_0 = -Minv_0 (r_0 + B_0'v),
-   *   P_0 = Q_0 + A_0'P_1 A_0 + (S_0 + B_0'P_1 A_0)'K_0,  p_0 = q_0 + A_0'v + K_0'(r_0 + B_0'v). */
+   * own reconstruction (HpipmInterface.cpp:334-347, 376-389, 416-453) from the stage-0 data (record's A_0, B_0, b_0,
+   * Q_0, S_0, R_0, q_0, r_0) and the factor Lr_0, by triangular solves as there:
+   *   T1 = Lr_0^-1 (S_0 + B_0'P_1 A_0), v = p_1 + P_1 b_0, t2 = Lr_0^-1 (r_0 + B_0'v), K_0 = -Lr_0^-T T1,
+   *   k_0 = -Lr_0^-T t2, P_0 = Q_0 + A_0'P_1 A_0 - T1'T1, p_0 = q_0 + A_0'v - T1't2. */
   (void)factored;
   if (ric && status != CMPC_NAN_SOL) {
     for (int j = 0; j < m; ++j) sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
@@ -618,15 +619,9 @@ int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0
         ltsolve(mk, Lr, iLd, col);
         for (int a = 0; a < mk; ++a) CM(Kk, mk, a, j) = col[a];
       }
-      double* Mi = ric->Minv ? ric->Minv + p.oMi[k] : NULL;
-      double mloc[64 * 64];
-      if (!Mi) Mi = mloc;
-      for (int b = 0; b < mk; ++b) { /* (Lr Lr')^-1 e_b */
-        for (int a = 0; a < mk; ++a) col[a] = a == b ? 1.0 : 0.0;
-        lsolve(mk, Lr, iLd, col);
-        ltsolve(mk, Lr, iLd, col);
-        for (int a = 0; a < mk; ++a) CM(Mi, mk, a, b) = col[a];
-      }
+      if (ric->Lr) /* HPIPM's ric_Lr: lower Cholesky factor, column-major out */
+        for (int b = 0; b < mk; ++b)
+          for (int a = 0; a < mk; ++a) CM(ric->Lr + p.oMi[k], mk, a, b) = Lr[a * mk + b];
       if (k >= 1) {
         for (int a = 0; a < mk; ++a) col[a] = -F.l[p.cu[k] + a];
         ltsolve(mk, Lr, iLd, col); /* step feedforward */
@@ -659,7 +654,6 @@ int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0
       const double* r0 = rec + p.or_[0];
       const double* P1 = ric->P + (size_t)nx * nx; /* column-major, symmetric */
       const double* p1 = ric->p + nx;
-      const double* Mi = ric->Minv ? ric->Minv : NULL;
       double* PA = wk;                       /* nx x nx row-major: P_1 A_0 */
       double* Mux = PA + (size_t)nx * nx;    /* m0 x nx row-major */
       double v[64], gr[64];
@@ -673,16 +667,8 @@ int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0
         for (int t = 0; t < nx; ++t) sacc += CM(P1, nx, i, t) * bv[t];
         v[i] = sacc;
       }
-      double mloc[64 * 64];
-      if (!Mi) { /* Minv_0 not requested: recompute from the factorisation */
-        for (int b = 0; b < m0; ++b) {
-          for (int a = 0; a < m0; ++a) col[a] = a == b ? 1.0 : 0.0;
-          lsolve(m0, F.Lr, F.iLd, col);
-          ltsolve(m0, F.Lr, F.iLd, col);
-          for (int a = 0; a < m0; ++a) CM(mloc, m0, a, b) = col[a];
-        }
-        Mi = mloc;
-      }
+      double* T1 = Mux + (size_t)64 * nx; /* m0 x nx row-major: Lr_0^-1 Mux */
+      double t2[64];
       for (int a = 0; a < m0; ++a) {
         for (int j = 0; j < nx; ++j) {
           double sacc = CM(S, m0, a, j);
@@ -693,26 +679,28 @@ int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0
         for (int t = 0; t < nx; ++t) sacc += CM(Bm, nx, t, a) * v[t];
         gr[a] = sacc;
       }
-      for (int a = 0; a < m0; ++a) {
-        for (int j = 0; j < nx; ++j) {
-          double sacc = 0.0;
-          for (int b = 0; b < m0; ++b) sacc -= CM(Mi, m0, a, b) * Mux[b * nx + j];
-          CM(ric->K, m0, a, j) = sacc;
-        }
-        double sacc = 0.0;
-        for (int b = 0; b < m0; ++b) sacc -= CM(Mi, m0, a, b) * gr[b];
-        ric->k[a] = sacc;
+      for (int j = 0; j < nx; ++j) { /* T1 = Lr^-1 Mux, K_0 = -Lr^-T T1 */
+        for (int a = 0; a < m0; ++a) col[a] = Mux[a * nx + j];
+        lsolve(m0, F.Lr, F.iLd, col);
+        for (int a = 0; a < m0; ++a) T1[a * nx + j] = col[a];
+        ltsolve(m0, F.Lr, F.iLd, col);
+        for (int a = 0; a < m0; ++a) CM(ric->K, m0, a, j) = -col[a];
       }
-      for (int i = 0; i < nx; ++i) {
+      for (int a = 0; a < m0; ++a) t2[a] = gr[a];
+      lsolve(m0, F.Lr, F.iLd, t2);
+      for (int a = 0; a < m0; ++a) col[a] = t2[a];
+      ltsolve(m0, F.Lr, F.iLd, col);
+      for (int a = 0; a < m0; ++a) ric->k[a] = -col[a];
+      for (int i = 0; i < nx; ++i) { /* P_0 = Q_0 + A_0'PA - T1'T1, p_0 = q_0 + A_0'v - T1't2 */
         for (int j = 0; j < nx; ++j) {
           double sacc = CM(Q, nx, i, j);
           for (int t = 0; t < nx; ++t) sacc += CM(A, nx, t, i) * PA[t * nx + j];
-          for (int a = 0; a < m0; ++a) sacc += Mux[a * nx + i] * CM(ric->K, m0, a, j);
+          for (int a = 0; a < m0; ++a) sacc -= T1[a * nx + i] * T1[a * nx + j];
           CM(ric->P, nx, i, j) = sacc;
         }
         double sacc = q0[i];
         for (int t = 0; t < nx; ++t) sacc += CM(A, nx, t, i) * v[t];
-        for (int a = 0; a < m0; ++a) sacc += CM(ric->K, m0, a, i) * gr[a];
+        for (int a = 0; a < m0; ++a) sacc -= T1[a * nx + i] * t2[a];
         ric->p[i] = sacc;
       }
     }
@@ -808,4 +796,52 @@ int oracle_ocp_first_step(int N, int nx, const int* nu, const int* nc, const dou
   free(buf);
   prob_free(&p);
   return st;
+}
+
+/* Batch over problems with nthreads pthreads (bench.py's OCP cpu_baseline): problem b has x0 + b nx, rec + b rec_size,
+ * crec + b crec_size; outputs x [b][(N+1) nx], u [b][nU], status / iters [b]. */
+#include <pthread.h>
+typedef struct ocp_batch_job {
+  int N, nx, B, next_stride;
+  const int *nu, *nc;
+  const double *x0, *rec, *crec;
+  size_t rs, cs;
+  const cmpc_settings* s;
+  double *x, *u;
+  int *status, *iters;
+  int nU, b0, b1;
+} ocp_batch_job;
+
+static void* ocp_batch_worker(void* arg) {
+  ocp_batch_job* j = (ocp_batch_job*)arg;
+  for (int b = j->b0; b < j->b1; ++b)
+    j->status[b] = oracle_ocp_ipm(j->N, j->nx, j->nu, j->nc, j->x0 + (size_t)b * j->nx, j->rec + (size_t)b * j->rs,
+                                  j->crec ? j->crec + (size_t)b * j->cs : NULL, j->s,
+                                  j->x + (size_t)b * (j->N + 1) * j->nx, j->u + (size_t)b * (j->nU ? j->nU : 1),
+                                  j->iters + b, NULL, NULL, NULL, 0);
+  return NULL;
+}
+
+int oracle_ocp_ipm_batch(int B, int N, int nx, const int* nu, const int* nc, const double* x0, const double* rec,
+                         size_t rec_size, const double* crec, size_t crec_size, const cmpc_settings* s, double* x,
+                         double* u, int* status, int* iters, int nthreads) {
+  int nU = 0;
+  for (int k = 0; k < N; ++k) nU += nu[k];
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > B) nthreads = B;
+  pthread_t th[256];
+  ocp_batch_job jobs[256];
+  if (nthreads > 256) nthreads = 256;
+  for (int t = 0; t < nthreads; ++t) {
+    ocp_batch_job j = {N, nx, B, 0, nu, nc, x0, rec, crec, rec_size, crec_size, s, x, u, status, iters, nU,
+                       (int)((long)B * t / nthreads), (int)((long)B * (t + 1) / nthreads)};
+    jobs[t] = j;
+  }
+  if (nthreads == 1) {
+    ocp_batch_worker(&jobs[0]);
+    return 0;
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, ocp_batch_worker, &jobs[t]);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  return 0;
 }

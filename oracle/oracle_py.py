@@ -101,6 +101,8 @@ def lib():
         L.oracle_ocp_riccati.argtypes = [C.c_int, C.c_int, i, d, d, d, d, d]
         L.oracle_ocp_ipm.argtypes = [C.c_int, C.c_int, i, i, d, d, d, P(Settings), d, d, i, d, C.c_void_p, d,
                                      C.c_int]
+        L.oracle_ocp_ipm_batch.argtypes = [C.c_int, C.c_int, C.c_int, i, i, d, d, C.c_size_t, d, C.c_size_t,
+                                           P(Settings), d, d, i, i, C.c_int]
         L.oracle_ocp_first_step.argtypes = [C.c_int, C.c_int, i, i, d, d, d, P(Settings), d, d, d, d, d, d, d]
         L.oracle_gait_contact.argtypes = [C.c_void_p, i, C.c_double, C.c_double, C.c_double, C.c_int,
                                           C.POINTER(C.c_uint8)]
@@ -494,12 +496,12 @@ def ocp_riccati(N, nx, nu, rec):
 
 class OcpRic(C.Structure):
     _fields_ = [("P", C.POINTER(C.c_double)), ("p", C.POINTER(C.c_double)), ("K", C.POINTER(C.c_double)),
-                ("k", C.POINTER(C.c_double)), ("Minv", C.POINTER(C.c_double))]
+                ("k", C.POINTER(C.c_double)), ("Lr", C.POINTER(C.c_double))]
 
 
 def ocp_ipm(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, ric=False, stats_rows=0):
     """Stage-wise OCP IPM (oracle/ocp_ipm.c). Returns dict: x [(N+1),nx], u [nU], status, iters, res [4], and with
-    ric=True P [(N+1),nx,nx], p [(N+1),nx], K (list of nu_k x nx), k (list), Minv (list); stats [rows,10]."""
+    ric=True P [(N+1),nx,nx], p [(N+1),nx], K (list of nu_k x nx), k (list), Lr (list, lower); stats [rows,10]."""
     s = settings if settings is not None else default_settings()
     nua = np.asarray(list(nu) + [0], dtype=np.int32)
     nU = int(nua[:N].sum())
@@ -541,8 +543,31 @@ def ocp_ipm(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, ric=False, st
             o += m * nx
             om += m * m
             ok += m
-        out.update(P=P.reshape(N + 1, nx, nx).transpose(0, 2, 1).copy(), p=pv.reshape(N + 1, nx), K=Ks, k=ks, Minv=Ms)
+        out.update(P=P.reshape(N + 1, nx, nx).transpose(0, 2, 1).copy(), p=pv.reshape(N + 1, nx), K=Ks, k=ks, Lr=Ms)
     return out
+
+
+def ocp_ipm_batch(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, nthreads=1):
+    """oracle_ocp_ipm over a batch (x0 [B,nx], rec [B,rec_size], crec [B,crec_size]) on nthreads pthreads."""
+    s = settings if settings is not None else default_settings()
+    x0 = np.ascontiguousarray(x0, np.float64)
+    B = x0.shape[0]
+    rec = np.ascontiguousarray(rec, np.float64).reshape(B, -1)
+    nua = np.asarray(list(nu) + [0], dtype=np.int32)
+    nU = int(nua[:N].sum())
+    nca = None if nc is None else np.asarray(nc, dtype=np.int32)
+    cr = None if nca is None or int(nca.sum()) == 0 else np.ascontiguousarray(crec, np.float64).reshape(B, -1)
+    if cr is None:
+        nca = None
+    x = np.zeros((B, N + 1, nx))
+    u = np.zeros((B, max(nU, 1)))
+    st = np.zeros(B, np.int32)
+    it = np.zeros(B, np.int32)
+    lib().oracle_ocp_ipm_batch(B, N, nx, _p(nua, C.c_int), _p(nca, C.c_int) if nca is not None else None, _p(x0),
+                               _p(rec), rec.shape[1], _p(cr) if cr is not None else None,
+                               cr.shape[1] if cr is not None else 0, C.byref(s), _p(x), _p(u), _p(st, C.c_int),
+                               _p(it, C.c_int), int(nthreads))
+    return x, u[:, :nU], st, it
 
 
 def ocp_first_step(N, nx, nu, x0, rec, nc=None, crec=None, settings=None):

@@ -136,3 +136,26 @@ def test_path_option_constants_match_header():
     assert set(enum) == {"FUSED64", "FUSED128", "DIRECT", "RICCATI", "IPM72"}
     for k, v in enum.items():
         assert getattr(cheeta_mpc, "PATH_" + k) == v, k
+
+
+def test_status_strings_cover_every_code(cmh):
+    """cmpc_status_string names every cmpc_qp_status (INFEASIBLE_STEP printed as UNKNOWN) and the Python
+    table agrees."""
+    L = cmh.lib()
+    for code, name in cmh.STATUS.items():
+        assert L.cmpc_status_string(code).decode() == name
+    assert L.cmpc_status_string(7).decode() == "INFEASIBLE_STEP"
+
+
+@pytest.mark.gpu
+def test_fused64_off_refused_while_riccati_path_is_on(cm):
+    """CMPC_PATH_RICCATI = 1 runs on the fused path, so switching FUSED64 off under it is refused instead of
+    silently skipping the stage-wise kernel."""
+    eng = cm.Engine(cm.default_model(10), max_batch=8)
+    eng.set_path(cm.PATH_RICCATI, 1)
+    with pytest.raises(RuntimeError):
+        eng.set_path(cm.PATH_FUSED64, 0)
+    assert eng.get_path(cm.PATH_FUSED64) == 1 and eng.get_path(cm.PATH_RICCATI) == 1
+    eng.set_path(cm.PATH_RICCATI, 0)
+    eng.set_path(cm.PATH_FUSED64, 0)
+    assert eng.get_path(cm.PATH_FUSED64) == 0

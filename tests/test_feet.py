@@ -189,6 +189,36 @@ def test_empty_step_box_is_reported(op):
     assert stc == 7
 
 
+def _first_run_leg(contact):
+    """A leg in stance at step 0 and the last node of that run (e + 1)."""
+    N = contact.shape[0]
+    for i in range(NL):
+        if contact[0, i]:
+            e = 0
+            while e + 1 < N and contact[e + 1, i]:
+                e += 1
+            return i, min(e + 1, N)
+    return None
+
+
+def test_current_foot_outside_step_box_is_reported(op):
+    """the step box of CentroidalMPC.cpp:196-198 also binds the nodes of a stance run from step 0, where
+    foot_pos is pinned to the current foot (:165-167); a current foot 0.5 m off des_foot_pos there makes the reference
+    NLP infeasible: INFEASIBLE_STEP (oracle condensing and SQP)."""
+    N = 10
+    mo = op.default_model(N)
+    x0, xref, foot, contact = op.generate(mo, SEED, 1, gait=0)
+    i, j = _first_run_leg(contact[0])
+    foot2 = foot[0].copy()
+    foot2[j, i, 1] += 0.5  # des at a node of the first run, 0.5 m from the planted current foot
+    u, D, feet, x, st, qi, si = op.sqp_solve_feet(mo, op.default_settings(), x0[0], xref[0], foot2, contact[0])
+    assert st == 7
+    n, *_, stc = op.condense_feet(mo, x0[0], xref[0], foot2, contact[0], np.zeros((N, 6)), u, D)
+    assert stc == 7
+    u, D, feet, x, st, qi, si = op.sqp_solve_feet(mo, op.default_settings(), x0[0], xref[0], foot[0], contact[0])
+    assert st == 0
+
+
 # ------------------------------------------------------------------------------------------------ device (gpu)
 
 def rel_err(u, ur):
@@ -283,6 +313,11 @@ def test_device_nlp_empty_step_box(cm, op):
     eng = cm.Engine(m, precision=0, max_batch=B)
     u, feet, x, st, qi, si = eng.nlp_solve(x0, xref, foot, contact)
     assert st[1] == 7 and all(st[q] == 0 for q in (0, 2, 3))
+    # the current foot outside the box at a node of a run from step 0 (QP 2)
+    i, j = _first_run_leg(contact[2])
+    foot[2, j, i, 1] += 0.5
+    u, feet, x, st, qi, si = eng.nlp_solve(x0, xref, foot, contact)
+    assert st[1] == 7 and st[2] == 7 and all(st[q] == 0 for q in (0, 3))
 
 
 @pytest.mark.gpu

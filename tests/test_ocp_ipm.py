@@ -386,7 +386,7 @@ def test_device_inconsistent_rows_status(cm, op):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["small", "legged_projected", "legged_rows"])
 def test_device_riccati_matches_oracle(cm, op, case):
-    """cmpc_ocp_riccati vs the oracle's Riccati quantities (P, p, K, k, Minv per stage) at 1e-9; without rows also vs
+    """cmpc_ocp_riccati vs the oracle's Riccati quantities (P, p, K, k, Lr per stage) at 1e-9; without rows also vs
     the closed-form recursion of retrieveRiccati (testHpipmInterface.cpp:280-304) and u = K x + k."""
     if case == "small":
         ps = [_small(70 + i, rows=False) for i in range(3)]
@@ -395,7 +395,7 @@ def test_device_riccati_matches_oracle(cm, op, case):
     else:
         ps = [ocpgen.legged_problem(310 + i, projected=False) for i in range(3)]
     solver, x, u, st, it = _device_batch(cm, ps)
-    P, pv, K, kf, Mi, rst = solver.riccati(len(ps))
+    P, pv, K, kf, Lr, rst = solver.riccati(len(ps))
     assert np.all(rst == 0)
     for i, p in enumerate(ps):
         r = _oracle(op, p, ric=True)
@@ -406,7 +406,7 @@ def test_device_riccati_matches_oracle(cm, op, case):
         for k in range(N):
             assert _rel(K[i][k], r["K"][k]) < 1e-9, ("K", k)
             assert _rel(kf[i][k], r["k"][k]) < 1e-8, ("k", k)
-            assert _rel(Mi[i][k], r["Minv"][k]) < 1e-9, ("Minv", k)
+            assert _rel(Lr[i][k], r["Lr"][k]) < 1e-9, ("Lr", k)
         if p.get("nc") is None:
             Sm, sv, Kc, kc = _closed_form_riccati(p)
             us = _split(p, u[i])
