@@ -516,7 +516,7 @@ int cmpc_ocp_riccati_batch_host(int B, int N, int nx, const int* nu, const doubl
   if (r == CMPC_OK) r = cmpc_ocp_riccati_host(o, B, Sm, sv, K, kff, nullptr, status);
   if (r == CMPC_OK)
     for (int b = 0; b < B; ++b)
-      if (st[(size_t)b] == CMPC_NAN_SOL) status[b] = CMPC_NAN_SOL;
+      if (st[(size_t)b] != CMPC_SUCCESS) status[b] = st[(size_t)b];  // e.g. an indefinite stage: MAX_ITER
   cmpc_ocp_destroy(o);
   return r;
 }

@@ -307,14 +307,20 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
 #pragma unroll
   for (int p = 0; p < TPW; ++p) acc[p] = acc_t{T(0), T(0), T(0), T(0)};
   // this wave's lower tiles (slot p = tile wave + WAVES p, row-major lower order)
-  constexpr int TT = NMAX <= 128 ? TPW : 1;  // tile table (NMAX <= 128 only)
-  int tile_i[TT], tile_j[TT];
-  bool tile_ok[TT];
+  // tile table (NMAX <= 128 only), packed 8 bits per tile (ti | tj << 4, 15 = no tile) in TW words: unpacked at each
+  // use from an opaque copy, so the compiler cannot hoist 2 TPW tile addresses across the step loop (as unpacked
+  // per-tile registers they were spilled to scratch in k_solve128<float>)
+  constexpr int TT = NMAX <= 128 ? TPW : 1;
+  constexpr int TW = (TT + 3) / 4;
+  int tile_pk[TW];
+#pragma unroll
+  for (int w4 = 0; w4 < TW; ++w4) tile_pk[w4] = 0;
 #pragma unroll
   for (int p = 0; p < TT; ++p) {
     const int idx = wave + p * WAVES;
-    tile_ok[p] = idx < NLT;
-    tile_of(tile_ok[p] ? idx : 0, tile_i[p], tile_j[p]);
+    int ti = 15, tj = 15;
+    if (idx < NLT) tile_of(idx, ti, tj);
+    tile_pk[p >> 2] |= (ti | (tj << 4)) << (8 * (p & 3));
   }
 
   const T dt = T(M->dt);
@@ -420,9 +426,17 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
     //     class keeps tile-outer order: its 17 tiles per wave leave no registers for the tile table)
     const int ncols = S.s_cb[k];
     if constexpr (NMAX <= 128) {
+      int tpk[TW];
+#pragma unroll
+      for (int w4 = 0; w4 < TW; ++w4) {
+        tpk[w4] = tile_pk[w4];
+        asm volatile("" : "+v"(tpk[w4]));
+      }
+      auto tile_i = [&](int p) { return (tpk[p >> 2] >> (8 * (p & 3))) & 15; };
+      auto tile_j = [&](int p) { return (tpk[p >> 2] >> (8 * (p & 3) + 4)) & 15; };
       int np = 0;
 #pragma unroll
-      for (int p = 0; p < TPW; ++p) np += (tile_ok[p] && 16 * tile_i[p] < ncols) ? 1 : 0;
+      for (int p = 0; p < TPW; ++p) np += (tile_i(p) != 15 && 16 * tile_i(p) < ncols) ? 1 : 0;
       // K = 12: Bqp row 12 (g_z) is identically 0 and unweighted, rows 13..15 are padding
 #pragma unroll
       for (int s4 = 0; s4 < 3; ++s4) {
@@ -431,8 +445,8 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
 #pragma unroll
         for (int p = 0; p < TPW; ++p) {
           if (p < np) {
-            const T av = qs * S.s_G[buf][s][16 * tile_i[p] + (lane & 15)];
-            const T bv = S.s_G[buf][s][16 * tile_j[p] + (lane & 15)];
+            const T av = qs * S.s_G[buf][s][16 * tile_i(p) + (lane & 15)];
+            const T bv = S.s_G[buf][s][16 * tile_j(p) + (lane & 15)];
             acc[p] = MF::run(av, bv, acc[p]);
           }
         }

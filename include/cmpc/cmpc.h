@@ -355,7 +355,9 @@ int cmpc_ocp_get_stats_host(cmpc_ocp* ocp, int B, double* stats);
 /* One-shot host entry points (create, solve, destroy; kept from the 0.3 ABI): the equality-free problem
  * (cmpc_ocp_solve_batch_host), with rows (cmpc_ocp_solve_batch_eq_host; nc == NULL is CMPC_ERR_ARG), and its Riccati
  * quantities at x0 = 0 (cmpc_ocp_riccati_batch_host: Sm = P, sv = p, K, kff as cmpc_ocp_riccati, the recursion of
- * testHpipmInterface.cpp:280-304 with reg_prim on the Hessian diagonals; status 0 or 3). */
+ * testHpipmInterface.cpp:280-304 with reg_prim on the Hessian diagonals; status: the solve's when it did not succeed
+ * (an indefinite stage is no NaN: the guarded factorisation drops the direction, as BLASFEO's, and the IPM ends at
+ * MAX_ITER), else 0 or 3 from the factorisation). */
 int cmpc_ocp_solve_batch_host(int B, int N, int nx, const int* nu, const double* x0, const double* rec, double* x,
                               double* u, int* status);
 int cmpc_ocp_solve_batch_eq_host(int B, int N, int nx, const int* nu, const int* nc, const double* x0,

@@ -324,7 +324,7 @@ def test_riccati_on_device_matches_recursion(cm, op):
     assert np.all(st == 0)
     for b, (A, B, bb, Q, S, R, q, r) in enumerate(probs):
         Sg, sg = Q[N], q[N]
-        assert np.abs(Sm[b, N] - Sg).max() < 1e-12
+        assert np.abs(Sm[b, N] - Sg).max() < 2e-12  # reg_prim (1e-12) on the diagonal
         for k in range(N - 1, -1, -1):
             m = nu[k]
             if m:
@@ -358,7 +358,10 @@ def test_riccati_not_pd_status(cm, op):
     R[1] = -1000.0 * np.eye(2)  # R + B'Sm B indefinite at stage 1
     rec = op.ocp_pack(N, nx, nu, A, B, bb, Q, S, R, q, r)
     *_, st = cm.ocp_riccati(N, nx, nu, rec[None])
-    assert st[0] == 3
+    # the factorisation guards non-positive pivots as BLASFEO's dpotrf does (inverse 0, no NaN): the IPM cannot meet
+    # stationarity along the dropped direction and ends at MAX_ITER, as the oracle's does
+    r = op.ocp_ipm(N, nx, nu, np.zeros(nx), rec)
+    assert st[0] == r["status"] == 1
 
 
 @pytest.fixture(scope="module")
