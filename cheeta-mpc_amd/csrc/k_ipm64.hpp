@@ -149,16 +149,24 @@ __device__ __forceinline__ T pivot_inv(T p) {
 }
 
 
+// Strides of the partial-sum buffers, chosen so that every access is bank-conflict free under the MI355X rules
+// (MI355X_MICROARCH.md §LDS; a ds_write_b64 covers 16 lanes of one row a = lane / 16, a ds_read_b64 32 lanes):
+//   row partials: partial b of row i at b * RS + i (RS odd: 16 lanes b of one write on distinct banks; a read is 32
+//     consecutive rows); column partials: partial a of column j at a * 64 + j; z at row stride ZS = 20 (the 16 lanes
+//     of a write, (i % 4, i / 4), on 16 distinct bank pairs); block rows at stride 80 (rows e, e + 1 read by one lane
+//     group half a bank row apart).
+constexpr int RS = 65, ZS = 20, BS = 80;
+
 template <typename T>
 struct Lds {
   T v[64];          // lane-per-variable broadcast
   T w[128];         // pyramid-row broadcast
   T rowbuf[2][64];  // factorisation: row s of K as [c*16 + b]
   T dg[64];         // pivots d_s
-  T z[64];          // solve: z permuted as [i % 4][i / 4]
-  T blk[3][64];     // Newton 3x3 block rows
+  T z[4 * ZS];      // solve: z permuted as [i % 4][i / 4]
+  T blk[3][BS];     // Newton 3x3 block rows
   T rl[128], ru[128], itl[128], itu[128], rml[128], rmu[128];  // lane-private pyramid-row scratch
-  T scr[1024];      // Hu and solve partial sums
+  T scr[16 * RS];   // Hu and solve partial sums
 };
 
 }  // namespace ipm64
@@ -314,8 +322,7 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
     for (int c = 0; c < 4; ++c) tc[c] = L.v[olb + 16 * c];
     cbar();
     {
-      const int base0 = ola * 16 + ((((olb >> 1) + ola) & 7) << 1) + (olb & 1);
-      const int base1 = ola * 16 + ((((olb >> 1) + ola + 4) & 7) << 1) + (olb & 1);
+      const int base = olb * RS + ola;  // row 4 r + ola, partial olb
       sfor<0, 16>([&](auto r_) {
         constexpr int r = decltype(r_)::value;
         T p = K[r * 4] * tc[0];
@@ -323,23 +330,20 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
           constexpr int c = decltype(c_)::value;
           p = fma(K[r * 4 + c], tc[c], p);
         });
-        L.scr[((r & 1) ? base1 : base0) + 64 * r] = p;
+        L.scr[base + 4 * r] = p;
       });
     }
     cbar();
     T sv = T(0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = ol * 16 + (((k + ol) & 7) << 1);
-      sv += L.scr[idx] + L.scr[idx + 1];
-    }
+    for (int k = 0; k < 16; k += 2) sv += L.scr[k * RS + ol] + L.scr[(k + 1) * RS + ol];
     cbar();
     const T z = (y - sv) * invd_v;
-    L.z[(ol & 3) * 16 + (ol >> 2)] = z;
+    L.z[(ol & 3) * ZS + (ol >> 2)] = z;
     cbar();
     T zr[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) zr[r] = L.z[ola * 16 + r];
+    for (int r = 0; r < 16; ++r) zr[r] = L.z[ola * ZS + r];
     cbar();
     sfor<0, 4>([&](auto c_) {
       constexpr int c = decltype(c_)::value;
@@ -348,10 +352,10 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
         constexpr int r = decltype(r_)::value;
         q = fma(K[r * 4 + c], zr[r], q);
       });
-      L.scr[(c * 16 + olb) * 4 + ola] = q;
+      L.scr[ola * 64 + c * 16 + olb] = q;
     });
     cbar();
-    const T qs = (L.scr[ol * 4] + L.scr[ol * 4 + 1]) + (L.scr[ol * 4 + 2] + L.scr[ol * 4 + 3]);
+    const T qs = (L.scr[ol] + L.scr[64 + ol]) + (L.scr[128 + ol] + L.scr[192 + ol]);
     cbar();
     y = fma(-invd_v, qs, z);
   };
@@ -462,29 +466,25 @@ __device__ __forceinline__ void ipm64_body(const IpmArgs<T>& A, const CondenseAr
       const T wv[2] = {ll[0] - lu[0], ll[1] - lu[1]};
       ctw = apply_CT(wv);
     }
-    // ---- Hu from the tile: 16 partial row sums per lane, reduced through LDS (row i's 16 partials at i*16 +
-    //      rotated 16-B slot, so both the writes and the row reads are conflict-free)
+    // ---- Hu from the tile: 16 partial row sums per lane, reduced through LDS (partial b of row i at b * RS + i,
+    //      conflict-free writes and row reads)
     T hu = hu_v;  // H u kept up to date incrementally; computed from the tile only at the first iteration
     if (it == 0) {
       T uc[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) uc[c] = L.v[lb + 16 * c];
-      const int base0 = la * 16 + ((((lb >> 1) + la) & 7) << 1) + (lb & 1);
-      const int base1 = la * 16 + ((((lb >> 1) + la + 4) & 7) << 1) + (lb & 1);
+      const int base = lb * RS + la;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         T p = K[r * 4] * uc[0];
         p = fma(K[r * 4 + 1], uc[1], p);
         p = fma(K[r * 4 + 2], uc[2], p);
         p = fma(K[r * 4 + 3], uc[3], p);
-        L.scr[((r & 1) ? base1 : base0) + 64 * r] = p;
+        L.scr[base + 4 * r] = p;
       }
       cbar();
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int idx = lane * 16 + (((k + lane) & 7) << 1);
-        hu += L.scr[idx] + L.scr[idx + 1];
-      }
+      for (int k = 0; k < 16; k += 2) hu += L.scr[k * RS + lane] + L.scr[(k + 1) * RS + lane];
       cbar();
       hu_v = hu;
     }

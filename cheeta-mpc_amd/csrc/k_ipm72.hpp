@@ -27,19 +27,21 @@ namespace ipm72 {
 constexpr int NP = 128;  // row stride of the class-128 H block
 
 constexpr int NB = 8;  // border variables at most (n <= 72)
+constexpr int RS2 = 33;  // row stride of the half-tile partial sums
 
 template <typename T>
 struct Lds72 {
   T v[64 + NB];  // lane-per-variable broadcast
   T w[128];      // pyramid-row broadcast
   union {
-    T rowbuf[2][64];  // factorisation: row s of K_AA as [c*16 + b]
-    T z[64];          // tile solve (after the factorisation): z permuted as [i % 4][i / 4]
+    T rowbuf[2][64];     // factorisation: row s of K_AA as [c*16 + b]
+    T z[4 * ipm64::ZS];  // tile solve (after the factorisation): z permuted as [i % 4][i / 4], row stride ZS
   };
   T dg[64];           // pivots of K_AA
   T blk[3][64 + NB];  // Newton 3x3 block rows
   T rl[128], ru[128], itl[128], itu[128], rml[128], rmu[128];  // lane-private pyramid-row scratch
-  T scr[512];         // H u and tile-solve partial sums (half the rows at a time); result scatter
+  T scr[16 * RS2];    // H u and tile-solve partial sums (half the rows at a time: partial b of row il at b RS2 + il,
+                      // RS2 odd, conflict-free as ipm64::RS); result scatter
   T kab[NB][64];      // K_AB columns, then W = K_AA^-1 K_AB
   T sb[NB * NB];      // S, then S^-1 (row-major 8 x 8, identity-padded)
   T hb[NB * NB];      // H_BB (row-major 8 x 8, zero-padded)
@@ -146,8 +148,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     // row partials of rows 0..31 (register rows 0..7), then 32..63, each half through the same 512 entries
     T sv = T(0);
     {
-      const int base0 = ola * 16 + ((((olb >> 1) + ola) & 7) << 1) + (olb & 1);
-      const int base1 = ola * 16 + ((((olb >> 1) + ola + 4) & 7) << 1) + (olb & 1);
+      const int base = olb * ipm72::RS2 + ola;
       sfor<0, 2>([&](auto h_) {
         constexpr int h = decltype(h_)::value;
         sfor<8 * h, 8 * h + 8>([&](auto r_) {
@@ -157,25 +158,23 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
             constexpr int c = decltype(c_)::value;
             p = fma(K[r * 4 + c], tc[c], p);
           });
-          L.scr[((r & 1) ? base1 : base0) + 64 * (r - 8 * h)] = p;
+          L.scr[base + 4 * (r - 8 * h)] = p;
         });
         cbar();
         if ((ol >> 5) == h) {
+          const int il = ol - 32 * h;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int idx = (ol - 32 * h) * 16 + (((k + ol) & 7) << 1);
-            sv += L.scr[idx] + L.scr[idx + 1];
-          }
+          for (int k = 0; k < 16; k += 2) sv += L.scr[k * ipm72::RS2 + il] + L.scr[(k + 1) * ipm72::RS2 + il];
         }
         cbar();
       });
     }
     const T z = (y - sv) * invd_v;
-    L.z[(ol & 3) * 16 + (ol >> 2)] = z;
+    L.z[(ol & 3) * ipm64::ZS + (ol >> 2)] = z;
     cbar();
     T zr[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) zr[r] = L.z[ola * 16 + r];
+    for (int r = 0; r < 16; ++r) zr[r] = L.z[ola * ipm64::ZS + r];
     cbar();
     sfor<0, 4>([&](auto c_) {
       constexpr int c = decltype(c_)::value;
@@ -184,10 +183,10 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
         constexpr int r = decltype(r_)::value;
         qv = fma(K[r * 4 + c], zr[r], qv);
       });
-      L.scr[(c * 16 + olb) * 4 + ola] = qv;
+      L.scr[ola * 64 + c * 16 + olb] = qv;
     });
     cbar();
-    const T qs = (L.scr[ol * 4] + L.scr[ol * 4 + 1]) + (L.scr[ol * 4 + 2] + L.scr[ol * 4 + 3]);
+    const T qs = (L.scr[ol] + L.scr[64 + ol]) + (L.scr[128 + ol] + L.scr[192 + ol]);
     cbar();
     y = fma(-invd_v, qs, z);
   };
@@ -305,8 +304,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       T uc[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) uc[c] = L.v[lb + 16 * c];
-      const int base0 = la * 16 + ((((lb >> 1) + la) & 7) << 1) + (lb & 1);
-      const int base1 = la * 16 + ((((lb >> 1) + la + 4) & 7) << 1) + (lb & 1);
+      const int base = lb * ipm72::RS2 + la;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -315,15 +313,13 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
           p = fma(K[r * 4 + 1], uc[1], p);
           p = fma(K[r * 4 + 2], uc[2], p);
           p = fma(K[r * 4 + 3], uc[3], p);
-          L.scr[((r & 1) ? base1 : base0) + 64 * (r - 8 * h)] = p;
+          L.scr[base + 4 * (r - 8 * h)] = p;
         }
         cbar();
         if ((lane >> 5) == h) {
+          const int il = lane - 32 * h;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int idx = (lane - 32 * h) * 16 + (((k + lane) & 7) << 1);
-            hu += L.scr[idx] + L.scr[idx + 1];
-          }
+          for (int k = 0; k < 16; k += 2) hu += L.scr[k * ipm72::RS2 + il] + L.scr[(k + 1) * ipm72::RS2 + il];
         }
         cbar();
       }

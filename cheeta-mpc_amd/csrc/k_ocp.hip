@@ -539,9 +539,13 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
             if (l >= mk && l < nz) Kk[(long long)(l - mk) * mk + i] = -v;
             else if (l == nz) kf[i] = -v;
           } else if (i < nz) {
-            if (l >= mk && l < nz) {
-              Pk[(long long)(l - mk) * nx + (i - mk)] = v;
-              S.Paug[(i - mk) * np1 + (l - mk)] = v;
+            if (l >= mk && l < nz) {  // P_k from its lower triangle, mirrored (HPIPM keeps the lower one)
+              if (i >= l) {
+                Pk[(long long)(l - mk) * nx + (i - mk)] = v;
+                Pk[(long long)(i - mk) * nx + (l - mk)] = v;
+                S.Paug[(i - mk) * np1 + (l - mk)] = v;
+                S.Paug[(l - mk) * np1 + (i - mk)] = v;
+              }
             } else if (l == nz) {
               pk[i - mk] = v;
               S.Paug[(i - mk) * np1 + nx] = v;

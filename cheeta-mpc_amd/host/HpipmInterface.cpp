@@ -96,7 +96,9 @@ class HpipmInterface::Impl {
     int nx = 0;
     for (int k = 1; k <= N; ++k) nx = std::max(nx, size_.numStates[(size_t)k]);
     std::vector<int> nc(size_.numIneqConstraints.begin(), size_.numIneqConstraints.end());
-    create(N, nx, std::vector<int>(size_.numInputs.begin(), size_.numInputs.begin() + N), nc);
+    // without a visible device the handle is left to the first solve(), which then reports it (the host-side size
+    // checks and record packing stay usable, as the reference's are without a solve)
+    create(N, nx, std::vector<int>(size_.numInputs.begin(), size_.numInputs.begin() + N), nc, /*defer_no_device=*/true);
   }
 
   hpipm_status solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dyn,
@@ -241,7 +243,7 @@ class HpipmInterface::Impl {
     if (ocp_) cmpc_ocp_destroy(ocp_);
     ocp_ = nullptr;
   }
-  void create(int N, int nx, const std::vector<int>& nu, const std::vector<int>& nc) {
+  void create(int N, int nx, const std::vector<int>& nu, const std::vector<int>& nc, bool defer_no_device = false) {
     release();
     cmpc_settings s;
     cmpc_settings_default(&s);
@@ -262,6 +264,7 @@ class HpipmInterface::Impl {
     const int r = cmpc_ocp_create(N, nx, nu.data(), rows ? nc.data() : nullptr, &s, 1, &ocp_);
     if (r != CMPC_OK) {
       ocp_ = nullptr;
+      if (defer_no_device && r == CMPC_ERR_NO_DEVICE) return;
       throw std::runtime_error(std::string("[HpipmInterface] cannot create the device solver: ") + cmpc_error_string(r));
     }
     ocpN_ = N;

@@ -251,13 +251,14 @@ static int ocp_factor(const ocp_prob* p, const double* sig, ocp_fact* F, double*
       lsolve(m, Lr, iLd, col);
       for (int a = 0; a < m; ++a) LsT[a * nx + j] = col[a];
     }
-    /* P_k = Q~ + A'PA - Ls Ls' */
+    /* P_k = Q~ + A'PA - Ls Ls', from its lower triangle (HPIPM keeps the lower one), mirrored */
     for (int i = 0; i < nx; ++i)
-      for (int j = 0; j < nx; ++j) {
+      for (int j = 0; j <= i; ++j) {
         double s = 0.0;
         for (int t = 0; t < nx; ++t) s += CM(A, nx, t, i) * PA[t * nx + j];
         for (int a = 0; a < m; ++a) s -= LsT[a * nx + i] * LsT[a * nx + j];
         Pk[i * nx + j] += s;
+        if (j < i) Pk[j * nx + i] = Pk[i * nx + j];
       }
   }
   return 0;
