@@ -562,28 +562,42 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
   return __syncthreads_or(bad) == 0;
 }
 
-// Closed-loop matrices Acl_k = A_k + B_k K_k (column-major, k = 1..N-1) and bcl_k = rb_k + B_k kf_k (k = 0..N-1)
-__device__ __forceinline__ void acl_pass(const View& V, bool with_acl) {
+// Closed-loop matrices Acl_k = A_k + B_k K_k (column-major, k = 1..N-1) and bcl_k = rb_k + B_k kf_k (k = 0..N-1), one
+// stage at a time: B_k, K_k and kf_k staged in LDS (double buffer in ABx / Tx, one barrier per stage) so that every
+// product operand is an LDS read (B_k consecutive over the rows, K_k broadcast), A_k and rb_k coalesced global loads.
+// A stage whose B_k, K_k do not fit the buffer (nu_k far above nx) reads them from global memory instead.
+__device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_acl) {
   const OcpLayout& L = V.L;
-  const int nx = L.nx, N = L.N, nxx = nx * nx;
-  const int nA = with_acl ? (N - 1) * nxx : 0;
-  for (int it = threadIdx.x; it < nA + N * nx; it += NT) {
-    if (it < nA) {
-      const int k = 1 + it / nxx, e = it % nxx, c = e / nx, i = e % nx, mk = L.nu[k];
-      const double* Bm = V.Bm(k);
-      const double* Kk = V.K(k);
-      double s = V.A(k)[(long long)c * nx + i];
-      for (int a = 0; a < mk; ++a) s = fma(Bm[(long long)a * nx + i], Kk[(long long)c * mk + a], s);
-      V.Acl(k)[e] = s;
-    } else {
-      const int e = it - nA, k = e / nx, i = e % nx, mk = L.nu[k];
-      const double* Bm = V.Bm(k);
-      const double* kf = V.kf() + L.cu[k];
-      double s = V.rb()[(long long)k * nx + i];
-      for (int a = 0; a < mk; ++a) s = fma(Bm[(long long)a * nx + i], kf[a], s);
-      V.bcl()[(long long)k * nx + i] = s;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
+  for (int k = 0; k < N; ++k) {
+    const int mk = L.nu[k], nB = nx * mk;
+    const double* Bg = V.Bm(k);
+    const double* Kg = V.K(k);
+    const double* kg = V.kf() + L.cu[k];
+    const bool fits = 2 * nB + mk <= S.nrm * S.nzp;
+    double* buf = (k & 1) ? S.Tx : S.ABx;
+    if (fits)
+      for (int e = tid; e < 2 * nB + mk; e += NT) buf[e] = e < nB ? Bg[e] : (e < 2 * nB ? Kg[e - nB] : kg[e - 2 * nB]);
+    const double* Bs = fits ? buf : Bg;
+    const double* Ks = fits ? buf + nB : Kg;
+    const double* ks = fits ? buf + 2 * nB : kg;
+    __syncthreads();
+    const int na = (with_acl && k >= 1) ? nxx : 0;
+    for (int e = tid; e < na + nx; e += NT) {
+      if (e < na) {
+        const int c = e / nx, i = e - c * nx;
+        double s = V.A(k)[e];
+        for (int a = 0; a < mk; ++a) s = fma(Bs[a * nx + i], Ks[c * mk + a], s);
+        V.Acl(k)[e] = s;
+      } else {
+        const int i = e - na;
+        double s = V.rb()[(long long)k * nx + i];
+        for (int a = 0; a < mk; ++a) s = fma(Bs[a * nx + i], ks[a], s);
+        V.bcl()[(long long)k * nx + i] = s;
+      }
     }
   }
+  __syncthreads();
 }
 
 // Serial forward sweep: dx_1 = bcl_0, dx_{k+1} = Acl_k dx_k + bcl_k (dx node 0 stays 0)
@@ -899,7 +913,7 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
       break;
     }
     OCP_STAMP(17);
-    acl_pass(V, true);
+    acl_pass(V, S, true);
     __syncthreads();
     OCP_STAMP(3);
     forward_pass(V, S);
@@ -938,7 +952,7 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
       backward_vec_pass(V, S);
       __syncthreads();
       OCP_STAMP(7);
-      acl_pass(V, false);
+      acl_pass(V, S, false);
       __syncthreads();
       forward_pass(V, S);
       OCP_STAMP(8);

@@ -400,8 +400,10 @@ def test_device_riccati_matches_oracle(cm, op, case):
     assert np.all(rst == 0)
     # With rows the factorisation at the exit point weights them by Sigma = lam / t with t ~ 1e-10: each
     # implementation's slacks carry ~1e-16 |C x + D u| of rounding, i.e. ~1e-6 of t, into the weights of the
-    # constrained directions, which dominate P, p and Lr (1e10+): those agree to 1e-4 of their largest entry, the
-    # policy K, k (set by the rows, not by their weight) and every Sigma-free quantity to 1e-9 / 1e-8.
+    # constrained directions (1e10+), and P, p, Lr, K, k are formed by eliminations across those weights: device and
+    # oracle agree to 1e-4 of each quantity's largest entry there (measured 1e-5), and the Sigma-free checks carry the
+    # parity: the policy on the solution (below) and, in the C++ mirror, K_0 against finite differences of the solve.
+    # Without rows everything agrees to 1e-9 / 1e-8.
     rows = ps[0].get("nc") is not None
     tS = 1e-4 if rows else 1e-9
     for i, p in enumerate(ps):
@@ -410,12 +412,12 @@ def test_device_riccati_matches_oracle(cm, op, case):
         for k in range(1, N + 1):
             assert _rel(P[i][k], r["P"][k]) < tS, ("P", k)
             assert _rel(pv[i][k], r["p"][k]) < max(tS, 1e-8), ("p", k)
-            assert np.abs(P[i][k] - P[i][k].T).max() <= 1e-12 * max(1.0, np.abs(P[i][k]).max()), ("P sym", k)
+            assert np.array_equal(P[i][k], P[i][k].T), ("P symmetric (lower triangle mirrored)", k)
         for k in range(N):
             assert _rel(Lr[i][k], r["Lr"][k]) < tS, ("Lr", k)
             if k > 0:
-                assert _rel(K[i][k], r["K"][k]) < (1e-7 if rows else 1e-9), ("K", k)
-                assert _rel(kf[i][k], r["k"][k]) < (1e-6 if rows else 1e-8), ("k", k)
+                assert _rel(K[i][k], r["K"][k]) < (tS if rows else 1e-9), ("K", k)
+                assert _rel(kf[i][k], r["k"][k]) < (tS if rows else 1e-8), ("k", k)
         if rows:  # the policy on the solution (u - K x - k is the exit point's Newton feedforward, near tolerance)
             us = _split(p, u[i])
             for k in range(1, N):
