@@ -50,7 +50,7 @@ def condense_flops(contact):
 
 
 def ocp_flops(nu, nc, nx, iters):
-    """Algorithmic FLOPs of one stage-wise OCP solve (DESIGN.md §10): per IPM iteration the Riccati factorisation of
+    """Algorithmic FLOPs of one stage-wise OCP solve (DESIGN.md §4.5): per IPM iteration the Riccati factorisation of
     every stage k (nu_k = m, nc_k = g rows, n = nx): P [B A] 2 n^2 (n+m), the symmetric [B A]'(P [B A]) and the rows'
     Gc' Sigma Gc, lower triangles, (n+m)(n+m+1)(n+g), the Cholesky of R~ + B'PB m^3/3, Ls = M_xu Lr^-T m^2 n,
     P_k = M_xx - Ls Ls' n^2 m; two Newton solves (predictor, corrector; one without rows) of 2 (2 n^2 + 3 n m + m^2
