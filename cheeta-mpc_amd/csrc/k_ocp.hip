@@ -26,6 +26,7 @@ namespace cmpc {
 namespace {
 
 constexpr int NT = OCP_NT;
+typedef double v4d __attribute__((ext_vector_type(4)));
 constexpr double TAU_OCP = 0.995;  // fraction-to-boundary, as oracle/ocp_ipm.c
 
 // Lab instrumentation (-DCMPC_OCP_STAMPS, lab/ocp_stamps.sh only, never in libcmpc.so): thread 0 of problem 0
@@ -326,6 +327,11 @@ struct StagePrefetch {
   double v[EPT];
 };
 
+// Workgroup barrier for LDS traffic only: lgkmcnt(0) and s_barrier, without the vmcnt(0) of __syncthreads(), so the
+// next stage's global prefetch (registers) stays in flight across the sweep's barriers instead of being waited for at
+// the first one. Used inside the factorisation's stage loop, whose threads exchange data through LDS only.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Backward factorisation of the barrier-weighted Newton matrix with the right-hand side (gu, gx, rb) of ws.
 // Writes P_k, pv_k (k = 0..N), K_k, kf_k and the LDL' columns Lf_k (k = 0..N-1). Returns false on a NaN pivot.
 template <int NZP>
@@ -381,31 +387,44 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
   OCP_STAMP(10);
   for (int k = N - 1; k >= 0; --k) {
     const int mk = L.nu[k], nz = mk + nx, nrk = np1 + L.ng[k];
-    // --- T = Paug [B A rb; 0 0 1] (rows 0..nx), eight accumulators per pass ---
-    for (int l = tid & 63; l < NZP; l += 64) {
-#pragma unroll 1
-      for (int half = 0; half < 2; ++half) {
-        const int rbase = (tid >> 6) + 32 * half;
-        if (rbase >= np1) break;
-        double acc[8];
+    // --- T = Paug [B A rb; 0 0 1] (rows 0..nx) on v_mfma_f64_16x16x4_f64: wave w owns the 16-column blocks
+    //     w, w + 4, .. and all (at most four) 16-row blocks of T, K = np1 in steps of 4; operands straight from LDS
+    //     (A: Paug[16 rb + lane % 16][4 kk + lane / 16], 0 beyond np1; B: ABx[4 kk + lane / 16][16 cb + lane % 16]);
+    //     C/D rows (lane / 16) + 4 reg, columns lane % 16. Four independent accumulator chains per wave: the
+    //     dependent VALU form left each s-step waiting on its LDS loads (26 % of a B = 1 solve) ---
+    {
+      const int lane = tid & 63, wv = tid >> 6, lr = lane & 15, lk = lane >> 4;
+      const int nrb = (np1 + 15) >> 4, nks = (np1 + 3) >> 2;
+      for (int cb = wv; cb < NZP / 16; cb += 4) {
+        v4d acc[4];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] = 0.0;
-        for (int s2 = 0; s2 < np1; ++s2) {
-          const double abv = S.ABx[s2 * NZP + l];
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = v4d{0.0, 0.0, 0.0, 0.0};
+        for (int kk = 0; kk < nks; ++kk) {
+          const int s2 = 4 * kk + lk;
+          const bool sin = s2 < np1;
+          const double bv = sin ? S.ABx[s2 * NZP + 16 * cb + lr] : 0.0;
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const int r = rbase + 4 * t;
-            if (r < np1) acc[t] = fma(S.Paug[r * np1 + s2], abv, acc[t]);
+          for (int rb = 0; rb < 4; ++rb) {
+            if (rb < nrb) {
+              const int r = 16 * rb + lr;
+              const double av = (sin && r < np1) ? S.Paug[r * np1 + s2] : 0.0;
+              acc[rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[rb], 0, 0, 0);
+            }
           }
         }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int r = rbase + 4 * t;
-          if (r < np1) S.Tx[r * NZP + l] = acc[t];
+        for (int rb = 0; rb < 4; ++rb) {
+          if (rb < nrb) {
+#pragma unroll
+            for (int q2 = 0; q2 < 4; ++q2) {
+              const int r = 16 * rb + lk + 4 * q2;
+              if (r < np1) S.Tx[r * NZP + 16 * cb + lr] = acc[rb][q2];
+            }
+          }
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     OCP_STAMP(11);
     // --- M = H + ABx' Tx over the stage's nrk rows (register tile) ---
     double m[R][R];
@@ -424,11 +443,12 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
 #pragma unroll
         for (int b = 0; b < R; ++b) m[a][b] = fma(ai[a], tl[b], m[a][b]);
     }
-    __syncthreads();  // ABx / Tx are free: the next stage's data goes there
+    lds_barrier();  // ABx / Tx are free: the next stage's data goes there
     OCP_STAMP(12);
     // --- prefetch stage k-1 (its data rows, its H tile, its rows' Sigma) ---
     StagePrefetch<NZP> pf;
     const int kn = k - 1;
+    double sgv = 0.0;
     if (kn >= 0) {
       const StagePtrs P = stage_ptrs(V, kn);
       const int nrn = np1 + P.g;
@@ -439,7 +459,7 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
           pf.v[s2] = e < nrn * NZP ? stage_load(P, nx, e / NZP, e % NZP) : 0.0;
         }
       }
-      if (tid < P.g) S.sgn[tid] = V.row(R_SIG)[L.cr[kn] + tid];
+      sgv = tid < P.g ? V.row(R_SIG)[L.cr[kn] + tid] : 0.0;  // into S.sgn at the sweep's last barrier
       const HPtrs H = h_ptrs(V, kn);
 #pragma unroll
       for (int a = 0; a < R; ++a)
@@ -453,7 +473,7 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
 #pragma unroll
         for (int a = 0; a < R; ++a) S.col[ti + 16 * a] = m[a][0];
       }
-      __syncthreads();
+      lds_barrier();
       double* Lf = V.Lf(k);
       for (int j = 0; j < mk; ++j) {
         const double* cb = S.col + (j & 1) * NZP;
@@ -494,10 +514,12 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
               for (int a = 0; a < R; ++a) nb[ti + 16 * a] = m[a][b];
             }
         }
-        __syncthreads();
+        if (j == mk - 1 && kn >= 0 && tid < L.ng[kn]) S.sgn[tid] = sgv;
+        lds_barrier();
       }
     } else {
-      __syncthreads();  // S.sgn visible to the stores below
+      if (kn >= 0 && tid < L.ng[kn]) S.sgn[tid] = sgv;
+      lds_barrier();  // S.sgn visible to the stores below
     }
     OCP_STAMP(14);
     // --- next stage's data into LDS ---
@@ -556,32 +578,52 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
           }
         }
     }
-    __syncthreads();
+    lds_barrier();
     OCP_STAMP(16);
   }
   return __syncthreads_or(bad) == 0;
 }
 
 // Closed-loop matrices Acl_k = A_k + B_k K_k (column-major, k = 1..N-1) and bcl_k = rb_k + B_k kf_k (k = 0..N-1), one
-// stage at a time: B_k, K_k and kf_k staged in LDS (double buffer in ABx / Tx, one barrier per stage) so that every
-// product operand is an LDS read (B_k consecutive over the rows, K_k broadcast), A_k and rb_k coalesced global loads.
-// A stage whose B_k, K_k do not fit the buffer (nu_k far above nx) reads them from global memory instead.
+// stage at a time: B_k, K_k and kf_k staged in LDS (double buffer in ABx / Tx, one LDS barrier per stage; the next
+// stage's operands are loaded into registers while this one computes) so that every product operand is an LDS read
+// (B_k consecutive over the rows, K_k broadcast), A_k and rb_k coalesced global loads. A stage whose operands exceed
+// the register staging (nu_k far above nx) reads them from global memory instead.
 __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_acl) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
+  constexpr int EPS = 6;  // staged operand doubles per thread
+  auto opn = [&](int k) { return 2 * nx * L.nu[k] + L.nu[k]; };
+  auto fits = [&](int k) { return opn(k) <= EPS * NT && opn(k) <= S.nrm * S.nzp; };
+  auto op_load = [&](int k, int e) -> double {  // operand e of stage k: B_k, then K_k, then kf_k
+    const int nB = nx * L.nu[k];
+    const double* p = e < nB ? V.Bm(k) + e : (e < 2 * nB ? V.K(k) + (e - nB) : V.kf() + L.cu[k] + (e - 2 * nB));
+    return *p;
+  };
+  double st[EPS];
+  if (fits(0)) {
+#pragma unroll
+    for (int q = 0; q < EPS; ++q) {
+      const int e = tid + NT * q;
+      if (e < opn(0)) S.ABx[e] = op_load(0, e);
+    }
+  }
+  lds_barrier();
   for (int k = 0; k < N; ++k) {
     const int mk = L.nu[k], nB = nx * mk;
-    const double* Bg = V.Bm(k);
-    const double* Kg = V.K(k);
-    const double* kg = V.kf() + L.cu[k];
-    const bool fits = 2 * nB + mk <= S.nrm * S.nzp;
-    double* buf = (k & 1) ? S.Tx : S.ABx;
-    if (fits)
-      for (int e = tid; e < 2 * nB + mk; e += NT) buf[e] = e < nB ? Bg[e] : (e < 2 * nB ? Kg[e - nB] : kg[e - 2 * nB]);
-    const double* Bs = fits ? buf : Bg;
-    const double* Ks = fits ? buf + nB : Kg;
-    const double* ks = fits ? buf + 2 * nB : kg;
-    __syncthreads();
+    const bool fk = fits(k);
+    const double* buf = (k & 1) ? S.Tx : S.ABx;
+    const bool pre = k + 1 < N && fits(k + 1);
+    if (pre) {
+#pragma unroll
+      for (int q = 0; q < EPS; ++q) {
+        const int e = tid + NT * q;
+        st[q] = e < opn(k + 1) ? op_load(k + 1, e) : 0.0;
+      }
+    }
+    const double* Bs = fk ? buf : V.Bm(k);
+    const double* Ks = fk ? buf + nB : V.K(k);
+    const double* ks = fk ? buf + 2 * nB : V.kf() + L.cu[k];
     const int na = (with_acl && k >= 1) ? nxx : 0;
     for (int e = tid; e < na + nx; e += NT) {
       if (e < na) {
@@ -596,6 +638,15 @@ __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_
         V.bcl()[(long long)k * nx + i] = s;
       }
     }
+    if (pre) {
+      double* nbuf = ((k + 1) & 1) ? S.Tx : S.ABx;
+#pragma unroll
+      for (int q = 0; q < EPS; ++q) {
+        const int e = tid + NT * q;
+        if (e < opn(k + 1)) nbuf[e] = st[q];
+      }
+    }
+    lds_barrier();
   }
   __syncthreads();
 }
@@ -1008,8 +1059,10 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
   }
 }
 
-template <int NZP>
-__global__ __launch_bounds__(NT) void k_ocp_ipm(OcpSolveArgs a) {
+// MINB workgroups per CU: 1 (the whole register file for one problem's chain: the lowest latency, B <= #CUs) or 2
+// (bounded at 256 VGPRs, spilling some bookkeeping: 1.4-1.5x the solves/s of a full chip, 10 % slower per problem)
+template <int NZP, int MINB>
+__global__ __launch_bounds__(NT, MINB) void k_ocp_ipm(OcpSolveArgs a) {
   extern __shared__ double smem[];
   const Lds S = carve(smem, a.L, NZP);
   OCP_STAMP(31);
@@ -1182,15 +1235,19 @@ int launch_ocp_ipm(const OcpSolveArgs& a, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   const size_t lds = ocp_lds_bytes(a.L);
   if (a.L.nzp == 64) {
-    if (hipFuncSetAttribute((const void*)k_ocp_ipm<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
-      return -1;
-    hipLaunchKernelGGL(k_ocp_ipm<64>, dim3(B), dim3(NT), lds, stream, a);
+    // one problem per CU while the batch leaves CUs idle anyway, two per CU beyond (cmpc_ocp_solve's B)
+    const bool two = B > OCP_ONE_PER_CU_MAX;
+    const void* kf = two ? (const void*)k_ocp_ipm<64, 2> : (const void*)k_ocp_ipm<64, 1>;
+    if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
+    if (two)
+      hipLaunchKernelGGL((k_ocp_ipm<64, 2>), dim3(B), dim3(NT), lds, stream, a);
+    else
+      hipLaunchKernelGGL((k_ocp_ipm<64, 1>), dim3(B), dim3(NT), lds, stream, a);
   } else {
-    if (hipFuncSetAttribute((const void*)k_ocp_ipm<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+    if (hipFuncSetAttribute((const void*)k_ocp_ipm<128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
       return -1;
-    hipLaunchKernelGGL(k_ocp_ipm<128>, dim3(B), dim3(NT), lds, stream, a);
+    hipLaunchKernelGGL((k_ocp_ipm<128, 1>), dim3(B), dim3(NT), lds, stream, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -11,6 +11,7 @@ namespace cmpc {
 constexpr int OCP_NT = 256;       // threads per problem (one workgroup)
 constexpr int OCP_ROWS = 17;      // per-row workspace arrays (see OcpLayout::row)
 constexpr int OCP_MAX_NX = 63;    // nx + 1 <= 64
+constexpr int OCP_ONE_PER_CU_MAX = 256;  // batches up to this size run one problem per CU (k_ocp_ipm<64, 1>)
 constexpr int OCP_MAX_NG = 64;    // general-constraint rows per node
 constexpr int OCP_MAX_N = 4096;   // stages
 

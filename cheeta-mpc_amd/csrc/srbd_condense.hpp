@@ -60,7 +60,10 @@ template <typename T, int NMAX, int WAVES, bool FEET = false>
 struct SrbdLds {
   static constexpr int NTRI = NMAX / 3;
   static constexpr int FT = FEET ? NTRI : 1;  // foothold arrays only in the FEET instantiation (LDS of k_solve128)
-  T s_G[2][16][NMAX];
+  // Bqp block rows, double-buffered; row stride NMAX + 16 (16 mod 32 in fp32, half a 64-bank row in fp64): the MFMA
+  // operand reads take rows s and s + 1 in one lane group, which then fall on disjoint banks
+  static constexpr int GS = NMAX + 16;
+  T s_G[2][16][GS];
   T s_w[2][16];
   T s_q[2][16];
   double s_xref[(MAXN + 1) * NX];
@@ -125,7 +128,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
         S.s_D[i] = a.dbar[(size_t)q * N * NU + i];
       }
   }
-  for (int i = tid; i < 2 * 16 * NMAX; i += NTHR) (&S.s_G[0][0][0])[i] = T(0);
+  for (int i = tid; i < 2 * 16 * S.GS; i += NTHR) (&S.s_G[0][0][0])[i] = T(0);
   if (tid < 32) (&S.s_w[0][0])[tid] = T(0), (&S.s_q[0][0])[tid] = T(0);
   if (tid == 0) S.s_flag = 0;
   const int ne = N * L;

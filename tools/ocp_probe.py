@@ -1,5 +1,6 @@
 """Quick GPU timing of cmpc_ocp_solve on legged-size problems (device pointers, HIP events on the solve stream).
-Usage: python tools/ocp_probe.py [B ...]"""
+Usage: python tools/ocp_probe.py [B ...]; phase stamps of a lab build (lab/ocp_stamps.sh):
+CMPC_LIB=lab/_stamps/libcmpc_ocpstamps.so python tools/ocp_probe.py --stamps"""
 import ctypes as C
 import os
 import sys
@@ -51,7 +52,7 @@ def run(projected, B, reps=5):
           f"status ok {np.mean(st == 0):.2f}; host path {th:.2f} ms", flush=True)
 
 
-if __name__ == "__main__" and not os.environ.get("CMPC_LIB"):
+if __name__ == "__main__" and "--stamps" not in sys.argv:
     Bs = [int(a) for a in sys.argv[1:]] or [1, 64, 256, 1024]
     for proj in (True, False):
         for B in Bs:
@@ -81,6 +82,6 @@ def stamps(projected, B=1):
         print(f"  {n:22s} {buf[i]:12d}  {100.0 * buf[i] / max(tot, 1):5.1f} %")
 
 
-if __name__ == "__main__" and os.environ.get("CMPC_LIB"):
+if __name__ == "__main__" and "--stamps" in sys.argv:
     stamps(True)
     stamps(False)
