@@ -136,11 +136,16 @@ __device__ __forceinline__ Lds carve(double* smem, const OcpLayout& L, int NZP) 
   s.ABx = s.Paug + pa;
   s.Tx = s.ABx + s.nrm * NZP;
   s.col = s.Tx + s.nrm * NZP;
-  s.vec = s.col + 2 * NZP;
+  s.vec = s.col + 4 * NZP;
   s.red = s.vec + 128;
   s.sgn = s.red + 64;
   return s;
 }
+
+// Workgroup barrier for LDS traffic only: lgkmcnt(0) and s_barrier, without the vmcnt(0) of __syncthreads(), so the
+// next stage's global prefetch (registers) stays in flight across the sweep's barriers instead of being waited for at
+// the first one. Used inside the factorisation's stage loop, whose threads exchange data through LDS only.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // c = C x + D u for every row (node 0's x is x0; the step's dx node 0 is 0)
 __device__ __forceinline__ void rows_value(const View& V, const double* xs, const double* us, double* out) {
@@ -221,6 +226,129 @@ __device__ __forceinline__ void residuals(const View& V, double& rs, double& re)
       re = nmax(re, fabs(s));
     }
   }
+}
+
+// The same residuals one node at a time, the node's matrices staged in LDS (ABx and Tx as one buffer): the
+// transposed products (B'pi, A'pi, S'u, D'w, C'w) read LDS instead of strided global loads, and the next node's
+// matrices are loaded into registers while this one computes. A node whose matrices exceed the staging (nu_k far
+// above nx) reads them from global memory.
+struct NodeMats {
+  int nA, nB, nQ, nS, nR, nC, nD, oB, oQ, oS, oR, oC, oD, tot;
+};
+__device__ __forceinline__ NodeMats node_mats(const OcpLayout& L, int k) {
+  NodeMats M;
+  const int nx = L.nx, mk = L.nu[k], g = L.ng[k];
+  M.nA = k < L.N ? nx * nx : 0;
+  M.nB = k < L.N ? nx * mk : 0;
+  M.nQ = nx * nx;
+  M.nS = mk * nx;
+  M.nR = mk * mk;
+  M.nC = g * nx;
+  M.nD = g * mk;
+  M.oB = M.nA;
+  M.oQ = M.oB + M.nB;
+  M.oS = M.oQ + M.nQ;
+  M.oR = M.oS + M.nS;
+  M.oC = M.oR + M.nR;
+  M.oD = M.oC + M.nC;
+  M.tot = M.oD + M.nD;
+  return M;
+}
+__device__ __forceinline__ double node_load(const View& V, const NodeMats& M, int k, int e) {
+  const double* p = e < M.oB   ? V.A(k) + e
+                    : e < M.oQ ? V.Bm(k) + (e - M.oB)
+                    : e < M.oS ? V.Q(k) + (e - M.oQ)
+                    : e < M.oR ? V.S(k) + (e - M.oS)
+                    : e < M.oC ? V.R(k) + (e - M.oR)
+                    : e < M.oD ? V.C(k) + (e - M.oC)
+                               : V.D(k) + (e - M.oD);
+  return *p;
+}
+__device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, double& rs, double& re) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N;
+  const double *x = V.x(), *u = V.u(), *pi = V.pi(), *wl = V.row(R_W);
+  double* buf = S.ABx;  // ABx and Tx are contiguous
+  const int cap = 2 * S.nrm * S.nzp;
+  constexpr int EPR = 16;
+  auto staged = [&](const NodeMats& M) { return M.tot <= cap && M.tot <= EPR * NT; };
+  double pre[EPR];
+  {
+    const NodeMats M0 = node_mats(L, 0);
+    if (staged(M0))
+      for (int e = tid; e < M0.tot; e += NT) buf[e] = node_load(V, M0, 0, e);
+  }
+  __syncthreads();
+  for (int k = 0; k <= N; ++k) {
+    const NodeMats M = node_mats(L, k);
+    const bool st = staged(M);
+    const int mk = L.nu[k], g = L.ng[k];
+    const NodeMats Mn = node_mats(L, k < N ? k + 1 : k);
+    const bool pn = k < N && staged(Mn);
+    if (pn) {
+#pragma unroll
+      for (int q = 0; q < EPR; ++q) {
+        const int e = tid + NT * q;
+        pre[q] = e < Mn.tot ? node_load(V, Mn, k + 1, e) : 0.0;
+      }
+    }
+    const double* A = st ? buf : V.A(k);
+    const double* Bm = st ? buf + M.oB : V.Bm(k);
+    const double* Q = st ? buf + M.oQ : V.Q(k);
+    const double* Sm = st ? buf + M.oS : V.S(k);
+    const double* R = st ? buf + M.oR : V.R(k);
+    const double* C = st ? buf + M.oC : (g ? V.C(k) : nullptr);
+    const double* D = st ? buf + M.oD : (g ? V.D(k) : nullptr);
+    const double* xk = x + (long long)k * nx;
+    const double* uk = u + L.cu[k];
+    const double* wk = wl + L.cr[k];
+    const int n1 = mk, n2 = k >= 1 ? nx : 0, n3 = k < N ? nx : 0;
+    for (int e = tid; e < n1 + n2 + n3; e += NT) {
+      if (e < n1) {
+        const int a = e;
+        double s = V.r(k)[a];
+        for (int c = 0; c < mk; ++c) s = fma(R[c * mk + a], uk[c], s);
+        for (int j = 0; j < nx; ++j) s = fma(Sm[j * mk + a], xk[j], s);
+        for (int t = 0; t < nx; ++t) s = fma(Bm[a * nx + t], pi[(long long)k * nx + t], s);
+        double d = 0.0;
+        for (int j = 0; j < g; ++j) d = fma(D[a * g + j], wk[j], d);
+        s -= d;
+        V.rgu()[L.cu[k] + a] = s;
+        rs = nmax(rs, fabs(s));
+      } else if (e < n1 + n2) {
+        const int i = e - n1;
+        double s = V.q(k)[i] - pi[(long long)(k - 1) * nx + i];
+        for (int j = 0; j < nx; ++j) s = fma(Q[j * nx + i], xk[j], s);
+        for (int a = 0; a < mk; ++a) s = fma(Sm[i * mk + a], uk[a], s);
+        if (k < N)
+          for (int t = 0; t < nx; ++t) s = fma(A[i * nx + t], pi[(long long)k * nx + t], s);
+        double d = 0.0;
+        for (int j = 0; j < g; ++j) d = fma(C[i * g + j], wk[j], d);
+        s -= d;
+        V.rgx()[(long long)k * nx + i] = s;
+        rs = nmax(rs, fabs(s));
+      } else {
+        const int i = e - n1 - n2;
+        double s = V.b(k)[i] - x[(long long)(k + 1) * nx + i];
+        for (int j = 0; j < nx; ++j) s = fma(A[j * nx + i], xk[j], s);
+        for (int a = 0; a < mk; ++a) s = fma(Bm[a * nx + i], uk[a], s);
+        V.rb()[(long long)k * nx + i] = s;
+        re = nmax(re, fabs(s));
+      }
+    }
+    if (k < N) {
+      lds_barrier();  // every thread is done with node k's staging buffer
+      if (pn) {
+#pragma unroll
+        for (int q = 0; q < EPR; ++q) {
+          const int e = tid + NT * q;
+          if (e < Mn.tot) buf[e] = pre[q];
+        }
+      }
+      lds_barrier();
+    }
+  }
+  __syncthreads();
 }
 
 // Step right-hand side g = r_g + Gc' w (node 0 has no state entries)
@@ -327,10 +455,6 @@ struct StagePrefetch {
   double v[EPT];
 };
 
-// Workgroup barrier for LDS traffic only: lgkmcnt(0) and s_barrier, without the vmcnt(0) of __syncthreads(), so the
-// next stage's global prefetch (registers) stays in flight across the sweep's barriers instead of being waited for at
-// the first one. Used inside the factorisation's stage loop, whose threads exchange data through LDS only.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Backward factorisation of the barrier-weighted Newton matrix with the right-hand side (gu, gx, rb) of ws.
 // Writes P_k, pv_k (k = 0..N), K_k, kf_k and the LDL' columns Lf_k (k = 0..N-1). Returns false on a NaN pivot.
@@ -467,31 +591,32 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
         for (int b = 0; b < R; ++b) hm[a][b] = h_load(H, nx, ti + 16 * a, tj + 16 * b, reg);
     }
     OCP_STAMP(13);
-    // --- Gauss-Jordan sweep of the u block ---
+    // --- Gauss-Jordan sweep of the u block, two pivots per barrier: columns j and j + 1 are published together
+    //     (parity double buffer, [parity][column][NZP]) before pivot j; every thread forms column j + 1 after pivot j
+    //     itself, by the owner's own FMA (bit-identical to one pivot per barrier), then applies both pivots ---
     if (mk > 0) {
-      if (tj == 0) {
+      auto publish = [&](int c, double* dst) {  // owner threads of column c write it (all rows)
+        if (c < mk && tj == (c & 15)) {
 #pragma unroll
-        for (int a = 0; a < R; ++a) S.col[ti + 16 * a] = m[a][0];
-      }
-      lds_barrier();
-      double* Lf = V.Lf(k);
-      for (int j = 0; j < mk; ++j) {
-        const double* cb = S.col + (j & 1) * NZP;
-        const double d = cb[j];
-        bad = bad || (d != d);
-        const double dinv = d > 1e-200 ? 1.0 / d : 0.0;
-        // the pivot column of the Schur complement is column j of L D (the LDL' factor of M_uu) for rows j..mk-1
-        if (tid >= j && tid < mk) Lf[(long long)j * mk + tid] = cb[tid];
+          for (int b = 0; b < R; ++b)
+            if (b == (c >> 4)) {
+#pragma unroll
+              for (int a = 0; a < R; ++a) dst[ti + 16 * a] = m[a][b];
+            }
+        }
+      };
+      // one GJ step with the pivot column pc (all rows) of pivot p: m <- (mask p) - a a' / d, a_p = -1
+      auto step = [&](int p, const double* pc, double dinv) {
         double ci[R], cl[R];
 #pragma unroll
         for (int a = 0; a < R; ++a) {
           const int i = ti + 16 * a;
-          ci[a] = i == j ? -1.0 : cb[i];
+          ci[a] = i == p ? -1.0 : pc[i];
         }
 #pragma unroll
         for (int b = 0; b < R; ++b) {
           const int l = tj + 16 * b;
-          cl[b] = l == j ? -1.0 : cb[l];
+          cl[b] = l == p ? -1.0 : pc[l];
         }
 #pragma unroll
         for (int a = 0; a < R; ++a) {
@@ -500,21 +625,68 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
 #pragma unroll
           for (int b = 0; b < R; ++b) {
             const int l = tj + 16 * b;
-            const double base = (i == j || l == j) ? 0.0 : m[a][b];
+            const double base = (i == p || l == p) ? 0.0 : m[a][b];
             m[a][b] = fma(f, cl[b], base);
           }
         }
-        const int jn = j + 1;
-        if (jn < mk && tj == (jn & 15)) {
-          double* nb = S.col + (jn & 1) * NZP;
+      };
+      publish(0, S.col);
+      publish(1, S.col + NZP);
+      lds_barrier();
+      double* Lf = V.Lf(k);
+      for (int j = 0; j < mk; j += 2) {
+        const double* c0 = S.col + ((j >> 1) & 1) * 2 * NZP;
+        const double* c1 = c0 + NZP;
+        const double d0 = c0[j];
+        bad = bad || (d0 != d0);
+        const double dinv0 = d0 > 1e-200 ? 1.0 / d0 : 0.0;
+        // the pivot columns of the Schur complement are the columns of L D (the LDL' factor of M_uu), rows p..mk-1
+        if (tid >= j && tid < mk) Lf[(long long)j * mk + tid] = c0[tid];
+        if (j + 1 < mk) {
+          const double a1 = c0[j + 1];  // a_{j+1} of pivot j
+          // column j + 1 after pivot j, at the rows this thread needs (its tile rows and columns) and at j + 1
+          double e1[R], e2[R];
 #pragma unroll
-          for (int b = 0; b < R; ++b)
-            if (b == (jn >> 4)) {
+          for (int a = 0; a < R; ++a) {
+            const int i = ti + 16 * a;
+            const double ai = i == j ? -1.0 : c0[i];
+            e1[a] = fma(-ai * dinv0, a1, i == j ? 0.0 : c1[i]);
+          }
 #pragma unroll
-              for (int a = 0; a < R; ++a) nb[ti + 16 * a] = m[a][b];
+          for (int b = 0; b < R; ++b) {
+            const int l = tj + 16 * b;
+            const double al = l == j ? -1.0 : c0[l];
+            e2[b] = fma(-al * dinv0, a1, l == j ? 0.0 : c1[l]);
+          }
+          const double d1 = fma(-a1 * dinv0, a1, c1[j + 1]);
+          bad = bad || (d1 != d1);
+          const double dinv1 = d1 > 1e-200 ? 1.0 / d1 : 0.0;
+          if (tid > j && tid < mk) {
+            const double at = c0[tid];
+            Lf[(long long)(j + 1) * mk + tid] = fma(-at * dinv0, a1, c1[tid]);
+          }
+          step(j, c0, dinv0);
+          // pivot j + 1 with the column formed above (a_{j+1} = -1)
+#pragma unroll
+          for (int a = 0; a < R; ++a) {
+            const int i = ti + 16 * a;
+            const double bi = i == j + 1 ? -1.0 : e1[a];
+            const double f = -bi * dinv1;
+#pragma unroll
+            for (int b = 0; b < R; ++b) {
+              const int l = tj + 16 * b;
+              const double bl = l == j + 1 ? -1.0 : e2[b];
+              const double base = (i == j + 1 || l == j + 1) ? 0.0 : m[a][b];
+              m[a][b] = fma(f, bl, base);
             }
+          }
+        } else {
+          step(j, c0, dinv0);
         }
-        if (j == mk - 1 && kn >= 0 && tid < L.ng[kn]) S.sgn[tid] = sgv;
+        double* nb = S.col + (((j >> 1) + 1) & 1) * 2 * NZP;
+        publish(j + 2, nb);
+        publish(j + 3, nb + NZP);
+        if (j + 2 >= mk && kn >= 0 && tid < L.ng[kn]) S.sgn[tid] = sgv;
         lds_barrier();
       }
     } else {
@@ -896,7 +1068,7 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
     load_lamdiff(V);
     __syncthreads();
     double lrs = 0.0, lre = 0.0, lri = 0.0, lrc = 0.0, lmu = 0.0;
-    residuals(V, lrs, lre);
+    residuals_staged(V, S, lrs, lre);
     {
       const double *c = V.row(R_C), *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU),
                    *ll = V.row(R_LL), *lu = V.row(R_LU);
@@ -1228,7 +1400,7 @@ extern "C" int cmpc_ocp_debug_stamps(unsigned long long* out, int reset) {
 size_t ocp_lds_bytes(const OcpLayout& L) {
   const int np1 = L.nx + 1, nrm = L.nx + 1 + L.ngmax;
   const size_t pa = (size_t)((np1 * np1 + 1) & ~1);
-  return sizeof(double) * (pa + 2 * (size_t)nrm * L.nzp + 2 * (size_t)L.nzp + 128 + 64 + 64);
+  return sizeof(double) * (pa + 2 * (size_t)nrm * L.nzp + 4 * (size_t)L.nzp + 128 + 64 + 64);
 }
 
 int launch_ocp_ipm(const OcpSolveArgs& a, int B, hipStream_t stream) {
