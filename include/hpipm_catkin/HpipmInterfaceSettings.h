@@ -2,11 +2,14 @@
  * HpipmInterfaceSettings.h — hpipm_interface::Settings (reference
  * ocs2_sqp/hpipm_catkin/include/hpipm_catkin/HpipmInterfaceSettings.h:44-57), same fields and defaults.
  *
- * What the MI355X engine does with them (cheeta-mpc_amd/host/HpipmInterface.cpp): the OCP path is a direct
- * equality-constrained solve, not an interior point method, so only reg_prim acts (added to the input Hessians, as
- * HPIPM's primal regularisation); hpipmMode, iter_max, alpha_min, mu0, the tolerances, warm_start, pred_corr and
- * ric_alg are stored and printed but cannot change the result of a problem without inequalities. The centroidal
- * engine's interior point method (cmpc_settings) honours every field.
+ * What the MI355X engine does with them (cheeta-mpc_amd/host/HpipmInterface.cpp -> cmpc_ocp_create / set_settings):
+ * the OCP path runs HPIPM's interior point method on the device (k_ocp_ipm), so iter_max, alpha_min, mu0 and the four
+ * tolerances act as in HPIPM; reg_prim is the factorisation's primal regularisation (the returned trajectory is the
+ * unregularised problem's). pred_corr must be 1 (the Mehrotra corrector HPIPM's default runs; 0 is refused), ric_alg
+ * 0 or 1 (both give the same Newton steps here: one factorisation form), hpipmMode is accepted and stored (the
+ * device's tolerances, not the mode's presets, decide); warm_start is accepted and the device solve cold-starts, as
+ * HPIPM does at the default warm_start = 0.
+ * The centroidal engine's interior point method (cmpc_settings) honours every field.
  */
 #pragma once
 

@@ -479,3 +479,17 @@ def test_device_pointer_entry_equals_host_entry(cm, op):
     solver.solve_device(B, dx0, drec, dcrec, dx, du, dst, dit)
     assert np.array_equal(dx.host(), x) and np.array_equal(du.host(), u)
     assert np.array_equal(dst.host(), st) and np.array_equal(dit.host(), it)
+
+
+@pytest.mark.gpu
+def test_device_two_per_cu_instantiation_equals_one_per_cu(cm, op):
+    """Batches above 256 run k_ocp_ipm<64, 2> (bounded at 256 VGPRs), smaller ones k_ocp_ipm<64, 1>: same arithmetic,
+    so the same problems give bit-identical results either way."""
+    ps = [ocpgen.legged_problem(500 + i, projected=False) for i in range(8)]
+    _, x1, u1, st1, it1 = _device_batch(cm, ps)
+    big = [ps[i % 8] for i in range(264)]
+    _, x2, u2, st2, it2 = _device_batch(cm, big)
+    for i in range(264):
+        j = i % 8
+        assert st2[i] == st1[j] and it2[i] == it1[j]
+        assert np.array_equal(x2[i], x1[j]) and np.array_equal(u2[i], u1[j])
