@@ -493,3 +493,13 @@ def test_device_two_per_cu_instantiation_equals_one_per_cu(cm, op):
         j = i % 8
         assert st2[i] == st1[j] and it2[i] == it1[j]
         assert np.array_equal(x2[i], x1[j]) and np.array_equal(u2[i], u1[j])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [False, True])
+def test_device_wide_stage_class_matches_oracle(cm, op, rows):
+    """nu_k + nx + 1 > 64 takes the NZP = 128 instantiation (k_ocp_ipm<128, 1>): nx = 20, nu_k up to 50."""
+    shape = dict(N=4, nx=20, nu=[50, 30, 45, 10], nc=[0, 6, 3, 4, 2] if rows else None, rows=rows)
+    ps = [_small(90 + i, **shape) for i in range(3)]
+    solver, x, u, st, it = _device_batch(cm, ps)
+    _check_vs_oracle(op, ps, x, u, st, it)
