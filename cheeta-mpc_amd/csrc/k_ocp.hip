@@ -424,27 +424,22 @@ __device__ __forceinline__ HPtrs h_ptrs(const View& V, int k) {
   return H;
 }
 __device__ __forceinline__ double h_load(const HPtrs& H, int nx, int i, int l, double reg) {
+  // branch-free: every candidate offset formed with clamped indices, the pointer picked by selects, one load
+  const int mk = H.mk, nz = H.nz;
+  const bool iu = i < mk, lu = l < mk, ix = i >= mk && i < nz, lx = l >= mk && l < nz;
+  const bool ig = i == nz, lg = l == nz;
+  const int ic = iu ? i : 0, lc = lu ? l : 0, ixc = ix ? i - mk : 0, lxc = lx ? l - mk : 0;
   const double* p = H.gx;
-  bool use = false;
-  double add = 0.0;
-  if (i <= H.nz && l <= H.nz && !(i == H.nz && l == H.nz)) {
-    use = true;
-    if (l == H.nz) {
-      p = i < H.mk ? H.gu + i : H.gx + (i - H.mk);
-    } else if (i == H.nz) {
-      p = l < H.mk ? H.gu + l : H.gx + (l - H.mk);
-    } else if (i < H.mk && l < H.mk) {
-      p = H.R + (long long)l * H.mk + i;
-      add = i == l ? reg : 0.0;
-    } else if (i < H.mk) {
-      p = H.S + (long long)(l - H.mk) * H.mk + i;
-    } else if (l < H.mk) {
-      p = H.S + (long long)(i - H.mk) * H.mk + l;
-    } else {
-      p = H.Q + (long long)(l - H.mk) * nx + (i - H.mk);
-      add = i == l ? reg : 0.0;
-    }
-  }
+  p = (iu && lu) ? H.R + (long long)lc * mk + ic : p;
+  p = (iu && lx) ? H.S + (long long)lxc * mk + ic : p;
+  p = (ix && lu) ? H.S + (long long)ixc * mk + lc : p;
+  p = (ix && lx) ? H.Q + (long long)lxc * nx + ixc : p;
+  p = (lg && iu) ? H.gu + ic : p;
+  p = (lg && ix) ? H.gx + ixc : p;
+  p = (ig && lu) ? H.gu + lc : p;
+  p = (ig && lx) ? H.gx + lxc : p;
+  const bool use = (iu || ix || ig) && (lu || lx || lg) && !(ig && lg);
+  const double add = (i == l && ((iu && lu) || (ix && lx))) ? reg : 0.0;
   const double v = *p;
   return use ? v + add : 0.0;
 }
@@ -577,10 +572,20 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
       const StagePtrs P = stage_ptrs(V, kn);
       const int nrn = np1 + P.g;
       if constexpr (NZP == 64) {
+        // element e = tid + NT s2 is (row wave + 4 s2, column tid % 64): the column's two source pointers (dynamics
+        // rows, constraint rows) are fixed per thread, so each element is one select and one load
+        const int l = tid & 63, r0 = tid >> 6;
+        const double* dyn = l < P.mk ? P.B + (long long)l * nx : (l < P.nz ? P.A + (long long)(l - P.mk) * nx : P.rb);
+        const double* con = l < P.mk ? P.D + (long long)l * P.g : P.C + (long long)(l - P.mk) * P.g;
+        const bool live = l <= P.nz, conl = l < P.nz;
+        const double one = l == P.nz ? 1.0 : 0.0;
 #pragma unroll
         for (int s2 = 0; s2 < StagePrefetch<NZP>::EPT; ++s2) {
-          const int e = tid + NT * s2;
-          pf.v[s2] = e < nrn * NZP ? stage_load(P, nx, e / NZP, e % NZP) : 0.0;
+          const int r = r0 + 4 * s2;
+          const bool dr = r < nx, cr = r > nx && r < nrn && conl;
+          const double* src = dr ? dyn + r : (cr ? con + (r - nx - 1) : P.rb);
+          const double v = *src;
+          pf.v[s2] = (live && dr) ? v : (cr ? v : (r == nx ? one : 0.0));
         }
       }
       sgv = tid < P.g ? V.row(R_SIG)[L.cr[kn] + tid] : 0.0;  // into S.sgn at the sweep's last barrier
@@ -1033,13 +1038,13 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
   double* x = V.x();
   double* u = V.u();
   // --- cold start ---
-  for (int i = tid; i < (N + 1) * nx; i += NT) {
-    x[i] = i < nx ? a.x0[(long long)q * nx + i] : 0.0;
+  for (int i = tid; i < (N + 1) * nx; i += NT) {  // warm: x (nodes >= 1), u from the caller's d_x / d_u
+    x[i] = i < nx ? a.x0[(long long)q * nx + i] : (a.warm ? a.x[(long long)q * (N + 1) * nx + i] : 0.0);
     V.dx()[i] = 0.0;
     V.gx()[i] = 0.0;
     V.rgx()[i] = 0.0;
   }
-  for (int i = tid; i < L.nU; i += NT) u[i] = 0.0;
+  for (int i = tid; i < L.nU; i += NT) u[i] = a.warm ? a.u[(long long)q * L.nU + i] : 0.0;
   for (int i = tid; i < N * nx; i += NT) V.pi()[i] = 0.0;
   __syncthreads();
   {

@@ -55,6 +55,7 @@ struct OcpSolveArgs {
   double* stats;       // [B][stat_rows][10] or nullptr
   int stat_rows;
   int iter_max;
+  int warm;  // Settings.warm_start: x (nodes >= 1), u start from x / u (HPIPM's primal warm start)
   double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp, reg;
 };
 

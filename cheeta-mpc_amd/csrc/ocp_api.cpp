@@ -205,6 +205,7 @@ cmpc::OcpSolveArgs solve_args(cmpc_ocp* o, const double* x0, const double* rec, 
   a.stats = o->d_stats;
   a.stat_rows = o->stat_rows;
   a.iter_max = o->s.iter_max;
+  a.warm = (o->s.warm_start != 0 && x && u) ? 1 : 0;
   a.alpha_min = o->s.alpha_min;
   a.mu0 = o->s.mu0;
   a.tol_stat = o->s.tol_stat;
@@ -382,6 +383,10 @@ int cmpc_ocp_solve_host(cmpc_ocp* o, int B, const double* x0, const double* rec,
   ck(hipMemcpyAsync(o->d_x0, x0, sizeof(double) * B * o->nx, hipMemcpyHostToDevice, st));
   ck(hipMemcpyAsync(o->d_rec, rec, sizeof(double) * B * o->rec_size, hipMemcpyHostToDevice, st));
   if (o->m > 0) ck(hipMemcpyAsync(o->d_crec, crec, sizeof(double) * B * o->crec_size, hipMemcpyHostToDevice, st));
+  if (o->s.warm_start) {  // x, u are in / out: the initial guess (HPIPM's primal warm start)
+    ck(hipMemcpyAsync(o->d_x, x, sizeof(double) * B * NP * o->nx, hipMemcpyHostToDevice, st));
+    if (o->nU > 0) ck(hipMemcpyAsync(o->d_u, u, sizeof(double) * B * o->nU, hipMemcpyHostToDevice, st));
+  }
   if (r != CMPC_OK) return r;
   r = cmpc_ocp_solve(o, B, o->d_x0, o->d_rec, o->d_crec, o->d_x, o->d_u, o->d_status, o->d_iters, st);
   if (r != CMPC_OK) return r;

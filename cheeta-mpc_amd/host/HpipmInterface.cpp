@@ -125,8 +125,9 @@ class HpipmInterface::Impl {
     const int nx = p.nx;
     int nU = 0;
     for (int v : p.nu) nU += v;
-    xbuf_.assign((size_t)(N + 1) * nx, 0.0);
-    ubuf_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
+    // with Settings::warm_start the last solution of the same size is the initial guess (HPIPM keeps it in qp_sol)
+    if (!settings_.warm_start || xbuf_.size() != (size_t)(N + 1) * nx) xbuf_.assign((size_t)(N + 1) * nx, 0.0);
+    if (!settings_.warm_start || ubuf_.size() != (size_t)(nU > 0 ? nU : 1)) ubuf_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
     std::vector<double> x0p((size_t)nx, 0.0);
     for (int i = 0; i < p.nxk[0]; ++i) x0p[(size_t)i] = x0(i);
     int status = -1, iters = 0;

@@ -532,15 +532,18 @@ class OcpSolver:
         _chk(lib().cmpc_ocp_set_settings(self.h, C.byref(s)), "cmpc_ocp_set_settings")
         self.stat_rows = lib().cmpc_ocp_stat_rows(self.h)
 
-    def solve(self, x0, rec, crec=None):
-        """Host path (cmpc_ocp_solve_host): x0 [B,nx], rec [B,rec_size], crec [B,crec_size]. Returns x [B,N+1,nx],
-        u [B,nU], status [B], iters [B]."""
+    def solve(self, x0, rec, crec=None, guess=None):
+        """Host path (cmpc_ocp_solve_host): x0 [B,nx], rec [B,rec_size], crec [B,crec_size]; guess = (x, u), the
+        initial guess read when the settings' warm_start is set. Returns x [B,N+1,nx], u [B,nU], status [B], iters."""
         x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)
         B = x0.shape[0]
         rec = np.ascontiguousarray(rec, np.float64).reshape(B, self.rec_size)
         cr = None if self.m == 0 else np.ascontiguousarray(crec, np.float64).reshape(B, self.crec_size)
         x = np.zeros((B, self.N + 1, self.nx))
         u = np.zeros((B, max(self.nU, 1)))
+        if guess is not None:
+            x[:] = np.asarray(guess[0], np.float64).reshape(B, self.N + 1, self.nx)
+            u[:, :self.nU] = np.asarray(guess[1], np.float64).reshape(B, self.nU)
         st = np.zeros(B, np.int32)
         it = np.zeros(B, np.int32)
         _chk(lib().cmpc_ocp_solve_host(self.h, B, _dp(x0), _dp(rec), _dp(cr), _dp(x), _dp(u), _dp(st), _dp(it)),

@@ -314,7 +314,9 @@ int cmpc_ocp_destroy(cmpc_ocp* ocp);
 int cmpc_ocp_set_settings(cmpc_ocp* ocp, const cmpc_settings* settings);
 /* Device pointers, asynchronous on stream: d_x0 [B][nx], d_rec [B][record], d_crec [B][constraint record] (NULL when
  * the handle has no rows), d_x [B][(N+1)][nx], d_u [B][sum nu], d_status [B] (HPIPM codes 0..3), d_iters [B] (may be
- * NULL). The records must stay valid until cmpc_ocp_riccati of this solve has run, if it is called. */
+ * NULL). The records must stay valid until cmpc_ocp_riccati of this solve has run, if it is called. With
+ * settings.warm_start != 0, d_x (nodes 1..N) and d_u are read first as the initial guess (HPIPM's primal warm start:
+ * slacks and multipliers start by the cold-start rule from it), as cmpc_ocp_solve_host's x and u then are. */
 int cmpc_ocp_solve(cmpc_ocp* ocp, int B, const double* d_x0, const double* d_rec, const double* d_crec, double* d_x,
                    double* d_u, int* d_status, int* d_iters, void* stream);
 /* Host pointers: one copy in (records into the handle's device buffers), the solve, one copy back; synchronous. */

@@ -396,7 +396,13 @@ int oracle_ocp_ipm(int N, int nx, const int* nu, const int* nc, const double* x0
     const int r = nc ? nc[k] : 0;
     for (int j = 0; j < r; ++j) lg[p.cr[k] + j] = ug[p.cr[k] + j] = -crec[p.oe[k] + j];
   }
-  /* cold start: u = 0, x = 0 (node 0 = x0), pi = 0; t = max(slack, THR0), lam = mu0 / t */
+  /* cold start: u = 0, x = 0 (node 0 = x0), pi = 0; t = max(slack, THR0), lam = mu0 / t. warm_start != 0 (HPIPM's
+   * primal warm start): x (nodes 1..N) and u start from the caller's xout / uout, slacks and multipliers by the
+   * same rule from C x + D u */
+  if (s->warm_start && xout && uout) {
+    memcpy(x + nx, xout + nx, sizeof(double) * (nX - (size_t)nx));
+    if (nU) memcpy(u, uout, sizeof(double) * (size_t)nU);
+  }
   memcpy(x, x0, sizeof(double) * nx);
   rows_eval(&p, x, u, c);
   for (int j = 0; j < m; ++j) {

@@ -499,7 +499,7 @@ class OcpRic(C.Structure):
                 ("k", C.POINTER(C.c_double)), ("Lr", C.POINTER(C.c_double))]
 
 
-def ocp_ipm(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, ric=False, stats_rows=0):
+def ocp_ipm(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, ric=False, stats_rows=0, guess=None):
     """Stage-wise OCP IPM (oracle/ocp_ipm.c). Returns dict: x [(N+1),nx], u [nU], status, iters, res [4], and with
     ric=True P [(N+1),nx,nx], p [(N+1),nx], K (list of nu_k x nx), k (list), Lr (list, lower); stats [rows,10]."""
     s = settings if settings is not None else default_settings()
@@ -511,6 +511,9 @@ def ocp_ipm(N, nx, nu, x0, rec, nc=None, crec=None, settings=None, ric=False, st
         nca = None
     x = np.zeros((N + 1) * nx)
     u = np.zeros(max(nU, 1))
+    if guess is not None:  # initial guess (x [(N+1), nx], u [nU]); read when settings.warm_start != 0
+        x[:] = np.asarray(guess[0], np.float64).reshape(-1)
+        u[:nU] = np.asarray(guess[1], np.float64).reshape(-1)[:nU]
     it = C.c_int(0)
     res = np.zeros(4)
     st_rows = np.full((max(stats_rows, 1), 10), np.nan)

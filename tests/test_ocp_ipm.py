@@ -503,3 +503,44 @@ def test_device_wide_stage_class_matches_oracle(cm, op, rows):
     ps = [_small(90 + i, **shape) for i in range(3)]
     solver, x, u, st, it = _device_batch(cm, ps)
     _check_vs_oracle(op, ps, x, u, st, it)
+
+
+def test_oracle_warm_start_from_solution(op):
+    """HPIPM's primal warm start (warm_start = 1): from the converged x, u the IPM needs no more iterations than cold
+    and lands on the same solution."""
+    p = _small(33)
+    r = _oracle(op, p)
+    s = op.default_settings()
+    s.warm_start = 1
+    rec, crec = ocpgen.pack(p)
+    w = op.ocp_ipm(p["N"], p["nx"], p["nu"], p["x0"], rec, nc=p["nc"], crec=crec, settings=s,
+                   guess=(r["x"], r["u"]))
+    assert w["status"] == 0 and w["iters"] <= r["iters"]
+    assert _rel(w["u"], r["u"]) < 1e-8
+
+
+@pytest.mark.gpu
+def test_device_warm_start_matches_oracle(cm, op):
+    """The same warm start on the device (cmpc_ocp_solve_host with x, u in / out): statuses, iterations and the
+    solution equal the oracle's from the same guess (a perturbed solution of the legged problem with rows)."""
+    ps = [ocpgen.legged_problem(600 + i, projected=False) for i in range(3)]
+    p0 = ps[0]
+    s = cm.default_settings()
+    s.warm_start = 1
+    recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+    solver = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), settings=s, max_batch=len(ps))
+    rng = np.random.default_rng(5)
+    guesses = []
+    for p in ps:
+        r = _oracle(op, p)
+        guesses.append((r["x"] + 1e-3 * rng.standard_normal(r["x"].shape), r["u"] + 1e-3 * rng.standard_normal(r["u"].shape)))
+    gx = np.array([g[0] for g in guesses])
+    gu = np.array([g[1] for g in guesses])
+    x, u, st, it = solver.solve(np.array([p["x0"] for p in ps]), np.array(recs), np.array(crecs), guess=(gx, gu))
+    so = op.default_settings()
+    so.warm_start = 1
+    for i, p in enumerate(ps):
+        w = op.ocp_ipm(p["N"], p["nx"], p["nu"], p["x0"], recs[i], nc=p["nc"], crec=crecs[i], settings=so,
+                       guess=guesses[i])
+        assert st[i] == w["status"] and it[i] == w["iters"], (i, st[i], w["status"], it[i], w["iters"])
+        assert _rel(x[i], w["x"]) < 1e-9 and _rel(u[i], w["u"]) < 1e-9
