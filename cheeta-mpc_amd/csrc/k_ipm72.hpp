@@ -6,12 +6,13 @@
 //     [K_AA  K_AB] [x_A]   [r_A]      A = variables 0..63: k_ipm64's 4 x 16-cyclic register tile and elimination
 //     [K_AB' K_BB] [x_B] = [r_B]      B = variables 64..n-1, nb = n - 64 <= NB = 8: LDS
 // solved through the Schur complement:
-//   * K_AA is eliminated in the tile exactly as in k_ipm64 (LDL' with L^-1 in place, DPP row updates, look-ahead);
-//   * W = K_AA^-1 K_AB by nb tile solves and S = K_BB - K_AB' W (by symmetry only k >= l), column l of K_AB overwritten
-//     by W's once the products that need it are taken;
+//   * K_AA is eliminated in the tile exactly as in k_ipm64 (LDL' with L^-1 in place, DPP row updates, look-ahead),
+//     so K_AA^-1 = M' D^-1 M with M unit triangular;
+//   * Y = M K_AB by nb forward half-solves (in place of K_AB) and S = K_BB - K_AB' K_AA^-1 K_AB = K_BB - Y' D^-1 Y (by
+//     symmetry only k >= l): W = K_AA^-1 K_AB is never formed, which saves nb backward half-solves per iteration;
 //   * S^-1 by Gauss-Jordan across the wave: lane 8k + l holds S[k][l], identity-padded to 8 x 8 (S is SPD as a Schur
 //     complement of the SPD K: no pivoting);
-//   * per right-hand side: x_B = S^-1 (r_B - W' r_A), x_A = K_AA^-1 r_A - W x_B (one tile solve).
+//   * per right-hand side: z = D^-1 M r_A, x_B = S^-1 (r_B - Y' z), x_A = M' (z - D^-1 Y x_B) (one tile solve, split).
 // Border variables live in a second per-lane slot (lane k carries variable 64 + k) next to k_ipm64's lane-per-variable
 // slot. H comes from the class-128 block of the workspace (row-major, stride 128) the workgroup condensing wrote. The
 // LDS stays under 20 KB, so 8 waves fit a CU as for k_ipm64: rowbuf and z share bytes, and the tile solve reduces its
@@ -135,8 +136,9 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
   T hu_b = T(0), rhs_b = T(0), rg_b = T(0), du_b = T(0);
   T dtl[2], dtu[2], dll[2], dlu[2];
 
-  // K_AA^-1 y with the eliminated tile, as k_ipm64's solve: X' D^-1 X y over the 40 lower registers
-  auto solve = [&](T& y) {
+  // K_AA^-1 = M' D^-1 M with the eliminated tile (k_ipm64's solve over the 40 lower registers), in two halves:
+  // fwd(y) = M y, bwd(z) = M' z
+  auto fwd = [&](T y) -> T {
     const int ol = olane();
     const int ola = ol >> 4, olb = ol & 15;
     L.v[ol] = y * invd_v;
@@ -169,7 +171,11 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
         cbar();
       });
     }
-    const T z = (y - sv) * invd_v;
+    return y - sv;
+  };
+  auto bwd = [&](T z) -> T {
+    const int ol = olane();
+    const int ola = ol >> 4, olb = ol & 15;
     L.z[(ol & 3) * ipm64::ZS + (ol >> 2)] = z;
     cbar();
     T zr[16];
@@ -188,7 +194,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     cbar();
     const T qs = (L.scr[ol] + L.scr[64 + ol]) + (L.scr[128 + ol] + L.scr[192 + ol]);
     cbar();
-    y = fma(-invd_v, qs, z);
+    return fma(-invd_v, qs, z);
   };
 
   // H_AA into the tile (4 rows x 16 consecutive columns per load) and this lane's row of H_AB into hab (written to
@@ -216,10 +222,11 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     const T ctw = apply_CT(wv, ctw_b);
     rhs_v = -rg_v - ctw;
     rhs_b = bin ? -rg_b - ctw_b : T(0);
-    // t = r_B - W' r_A (lane k), then x_B = S^-1 t
+    // z = D^-1 M r_A; t = r_B - W' r_A = r_B - Y' z (lane k), then x_B = S^-1 t
+    const T z = fwd(rhs_v) * invd_v;
     T tb = rhs_b;
     for (int k = 0; k < nb; ++k) {
-      const T s = wave_sum_dpp(L.kab[k][lane] * rhs_v);
+      const T s = wave_sum_dpp(L.kab[k][lane] * z);
       tb = lane0 == k ? tb - s : tb;
     }
     if (lane < NB) L.xb[lane] = bin ? tb : T(0);
@@ -230,10 +237,11 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     du_b = xk;
     cbar();
     if (lane < NB) L.xb[lane] = du_b;
-    // x_A = K_AA^-1 r_A - W x_B
-    du_v = rhs_v;
-    solve(du_v);
-    for (int k = 0; k < nb; ++k) du_v = fma(-L.kab[k][lane], L.xb[k], du_v);
+    cbar();
+    // x_A = K_AA^-1 (r_A - K_AB x_B) = M' (z - D^-1 Y x_B)
+    T yx = T(0);
+    for (int k = 0; k < nb; ++k) yx = fma(L.kab[k][lane], L.xb[k], yx);
+    du_v = bwd(fma(-invd_v, yx, z));
     L.v[lane] = du_v;
     if (lane < NB) L.v[64 + lane] = du_b;
     cbar();
@@ -526,20 +534,19 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       });
     }
 
-    // ---- W = K_AA^-1 K_AB (column l replaces K_AB's once S's products with it are taken) and S = K_BB - K_AB' W
+    // ---- Y = M K_AB in place of K_AB (forward halves only: W = K_AA^-1 K_AB = M' D^-1 Y is never formed) and
+    // S = K_BB - K_AB' W = K_BB - Y' D^-1 Y (by symmetry only k >= l)
+    for (int l = 0; l < nb; ++l) L.kab[l][lane] = fwd(L.kab[l][lane]);
     for (int l = 0; l < nb; ++l) {
-      T y = L.kab[l][lane];
-      solve(y);
+      const T zl = L.kab[l][lane] * invd_v;
       T sub = T(0);
       for (int k = l; k < nb; ++k) {
-        const T s = wave_sum_dpp(L.kab[k][lane] * y);
+        const T s = wave_sum_dpp(L.kab[k][lane] * zl);
         sub = lane0 == k * NB + l || lane0 == l * NB + k ? s : sub;
       }
       L.sb[lane] -= sub;
-      cbar();
-      L.kab[l][lane] = y;
-      cbar();
     }
+    cbar();
     {  // S^-1 by Gauss-Jordan across the wave (lane 8k + l holds S[k][l]); SPD: no pivoting
       const int gk = lane0 >> 3, gl = lane0 & 7;
       T s = L.sb[lane];

@@ -264,32 +264,77 @@ __device__ __forceinline__ double node_load(const View& V, const NodeMats& M, in
                                : V.D(k) + (e - M.oD);
   return *p;
 }
+// The node's vectors staged beside its matrices: r, q, b, x_k, u_k, pi_k, pi_{k-1}, x_{k+1}, w_k, so the node's
+// products read LDS only (a global load inside the dot-product loops is a full memory latency per node at B = 1)
+struct NodeVecs {
+  int o_q, o_b, o_x, o_u, o_pk, o_pm, o_xn, o_w, tot;
+};
+__device__ __forceinline__ NodeVecs node_vecs(const OcpLayout& L, int k) {
+  NodeVecs W;
+  const int nx = L.nx, mk = L.nu[k], g = L.ng[k], nd = k < L.N ? nx : 0;
+  W.o_q = mk;
+  W.o_b = W.o_q + nx;
+  W.o_x = W.o_b + nd;
+  W.o_u = W.o_x + nx;
+  W.o_pk = W.o_u + mk;
+  W.o_pm = W.o_pk + nd;
+  W.o_xn = W.o_pm + (k >= 1 ? nx : 0);
+  W.o_w = W.o_xn + nd;
+  W.tot = W.o_w + g;
+  return W;
+}
+__device__ __forceinline__ double vec_load(const View& V, const NodeVecs& W, int k, int e) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx;
+  const double* p = e < W.o_q    ? V.r(k) + e
+                    : e < W.o_b  ? V.q(k) + (e - W.o_q)
+                    : e < W.o_x  ? V.b(k) + (e - W.o_b)
+                    : e < W.o_u  ? V.x() + (long long)k * nx + (e - W.o_x)
+                    : e < W.o_pk ? V.u() + L.cu[k] + (e - W.o_u)
+                    : e < W.o_pm ? V.pi() + (long long)k * nx + (e - W.o_pk)
+                    : e < W.o_xn ? V.pi() + (long long)(k - 1) * nx + (e - W.o_pm)
+                    : e < W.o_w  ? V.x() + (long long)(k + 1) * nx + (e - W.o_xn)
+                                 : V.row(R_W) + L.cr[k] + (e - W.o_w);
+  return *p;
+}
 __device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, double& rs, double& re) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N;
   const double *x = V.x(), *u = V.u(), *pi = V.pi(), *wl = V.row(R_W);
   double* buf = S.ABx;  // ABx and Tx are contiguous
   const int cap = 2 * S.nrm * S.nzp;
-  constexpr int EPR = 16;
-  auto staged = [&](const NodeMats& M) { return M.tot <= cap && M.tot <= EPR * NT; };
-  double pre[EPR];
+  constexpr int EPR = 16, EPV = 2;
+  auto staged = [&](const NodeMats& M, const NodeVecs& W) {
+    return M.tot + W.tot <= cap && M.tot <= EPR * NT && W.tot <= EPV * NT;
+  };
+  double pre[EPR], prv[EPV];
   {
     const NodeMats M0 = node_mats(L, 0);
-    if (staged(M0))
+    const NodeVecs W0 = node_vecs(L, 0);
+    if (staged(M0, W0)) {
       for (int e = tid; e < M0.tot; e += NT) buf[e] = node_load(V, M0, 0, e);
+      for (int e = tid; e < W0.tot; e += NT) buf[M0.tot + e] = vec_load(V, W0, 0, e);
+    }
   }
   __syncthreads();
   for (int k = 0; k <= N; ++k) {
     const NodeMats M = node_mats(L, k);
-    const bool st = staged(M);
+    const NodeVecs W = node_vecs(L, k);
+    const bool st = staged(M, W);
     const int mk = L.nu[k], g = L.ng[k];
     const NodeMats Mn = node_mats(L, k < N ? k + 1 : k);
-    const bool pn = k < N && staged(Mn);
+    const NodeVecs Wn = node_vecs(L, k < N ? k + 1 : k);
+    const bool pn = k < N && staged(Mn, Wn);
     if (pn) {
 #pragma unroll
       for (int q = 0; q < EPR; ++q) {
         const int e = tid + NT * q;
         pre[q] = e < Mn.tot ? node_load(V, Mn, k + 1, e) : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < EPV; ++q) {
+        const int e = tid + NT * q;
+        prv[q] = e < Wn.tot ? vec_load(V, Wn, k + 1, e) : 0.0;
       }
     }
     const double* A = st ? buf : V.A(k);
@@ -299,17 +344,24 @@ __device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, do
     const double* R = st ? buf + M.oR : V.R(k);
     const double* C = st ? buf + M.oC : (g ? V.C(k) : nullptr);
     const double* D = st ? buf + M.oD : (g ? V.D(k) : nullptr);
-    const double* xk = x + (long long)k * nx;
-    const double* uk = u + L.cu[k];
-    const double* wk = wl + L.cr[k];
+    const double* vb = buf + M.tot;
+    const double* rk = st ? vb : V.r(k);
+    const double* qk = st ? vb + W.o_q : V.q(k);
+    const double* bk = st ? vb + W.o_b : V.b(k);
+    const double* xk = st ? vb + W.o_x : x + (long long)k * nx;
+    const double* uk = st ? vb + W.o_u : u + L.cu[k];
+    const double* pk = st ? vb + W.o_pk : pi + (long long)k * nx;
+    const double* pm = st ? vb + W.o_pm : pi + (long long)(k - 1) * nx;
+    const double* xn = st ? vb + W.o_xn : x + (long long)(k + 1) * nx;
+    const double* wk = st ? vb + W.o_w : wl + L.cr[k];
     const int n1 = mk, n2 = k >= 1 ? nx : 0, n3 = k < N ? nx : 0;
     for (int e = tid; e < n1 + n2 + n3; e += NT) {
       if (e < n1) {
         const int a = e;
-        double s = V.r(k)[a];
+        double s = rk[a];
         for (int c = 0; c < mk; ++c) s = fma(R[c * mk + a], uk[c], s);
         for (int j = 0; j < nx; ++j) s = fma(Sm[j * mk + a], xk[j], s);
-        for (int t = 0; t < nx; ++t) s = fma(Bm[a * nx + t], pi[(long long)k * nx + t], s);
+        for (int t = 0; t < n3; ++t) s = fma(Bm[a * nx + t], pk[t], s);
         double d = 0.0;
         for (int j = 0; j < g; ++j) d = fma(D[a * g + j], wk[j], d);
         s -= d;
@@ -317,11 +369,10 @@ __device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, do
         rs = nmax(rs, fabs(s));
       } else if (e < n1 + n2) {
         const int i = e - n1;
-        double s = V.q(k)[i] - pi[(long long)(k - 1) * nx + i];
+        double s = qk[i] - pm[i];
         for (int j = 0; j < nx; ++j) s = fma(Q[j * nx + i], xk[j], s);
         for (int a = 0; a < mk; ++a) s = fma(Sm[i * mk + a], uk[a], s);
-        if (k < N)
-          for (int t = 0; t < nx; ++t) s = fma(A[i * nx + t], pi[(long long)k * nx + t], s);
+        for (int t = 0; t < n3; ++t) s = fma(A[i * nx + t], pk[t], s);
         double d = 0.0;
         for (int j = 0; j < g; ++j) d = fma(C[i * g + j], wk[j], d);
         s -= d;
@@ -329,7 +380,7 @@ __device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, do
         rs = nmax(rs, fabs(s));
       } else {
         const int i = e - n1 - n2;
-        double s = V.b(k)[i] - x[(long long)(k + 1) * nx + i];
+        double s = bk[i] - xn[i];
         for (int j = 0; j < nx; ++j) s = fma(A[j * nx + i], xk[j], s);
         for (int a = 0; a < mk; ++a) s = fma(Bm[a * nx + i], uk[a], s);
         V.rb()[(long long)k * nx + i] = s;
@@ -343,6 +394,11 @@ __device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, do
         for (int q = 0; q < EPR; ++q) {
           const int e = tid + NT * q;
           if (e < Mn.tot) buf[e] = pre[q];
+        }
+#pragma unroll
+        for (int q = 0; q < EPV; ++q) {
+          const int e = tid + NT * q;
+          if (e < Wn.tot) buf[Mn.tot + e] = prv[q];
         }
       }
       lds_barrier();
@@ -424,22 +480,28 @@ __device__ __forceinline__ HPtrs h_ptrs(const View& V, int k) {
   return H;
 }
 __device__ __forceinline__ double h_load(const HPtrs& H, int nx, int i, int l, double reg) {
-  // branch-free: every candidate offset formed with clamped indices, the pointer picked by selects, one load
-  const int mk = H.mk, nz = H.nz;
-  const bool iu = i < mk, lu = l < mk, ix = i >= mk && i < nz, lx = l >= mk && l < nz;
-  const bool ig = i == nz, lg = l == nz;
-  const int ic = iu ? i : 0, lc = lu ? l : 0, ixc = ix ? i - mk : 0, lxc = lx ? l - mk : 0;
+  // (a select-only, branch-free form of this was measured 4-9 % slower on MI355X: more VGPRs, more spills)
   const double* p = H.gx;
-  p = (iu && lu) ? H.R + (long long)lc * mk + ic : p;
-  p = (iu && lx) ? H.S + (long long)lxc * mk + ic : p;
-  p = (ix && lu) ? H.S + (long long)ixc * mk + lc : p;
-  p = (ix && lx) ? H.Q + (long long)lxc * nx + ixc : p;
-  p = (lg && iu) ? H.gu + ic : p;
-  p = (lg && ix) ? H.gx + ixc : p;
-  p = (ig && lu) ? H.gu + lc : p;
-  p = (ig && lx) ? H.gx + lxc : p;
-  const bool use = (iu || ix || ig) && (lu || lx || lg) && !(ig && lg);
-  const double add = (i == l && ((iu && lu) || (ix && lx))) ? reg : 0.0;
+  bool use = false;
+  double add = 0.0;
+  if (i <= H.nz && l <= H.nz && !(i == H.nz && l == H.nz)) {
+    use = true;
+    if (l == H.nz) {
+      p = i < H.mk ? H.gu + i : H.gx + (i - H.mk);
+    } else if (i == H.nz) {
+      p = l < H.mk ? H.gu + l : H.gx + (l - H.mk);
+    } else if (i < H.mk && l < H.mk) {
+      p = H.R + (long long)l * H.mk + i;
+      add = i == l ? reg : 0.0;
+    } else if (i < H.mk) {
+      p = H.S + (long long)(l - H.mk) * H.mk + i;
+    } else if (l < H.mk) {
+      p = H.S + (long long)(i - H.mk) * H.mk + l;
+    } else {
+      p = H.Q + (long long)(l - H.mk) * nx + (i - H.mk);
+      add = i == l ? reg : 0.0;
+    }
+  }
   const double v = *p;
   return use ? v + add : 0.0;
 }
@@ -572,20 +634,10 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
       const StagePtrs P = stage_ptrs(V, kn);
       const int nrn = np1 + P.g;
       if constexpr (NZP == 64) {
-        // element e = tid + NT s2 is (row wave + 4 s2, column tid % 64): the column's two source pointers (dynamics
-        // rows, constraint rows) are fixed per thread, so each element is one select and one load
-        const int l = tid & 63, r0 = tid >> 6;
-        const double* dyn = l < P.mk ? P.B + (long long)l * nx : (l < P.nz ? P.A + (long long)(l - P.mk) * nx : P.rb);
-        const double* con = l < P.mk ? P.D + (long long)l * P.g : P.C + (long long)(l - P.mk) * P.g;
-        const bool live = l <= P.nz, conl = l < P.nz;
-        const double one = l == P.nz ? 1.0 : 0.0;
 #pragma unroll
         for (int s2 = 0; s2 < StagePrefetch<NZP>::EPT; ++s2) {
-          const int r = r0 + 4 * s2;
-          const bool dr = r < nx, cr = r > nx && r < nrn && conl;
-          const double* src = dr ? dyn + r : (cr ? con + (r - nx - 1) : P.rb);
-          const double v = *src;
-          pf.v[s2] = (live && dr) ? v : (cr ? v : (r == nx ? one : 0.0));
+          const int e = tid + NT * s2;
+          pf.v[s2] = e < nrn * NZP ? stage_load(P, nx, e / NZP, e % NZP) : 0.0;
         }
       }
       sgv = tid < P.g ? V.row(R_SIG)[L.cr[kn] + tid] : 0.0;  // into S.sgn at the sweep's last barrier
