@@ -217,6 +217,7 @@ CondenseArgs<T> condense_args(cmpc_ctx* c, const double* x0, const double* xref,
   a.nvar = c->nvar;
   a.status = c->status;
   a.n_lo = 0;
+  a.h72 = c->ipm72 ? 1 : 0;
   a.qlist = nullptr;
   a.qcount = nullptr;
   return a;
@@ -387,6 +388,7 @@ template <typename T>
 int run_fused_t(cmpc_ctx* c, int B, const double* x0, const double* xref, const double* foot, const uint8_t* contact,
                 hipStream_t st, hipEvent_t ev1, double* out_u, int* out_status, int* out_iters) {
   CondenseArgs<T> ca = condense_args<T>(c, x0, xref, foot, contact);
+  ca.h72 = 0;  // the fused path's 128 class (k_solve128 / k_ipm128) reads the whole block
   IpmArgs<T> ia = ipm_args<T>(c);
   ia.out_u = out_u;
   ia.out_status = out_status;

@@ -71,6 +71,9 @@ struct CondenseArgs {
                   // nvar[q] = n for every QP, so QPs with nvar[q] <= n_lo exit before any work
   const int* qlist;   // or null: workgroup b < *qcount serves QP qlist[b] (the class list of k_class_lists)
   const int* qcount;
+  // k_ipm72 serves 64 < n <= 72 (cmpc_ctx::ipm72): the 128-class block of such a QP is written for rows and columns
+  // < 80 only (k_ipm72 reads rows and columns < 72; the rest is the identity padding no kernel reads)
+  int h72 = 0;
 };
 
 template <typename T>

@@ -326,7 +326,8 @@ __global__ __launch_bounds__(256) void k_unpack_qp(const T* H_ws, const T* g_ws,
   double* ho = H + (size_t)q * ld * ld;
   for (int e = threadIdx.x; e < ld * ld; e += blockDim.x) {
     const int r = e / ld, c = e % ld;
-    ho[e] = (r < np && c < np) ? (double)hq[h_index_sym(np, r, c)] : (r == c ? 1.0 : 0.0);
+    // the padding rows / columns n.. are the identity (not stored for k_ipm72's QPs, CondenseArgs::h72)
+    ho[e] = (r < n && c < n) ? (double)hq[h_index_sym(np, r, c)] : (r == c ? 1.0 : 0.0);
   }
   for (int i = threadIdx.x; i < ld; i += blockDim.x) g[(size_t)q * ld + i] = i < np ? (double)g_ws[(size_t)q * ld + i] : 0.0;
 }

@@ -478,6 +478,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
 
   // ---- epilogue: Rbar, identity padding, write the class-padded block of H, g and the pyramid data
   const int npad = ipm_class(n);
+  const int hlim = (a.h72 && npad == 128 && n <= 72) ? 80 : npad;  // CondenseArgs::h72
   T* Hq = a.H + (size_t)q * ld * ld;
 #pragma unroll
   for (int p = 0; p < TPW; ++p) {
@@ -485,7 +486,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
     if (idx < NLT) {
       int ti, tj;
       tile_of(idx, ti, tj);
-      if (16 * ti < npad) {
+      if (16 * ti < hlim) {
         const int cc = 16 * tj + (lane & 15);
 #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4) {
