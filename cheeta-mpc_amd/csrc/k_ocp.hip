@@ -652,14 +652,26 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
     //     (parity double buffer, [parity][column][NZP]) before pivot j; every thread forms column j + 1 after pivot j
     //     itself, by the owner's own FMA (bit-identical to one pivot per barrier), then applies both pivots ---
     if (mk > 0) {
-      auto publish = [&](int c, double* dst) {  // owner threads of column c write it (all rows)
+      // owner threads of column c write it (all rows). The register column is picked by selects: written as
+      // m[a][c >> 4] (or a branch per b) the compiler kept m in scratch for a dynamic index, and the reload's
+      // vmcnt wait then also waited out the next stage's prefetch, every pivot pair
+      auto publish = [&](int c, double* dst) {
+        const int cb = c >> 4;
+        double v[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          double t = m[a][0];
+#pragma unroll
+          for (int b = 1; b < R; ++b) {
+            double mb = m[a][b];
+            asm volatile("" : "+v"(mb));  // no select-of-loads fold back into m[a][cb]
+            t = cb == b ? mb : t;
+          }
+          v[a] = t;
+        }
         if (c < mk && tj == (c & 15)) {
 #pragma unroll
-          for (int b = 0; b < R; ++b)
-            if (b == (c >> 4)) {
-#pragma unroll
-              for (int a = 0; a < R; ++a) dst[ti + 16 * a] = m[a][b];
-            }
+          for (int a = 0; a < R; ++a) dst[ti + 16 * a] = v[a];
         }
       };
       // one GJ step with the pivot column pc (all rows) of pivot p: m <- (mask p) - a a' / d, a_p = -1
