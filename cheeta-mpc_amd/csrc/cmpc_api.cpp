@@ -273,13 +273,17 @@ int run_condense_t(cmpc_ctx* c, int B, const double* x0, const double* xref, con
   *lists = false;
   // the one-wave condensing has no foothold columns: with footholds every QP goes through the workgroup kernel
   const bool small = c->model.N <= CMPC_C64_MAXN && !dbar;
+  // footholds, N <= 21, k_ipm72 on: the two-wave foothold condensing takes n <= 72 first (four workgroups per CU
+  // against two for the 128 class's), the 128 class the rest of its list
+  const bool feet72 = dbar && c->ipm72 && c->ld >= 128 && c->model.N <= CMPC_C64_MAXN;
   int r = small ? launch_condense64<T>(a, B, st) : 0;
-  if (r == 0 && !small) r = launch_srbd_condense<T>(a, c->ld < 128 ? 64 : 128, B, st);  // n_lo = 0: classes 64, 128
+  if (r == 0 && feet72) r = launch_srbd_condense<T>(a, 72, B, st);
+  else if (r == 0 && !small) r = launch_srbd_condense<T>(a, c->ld < 128 ? 64 : 128, B, st);  // n_lo = 0: 64, 128
   if (r != 0 || c->ld < 128) return r;
   if (launch_class_lists(c->status, c->nvar, B, 0, c->qlist, c->qcount, st) != 0) return -2;
   *lists = true;
-  if (small) {
-    a.n_lo = 64;
+  if (small || feet72) {
+    a.n_lo = feet72 ? 72 : 64;
     a.qlist = c->qlist + (size_t)1 * B;
     a.qcount = c->qcount + 1;
     r = launch_srbd_condense<T>(a, 128, B, st);

@@ -4,7 +4,7 @@
 
 namespace cmpc {
 
-template <typename T, int NMAX, int WAVES, bool FEET>
+template <typename T, int NMAX, int WAVES, bool FEET, int HN = MAXN>
 __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a) {
   int q = blockIdx.x;
   if (a.qlist) {  // class list: this class's QPs first, the surplus workgroups exit
@@ -20,7 +20,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_srbd_condense(CondenseArgs<T> a)
     }
     return;
   }
-  (void)srbd_condense_qp<T, NMAX, WAVES, false, FEET>(a, q, nullptr);
+  (void)srbd_condense_qp<T, NMAX, WAVES, false, FEET, HN>(a, q, nullptr);
 }
 
 template <typename T>
@@ -29,6 +29,10 @@ int launch_srbd_condense(const CondenseArgs<T>& a, int npad, int B, hipStream_t 
   if (npad > a.ld) return -1;
   const bool feet = a.dbar != nullptr;  // foothold columns (cmpc_nlp_solve_batch): the FEET instantiations
   switch (npad) {
+    case 72:  // foothold QPs with n <= 72 for k_ipm72 (N <= CMPC_C64_MAXN, h72 set): two waves, four workgroups per CU
+      if (!feet || !a.h72) return -1;  // the caller checks N <= CMPC_C64_MAXN
+      hipLaunchKernelGGL((k_srbd_condense<T, 80, 2, true, CMPC_C64_MAXN + 1>), dim3(B), dim3(128), 0, stream, a);
+      break;
     case 64:
       if (feet) hipLaunchKernelGGL((k_srbd_condense<T, 64, 4, true>), dim3(B), dim3(256), 0, stream, a);
       else hipLaunchKernelGGL((k_srbd_condense<T, 64, 4, false>), dim3(B), dim3(256), 0, stream, a);

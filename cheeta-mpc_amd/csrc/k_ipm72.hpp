@@ -23,6 +23,35 @@
 
 namespace cmpc {
 
+// Lab instrumentation (-DCMPC_IPM72_STAMPS, lab/ipm72_stamps.sh only, never in libcmpc.so): per-wave shader-clock
+// cycles per phase, summed over every QP into ipm72_stamp_acc (read by cmpc_ipm72_debug_stamps). Phases: 0 H +
+// residuals, 1 Newton blocks, 2 LDL' of K_AA, 3 Y = M K_AB, 4 S, 5 S^-1, 6 predictor, 7 corrector, 8 update,
+// 9 iterations, 10 total.
+#ifdef CMPC_IPM72_STAMPS
+__device__ unsigned long long ipm72_stamp_acc[16];
+#define I72_DECL                                                  \
+  unsigned long long i72_acc_[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+  const unsigned long long i72_t0_ = __builtin_amdgcn_s_memtime();  \
+  unsigned long long i72_prev_ = i72_t0_
+#define I72(id)                                                   \
+  do {                                                            \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    i72_acc_[id] += now_ - i72_prev_;                             \
+    i72_prev_ = now_;                                             \
+  } while (0)
+#define I72_STORE(iters)                                                                  \
+  do {                                                                                    \
+    i72_acc_[9] = (unsigned long long)(iters);                                            \
+    i72_acc_[10] = __builtin_amdgcn_s_memtime() - i72_t0_;                                \
+    if (threadIdx.x == 0)                                                                 \
+      for (int k_ = 0; k_ < 11; ++k_) atomicAdd(&ipm72_stamp_acc[k_], i72_acc_[k_]);      \
+  } while (0)
+#else
+#define I72_DECL (void)0
+#define I72(id) (void)0
+#define I72_STORE(iters) (void)0
+#endif
+
 namespace ipm72 {
 
 constexpr int NP = 128;  // row stride of the class-128 H block
@@ -271,6 +300,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
 
   int status = CMPC_MAX_ITER;
   int it = 0;
+  I72_DECL;
   for (it = 0;; ++it) {
     progress_prio(it);
     load_H();
@@ -384,6 +414,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       break;
     }
 
+    I72(0);
     // ---- Newton matrix K = H + C' diag(lam_l/t_l + lam_u/t_u) C + reg I: 3x3 block rows of both slots
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
@@ -456,6 +487,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     }
     cbar();
 
+    I72(1);
     // ---- LDL' of K_AA in the tile (k_ipm64's elimination; every pivot is real here)
     T piv = readlane(K[0], 0);
     T invd = pivot_inv(piv);
@@ -523,6 +555,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
         break;
       }
     }
+    I72(2);
     {  // strict lower part S only in the 16 registers that straddle the diagonal
       const int la_m = lane0 >> 4, lb_m = lane0 & 15;
       sfor<0, 4>([&](auto c_) {
@@ -537,6 +570,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     // ---- Y = M K_AB in place of K_AB (forward halves only: W = K_AA^-1 K_AB = M' D^-1 Y is never formed) and
     // S = K_BB - K_AB' W = K_BB - Y' D^-1 Y (by symmetry only k >= l)
     for (int l = 0; l < nb; ++l) L.kab[l][lane] = fwd(L.kab[l][lane]);
+    I72(3);
     for (int l = 0; l < nb; ++l) {
       const T zl = L.kab[l][lane] * invd_v;
       T sub = T(0);
@@ -547,6 +581,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       L.sb[lane] -= sub;
     }
     cbar();
+    I72(4);
     {  // S^-1 by Gauss-Jordan across the wave (lane 8k + l holds S[k][l]); SPD: no pivoting
       const int gk = lane0 >> 3, gl = lane0 & 7;
       T s = L.sb[lane];
@@ -569,6 +604,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       cbar();
     }
 
+    I72(5);
     // ---- predictor (affine scaling direction)
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
@@ -598,6 +634,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
         sr[1] = (double)maff;
         sr[2] = (double)sigma;
       }
+      I72(6);
       // ---- corrector: rm = t.lam + dt_aff.dlam_aff - sigma mu
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc) {
@@ -615,6 +652,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       double* sr = st_row();
       sr[3] = sr[4] = (double)alpha;
     }
+    I72(7);
     if (uflag(alpha < T(S.alpha_min))) {
       status = CMPC_MIN_STEP;
       break;
@@ -641,7 +679,9 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       ll[cc] = fma(alpha, dll[cc], ll[cc]);
       lu[cc] = fma(alpha, dlu[cc], lu[cc]);
     }
+    I72(8);
   }
+  I72_STORE(it);
 
   lane = olane();
   const bool fin = isfinite(u_v) && isfinite(u_b);

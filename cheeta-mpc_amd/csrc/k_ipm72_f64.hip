@@ -11,3 +11,15 @@ int launch_ipm72(const IpmArgs<double>& a, int B, hipStream_t stream) {
 }
 
 }  // namespace cmpc
+
+#ifdef CMPC_IPM72_STAMPS
+extern "C" int cmpc_ipm72_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cmpc::ipm72_stamp_acc), sizeof(unsigned long long) * 16) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cmpc::ipm72_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

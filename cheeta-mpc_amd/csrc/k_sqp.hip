@@ -44,16 +44,25 @@ constexpr double SQP_COST_TOL = 1e-4;
 // iterate / QP solution forces and foothold offsets. Dynamic LDS, sqp_lds_bytes(N).
 struct View {
   double *x0, *xr, *des, *pb, *S2, *u0, *u1, *D0, *D1;
+  double* lt;  // k_sqp_step only: the CoM path c_k [N][3] of the rollouts of lanes 0..3 and 14 (trial_slot)
   uint8_t* ct;
   int* rs;
 };
 
-__host__ __device__ inline size_t sqp_lds_doubles(int N) { return 16 + (size_t)(N + 1) * (NX + NL * 3) + (size_t)N * (NL * 3 + 9 + 4 * NU); }
-__host__ __device__ inline size_t sqp_lds_bytes(int N) {
-  return sqp_lds_doubles(N) * 8 + (size_t)N * NL * (sizeof(int) + 1);
+// k_sqp_step: the rollouts of alpha = 1, 1/2, 1/4, 1/8 (lanes 0..3) and of the current iterate (lane 14) keep their
+// CoM path in View::lt (3 N doubles each: the LDS stays small enough for every QP of a 4096 batch to be resident)
+constexpr int SQP_TRIALS = 5;
+__device__ __forceinline__ int trial_slot(int lane) { return lane < 4 ? lane : (lane == 14 ? 4 : -1); }
+
+__host__ __device__ inline size_t sqp_lds_doubles(int N, bool trial) {
+  return 16 + (size_t)(N + 1) * (NX + NL * 3) + (size_t)N * (NL * 3 + 9 + 4 * NU) +
+         (trial ? (size_t)SQP_TRIALS * N * 3 : 0);
+}
+__host__ __device__ inline size_t sqp_lds_bytes(int N, bool trial) {
+  return sqp_lds_doubles(N, trial) * 8 + (size_t)N * NL * (sizeof(int) + 1);
 }
 
-__device__ View carve(unsigned char* sm, int N) {
+__device__ View carve(unsigned char* sm, int N, bool trial) {
   View V;
   double* p = reinterpret_cast<double*>(sm);
   V.x0 = p; p += 16;
@@ -65,6 +74,7 @@ __device__ View carve(unsigned char* sm, int N) {
   V.u1 = p; p += N * NU;
   V.D0 = p; p += N * NU;
   V.D1 = p; p += N * NU;
+  V.lt = p; p += trial ? SQP_TRIALS * N * 3 : 0;
   V.rs = reinterpret_cast<int*>(p);
   V.ct = reinterpret_cast<uint8_t*>(V.rs + N * NL);
   return V;
@@ -72,10 +82,10 @@ __device__ View carve(unsigned char* sm, int N) {
 
 // Stage QP q (every lane calls; u1 / D0 / D1 may be null: not staged). The caller syncs before reading.
 __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* u0, const double* u1, const double* D0,
-                      const double* D1) {
+                      const double* D1, bool trial = false) {
   const DevModel* M = a.model;
   const int N = M->N, lane = threadIdx.x;
-  View V = carve(sm, N);
+  View V = carve(sm, N, trial);
   const double* xr = a.xref + (size_t)q * (N + 1) * NX;
   const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
   const uint8_t* ct = a.contact + (size_t)q * N * NL;
@@ -155,7 +165,7 @@ __device__ double foot_cost(const DevModel* M, const View& V, const double* D1, 
 // later runs' footholds D0 + alpha (D1 - D0) (has_u1 false: D0) in the lever arm plus their tracking cost. Writes
 // lin [N][6] and x [(N+1)][13] when non-null. Mirrors oracle_nlp_rollout_cost_feet operation for operation.
 __device__ double rollout_cost(const DevModel* M, const View& V, bool has_u1, double alpha, double* lin, double* xo,
-                               bool feet) {
+                               bool feet, double* cpath = nullptr) {
   const int N = M->N;
   const double dt = M->dt;
   const double* u0 = V.u0;
@@ -206,6 +216,8 @@ __device__ double rollout_cost(const DevModel* M, const View& V, bool has_u1, do
         lin[k * 6 + d] = xs[d];
         lin[k * 6 + 3 + d] = F[d];
       }
+    if (cpath)
+      for (int d = 0; d < 3; ++d) cpath[k * 3 + d] = xs[d];
     for (int j = 0; j < NU; ++j) {
       const int i = j / 3;
       const double fd = (j % 3 == 2 && V.ct[k * NL + i] && ns > 0) ? M->mass * GRAV / (double)ns : 0.0;
@@ -405,15 +417,20 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     }
     return;
   }
-  View V = stage(a, q, sqp_lds, uj, uq, dj, dq);
+  View V = stage(a, q, sqp_lds, uj, uq, dj, dq, true);
   __syncthreads();
   // lanes m < 14: trial step alpha = 2^-m; lane 14: the current iterate; lane 15: |dx| and the descent metric;
-  // lane 16: |du| (sequential, the oracle's order)
+  // lane 16: |du| (sequential, the oracle's order). Lanes 0..3 and 14 keep their rollout's CoM path: when the accepted
+  // trial is one of them (or no step is taken) the next linearisation point is copied out instead of rolled out again
+  // (the iterate u0 + alpha (u1 - u0) is formed by the same operations as the trial's inputs, so its rollout is the
+  // trial's bit for bit; F_k is re-summed lane-parallel in the rollout's order)
   double J = 0.0, aux = 0.0;
+  const int ts = trial_slot(lane);
+  double* cp = ts >= 0 ? V.lt + (size_t)ts * N * 3 : nullptr;
   if (lane < 14) {
-    J = rollout_cost(M, V, true, ldexp(1.0, -lane), nullptr, nullptr, feet);
+    J = rollout_cost(M, V, true, ldexp(1.0, -lane), nullptr, nullptr, feet, cp);
   } else if (lane == 14) {
-    J = rollout_cost(M, V, false, 0.0, nullptr, nullptr, feet);
+    J = rollout_cost(M, V, false, 0.0, nullptr, nullptr, feet, cp);
   } else if (lane == 15) {
     J = linstep_metric(M, V, &aux, feet);
   } else if (lane == 16) {
@@ -456,7 +473,24 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     }
   const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
   __syncthreads();
-  if (lane == 0) {
+  const int sel = trial_slot(ma >= 0 ? ma : 14);
+  if (sel >= 0) {
+    const double* cs = V.lt + (size_t)sel * N * 3;
+    double* lo = a.lin + (size_t)q * N * 6;
+    for (int i = lane; i < N * 6; i += 64) {
+      const int k = i / 6, d = i % 6;
+      double v;
+      if (d < 3) {
+        v = cs[k * 3 + d];
+      } else {
+        v = 0.0;
+        for (int l = 0; l < NL; ++l)
+          if (V.ct[k * NL + l]) v += V.u0[k * NU + 3 * l + (d - 3)];
+      }
+      lo[i] = v;
+    }
+    if (lane == 0 && conv) a.done[q] = 1;
+  } else if (lane == 0) {
     if (conv) a.done[q] = 1;
     rollout_cost(M, V, false, 0.0, a.lin + (size_t)q * N * 6, nullptr, feet);
   }
@@ -518,10 +552,10 @@ __global__ __launch_bounds__(256) void k_sqp_count(const int* done, int B, int* 
 int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   if (a.N < 1 || a.N > MAXN) return -1;
-  const size_t lds = sqp_lds_bytes(a.N);
+  const size_t lds = sqp_lds_bytes(a.N, false);
   switch (which) {
     case 0: hipLaunchKernelGGL(k_sqp_init, dim3(B), dim3(64), lds, stream, a); break;
-    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), sqp_lds_bytes(a.N, true), stream, a); break;
     case 2: hipLaunchKernelGGL(k_sqp_final, dim3(B), dim3(64), lds, stream, a); break;
     case 3: hipLaunchKernelGGL(k_sqp_count, dim3(1), dim3(256), 0, stream, a.done, B, a.count); break;
     case 4: hipLaunchKernelGGL(k_sqp_lin, dim3(B), dim3(64), lds, stream, a); break;

@@ -56,7 +56,9 @@ __device__ __forceinline__ void tile_of(int idx, int& ti, int& tj) {
 }
 
 
-template <typename T, int NMAX, int WAVES, bool FEET = false>
+// HN: the longest horizon the per-step arrays hold (MAXN; the small foothold instantiation k_srbd_condense<T, 80, 2,
+// true, C64_HN> holds N <= 21 and fits four workgroups per CU)
+template <typename T, int NMAX, int WAVES, bool FEET = false, int HN = MAXN>
 struct SrbdLds {
   static constexpr int NTRI = NMAX / 3;
   static constexpr int FT = FEET ? NTRI : 1;  // foothold arrays only in the FEET instantiation (LDS of k_solve128)
@@ -66,20 +68,20 @@ struct SrbdLds {
   T s_G[2][16][GS];
   T s_w[2][16];
   T s_q[2][16];
-  double s_xref[(MAXN + 1) * NX];
-  double s_foot[(MAXN + 1) * NL * 3];
-  double s_M[MAXN][9];
-  uint8_t s_e[MAXN * NL];
-  int s_ns[MAXN];
-  int s_cb[MAXN + 1];  // 3 * #triples of steps < k
+  double s_xref[(HN + 1) * NX];
+  double s_foot[(HN + 1) * NL * 3];
+  double s_M[HN][9];
+  uint8_t s_e[HN * NL];
+  int s_ns[HN];
+  int s_cb[HN + 1];  // 3 * #triples of steps < k
   int s_tk[NTRI], s_tleg[NTRI];
-  int s_nt[MAXN];  // triples acting first at step k (stance legs + later runs starting at k)
+  int s_nt[HN];  // triples acting first at step k (stance legs + later runs starting at k)
   // foothold triples (CondenseArgs::dbar): force triple of each stance (k, leg), foothold flag, run end, box (delta)
   // and the run's mean des position
-  int s_slot[FEET ? MAXN * NL : 1];
-  int s_rs[FEET ? MAXN * NL : 1];            // first step of the run of each stance (k, leg)
-  double s_fb[FEET ? MAXN * NU : 1];         // the iterate's forces f_bar [N][12] (CondenseArgs::ubar)
-  double s_D[FEET ? MAXN * NU : 1];          // the iterate's foothold offsets [N][4][3] (CondenseArgs::dbar)
+  int s_slot[FEET ? HN * NL : 1];
+  int s_rs[FEET ? HN * NL : 1];            // first step of the run of each stance (k, leg)
+  double s_fb[FEET ? HN * NU : 1];         // the iterate's forces f_bar [N][12] (CondenseArgs::ubar)
+  double s_D[FEET ? HN * NU : 1];          // the iterate's foothold offsets [N][4][3] (CondenseArgs::dbar)
   uint8_t s_tf[FT];
   int s_te[FT];
   double s_blo[FT][3], s_bhi[FT][3], s_pbar[FT][3];
@@ -96,15 +98,18 @@ struct SrbdLds {
 // Returns n when the QP was condensed here, -1 otherwise (invalid contact table / too large: status written; a
 // bigger class: nvar hint; a smaller class: nothing).
 // FEET: the instantiation that also serves CondenseArgs::dbar (foothold columns); without it dbar is ignored.
-template <typename T, int NMAX, int WAVES, bool EXT, bool FEET = false>
+// NMAX = 80 (the small foothold instantiation) condenses n <= 72 only, the QPs k_ipm72 serves from rows / columns < 80
+// of the class-128 block (CondenseArgs::h72 must be set); bigger ones are left to the 128 class.
+template <typename T, int NMAX, int WAVES, bool EXT, bool FEET = false, int HN = MAXN>
 __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
-                                                srbd::SrbdLds<T, NMAX, WAVES, FEET>* ext) {
+                                                srbd::SrbdLds<T, NMAX, WAVES, FEET, HN>* ext) {
   using namespace srbd;
   constexpr int NT = NMAX / 16;              // 16x16 tiles per dimension
   constexpr int NLT = NT * (NT + 1) / 2;     // lower tiles
   constexpr int TPW = (NLT + WAVES - 1) / WAVES;
   constexpr int NTRI = NMAX / 3;
   constexpr int NTHR = 64 * WAVES;
+  constexpr int NCAP = NMAX == 80 ? 72 : NMAX;  // largest n condensed here
   static_assert(NMAX <= NTHR, "one thread per column");
   using MF = Mfma<T>;
   using acc_t = typename MF::acc_t;
@@ -113,8 +118,8 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   const int N = M->N, L = NL;
   const int ld = a.ld;
 
-  __shared__ SrbdLds<T, NMAX, WAVES, FEET> Sl;  // stand-alone kernel: declared here (constant LDS base)
-  SrbdLds<T, NMAX, WAVES, FEET>& S = EXT ? *ext : Sl;
+  __shared__ SrbdLds<T, NMAX, WAVES, FEET, HN> Sl;  // stand-alone kernel: declared here (constant LDS base)
+  SrbdLds<T, NMAX, WAVES, FEET, HN>& S = EXT ? *ext : Sl;
 
   // ---- load the QP record into LDS
   const double* xr = a.xref + (size_t)q * (N + 1) * NX;
@@ -224,7 +229,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   int st = CMPC_SUCCESS;
   if (S.s_flag & 1) st = CMPC_INVALID_CONTACT;
   else if (S.s_flag & 2) st = CMPC_INFEASIBLE_STEP;
-  else if (n > NMAX) {
+  else if (n > NCAP) {
     if (NMAX < CMPC_IPM_MAX_N) {  // a bigger class follows: leave the hint, not the status
       if (tid == 0) a.nvar[q] = n;
       return -1;

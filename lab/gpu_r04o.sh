@@ -1,0 +1,14 @@
+#!/bin/bash
+# Session script: k_sqp_step lin from the accepted trial lane + two-wave foothold condensing (n <= 72): SQP / NLP
+# tests, then NLP bench A/B against the round's base build on one box.
+O=gpurun_out/r04o; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_feet.py tests/test_sqp.py tests/test_ipm72.py tests/test_reference_nlp.py -m gpu > $O/pytest.log 2>&1; rc=$?; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+nlp() { CMPC_LIB=$2 timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --sqp-iters 10 --nlp --no-e2e --cpu-sample 0 $3 > $O/nlp_$1.json 2>$O/nlp_$1.err || exit 9; python3 -c "import json;d=json.load(open('$O/nlp_$1.json'));print('$1',round(d['value']),round(d['ms_per_step'],4),d['solver'])"; }
+for i in 1 2; do
+  nlp new$i cheeta-mpc_amd/lib/libcmpc.so
+  nlp base$i lab/_ab/libcmpc_base.so
+  nlp newmix$i cheeta-mpc_amd/lib/libcmpc.so "--gait 1"
+  nlp basemix$i lab/_ab/libcmpc_base.so "--gait 1"
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_nlp -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --cpu-sample 0 --steps 5 --warmup 1 --sqp-iters 10 --nlp --no-e2e > $GRAFT_REPO_ROOT/$O/prof_nlp.log 2>&1; echo "prof rc $?"

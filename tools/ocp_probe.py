@@ -14,7 +14,7 @@ import cheeta_mpc as cm  # noqa: E402
 from cheeta_mpc import ocp as gen  # noqa: E402
 
 
-def run(projected, B, reps=5):
+def run(projected, B, reps=int(os.environ.get("OCP_REPS", "5"))):
     H = cm.hip()
     ps = [gen.legged_problem(1000 + (i % 16), projected=projected) for i in range(B)]
     p0 = ps[0]
