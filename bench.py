@@ -384,6 +384,10 @@ def main():
     # profiles/r03_warmup_ab.txt)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
+    # the W warm-up steps are extended, untimed, until the GPU has run the workload for at least this long: a 5-step
+    # warm-up (2.5 ms at the headline) leaves the first timed steps at the idle clock (driver's 20 / 5 command:
+    # 8.14 M QPs/s against 9.11 M at 200 / 50 on the same box, profiles/r04m_bench_*.json); reported as warmup_run
+    ap.add_argument("--min-warmup-s", type=float, default=0.5)
     ap.add_argument("--batch", type=int, default=4096, help="QPs per GPU per step")
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
@@ -504,6 +508,13 @@ def main():
     for i in range(args.warmup):
         step(i)
     H.hipDeviceSynchronize()
+    warmup_run = args.warmup
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < args.min_warmup_s:  # same steps, untimed, synchronised every 8 so the
+        for _ in range(8):                               # condition tracks GPU time rather than the launch queue
+            step(warmup_run)
+            warmup_run += 1
+        H.hipDeviceSynchronize()
 
     direct_step = step
     if args.graph and args.sqp_iters > 0:
@@ -698,6 +709,7 @@ def main():
         "devices": dev_ids,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_run": warmup_run,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",

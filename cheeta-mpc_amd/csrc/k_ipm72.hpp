@@ -78,6 +78,23 @@ struct Lds72 {
   T xb[NB];           // border vector exchange
 };
 
+// 16-lane row reduce-scatter: every lane holds p[0..15]; returns, in the lane at row position b = lane & 15, the sum of
+// p[b] over the 16 lanes of its DPP row. Four pairwise exchanges whose lane flips (row_mirror 1111, row_half_mirror
+// 0111, quad_perm 0010, 0001) are independent over GF(2): each halves the slots a lane keeps (the half whose slot
+// bit equals the lane's), 15 adds per lane in place of 16 LDS partials, a barrier and 16 LDS reads.
+template <typename T>
+__device__ __forceinline__ T row_reduce_scatter16(const T (&p)[16], int b) {
+  const bool b3 = (b & 8) != 0, b2 = (b & 4) != 0, b1 = (b & 2) != 0, b0 = (b & 1) != 0;
+  T q8[8], q4[4], q2[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) q8[k] = (b3 ? p[8 + k] : p[k]) + wdpp::dpp<0x140>(b3 ? p[k] : p[8 + k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q4[k] = (b2 ? q8[4 + k] : q8[k]) + wdpp::dpp<0x141>(b2 ? q8[k] : q8[4 + k]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) q2[k] = (b1 ? q4[2 + k] : q4[k]) + wdpp::dpp<0x4E>(b1 ? q4[k] : q4[2 + k]);
+  return (b0 ? q2[1] : q2[0]) + wdpp::dpp<0xB1>(b0 ? q2[0] : q2[1]);
+}
+
 }  // namespace ipm72
 
 template <typename T, int WPE>
@@ -175,31 +192,21 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     T tc[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) tc[c] = L.v[olb + 16 * c];
-    cbar();
-    // row partials of rows 0..31 (register rows 0..7), then 32..63, each half through the same 512 entries
-    T sv = T(0);
-    {
-      const int base = olb * ipm72::RS2 + ola;
-      sfor<0, 2>([&](auto h_) {
-        constexpr int h = decltype(h_)::value;
-        sfor<8 * h, 8 * h + 8>([&](auto r_) {
-          constexpr int r = decltype(r_)::value;
-          T p = K[r * 4] * tc[0];
-          sfor<1, r / 4 + 1>([&](auto c_) {
-            constexpr int c = decltype(c_)::value;
-            p = fma(K[r * 4 + c], tc[c], p);
-          });
-          L.scr[base + 4 * (r - 8 * h)] = p;
-        });
-        cbar();
-        if ((ol >> 5) == h) {
-          const int il = ol - 32 * h;
-#pragma unroll
-          for (int k = 0; k < 16; k += 2) sv += L.scr[k * ipm72::RS2 + il] + L.scr[(k + 1) * ipm72::RS2 + il];
-        }
-        cbar();
+    // row partials of the 4 x 16-cyclic tile, reduced across each 16-lane row (ipm72::row_reduce_scatter16)
+    T pr[16];
+    sfor<0, 16>([&](auto r_) {
+      constexpr int r = decltype(r_)::value;
+      T acc = K[r * 4] * tc[0];
+      sfor<1, r / 4 + 1>([&](auto c_) {
+        constexpr int c = decltype(c_)::value;
+        acc = fma(K[r * 4 + c], tc[c], acc);
       });
-    }
+      pr[r] = acc;
+    });
+    L.scr[ola + 4 * olb] = ipm72::row_reduce_scatter16(pr, olb);  // row ola + 4 olb
+    cbar();
+    const T sv = L.scr[ol];
+    cbar();
     return y - sv;
   };
   auto bwd = [&](T z) -> T {
@@ -254,10 +261,11 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
     // z = D^-1 M r_A; t = r_B - W' r_A = r_B - Y' z (lane k), then x_B = S^-1 t
     const T z = fwd(rhs_v) * invd_v;
     T tb = rhs_b;
-    for (int k = 0; k < nb; ++k) {
-      const T s = wave_sum_dpp(L.kab[k][lane] * z);
+    sfor<0, NB>([&](auto k_) {  // independent wave sums (zero beyond nb)
+      constexpr int k = decltype(k_)::value;
+      const T s = wave_sum_dpp((k < nb ? L.kab[k][lane] : T(0)) * z);
       tb = lane0 == k ? tb - s : tb;
-    }
+    });
     if (lane < NB) L.xb[lane] = bin ? tb : T(0);
     cbar();
     T xk = T(0);
@@ -569,8 +577,42 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
 
     // ---- Y = M K_AB in place of K_AB (forward halves only: W = K_AA^-1 K_AB = M' D^-1 Y is never formed) and
     // S = K_BB - K_AB' W = K_BB - Y' D^-1 Y (by symmetry only k >= l)
-    for (int l = 0; l < nb; ++l) L.kab[l][lane] = fwd(L.kab[l][lane]);
+    // all nb columns in one pass: row partials of the 4 x 16-cyclic tile reduced across each 16-lane row by
+    // row_reduce_scatter16 (no LDS partials), one LDS exchange and barrier for every column together
+    {
+      const int ol = olane();
+      const int ola = ol >> 4, olb = ol & 15;
+      T ivc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ivc[c] = pivot_inv(L.dg[olb + 16 * c]);  // = invd_v of lane olb + 16 c
+      sfor<0, NB>([&](auto l_) {
+        constexpr int l = decltype(l_)::value;
+        if (l < nb) {
+          T tc[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) tc[c] = L.kab[l][olb + 16 * c] * ivc[c];
+          T pr[16];
+          sfor<0, 16>([&](auto r_) {
+            constexpr int r = decltype(r_)::value;
+            T acc = K[r * 4] * tc[0];
+            sfor<1, r / 4 + 1>([&](auto c_) {
+              constexpr int c = decltype(c_)::value;
+              acc = fma(K[r * 4 + c], tc[c], acc);
+            });
+            pr[r] = acc;
+          });
+          L.scr[l * 64 + ola + 4 * olb] = ipm72::row_reduce_scatter16(pr, olb);  // row ola + 4 olb
+        }
+      });
+      cbar();
+      sfor<0, NB>([&](auto l_) {
+        constexpr int l = decltype(l_)::value;
+        if (l < nb) L.kab[l][ol] = L.kab[l][ol] - L.scr[l * 64 + ol];
+      });
+      cbar();
+    }
     I72(3);
+    // S -= Y' D^-1 Y (by symmetry only k >= l; the unrolled form with independent sums measured slower)
     for (int l = 0; l < nb; ++l) {
       const T zl = L.kab[l][lane] * invd_v;
       T sub = T(0);
