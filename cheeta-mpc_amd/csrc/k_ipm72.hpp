@@ -234,7 +234,7 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
   };
 
   // H_AA into the tile (4 rows x 16 consecutive columns per load) and this lane's row of H_AB into hab (written to
-  // L.kab after the residual work, so no wait on the loads sits in front of it)
+  // L.kab with the Newton blocks, so no wait on the loads sits in front of the residual work)
   T hab[NB];
   auto load_H = [&]() {
     const int ln = olane();
@@ -340,12 +340,13 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       const T wv[2] = {ll[0] - lu[0], ll[1] - lu[1]};
       ctw = apply_CT(wv, ctw_b);
     }
-#pragma unroll
-    for (int k = 0; k < NB; ++k)
-      if (k < nb) L.kab[k][lane] = hab[k];
-    cbar();
-    // ---- H u from H at the first iteration (then carried): tile rows + K_AB (raw H_AB in L.kab) + H_BB
+    // ---- H u from H at the first iteration (then carried): tile rows + K_AB (raw H_AB in L.kab) + H_BB. Later
+    // iterations write H_AB into L.kab only with the Newton blocks, so no wait on its loads sits in the residuals
     if (it == 0) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+        if (k < nb) L.kab[k][lane] = hab[k];
+      cbar();
       T hu = T(0);
       T uc[4];
 #pragma unroll
@@ -480,9 +481,10 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       });
     });
     // K_AB: row lane of border column k gets its block entry when both share a triple (only the triple 63..65)
-    for (int k = 0; k < nb; ++k) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
       const int t3k = 3 * ((64 + k) / 3);
-      if (lane >= t3k) L.kab[k][lane] += L.blk[lane - t3k][64 + k];
+      if (k < nb) L.kab[k][lane] = lane >= t3k ? hab[k] + L.blk[lane - t3k][64 + k] : hab[k];
     }
     {  // K_BB = H_BB + blocks into L.sb (identity-padded)
       const int hk = lane >> 3, hl = lane & 7;
@@ -612,15 +614,31 @@ __device__ __forceinline__ void ipm72_body(const IpmArgs<T>& A, int q) {
       cbar();
     }
     I72(3);
-    // S -= Y' D^-1 Y (by symmetry only k >= l; the unrolled form with independent sums measured slower)
-    for (int l = 0; l < nb; ++l) {
-      const T zl = L.kab[l][lane] * invd_v;
-      T sub = T(0);
-      for (int k = l; k < nb; ++k) {
-        const T s = wave_sum_dpp(L.kab[k][lane] * zl);
-        sub = lane0 == k * NB + l || lane0 == l * NB + k ? s : sub;
+    // S -= Y' D^-1 Y: slot 8 k + l of the 8 x 8 block, products Y_max(k,l) (Y_min(k,l) / d) (so S stays exactly
+    // symmetric), in four groups of 16 slots reduced across each 16-lane row (ipm72::row_reduce_scatter16), then the
+    // four rows' partials through LDS; zero beyond nb
+    {
+      const int ol = olane();
+      const int ola = ol >> 4, olb = ol & 15;
+      T yv[NB], zv[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        yv[k] = k < nb ? L.kab[k][ol] : T(0);
+        zv[k] = yv[k] * invd_v;
       }
-      L.sb[lane] -= sub;
+      sfor<0, 4>([&](auto m_) {
+        constexpr int m = decltype(m_)::value;
+        T pr[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int k = 2 * m + (t >> 3), l = t & 7;
+          pr[t] = k >= l ? yv[k] * zv[l] : yv[l] * zv[k];
+        }
+        L.scr[ola * 64 + 16 * m + olb] = ipm72::row_reduce_scatter16(pr, olb);
+      });
+      cbar();
+      const T sub = (L.scr[ol] + L.scr[64 + ol]) + (L.scr[128 + ol] + L.scr[192 + ol]);
+      L.sb[ol] -= sub;
     }
     cbar();
     I72(4);
