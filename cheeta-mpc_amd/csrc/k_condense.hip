@@ -55,3 +55,15 @@ template int launch_srbd_condense<double>(const CondenseArgs<double>&, int, int,
 template int launch_srbd_condense<float>(const CondenseArgs<float>&, int, int, hipStream_t);
 
 }  // namespace cmpc
+
+#ifdef CMPC_COND_STAMPS
+extern "C" int cmpc_cond_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cmpc::cond_stamp_acc), sizeof(unsigned long long) * 16) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cmpc::cond_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

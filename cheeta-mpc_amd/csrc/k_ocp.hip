@@ -228,6 +228,75 @@ __device__ __forceinline__ void residuals(const View& V, double& rs, double& re)
   }
 }
 
+// Residuals of every node at once: r_gu (u rows), r_gx (x rows, k >= 1) and r_b (dynamics, k < N) of node k depend on
+// that node's data and the current iterate only, so all nodes' outputs are spread over the workgroup (slot e of node k
+// at k P + e, P = nzp + nx >= nu_k + 2 nx) with operands straight from the L2-resident records / iterate and no
+// barrier between nodes; each output is the same fma chain as the node-by-node form (bit-identical). Used for
+// B <= OCP_PAR_RES_MAX (OcpSolveArgs::par_res). Node by node,
+// with ~72 of 256 threads busy and two barriers per node, it held a B = 1 solve 21 % longer (projected; rows 16 %);
+// its L2 traffic is ~2.5x the staged form's, which wins for full batches (-14 % solves/s at B = 256, -11 % at 1024
+// with this form).
+constexpr int OCP_PAR_RES_MAX = 64;
+__device__ __forceinline__ void residuals_par(const View& V, double& rs, double& re) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N;
+  const double *x = V.x(), *u = V.u(), *pi = V.pi(), *wl = V.row(R_W);
+  const int P = L.nzp + nx;
+  for (int w = tid; w < (N + 1) * P; w += NT) {
+    const int k = w / P, e = w - k * P;
+    const int mk = L.nu[k], g = L.ng[k];
+    const int n1 = mk, n2 = k >= 1 ? nx : 0, n3 = k < N ? nx : 0;
+    if (e >= n1 + n2 + n3) continue;
+    const double* A = V.A(k);
+    const double* Bm = V.Bm(k);
+    const double* xk = x + (long long)k * nx;
+    const double* uk = u + L.cu[k];
+    const double* pk = pi + (long long)k * nx;
+    const double* wk = wl + L.cr[k];
+    if (e < n1) {
+      const int a = e;
+      const double *R = V.R(k), *Sm = V.S(k);
+      double s = V.r(k)[a];
+      for (int c = 0; c < mk; ++c) s = fma(R[c * mk + a], uk[c], s);
+      for (int j = 0; j < nx; ++j) s = fma(Sm[j * mk + a], xk[j], s);
+      for (int t = 0; t < n3; ++t) s = fma(Bm[a * nx + t], pk[t], s);
+      double d = 0.0;
+      if (g) {
+        const double* D = V.D(k);
+        for (int j = 0; j < g; ++j) d = fma(D[a * g + j], wk[j], d);
+      }
+      s -= d;
+      V.rgu()[L.cu[k] + a] = s;
+      rs = nmax(rs, fabs(s));
+    } else if (e < n1 + n2) {
+      const int i = e - n1;
+      const double *Q = V.Q(k), *Sm = V.S(k);
+      const double* pm = pi + (long long)(k - 1) * nx;
+      double s = V.q(k)[i] - pm[i];
+      for (int j = 0; j < nx; ++j) s = fma(Q[j * nx + i], xk[j], s);
+      for (int a = 0; a < mk; ++a) s = fma(Sm[i * mk + a], uk[a], s);
+      for (int t = 0; t < n3; ++t) s = fma(A[i * nx + t], pk[t], s);
+      double d = 0.0;
+      if (g) {
+        const double* C = V.C(k);
+        for (int j = 0; j < g; ++j) d = fma(C[i * g + j], wk[j], d);
+      }
+      s -= d;
+      V.rgx()[(long long)k * nx + i] = s;
+      rs = nmax(rs, fabs(s));
+    } else {
+      const int i = e - n1 - n2;
+      const double* xn = x + (long long)(k + 1) * nx;
+      double s = V.b(k)[i] - xn[i];
+      for (int j = 0; j < nx; ++j) s = fma(A[j * nx + i], xk[j], s);
+      for (int a = 0; a < mk; ++a) s = fma(Bm[a * nx + i], uk[a], s);
+      V.rb()[(long long)k * nx + i] = s;
+      re = nmax(re, fabs(s));
+    }
+  }
+  __syncthreads();
+}
+
 // The same residuals one node at a time, the node's matrices staged in LDS (ABx and Tx as one buffer): the
 // transposed products (B'pi, A'pi, S'u, D'w, C'w) read LDS instead of strided global loads, and the next node's
 // matrices are loaded into registers while this one computes. A node whose matrices exceed the staging (nu_k far
@@ -830,64 +899,71 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
 // stage's operands are loaded into registers while this one computes) so that every product operand is an LDS read
 // (B_k consecutive over the rows, K_k broadcast), A_k and rb_k coalesced global loads. A stage whose operands exceed
 // the register staging (nu_k far above nx) reads them from global memory instead.
+// Acl_k = A_k + B_k K_k (k >= 1, with_acl) and bcl_k = rb_k + B_k kff_k for every stage at once: no stage depends on
+// another once the factorisation has produced K and kff, so the work is spread over all stages (4 x 4 blocks of Acl,
+// 4-row blocks of bcl per thread, operands straight from the L2-resident records / workspace) with no barrier
+// between stages; each entry is the same fma chain over a as the per-stage form, so the results are bit-identical
+// (was one stage per barrier with LDS-staged operands: 11 % of a B = 1 solve)
 __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_acl) {
+  (void)S;
   const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
-  constexpr int EPS = 6;  // staged operand doubles per thread
-  auto opn = [&](int k) { return 2 * nx * L.nu[k] + L.nu[k]; };
-  auto fits = [&](int k) { return opn(k) <= EPS * NT && opn(k) <= S.nrm * S.nzp; };
-  auto op_load = [&](int k, int e) -> double {  // operand e of stage k: B_k, then K_k, then kf_k
-    const int nB = nx * L.nu[k];
-    const double* p = e < nB ? V.Bm(k) + e : (e < 2 * nB ? V.K(k) + (e - nB) : V.kf() + L.cu[k] + (e - 2 * nB));
-    return *p;
-  };
-  double st[EPS];
-  if (fits(0)) {
+  const int tid = threadIdx.x, nx = L.nx, N = L.N;
+  const int nb4 = (nx + 3) >> 2;
+  const int pa = with_acl ? nb4 * nb4 : 0;  // Acl blocks per stage
+  const int ps = pa + nb4;                  // + bcl blocks
+  const double* kfv = V.kf();
+  const double* rbv = V.rb();
+  double* bclv = V.bcl();
+  for (int w = tid; w < N * ps; w += NT) {
+    const int k = w / ps, r = w - k * ps;
+    const int mk = L.nu[k];
+    const double* Bk = V.Bm(k);
+    if (r < pa) {
+      if (k == 0) continue;  // dx_0 = 0: Acl_0 is never used
+      const int i0 = 4 * (r / nb4), c0 = 4 * (r - (r / nb4) * nb4);
+      const double* Ak = V.A(k);
+      const double* Kk = V.K(k);
+      double acc[4][4];
 #pragma unroll
-    for (int q = 0; q < EPS; ++q) {
-      const int e = tid + NT * q;
-      if (e < opn(0)) S.ABx[e] = op_load(0, e);
-    }
-  }
-  lds_barrier();
-  for (int k = 0; k < N; ++k) {
-    const int mk = L.nu[k], nB = nx * mk;
-    const bool fk = fits(k);
-    const double* buf = (k & 1) ? S.Tx : S.ABx;
-    const bool pre = k + 1 < N && fits(k + 1);
-    if (pre) {
+      for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-      for (int q = 0; q < EPS; ++q) {
-        const int e = tid + NT * q;
-        st[q] = e < opn(k + 1) ? op_load(k + 1, e) : 0.0;
-      }
-    }
-    const double* Bs = fk ? buf : V.Bm(k);
-    const double* Ks = fk ? buf + nB : V.K(k);
-    const double* ks = fk ? buf + 2 * nB : V.kf() + L.cu[k];
-    const int na = (with_acl && k >= 1) ? nxx : 0;
-    for (int e = tid; e < na + nx; e += NT) {
-      if (e < na) {
-        const int c = e / nx, i = e - c * nx;
-        double s = V.A(k)[e];
-        for (int a = 0; a < mk; ++a) s = fma(Bs[a * nx + i], Ks[c * mk + a], s);
-        V.Acl(k)[e] = s;
-      } else {
-        const int i = e - na;
-        double s = V.rb()[(long long)k * nx + i];
-        for (int a = 0; a < mk; ++a) s = fma(Bs[a * nx + i], ks[a], s);
-        V.bcl()[(long long)k * nx + i] = s;
-      }
-    }
-    if (pre) {
-      double* nbuf = ((k + 1) & 1) ? S.Tx : S.ABx;
+        for (int cc = 0; cc < 4; ++cc) {
+          const int i = i0 + ii, c = c0 + cc;
+          acc[ii][cc] = (i < nx && c < nx) ? Ak[c * nx + i] : 0.0;
+        }
+      for (int aa = 0; aa < mk; ++aa) {
+        double bv[4], kv[4];
 #pragma unroll
-      for (int q = 0; q < EPS; ++q) {
-        const int e = tid + NT * q;
-        if (e < opn(k + 1)) nbuf[e] = st[q];
+        for (int ii = 0; ii < 4; ++ii) bv[ii] = i0 + ii < nx ? Bk[aa * nx + i0 + ii] : 0.0;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) kv[cc] = c0 + cc < nx ? Kk[(c0 + cc) * mk + aa] : 0.0;
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) acc[ii][cc] = fma(bv[ii], kv[cc], acc[ii][cc]);
       }
+      double* Ao = V.Acl(k);
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+          if (i0 + ii < nx && c0 + cc < nx) Ao[(c0 + cc) * nx + i0 + ii] = acc[ii][cc];
+    } else {
+      const int i0 = 4 * (r - pa);
+      const double* kk = kfv + L.cu[k];
+      double acc[4];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) acc[ii] = i0 + ii < nx ? rbv[(long long)k * nx + i0 + ii] : 0.0;
+      for (int aa = 0; aa < mk; ++aa) {
+        const double kv = kk[aa];
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+          acc[ii] = fma(i0 + ii < nx ? Bk[aa * nx + i0 + ii] : 0.0, kv, acc[ii]);
+      }
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+        if (i0 + ii < nx) bclv[(long long)k * nx + i0 + ii] = acc[ii];
     }
-    lds_barrier();
   }
   __syncthreads();
 }
@@ -1094,7 +1170,7 @@ __device__ __forceinline__ void load_lamdiff(const View& V) {
   for (int j = threadIdx.x; j < V.L.m; j += NT) w[j] = ll[j] - lu[j];
 }
 
-template <int NZP>
+template <int NZP, int MINB>
 __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds& S) {
   const View V(a, q);
   const OcpLayout& L = a.L;
@@ -1137,7 +1213,8 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
     load_lamdiff(V);
     __syncthreads();
     double lrs = 0.0, lre = 0.0, lri = 0.0, lrc = 0.0, lmu = 0.0;
-    residuals_staged(V, S, lrs, lre);
+    if (MINB == 1 && a.par_res) residuals_par(V, lrs, lre);  // small batches: all nodes at once (latency)
+    else residuals_staged(V, S, lrs, lre);                  // L2 traffic bounds bigger batches
     {
       const double *c = V.row(R_C), *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU),
                    *ll = V.row(R_LL), *lu = V.row(R_LU);
@@ -1307,7 +1384,7 @@ __global__ __launch_bounds__(NT, MINB) void k_ocp_ipm(OcpSolveArgs a) {
   extern __shared__ double smem[];
   const Lds S = carve(smem, a.L, NZP);
   OCP_STAMP(31);
-  ipm_body<NZP>(a, blockIdx.x, S);
+  ipm_body<NZP, MINB>(a, blockIdx.x, S);
 }
 
 // Riccati quantities at the exit point (see k_ocp.hpp / cmpc.h cmpc_ocp_riccati)
@@ -1472,8 +1549,10 @@ size_t ocp_lds_bytes(const OcpLayout& L) {
   return sizeof(double) * (pa + 2 * (size_t)nrm * L.nzp + 4 * (size_t)L.nzp + 128 + 64 + 64);
 }
 
-int launch_ocp_ipm(const OcpSolveArgs& a, int B, hipStream_t stream) {
+int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {
   if (B <= 0) return 0;
+  OcpSolveArgs a = a0;
+  a.par_res = B <= OCP_PAR_RES_MAX ? 1 : 0;
   const size_t lds = ocp_lds_bytes(a.L);
   if (a.L.nzp == 64) {
     // one problem per CU while the batch leaves CUs idle anyway, two per CU beyond (cmpc_ocp_solve's B)

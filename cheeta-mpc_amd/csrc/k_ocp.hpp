@@ -56,6 +56,7 @@ struct OcpSolveArgs {
   int stat_rows;
   int iter_max;
   int warm;  // Settings.warm_start: x (nodes >= 1), u start from x / u (HPIPM's primal warm start)
+  int par_res;  // residuals of all nodes at once (small batches, set by launch_ocp_ipm) or node by node staged
   double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp, reg;
 };
 

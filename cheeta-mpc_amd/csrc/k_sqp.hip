@@ -350,6 +350,34 @@ __device__ double linstep_metric(const DevModel* M, const View& V, double* dxn, 
 
 extern __shared__ __attribute__((aligned(16))) unsigned char sqp_lds[];
 
+// Lab instrumentation (-DCMPC_SQP_STAMPS, lab/sqp_stamps.sh only, never in libcmpc.so): k_sqp_step's per-wave
+// shader-clock cycles per phase summed over every QP into sqp_stamp_acc (cmpc_sqp_debug_stamps): 0 staging, 1 trial
+// rollouts (lanes 0..13), 2 current iterate (lane 14), 3 linearised response + metric (lane 15), 4 |du| (lane 16),
+// 5 selection + update, 6 next linearisation point; 15 the number of waves.
+#ifdef CMPC_SQP_STAMPS
+__device__ unsigned long long sqp_stamp_acc[16];
+#define SQ_DECL                                                 \
+  unsigned long long sq_acc_[7] = {0, 0, 0, 0, 0, 0, 0};         \
+  unsigned long long sq_prev_ = __builtin_amdgcn_s_memtime()
+#define SQ(id)                                                  \
+  do {                                                          \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    sq_acc_[id] += now_ - sq_prev_;                             \
+    sq_prev_ = now_;                                            \
+  } while (0)
+#define SQ_STORE()                                                                      \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      for (int k_ = 0; k_ < 7; ++k_) atomicAdd(&sqp_stamp_acc[k_], sq_acc_[k_]);        \
+      atomicAdd(&sqp_stamp_acc[15], 1ull);                                              \
+    }                                                                                   \
+  } while (0)
+#else
+#define SQ_DECL (void)0
+#define SQ(id) (void)0
+#define SQ_STORE() (void)0
+#endif
+
 // U_j <- the cold QP's solution, lin <- its rollout; QPs the cold QP rejected are done from the start. With footholds
 // the offsets start at clamp(0, lo, hi) (oracle_feet_init).
 __global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
@@ -417,8 +445,10 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     }
     return;
   }
+  SQ_DECL;
   View V = stage(a, q, sqp_lds, uj, uq, dj, dq, true);
   __syncthreads();
+  SQ(0);
   // lanes m < 14: trial step alpha = 2^-m; lane 14: the current iterate; lane 15: |dx| and the descent metric;
   // lane 16: |du| (sequential, the oracle's order). Lanes 0..3 and 14 keep their rollout's CoM path: when the accepted
   // trial is one of them (or no step is taken) the next linearisation point is copied out instead of rolled out again
@@ -427,13 +457,13 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   double J = 0.0, aux = 0.0;
   const int ts = trial_slot(lane);
   double* cp = ts >= 0 ? V.lt + (size_t)ts * N * 3 : nullptr;
-  if (lane < 14) {
-    J = rollout_cost(M, V, true, ldexp(1.0, -lane), nullptr, nullptr, feet, cp);
-  } else if (lane == 14) {
-    J = rollout_cost(M, V, false, 0.0, nullptr, nullptr, feet, cp);
-  } else if (lane == 15) {
-    J = linstep_metric(M, V, &aux, feet);
-  } else if (lane == 16) {
+  if (lane < 14) J = rollout_cost(M, V, true, ldexp(1.0, -lane), nullptr, nullptr, feet, cp);
+  SQ(1);
+  if (lane == 14) J = rollout_cost(M, V, false, 0.0, nullptr, nullptr, feet, cp);
+  SQ(2);
+  if (lane == 15) J = linstep_metric(M, V, &aux, feet);
+  SQ(3);
+  if (lane == 16) {
     double s2 = 0.0;
     for (int i = 0; i < nu; ++i) {
       const double d = V.u1[i] - V.u0[i];
@@ -446,6 +476,7 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
       }
     aux = sqrt(s2);
   }
+  SQ(4);
   const double J0 = __shfl(J, 14, 64);
   const double metric = __shfl(J, 15, 64), dxn = __shfl(aux, 15, 64), dun = __shfl(aux, 16, 64);
   const double tol = a.tol;
@@ -473,6 +504,7 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     }
   const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
   __syncthreads();
+  SQ(5);
   const int sel = trial_slot(ma >= 0 ? ma : 14);
   if (sel >= 0) {
     const double* cs = V.lt + (size_t)sel * N * 3;
@@ -494,6 +526,8 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
     if (conv) a.done[q] = 1;
     rollout_cost(M, V, false, 0.0, a.lin + (size_t)q * N * 6, nullptr, feet);
   }
+  SQ(6);
+  SQ_STORE();
 }
 
 // Final outputs: u <- U_j, x <- its nonlinear rollout, the foot_pos table (footholds), status stays.
@@ -565,3 +599,15 @@ int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream) {
 }
 
 }  // namespace cmpc
+
+#ifdef CMPC_SQP_STAMPS
+extern "C" int cmpc_sqp_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cmpc::sqp_stamp_acc), sizeof(unsigned long long) * 16) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cmpc::sqp_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

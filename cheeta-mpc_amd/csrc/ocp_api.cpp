@@ -192,6 +192,7 @@ int alloc_stats(cmpc_ocp* o) {
 cmpc::OcpSolveArgs solve_args(cmpc_ocp* o, const double* x0, const double* rec, const double* crec, double* x,
                               double* u, int* status, int* iters) {
   cmpc::OcpSolveArgs a;
+  a.par_res = 0;  // launch_ocp_ipm chooses by batch size
   a.L = o->L;
   a.x0 = x0;
   a.rec = rec;

@@ -26,6 +26,36 @@
 
 namespace cmpc {
 
+// Lab instrumentation (-DCMPC_COND_STAMPS on k_condense.hip only, lab/sqp_stamps.sh, never in libcmpc.so): wave 0 of
+// the two-wave foothold instantiation (NMAX = 80) sums its shader-clock cycles per phase over every QP into
+// cond_stamp_acc (cmpc_cond_debug_stamps): 0 record load + ballots, 1 per-step tables, 2 per-column setup, then per
+// step 3 gamma update, 4 free response (thread 0), 5 block row + barrier, 6 g and MFMA H update; 7 epilogue; 15 QPs.
+#ifdef CMPC_COND_STAMPS
+__device__ unsigned long long cond_stamp_acc[16];
+#define CD_DECL                                                  \
+  unsigned long long cd_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};      \
+  unsigned long long cd_prev_ = __builtin_amdgcn_s_memtime()
+#define CD(id)                                                   \
+  do {                                                           \
+    if constexpr (NMAX == 80) {                                  \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+      cd_acc_[id] += now_ - cd_prev_;                            \
+      cd_prev_ = now_;                                           \
+    }                                                            \
+  } while (0)
+#define CD_STORE()                                                                   \
+  do {                                                                               \
+    if (NMAX == 80 && threadIdx.x == 0) {                                            \
+      for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&cond_stamp_acc[k_], cd_acc_[k_]);    \
+      atomicAdd(&cond_stamp_acc[15], 1ull);                                          \
+    }                                                                                \
+  } while (0)
+#else
+#define CD_DECL (void)0
+#define CD(id) (void)0
+#define CD_STORE() (void)0
+#endif
+
 namespace srbd {
 
 template <typename T>
@@ -121,6 +151,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   __shared__ SrbdLds<T, NMAX, WAVES, FEET, HN> Sl;  // stand-alone kernel: declared here (constant LDS base)
   SrbdLds<T, NMAX, WAVES, FEET, HN>& S = EXT ? *ext : Sl;
 
+  CD_DECL;
   // ---- load the QP record into LDS
   const double* xr = a.xref + (size_t)q * (N + 1) * NX;
   const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
@@ -152,6 +183,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
   const int pre = __popcll(bal & below) + __popcll(balf & below);
   if (lane == 0) S.s_wtot[wave] = __popcll(bal) + __popcll(balf);
   __syncthreads();
+  CD(0);
   int off = 0;
   for (int w = 0; w < wave; ++w) off += S.s_wtot[w];
   int nt = 0;
@@ -225,6 +257,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
       }
   }
   __syncthreads();
+  CD(1);
   const int n = 3 * nt;
   int st = CMPC_SUCCESS;
   if (S.s_flag & 1) st = CMPC_INVALID_CONTACT;
@@ -333,6 +366,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
 
   const T dt = T(M->dt);
   const T dtm = T(M->dt_over_m);
+  CD(2);
   for (int k = 1; k <= N; ++k) {
     const int buf = k & 1;
     const int km = k - 1;
@@ -382,6 +416,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
         }
       }
     }
+    CD(3);
     // (b) free response and weighted tracking error w_k = Q_k (x_hat_k - xref_k)
     if (tid == 0) {
       double xn[NX];
@@ -415,12 +450,14 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
         S.s_w[buf][s] = T(qd * (xn[s] - S.s_xref[k * NX + s]));
       }
     }
+    CD(4);
     // (c) stage block row Bqp_k
     if (c < NMAX) {
 #pragma unroll
       for (int s = 0; s < NX; ++s) S.s_G[buf][s][c] = gam[s];
     }
     __syncthreads();
+    CD(5);
     // (d) g += Bqp_k' w_k
     if (col) {
       T acc_g = T(0);
@@ -478,6 +515,7 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
         }
       }
     }
+    CD(6);
   }
   __syncthreads();
 
@@ -535,6 +573,8 @@ __device__ __forceinline__ int srbd_condense_qp(const CondenseArgs<T>& a, int q,
     a.status[q] = CMPC_SUCCESS;
     a.nvar[q] = n;
   }
+  CD(7);
+  CD_STORE();
   return n;
 }
 
