@@ -84,16 +84,16 @@ __device__ View carve(unsigned char* sm, int N, bool trial) {
 __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* u0, const double* u1, const double* D0,
                       const double* D1, bool trial = false) {
   const DevModel* M = a.model;
-  const int N = M->N, lane = threadIdx.x;
+  const int N = M->N, lane = threadIdx.x, nth = blockDim.x;
   View V = carve(sm, N, trial);
   const double* xr = a.xref + (size_t)q * (N + 1) * NX;
   const double* ft = a.foot + (size_t)q * (N + 1) * NL * 3;
   const uint8_t* ct = a.contact + (size_t)q * N * NL;
-  for (int i = lane; i < NX; i += 64) V.x0[i] = a.x0[(size_t)q * NX + i];
-  for (int i = lane; i < (N + 1) * NX; i += 64) V.xr[i] = xr[i];
-  for (int i = lane; i < (N + 1) * NL * 3; i += 64) V.des[i] = ft[i];
-  for (int i = lane; i < N * NL; i += 64) V.ct[i] = ct[i];
-  for (int i = lane; i < N * NU; i += 64) {
+  for (int i = lane; i < NX; i += nth) V.x0[i] = a.x0[(size_t)q * NX + i];
+  for (int i = lane; i < (N + 1) * NX; i += nth) V.xr[i] = xr[i];
+  for (int i = lane; i < (N + 1) * NL * 3; i += nth) V.des[i] = ft[i];
+  for (int i = lane; i < N * NL; i += nth) V.ct[i] = ct[i];
+  for (int i = lane; i < N * NU; i += nth) {
     V.u0[i] = u0[i];
     if (u1) V.u1[i] = u1[i];
     if (D0) V.D0[i] = D0[i];
@@ -101,7 +101,7 @@ __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* 
   }
   // lever-arm points and run starts from the global record (the LDS copies are not visible before the sync)
   auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
-  for (int sl = lane; sl < N * NL; sl += 64) {
+  for (int sl = lane; sl < N * NL; sl += nth) {
     const int k = sl / NL, i = sl % NL;
     double p[3] = {0.0, 0.0, 0.0};
     int s0 = 0;
@@ -112,7 +112,7 @@ __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* 
     for (int d = 0; d < 3; ++d) V.pb[sl * 3 + d] = p[d];
     V.rs[sl] = s0;
   }
-  for (int k = lane; k < N; k += 64) {
+  for (int k = lane; k < N; k += nth) {
     double sp, cp;
     sincos(xr[k * NX + 11], &sp, &cp);
     const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
@@ -351,9 +351,9 @@ __device__ double linstep_metric(const DevModel* M, const View& V, double* dxn, 
 extern __shared__ __attribute__((aligned(16))) unsigned char sqp_lds[];
 
 // Lab instrumentation (-DCMPC_SQP_STAMPS, lab/sqp_stamps.sh only, never in libcmpc.so): k_sqp_step's per-wave
-// shader-clock cycles per phase summed over every QP into sqp_stamp_acc (cmpc_sqp_debug_stamps): 0 staging, 1 trial
-// rollouts (lanes 0..13), 2 current iterate (lane 14), 3 linearised response + metric (lane 15), 4 |du| (lane 16),
-// 5 selection + update, 6 next linearisation point; 15 the number of waves.
+// shader-clock cycles per phase (both waves) summed over every QP into sqp_stamp_acc (cmpc_sqp_debug_stamps):
+// 0 staging, 1 the wave's own pass (wave 0: rollouts, wave 1: linearised response + |du|), 2 waiting for the other
+// wave, 5 selection + update, 6 next linearisation point; 15 the number of waves.
 #ifdef CMPC_SQP_STAMPS
 __device__ unsigned long long sqp_stamp_acc[16];
 #define SQ_DECL                                                 \
@@ -367,8 +367,8 @@ __device__ unsigned long long sqp_stamp_acc[16];
   } while (0)
 #define SQ_STORE()                                                                      \
   do {                                                                                  \
-    if (threadIdx.x == 0) {                                                             \
-      for (int k_ = 0; k_ < 7; ++k_) atomicAdd(&sqp_stamp_acc[k_], sq_acc_[k_]);        \
+    if ((threadIdx.x & 63) == 0) {                                                      \
+      for (int k_ = 0; k_ < 7; ++k_) atomicAdd(&sqp_stamp_acc[k_ + 8 * (threadIdx.x >> 6)], sq_acc_[k_]); \
       atomicAdd(&sqp_stamp_acc[15], 1ull);                                              \
     }                                                                                   \
   } while (0)
@@ -421,11 +421,12 @@ __global__ __launch_bounds__(64) void k_sqp_init(SqpArgs a) {
   }
 }
 
-// One SQP step for every QP not yet done, after the QP at lin returned uq / status_q / iters_q.
-__global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
+// One SQP step for every QP not yet done, after the QP at lin returned uq / status_q / iters_q. Two waves: wave 0 runs
+// the line search's rollouts, wave 1 (on another SIMD, at the same time) the linearised response and the step norm.
+__global__ __launch_bounds__(128) void k_sqp_step(SqpArgs a) {
   const int q = blockIdx.x;
   if (a.done[q]) return;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const DevModel* M = a.model;
   const int N = M->N;
   const int nu = N * NU;
@@ -434,36 +435,40 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
   const bool feet = a.dj != nullptr;  // footholds (cmpc_nlp_solve_batch)
   double* dj = feet ? a.dj + (size_t)q * nu : nullptr;
   const double* dq = feet ? a.dq + (size_t)q * nu : nullptr;
-  if (lane == 0) {
+  if (tid == 0) {
     a.sqp_iters[q] += 1;
     a.qp_iters[q] += a.iters_q[q];
   }
   if (a.status_q[q] != CMPC_SUCCESS) {  // keep U_j, report the subproblem's status (oracle_sqp_solve)
-    if (lane == 0) {
+    if (tid == 0) {
       a.status[q] = a.status_q[q];
       a.done[q] = 1;
     }
     return;
   }
+  __shared__ double xch[3];  // wave 1 -> wave 0: descent metric, |dx|, |du|
+  __shared__ int xma;        // wave 0 -> all: the accepted trial (-1: none)
   SQ_DECL;
   View V = stage(a, q, sqp_lds, uj, uq, dj, dq, true);
   __syncthreads();
   SQ(0);
-  // lanes m < 14: trial step alpha = 2^-m; lane 14: the current iterate; lane 15: |dx| and the descent metric;
-  // lane 16: |du| (sequential, the oracle's order). Lanes 0..3 and 14 keep their rollout's CoM path: when the accepted
-  // trial is one of them (or no step is taken) the next linearisation point is copied out instead of rolled out again
-  // (the iterate u0 + alpha (u1 - u0) is formed by the same operations as the trial's inputs, so its rollout is the
-  // trial's bit for bit; F_k is re-summed lane-parallel in the rollout's order)
-  double J = 0.0, aux = 0.0;
-  const int ts = trial_slot(lane);
-  double* cp = ts >= 0 ? V.lt + (size_t)ts * N * 3 : nullptr;
-  if (lane < 14) J = rollout_cost(M, V, true, ldexp(1.0, -lane), nullptr, nullptr, feet, cp);
-  SQ(1);
-  if (lane == 14) J = rollout_cost(M, V, false, 0.0, nullptr, nullptr, feet, cp);
-  SQ(2);
-  if (lane == 15) J = linstep_metric(M, V, &aux, feet);
-  SQ(3);
-  if (lane == 16) {
+  // wave 0: lanes m < 14 trial step alpha = 2^-m, lane 14 the current iterate as the trial alpha = 0 (u0 + 0 (u1 - u0)
+  // is u0 exactly, so one convergent pass serves both); wave 1: lane 0 |dx| and the descent metric, lane 1 |du|
+  // (sequential, the oracle's order). Lanes 0..3 and 14 keep their rollout's CoM path: when the accepted trial is one
+  // of them (or no step is taken) the next linearisation point is copied out instead of rolled out again (the iterate
+  // u0 + alpha (u1 - u0) is formed by the same operations as the trial's inputs, so its rollout is the trial's bit for
+  // bit; F_k is re-summed lane-parallel in the rollout's order)
+  double J = 0.0;
+  if (wave == 0) {
+    const int ts = trial_slot(lane);
+    double* cp = ts >= 0 ? V.lt + (size_t)ts * N * 3 : nullptr;
+    if (lane < 15) J = rollout_cost(M, V, true, lane < 14 ? ldexp(1.0, -lane) : 0.0, nullptr, nullptr, feet, cp);
+  } else if (lane == 0) {
+    double dxn = 0.0;
+    const double mt = linstep_metric(M, V, &dxn, feet);
+    xch[0] = mt;
+    xch[1] = dxn;
+  } else if (lane == 1) {
     double s2 = 0.0;
     for (int i = 0; i < nu; ++i) {
       const double d = V.u1[i] - V.u0[i];
@@ -474,25 +479,36 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
         const double d = V.D1[i] - V.D0[i];
         s2 += d * d;
       }
-    aux = sqrt(s2);
+    xch[2] = sqrt(s2);
   }
-  SQ(4);
-  const double J0 = __shfl(J, 14, 64);
-  const double metric = __shfl(J, 15, 64), dxn = __shfl(aux, 15, 64), dun = __shfl(aux, 16, 64);
-  const double tol = a.tol;
-  // lane m: accepted (Armijo / decrease), and the early exit after a rejection at alpha = 2^-m (m >= 1)
-  const double am = ldexp(1.0, -(lane < 14 ? lane : 0));
-  const bool okm = lane < 14 && (metric < 0.0 ? (J < J0 + SQP_ARMIJO * am * metric) : (J < J0));
-  const bool exm = lane >= 1 && lane < 14 && am * dxn < tol && am * dun < tol;
-  const unsigned long long okb = __ballot(okm), exb = __ballot(exm);
-  const int e = exb ? __ffsll((long long)exb) - 1 : 14;  // trials m >= e are never reached
-  const unsigned long long reach = okb & ((1ull << e) - 1ull);
-  const int ma = reach ? __ffsll((long long)reach) - 1 : -1;
-  const double alpha = ma >= 0 ? ldexp(1.0, -ma) : 0.0;
-  const double Jn = ma >= 0 ? __shfl(J, ma, 64) : J0;
+  SQ(1);
   __syncthreads();
+  SQ(2);
+  const double tol = a.tol;
+  if (wave == 0) {
+    const double metric = xch[0], dxn = xch[1], dun = xch[2];
+    const double J0 = __shfl(J, 14, 64);
+    // lane m: accepted (Armijo / decrease), and the early exit after a rejection at alpha = 2^-m (m >= 1)
+    const double am = ldexp(1.0, -(lane < 14 ? lane : 0));
+    const bool okm = lane < 14 && (metric < 0.0 ? (J < J0 + SQP_ARMIJO * am * metric) : (J < J0));
+    const bool exm = lane >= 1 && lane < 14 && am * dxn < tol && am * dun < tol;
+    const unsigned long long okb = __ballot(okm), exb = __ballot(exm);
+    const int e = exb ? __ffsll((long long)exb) - 1 : 14;  // trials m >= e are never reached
+    const unsigned long long reach = okb & ((1ull << e) - 1ull);
+    const int ma = reach ? __ffsll((long long)reach) - 1 : -1;
+    const double alpha = ma >= 0 ? ldexp(1.0, -ma) : 0.0;
+    const double Jn = ma >= 0 ? __shfl(J, ma, 64) : J0;
+    const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
+    if (lane == 0) {
+      xma = ma;
+      if (conv) a.done[q] = 1;
+    }
+  }
+  __syncthreads();
+  const int ma = xma;
+  const double alpha = ma >= 0 ? ldexp(1.0, -ma) : 0.0;
   if (alpha > 0.0)
-    for (int i = lane; i < nu; i += 64) {
+    for (int i = tid; i < nu; i += 128) {
       const double un = V.u0[i] + alpha * (V.u1[i] - V.u0[i]);
       uj[i] = un;
       V.u0[i] = un;
@@ -502,14 +518,13 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
         V.D0[i] = dn;
       }
     }
-  const bool conv = alpha == 0.0 || fabs(Jn - J0) < SQP_COST_TOL || (alpha * dxn < tol && alpha * dun < tol);
   __syncthreads();
   SQ(5);
   const int sel = trial_slot(ma >= 0 ? ma : 14);
   if (sel >= 0) {
     const double* cs = V.lt + (size_t)sel * N * 3;
     double* lo = a.lin + (size_t)q * N * 6;
-    for (int i = lane; i < N * 6; i += 64) {
+    for (int i = tid; i < N * 6; i += 128) {
       const int k = i / 6, d = i % 6;
       double v;
       if (d < 3) {
@@ -521,9 +536,7 @@ __global__ __launch_bounds__(64) void k_sqp_step(SqpArgs a) {
       }
       lo[i] = v;
     }
-    if (lane == 0 && conv) a.done[q] = 1;
-  } else if (lane == 0) {
-    if (conv) a.done[q] = 1;
+  } else if (tid == 0) {
     rollout_cost(M, V, false, 0.0, a.lin + (size_t)q * N * 6, nullptr, feet);
   }
   SQ(6);
@@ -589,7 +602,7 @@ int launch_sqp(int which, const SqpArgs& a, int B, hipStream_t stream) {
   const size_t lds = sqp_lds_bytes(a.N, false);
   switch (which) {
     case 0: hipLaunchKernelGGL(k_sqp_init, dim3(B), dim3(64), lds, stream, a); break;
-    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(64), sqp_lds_bytes(a.N, true), stream, a); break;
+    case 1: hipLaunchKernelGGL(k_sqp_step, dim3(B), dim3(128), sqp_lds_bytes(a.N, true), stream, a); break;
     case 2: hipLaunchKernelGGL(k_sqp_final, dim3(B), dim3(64), lds, stream, a); break;
     case 3: hipLaunchKernelGGL(k_sqp_count, dim3(1), dim3(256), 0, stream, a.done, B, a.count); break;
     case 4: hipLaunchKernelGGL(k_sqp_lin, dim3(B), dim3(64), lds, stream, a); break;

@@ -10,9 +10,9 @@ import cheeta_mpc as cm  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 L = cm.lib()
-fns = {"k_sqp_step": (L.cmpc_sqp_debug_stamps, ["staging", "trial rollouts (0..13)", "current iterate (14)",
-                                                 "linearised response (15)", "|du| (16)", "selection + update",
-                                                 "next lin point"]),
+SQ = ["staging", "own pass", "wait for the other wave", "-", "-", "selection + update", "next lin point"]
+fns = {"k_sqp_step wave 0 (rollouts)": (L.cmpc_sqp_debug_stamps, SQ),
+       "k_sqp_step wave 1 (lin. response, |du|)": (L.cmpc_sqp_debug_stamps, SQ),
        "condense80 (wave 0)": (L.cmpc_cond_debug_stamps, ["record + ballots", "per-step tables", "column setup",
                                                            "gamma update", "free response (t0)", "block row + barrier",
                                                            "g + MFMA", "epilogue"])}
@@ -26,10 +26,14 @@ buf = (C.c_ulonglong * 16)()
 for f, _ in fns.values():
     f(buf, 1)
 eng.nlp_solve(x0, xref, foot, contact)
+sq = (C.c_ulonglong * 16)()
+L.cmpc_sqp_debug_stamps(sq, 1)
+cd = (C.c_ulonglong * 16)()
+L.cmpc_cond_debug_stamps(cd, 1)
 for name, (f, names) in fns.items():
-    f(buf, 1)
-    n = max(buf[15], 1)
-    tot = sum(buf[k] for k in range(len(names)))
-    print(f"{name}: {buf[15]} waves / QPs, {tot / n:.0f} cycles each")
+    src, off, cnt = (cd, 0, cd[15]) if f is L.cmpc_cond_debug_stamps else (sq, 8 if "wave 1" in name else 0, sq[15] // 2)
+    n = max(cnt, 1)
+    tot = sum(src[off + k] for k in range(len(names)))
+    print(f"{name}: {cnt} QPs, {tot / n:.0f} cycles each")
     for k, nm in enumerate(names):
-        print(f"  {nm:26s} {buf[k] / n:9.0f}  {100.0 * buf[k] / max(tot, 1):5.1f} %")
+        print(f"  {nm:26s} {src[off + k] / n:9.0f}  {100.0 * src[off + k] / max(tot, 1):5.1f} %")
