@@ -482,10 +482,12 @@ def test_device_pointer_entry_equals_host_entry(cm, op):
 
 
 @pytest.mark.gpu
-def test_device_two_per_cu_instantiation_equals_one_per_cu(cm, op):
-    """Batches above 256 run k_ocp_ipm<64, 2> (bounded at 256 VGPRs), smaller ones k_ocp_ipm<64, 1>: same arithmetic,
-    so the same problems give bit-identical results either way."""
-    ps = [ocpgen.legged_problem(500 + i, projected=False) for i in range(8)]
+@pytest.mark.parametrize("projected", [False, True])
+def test_device_two_per_cu_instantiation_equals_one_per_cu(cm, op, projected):
+    """Batches above 256 run k_ocp_ipm<64, 2> (bounded at 256 VGPRs) with the node-by-node staged residuals, batches up
+    to 64 k_ocp_ipm<64, 1> with every node's residuals at once (OcpSolveArgs::par_res): the same fma chains, so the
+    same problems give bit-identical results either way."""
+    ps = [ocpgen.legged_problem(500 + i, projected=projected) for i in range(8)]
     _, x1, u1, st1, it1 = _device_batch(cm, ps)
     big = [ps[i % 8] for i in range(264)]
     _, x2, u2, st2, it2 = _device_batch(cm, big)
