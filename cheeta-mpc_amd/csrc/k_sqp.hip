@@ -80,7 +80,8 @@ __device__ View carve(unsigned char* sm, int N, bool trial) {
   return V;
 }
 
-// Stage QP q (every lane calls; u1 / D0 / D1 may be null: not staged). The caller syncs before reading.
+// Stage QP q (every thread of the block calls: it syncs inside; u1 / D0 / D1 may be null: not staged). The caller
+// syncs before reading.
 __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* u0, const double* u1, const double* D0,
                       const double* D1, bool trial = false) {
   const DevModel* M = a.model;
@@ -99,14 +100,17 @@ __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* 
     if (D0) V.D0[i] = D0[i];
     if (D1) V.D1[i] = D1[i];
   }
-  // lever-arm points and run starts from the global record (the LDS copies are not visible before the sync)
-  auto st = [ct](int k, int l) { return ct[k * NL + l] != 0; };
+  // lever-arm points and run starts from the LDS copies of the record (their loops walk back along a stance run: one
+  // LDS latency per step instead of a global one)
+  __syncthreads();
+  const uint8_t* cl = V.ct;
+  auto st = [cl](int k, int l) { return cl[k * NL + l] != 0; };
   for (int sl = lane; sl < N * NL; sl += nth) {
     const int k = sl / NL, i = sl % NL;
     double p[3] = {0.0, 0.0, 0.0};
     int s0 = 0;
-    if (ct[sl]) {
-      stance_point(ft, N, k, i, st, p);
+    if (cl[sl]) {
+      stance_point(V.des, N, k, i, st, p);
       s0 = run_start(k, i, st);
     }
     for (int d = 0; d < 3; ++d) V.pb[sl * 3 + d] = p[d];
@@ -114,7 +118,7 @@ __device__ View stage(const SqpArgs& a, int q, unsigned char* sm, const double* 
   }
   for (int k = lane; k < N; k += nth) {
     double sp, cp;
-    sincos(xr[k * NX + 11], &sp, &cp);
+    sincos(V.xr[k * NX + 11], &sp, &cp);
     const double RzT[9] = {cp, sp, 0.0, -sp, cp, 0.0, 0.0, 0.0, 1.0};
     for (int r = 0; r < 3; ++r)
       for (int b = 0; b < 3; ++b) {
