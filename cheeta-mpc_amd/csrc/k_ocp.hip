@@ -257,12 +257,16 @@ __device__ __forceinline__ void residuals_par(const View& V, double& rs, double&
       const int a = e;
       const double *R = V.R(k), *Sm = V.S(k);
       double s = V.r(k)[a];
+      #pragma unroll 8
       for (int c = 0; c < mk; ++c) s = fma(R[c * mk + a], uk[c], s);
+      #pragma unroll 8
       for (int j = 0; j < nx; ++j) s = fma(Sm[j * mk + a], xk[j], s);
+      #pragma unroll 8
       for (int t = 0; t < n3; ++t) s = fma(Bm[a * nx + t], pk[t], s);
       double d = 0.0;
       if (g) {
         const double* D = V.D(k);
+        #pragma unroll 8
         for (int j = 0; j < g; ++j) d = fma(D[a * g + j], wk[j], d);
       }
       s -= d;
@@ -273,12 +277,16 @@ __device__ __forceinline__ void residuals_par(const View& V, double& rs, double&
       const double *Q = V.Q(k), *Sm = V.S(k);
       const double* pm = pi + (long long)(k - 1) * nx;
       double s = V.q(k)[i] - pm[i];
+      #pragma unroll 8
       for (int j = 0; j < nx; ++j) s = fma(Q[j * nx + i], xk[j], s);
+      #pragma unroll 8
       for (int a = 0; a < mk; ++a) s = fma(Sm[i * mk + a], uk[a], s);
+      #pragma unroll 8
       for (int t = 0; t < n3; ++t) s = fma(A[i * nx + t], pk[t], s);
       double d = 0.0;
       if (g) {
         const double* C = V.C(k);
+        #pragma unroll 8
         for (int j = 0; j < g; ++j) d = fma(C[i * g + j], wk[j], d);
       }
       s -= d;
@@ -288,7 +296,9 @@ __device__ __forceinline__ void residuals_par(const View& V, double& rs, double&
       const int i = e - n1 - n2;
       const double* xn = x + (long long)(k + 1) * nx;
       double s = V.b(k)[i] - xn[i];
+      #pragma unroll 8
       for (int j = 0; j < nx; ++j) s = fma(A[j * nx + i], xk[j], s);
+      #pragma unroll 8
       for (int a = 0; a < mk; ++a) s = fma(Bm[a * nx + i], uk[a], s);
       V.rb()[(long long)k * nx + i] = s;
       re = nmax(re, fabs(s));
@@ -931,6 +941,7 @@ __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_
           const int i = i0 + ii, c = c0 + cc;
           acc[ii][cc] = (i < nx && c < nx) ? Ak[c * nx + i] : 0.0;
         }
+#pragma unroll 4
       for (int aa = 0; aa < mk; ++aa) {
         double bv[4], kv[4];
 #pragma unroll
@@ -954,6 +965,7 @@ __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_
       double acc[4];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) acc[ii] = i0 + ii < nx ? rbv[(long long)k * nx + i0 + ii] : 0.0;
+#pragma unroll 4
       for (int aa = 0; aa < mk; ++aa) {
         const double kv = kk[aa];
 #pragma unroll
