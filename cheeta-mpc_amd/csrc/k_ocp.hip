@@ -994,6 +994,8 @@ __device__ __forceinline__ void forward_pass(const View& V, const Lds& S) {
   }
   if (N > 1)
     for (int e = tid; e < nxx; e += NT) S.ABx[e] = V.Acl(1)[e];
+  // bcl_k is loaded one stage ahead with Acl_{k+1}: no global latency at the head of a stage's chain
+  double bn = (N > 1 && tid < nx) ? V.bcl()[(long long)nx + tid] : 0.0;
   __syncthreads();
   for (int k = 1; k < N; ++k) {
     double* cur = (k & 1) ? S.ABx : S.Tx;
@@ -1002,13 +1004,16 @@ __device__ __forceinline__ void forward_pass(const View& V, const Lds& S) {
     double* vout = (k & 1) ? v1 : v0;
     double pre[16];
     const bool more = k + 1 < N;
+    const double bk = bn;
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) {
       const int e = tid + NT * s2;
       pre[s2] = (more && e < nxx) ? V.Acl(k + 1)[e] : 0.0;
     }
+    if (more && tid < nx) bn = V.bcl()[(long long)(k + 1) * nx + tid];
     if (tid < nx) {
-      double acc = V.bcl()[(long long)k * nx + tid];
+      double acc = bk;
+#pragma unroll 8
       for (int c = 0; c < nx; ++c) acc = fma(cur[c * nx + tid], vin[c], acc);
       vout[tid] = acc;
       dx[(long long)(k + 1) * nx + tid] = acc;
@@ -1107,6 +1112,7 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     const int k = it / nx, i = it % nx;
     const double* Pn = V.P(k + 1);
     double s = 0.0;
+#pragma unroll 8
     for (int t = 0; t < nx; ++t) s = fma(Pn[(long long)t * nx + i], V.rb()[(long long)k * nx + t], s);
     y[it] = s;
   }
@@ -1117,7 +1123,9 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     const double* Kk = V.K(k);
     const double* Ac = V.Acl(k);
     double s = V.gx()[(long long)k * nx + i];
+#pragma unroll 8
     for (int a = 0; a < mk; ++a) s = fma(Kk[(long long)i * mk + a], V.gu()[L.cu[k] + a], s);
+#pragma unroll 8
     for (int t = 0; t < nx; ++t) s = fma(Ac[(long long)i * nx + t], y[(long long)k * nx + t], s);
     h[(long long)k * nx + i] = s;
   }
@@ -1131,6 +1139,7 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
       S.ABx[r * nx + c] = V.Acl(N - 1)[e];
     }
   __syncthreads();
+  double hn = (N > 1 && tid < nx) ? h[(long long)(N - 1) * nx + tid] : 0.0;  // h_k one stage ahead, as bcl above
   for (int k = N - 1, t2 = 0; k >= 1; --k, ++t2) {
     double* cur = (t2 & 1) ? S.Tx : S.ABx;
     double* nxt = (t2 & 1) ? S.ABx : S.Tx;
@@ -1138,13 +1147,16 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     double* vout = (t2 & 1) ? v0 : v1;
     double pre[16];
     const bool more = k - 1 >= 1;
+    const double hk = hn;
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) {
       const int e = tid + NT * s2;
       pre[s2] = (more && e < nxx) ? V.Acl(k - 1)[e] : 0.0;
     }
+    if (more && tid < nx) hn = h[(long long)(k - 1) * nx + tid];
     if (tid < nx) {  // p_k[i] = sum_t Acl(t, i) p_{k+1}[t] + h_k[i]; cur[t * nx + i] = Acl(t, i)
-      double acc = h[(long long)k * nx + tid];
+      double acc = hk;
+#pragma unroll 8
       for (int t = 0; t < nx; ++t) acc = fma(cur[t * nx + tid], vin[t], acc);
       vout[tid] = acc;
       pv[(long long)k * nx + tid] = acc;
@@ -1167,6 +1179,7 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     const int k = L.ustage[it], a = it - L.cu[k];
     const double* Bm = V.Bm(k);
     double s = V.gu()[it];
+#pragma unroll 8
     for (int t = 0; t < nx; ++t)
       s = fma(Bm[(long long)a * nx + t], y[(long long)k * nx + t] + pv[(long long)(k + 1) * nx + t], s);
     z[it] = s;
