@@ -3,7 +3,7 @@
 # OCP bench lines (projected / rows, with the CPU oracle), rocprofv3 kernel stats of the headline and of B = 1 OCP
 # solves, FETCH_SIZE / WRITE_SIZE traffic and SQ counter passes for the headline and configs 3 / 5 (md5-stamped).
 # Every GPU step has its own time limit; a fault / abort / time-out ends the script.
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/final4; mkdir -p $O; cd $R
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/final5; mkdir -p $O; cd $R
 fatal() { case $1 in 124|134|137|139) echo "fatal exit $1 in $2"; exit 1;; esac; }
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
 tail -3 $O/gpu_tests.log; fatal $rc tests
