@@ -32,19 +32,39 @@ constexpr double TAU_OCP = 0.995;  // fraction-to-boundary, as oracle/ocp_ipm.c
 // Lab instrumentation (-DCMPC_OCP_STAMPS, lab/ocp_stamps.sh only, never in libcmpc.so): thread 0 of problem 0
 // accumulates shader-clock cycles per phase (s_memtime) into a device array read by cmpc_ocp_debug_stamps.
 #ifdef CMPC_OCP_STAMPS
+// thread 0 of problem 0 accumulates in LDS (no global round trip on the timed path) and adds to the device array at
+// the kernel's end
 __device__ unsigned long long ocp_stamp_acc[32];
-__device__ unsigned long long ocp_stamp_prev;
+__shared__ unsigned long long ocp_stamp_lds[33];
 #define OCP_STAMP(id)                                                         \
   do {                                                                        \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
       const unsigned long long now_ = __builtin_amdgcn_s_memtime();           \
-      ocp_stamp_acc[id] += now_ - ocp_stamp_prev;                             \
-      ocp_stamp_prev = now_;                                                  \
+      ocp_stamp_lds[id] += now_ - ocp_stamp_lds[32];                          \
+      ocp_stamp_lds[32] = now_;                                               \
     }                                                                         \
+  } while (0)
+#define OCP_STAMP_BEGIN()                                                     \
+  do {                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
+      for (int i_ = 0; i_ < 32; ++i_) ocp_stamp_lds[i_] = 0;                  \
+      ocp_stamp_lds[32] = __builtin_amdgcn_s_memtime();                       \
+    }                                                                         \
+  } while (0)
+#define OCP_STAMP_END()                                                       \
+  do {                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                  \
+      for (int i_ = 0; i_ < 32; ++i_) ocp_stamp_acc[i_] += ocp_stamp_lds[i_]; \
   } while (0)
 #else
 #define OCP_STAMP(id) \
   do {                \
+  } while (0)
+#define OCP_STAMP_BEGIN() \
+  do {                    \
+  } while (0)
+#define OCP_STAMP_END() \
+  do {                  \
   } while (0)
 #endif
 
@@ -148,9 +168,11 @@ __device__ __forceinline__ Lds carve(double* smem, const OcpLayout& L, int NZP) 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // c = C x + D u for every row (node 0's x is x0; the step's dx node 0 is 0)
-__device__ __forceinline__ void rows_value(const View& V, const double* xs, const double* us, double* out) {
+__device__ __forceinline__ void rows_value(const View& V, const double* xs, const double* us, double* out, int j0 = 0,
+                                           int j1 = -1) {
   const OcpLayout& L = V.L;
-  for (int j = threadIdx.x; j < L.m; j += NT) {
+  if (j1 < 0) j1 = L.m;
+  for (int j = j0 + threadIdx.x; j < j1; j += NT) {
     const int k = L.rstage[j], jl = j - L.cr[k], g = L.ng[k], mk = L.nu[k];
     const double* C = V.C(k);
     const double* D = V.D(k);
@@ -237,12 +259,13 @@ __device__ __forceinline__ void residuals(const View& V, double& rs, double& re)
 // its L2 traffic is ~2.5x the staged form's, which wins for full batches (-14 % solves/s at B = 256, -11 % at 1024
 // with this form).
 constexpr int OCP_PAR_RES_MAX = 64;
-__device__ __forceinline__ void residuals_par(const View& V, double& rs, double& re) {
+__device__ __forceinline__ void residuals_par(const View& V, double& rs, double& re, int n0 = 0, int n1 = -1) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N;
   const double *x = V.x(), *u = V.u(), *pi = V.pi(), *wl = V.row(R_W);
   const int P = L.nzp + nx;
-  for (int w = tid; w < (N + 1) * P; w += NT) {
+  if (n1 < 0) n1 = N + 1;
+  for (int w = n0 * P + tid; w < n1 * P; w += NT) {
     const int k = w / P, e = w - k * P;
     const int mk = L.nu[k], g = L.ng[k];
     const int n1 = mk, n2 = k >= 1 ? nx : 0, n3 = k < N ? nx : 0;
@@ -484,6 +507,23 @@ __device__ __forceinline__ void residuals_staged(const View& V, const Lds& S, do
     }
   }
   __syncthreads();
+}
+
+// Step right-hand side over stages [k0, k1) (u entries) and nodes [max(k0, 1), n1) (x entries)
+__device__ __forceinline__ void step_rhs_range(const View& V, int k0, int k1, int n1) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx, u0 = L.cu[k0], u1 = L.cu[k1], x0 = (k0 > 1 ? k0 : 1) * nx, x1 = n1 * nx;
+  const double* w = V.row(R_W);
+  const int nu = u1 - u0, nxr = x1 > x0 ? x1 - x0 : 0;
+  for (int it = threadIdx.x; it < nu + nxr; it += NT) {
+    if (it < nu) {
+      const int e = u0 + it, k = L.ustage[e], a = e - L.cu[k];
+      V.gu()[e] = V.rgu()[e] + gct_u(V, k, a, w);
+    } else {
+      const int e = x0 + it - nu, k = e / nx, i = e - k * nx;
+      V.gx()[e] = V.rgx()[e] + gct_x(V, k, i, w);
+    }
+  }
 }
 
 // Step right-hand side g = r_g + Gc' w (node 0 has no state entries)
@@ -914,7 +954,8 @@ __device__ __forceinline__ bool factor_pass(const View& V, const Lds& S, double 
 // 4-row blocks of bcl per thread, operands straight from the L2-resident records / workspace) with no barrier
 // between stages; each entry is the same fma chain over a as the per-stage form, so the results are bit-identical
 // (was one stage per barrier with LDS-staged operands: 11 % of a B = 1 solve)
-__device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_acl) {
+__device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_acl, int k0 = 0, int k1 = -1,
+                                         bool sync = true) {
   (void)S;
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N;
@@ -924,7 +965,8 @@ __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_
   const double* kfv = V.kf();
   const double* rbv = V.rb();
   double* bclv = V.bcl();
-  for (int w = tid; w < N * ps; w += NT) {
+  if (k1 < 0) k1 = N;
+  for (int w = k0 * ps + tid; w < k1 * ps; w += NT) {
     const int k = w / ps, r = w - k * ps;
     const int mk = L.nu[k];
     const double* Bk = V.Bm(k);
@@ -977,7 +1019,7 @@ __device__ __forceinline__ void acl_pass(const View& V, const Lds& S, bool with_
         if (i0 + ii < nx) bclv[(long long)k * nx + i0 + ii] = acc[ii];
     }
   }
-  __syncthreads();
+  if (sync) __syncthreads();
 }
 
 // Serial forward sweep: dx_1 = bcl_0, dx_{k+1} = Acl_k dx_k + bcl_k (dx node 0 stays 0)
@@ -1031,11 +1073,15 @@ __device__ __forceinline__ void forward_pass(const View& V, const Lds& S) {
 
 // du_k = K_k dx_k + kf_k, dpi_k = P_{k+1} dx_{k+1} + p_{k+1}; then the row directions and the largest step
 // (returns the local min over rows of the fraction-to-boundary step, 1e300 if none)
-__device__ __forceinline__ double post_pass(const View& V) {
+__device__ __forceinline__ double post_pass(const View& V, int k0 = 0, int k1 = -1, int n1 = -1) {
   const OcpLayout& L = V.L;
   const int nx = L.nx, N = L.N;
   const double* dx = V.dx();
-  for (int it = threadIdx.x; it < L.nU + N * nx; it += NT) {
+  if (k1 < 0) k1 = N;
+  if (n1 < 0) n1 = N + 1;
+  const int u0 = L.cu[k0], nuR = L.cu[k1] - u0, r0 = L.cr[k0], r1 = L.cr[n1];
+  for (int itr = threadIdx.x; itr < nuR + (k1 - k0) * nx; itr += NT) {
+    const int it = itr < nuR ? u0 + itr : L.nU + k0 * nx + (itr - nuR);
     if (it < L.nU) {
       const int k = L.ustage[it], a = it - L.cu[k], mk = L.nu[k];
       double s = V.kf()[it];
@@ -1054,13 +1100,13 @@ __device__ __forceinline__ double post_pass(const View& V) {
   }
   __syncthreads();
   double amax = 1e300;
-  if (L.m > 0) {
+  if (r1 > r0) {
     double* dc = V.row(R_DTL);
-    rows_value(V, dx, V.du(), dc);  // each thread reads back only its own rows below
+    rows_value(V, dx, V.du(), dc, r0, r1);  // each thread reads back only its own rows below
     const double *rl = V.row(R_RL), *ru = V.row(R_RU), *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL),
                  *lu = V.row(R_LU), *rml = V.row(R_RML), *rmu = V.row(R_RMU);
     double *dtl = V.row(R_DTL), *dtu = V.row(R_DTU), *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
-    for (int j = threadIdx.x; j < L.m; j += NT) {
+    for (int j = r0 + threadIdx.x; j < r1; j += NT) {
       const double c = dtl[j];
       const double a1 = c + rl[j], a2 = ru[j] - c;
       const double b1 = -(rml[j] + ll[j] * a1) / tl[j], b2 = -(rmu[j] + lu[j] * a2) / tu[j];
@@ -1100,26 +1146,129 @@ __device__ __forceinline__ void ldl_solve(const double* __restrict__ F, int m, c
   for (int i = 0; i < m; ++i) x[i] = -x[i];
 }
 
-// Corrector's backward vector pass with the factorisation kept: y_k = P_{k+1} rb_k; h_k = g_x,k + K_k' g_u,k +
-// Acl_k' y_k; p_N = g_x,N, p_k = Acl_k' p_{k+1} + h_k (serial, k = N-1..1); kf_k = -M_uu,k^{-1} (g_u,k + B_k'(y_k + p_{k+1})) by the LDL' factors
-__device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
+#include "ocp_chain.hpp"
+
+// LDS of the latency form: G images (two), T, Paug, the pivot-column buffers and the rows' Sigma (two), then red and
+// vec; the other passes of the kernel see G0 / G1 as ABx / Tx (contiguous: the staged residuals' buffer)
+__device__ __forceinline__ Lds carve_fast(double* smem, const OcpLayout& L, ChainLds& C) {
+  const int ngr = CH_NRP + L.ngmax, ngp = (L.ngmax + 2) & ~1;
+  C.G0 = smem;
+  C.G1 = C.G0 + ngr * CH_GS;
+  C.T = C.G1 + ngr * CH_GS;
+  C.Pa = C.T + CH_NRP * CH_GS;
+  C.C = C.Pa + CH_PS * CH_PS;
+  C.sg0 = C.C + 256;
+  C.sg1 = C.sg0 + ngp;
+  C.desc = (int*)(C.sg1 + ngp + 64 + 128);
+  Lds s;
+  s.np1 = L.nx + 1;
+  s.nrm = L.nx + 1 + L.ngmax;
+  s.nzp = 64;
+  s.Paug = C.Pa;
+  s.ABx = C.G0;
+  s.Tx = C.G1;
+  s.col = C.C;
+  s.red = C.sg1 + ngp;
+  s.vec = s.red + 64;
+  s.sgn = C.sg0;
+  return s;
+}
+
+// ---- grid form (small batches): G workgroups per problem, stage ranges, grid barriers -----------------------------
+// Workgroup g of problem q owns stages [k0, k1) and nodes [k0, n1) (n1 = k1, the last one N + 1), their rows
+// [r0, r1) and inputs [u0, u1): every stage-parallel pass runs on the owned range; the serial chains (the
+// factorisation, the forward rollout, the corrector's cost-to-go recursion) run on workgroup 0; grid barriers between
+// the phases. Reductions (residual maxima, mu, the step length) go through per-workgroup partials read back in a fixed
+// order by every workgroup, so all workgroups take the same decisions.
+struct GridRange {
+  int g, G, k0, k1, n1, u0, u1, r0, r1;
+};
+__device__ __forceinline__ GridRange grid_range(const OcpLayout& L, int g, int G) {
+  GridRange R;
+  R.g = g;
+  R.G = G;
+  R.k0 = (int)((long long)L.N * g / G);
+  R.k1 = (int)((long long)L.N * (g + 1) / G);
+  R.n1 = g == G - 1 ? L.N + 1 : R.k1;
+  R.u0 = L.cu[R.k0];
+  R.u1 = L.cu[R.k1];
+  R.r0 = L.cr[R.k0];
+  R.r1 = L.cr[R.n1];
+  return R;
+}
+
+// Grid barrier of one problem's G workgroups (the hand-off recipe of the MI355X guide: every wave's stores drained,
+// lane-0 agent release, a relaxed agent-scope arrive on a counter zeroed before the launch, a relaxed poll with
+// s_sleep, one agent acquire). The spin is bounded: on a timeout (or another workgroup's) the problem's fail word is
+// set and every workgroup returns false at its next barrier, so the grid drains instead of hanging.
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, double* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool good = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (good && __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) good = false;
+      if (++spins > (1u << 22)) {
+        __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        good = false;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    flag_lds[0] = good ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  return flag_lds[0] != 0.0;
+}
+
+// Every workgroup's nv partials (slot [g][0..nv)) reduced in workgroup order by lanes of wave 0, the same in every
+// workgroup; ops: 0 max (NaN-propagating), 1 sum, 2 min. Result in out (LDS), valid after the trailing barrier.
+__device__ __forceinline__ void grid_collect(const double* part, int G, int nv, const int* ops, double* out) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    for (int c = 0; c < nv; ++c) {
+      const int op = ops[c];
+      const double idv = op == 0 ? 0.0 : (op == 1 ? 0.0 : 1e300);
+      double v = lane < G ? __hip_atomic_load(part + lane * 8 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : idv;
+      // fixed-order tree over the 64 lanes (identical in every workgroup)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double w = __shfl_xor(v, o, 64);
+        v = op == 0 ? nmax(v, w) : (op == 1 ? ((lane & o) ? w + v : v + w) : (v < w ? v : w));
+      }
+      if (lane == 0) out[c] = v;
+    }
+  }
+  __syncthreads();
+}
+
+// Corrector's backward vector pass split for the grid form: (a) y_k = P_{k+1} rb_k and h_k on the owned stages
+// (p_N = g_x,N on the last workgroup), (b) the serial recursion p_k = Acl_k' p_{k+1} + h_k on workgroup 0, (c) the
+// feedforward kf_k = -M_uu,k^{-1} (g_u,k + B_k'(y_k + p_{k+1})) on the owned stages. (a) + (b) + (c) = backward_vec_pass.
+__device__ __forceinline__ void bwd_vec_a(const View& V, int k0, int k1, bool last) {
   const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N;
   double* y = V.y();
   double* h = V.h();
-  double* pv = V.pv();
-  for (int it = tid; it < N * nx; it += NT) {
-    const int k = it / nx, i = it % nx;
+  for (int it = k0 * nx + tid; it < k1 * nx; it += NT) {
+    const int k = it / nx, i = it - k * nx;
     const double* Pn = V.P(k + 1);
     double s = 0.0;
 #pragma unroll 8
     for (int t = 0; t < nx; ++t) s = fma(Pn[(long long)t * nx + i], V.rb()[(long long)k * nx + t], s);
     y[it] = s;
   }
-  for (int it = tid; it < nx; it += NT) pv[(long long)N * nx + it] = V.gx()[(long long)N * nx + it];
+  if (last)
+    for (int it = tid; it < nx; it += NT) V.pv()[(long long)N * nx + it] = V.gx()[(long long)N * nx + it];
   __syncthreads();
-  for (int it = tid; it < (N - 1) * nx; it += NT) {
-    const int k = 1 + it / nx, i = it % nx, mk = L.nu[k];
+  const int ka = k0 > 1 ? k0 : 1;
+  for (int it = ka * nx + tid; it < k1 * nx; it += NT) {
+    const int k = it / nx, i = it - k * nx, mk = L.nu[k];
     const double* Kk = V.K(k);
     const double* Ac = V.Acl(k);
     double s = V.gx()[(long long)k * nx + i];
@@ -1129,7 +1278,15 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     for (int t = 0; t < nx; ++t) s = fma(Ac[(long long)i * nx + t], y[(long long)k * nx + t], s);
     h[(long long)k * nx + i] = s;
   }
-  // serial p recursion; Acl_k' staged transposed in LDS (double buffer in ABx / Tx)
+}
+
+// Corrector's serial cost-to-go recursion (backward_vec_pass part b): p_N = g_x,N, p_k = Acl_k' p_{k+1} + h_k
+// (k = N-1..1); Acl_k' staged transposed in LDS (double buffer in ABx / Tx)
+__device__ __forceinline__ void bwd_vec_b(const View& V, const Lds& S) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx;
+  double* h = V.h();
+  double* pv = V.pv();
   double* v0 = S.vec;
   double* v1 = S.vec + 64;
   if (tid < nx) v0[tid] = V.gx()[(long long)N * nx + tid];
@@ -1173,9 +1330,17 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     }
     __syncthreads();
   }
-  // z_k = g_u + B'(y_k + p_{k+1}) into du (scratch), then kf = -M_uu^{-1} z
+}
+
+// Corrector's feedforward on stages [k0, k1) (backward_vec_pass part c): z_k = g_u + B'(y_k + p_{k+1}) into du
+// (scratch), then kf_k = -M_uu,k^{-1} z_k by the LDL' factors
+__device__ __forceinline__ void bwd_vec_c(const View& V, int k0, int k1) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx;
+  const double* y = V.y();
+  const double* pv = V.pv();
   double* z = V.du();
-  for (int it = tid; it < L.nU; it += NT) {
+  for (int it = L.cu[k0] + tid; it < L.cu[k1]; it += NT) {
     const int k = L.ustage[it], a = it - L.cu[k];
     const double* Bm = V.Bm(k);
     double s = V.gu()[it];
@@ -1185,7 +1350,19 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
     z[it] = s;
   }
   __syncthreads();
-  for (int k = tid; k < N; k += NT) ldl_solve(V.Lf(k), L.nu[k], z + L.cu[k], V.kf() + L.cu[k]);
+  for (int k = k0 + tid; k < k1; k += NT) ldl_solve(V.Lf(k), L.nu[k], z + L.cu[k], V.kf() + L.cu[k]);
+}
+
+// Corrector's backward vector pass with the factorisation kept: y_k = P_{k+1} rb_k; h_k = g_x,k + K_k' g_u,k +
+// Acl_k' y_k; p_N = g_x,N, p_k = Acl_k' p_{k+1} + h_k (serial, k = N-1..1); kf_k = -M_uu,k^{-1} (g_u,k + B_k'(y_k +
+// p_{k+1})) by the LDL' factors
+__device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
+  const int N = V.L.N;
+  bwd_vec_a(V, 0, N, true);
+  __syncthreads();
+  bwd_vec_b(V, S);
+  __syncthreads();
+  bwd_vec_c(V, 0, N);
 }
 
 // (l_l - l_u) into R_W
@@ -1195,13 +1372,16 @@ __device__ __forceinline__ void load_lamdiff(const View& V) {
   for (int j = threadIdx.x; j < V.L.m; j += NT) w[j] = ll[j] - lu[j];
 }
 
-template <int NZP, int MINB>
-__device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds& S) {
+template <int NZP, int MINB, bool FAST>
+__device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds& S, const ChainLds& CS) {
   const View V(a, q);
   const OcpLayout& L = a.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N, m = L.m;
   double* x = V.x();
   double* u = V.u();
+  constexpr bool fast = FAST;
+  double* hp = fast ? a.hp + (long long)q * a.hp_stride : nullptr;
+  if (fast) hp_build(V, hp, a.reg);  // the stages' constant Hessian blocks, once per solve (read after a barrier)
   // --- cold start ---
   for (int i = tid; i < (N + 1) * nx; i += NT) {  // warm: x (nodes >= 1), u from the caller's d_x / d_u
     x[i] = i < nx ? a.x0[(long long)q * nx + i] : (a.warm ? a.x[(long long)q * (N + 1) * nx + i] : 0.0);
@@ -1302,7 +1482,13 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
     step_rhs(V);
     __syncthreads();
     OCP_STAMP(2);
-    if (!factor_pass<NZP>(V, S, a.reg)) {
+    bool fok;
+    if constexpr (FAST) {
+      fok = chain_factor(V, CS, hp, a.reg);
+    } else {
+      fok = factor_pass<NZP>(V, S, a.reg);
+    }
+    if (!fok) {
       status = 3;
       break;
     }
@@ -1400,16 +1586,501 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
       a.res[(long long)q * 4 + 3] = rc;
     }
   }
+  if (a.stats)  // rows after the last iteration: NaN (cmpc.h)
+    for (int e = tid; e < (a.stat_rows - it - 1) * 10; e += NT)
+      a.stats[((long long)q * a.stat_rows + it + 1) * 10 + e] = __builtin_nan("");
 }
 
 // MINB workgroups per CU: 1 (the whole register file for one problem's chain: the lowest latency, B <= #CUs) or 2
 // (bounded at 256 VGPRs, spilling some bookkeeping: 1.4-1.5x the solves/s of a full chip, 10 % slower per problem)
-template <int NZP, int MINB>
+// Stage 0 of the Riccati getters, the reference's reconstruction (HpipmInterface.cpp:334-347, 376-389, 416-453) from
+// node 1's P, p (in Po, po), stage 0's Lr (Lro) and the stage-0 record; writes P_0, p_0, K_0, k_0. Workgroup-wide.
+__device__ __forceinline__ void ric_stage0(const View& V, const Lds& S, double* Po, double* po, double* Ko, double* ko,
+                                           const double* Lro) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx;
+  // stage 0, the reference's reconstruction (HpipmInterface.cpp:334-347, 376-389, 416-453) from P_1, p_1, Lr_0 and the
+  // stage-0 record: PA = P_1 A_0, v = p_1 + P_1 b_0, Mux = S_0 + B_0'PA, gr = r_0 + B_0'v, T1 = Lr_0^-1 Mux,
+  // t2 = Lr_0^-1 gr, K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2, P_0 = Q_0 + A_0'PA - T1'T1, p_0 = q_0 + A_0'v - T1't2.
+  // LDS: PA [nx][nx] in ABx, Mux / T1 [m0][nx] in Tx, v, gr / t2.
+  {
+    const int m0 = L.nu[0];
+    const double* P1 = Po + (long long)nx * nx;
+    const double* p1 = po + nx;
+    const double* A = V.A(0);
+    const double* Bm = V.Bm(0);
+    double* PA = S.ABx;
+    double* Mux = S.Tx;
+    double* v = S.vec;
+    double* gr = S.vec + 64;
+    for (int e = tid; e < nx * nx; e += NT) {
+      const int i = e / nx, j = e % nx;  // PA[i][j]
+      double s = 0.0;
+      for (int t = 0; t < nx; ++t) s = fma(P1[(long long)t * nx + i], A[(long long)j * nx + t], s);
+      PA[i * nx + j] = s;
+    }
+    for (int i = tid; i < nx; i += NT) {
+      double s = p1[i];
+      for (int t = 0; t < nx; ++t) s = fma(P1[(long long)t * nx + i], V.b(0)[t], s);
+      v[i] = s;
+    }
+    __syncthreads();
+    for (int e = tid; e < m0 * nx + m0; e += NT) {
+      if (e < m0 * nx) {
+        const int a2 = e / nx, j = e % nx;
+        double s = V.S(0)[(long long)j * m0 + a2];
+        for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a2 * nx + t], PA[t * nx + j], s);
+        Mux[a2 * nx + j] = s;
+      } else {
+        const int a2 = e - m0 * nx;
+        double s = V.r(0)[a2];
+        for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a2 * nx + t], v[t], s);
+        gr[a2] = s;
+      }
+    }
+    __syncthreads();
+    // T1 = Lr_0^-1 Mux (in place, Tx), t2 = Lr_0^-1 gr (in place); K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2 (in place in
+    // the outputs); one thread per right-hand side, the factor's guarded pivots (diag 0) contributing 0 as in HPIPM
+    const double* Lr0 = Lro;
+    for (int j = tid; j <= nx; j += NT) {
+      double* c = j < nx ? Mux + j : gr;
+      const int cs = j < nx ? nx : 1;
+      double* o = j < nx ? Ko + (long long)j * m0 : ko;
+      for (int a2 = 0; a2 < m0; ++a2) {
+        double s = c[a2 * cs];
+        for (int b = 0; b < a2; ++b) s = fma(-Lr0[(long long)b * m0 + a2], c[b * cs], s);
+        const double d = Lr0[(long long)a2 * m0 + a2];
+        c[a2 * cs] = d > 0.0 ? s / d : 0.0;
+      }
+      for (int a2 = m0 - 1; a2 >= 0; --a2) {
+        double s = c[a2 * cs];
+        for (int b = a2 + 1; b < m0; ++b) s = fma(-Lr0[(long long)a2 * m0 + b], o[b], s);
+        const double d = Lr0[(long long)a2 * m0 + a2];
+        o[a2] = d > 0.0 ? s / d : 0.0;
+      }
+      for (int a2 = 0; a2 < m0; ++a2) o[a2] = -o[a2];
+    }
+    __syncthreads();
+    for (int e = tid; e < nx * nx + nx; e += NT) {
+      if (e < nx * nx) {
+        const int j = e / nx, i = e % nx;  // P_0 (i, j) = Q_0 + A_0'PA - T1'T1
+        double s = V.Q(0)[(long long)j * nx + i];
+        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], PA[t * nx + j], s);
+        for (int a2 = 0; a2 < m0; ++a2) s = fma(-Mux[a2 * nx + i], Mux[a2 * nx + j], s);
+        Po[e] = s;
+      } else {
+        const int i = e - nx * nx;  // p_0 = q_0 + A_0'v - T1't2
+        double s = V.q(0)[i];
+        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], v[t], s);
+        for (int a2 = 0; a2 < m0; ++a2) s = fma(-Mux[a2 * nx + i], gr[a2], s);
+        po[i] = s;
+      }
+    }
+  }
+}
+
+// The IPM of ipm_body in the grid form: problem q on workgroups q G .. q G + G - 1 (see grid_range). Same iteration,
+// same stopping rule, statistics and outputs; the latency-form factorisation (FAST) or factor_pass on workgroup 0.
+template <bool FAST>
+__device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, const Lds& S, const ChainLds& CS) {
+  const View V(a, q);
+  const OcpLayout& L = a.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, m = L.m, G = a.G;
+  const GridRange R = grid_range(L, g, G);
+  const bool lead = g == 0, last = g == G - 1;
+  unsigned* bar = a.bar + 4 * (long long)q;
+  double* part = a.gpart + 8 * (long long)G * q;  // [G][8] partials of this problem
+  // Slots: a workgroup may write its next partial while a slower one still reads the last collected values (the
+  // barrier precedes the collect, not the next write), so partials collected back to back use different slots:
+  // 0-4 residuals, 5 factorisation status / corrector step / exit checks, 6 predictor step, 7 mu_aff / finite check.
+  double* mine = part + 8 * g;
+  double* fl = S.red + 32;   // LDS: barrier flag [0], reduced values [1..8]
+  double* red = S.red + 40;  // reduced partials
+  unsigned nbar = 0;
+  bool alive = true;
+  auto sync = [&]() {
+    if (alive) alive = grid_sync(bar, (++nbar) * (unsigned)G, fl);
+    return alive;
+  };
+  double* x = V.x();
+  double* u = V.u();
+  double* hp = FAST ? a.hp + (long long)q * a.hp_stride : nullptr;
+  if (FAST) {  // this workgroup's stages' constant Hessian blocks (read by workgroup 0's chain after a barrier)
+    const int e0 = L.cHp[R.k0], e1 = L.cHp[R.k1];
+    int k = R.k0;
+    for (int e = e0 + tid; e < e1; e += NT) {
+      while (e >= L.cHp[k + 1]) ++k;
+      const int le = e - L.cHp[k], tau = le >> 2, aa = (le >> 1) & 1, bb = le & 1;
+      int bi, bj;
+      ch_block(tau, bi, bj);
+      const int i = 2 * bi + aa, l = 2 * bj + bb;
+      const int mk = L.nu[k], nz = mk + nx;
+      double v = 0.0;
+      if (i >= l && i < nz && l < nz) {
+        if (i < mk) v = V.R(k)[l * mk + i] + (i == l ? a.reg : 0.0);
+        else if (l < mk) v = V.S(k)[(i - mk) * mk + l];
+        else v = V.Q(k)[(l - mk) * nx + (i - mk)] + (i == l ? a.reg : 0.0);
+      }
+      hp[e] = v;
+    }
+  }
+  // --- cold start on the owned nodes / stages / rows ---
+  for (int i = R.k0 * nx + tid; i < R.n1 * nx; i += NT) {
+    x[i] = i < nx ? a.x0[(long long)q * nx + i] : (a.warm ? a.x[(long long)q * (N + 1) * nx + i] : 0.0);
+    V.dx()[i] = 0.0;
+    V.gx()[i] = 0.0;
+    V.rgx()[i] = 0.0;
+  }
+  for (int i = R.u0 + tid; i < R.u1; i += NT) u[i] = a.warm ? a.u[(long long)q * L.nU + i] : 0.0;
+  for (int i = R.k0 * nx + tid; i < R.k1 * nx; i += NT) V.pi()[i] = 0.0;
+  __syncthreads();
+  {
+    double* c = V.row(R_C);
+    rows_value(V, x, u, c, R.r0, R.r1);
+    double *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL),
+           *lu = V.row(R_LU);
+    for (int j = R.r0 + tid; j < R.r1; j += NT) {
+      const int k = L.rstage[j];
+      const double bnd = -V.e(k)[j - L.cr[k]];
+      lg[j] = bnd;
+      ug[j] = bnd;
+      tl[j] = fmax(c[j] - bnd, 1.0);
+      tu[j] = fmax(bnd - c[j], 1.0);
+      ll[j] = a.mu0 / tl[j];
+      lu[j] = a.mu0 / tu[j];
+    }
+  }
+  sync();  // every node's iterate before the first residuals
+  int status = 1, it = 0;
+  double rs = 0, re = 0, ri = 0, rc = 0;
+  const int ops_res[5] = {0, 0, 0, 0, 1};
+  const int ops_min[1] = {2};
+  const int ops_sum[1] = {1};
+  const int ops_max[1] = {0};
+  for (it = 0; alive; ++it) {
+    // --- residuals (owned nodes / rows), reduced over the grid ---
+    rows_value(V, x, u, V.row(R_C), R.r0, R.r1);
+    {
+      double* w = V.row(R_W);
+      const double *ll = V.row(R_LL), *lu = V.row(R_LU);
+      for (int j = R.r0 + tid; j < R.r1; j += NT) w[j] = ll[j] - lu[j];
+    }
+    __syncthreads();
+    double lrs = 0.0, lre = 0.0, lri = 0.0, lrc = 0.0, lmu = 0.0;
+    residuals_par(V, lrs, lre, R.k0, R.n1);
+    {
+      const double *c = V.row(R_C), *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU),
+                   *ll = V.row(R_LL), *lu = V.row(R_LU);
+      double *rl = V.row(R_RL), *ru = V.row(R_RU);
+      for (int j = R.r0 + tid; j < R.r1; j += NT) {
+        const double a1 = c[j] - lg[j] - tl[j], a2 = ug[j] - c[j] - tu[j];
+        rl[j] = a1;
+        ru[j] = a2;
+        lri = nmax(lri, nmax(fabs(a1), fabs(a2)));
+        const double c1 = tl[j] * ll[j], c2 = tu[j] * lu[j];
+        lrc = nmax(lrc, nmax(c1, c2));
+        lmu += c1 + c2;
+      }
+    }
+    {
+      const double v0 = block_reduce(lrs, S.red, OpMax()), v1 = block_reduce(lre, S.red, OpMax()),
+                   v2 = block_reduce(lri, S.red, OpMax()), v3 = block_reduce(lrc, S.red, OpMax()),
+                   v4 = block_reduce(lmu, S.red, OpSum());
+      if (tid == 0) {
+        mine[0] = v0;
+        mine[1] = v1;
+        mine[2] = v2;
+        mine[3] = v3;
+        mine[4] = v4;
+      }
+    }
+    if (!sync()) break;
+    grid_collect(part, G, 5, ops_res, red);
+    OCP_STAMP(1);
+    rs = red[0];
+    re = red[1];
+    ri = red[2];
+    rc = red[3];
+    const double mu = m > 0 ? red[4] / (2.0 * m) : 0.0;
+    double* sr = (lead && a.stats && it < a.stat_rows) ? a.stats + ((long long)q * a.stat_rows + it) * 10 : nullptr;
+    if (sr && tid == 0) {
+      for (int c = 0; c < 5; ++c) sr[c] = __builtin_nan("");
+      sr[5] = mu;
+      sr[6] = rs;
+      sr[7] = re;
+      sr[8] = ri;
+      sr[9] = rc;
+    }
+    if (!(isfinite(rs) && isfinite(re) && isfinite(ri) && isfinite(rc))) {
+      status = 3;
+      break;
+    }
+    if (rs <= a.tol_stat && re <= a.tol_eq && ri <= a.tol_ineq && rc <= a.tol_comp) {
+      status = 0;
+      break;
+    }
+    if (it >= a.iter_max) {
+      status = 1;
+      break;
+    }
+    if (m > 0 && !(mu > 1e-300)) {
+      status = 2;
+      break;
+    }
+    // --- predictor right-hand side (owned rows / nodes) ---
+    {
+      const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
+                   *ru = V.row(R_RU);
+      double *sig = V.row(R_SIG), *rml = V.row(R_RML), *rmu = V.row(R_RMU), *w = V.row(R_W);
+      for (int j = R.r0 + tid; j < R.r1; j += NT) {
+        sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
+        rml[j] = tl[j] * ll[j];
+        rmu[j] = tu[j] * lu[j];
+        w[j] = (rml[j] + ll[j] * rl[j]) / tl[j] - (rmu[j] + lu[j] * ru[j]) / tu[j];
+      }
+    }
+    __syncthreads();
+    step_rhs_range(V, R.k0, R.k1, R.n1);
+    if (!sync()) break;
+    OCP_STAMP(2);
+    // --- factorisation on workgroup 0 ---
+    if (lead) {
+      bool fok;
+      if constexpr (FAST) fok = chain_factor(V, CS, hp, a.reg);
+      else fok = factor_pass<64>(V, S, a.reg);
+      if (tid == 0) mine[5] = fok ? 0.0 : 1.0;
+    } else if (tid == 0) {
+      mine[5] = 0.0;
+    }
+    if (!sync()) break;
+    grid_collect(part + 5, G, 1, ops_max, red);
+    OCP_STAMP(17);
+    if (red[0] != 0.0) {
+      status = 3;
+      break;
+    }
+    acl_pass(V, S, true, R.k0, R.k1, true);
+    if (!sync()) break;
+    OCP_STAMP(3);
+    if (lead) forward_pass(V, S);
+    if (!sync()) break;
+    OCP_STAMP(4);
+    double amax = block_reduce(post_pass(V, R.k0, R.k1, R.n1), S.red, OpMin());
+    if (m > 0) {
+      if (tid == 0) mine[6] = amax;
+      if (!sync()) break;
+      grid_collect(part + 6, G, 1, ops_min, red);
+      amax = red[0];
+    }
+    OCP_STAMP(5);
+    double alpha = fmin(1.0, amax);
+    if (m > 0) {
+      // mu_aff and the corrector
+      double lm = 0.0;
+      const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *dtl = V.row(R_DTL),
+                   *dtu = V.row(R_DTU), *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
+      for (int j = R.r0 + tid; j < R.r1; j += NT)
+        lm += (tl[j] + alpha * dtl[j]) * (ll[j] + alpha * dll[j]) + (tu[j] + alpha * dtu[j]) * (lu[j] + alpha * dlu[j]);
+      {
+        const double v = block_reduce(lm, S.red, OpSum());
+        if (tid == 0) mine[7] = v;
+      }
+      if (!sync()) break;
+      grid_collect(part + 7, G, 1, ops_sum, red);
+      const double maff = red[0] / (2.0 * m);
+      const double ratio = maff / mu;
+      const double sigma = ratio * ratio * ratio;
+      if (sr && tid == 0) {
+        sr[0] = alpha;
+        sr[1] = maff;
+        sr[2] = sigma;
+      }
+      {
+        const double *rl = V.row(R_RL), *ru = V.row(R_RU);
+        double *rml = V.row(R_RML), *rmu = V.row(R_RMU), *w = V.row(R_W);
+        for (int j = R.r0 + tid; j < R.r1; j += NT) {
+          rml[j] = tl[j] * ll[j] + dtl[j] * dll[j] - sigma * mu;
+          rmu[j] = tu[j] * lu[j] + dtu[j] * dlu[j] - sigma * mu;
+          w[j] = (rml[j] + ll[j] * rl[j]) / tl[j] - (rmu[j] + lu[j] * ru[j]) / tu[j];
+        }
+      }
+      __syncthreads();
+      step_rhs_range(V, R.k0, R.k1, R.n1);
+      __syncthreads();
+      OCP_STAMP(6);
+      bwd_vec_a(V, R.k0, R.k1, last);
+      if (!sync()) break;
+      if (lead) bwd_vec_b(V, S);
+      if (!sync()) break;
+      bwd_vec_c(V, R.k0, R.k1);
+      __syncthreads();
+      OCP_STAMP(7);
+      acl_pass(V, S, false, R.k0, R.k1, true);
+      if (!sync()) break;
+      if (lead) forward_pass(V, S);
+      if (!sync()) break;
+      OCP_STAMP(8);
+      {
+        const double v = block_reduce(post_pass(V, R.k0, R.k1, R.n1), S.red, OpMin());
+        if (tid == 0) mine[5] = v;
+      }
+      if (!sync()) break;
+      grid_collect(part + 5, G, 1, ops_min, red);
+      amax = red[0];
+      alpha = fmin(1.0, TAU_OCP * amax);
+    }
+    if (sr && tid == 0) sr[3] = sr[4] = alpha;
+    if (alpha < a.alpha_min) {
+      status = 2;
+      break;
+    }
+    // --- update (owned) ---
+    for (int i = (R.k0 > 1 ? R.k0 : 1) * nx + tid; i < R.n1 * nx; i += NT) x[i] = fma(alpha, V.dx()[i], x[i]);
+    for (int i = R.u0 + tid; i < R.u1; i += NT) u[i] = fma(alpha, V.du()[i], u[i]);
+    for (int i = R.k0 * nx + tid; i < R.k1 * nx; i += NT) V.pi()[i] = fma(alpha, V.dpi()[i], V.pi()[i]);
+    {
+      double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU);
+      const double *dtl = V.row(R_DTL), *dtu = V.row(R_DTU), *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
+      for (int j = R.r0 + tid; j < R.r1; j += NT) {
+        tl[j] = fma(alpha, dtl[j], tl[j]);
+        tu[j] = fma(alpha, dtu[j], tu[j]);
+        ll[j] = fma(alpha, dll[j], ll[j]);
+        lu[j] = fma(alpha, dlu[j], lu[j]);
+      }
+    }
+    if (!sync()) break;
+    OCP_STAMP(9);
+  }
+  if (!alive) status = 3;  // a barrier timed out: the grid drained, the result is not valid
+  // --- the exit point's Riccati quantities (cmpc_ocp_set_keep_riccati; k_ocp_ric's outputs, same formulas) ---
+  if (a.ric && alive && status != 3) {
+    // Sigma and the rows' step term at the exit iterate (complementarity kept), the step's right-hand side
+    {
+      const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
+                   *ru = V.row(R_RU);
+      double *sig = V.row(R_SIG), *w = V.row(R_W);
+      for (int j = R.r0 + tid; j < R.r1; j += NT) {
+        sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
+        w[j] = ll[j] * rl[j] / tl[j] - lu[j] * ru[j] / tu[j];
+      }
+    }
+    __syncthreads();
+    step_rhs_range(V, R.k0, R.k1, R.n1);
+    sync();
+    // without rows the last Newton step's factorisation is the exit point's (no Sigma): only the vector parts are
+    // redone (p_k, kff_k by the corrector's recursion on the kept K, Acl, LDL' factors); with rows (or no step taken)
+    // the factorisation itself at the exit point's Sigma
+    const bool full = m > 0 || it == 0;
+    if (full) {
+      if (lead) {
+        bool fok;
+        if constexpr (FAST) fok = chain_factor(V, CS, hp, a.reg);
+        else fok = factor_pass<64>(V, S, a.reg);
+        if (tid == 0) mine[5] = fok ? 0.0 : 1.0;
+      } else if (tid == 0) {
+        mine[5] = 0.0;
+      }
+    } else {
+      bwd_vec_a(V, R.k0, R.k1, last);
+      sync();
+      if (lead) bwd_vec_b(V, S);
+      sync();
+      bwd_vec_c(V, R.k0, R.k1);
+      if (tid == 0) mine[5] = 0.0;
+    }
+    sync();
+    grid_collect(part + 5, G, 1, ops_max, red);
+    const bool rok = alive && red[0] == 0.0;
+    const long long oP = (long long)q * (N + 1) * nx * nx, op = (long long)q * (N + 1) * nx;
+    const long long oK = (long long)q * (L.nK > 0 ? L.nK : 1), ok2 = (long long)q * (L.nU > 0 ? L.nU : 1),
+                    oM = (long long)q * (L.nM > 0 ? L.nM : 1);
+    if (rok) {  // owned stages / nodes >= 1; the Lr factor of every owned stage
+      for (int e = L.cK[R.k0] + tid; e < L.cK[R.k1]; e += NT) a.ricK[oK + e] = V.ws[L.o_K + e];
+      for (int k = R.k0; k < R.k1; ++k) {
+        const int mk = L.nu[k];
+        const double* F = V.Lf(k);
+        double* Lo = a.ricLr + oM + L.cM[k];
+        for (int e = tid; e < mk * mk; e += NT) {
+          const int j = e / mk, i = e - j * mk;
+          const double d = F[(long long)j * mk + j];
+          Lo[e] = (i >= j && d > 1e-200) ? F[e] / sqrt(d) : 0.0;
+        }
+      }
+      for (int e = (R.k0 > 1 ? L.cu[R.k0] : L.cu[1]) + tid; e < R.u1; e += NT) {
+        const int k = L.ustage[e], a2 = e - L.cu[k], mk = L.nu[k];
+        const double* Kk = V.K(k);
+        double s2 = u[e] + V.kf()[e];
+        for (int c = 0; c < nx; ++c) s2 = fma(-Kk[(long long)c * mk + a2], x[(long long)k * nx + c], s2);
+        a.rick[ok2 + e] = s2;
+      }
+      const int na = R.k0 > 1 ? R.k0 : 1;
+      for (int e = na * nx * nx + tid; e < R.n1 * nx * nx; e += NT) a.ricP[oP + e] = V.ws[L.o_P + e];
+      for (int e = na * nx + tid; e < R.n1 * nx; e += NT) {
+        const int k = e / nx, i = e - k * nx;
+        const double* Pk = V.P(k);
+        double s2 = V.pi()[(long long)(k - 1) * nx + i] + V.pv()[e];
+        for (int j = 0; j < nx; ++j) s2 = fma(-Pk[(long long)j * nx + i], x[(long long)k * nx + j], s2);
+        a.ricp[op + e] = s2;
+      }
+    }
+    sync();  // node 1's P, p and stage 0's Lr before the stage-0 reconstruction
+    if (lead && rok) ric_stage0(V, S, a.ricP + oP, a.ricp + op, a.ricK + oK, a.rick + ok2, a.ricLr + oM);
+    if (lead && tid == 0) a.ricst[q] = rok ? 0 : 3;
+  } else if (a.ric && lead && tid == 0) {
+    a.ricst[q] = 3;
+  }
+  // --- outputs (owned nodes / stages) ---
+  bool fin = true;
+  for (int i = R.k0 * nx + tid; i < R.n1 * nx; i += NT) {
+    const double v = x[i];
+    fin = fin && isfinite(v);
+    a.x[(long long)q * (N + 1) * nx + i] = v;
+  }
+  for (int i = R.u0 + tid; i < R.u1; i += NT) {
+    const double v = u[i];
+    fin = fin && isfinite(v);
+    a.u[(long long)q * L.nU + i] = v;
+  }
+  const bool allfin = __syncthreads_and(fin) != 0;
+  if (tid == 0) mine[7] = allfin ? 0.0 : 1.0;
+  const bool ok_end = sync();
+  if (ok_end) grid_collect(part + 7, G, 1, ops_max, red);
+  if (lead && tid == 0) {
+    if (!ok_end || red[0] != 0.0) status = 3;
+    a.status[q] = status;
+    if (a.iters) a.iters[q] = it;
+    if (a.res) {
+      a.res[(long long)q * 4 + 0] = rs;
+      a.res[(long long)q * 4 + 1] = re;
+      a.res[(long long)q * 4 + 2] = ri;
+      a.res[(long long)q * 4 + 3] = rc;
+    }
+    if (a.stats)  // rows after the last iteration: NaN (cmpc.h)
+      for (int r = it + 1; r < a.stat_rows; ++r)
+        for (int c = 0; c < 10; ++c) a.stats[((long long)q * a.stat_rows + r) * 10 + c] = __builtin_nan("");
+  }
+}
+
+// Grid form: G workgroups per problem (B G <= 256, one per CU), launched as k_ocp_grid<FAST>
+template <bool FAST>
+__global__ __launch_bounds__(NT, 1) void k_ocp_grid(OcpSolveArgs a) {
+  extern __shared__ double smem[];
+  ChainLds CS{};
+  const Lds S = FAST ? carve_fast(smem, a.L, CS) : carve(smem, a.L, 64);
+  const int q = blockIdx.x / a.G, g = blockIdx.x - q * a.G;
+  OCP_STAMP_BEGIN();
+  ipm_grid<FAST>(a, q, g, S, CS);
+  OCP_STAMP_END();
+}
+
+template <int NZP, int MINB, bool FAST>
 __global__ __launch_bounds__(NT, MINB) void k_ocp_ipm(OcpSolveArgs a) {
   extern __shared__ double smem[];
-  const Lds S = carve(smem, a.L, NZP);
-  OCP_STAMP(31);
-  ipm_body<NZP, MINB>(a, blockIdx.x, S);
+  ChainLds CS{};
+  const Lds S = FAST ? carve_fast(smem, a.L, CS) : carve(smem, a.L, NZP);
+  OCP_STAMP_BEGIN();
+  ipm_body<NZP, MINB, FAST>(a, blockIdx.x, S, CS);
+  OCP_STAMP_END();
 }
 
 // Riccati quantities at the exit point (see k_ocp.hpp / cmpc.h cmpc_ocp_riccati)
@@ -1474,88 +2145,37 @@ __global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
     r.p[op + (long long)k * nx + i] = s;
   }
   __syncthreads();
-  // stage 0, the reference's reconstruction (HpipmInterface.cpp:334-347, 376-389, 416-453) from P_1, p_1, Lr_0 and the
-  // stage-0 record: PA = P_1 A_0, v = p_1 + P_1 b_0, Mux = S_0 + B_0'PA, gr = r_0 + B_0'v, T1 = Lr_0^-1 Mux,
-  // t2 = Lr_0^-1 gr, K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2, P_0 = Q_0 + A_0'PA - T1'T1, p_0 = q_0 + A_0'v - T1't2.
-  // LDS: PA [nx][nx] in ABx, Mux / T1 [m0][nx] in Tx, v, gr / t2.
-  {
-    const int m0 = L.nu[0];
-    const double* P1 = r.P + oP + (long long)nx * nx;
-    const double* p1 = r.p + op + nx;
-    const double* A = V.A(0);
-    const double* Bm = V.Bm(0);
-    double* PA = S.ABx;
-    double* Mux = S.Tx;
-    double* v = S.vec;
-    double* gr = S.vec + 64;
-    for (int e = tid; e < nx * nx; e += NT) {
-      const int i = e / nx, j = e % nx;  // PA[i][j]
-      double s = 0.0;
-      for (int t = 0; t < nx; ++t) s = fma(P1[(long long)t * nx + i], A[(long long)j * nx + t], s);
-      PA[i * nx + j] = s;
-    }
-    for (int i = tid; i < nx; i += NT) {
-      double s = p1[i];
-      for (int t = 0; t < nx; ++t) s = fma(P1[(long long)t * nx + i], V.b(0)[t], s);
-      v[i] = s;
-    }
-    __syncthreads();
-    for (int e = tid; e < m0 * nx + m0; e += NT) {
-      if (e < m0 * nx) {
-        const int a2 = e / nx, j = e % nx;
-        double s = V.S(0)[(long long)j * m0 + a2];
-        for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a2 * nx + t], PA[t * nx + j], s);
-        Mux[a2 * nx + j] = s;
-      } else {
-        const int a2 = e - m0 * nx;
-        double s = V.r(0)[a2];
-        for (int t = 0; t < nx; ++t) s = fma(Bm[(long long)a2 * nx + t], v[t], s);
-        gr[a2] = s;
-      }
-    }
-    __syncthreads();
-    // T1 = Lr_0^-1 Mux (in place, Tx), t2 = Lr_0^-1 gr (in place); K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2 (in place in
-    // the outputs); one thread per right-hand side, the factor's guarded pivots (diag 0) contributing 0 as in HPIPM
-    const double* Lr0 = r.Lr + oM;
-    for (int j = tid; j <= nx; j += NT) {
-      double* c = j < nx ? Mux + j : gr;
-      const int cs = j < nx ? nx : 1;
-      double* o = j < nx ? r.K + oK + (long long)j * m0 : r.k + ok2;
-      for (int a2 = 0; a2 < m0; ++a2) {
-        double s = c[a2 * cs];
-        for (int b = 0; b < a2; ++b) s = fma(-Lr0[(long long)b * m0 + a2], c[b * cs], s);
-        const double d = Lr0[(long long)a2 * m0 + a2];
-        c[a2 * cs] = d > 0.0 ? s / d : 0.0;
-      }
-      for (int a2 = m0 - 1; a2 >= 0; --a2) {
-        double s = c[a2 * cs];
-        for (int b = a2 + 1; b < m0; ++b) s = fma(-Lr0[(long long)a2 * m0 + b], o[b], s);
-        const double d = Lr0[(long long)a2 * m0 + a2];
-        o[a2] = d > 0.0 ? s / d : 0.0;
-      }
-      for (int a2 = 0; a2 < m0; ++a2) o[a2] = -o[a2];
-    }
-    __syncthreads();
-    for (int e = tid; e < nx * nx + nx; e += NT) {
-      if (e < nx * nx) {
-        const int j = e / nx, i = e % nx;  // P_0 (i, j) = Q_0 + A_0'PA - T1'T1
-        double s = V.Q(0)[(long long)j * nx + i];
-        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], PA[t * nx + j], s);
-        for (int a2 = 0; a2 < m0; ++a2) s = fma(-Mux[a2 * nx + i], Mux[a2 * nx + j], s);
-        r.P[oP + e] = s;
-      } else {
-        const int i = e - nx * nx;  // p_0 = q_0 + A_0'v - T1't2
-        double s = V.q(0)[i];
-        for (int t = 0; t < nx; ++t) s = fma(A[(long long)i * nx + t], v[t], s);
-        for (int a2 = 0; a2 < m0; ++a2) s = fma(-Mux[a2 * nx + i], gr[a2], s);
-        r.p[op + i] = s;
-      }
-    }
-  }
+  ric_stage0(V, S, r.P + oP, r.p + op, r.K + oK, r.k + ok2, r.Lr + oM);
   if (tid == 0) r.rstatus[q] = ok ? 0 : 3;
 }
 
 }  // namespace
+
+#ifdef CMPC_OCP_CHAIN_LAB
+// Lab only (lab/ocp_stamps.sh): the latency-form factorisation alone on the workspace of the last solve, for timing
+// the chain in isolation (cmpc_ocp_debug_chain)
+namespace {
+__global__ __launch_bounds__(NT, 1) void k_ocp_chain_lab(OcpSolveArgs a) {
+  extern __shared__ double smem[];
+  ChainLds CS{};
+  (void)carve_fast(smem, a.L, CS);
+  const View V(a, blockIdx.x);
+  double* hp = a.hp + (long long)blockIdx.x * a.hp_stride;
+  hp_build(V, hp, a.reg);
+  __syncthreads();
+  if (!chain_factor(V, CS, hp, a.reg) && threadIdx.x == 0) a.status[blockIdx.x] = 3;
+}
+}  // namespace
+int launch_ocp_chain_lab(const OcpSolveArgs& a, int B, hipStream_t stream) {
+  const size_t lc = ocp_chain_lds_bytes(a.L, a.L.numax);
+  if (!lc || !a.hp) return -1;
+  if (hipFuncSetAttribute((const void*)k_ocp_chain_lab, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lc) !=
+      hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(k_ocp_chain_lab, dim3(B), dim3(NT), lc, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef CMPC_OCP_STAMPS
 extern "C" int cmpc_ocp_debug_stamps(unsigned long long* out, int reset) {
@@ -1574,25 +2194,68 @@ size_t ocp_lds_bytes(const OcpLayout& L) {
   return sizeof(double) * (pa + 2 * (size_t)nrm * L.nzp + 4 * (size_t)L.nzp + 128 + 64 + 64);
 }
 
+int ocp_grid_width(int N, int B, int want) {
+  if (B <= 0 || B > OCP_GRID_MAX_B) return 0;
+  static int ncu = 0;  // every workgroup of the grid needs a CU of its own (co-residency of the grid barriers)
+  if (ncu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                hipSuccess)
+      ncu = n;
+    if (ncu <= 0) ncu = 1;
+  }
+  const int cap = ncu < OCP_GRID_MAX_WG ? ncu : OCP_GRID_MAX_WG;
+  int G = want > 0 ? want : OCP_GRID_MAX_G;
+  if (G > N) G = N;
+  if (G * B > cap) G = cap / B;
+  if (G > OCP_GRID_MAX_G) G = OCP_GRID_MAX_G;
+  return G >= 2 ? G : 0;
+}
+
+size_t ocp_chain_lds_bytes(const OcpLayout& L, int numax) {
+  if (L.nzp != 64 || L.nx > OCP_CHAIN_MAX_NX || numax > OCP_CHAIN_MAX_NU || L.nx + numax + 1 > 64 ||
+      L.ngmax > CH_MAXG || L.N > CH_MAXN)
+    return 0;
+  const size_t ngr = CH_NRP + (size_t)L.ngmax, ngp = (size_t)((L.ngmax + 2) & ~1);
+  const size_t d = 2 * ngr * CH_GS + (size_t)CH_NRP * CH_GS + CH_PS * CH_PS + 256 + 2 * ngp + 64 + 128;
+  return sizeof(double) * d + sizeof(int) * CH_DESC * (size_t)L.N;
+}
+
 int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   OcpSolveArgs a = a0;
   a.par_res = B <= OCP_PAR_RES_MAX ? 1 : 0;
-  const size_t lds = ocp_lds_bytes(a.L);
-  if (a.L.nzp == 64) {
-    // one problem per CU while the batch leaves CUs idle anyway, two per CU beyond (cmpc_ocp_solve's B)
-    const bool two = B > OCP_ONE_PER_CU_MAX;
-    const void* kf = two ? (const void*)k_ocp_ipm<64, 2> : (const void*)k_ocp_ipm<64, 1>;
-    if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
-    if (two)
-      hipLaunchKernelGGL((k_ocp_ipm<64, 2>), dim3(B), dim3(NT), lds, stream, a);
-    else
-      hipLaunchKernelGGL((k_ocp_ipm<64, 1>), dim3(B), dim3(NT), lds, stream, a);
-  } else {
-    if (hipFuncSetAttribute((const void*)k_ocp_ipm<128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+  const size_t lc = ocp_chain_lds_bytes(a.L, a.L.numax);
+  a.fast = (a0.fast && a0.hp && lc > 0 && B <= OCP_ONE_PER_CU_MAX) ? 1 : 0;
+  size_t lds = ocp_lds_bytes(a.L);
+  if (a.fast && lc > lds) lds = lc;
+  const int G = a.fast && a.bar && a.gpart ? ocp_grid_width(a.L.N, B, a.G) : 0;
+  if (G > 0) {  // grid form: G workgroups per problem, one per CU; the barrier words zeroed before every launch
+    a.G = G;
+    if (hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 4 * (size_t)B, stream) != hipSuccess) return -1;
+    if (hipFuncSetAttribute((const void*)k_ocp_grid<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
       return -1;
-    hipLaunchKernelGGL((k_ocp_ipm<128, 1>), dim3(B), dim3(NT), lds, stream, a);
+    hipLaunchKernelGGL(k_ocp_grid<true>, dim3(B * G), dim3(NT), lds, stream, a);
+  } else if (a.fast) {  // the latency form (k_ocp_ipm<64, 1, true>): B <= OCP_ONE_PER_CU_MAX, one problem per CU
+    if (hipFuncSetAttribute((const void*)k_ocp_ipm<64, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return -1;
+    hipLaunchKernelGGL((k_ocp_ipm<64, 1, true>), dim3(B), dim3(NT), lds, stream, a);
+  } else if (a.L.nzp == 64) {
+    // one problem per CU while the batch leaves CUs idle anyway, two per CU beyond (cmpc_ocp_solve's B)
+    const bool two = B > OCP_ONE_PER_CU_MAX;
+    const void* kf = two ? (const void*)k_ocp_ipm<64, 2, false> : (const void*)k_ocp_ipm<64, 1, false>;
+    if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
+    if (two)
+      hipLaunchKernelGGL((k_ocp_ipm<64, 2, false>), dim3(B), dim3(NT), lds, stream, a);
+    else
+      hipLaunchKernelGGL((k_ocp_ipm<64, 1, false>), dim3(B), dim3(NT), lds, stream, a);
+  } else {
+    if (hipFuncSetAttribute((const void*)k_ocp_ipm<128, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return -1;
+    hipLaunchKernelGGL((k_ocp_ipm<128, 1, false>), dim3(B), dim3(NT), lds, stream, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -22,7 +22,7 @@ enum OcpRow { R_C = 0, R_LG, R_UG, R_TL, R_TU, R_LL, R_LU, R_RL, R_RU, R_RML, R_
 // Device arrays are owned by the cmpc_ocp handle (allocated once in cmpc_ocp_create, as HpipmInterface::resize
 // reserves HPIPM's memory, HpipmInterface.cpp:92-129).
 struct OcpLayout {
-  int N, nx, nU, m, nzp, ngmax;
+  int N, nx, nU, m, nzp, ngmax, numax;
   int nK, nM;                    // sum nu_k nx, sum nu_k^2
   const int* nu;                 // [N+1], nu[N] = 0
   const int* ng;                 // [N+1]
@@ -34,12 +34,23 @@ struct OcpLayout {
   const long long* ocon;         // [N+1][4] constraint-record offsets: C, D, e, (pad)
   const int* ustage;             // [nU] stage of each input entry
   const int* rstage;             // [m] node of each row
+  const int* cHp;                // [N+1] offsets of the stages' Hc images (ocp_chain.hpp; cHp[N] = per-problem size)
   long long rec_size, crec_size;
   // workspace (doubles) per problem: stride and array offsets
   long long ws_stride;
   long long o_x, o_u, o_pi, o_rgu, o_rgx, o_rb, o_gu, o_gx, o_du, o_dx, o_dpi, o_rows, o_P, o_pv, o_K, o_kf,
       o_Lf, o_Acl, o_h, o_y, o_bcl;  // o_Lf: the u-block's LDL' columns per stage (nu_k x nu_k, column-major)
 };
+
+// Grid form (k_ocp_grid, batches up to OCP_GRID_MAX_B): G workgroups per problem, one per CU, B G <= OCP_GRID_MAX_WG
+constexpr int OCP_GRID_MAX_B = 32;
+constexpr int OCP_GRID_MAX_G = 32;
+constexpr int OCP_GRID_MAX_WG = 256;
+int ocp_grid_width(int N, int B, int want);  // G for a batch (0: not the grid form)
+
+// Limits of the latency form of the factorisation (ocp_chain.hpp, small batches)
+constexpr int OCP_CHAIN_MAX_NX = 27;
+constexpr int OCP_CHAIN_MAX_NU = 36;  // nu_k + nx + 1 <= 64 bounds it as well
 
 struct OcpSolveArgs {
   OcpLayout L;
@@ -57,6 +68,15 @@ struct OcpSolveArgs {
   int iter_max;
   int warm;  // Settings.warm_start: x (nodes >= 1), u start from x / u (HPIPM's primal warm start)
   int par_res;  // residuals of all nodes at once (small batches, set by launch_ocp_ipm) or node by node staged
+  int fast;     // latency form of the factorisation (ocp_chain.hpp; k_ocp_ipm<64, 1> only, set by launch_ocp_ipm)
+  double* hp;   // [B][hp_stride] Hc images of the latency form (nullptr when the handle has none)
+  long long hp_stride;
+  int G;           // grid form: workgroups per problem (0: one workgroup per problem)
+  unsigned* bar;   // grid form: [B][4] barrier counter, fail word (zeroed before every launch)
+  double* gpart;   // grid form: [B][G][8] per-workgroup partials of the reductions
+  int ric;         // grid form: the exit Riccati quantities into ricP .. ricst (cmpc_ocp_set_keep_riccati)
+  double *ricP, *ricp, *ricK, *rick, *ricLr;
+  int* ricst;
   double alpha_min, mu0, tol_stat, tol_eq, tol_ineq, tol_comp, reg;
 };
 
@@ -68,9 +88,14 @@ struct OcpRicArgs {
   int* rstatus;
 };
 
-// LDS bytes of the kernels for a layout
+// LDS bytes of the kernels for a layout (the latency form's, 0 when the layout is outside its limits)
 size_t ocp_lds_bytes(const OcpLayout& L);
+size_t ocp_chain_lds_bytes(const OcpLayout& L, int numax);
+// launch_ocp_ipm takes the latency form for B <= OCP_ONE_PER_CU_MAX when a.fast != 0 on entry (the handle has it)
 int launch_ocp_ipm(const OcpSolveArgs& a, int B, hipStream_t stream);
 int launch_ocp_ric(const OcpRicArgs& a, int B, hipStream_t stream);
+#ifdef CMPC_OCP_CHAIN_LAB
+int launch_ocp_chain_lab(const OcpSolveArgs& a, int B, hipStream_t stream);
+#endif
 
 }  // namespace cmpc

@@ -1,7 +1,9 @@
 // ocp_api.cpp — C ABI of the HpipmInterface::solve path (cmpc.h "Generic OCP-QP"): the cmpc_ocp handle owns the
-// problem dimensions, the settings and every device buffer, sized once at creation as HpipmInterface's
-// initializeMemory reserves HPIPM's memory (reference HpipmInterface.cpp:92-129); solves launch k_ocp_ipm
-// (k_ocp.hip) and allocate nothing.
+// problem dimensions, the settings and every device buffer. As HpipmInterface's MemoryBlock::reserve grows HPIPM's
+// memory only (reference HpipmInterface.cpp:46-67, :92-129), every buffer has a capacity that only grows: a new size
+// (cmpc_ocp_reshape, the mirror's resize) re-lays out the dimensions and offsets with one small upload and allocates
+// only where it exceeds the capacity (with headroom for the MPC's shifting event nodes). Solves launch k_ocp_ipm /
+// k_ocp_grid (k_ocp.hip) and allocate nothing; the host entry point copies through pinned staging buffers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,22 +16,32 @@
 
 using cmpc::OcpLayout;
 
+namespace {
+struct DBuf {  // device buffer with a grow-only capacity (bytes)
+  void* p = nullptr;
+  size_t cap = 0;
+};
+}  // namespace
+
 struct cmpc_ocp {
   int N = 0, nx = 0, nU = 0, m = 0, max_batch = 0, stat_rows = 0;
   std::vector<int> nu, ng;
   cmpc_settings s{};
   OcpLayout L{};
   size_t rec_size = 0, crec_size = 0;
-  void* d_dims = nullptr;  // layout arrays
-  double* d_ws = nullptr;  // [max_batch][ws_stride]
-  // staging of the host entry points and the per-problem outputs the device path keeps
-  double *d_x0 = nullptr, *d_rec = nullptr, *d_crec = nullptr, *d_x = nullptr, *d_u = nullptr, *d_res = nullptr,
-         *d_stats = nullptr;
-  int *d_status = nullptr, *d_iters = nullptr, *d_rst = nullptr;
-  double *d_P = nullptr, *d_p = nullptr, *d_K = nullptr, *d_k = nullptr, *d_Lr = nullptr;
+  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart;
+  long long hp_stride = 0;
+  int hp_batch = 0, chain = 1;  // chain: cmpc_ocp_set_path (1 = the latency form where it applies, 0 = never)
+  int grid = 0;                 // cmpc_ocp_set_grid: workgroups per problem of the grid form (0 auto, 1 off)
+  int keep_ric = 0;             // cmpc_ocp_set_keep_riccati: the grid-form solve leaves the exit Riccati quantities
+  void* pin = nullptr;          // pinned host staging of cmpc_ocp_solve_host / _riccati_host (small batches)
+  size_t pin_cap = 0;
+  int allocs = 0;               // device / pinned allocations made (cmpc_ocp_alloc_count)
+  int timing = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t ev_done = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;  // the last solve's end; timing events
   // the last solve (for cmpc_ocp_riccati)
-  int last_B = 0;
+  int last_B = 0, ric_B = 0;  // ric_B: problems whose exit Riccati quantities the last solve left in P .. Lr
   const double *last_rec = nullptr, *last_crec = nullptr;
   int* last_status = nullptr;
 };
@@ -63,7 +75,7 @@ bool settings_ok(const cmpc_settings* s) {
 
 // host image of the layout arrays; also fills the scalar fields of L (workspace map)
 struct Dims {
-  std::vector<int> nu, ng, cu, cr, cK, cM, ustage, rstage;
+  std::vector<int> nu, ng, cu, cr, cK, cM, ustage, rstage, cHp;
   std::vector<long long> orec, ocon;
 };
 
@@ -79,7 +91,13 @@ Dims build_dims(int N, int nx, const int* nu, const int* nc, OcpLayout& L, size_
   d.cr.assign((size_t)NP + 1, 0);
   d.cK.assign((size_t)NP, 0);
   d.cM.assign((size_t)NP, 0);
-  int nK = 0, nM = 0;
+  d.cHp.assign((size_t)NP, 0);
+  int nK = 0, nM = 0, numax = 0;
+  for (int k = 0; k < N; ++k) {  // the latency form's Hc images: 2 x 2 lower blocks of the (nu_k + nx + 1) matrix
+    const int n1 = d.nu[(size_t)k] + nx + 1, nb = (n1 + 1) / 2;
+    d.cHp[(size_t)k + 1] = d.cHp[(size_t)k] + 4 * (nb * (nb + 1) / 2);
+    numax = std::max(numax, d.nu[(size_t)k]);
+  }
   for (int k = 0; k <= N; ++k) {
     d.cu[(size_t)k + 1] = d.cu[(size_t)k] + d.nu[(size_t)k];
     d.cr[(size_t)k + 1] = d.cr[(size_t)k] + d.ng[(size_t)k];
@@ -120,6 +138,7 @@ Dims build_dims(int N, int nx, const int* nu, const int* nc, OcpLayout& L, size_
   crec_size = (size_t)oc;
   L.N = N;
   L.nx = nx;
+  L.numax = numax;
   L.nU = nU;
   L.m = m;
   L.nK = nK;
@@ -165,48 +184,199 @@ size_t vbytes(const std::vector<T>& v) {
 }
 
 void free_all(cmpc_ocp* o) {
-  for (void* p : {(void*)o->d_dims, (void*)o->d_ws, (void*)o->d_x0, (void*)o->d_rec, (void*)o->d_crec, (void*)o->d_x,
-                  (void*)o->d_u, (void*)o->d_res, (void*)o->d_stats, (void*)o->d_status, (void*)o->d_iters,
-                  (void*)o->d_rst, (void*)o->d_P, (void*)o->d_p, (void*)o->d_K, (void*)o->d_k, (void*)o->d_Lr})
-    if (p) (void)hipFree(p);
+  for (DBuf* b : {&o->dims, &o->ws, &o->x0, &o->rec, &o->crec, &o->x, &o->u, &o->res, &o->stats, &o->status,
+                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart})
+    if (b->p) (void)hipFree(b->p);
+  if (o->pin) (void)hipHostFree(o->pin);
+  if (o->ev_done) (void)hipEventDestroy(o->ev_done);
+  if (o->ev_t0) (void)hipEventDestroy(o->ev_t0);
+  if (o->ev_t1) (void)hipEventDestroy(o->ev_t1);
   if (o->stream) (void)hipStreamDestroy(o->stream);
 }
 
-size_t per_problem_doubles(const cmpc_ocp* o) {
-  const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx;
-  return (size_t)o->L.ws_stride + nx + o->rec_size + o->crec_size + NP * nx + (size_t)std::max(o->nU, 1) + 4 +
-         (size_t)o->stat_rows * CMPC_STAT_COLS + NP * nx * nx + NP * nx + (size_t)std::max(o->L.nK, 1) +
-         (size_t)std::max(o->nU, 1) + (size_t)std::max(o->L.nM, 1) + 3;
+// Grow-only capacity: a buffer is reallocated only when a size exceeds it; handles for small batches (the MPC tick)
+// take 25 % headroom at the first allocation and 50 % at a growth, so the event nodes and per-stage input counts that
+// shift from tick to tick stay inside it
+int grow(cmpc_ocp* o, DBuf& b, size_t need) {
+  if (need <= b.cap) return CMPC_OK;
+  const bool small = o->max_batch <= cmpc::OCP_GRID_MAX_B;
+  const size_t want = b.cap == 0 ? need + (small ? need / 4 : 0) : need + need / 2;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  if (hipMalloc(&b.p, want) != hipSuccess) return CMPC_ERR_HIP;
+  b.cap = want;
+  ++o->allocs;
+  return CMPC_OK;
+}
+
+// pinned staging bytes of the host entry points for B problems (inputs, then outputs, then the Riccati outputs)
+struct PinMap {
+  size_t x0, rec, crec, x, u, st, it, P, p, K, k, Lr, rst, total;
+};
+PinMap pin_map(const cmpc_ocp* o, int B) {
+  PinMap m;
+  const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx, b = (size_t)B;
+  auto al = [](size_t n) { return (n + 63) & ~(size_t)63; };
+  size_t at = 0;
+  m.x0 = at, at += al(sizeof(double) * b * nx);
+  m.rec = at, at += al(sizeof(double) * b * o->rec_size);
+  m.crec = at, at += al(sizeof(double) * b * std::max<size_t>(o->crec_size, 1));
+  m.x = at, at += al(sizeof(double) * b * NP * nx);
+  m.u = at, at += al(sizeof(double) * b * (size_t)std::max(o->nU, 1));
+  m.st = at, at += al(sizeof(int) * b);
+  m.it = at, at += al(sizeof(int) * b);
+  m.P = at, at += al(sizeof(double) * b * NP * nx * nx);
+  m.p = at, at += al(sizeof(double) * b * NP * nx);
+  m.K = at, at += al(sizeof(double) * b * (size_t)std::max(o->L.nK, 1));
+  m.k = at, at += al(sizeof(double) * b * (size_t)std::max(o->nU, 1));
+  m.Lr = at, at += al(sizeof(double) * b * (size_t)std::max(o->L.nM, 1));
+  m.rst = at, at += al(sizeof(int) * b);
+  m.total = at;
+  return m;
+}
+
+int grow_pin(cmpc_ocp* o, size_t need) {
+  if (need <= o->pin_cap) return CMPC_OK;
+  const size_t want = o->pin_cap == 0 ? need + need / 4 : need + need / 2;
+  if (o->pin) (void)hipHostFree(o->pin);
+  o->pin = nullptr;
+  o->pin_cap = 0;
+  if (hipHostMalloc(&o->pin, want, hipHostMallocDefault) != hipSuccess) return CMPC_ERR_HIP;
+  o->pin_cap = want;
+  ++o->allocs;
+  return CMPC_OK;
 }
 
 int alloc_stats(cmpc_ocp* o) {
-  if (o->d_stats) (void)hipFree(o->d_stats);
-  o->d_stats = nullptr;
   o->stat_rows = o->s.iter_max + 1;
-  return hipMalloc((void**)&o->d_stats, sizeof(double) * (size_t)o->max_batch * o->stat_rows * CMPC_STAT_COLS) ==
-                 hipSuccess
-             ? CMPC_OK
-             : CMPC_ERR_HIP;
+  return grow(o, o->stats, sizeof(double) * (size_t)o->max_batch * o->stat_rows * CMPC_STAT_COLS);
 }
+
+// (Re-)lay out the handle for dimensions (N, nx, nu, nc): the layout arrays are uploaded into the dims block, every
+// device buffer grows to the new size if it exceeds its capacity, nothing else is allocated
+int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
+  int nzp = 0, ngmax = 0;
+  if (!dims_ok(N, nx, nu, nc, nzp, ngmax)) return CMPC_ERR_ARG;
+  OcpLayout L{};
+  L.nzp = nzp;
+  L.ngmax = ngmax;
+  size_t rec_size = 0, crec_size = 0;
+  Dims d = build_dims(N, nx, nu, nc, L, rec_size, crec_size);
+  if (cmpc::ocp_lds_bytes(L) > 160 * 1024) return CMPC_ERR_ARG;
+  // work of an earlier layout may still be in flight on the device (its dims block is about to be overwritten)
+  if (o->ev_done && hipEventSynchronize(o->ev_done) != hipSuccess) return CMPC_ERR_HIP;
+  const size_t b_int = vbytes(d.nu) + vbytes(d.ng) + vbytes(d.cu) + vbytes(d.cr) + vbytes(d.cK) + vbytes(d.cM) +
+                       vbytes(d.ustage) + vbytes(d.rstage) + vbytes(d.cHp) + 10 * 8;
+  const size_t b_ll = vbytes(d.orec) + vbytes(d.ocon);
+  int r = grow(o, o->dims, b_ll + b_int + 64);
+  if (r != CMPC_OK) return r;
+  std::vector<unsigned char> img(b_ll + b_int + 64, 0);
+  size_t off = 0;
+  auto put = [&](const void* src, size_t n) {
+    std::memcpy(img.data() + off, src, n);
+    const size_t at = off;
+    off += (n + 7) & ~(size_t)7;
+    return (const void*)((unsigned char*)o->dims.p + at);
+  };
+  L.orec = (const long long*)put(d.orec.data(), vbytes(d.orec));
+  L.ocon = (const long long*)put(d.ocon.data(), vbytes(d.ocon));
+  L.nu = (const int*)put(d.nu.data(), vbytes(d.nu));
+  L.ng = (const int*)put(d.ng.data(), vbytes(d.ng));
+  L.cu = (const int*)put(d.cu.data(), vbytes(d.cu));
+  L.cr = (const int*)put(d.cr.data(), vbytes(d.cr));
+  L.cK = (const int*)put(d.cK.data(), vbytes(d.cK));
+  L.cM = (const int*)put(d.cM.data(), vbytes(d.cM));
+  L.ustage = (const int*)put(d.ustage.data(), vbytes(d.ustage));
+  L.rstage = (const int*)put(d.rstage.data(), vbytes(d.rstage));
+  L.cHp = (const int*)put(d.cHp.data(), vbytes(d.cHp));
+  if (hipMemcpy(o->dims.p, img.data(), off, hipMemcpyHostToDevice) != hipSuccess) return CMPC_ERR_HIP;
+  const size_t B = (size_t)o->max_batch, NP = (size_t)N + 1, D = sizeof(double);
+  const int nU = L.nU;
+  auto ck = [&r](int e) {
+    if (r == CMPC_OK) r = e;
+  };
+  ck(grow(o, o->ws, D * B * (size_t)L.ws_stride));
+  ck(grow(o, o->x0, D * B * nx));
+  ck(grow(o, o->rec, D * B * rec_size));
+  ck(grow(o, o->crec, D * B * std::max<size_t>(crec_size, 1)));
+  ck(grow(o, o->x, D * B * NP * nx));
+  ck(grow(o, o->u, D * B * (size_t)std::max(nU, 1)));
+  ck(grow(o, o->res, D * B * 4));
+  ck(grow(o, o->status, sizeof(int) * B));
+  ck(grow(o, o->iters, sizeof(int) * B));
+  ck(grow(o, o->rst, sizeof(int) * B));
+  ck(grow(o, o->P, D * B * NP * nx * nx));
+  ck(grow(o, o->p, D * B * NP * nx));
+  ck(grow(o, o->K, D * B * (size_t)std::max(L.nK, 1)));
+  ck(grow(o, o->k, D * B * (size_t)std::max(nU, 1)));
+  ck(grow(o, o->Lr, D * B * (size_t)std::max(L.nM, 1)));
+  // the latency form (small batches: one problem per CU, or G per problem) where the dimensions fit it
+  long long hp_stride = 0;
+  int hp_batch = 0;
+  const size_t lc = cmpc::ocp_chain_lds_bytes(L, L.numax);
+  if (lc > 0 && lc <= 160 * 1024) {
+    hp_batch = std::min(o->max_batch, cmpc::OCP_ONE_PER_CU_MAX);
+    hp_stride = ((long long)d.cHp[(size_t)N] + 1) & ~1LL;
+    ck(grow(o, o->hp, D * (size_t)hp_batch * (size_t)hp_stride));
+    if (!o->bar.p) {
+      ck(grow(o, o->bar, sizeof(unsigned) * 4 * (size_t)cmpc::OCP_GRID_MAX_B));
+      ck(grow(o, o->gpart, D * 8 * (size_t)cmpc::OCP_GRID_MAX_WG));
+    }
+  }
+  if (r != CMPC_OK) return r;
+  o->N = N;
+  o->nx = nx;
+  o->L = L;
+  o->nu = d.nu;
+  o->ng = d.ng;
+  o->nU = nU;
+  o->m = L.m;
+  o->rec_size = rec_size;
+  o->crec_size = crec_size;
+  o->hp_stride = hp_stride;
+  o->hp_batch = hp_batch;
+  o->last_B = 0;  // the Riccati quantities of a solve of another layout are gone
+  o->ric_B = 0;
+  o->last_rec = o->last_crec = nullptr;
+  o->last_status = nullptr;
+  return CMPC_OK;
+}
+
+bool has_chain(const cmpc_ocp* o) { return o->chain && o->hp_batch > 0 && o->hp.p; }
 
 cmpc::OcpSolveArgs solve_args(cmpc_ocp* o, const double* x0, const double* rec, const double* crec, double* x,
                               double* u, int* status, int* iters) {
-  cmpc::OcpSolveArgs a;
+  cmpc::OcpSolveArgs a{};
   a.par_res = 0;  // launch_ocp_ipm chooses by batch size
   a.L = o->L;
   a.x0 = x0;
   a.rec = rec;
   a.crec = o->m > 0 ? crec : nullptr;
-  a.ws = o->d_ws;
+  a.ws = (double*)o->ws.p;
   a.x = x;
   a.u = u;
   a.status = status;
   a.iters = iters;
-  a.res = o->d_res;
-  a.stats = o->d_stats;
+  a.res = (double*)o->res.p;
+  a.stats = (double*)o->stats.p;
   a.stat_rows = o->stat_rows;
   a.iter_max = o->s.iter_max;
   a.warm = (o->s.warm_start != 0 && x && u) ? 1 : 0;
+  a.fast = has_chain(o) ? 1 : 0;  // launch_ocp_ipm applies it to batches up to hp_batch
+  a.hp = (double*)o->hp.p;
+  a.hp_stride = o->hp_stride;
+  a.G = o->grid;  // 0 auto; 1 disables the grid form (ocp_grid_width returns 0 below 2)
+  a.bar = o->grid == 1 ? nullptr : (unsigned*)o->bar.p;
+  a.gpart = (double*)o->gpart.p;
+  // the exit Riccati quantities of the grid form (cmpc_ocp_set_keep_riccati) into the handle's arrays
+  a.ric = o->keep_ric;
+  a.ricP = (double*)o->P.p;
+  a.ricp = (double*)o->p.p;
+  a.ricK = (double*)o->K.p;
+  a.rick = (double*)o->k.p;
+  a.ricLr = (double*)o->Lr.p;
+  a.ricst = (int*)o->rst.p;
   a.alpha_min = o->s.alpha_min;
   a.mu0 = o->s.mu0;
   a.tol_stat = o->s.tol_stat;
@@ -245,15 +415,22 @@ size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* 
 size_t cmpc_ocp_memsize(int N, int nx, const int* nu, const int* nc, int max_batch) {
   int nzp = 0, ngmax = 0;
   if (!dims_ok(N, nx, nu, nc, nzp, ngmax) || max_batch <= 0) return 0;
-  cmpc_ocp o;
-  o.N = N;
-  o.nx = nx;
-  o.L.ngmax = ngmax;
-  Dims d = build_dims(N, nx, nu, nc, o.L, o.rec_size, o.crec_size);
-  o.nU = o.L.nU;
-  o.stat_rows = 31;
-  return sizeof(double) * per_problem_doubles(&o) * (size_t)max_batch + vbytes(d.nu) * 8 + vbytes(d.orec) +
-         vbytes(d.ocon) + vbytes(d.ustage) + vbytes(d.rstage);
+  OcpLayout L{};
+  L.nzp = nzp;
+  L.ngmax = ngmax;
+  size_t rec_size = 0, crec_size = 0;
+  Dims d = build_dims(N, nx, nu, nc, L, rec_size, crec_size);
+  if (cmpc::ocp_lds_bytes(L) > 160 * 1024) return 0;  // cmpc_ocp_create refuses these dimensions
+  const size_t NP = (size_t)N + 1, B = (size_t)max_batch;
+  const size_t per = (size_t)L.ws_stride + nx + rec_size + crec_size + NP * nx + (size_t)std::max(L.nU, 1) + 4 +
+                     31 * CMPC_STAT_COLS + NP * nx * nx + NP * nx + (size_t)std::max(L.nK, 1) +
+                     (size_t)std::max(L.nU, 1) + (size_t)std::max(L.nM, 1) + 3;
+  const size_t hp = cmpc::ocp_chain_lds_bytes(L, L.numax) > 0
+                        ? sizeof(double) * (size_t)std::min(max_batch, cmpc::OCP_ONE_PER_CU_MAX) *
+                              (size_t)(d.cHp[(size_t)N] + 1)
+                        : 0;
+  return sizeof(double) * per * B + vbytes(d.nu) * 9 + vbytes(d.orec) + vbytes(d.ocon) + vbytes(d.ustage) +
+         vbytes(d.rstage) + hp;
 }
 
 int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_settings* settings, int max_batch,
@@ -269,69 +446,17 @@ int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_sett
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return CMPC_ERR_NO_DEVICE;
   cmpc_ocp* o = new cmpc_ocp();
-  o->N = N;
-  o->nx = nx;
   o->max_batch = max_batch;
   o->s = s;
-  o->L.nzp = nzp;
-  o->L.ngmax = ngmax;
-  Dims d = build_dims(N, nx, nu, nc, o->L, o->rec_size, o->crec_size);
-  o->nu = d.nu;
-  o->ng = d.ng;
-  o->nU = o->L.nU;
-  o->m = o->L.m;
-  if (cmpc::ocp_lds_bytes(o->L) > 160 * 1024) {
-    delete o;
-    return CMPC_ERR_ARG;
-  }
-  // one device block for the layout arrays
-  const size_t b_int = vbytes(d.nu) + vbytes(d.ng) + vbytes(d.cu) + vbytes(d.cr) + vbytes(d.cK) + vbytes(d.cM) +
-                       vbytes(d.ustage) + vbytes(d.rstage) + 8 * sizeof(int);
-  const size_t b_ll = vbytes(d.orec) + vbytes(d.ocon);
   int r = CMPC_OK;
-  auto ck = [&r](hipError_t e) {
-    if (e != hipSuccess) r = CMPC_ERR_HIP;
-  };
-  ck(hipMalloc(&o->d_dims, b_ll + b_int + 64));
-  if (r == CMPC_OK) {
-    std::vector<unsigned char> img(b_ll + b_int + 64, 0);
-    size_t off = 0;
-    auto put = [&](const void* src, size_t n) {
-      std::memcpy(img.data() + off, src, n);
-      const size_t at = off;
-      off += (n + 7) & ~(size_t)7;
-      return (const void*)((unsigned char*)o->d_dims + at);
-    };
-    o->L.orec = (const long long*)put(d.orec.data(), vbytes(d.orec));
-    o->L.ocon = (const long long*)put(d.ocon.data(), vbytes(d.ocon));
-    o->L.nu = (const int*)put(d.nu.data(), vbytes(d.nu));
-    o->L.ng = (const int*)put(d.ng.data(), vbytes(d.ng));
-    o->L.cu = (const int*)put(d.cu.data(), vbytes(d.cu));
-    o->L.cr = (const int*)put(d.cr.data(), vbytes(d.cr));
-    o->L.cK = (const int*)put(d.cK.data(), vbytes(d.cK));
-    o->L.cM = (const int*)put(d.cM.data(), vbytes(d.cM));
-    o->L.ustage = (const int*)put(d.ustage.data(), vbytes(d.ustage));
-    o->L.rstage = (const int*)put(d.rstage.data(), vbytes(d.rstage));
-    ck(hipMemcpy(o->d_dims, img.data(), img.size(), hipMemcpyHostToDevice));
-  }
-  const size_t B = (size_t)max_batch, NP = (size_t)N + 1;
-  ck(hipMalloc((void**)&o->d_ws, sizeof(double) * B * (size_t)o->L.ws_stride));
-  ck(hipMalloc((void**)&o->d_x0, sizeof(double) * B * nx));
-  ck(hipMalloc((void**)&o->d_rec, sizeof(double) * B * o->rec_size));
-  if (o->crec_size) ck(hipMalloc((void**)&o->d_crec, sizeof(double) * B * o->crec_size));
-  ck(hipMalloc((void**)&o->d_x, sizeof(double) * B * NP * nx));
-  ck(hipMalloc((void**)&o->d_u, sizeof(double) * B * (size_t)std::max(o->nU, 1)));
-  ck(hipMalloc((void**)&o->d_res, sizeof(double) * B * 4));
-  ck(hipMalloc((void**)&o->d_status, sizeof(int) * B));
-  ck(hipMalloc((void**)&o->d_iters, sizeof(int) * B));
-  ck(hipMalloc((void**)&o->d_rst, sizeof(int) * B));
-  ck(hipMalloc((void**)&o->d_P, sizeof(double) * B * NP * nx * nx));
-  ck(hipMalloc((void**)&o->d_p, sizeof(double) * B * NP * nx));
-  ck(hipMalloc((void**)&o->d_K, sizeof(double) * B * (size_t)std::max(o->L.nK, 1)));
-  ck(hipMalloc((void**)&o->d_k, sizeof(double) * B * (size_t)std::max(o->nU, 1)));
-  ck(hipMalloc((void**)&o->d_Lr, sizeof(double) * B * (size_t)std::max(o->L.nM, 1)));
+  if (hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&o->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&o->ev_t0) != hipSuccess || hipEventCreate(&o->ev_t1) != hipSuccess)
+    r = CMPC_ERR_HIP;
+  if (r == CMPC_OK) r = layout(o, N, nx, nu, nc);
   if (r == CMPC_OK) r = alloc_stats(o);
-  if (r == CMPC_OK) ck(hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking));
+  if (r == CMPC_OK && o->bar.p && hipMemset(o->bar.p, 0, o->bar.cap) != hipSuccess) r = CMPC_ERR_HIP;
+  if (r == CMPC_OK && max_batch <= cmpc::OCP_GRID_MAX_B) r = grow_pin(o, pin_map(o, max_batch).total);
   if (r != CMPC_OK) {
     free_all(o);
     delete o;
@@ -341,8 +466,18 @@ int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_sett
   return CMPC_OK;
 }
 
+int cmpc_ocp_reshape(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
+  if (!o) return CMPC_ERR_ARG;
+  const int r = layout(o, N, nx, nu, nc);
+  if (r != CMPC_OK) return r;
+  return o->max_batch <= cmpc::OCP_GRID_MAX_B ? grow_pin(o, pin_map(o, o->max_batch).total) : CMPC_OK;
+}
+
+int cmpc_ocp_alloc_count(const cmpc_ocp* o) { return o ? o->allocs : CMPC_ERR_ARG; }
+
 int cmpc_ocp_destroy(cmpc_ocp* o) {
   if (!o) return CMPC_ERR_ARG;
+  if (o->ev_done) (void)hipEventSynchronize(o->ev_done);
   if (o->stream) (void)hipStreamSynchronize(o->stream);
   free_all(o);
   delete o;
@@ -351,9 +486,60 @@ int cmpc_ocp_destroy(cmpc_ocp* o) {
 
 int cmpc_ocp_set_settings(cmpc_ocp* o, const cmpc_settings* s) {
   if (!o || !settings_ok(s)) return CMPC_ERR_ARG;
-  const bool grow = s->iter_max + 1 != o->stat_rows;
+  if (o->ev_done) (void)hipEventSynchronize(o->ev_done);
   o->s = *s;
-  return grow ? alloc_stats(o) : CMPC_OK;
+  return alloc_stats(o);
+}
+
+int cmpc_ocp_set_path(cmpc_ocp* o, int chain) {
+  if (!o || chain < 0 || chain > 1) return CMPC_ERR_ARG;
+  o->chain = chain;
+  return CMPC_OK;
+}
+
+int cmpc_ocp_path(const cmpc_ocp* o) { return o ? (has_chain(o) ? 1 : 0) : CMPC_ERR_ARG; }
+
+int cmpc_ocp_set_grid(cmpc_ocp* o, int G) {
+  if (!o || G < 0 || G > cmpc::OCP_GRID_MAX_G) return CMPC_ERR_ARG;
+  o->grid = G;
+  return CMPC_OK;
+}
+
+int cmpc_ocp_grid(const cmpc_ocp* o, int B) {
+  if (!o || B <= 0) return CMPC_ERR_ARG;
+  if (!has_chain(o) || !o->bar.p || o->grid == 1) return 0;
+  return cmpc::ocp_grid_width(o->N, B, o->grid);
+}
+
+int cmpc_ocp_set_keep_riccati(cmpc_ocp* o, int on) {
+  if (!o || on < 0 || on > 1) return CMPC_ERR_ARG;
+  o->keep_ric = on;
+  return CMPC_OK;
+}
+
+int cmpc_ocp_enable_timing(cmpc_ocp* o, int on) {
+  if (!o || on < 0 || on > 1) return CMPC_ERR_ARG;
+  o->timing = on;
+  return CMPC_OK;
+}
+
+int cmpc_ocp_last_solve_ms(cmpc_ocp* o, float* ms) {
+  if (!o || !ms || !o->timing || o->last_B == 0) return CMPC_ERR_ARG;
+  if (hipEventSynchronize(o->ev_t1) != hipSuccess || hipEventElapsedTime(ms, o->ev_t0, o->ev_t1) != hipSuccess)
+    return CMPC_ERR_HIP;
+  return CMPC_OK;
+}
+
+double* cmpc_ocp_staging(cmpc_ocp* o, int which) {
+  if (!o || !o->pin || o->max_batch > cmpc::OCP_GRID_MAX_B) return nullptr;
+  const PinMap m = pin_map(o, o->max_batch);
+  unsigned char* b = (unsigned char*)o->pin;
+  switch (which) {
+    case CMPC_OCP_STAGE_X0: return (double*)(b + m.x0);
+    case CMPC_OCP_STAGE_REC: return (double*)(b + m.rec);
+    case CMPC_OCP_STAGE_CREC: return (double*)(b + m.crec);
+    default: return nullptr;
+  }
 }
 
 int cmpc_ocp_solve(cmpc_ocp* o, int B, const double* d_x0, const double* d_rec, const double* d_crec, double* d_x,
@@ -362,11 +548,17 @@ int cmpc_ocp_solve(cmpc_ocp* o, int B, const double* d_x0, const double* d_rec, 
   if (o->m > 0 && !d_crec) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
   const cmpc::OcpSolveArgs a = solve_args(o, d_x0, d_rec, d_crec, d_x, d_u, d_status, d_iters);
-  if (cmpc::launch_ocp_ipm(a, B, (hipStream_t)stream) != 0) return CMPC_ERR_HIP;
+  hipStream_t st = (hipStream_t)stream;
+  if (o->timing) (void)hipEventRecord(o->ev_t0, st);
+  if (cmpc::launch_ocp_ipm(a, B, st) != 0) return CMPC_ERR_HIP;
+  if (o->timing) (void)hipEventRecord(o->ev_t1, st);
+  // the handle's getters (own stream) are ordered after this solve on the caller's stream
+  if (hipEventRecord(o->ev_done, st) != hipSuccess) return CMPC_ERR_HIP;
   o->last_B = B;
   o->last_rec = d_rec;
   o->last_crec = d_crec;
   o->last_status = d_status;
+  o->ric_B = (a.ric && a.fast && cmpc::ocp_grid_width(o->N, B, o->grid) > 0 && o->grid != 1) ? B : 0;
   return CMPC_OK;
 }
 
@@ -375,26 +567,62 @@ int cmpc_ocp_solve_host(cmpc_ocp* o, int B, const double* x0, const double* rec,
   if (!o || B < 0 || B > o->max_batch || !x0 || !rec || !x || (!u && o->nU > 0) || !status) return CMPC_ERR_ARG;
   if (o->m > 0 && !crec) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
-  const size_t NP = (size_t)o->N + 1;
+  const size_t NP = (size_t)o->N + 1, D = sizeof(double);
+  const size_t bx0 = D * B * o->nx, brec = D * B * o->rec_size, bcrec = D * B * o->crec_size,
+               bx = D * B * NP * o->nx, bu = D * B * o->nU;
   hipStream_t st = o->stream;
   int r = CMPC_OK;
   auto ck = [&r](hipError_t e) {
     if (e != hipSuccess) r = CMPC_ERR_HIP;
   };
-  ck(hipMemcpyAsync(o->d_x0, x0, sizeof(double) * B * o->nx, hipMemcpyHostToDevice, st));
-  ck(hipMemcpyAsync(o->d_rec, rec, sizeof(double) * B * o->rec_size, hipMemcpyHostToDevice, st));
-  if (o->m > 0) ck(hipMemcpyAsync(o->d_crec, crec, sizeof(double) * B * o->crec_size, hipMemcpyHostToDevice, st));
-  if (o->s.warm_start) {  // x, u are in / out: the initial guess (HPIPM's primal warm start)
-    ck(hipMemcpyAsync(o->d_x, x, sizeof(double) * B * NP * o->nx, hipMemcpyHostToDevice, st));
-    if (o->nU > 0) ck(hipMemcpyAsync(o->d_u, u, sizeof(double) * B * o->nU, hipMemcpyHostToDevice, st));
+  const bool pinned = o->pin && B <= o->max_batch && o->max_batch <= cmpc::OCP_GRID_MAX_B;
+  if (pinned) {  // through the pinned staging: the DMA runs from locked pages (a caller packing into
+    // cmpc_ocp_staging's buffers skips the host copy)
+    const PinMap m = pin_map(o, o->max_batch);
+    unsigned char* b = (unsigned char*)o->pin;
+    auto in = [&](size_t off, const void* src, size_t n, void* dev) {
+      if (n == 0) return;
+      if ((const void*)(b + off) != src) std::memcpy(b + off, src, n);
+      ck(hipMemcpyAsync(dev, b + off, n, hipMemcpyHostToDevice, st));
+    };
+    in(m.x0, x0, bx0, o->x0.p);
+    in(m.rec, rec, brec, o->rec.p);
+    if (o->m > 0) in(m.crec, crec, bcrec, o->crec.p);
+    if (o->s.warm_start) {  // x, u are in / out: the initial guess (HPIPM's primal warm start)
+      in(m.x, x, bx, o->x.p);
+      if (o->nU > 0) in(m.u, u, bu, o->u.p);
+    }
+    if (r != CMPC_OK) return r;
+    r = cmpc_ocp_solve(o, B, (double*)o->x0.p, (double*)o->rec.p, (double*)o->crec.p, (double*)o->x.p,
+                       (double*)o->u.p, (int*)o->status.p, (int*)o->iters.p, st);
+    if (r != CMPC_OK) return r;
+    ck(hipMemcpyAsync(b + m.x, o->x.p, bx, hipMemcpyDeviceToHost, st));
+    if (o->nU > 0) ck(hipMemcpyAsync(b + m.u, o->u.p, bu, hipMemcpyDeviceToHost, st));
+    ck(hipMemcpyAsync(b + m.st, o->status.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    ck(hipMemcpyAsync(b + m.it, o->iters.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+    ck(hipStreamSynchronize(st));
+    if (r != CMPC_OK) return r;
+    std::memcpy(x, b + m.x, bx);
+    if (o->nU > 0) std::memcpy(u, b + m.u, bu);
+    std::memcpy(status, b + m.st, sizeof(int) * B);
+    if (iters) std::memcpy(iters, b + m.it, sizeof(int) * B);
+    return r;
+  }
+  ck(hipMemcpyAsync(o->x0.p, x0, bx0, hipMemcpyHostToDevice, st));
+  ck(hipMemcpyAsync(o->rec.p, rec, brec, hipMemcpyHostToDevice, st));
+  if (o->m > 0) ck(hipMemcpyAsync(o->crec.p, crec, bcrec, hipMemcpyHostToDevice, st));
+  if (o->s.warm_start) {
+    ck(hipMemcpyAsync(o->x.p, x, bx, hipMemcpyHostToDevice, st));
+    if (o->nU > 0) ck(hipMemcpyAsync(o->u.p, u, bu, hipMemcpyHostToDevice, st));
   }
   if (r != CMPC_OK) return r;
-  r = cmpc_ocp_solve(o, B, o->d_x0, o->d_rec, o->d_crec, o->d_x, o->d_u, o->d_status, o->d_iters, st);
+  r = cmpc_ocp_solve(o, B, (double*)o->x0.p, (double*)o->rec.p, (double*)o->crec.p, (double*)o->x.p,
+                     (double*)o->u.p, (int*)o->status.p, (int*)o->iters.p, st);
   if (r != CMPC_OK) return r;
-  ck(hipMemcpyAsync(x, o->d_x, sizeof(double) * B * NP * o->nx, hipMemcpyDeviceToHost, st));
-  if (o->nU > 0) ck(hipMemcpyAsync(u, o->d_u, sizeof(double) * B * o->nU, hipMemcpyDeviceToHost, st));
-  ck(hipMemcpyAsync(status, o->d_status, sizeof(int) * B, hipMemcpyDeviceToHost, st));
-  if (iters) ck(hipMemcpyAsync(iters, o->d_iters, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+  ck(hipMemcpyAsync(x, o->x.p, bx, hipMemcpyDeviceToHost, st));
+  if (o->nU > 0) ck(hipMemcpyAsync(u, o->u.p, bu, hipMemcpyDeviceToHost, st));
+  ck(hipMemcpyAsync(status, o->status.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+  if (iters) ck(hipMemcpyAsync(iters, o->iters.p, sizeof(int) * B, hipMemcpyDeviceToHost, st));
   ck(hipStreamSynchronize(st));
   return r;
 }
@@ -404,43 +632,83 @@ int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, 
   if (!o || B <= 0 || B > o->last_B || !d_P || !d_p || !d_status || (o->nU > 0 && (!d_K || !d_k)) ||
       !o->last_rec || !o->last_status)
     return CMPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipStreamWaitEvent(st, o->ev_done, 0) != hipSuccess) return CMPC_ERR_HIP;  // after the solve's stream
+  if (B <= o->ric_B) {  // the solve left them (the grid form with keep_riccati): copies
+    const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx, D = sizeof(double);
+    int r = CMPC_OK;
+    auto cp = [&](void* dst, const void* src, size_t n) {
+      if (dst != src && n && hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st) != hipSuccess) r = CMPC_ERR_HIP;
+    };
+    cp(d_P, o->P.p, D * B * NP * nx * nx);
+    cp(d_p, o->p.p, D * B * NP * nx);
+    if (o->nU > 0) {
+      cp(d_K, o->K.p, D * B * o->L.nK);
+      cp(d_k, o->k.p, D * B * o->nU);
+    }
+    if (d_Lr_out && o->L.nM > 0) cp(d_Lr_out, o->Lr.p, D * B * o->L.nM);
+    cp(d_status, o->rst.p, sizeof(int) * B);
+    return r;
+  }
   cmpc::OcpRicArgs a;
   a.S = solve_args(o, nullptr, o->last_rec, o->last_crec, nullptr, nullptr, o->last_status, nullptr);
   a.P = d_P;
   a.p = d_p;
-  a.K = o->nU > 0 ? d_K : o->d_K;
-  a.k = o->nU > 0 ? d_k : o->d_k;
-  a.Lr = d_Lr_out ? d_Lr_out : o->d_Lr;
+  a.K = o->nU > 0 ? d_K : (double*)o->K.p;
+  a.k = o->nU > 0 ? d_k : (double*)o->k.p;
+  a.Lr = d_Lr_out ? d_Lr_out : (double*)o->Lr.p;
   a.rstatus = d_status;
-  return cmpc::launch_ocp_ric(a, B, (hipStream_t)stream) == 0 ? CMPC_OK : CMPC_ERR_HIP;
+  if (cmpc::launch_ocp_ric(a, B, st) != 0) return CMPC_ERR_HIP;
+  if (o->ric_B == 0 || d_P != o->P.p) o->ric_B = 0;  // the workspace's factorisation is the refactorised one now
+  return CMPC_OK;
 }
 
 int cmpc_ocp_riccati_host(cmpc_ocp* o, int B, double* P, double* p, double* K, double* k, double* Lr,
                           int* status) {
   if (!o || B <= 0 || B > o->last_B || !P || !p || !status || (o->nU > 0 && (!K || !k))) return CMPC_ERR_ARG;
   hipStream_t st = o->stream;
-  int r = cmpc_ocp_riccati(o, B, o->d_P, o->d_p, o->d_K, o->d_k, o->d_Lr, o->d_rst, st);
+  int r = cmpc_ocp_riccati(o, B, (double*)o->P.p, (double*)o->p.p, (double*)o->K.p, (double*)o->k.p,
+                           (double*)o->Lr.p, (int*)o->rst.p, st);
   if (r != CMPC_OK) return r;
-  const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx;
+  const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx, D = sizeof(double);
+  const size_t bP = D * B * NP * nx * nx, bp = D * B * NP * nx, bK = D * B * o->L.nK, bk = D * B * o->nU,
+               bL = D * B * o->L.nM;
   auto ck = [&r](hipError_t e) {
     if (e != hipSuccess) r = CMPC_ERR_HIP;
   };
-  ck(hipMemcpyAsync(P, o->d_P, sizeof(double) * B * NP * nx * nx, hipMemcpyDeviceToHost, st));
-  ck(hipMemcpyAsync(p, o->d_p, sizeof(double) * B * NP * nx, hipMemcpyDeviceToHost, st));
+  const bool pinned = o->pin && o->max_batch <= cmpc::OCP_GRID_MAX_B;
+  unsigned char* b = (unsigned char*)o->pin;
+  const PinMap m = pinned ? pin_map(o, o->max_batch) : PinMap{};
+  auto out = [&](void* dst, size_t off, const void* src, size_t n) {
+    if (n) ck(hipMemcpyAsync(pinned ? (void*)(b + off) : dst, src, n, hipMemcpyDeviceToHost, st));
+  };
+  out(P, m.P, o->P.p, bP);
+  out(p, m.p, o->p.p, bp);
   if (o->nU > 0) {
-    ck(hipMemcpyAsync(K, o->d_K, sizeof(double) * B * o->L.nK, hipMemcpyDeviceToHost, st));
-    ck(hipMemcpyAsync(k, o->d_k, sizeof(double) * B * o->nU, hipMemcpyDeviceToHost, st));
+    out(K, m.K, o->K.p, bK);
+    out(k, m.k, o->k.p, bk);
   }
-  if (Lr && o->L.nM > 0) ck(hipMemcpyAsync(Lr, o->d_Lr, sizeof(double) * B * o->L.nM, hipMemcpyDeviceToHost, st));
-  ck(hipMemcpyAsync(status, o->d_rst, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+  if (Lr && o->L.nM > 0) out(Lr, m.Lr, o->Lr.p, bL);
+  out(status, m.rst, o->rst.p, sizeof(int) * B);
   ck(hipStreamSynchronize(st));
+  if (r == CMPC_OK && pinned) {
+    std::memcpy(P, b + m.P, bP);
+    std::memcpy(p, b + m.p, bp);
+    if (o->nU > 0) {
+      std::memcpy(K, b + m.K, bK);
+      std::memcpy(k, b + m.k, bk);
+    }
+    if (Lr && o->L.nM > 0) std::memcpy(Lr, b + m.Lr, bL);
+    std::memcpy(status, b + m.rst, sizeof(int) * B);
+  }
   return r;
 }
 
 int cmpc_ocp_get_residuals(cmpc_ocp* o, int B, double* d_res, void* stream) {
   if (!o || B < 0 || B > o->max_batch || !d_res) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
-  return hipMemcpyAsync(d_res, o->d_res, sizeof(double) * B * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream) ==
+  if (hipStreamWaitEvent((hipStream_t)stream, o->ev_done, 0) != hipSuccess) return CMPC_ERR_HIP;
+  return hipMemcpyAsync(d_res, o->res.p, sizeof(double) * B * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream) ==
                  hipSuccess
              ? CMPC_OK
              : CMPC_ERR_HIP;
@@ -451,7 +719,8 @@ int cmpc_ocp_stat_rows(const cmpc_ocp* o) { return o ? o->stat_rows : CMPC_ERR_A
 int cmpc_ocp_get_stats(cmpc_ocp* o, int B, double* d_stats, void* stream) {
   if (!o || B < 0 || B > o->max_batch || !d_stats) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
-  return hipMemcpyAsync(d_stats, o->d_stats, sizeof(double) * B * o->stat_rows * CMPC_STAT_COLS,
+  if (hipStreamWaitEvent((hipStream_t)stream, o->ev_done, 0) != hipSuccess) return CMPC_ERR_HIP;
+  return hipMemcpyAsync(d_stats, o->stats.p, sizeof(double) * B * o->stat_rows * CMPC_STAT_COLS,
                         hipMemcpyDeviceToDevice, (hipStream_t)stream) == hipSuccess
              ? CMPC_OK
              : CMPC_ERR_HIP;
@@ -460,7 +729,8 @@ int cmpc_ocp_get_stats(cmpc_ocp* o, int B, double* d_stats, void* stream) {
 int cmpc_ocp_get_residuals_host(cmpc_ocp* o, int B, double* res) {
   if (!o || B < 0 || B > o->max_batch || !res) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
-  if (hipMemcpyAsync(res, o->d_res, sizeof(double) * B * 4, hipMemcpyDeviceToHost, o->stream) != hipSuccess ||
+  if (hipStreamWaitEvent(o->stream, o->ev_done, 0) != hipSuccess ||
+      hipMemcpyAsync(res, o->res.p, sizeof(double) * B * 4, hipMemcpyDeviceToHost, o->stream) != hipSuccess ||
       hipStreamSynchronize(o->stream) != hipSuccess)
     return CMPC_ERR_HIP;
   return CMPC_OK;
@@ -469,12 +739,35 @@ int cmpc_ocp_get_residuals_host(cmpc_ocp* o, int B, double* res) {
 int cmpc_ocp_get_stats_host(cmpc_ocp* o, int B, double* stats) {
   if (!o || B < 0 || B > o->max_batch || !stats) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
-  if (hipMemcpyAsync(stats, o->d_stats, sizeof(double) * B * o->stat_rows * CMPC_STAT_COLS, hipMemcpyDeviceToHost,
+  if (hipStreamWaitEvent(o->stream, o->ev_done, 0) != hipSuccess ||
+      hipMemcpyAsync(stats, o->stats.p, sizeof(double) * B * o->stat_rows * CMPC_STAT_COLS, hipMemcpyDeviceToHost,
                      o->stream) != hipSuccess ||
       hipStreamSynchronize(o->stream) != hipSuccess)
     return CMPC_ERR_HIP;
   return CMPC_OK;
 }
+
+#ifdef CMPC_OCP_CHAIN_LAB
+// Lab only: time reps launches of the latency-form factorisation on the last solve's workspace (ms per launch)
+int cmpc_ocp_debug_chain(cmpc_ocp* o, int B, int reps, float* ms) {
+  if (!o || B <= 0 || B > o->last_B || !o->hp.p || reps <= 0 || !ms) return CMPC_ERR_ARG;
+  cmpc::OcpSolveArgs a = solve_args(o, nullptr, o->last_rec, o->last_crec, nullptr, nullptr, (int*)o->rst.p, nullptr);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, o->stream);
+  for (int r = 0; r < reps; ++r)
+    if (cmpc::launch_ocp_chain_lab(a, B, o->stream) != 0) return CMPC_ERR_HIP;
+  (void)hipEventRecord(e1, o->stream);
+  (void)hipEventSynchronize(e1);
+  float t = 0.f;
+  (void)hipEventElapsedTime(&t, e0, e1);
+  *ms = t / reps;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return CMPC_OK;
+}
+#endif
 
 // ---- one-shot host entry points of the 0.3 ABI ----
 

@@ -1,7 +1,9 @@
 // HpipmInterface.cpp — ocs2::HpipmInterface mirror (reference HpipmInterface.cpp:86-554) on the MI355X engine: the
-// Impl owns a cmpc_ocp handle (device dimensions, settings and memory, created in initializeMemory / resize as the
-// reference reserves HPIPM's memory, :92-129) and solves through cmpc_ocp_solve_host (one copy in, the stage-wise
-// interior-point kernel, one copy back).
+// Impl owns a cmpc_ocp handle (device dimensions, settings and memory) created once; resize re-lays it out for the new
+// sizes with grow-only buffers (cmpc_ocp_reshape), as the reference's MemoryBlock::reserve grows HPIPM's memory only
+// (:46-67, :92-129). solve packs the problem straight into the handle's pinned staging and runs cmpc_ocp_solve_host
+// (one copy in, the stage-wise interior-point kernel, one copy back); the solve also leaves the Riccati quantities of
+// its exit point (cmpc_ocp_set_keep_riccati), so the getters copy them (HPIPM's read its workspace, :336-360).
 //
 // Written against the API the real ocs2 / Eigen types and the stand-ins of ocs2_types.h share (rows(), cols(),
 // size(), data(), resize(), operator()), so an ocs2 build compiles this file inside its hpipm_catkin target against
@@ -74,7 +76,6 @@ struct Packed {
   int N = 0, nx = 0;        // nx: the padded state dimension, max over the nodes
   std::vector<int> nxk;     // the problem's own state dimension per node (OcpSize::numStates)
   std::vector<int> nu, nc;
-  std::vector<double> rec, crec;
 };
 
 }  // namespace
@@ -84,13 +85,13 @@ class HpipmInterface::Impl {
   Impl(OcpSize s, Settings st) : settings_(st) { initializeMemory(std::move(s), true); }
   ~Impl() { release(); }
 
-  // HpipmInterface.cpp:92-129: x0 is eliminated (numStates[0] = 0); the device handle (dimensions, settings and all
-  // device memory, cmpc_ocp_create) is re-created only when the size changes (:97-100)
+  // HpipmInterface.cpp:92-129: x0 is eliminated (numStates[0] = 0); on a size change (:97-100) the device handle is
+  // re-laid out (cmpc_ocp_reshape: one small upload, buffers reallocated only beyond their capacity) or, the first
+  // time, created
   void initializeMemory(OcpSize s, bool force = false) {
     s.numStates[0] = 0;
     if (!force && s == size_) return;
     size_ = std::move(s);
-    release();
     const int N = size_.numStages;
     if (N <= 0) return;
     int nx = 0;
@@ -98,7 +99,7 @@ class HpipmInterface::Impl {
     std::vector<int> nc(size_.numIneqConstraints.begin(), size_.numIneqConstraints.end());
     // without a visible device the handle is left to the first solve(), which then reports it (the host-side size
     // checks and record packing stay usable, as the reference's are without a solve)
-    create(N, nx, std::vector<int>(size_.numInputs.begin(), size_.numInputs.begin() + N), nc, /*defer_no_device=*/true);
+    shape(N, nx, std::vector<int>(size_.numInputs.begin(), size_.numInputs.begin() + N), nc, /*defer_no_device=*/true);
   }
 
   hpipm_status solve(const vector_t& x0, std::vector<VectorFunctionLinearApproximation>& dyn,
@@ -117,22 +118,39 @@ class HpipmInterface::Impl {
       throw std::runtime_error("[HpipmInterface] Inconsistent size of constraints: " +
                                std::to_string(constraints->size()) + " with " + std::to_string(N + 1) + " nodes.");
     Packed& p = last_;
-    pack(p, x0, dyn, cost, constraints);
+    sizes(p, x0, dyn, cost, constraints);
     // the handle must have the problem's dimensions: node 0's state (x0.size()) may exceed numStates[1..N], and rows
-    // passed for nodes the size has none for (or without rows where it has some) re-create it, as a resize would
-    std::vector<int> nc = p.nc;
-    if (!ocp_ || ocpN_ != N || ocpNx_ != p.nx || ocpNu_ != p.nu || ocpNc_ != nc) create(N, p.nx, p.nu, nc);
+    // passed for nodes the size has none for (or without rows where it has some) re-shape it, as a resize would
+    const std::vector<int>& nc = p.nc;
+    if (!ocp_ || ocpN_ != N || ocpNx_ != p.nx || ocpNu_ != p.nu || ocpNc_ != nc) shape(N, p.nx, p.nu, nc);
     const int nx = p.nx;
-    int nU = 0;
+    int nU = 0, m = 0;
     for (int v : p.nu) nU += v;
+    for (int v : nc) m += v;
+    // the records go straight into the handle's pinned staging (host buffers when it has none)
+    const size_t rs = cmpc_ocp_record_size(N, nx, p.nu.data());
+    double* rec = cmpc_ocp_staging(ocp_, CMPC_OCP_STAGE_REC);
+    double* crec = m > 0 ? cmpc_ocp_staging(ocp_, CMPC_OCP_STAGE_CREC) : nullptr;
+    double* x0p = cmpc_ocp_staging(ocp_, CMPC_OCP_STAGE_X0);
+    if (!rec) {
+      recbuf_.assign(rs, 0.0);
+      rec = recbuf_.data();
+    }
+    if (m > 0 && !crec) {
+      crecbuf_.assign(cmpc_ocp_constraint_record_size(N, nx, p.nu.data(), nc.data()), 0.0);
+      crec = crecbuf_.data();
+    }
+    if (!x0p) {
+      x0buf_.assign((size_t)nx, 0.0);
+      x0p = x0buf_.data();
+    }
+    fill(p, dyn, cost, constraints, rec, crec);
+    for (int i = 0; i < nx; ++i) x0p[i] = i < p.nxk[0] ? x0(i) : 0.0;
     // with Settings::warm_start the last solution of the same size is the initial guess (HPIPM keeps it in qp_sol)
     if (!settings_.warm_start || xbuf_.size() != (size_t)(N + 1) * nx) xbuf_.assign((size_t)(N + 1) * nx, 0.0);
     if (!settings_.warm_start || ubuf_.size() != (size_t)(nU > 0 ? nU : 1)) ubuf_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
-    std::vector<double> x0p((size_t)nx, 0.0);
-    for (int i = 0; i < p.nxk[0]; ++i) x0p[(size_t)i] = x0(i);
     int status = -1, iters = 0;
-    const int r = cmpc_ocp_solve_host(ocp_, 1, x0p.data(), p.rec.data(), p.crec.empty() ? nullptr : p.crec.data(),
-                                      xbuf_.data(), ubuf_.data(), &status, &iters);
+    const int r = cmpc_ocp_solve_host(ocp_, 1, x0p, rec, crec, xbuf_.data(), ubuf_.data(), &status, &iters);
     if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device solve failed: ") + cmpc_error_string(r));
     // getStateSolution / getInputSolution (:303-328): x[0] = x0, each node in its own dimension; non-finite -> NAN_SOL
     bool finite = true;
@@ -188,9 +206,18 @@ class HpipmInterface::Impl {
       if (r != CMPC_OK)
         throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
       if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati factorisation: NaN pivot");
+      if (minEig_ > 0.0) clampFactors(nx);
       riccatiValid_ = true;
     }
     stage0(dyn0, cost0);
+  }
+
+  int allocations() const { return ocp_ ? cmpc_ocp_alloc_count(ocp_) : -1; }
+
+  void setMinimumEigenvalue(double v) {
+    if (!(v >= 0.0)) throw std::invalid_argument("[HpipmInterface] minimum eigenvalue must be >= 0");
+    minEig_ = v;
+    riccatiValid_ = false;
   }
 
   std::vector<ScalarFunctionQuadraticApproximation> costToGo(const VectorFunctionLinearApproximation& d0,
@@ -244,6 +271,23 @@ class HpipmInterface::Impl {
     if (ocp_) cmpc_ocp_destroy(ocp_);
     ocp_ = nullptr;
   }
+  // the handle in the given dimensions: re-laid out (grow-only) when it exists, created otherwise
+  void shape(int N, int nx, const std::vector<int>& nu, const std::vector<int>& nc, bool defer_no_device = false) {
+    bool rows = false;
+    for (int v : nc) rows = rows || v > 0;
+    if (ocp_) {
+      const int r = cmpc_ocp_reshape(ocp_, N, nx, nu.data(), rows ? nc.data() : nullptr);
+      if (r != CMPC_OK)
+        throw std::runtime_error(std::string("[HpipmInterface] cannot resize the device solver: ") + cmpc_error_string(r));
+      ocpN_ = N;
+      ocpNx_ = nx;
+      ocpNu_ = nu;
+      ocpNc_ = nc;
+      riccatiValid_ = false;
+      return;
+    }
+    create(N, nx, nu, nc, defer_no_device);
+  }
   void create(int N, int nx, const std::vector<int>& nu, const std::vector<int>& nc, bool defer_no_device = false) {
     release();
     cmpc_settings s;
@@ -268,17 +312,21 @@ class HpipmInterface::Impl {
       if (defer_no_device && r == CMPC_ERR_NO_DEVICE) return;
       throw std::runtime_error(std::string("[HpipmInterface] cannot create the device solver: ") + cmpc_error_string(r));
     }
+    // the MPC reads the feedback policy of every solve (MultipleShootingSolver.cpp:337-341, useFeedbackPolicy): the
+    // solve leaves its exit Riccati quantities, the getters copy them
+    (void)cmpc_ocp_set_keep_riccati(ocp_, 1);
     ocpN_ = N;
     ocpNx_ = nx;
     ocpNu_ = nu;
     ocpNc_ = nc;
   }
 
-  // The problem in the engine's packed forms, nodes embedded in the padded state dimension (per-node nx, HPIPM's
-  // nx[k]: the padding rows and columns of A, B, b, Q, S, q and C are 0, so padding states stay 0 and never couple)
-  static void pack(Packed& p, const vector_t& x0, const std::vector<VectorFunctionLinearApproximation>& dyn,
-                   const std::vector<ScalarFunctionQuadraticApproximation>& cost,
-                   const std::vector<VectorFunctionLinearApproximation>* constraints) {
+  // The problem's dimensions (the reference's verifySizes, HpipmInterface.cpp:146-164, per node), nodes embedded in the
+  // padded state dimension (per-node nx, HPIPM's nx[k]: the padding rows and columns of A, B, b, Q, S, q and C are 0,
+  // so padding states stay 0 and never couple)
+  static void sizes(Packed& p, const vector_t& x0, const std::vector<VectorFunctionLinearApproximation>& dyn,
+                    const std::vector<ScalarFunctionQuadraticApproximation>& cost,
+                    const std::vector<VectorFunctionLinearApproximation>* constraints) {
     const int N = (int)dyn.size();
     p.N = N;
     p.nxk.assign((size_t)N + 1, 0);
@@ -301,12 +349,32 @@ class HpipmInterface::Impl {
         throw std::runtime_error("[HpipmInterface] cost " + std::to_string(k) + " has inconsistent sizes");
     }
     p.nx = *std::max_element(p.nxk.begin(), p.nxk.end());
-    const int nx = p.nx;
-    p.rec.assign(cmpc_ocp_record_size(N, nx, p.nu.data()), 0.0);
+    p.nc.assign((size_t)N + 1, 0);
+    if (constraints != nullptr) {
+      for (int k = 0; k <= N; ++k) {
+        const auto& c = (*constraints)[(size_t)k];
+        const int rows = (int)c.f.size();
+        const int m = k < N ? p.nu[(size_t)k] : 0;
+        if (rows == 0) continue;
+        const int xk = p.nxk[(size_t)k];
+        if ((int)c.dfdx.rows() != rows || (int)c.dfdx.cols() != xk ||
+            (m > 0 && ((int)c.dfdu.rows() != rows || (int)c.dfdu.cols() != m)))
+          throw std::runtime_error("[HpipmInterface] constraint " + std::to_string(k) + " has inconsistent sizes");
+        p.nc[(size_t)k] = rows;
+      }
+    }
+  }
+
+  // The problem in the engine's packed forms (cmpc.h: OCP record [A,B,b] per stage then [Q,S,R,q,r] per node;
+  // constraint record [C,D,e] per node with rows), column-major blocks as Eigen stores them, into rec / crec
+  static void fill(const Packed& p, const std::vector<VectorFunctionLinearApproximation>& dyn,
+                   const std::vector<ScalarFunctionQuadraticApproximation>& cost,
+                   const std::vector<VectorFunctionLinearApproximation>* constraints, double* rec, double* crec) {
+    const int N = p.N, nx = p.nx;
     size_t o = 0;
     auto put = [&](const double* src, int r, int c, int R, int Cc) {  // column-major r x c block into an R x C slot
       for (int j = 0; j < Cc; ++j)
-        for (int i = 0; i < R; ++i) p.rec[o + (size_t)j * R + i] = (src && i < r && j < c) ? src[(size_t)j * r + i] : 0.0;
+        for (int i = 0; i < R; ++i) rec[o + (size_t)j * R + i] = (src && i < r && j < c) ? src[(size_t)j * r + i] : 0.0;
       o += (size_t)R * Cc;
     };
     for (int k = 0; k < N; ++k) {
@@ -327,24 +395,47 @@ class HpipmInterface::Impl {
     }
     // === Constraints === C dx + D du + e = 0 per node, the reference's lg = ug = -e rows (HpipmInterface.cpp:223-264,
     // stage 0 bounded through x0 on the device); an empty node (f.size() == 0) has none
-    p.nc.assign((size_t)N + 1, 0);
-    p.crec.clear();
-    if (constraints != nullptr) {
-      for (int k = 0; k <= N; ++k) {
-        const auto& c = (*constraints)[(size_t)k];
-        const int rows = (int)c.f.size();
-        const int m = k < N ? p.nu[(size_t)k] : 0;
-        if (rows == 0) continue;
-        const int xk = p.nxk[(size_t)k];
-        if ((int)c.dfdx.rows() != rows || (int)c.dfdx.cols() != xk ||
-            (m > 0 && ((int)c.dfdu.rows() != rows || (int)c.dfdu.cols() != m)))
-          throw std::runtime_error("[HpipmInterface] constraint " + std::to_string(k) + " has inconsistent sizes");
-        p.nc[(size_t)k] = rows;
-        p.crec.insert(p.crec.end(), c.dfdx.data(), c.dfdx.data() + (size_t)rows * xk);
-        p.crec.insert(p.crec.end(), (size_t)rows * (nx - xk), 0.0);  // padding state columns
-        if (m > 0) p.crec.insert(p.crec.end(), c.dfdu.data(), c.dfdu.data() + (size_t)rows * m);
-        p.crec.insert(p.crec.end(), c.f.data(), c.f.data() + rows);
+    if (constraints == nullptr || !crec) return;
+    size_t oc = 0;
+    for (int k = 0; k <= N; ++k) {
+      const auto& c = (*constraints)[(size_t)k];
+      const int rows = p.nc[(size_t)k];
+      const int m = k < N ? p.nu[(size_t)k] : 0;
+      if (rows == 0) continue;
+      const int xk = p.nxk[(size_t)k];
+      std::copy(c.dfdx.data(), c.dfdx.data() + (size_t)rows * xk, crec + oc);
+      oc += (size_t)rows * xk;
+      std::fill(crec + oc, crec + oc + (size_t)rows * (nx - xk), 0.0);  // padding state columns
+      oc += (size_t)rows * (nx - xk);
+      if (m > 0) {
+        std::copy(c.dfdu.data(), c.dfdu.data() + (size_t)rows * m, crec + oc);
+        oc += (size_t)rows * m;
       }
+      std::copy(c.f.data(), c.f.data() + rows, crec + oc);
+      oc += (size_t)rows;
+    }
+  }
+
+  // LinearAlgebra::setTriangularMinimumEigenvalues(Lr) of every getter (HpipmInterface.cpp:340, :357, :379, :419), when
+  // a minimum is set (setRiccatiMinimumEigenvalue): the diagonal of each Lr_k is moved away from 0 to at least the
+  // minimum in magnitude (hpipm_interface::setTriangularMinimumEigenvalues); K_k (k >= 1) is re-derived from the
+  // clamped factor as the reference's getRiccatiFeedback does, K_k = -Lr_c^-T Ls', with Ls' = -Lr' K_k of the
+  // device's factor; stage 0 uses the clamped Lr_0. The feedforward of k >= 1 is read as the reference reads ric_k.
+  void clampFactors(int nx) {
+    const Packed& p = last_;
+    size_t oK = 0, oM = 0;
+    std::vector<double> Lc, Ls;
+    for (int k = 0; k < p.N; ++k) {
+      const int m = p.nu[(size_t)k];
+      double* Lr = Lr_.data() + oM;
+      Lc.assign(Lr, Lr + (size_t)m * m);
+      if (hpipm_interface::setTriangularMinimumEigenvalues(Lc.data(), m, minEig_) && k >= 1) {
+        Ls.resize((size_t)m);
+        hpipm_interface::rederiveFeedback(Lr, Lc.data(), K_.data() + oK, m, nx, Ls.data());
+      }
+      std::copy(Lc.begin(), Lc.end(), Lr);
+      oK += (size_t)m * nx;
+      oM += (size_t)m * m;
     }
   }
 
@@ -352,8 +443,9 @@ class HpipmInterface::Impl {
   // variable), by triangular solves with Lr_0 of the device factorisation (HPIPM's ric_Lr(0)) and P_1, p_1 of node 1:
   //   T1 = Lr_0^-1 (S_0 + B_0'P_1 A_0), t2 = Lr_0^-1 (r_0 + B_0'(p_1 + P_1 b_0)), K_0 = -Lr_0^-T T1, k_0 = -Lr_0^-T t2,
   //   S_0 = Q_0 + A_0'P_1 A_0 - T1'T1, s_0 = q_0 + A_0'(p_1 + P_1 b_0) - T1't2.
-  // LinearAlgebra::setTriangularMinimumEigenvalues (ocs2_core, not in the reference tree) is not applied: the device
-  // factorisation already guards its pivots (a pivot <= 1e-200 gives a zero column, whose solves contribute 0).
+  // Lr_0 is the clamped factor when setRiccatiMinimumEigenvalue set a minimum (clampFactors, the reference's
+  // LinearAlgebra::setTriangularMinimumEigenvalues(Lr0), :340, :379, :419); without one, the device factorisation's
+  // pivot guard stands (a pivot <= 1e-200 gives a zero column, whose solves contribute 0).
   void stage0(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
     const Packed& p = last_;
     const int nx = p.nx, x0n = p.nxk[0], x1n = p.nxk[1], m = p.nu[0];
@@ -462,7 +554,8 @@ class HpipmInterface::Impl {
   std::vector<int> ocpNu_, ocpNc_;
   Packed last_;
   bool riccatiValid_ = false;
-  std::vector<double> xbuf_, ubuf_, Pm_, pv_, K_, k_, Lr_, K0_, k0_, S0_, s0_;
+  double minEig_ = 0.0;  // setRiccatiMinimumEigenvalue (0: no clamp)
+  std::vector<double> xbuf_, ubuf_, recbuf_, crecbuf_, x0buf_, Pm_, pv_, K_, k_, Lr_, K0_, k0_, S0_, s0_;
 };
 
 HpipmInterface::HpipmInterface(OcpSize s, const Settings& st) : pImpl_(new Impl(std::move(s), st)) {}
@@ -486,5 +579,7 @@ vector_array_t HpipmInterface::getRiccatiFeedforward(const VectorFunctionLinearA
                                                      const ScalarFunctionQuadraticApproximation& cost0) {
   return pImpl_->feedforward(dynamics0, cost0);
 }
+void HpipmInterface::setRiccatiMinimumEigenvalue(double minEigenValue) { pImpl_->setMinimumEigenvalue(minEigenValue); }
+int HpipmInterface::deviceAllocations() const { return pImpl_->allocations(); }
 
 }  // namespace ocs2

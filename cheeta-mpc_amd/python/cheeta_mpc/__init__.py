@@ -118,6 +118,17 @@ def lib():
     L.cmpc_ocp_create.argtypes = [C.c_int, C.c_int, i, i, P(Settings), C.c_int, P(vp)]
     L.cmpc_ocp_destroy.argtypes = [vp]
     L.cmpc_ocp_set_settings.argtypes = [vp, P(Settings)]
+    L.cmpc_ocp_set_path.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_path.argtypes = [vp]
+    L.cmpc_ocp_set_grid.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_grid.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_reshape.argtypes = [vp, C.c_int, C.c_int, i, i]
+    L.cmpc_ocp_alloc_count.argtypes = [vp]
+    L.cmpc_ocp_set_keep_riccati.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_enable_timing.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_last_solve_ms.argtypes = [vp, P(C.c_float)]
+    L.cmpc_ocp_staging.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_staging.restype = d
     L.cmpc_ocp_solve.argtypes = [vp, C.c_int, d, d, d, d, d, i, i, vp]
     L.cmpc_ocp_solve_host.argtypes = [vp, C.c_int, d, d, d, d, d, i, i]
     L.cmpc_ocp_riccati.argtypes = [vp, C.c_int, d, d, d, d, d, i, vp]
@@ -531,6 +542,51 @@ class OcpSolver:
         self.settings = s
         _chk(lib().cmpc_ocp_set_settings(self.h, C.byref(s)), "cmpc_ocp_set_settings")
         self.stat_rows = lib().cmpc_ocp_stat_rows(self.h)
+
+    def set_path(self, chain):
+        """cmpc_ocp_set_path: 1 = the latency form of the factorisation for batches <= 256 (default, where the
+        dimensions fit it), 0 = the batched form everywhere."""
+        _chk(lib().cmpc_ocp_set_path(self.h, int(chain)), "cmpc_ocp_set_path")
+
+    @property
+    def path(self):
+        return int(lib().cmpc_ocp_path(self.h))
+
+    def set_grid(self, G):
+        """cmpc_ocp_set_grid: workgroups per problem of the grid form (0 auto, 1 off)."""
+        _chk(lib().cmpc_ocp_set_grid(self.h, int(G)), "cmpc_ocp_set_grid")
+
+    def grid(self, B):
+        return int(lib().cmpc_ocp_grid(self.h, int(B)))
+
+    def reshape(self, N, nx, nu, nc=None):
+        """cmpc_ocp_reshape: new dimensions on the same handle (grow-only buffers, HpipmInterface::resize)."""
+        nu_a = np.ascontiguousarray(list(nu)[:N], dtype=np.int32)
+        nc_a = None if nc is None else np.ascontiguousarray(list(nc), dtype=np.int32)
+        _chk(lib().cmpc_ocp_reshape(self.h, int(N), int(nx), _dp(nu_a), _dp(nc_a)), "cmpc_ocp_reshape")
+        self.N, self.nx, self.nu, self.nc = int(N), int(nx), nu_a, nc_a
+        self.nU = int(nu_a.sum())
+        self.m = 0 if nc_a is None else int(nc_a.sum())
+        self.nK = self.nU * self.nx
+        self.nM = int((nu_a.astype(np.int64) ** 2).sum())
+        self.rec_size = int(lib().cmpc_ocp_record_size(self.N, self.nx, _dp(nu_a)))
+        self.crec_size = (int(lib().cmpc_ocp_constraint_record_size(self.N, self.nx, _dp(nu_a), _dp(nc_a)))
+                          if nc_a is not None else 0)
+
+    @property
+    def alloc_count(self):
+        return int(lib().cmpc_ocp_alloc_count(self.h))
+
+    def set_keep_riccati(self, on):
+        _chk(lib().cmpc_ocp_set_keep_riccati(self.h, int(on)), "cmpc_ocp_set_keep_riccati")
+
+    def enable_timing(self, on):
+        _chk(lib().cmpc_ocp_enable_timing(self.h, int(on)), "cmpc_ocp_enable_timing")
+
+    def last_solve_ms(self):
+        ms = C.c_float()
+        _chk(lib().cmpc_ocp_last_solve_ms(self.h, C.byref(ms)), "cmpc_ocp_last_solve_ms")
+        return float(ms.value)
 
     def solve(self, x0, rec, crec=None, guess=None):
         """Host path (cmpc_ocp_solve_host): x0 [B,nx], rec [B,rec_size], crec [B,crec_size]; guess = (x, u), the

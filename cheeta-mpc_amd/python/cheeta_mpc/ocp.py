@@ -21,14 +21,14 @@ NU_LEGGED = 24
 DT_LEGGED = 0.015
 
 
-def legged_schedule(N_int=67, period=0.6, dt=DT_LEGGED, stance_time=0.15):
+def legged_schedule(N_int=67, period=0.6, dt=DT_LEGGED, stance_time=0.15, t0=0.0):
     """Mode per interval and the event positions of a trot started from full stance: [('stance'|'trotA'|'trotB')],
     with an event node inserted at every mode switch (ocs2's PreEvent nodes). Returns a list of (kind) per node
     k = 0..N-1 where kind in {'stance', 'trotA', 'trotB', 'event'}."""
     kinds = []
     prev = None
     for i in range(N_int):
-        t = i * dt
+        t = t0 + i * dt
         if t < stance_time:
             mode = "stance"
         else:
@@ -52,14 +52,14 @@ def _rows_of(kind):
 
 
 def legged_problem(seed=0, projected=True, N_int=67, nx=NX_LEGGED, nu_full=NU_LEGGED, dt=DT_LEGGED,
-                   known_solution=False, rows_hold=False, cost="legged"):
+                   known_solution=False, rows_hold=False, cost="legged", t0=0.0):
     """One synthetic OCP of the legged-robot shape. projected: nu_k = nu_full - rows_k and no rows; else nu_k =
     nu_full (0 at events) and the rows as constraints. known_solution: q, r chosen so that a random (x*, u*)
     rollout is the unconstrained optimum (testHpipmInterface.cpp:112-152); rows_hold: e chosen so the rows hold at
     it (then it is the constrained optimum too). Returns a dict with per-stage lists and x0 (plus xs, us when
     known_solution)."""
     rng = np.random.default_rng(seed)
-    kinds = legged_schedule(N_int, dt=dt)
+    kinds = legged_schedule(N_int, dt=dt, t0=t0)
     N = len(kinds)
     nu, nc = [], []
     for kd in kinds:

@@ -304,14 +304,56 @@ size_t cmpc_ocp_constraint_record_size(int N, int nx, const int* nu, const int* 
  * |r_stat| <= tol_stat, |r_eq| <= tol_eq (dynamics), |r_ineq| <= tol_ineq (rows), max t lam <= tol_comp, iter_max /
  * alpha_min honoured (an inconsistent set of rows ends at MAX_ITER or MIN_STEP, as HPIPM's IPM does); every Newton
  * system solved stage-wise by a Riccati recursion on the barrier-weighted Hessian with reg_prim on the diagonal of
- * the stage Hessians. Without rows the first Newton step is the solution (iters = 1). warm_start is ignored (cold
- * start: the reference's default, HpipmInterfaceSettings.h:54). */
+ * the stage Hessians. Without rows the first Newton step is the solution (iters = 1). Settings.warm_start != 0 starts
+ * x, u from the caller's arrays (cmpc_ocp_solve below). The LDS bound of the batched kernels: the handle is refused
+ * (CMPC_ERR_ARG, and cmpc_ocp_memsize returns 0) when 8 ((nx + 1)^2 + 2 (nx + 1 + max nc) nzp + 4 nzp + 256) bytes,
+ * nzp = 64 or 128 by max (nu_k + nx + 1, nx + 1 + max nc), exceed 160 KB. */
 typedef struct cmpc_ocp cmpc_ocp;
 size_t cmpc_ocp_memsize(int N, int nx, const int* nu, const int* nc, int max_batch); /* device bytes */
 int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_settings* settings, int max_batch,
                     cmpc_ocp** out);
 int cmpc_ocp_destroy(cmpc_ocp* ocp);
 int cmpc_ocp_set_settings(cmpc_ocp* ocp, const cmpc_settings* settings);
+/* Form of the Riccati factorisation for batches of up to 256 problems (one problem per CU; the MPC tick's B = 1):
+ * chain = 1 (default) takes the latency form (csrc/ocp_chain.hpp: the stage's constant Hessian blocks laid out once
+ * per solve, a symmetric sweep of the input pivots on the lower triangle in 2 x 2 register blocks, two pivots per
+ * workgroup barrier) wherever the dimensions fit it (nx <= 27, nu_k + nx + 1 <= 64, nc_k <= 16, N <= 512);
+ * chain = 0 the batched form (a Gauss-Jordan sweep on the full stage matrix). Both run the same iteration; statuses and iteration counts agree, trajectories to rounding.
+ * cmpc_ocp_path returns 1 when small batches take the latency form. */
+int cmpc_ocp_set_path(cmpc_ocp* ocp, int chain);
+int cmpc_ocp_path(const cmpc_ocp* ocp);
+/* Grid form of the latency path for batches of up to 32 problems (the MPC tick's B = 1): each problem runs on G
+ * workgroups, one per CU (B G <= 256), every stage-parallel pass (residuals, right-hand sides, closed-loop matrices,
+ * step directions, the rows) split over them by stage ranges, the serial chains (factorisation, forward rollout,
+ * cost-to-go recursion) on the first, grid barriers between the phases; reductions in a fixed order, so the
+ * iteration is the single-workgroup one up to the order of the sums. G = 0 (default) picks min(32, N, 256 / B); G = 1
+ * turns the grid form off (one workgroup per problem). cmpc_ocp_grid returns the G a batch of B problems runs with
+ * (0: one workgroup per problem). */
+int cmpc_ocp_set_grid(cmpc_ocp* ocp, int G);
+int cmpc_ocp_grid(const cmpc_ocp* ocp, int B);
+/* New dimensions for an existing handle (HpipmInterface::resize, HpipmInterface.cpp:92-129): the layout arrays are
+ * re-uploaded and a device (or pinned host) buffer is reallocated only when the new size exceeds its capacity, as
+ * HPIPM's MemoryBlock::reserve grows only (:46-67); handles for up to 32 problems keep 25 % headroom from the first
+ * allocation (50 % at a growth), so the MPC's shifting event nodes and per-stage input counts reallocate nothing.
+ * Waits for the handle's last solve first. The Riccati quantities of an earlier solve are dropped.
+ * cmpc_ocp_alloc_count returns the allocations the handle has made (device and pinned host). */
+int cmpc_ocp_reshape(cmpc_ocp* ocp, int N, int nx, const int* nu, const int* nc);
+int cmpc_ocp_alloc_count(const cmpc_ocp* ocp);
+/* keep = 1: a grid-form solve (batches up to 32) also leaves the Riccati quantities of cmpc_ocp_riccati at its exit
+ * point (the factorisation the solve ends on: without rows the last Newton step's, with rows refactorised at the
+ * exit point's Sigma), so cmpc_ocp_riccati becomes a copy (HPIPM's getters read its workspace,
+ * HpipmInterface.cpp:336-360, :378-394). Default 0 (cmpc_ocp_riccati refactorises on demand). */
+int cmpc_ocp_set_keep_riccati(cmpc_ocp* ocp, int keep);
+/* on = 1: every solve records HIP events around its launch; cmpc_ocp_last_solve_ms synchronises on the last one and
+ * returns its device time. */
+int cmpc_ocp_enable_timing(cmpc_ocp* ocp, int on);
+int cmpc_ocp_last_solve_ms(cmpc_ocp* ocp, float* ms);
+/* Pinned host staging of cmpc_ocp_solve_host for handles of up to 32 problems (NULL otherwise): a caller that packs
+ * its records straight into these (sized for max_batch problems) saves the host copy into the staging. */
+#define CMPC_OCP_STAGE_X0 0
+#define CMPC_OCP_STAGE_REC 1
+#define CMPC_OCP_STAGE_CREC 2
+double* cmpc_ocp_staging(cmpc_ocp* ocp, int which);
 /* Device pointers, asynchronous on stream: d_x0 [B][nx], d_rec [B][record], d_crec [B][constraint record] (NULL when
  * the handle has no rows), d_x [B][(N+1)][nx], d_u [B][sum nu], d_status [B] (HPIPM codes 0..3), d_iters [B] (may be
  * NULL). The records must stay valid until cmpc_ocp_riccati of this solve has run, if it is called. With

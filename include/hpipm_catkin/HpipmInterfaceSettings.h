@@ -7,8 +7,9 @@
  * tolerances act as in HPIPM; reg_prim is the factorisation's primal regularisation (the returned trajectory is the
  * unregularised problem's). pred_corr must be 1 (the Mehrotra corrector HPIPM's default runs; 0 is refused), ric_alg
  * 0 or 1 (both give the same Newton steps here: one factorisation form), hpipmMode is accepted and stored (the
- * device's tolerances, not the mode's presets, decide); warm_start is accepted and the device solve cold-starts, as
- * HPIPM does at the default warm_start = 0.
+ * device's tolerances, not the mode's presets, decide); warm_start != 0 is HPIPM's primal warm start: the mirror keeps
+ * the last solution of the same size and the device solve starts x, u from it (slacks and multipliers by the
+ * cold-start rule); at the default warm_start = 0 every solve cold-starts, as HPIPM's does.
  * The centroidal engine's interior point method (cmpc_settings) honours every field.
  */
 #pragma once

@@ -678,6 +678,91 @@ static void varying_state_dims() {
   CHECK(e < 1e-9 && er < 1e-9 && ec < 1e-8, "varying state dims");
 }
 
+// setRiccatiMinimumEigenvalue on the device path: stage 2 gets R = diag(1e-14, R11) with B_2's first column 0 and a
+// small S row, so Lr_2(0,0) = sqrt(1e-14 + reg_prim) ~ 1e-6. Clamped to 1e-3, K_2's first row scales by one factor
+// Lr_2(0,0) / 1e-3 and every other row and stage is unchanged (the reference's getRiccatiFeedback on a clamped Lr).
+static void riccati_clamp_device() {
+  const int nx = 3, nu = 2, N = 5;
+  const vector_t x0 = randv(nx);
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+  }
+  cost.push_back(randomCost(nx, 0));
+  for (int i = 0; i < nx; ++i) sys[2].dfdu(i, 0) = 0.0;
+  cost[2].dfduu(0, 0) = 1e-14;
+  cost[2].dfduu(0, 1) = cost[2].dfduu(1, 0) = 0.0;
+  for (int j = 0; j < nx; ++j) cost[2].dfdux(0, j) *= 1e-6;
+  cost[2].dfdu[0] *= 1e-6;
+  HpipmInterface hpipm(HpipmInterface::OcpSize(N, nx, nu));
+  vector_array_t xs, us;
+  CHECK(hpipm.solve(x0, sys, cost, nullptr, xs, us, false) == SUCCESS, "riccati clamp status");
+  const auto Ku = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  hpipm.setRiccatiMinimumEigenvalue(1e-3);
+  const auto Kc = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  double e_same = 0.0, rmin = 1e300, rmax = -1e300;
+  for (int k = 0; k < N; ++k)
+    for (int j = 0; j < nx; ++j)
+      for (int a = 0; a < nu; ++a) {
+        if (k == 2 && a == 0) {
+          const double r = Kc[2](0, j) / Ku[2](0, j);
+          rmin = std::fmin(rmin, r);
+          rmax = std::fmax(rmax, r);
+        } else {
+          e_same = std::fmax(e_same, std::fabs(Kc[(size_t)k](a, j) - Ku[(size_t)k](a, j)) /
+                                         std::fmax(1.0, std::fabs(Ku[(size_t)k](a, j))));
+        }
+      }
+  const double want = std::sqrt(1e-14 + HpipmInterface::Settings().reg_prim) / 1e-3;
+  std::printf("riccati clamp (device): other rows %.3e, clamped row factor [%.6e, %.6e] (want %.6e)\n", e_same, rmin,
+              rmax, want);
+  CHECK(e_same < 1e-12, "riccati clamp leaves unclamped rows");
+  CHECK(std::fabs(rmin - want) < 1e-6 * want && std::fabs(rmax - want) < 1e-6 * want, "riccati clamp row factor");
+}
+
+// An MPC loop's ticks through resize (MultipleShootingSolver.cpp:275-277 resizes every iteration): the sizes shift
+// between the legged shapes (rows at some nodes, then none, nu changing), each tick's solution against a fresh
+// interface; after the first round of shapes no device buffer is allocated again (cmpc_ocp_alloc_count).
+static void resize_ticks() {
+  const int nx = 6, N = 12;
+  int allocs_after_warm = -1;
+  HpipmInterface ticker;
+  for (int tick = 0; tick < 12; ++tick) {
+    const int nu = 3 + (tick % 3);
+    const bool rows = (tick % 2) == 0;
+    std::vector<VectorFunctionLinearApproximation> sys, con;
+    std::vector<ScalarFunctionQuadraticApproximation> cost;
+    for (int k = 0; k < N; ++k) {
+      sys.push_back(randomDynamics(nx, nu));
+      cost.push_back(randomCost(nx, nu));
+      con.push_back(rows && k > 0 && (k + tick) % 3 ? randomConstraints(nx, nu, 1 + (k + tick) % 2)
+                                                    : VectorFunctionLinearApproximation());
+    }
+    cost.push_back(randomCost(nx, 0));
+    con.push_back(VectorFunctionLinearApproximation());
+    const vector_t x0 = randv(nx);
+    const auto size = hpipm_interface::extractSizesFromProblem(sys, cost, rows ? &con : nullptr);
+    ticker.resize(size);
+    vector_array_t xs, us, xf, uf;
+    const auto st = ticker.solve(x0, sys, cost, rows ? &con : nullptr, xs, us, false);
+    HpipmInterface fresh(size);
+    const auto sf = fresh.solve(x0, sys, cost, rows ? &con : nullptr, xf, uf, false);
+    const auto K = ticker.getRiccatiFeedback(sys[0], cost[0]);
+    const auto Kf = fresh.getRiccatiFeedback(sys[0], cost[0]);
+    double e = 0.0;
+    for (int k = 0; k <= N; ++k) e = std::fmax(e, maxdiff(xs[(size_t)k], xf[(size_t)k]));
+    for (int k = 0; k < N; ++k) e = std::fmax(e, std::fmax(maxdiff(us[(size_t)k], uf[(size_t)k]), maxdiffm(K[(size_t)k], Kf[(size_t)k])));
+    CHECK(st == sf && e == 0.0, "resize tick equals a fresh interface");
+    if (e != 0.0) std::printf("  tick %d: diff %.3e\n", tick, e);
+    if (tick == 5) allocs_after_warm = ticker.deviceAllocations();
+  }
+  std::printf("resize ticks: allocations after the first six %d, after twelve %d\n", allocs_after_warm,
+              ticker.deviceAllocations());
+  CHECK(ticker.deviceAllocations() == allocs_after_warm, "resize ticks allocate nothing after the first shapes");
+}
+
 int main() {
   dynamics_feasible(false);
   dynamics_feasible(true);
@@ -687,6 +772,8 @@ int main() {
   retrieve_riccati();
   constrained_riccati();
   varying_state_dims();
+  riccati_clamp_device();
+  resize_ticks();
   legged_size();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;

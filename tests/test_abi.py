@@ -127,6 +127,16 @@ def test_step_ratio_extreme_fp32_values():
     assert "step_ratio: ok" in out, out
 
 
+def test_riccati_getter_clamp_near_singular_R():
+    """The HpipmInterface mirror's optional Lr clamp (setRiccatiMinimumEigenvalue; the reference's
+    LinearAlgebra::setTriangularMinimumEigenvalues in every getter, HpipmInterface.cpp:340, :357, :379, :419) on a stage
+    with a near-singular R + B'PB (Lr(0,0) = 1e-7): the clamp rule, and K re-derived as -Lc^-T Ls' (:361) matching an
+    independent solve and the closed form of the clamped row (host build of the header, no device)."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp"), "bin/test_riccati_clamp"])
+    out = subprocess.check_output([os.path.join(ROOT, "tests", "cpp", "bin", "test_riccati_clamp")], text=True)
+    assert "riccati_clamp: ok" in out, out
+
+
 def test_path_option_constants_match_header():
     """cheeta_mpc.PATH_* mirror enum cmpc_path_option of include/cmpc/cmpc.h (cmpc_set_path / cmpc_get_path)."""
     import cheeta_mpc

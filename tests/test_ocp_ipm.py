@@ -455,7 +455,7 @@ def test_device_residuals_and_stats_match_oracle(cm, op):
         r = _oracle(op, p, stats_rows=solver.stat_rows)
         # final residuals sit at rounding level (1e-12): agreement to 1e-10 absolute, 1e-6 relative above it
         assert np.allclose(res[i], r["res"], rtol=1e-6, atol=1e-10)
-        n = r["iters"] + 1
+        n = solver.stat_rows  # every row: those after the last iteration are NaN on both sides (cmpc.h)
         a, b = stats[i][:n], r["stats"][:n]
         assert np.array_equal(np.isnan(a), np.isnan(b))
         fin = ~np.isnan(b)
@@ -481,20 +481,76 @@ def test_device_pointer_entry_equals_host_entry(cm, op):
     assert np.array_equal(dst.host(), st) and np.array_equal(dit.host(), it)
 
 
+def _device_batch_path(cm, ps, chain, grid=0):
+    p0 = ps[0]
+    recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+    solver = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=len(ps))
+    solver.set_path(chain)
+    solver.set_grid(grid)
+    x, u, st, it = solver.solve(np.array([p["x0"] for p in ps]), np.array(recs),
+                                np.array(crecs) if p0.get("nc") else None)
+    return solver, x, u, st, it
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("projected", [False, True])
 def test_device_two_per_cu_instantiation_equals_one_per_cu(cm, op, projected):
     """Batches above 256 run k_ocp_ipm<64, 2> (bounded at 256 VGPRs) with the node-by-node staged residuals, batches up
-    to 64 k_ocp_ipm<64, 1> with every node's residuals at once (OcpSolveArgs::par_res): the same fma chains, so the
-    same problems give bit-identical results either way."""
+    to 64 k_ocp_ipm<64, 1> with every node's residuals at once (OcpSolveArgs::par_res): with the batched form of the
+    factorisation in both (cmpc_ocp_set_path(0)) the same fma chains, so the same problems give bit-identical
+    results either way."""
     ps = [ocpgen.legged_problem(500 + i, projected=projected) for i in range(8)]
-    _, x1, u1, st1, it1 = _device_batch(cm, ps)
+    _, x1, u1, st1, it1 = _device_batch_path(cm, ps, 0)
     big = [ps[i % 8] for i in range(264)]
-    _, x2, u2, st2, it2 = _device_batch(cm, big)
+    _, x2, u2, st2, it2 = _device_batch_path(cm, big, 0)
     for i in range(264):
         j = i % 8
         assert st2[i] == st1[j] and it2[i] == it1[j]
         assert np.array_equal(x2[i], x1[j]) and np.array_equal(u2[i], u1[j])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_grid_form_equals_one_workgroup(cm, op, projected):
+    """Batches of up to 32 run in the grid form (G workgroups per problem, stage ranges, grid barriers, reductions in
+    a fixed order): statuses and iterations equal to the single-workgroup latency form and to the oracle, trajectories
+    to rounding (the sums of mu and of the step's complementarity are ordered differently), for the automatic width,
+    an uneven G = 7 and G = 2."""
+    ps = [ocpgen.legged_problem(540 + i, projected=projected) for i in range(3)]
+    s1, x1, u1, st1, it1 = _device_batch_path(cm, ps, 1, grid=1)
+    assert s1.grid(3) == 0
+    _check_vs_oracle(op, ps, x1, u1, st1, it1)
+    for G in (0, 7, 2):
+        sg, xg, ug, stg, itg = _device_batch_path(cm, ps, 1, grid=G)
+        assert sg.grid(3) == (min(32, ps[0]["N"], 256 // 3) if G == 0 else G)
+        assert np.array_equal(stg, st1) and np.array_equal(itg, it1), G
+        for i in range(len(ps)):
+            assert _rel(xg[i], x1[i]) < 1e-10 and _rel(ug[i], u1[i]) < 1e-10, G
+        _check_vs_oracle(op, ps, xg, ug, stg, itg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_latency_form_equals_batched_form(cm, op, projected):
+    """Small batches take the latency form of the factorisation (ocp_chain.hpp: LDL' on 2 x 2 lower blocks, gains by
+    back substitution); the batched form (Gauss-Jordan sweep) is the other factorisation of the same Newton systems:
+    statuses and iteration counts equal, trajectories to rounding, both against the oracle at 1e-9; a batch of 264
+    (above the latency form's 256) takes the batched form and equals the small batch to rounding as well."""
+    ps = [ocpgen.legged_problem(520 + i, projected=projected) for i in range(6)]
+    s1, x1, u1, st1, it1 = _device_batch_path(cm, ps, 1)
+    assert s1.path == 1
+    s0, x0, u0, st0, it0 = _device_batch_path(cm, ps, 0)
+    assert s0.path == 0
+    assert np.array_equal(st1, st0) and np.array_equal(it1, it0)
+    for i in range(len(ps)):
+        assert _rel(x1[i], x0[i]) < 1e-10 and _rel(u1[i], u0[i]) < 1e-10
+    _check_vs_oracle(op, ps, x1, u1, st1, it1)
+    big = [ps[i % 6] for i in range(264)]
+    _, x2, u2, st2, it2 = _device_batch_path(cm, big, 1)
+    for i in range(264):
+        j = i % 6
+        assert st2[i] == st1[j] and it2[i] == it1[j]
+        assert _rel(x2[i], x1[j]) < 1e-10 and _rel(u2[i], u1[j]) < 1e-10
 
 
 @pytest.mark.gpu
@@ -546,3 +602,68 @@ def test_device_warm_start_matches_oracle(cm, op):
                        guess=guesses[i])
         assert st[i] == w["status"] and it[i] == w["iters"], (i, st[i], w["status"], it[i], w["iters"])
         assert _rel(x[i], w["x"]) < 1e-9 and _rel(u[i], w["u"]) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_keep_riccati_equals_refactorisation(cm, op, projected):
+    """cmpc_ocp_set_keep_riccati: the grid-form solve leaves the exit point's Riccati quantities (HPIPM's getters read
+    its workspace, HpipmInterface.cpp:336-360), so cmpc_ocp_riccati is a copy: equal to the on-demand refactorisation
+    (k_ocp_ric) of the same solve, without rows to rounding (the factorisation is the last Newton step's), with rows to
+    the Sigma-conditioning bound of test_device_riccati_matches_oracle; and the oracle's."""
+    ps = [ocpgen.legged_problem(320 + i, projected=projected) for i in range(3)]
+    p0 = ps[0]
+    recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+    out = []
+    for keep in (1, 0):
+        solver = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=len(ps))
+        solver.set_keep_riccati(keep)
+        x, u, st, it = solver.solve(np.array([p["x0"] for p in ps]), np.array(recs),
+                                    np.array(crecs) if p0.get("nc") else None)
+        assert np.all(st == 0)
+        out.append(solver.riccati(len(ps)))
+    (P1, p1, K1, k1, L1, r1), (P0, p0_, K0, k0, L0, r0) = out
+    assert np.all(r1 == 0) and np.all(r0 == 0)
+    rows = p0.get("nc") is not None
+    tS = 1e-4 if rows else 1e-9
+    for i, p in enumerate(ps):
+        r = _oracle(op, p, ric=True)
+        for k in range(1, p["N"] + 1):
+            assert _rel(P1[i][k], P0[i][k]) < tS and _rel(P1[i][k], r["P"][k]) < tS, ("P", k)
+            assert _rel(p1[i][k], p0_[i][k]) < max(tS, 1e-8), ("p", k)
+        for k in range(p["N"]):
+            assert _rel(L1[i][k], L0[i][k]) < tS, ("Lr", k)
+            assert _rel(K1[i][k], K0[i][k]) < tS and _rel(k1[i][k], k0[i][k]) < max(tS, 1e-8), ("K, k", k)
+
+
+@pytest.mark.gpu
+def test_device_reshape_ticks_allocate_nothing(cm, op):
+    """The MPC tick on one handle (HpipmInterface::resize + solve + getRiccatiFeedback, MultipleShootingSolver.cpp:276,
+    :337-341): 50 ticks of the legged problem with the event nodes moving as the gait advances (N 70 / 71, the inputs
+    per stage 10 / 12 / 0 shifting), reshaped on one handle with the exit Riccati kept: after the handle's first
+    allocation no device or pinned allocation happens, and every tick's solution and Riccati quantities equal a fresh
+    handle's bit for bit."""
+    h = None
+    base = None
+    for t in range(50):
+        p = ocpgen.legged_problem(700 + t, projected=True, t0=0.015 * t)
+        rec, _ = ocpgen.pack(p)
+        if h is None:
+            h = cm.OcpSolver(p["N"], p["nx"], p["nu"], None, max_batch=1)
+            h.set_keep_riccati(1)
+            base = h.alloc_count
+        else:
+            h.reshape(p["N"], p["nx"], p["nu"])
+        x, u, st, it = h.solve(p["x0"][None], rec[None])
+        ric = h.riccati(1)
+        assert h.alloc_count == base, (t, h.alloc_count, base)
+        f = cm.OcpSolver(p["N"], p["nx"], p["nu"], None, max_batch=1)
+        f.set_keep_riccati(1)
+        xf, uf, stf, itf = f.solve(p["x0"][None], rec[None])
+        rf = f.riccati(1)
+        f.close()
+        assert st[0] == 0 and stf[0] == 0 and it[0] == itf[0]
+        assert np.array_equal(x, xf) and np.array_equal(u, uf), t
+        assert np.array_equal(ric[0], rf[0]) and np.array_equal(ric[1], rf[1]), t
+        for k in range(p["N"]):
+            assert np.array_equal(ric[2][0][k], rf[2][0][k]) and np.array_equal(ric[3][0][k], rf[3][0][k]), (t, k)

@@ -20,6 +20,8 @@ def run(projected, B, reps=int(os.environ.get("OCP_REPS", "5"))):
     p0 = ps[0]
     recs, crecs = zip(*[gen.pack(p) for p in ps])
     s = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=B)
+    s.set_path(int(os.environ.get("OCP_CHAIN", "1")))
+    s.set_grid(int(os.environ.get("OCP_GRID", "0")))
     dx0 = cm.DeviceArray.from_host(np.array([p["x0"] for p in ps]))
     drec = cm.DeviceArray.from_host(np.array(recs))
     dcrec = cm.DeviceArray.from_host(np.array(crecs)) if not projected else None
@@ -49,10 +51,10 @@ def run(projected, B, reps=int(os.environ.get("OCP_REPS", "5"))):
     per = ms.value / reps
     print(f"{'projected' if projected else 'rows     '} B={B:5d} N={p0['N']} nx=24 nu={sorted(set(p0['nu']))} "
           f"kernel {per:8.3f} ms/solve ({B / per * 1e3:9.0f} solves/s), iters {it.mean():.2f}, "
-          f"status ok {np.mean(st == 0):.2f}; host path {th:.2f} ms", flush=True)
+          f"status ok {np.mean(st == 0):.2f}; host path {th:.2f} ms; path {s.path} grid {s.grid(B)}", flush=True)
 
 
-if __name__ == "__main__" and "--stamps" not in sys.argv:
+if __name__ == "__main__" and "--stamps" not in sys.argv and "--chain" not in sys.argv:
     Bs = [int(a) for a in sys.argv[1:]] or [1, 64, 256, 1024]
     for proj in (True, False):
         for B in Bs:
@@ -68,13 +70,16 @@ def stamps(projected, B=1):
     p0 = ps[0]
     recs, crecs = zip(*[gen.pack(p) for p in ps])
     s = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=B)
+    s.set_path(int(os.environ.get("OCP_CHAIN", "1")))
+    s.set_grid(int(os.environ.get("OCP_GRID", "0")))
     x0 = np.array([p["x0"] for p in ps])
     s.solve(x0, np.array(recs), np.array(crecs) if not projected else None)
     L.cmpc_ocp_debug_stamps(buf, 1)
     x, u, st, it = s.solve(x0, np.array(recs), np.array(crecs) if not projected else None)
     L.cmpc_ocp_debug_stamps(buf, 1)
     names = {1: "residuals", 2: "rhs", 10: "fact:init", 11: "fact:T", 12: "fact:M", 13: "fact:prefetch",
-             14: "fact:sweep", 15: "fact:store", 16: "fact:out", 17: "fact:exit", 3: "acl", 4: "forward",
+             14: "fact:sweep", 15: "fact:store", 16: "fact:out", 20: "chain:init", 21: "chain:T", 22: "chain:M",
+             23: "chain:elim", 24: "chain:out", 25: "gains", 17: "fact:exit", 3: "acl", 4: "forward",
              5: "post", 6: "corr rhs", 7: "backward", 8: "acl+forward (corr)", 9: "update"}
     tot = sum(buf[i] for i in names)
     print(f"stamps {'projected' if projected else 'rows'} B={B} iters {it[0]} total {tot} cycles")
@@ -82,6 +87,32 @@ def stamps(projected, B=1):
         print(f"  {n:22s} {buf[i]:12d}  {100.0 * buf[i] / max(tot, 1):5.1f} %")
 
 
+def chain_only(projected, B=1, reps=50):
+    """The latency-form factorisation alone (lab build: CMPC_LIB=lab/_stamps/libcmpc_ocpchain.so), ms per launch."""
+    L = cm.lib()
+    L.cmpc_ocp_debug_chain.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]
+    ps = [gen.legged_problem(1000 + i, projected=projected) for i in range(B)]
+    p0 = ps[0]
+    recs, crecs = zip(*[gen.pack(p) for p in ps])
+    s = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=B)
+    dx0 = cm.DeviceArray.from_host(np.array([p["x0"] for p in ps]))
+    drec = cm.DeviceArray.from_host(np.array(recs))
+    dcrec = cm.DeviceArray.from_host(np.array(crecs)) if not projected else None
+    dx = cm.DeviceArray((B, p0["N"] + 1, p0["nx"]), np.float64)
+    du = cm.DeviceArray((B, max(s.nU, 1)), np.float64)
+    dst = cm.DeviceArray((B,), np.int32)
+    s.solve_device(B, dx0, drec, dcrec, dx, du, dst, None)
+    cm.hip().hipDeviceSynchronize()
+    ms = C.c_float()
+    L.cmpc_ocp_debug_chain(s.h, B, 3, C.byref(ms))
+    r = L.cmpc_ocp_debug_chain(s.h, B, reps, C.byref(ms))
+    print(f"chain-only {'projected' if projected else 'rows'} B={B}: rc {r} {ms.value * 1e3:.1f} us per factorisation "
+          f"({ms.value * 1e3 / p0['N']:.2f} us per stage)", flush=True)
+
+
 if __name__ == "__main__" and "--stamps" in sys.argv:
     stamps(True)
     stamps(False)
+if __name__ == "__main__" and "--chain" in sys.argv:
+    chain_only(True)
+    chain_only(False)
