@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "k_ocp.hpp"
 
 namespace cmpc {
@@ -44,6 +46,12 @@ __shared__ unsigned long long ocp_stamp_lds[33];
       ocp_stamp_lds[32] = now_;                                               \
     }                                                                         \
   } while (0)
+// a span of one thread other than 0 (t, e.g. a helper wave's work): cycles between OCP_SPAN_BEGIN and OCP_SPAN_END
+#define OCP_SPAN_BEGIN(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define OCP_SPAN_END(id, var, t)                                                          \
+  do {                                                                                    \
+    if (blockIdx.x == 0 && threadIdx.x == (t)) ocp_stamp_lds[id] += __builtin_amdgcn_s_memtime() - (var); \
+  } while (0)
 #define OCP_STAMP_BEGIN()                                                     \
   do {                                                                        \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
@@ -62,6 +70,12 @@ __shared__ unsigned long long ocp_stamp_lds[33];
   } while (0)
 #define OCP_STAMP_BEGIN() \
   do {                    \
+  } while (0)
+#define OCP_SPAN_BEGIN(var) \
+  do {                      \
+  } while (0)
+#define OCP_SPAN_END(id, var, t) \
+  do {                           \
   } while (0)
 #define OCP_STAMP_END() \
   do {                  \
@@ -1152,14 +1166,21 @@ __device__ __forceinline__ void ldl_solve(const double* __restrict__ F, int m, c
 // vec; the other passes of the kernel see G0 / G1 as ABx / Tx (contiguous: the staged residuals' buffer)
 __device__ __forceinline__ Lds carve_fast(double* smem, const OcpLayout& L, ChainLds& C) {
   const int ngr = CH_NRP + L.ngmax, ngp = (L.ngmax + 2) & ~1;
+  const int g1 = ngr * CH_GS > CH_MAXU * CH_FS ? ngr * CH_GS : CH_MAXU * CH_FS;
   C.G0 = smem;
   C.G1 = C.G0 + ngr * CH_GS;
-  C.T = C.G1 + ngr * CH_GS;
+  C.F1 = C.G1;  // the chain's second factor image (G1 is the other passes' scratch)
+  C.T = C.G1 + g1;
   C.Pa = C.T + CH_NRP * CH_GS;
   C.C = C.Pa + CH_PS * CH_PS;
   C.sg0 = C.C + 256;
   C.sg1 = C.sg0 + ngp;
-  C.desc = (int*)(C.sg1 + ngp + 64 + 128);
+  C.Ml = C.sg1 + ngp + 64 + 128;
+  C.Hc = C.Ml + CH_MR * CH_GS;
+  C.gb = C.Hc + 4 * CH_MAXNT;
+  C.Pa2 = C.gb + 64;
+  C.F0 = C.Pa2 + CH_PS * CH_PS;
+  C.desc = (int*)(C.F0 + CH_MAXU * CH_FS);
   Lds s;
   s.np1 = L.nx + 1;
   s.nrm = L.nx + 1 + L.ngmax;
@@ -1485,6 +1506,8 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
     bool fok;
     if constexpr (FAST) {
       fok = chain_factor(V, CS, hp, a.reg);
+      chain_gains(V, 0, N);
+      __syncthreads();
     } else {
       fok = factor_pass<NZP>(V, S, a.reg);
     }
@@ -1859,6 +1882,10 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       status = 3;
       break;
     }
+    if constexpr (FAST) {  // the owned stages' gains from the chain's factor
+      chain_gains(V, R.k0, R.k1);
+      __syncthreads();
+    }
     acl_pass(V, S, true, R.k0, R.k1, true);
     if (!sync()) break;
     OCP_STAMP(3);
@@ -1991,6 +2018,10 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     sync();
     grid_collect(part + 5, G, 1, ops_max, red);
     const bool rok = alive && red[0] == 0.0;
+    if (FAST && full) {
+      chain_gains(V, R.k0, R.k1);
+      __syncthreads();
+    }
     const long long oP = (long long)q * (N + 1) * nx * nx, op = (long long)q * (N + 1) * nx;
     const long long oK = (long long)q * (L.nK > 0 ? L.nK : 1), ok2 = (long long)q * (L.nU > 0 ? L.nU : 1),
                     oM = (long long)q * (L.nM > 0 ? L.nM : 1);
@@ -2164,6 +2195,7 @@ __global__ __launch_bounds__(NT, 1) void k_ocp_chain_lab(OcpSolveArgs a) {
   hp_build(V, hp, a.reg);
   __syncthreads();
   if (!chain_factor(V, CS, hp, a.reg) && threadIdx.x == 0) a.status[blockIdx.x] = 3;
+  chain_gains(V, 0, a.L.N);
 }
 }  // namespace
 int launch_ocp_chain_lab(const OcpSolveArgs& a, int B, hipStream_t stream) {
@@ -2213,12 +2245,15 @@ int ocp_grid_width(int N, int B, int want) {
 }
 
 size_t ocp_chain_lds_bytes(const OcpLayout& L, int numax) {
-  if (L.nzp != 64 || L.nx > OCP_CHAIN_MAX_NX || numax > OCP_CHAIN_MAX_NU || L.nx + numax + 1 > 64 ||
+  if (L.nzp != 64 || L.nx > OCP_CHAIN_MAX_NX || numax > OCP_CHAIN_MAX_NU || L.nx + numax + 1 > OCP_CHAIN_MAX_N1 ||
       L.ngmax > CH_MAXG || L.N > CH_MAXN)
     return 0;
   const size_t ngr = CH_NRP + (size_t)L.ngmax, ngp = (size_t)((L.ngmax + 2) & ~1);
-  const size_t d = 2 * ngr * CH_GS + (size_t)CH_NRP * CH_GS + CH_PS * CH_PS + 256 + 2 * ngp + 64 + 128;
-  return sizeof(double) * d + sizeof(int) * CH_DESC * (size_t)L.N;
+  const size_t g1 = std::max(ngr * CH_GS, (size_t)CH_MAXU * CH_FS);
+  const size_t d = ngr * CH_GS + g1 + (size_t)CH_NRP * CH_GS + CH_PS * CH_PS + 256 + 2 * ngp + 64 + 128 +
+                   (size_t)CH_MR * CH_GS + 4 * CH_MAXNT + 64 + CH_PS * CH_PS + (size_t)CH_MAXU * CH_FS;
+  const size_t bytes = sizeof(double) * d + sizeof(int) * CH_DESC * (size_t)L.N;
+  return bytes <= 160 * 1024 ? bytes : 0;  // beyond the LDS: the batched form
 }
 
 int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {

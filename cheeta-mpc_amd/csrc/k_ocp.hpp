@@ -50,7 +50,8 @@ int ocp_grid_width(int N, int B, int want);  // G for a batch (0: not the grid f
 
 // Limits of the latency form of the factorisation (ocp_chain.hpp, small batches)
 constexpr int OCP_CHAIN_MAX_NX = 27;
-constexpr int OCP_CHAIN_MAX_NU = 36;  // nu_k + nx + 1 <= 64 bounds it as well
+constexpr int OCP_CHAIN_MAX_NU = 36;
+constexpr int OCP_CHAIN_MAX_N1 = 60;  // nu_k + nx + 1: two 4 x 4 blocks of the stage matrix per lane of wave 0
 
 struct OcpSolveArgs {
   OcpLayout L;

@@ -1,35 +1,40 @@
 // ocp_chain.hpp — latency form of the OCP Riccati factorisation (the HpipmInterface::solve path's only serial chain,
 // reference HpipmInterface.cpp:282-284 -> HPIPM's backward Riccati recursion; restated by oracle/ocp_ipm.c:ocp_factor)
-// for small batches: k_ocp_ipm<64, 1, true>. Included inside k_ocp.hip's anonymous namespace (uses NT, View,
-// lds_barrier, OCP_STAMP).
+// for small batches: k_ocp_ipm<64, 1, true> and the grid form. Included inside k_ocp.hip's anonymous namespace (uses
+// NT, View, lds_barrier, OCP_STAMP).
 //
 // Per stage k (backward), with Paug = [P p; p' 0] of node k + 1 in LDS:
-//   T = Paug [B A rb; 0 0 1]                            (nx + 1) x n1, 2 x 2 register blocks per thread
-//   M = Hc_k + [B A rb; 0 0 1]' T + Gc' Sigma Gc        lower triangle only, 2 x 2 blocks (one to three per thread)
-//   symmetric sweep (Gauss-Jordan on the lower triangle) of the nu_k input pivots, two per workgroup barrier: the
-//   pivot pair's row / column of M is published after the previous round's update, every thread forms the pair's
-//   2 x 2 pivot block and updates its blocks itself. After the sweep the lower triangle holds
-//   [. ; -K' ; -kff' | P_k ; p_k'] (the x / rhs rows of the input columns are -M_xu M_uu^-1, the trailing block the
-//   Schur complement), and the pivot columns at their pivot's round are the LDL' factor of
-//   M_uu = R~ + B'PB + D'Sigma D (kept for the corrector's feedforward and HPIPM's ric_Lr).
+//   (A) T = Paug [B A rb; 0 0 1]                        (nx + 1) x n1, 2 x 2 blocks, all four waves
+//   (B) M = Hc_k + g + [B A rb; 0 0 1]' T + Gc' Sigma Gc lower triangle, 2 x 2 blocks, all four waves, into LDS
+//   (C) wave 0 alone: the LDL' elimination of the nu_k input pivots, two per round, on 4 x 4 register blocks of M: the
+//       pivot pair's columns are published to LDS and read back by the same wave (LDS instructions of one wave run
+//       in order, so a round needs no barrier); the trailing entries take the pair's rank-2 update
+//       M -= c0 c0' / d0 + c1~ c1~' / d1 (c1~ = c1 - c0 a1 / d0), the same fma sequence as the symmetric sweep of
+//       factor_pass on the entries that stay live, so P_k = the x / rhs block of the result is that sweep's. The
+//       pivot columns are the LDL' factor F = L D of M_uu = R~ + B'PB + D'Sigma D (Lf, HPIPM's ric_Lr) and of its
+//       x / rhs rows (stored in K / kf and turned into K_k = -L_uu^-T L_xu', kff_k by chain_gains, stage-parallel,
+//       after the chain).
+//       Waves 1-3 meanwhile load stage k - 1's operands (A_k-1, B_k-1, rb, the rows C, D and Sigma, the Hc image,
+//       g) and write them into the LDS images: their load latency is off the chain, and wave 0 issues no global
+//       load, so nothing on the chain waits on the vector-memory counter.
 // Hc_k = [R + reg I, S'; S, Q + reg I] (the constant part of the stage Hessian) is laid out once per solve in the
-// chain's register-block order (hp_build), so a stage's prefetch is two 16-byte loads per block; A_k, B_k, rb_k, the
-// rows C_k, D_k and their Sigma are loaded straight from the record / workspace one stage ahead into registers and
-// written into the other half of a double-buffered LDS image at the end of the stage. The stage descriptors
-// (dimensions, offsets) sit in an LDS table. No global load and no scalar load sits on the chain: every barrier inside
-// it is an LDS-only barrier, so the prefetch stays in flight across the rounds. The number of register blocks per
-// thread is uniform per stage (1..3 by n1) and compiled per count, so no LDS load sits behind a divergent branch.
-// The other factorisation (factor_pass: a Gauss-Jordan sweep over the full 4 x 4-cyclic register tile, the stage's
-// data addressed by pointer selects on the chain) stays for the batched instantiations.
+// 2 x 2 block order of (B) (hp_build). The stage descriptors (dimensions, offsets) sit in an LDS table. Three
+// barriers per stage, all LDS-only.
+// The other factorisation (factor_pass: a Gauss-Jordan sweep over the full 4 x 4-cyclic register tile) stays for the
+// batched instantiations.
 #pragma once
 
-constexpr int CH_GS = 66;    // row stride (doubles) of the G and T images (16-byte aligned rows)
-constexpr int CH_PS = 28;    // row stride of Paug
-constexpr int CH_NRP = 28;   // G image rows of [B A rb] / [0 0 1] (np1 = nx + 1 <= 28); the rows' block follows
-constexpr int CH_MAXT = 3;   // 2 x 2 lower blocks per thread (n1 <= 64: at most 528 blocks)
-constexpr int CH_MAXG = 16;  // rows per node of the fast path
-constexpr int CH_MAXN = 512; // stages of the fast path (LDS descriptor table)
-constexpr int CH_DESC = 8;   // ints per stage descriptor
+constexpr int CH_GS = 66;     // row stride (doubles) of the G, T and M images (16-byte aligned rows)
+constexpr int CH_PS = 28;     // row stride of Paug
+constexpr int CH_NRP = 28;    // G image rows of [B A rb] / [0 0 1] (np1 = nx + 1 <= 28); the rows' block follows
+constexpr int CH_MAXT = 3;    // 2 x 2 lower blocks per thread in (B) (n1 <= 64: at most 528 blocks)
+constexpr int CH_MAXNT = 528; // 2 x 2 lower blocks of a stage (Hc image)
+constexpr int CH_MAXG = 16;   // rows per node of the fast path
+constexpr int CH_MAXN = 512;  // stages of the fast path (LDS descriptor table)
+constexpr int CH_DESC = 10;   // ints per stage descriptor
+constexpr int CH_MR = 60;     // rows of the M image (n1 <= OCP_CHAIN_MAX_N1)
+constexpr int CH_FS = 60;     // column stride of the factor image F (rows x of the pivot column j at F[j CH_FS + x])
+constexpr int CH_MAXU = 36;   // pivot columns of the factor image (nu_k <= OCP_CHAIN_MAX_NU)
 typedef double d2v __attribute__((ext_vector_type(2)));
 
 // 2 x 2 block tau of the lower triangle in row order: tau = bi (bi + 1) / 2 + bj, bj <= bi
@@ -43,7 +48,9 @@ __device__ __forceinline__ void ch_block(int tau, int& bi, int& bj) {
 
 struct ChainLds {
   double *G0, *G1, *T, *Pa, *C, *sg0, *sg1;
-  int* desc;  // [N][CH_DESC]: nu, ng, cu, cr, cHp, record offset of A, constraint-record offset of C, nt
+  double *Ml, *Hc, *gb;  // M image (CH_MR x CH_GS), the stage's Hc image (4 CH_MAXNT), g of the stage (64)
+  double *Pa2, *F0, *F1;  // the other Paug; the factor images of alternate stages (F1 aliases G1: unused by the chain)
+  int* desc;  // [N][CH_DESC]: nu, ng, cu, cr, cHp, record offset of A, constraint-record offset of C, nt, cM, cK
 };
 
 // Hc image of every stage (once per solve): block tau of stage k at hp[cHp[k] + 4 tau + 2 a + b] = M(2 bi + a,
@@ -71,112 +78,136 @@ __device__ __forceinline__ void hp_build(const View& V, double* hp, double reg) 
   }
 }
 
-// One stage's operands in registers (the prefetch of the next stage in the chain)
-struct ChainRegs {
-  double gv[8];              // [B A rb] image: row tid & 31, columns (tid >> 5) + 8 q
-  double cv[4];              // rows' [D C] image: row tid & 15, columns (tid >> 4) + 16 q
-  double sv;                 // Sigma of row tid (tid < ng)
-  double hc[CH_MAXT][2][2];  // Hc blocks
-  double gr[CH_MAXT][2];     // rhs-row entries (g_u, g_x) of a block in row nz
-};
-
-__device__ __forceinline__ void chain_fetch(const View& V, const int* d, int k, const int (&bi)[CH_MAXT],
-                                            const int (&bj)[CH_MAXT], const double* hp, ChainRegs& R) {
+// Waves 1-3 (t = threadIdx.x - 64 in [0, 192)): stage k's operands into the LDS images — G (rows 0..nx-1 = [B A rb],
+// row nx = e_nz, rows CH_NRP.. = the rows' [D C 0]; columns up to the even width w >= n1, the pad column zero), sg
+// (Sigma of the rows), Hc (the stage's Hc image, 4 nt doubles) and gb (g_u, g_x, then zeros up to w). Every load is
+// issued before the first store, so one wait covers them.
+__device__ __forceinline__ void chain_out(const View& V, const int* d, int k, const double* Pb, const double* Fb, int t,
+                                          int nthr);
+__device__ __forceinline__ void chain_load(const View& V, const int* d, int k, const double* hp, const ChainLds& S,
+                                           const int* dout, const double* Pout, const double* Fout) {
   const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx;
+  const int t = threadIdx.x - 64, nx = L.nx;
   const int mk = d[0], g = d[1], cu = d[2], cr = d[3], chp = d[4], nt = d[7];
-  const int nz = mk + nx, n1 = nz + 1;
+  const int nz = mk + nx, n1 = nz + 1, w = (n1 + 1) & ~1;
   const double* A = V.rec + d[5];
   const double* B = A + nx * nx;
   const double* rb = V.rb() + (long long)k * nx;
+  // unconditional loads (an out-of-range entry reads A_k[0]; zeroed at the store): a load whose value is selected
+  // against 0 at the fetch would make the compiler wait for it there, one load at a time
+  double gv[11], cv[6], hv[12], sv, gg;
   {
-    const int r = tid & 31, c0 = tid >> 5;
+    const int r = t & 31, c0 = t >> 5;  // [B A rb]: row r, columns c0 + 6 q
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = c0 + 8 * q;
+    for (int q = 0; q < 11; ++q) {
+      const int c = c0 + 6 * q;
+      const bool on = r < nx && c < n1;
       const double* p = c < mk ? B + c * nx + r : (c < nz ? A + (c - mk) * nx + r : rb + r);
-      R.gv[q] = (r < nx && c < n1) ? *p : 0.0;
+      gv[q] = *(on ? p : A);
     }
   }
+  const double* C = V.crec ? V.crec + d[6] : rb;
   {
-    const int r = tid & 15, c0 = tid >> 4;
-    const double* C = V.crec ? V.crec + d[6] : rb;
+    const int r = t & 15, c0 = t >> 4;  // rows' [D C]: row r, columns c0 + 12 q
     const double* D = C + g * nx;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = c0 + 16 * q;
+    for (int q = 0; q < 6; ++q) {
+      const int c = c0 + 12 * q;
+      const bool on = r < g && c < nz;
       const double* p = c < mk ? D + c * g + r : C + (c - mk) * g + r;
-      R.cv[q] = (r < g && c < nz) ? *p : 0.0;
+      cv[q] = *(on ? p : A);
     }
   }
-  R.sv = tid < g ? V.row(R_SIG)[cr + tid] : 0.0;
-  const double* hk = hp + chp;
-  const double* gu = V.gu() + cu;
-  const double* gx = V.gx() + (long long)k * nx;
+  sv = *(t < g ? V.row(R_SIG) + cr + t : A);
+  gg = *(t < mk ? V.gu() + cu + t : (t < nz ? V.gx() + (long long)k * nx + t - mk : A));
+  {
+    const d2v* h = (const d2v*)(hp + chp);
 #pragma unroll
-  for (int r = 0; r < CH_MAXT; ++r) {
-    const int tau = tid + NT * r;
-    const bool act = tau < nt;
-    const d2v* h = (const d2v*)(hk + 4 * (act ? tau : 0));
-    const d2v h0 = h[0], h1 = h[1];
-    R.hc[r][0][0] = act ? h0.x : 0.0;
-    R.hc[r][0][1] = act ? h0.y : 0.0;
-    R.hc[r][1][0] = act ? h1.x : 0.0;
-    R.hc[r][1][1] = act ? h1.y : 0.0;
-    // the block holding row nz carries g there (the rhs column of the stage Hessian)
-    const int arow = nz - 2 * bi[r];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int l = 2 * bj[r] + b;
-      const bool on = act && (arow == 0 || arow == 1) && l < nz;
-      const double* p = l < mk ? gu + l : gx + (l - mk);
-      R.gr[r][b] = on ? *p : 0.0;
+    for (int q = 0; q < 6; ++q) {
+      const int e = t + 192 * q;
+      const d2v v = h[e < 2 * nt ? e : 0];
+      hv[2 * q] = v.x;
+      hv[2 * q + 1] = v.y;
     }
+  }
+  // stage k + 2's outputs (the chain's stage before the current one) to global memory while the loads are in flight
+  if (dout) chain_out(V, dout, k + 2, Pout, Fout, t, 192);
+  double* G = S.G0;
+  {
+    const int r = t & 31, c0 = t >> 5;
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      const int c = c0 + 6 * q;
+      if (r < nx && c < w) G[r * CH_GS + c] = c < n1 ? gv[q] : 0.0;
+    }
+  }
+  if (t < w) G[nx * CH_GS + t] = t == nz ? 1.0 : 0.0;
+  {
+    const int r = t & 15, c0 = t >> 4;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int c = c0 + 12 * q;
+      if (r < g && c < w) G[(CH_NRP + r) * CH_GS + c] = c < nz ? cv[q] : 0.0;
+    }
+  }
+  if (t < g) S.sg0[t] = sv;
+  if (t < w) S.gb[t] = t < nz ? gg : 0.0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int e = t + 192 * q;
+    if (e < 2 * nt) *(d2v*)(S.Hc + 2 * e) = d2v{hv[2 * q], hv[2 * q + 1]};
   }
 }
 
-// Registers of a stage into the LDS image G (rows 0..nx-1 = [B A rb], row nx = e_nz, rows CH_NRP.. = [D C 0]) and sg;
-// columns up to the even width w >= n1 (the odd pad column is zero)
-__device__ __forceinline__ void chain_commit(const View& V, const int* d, const ChainRegs& R, double* G, double* sg) {
-  const int tid = threadIdx.x, nx = V.L.nx;
-  const int mk = d[0], g = d[1], nz = mk + nx, n1 = nz + 1, w = (n1 + 1) & ~1;
-  {
-    const int r = tid & 31, c0 = tid >> 5;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = c0 + 8 * q;
-      if (r < nx && c < w) G[r * CH_GS + c] = R.gv[q];
-    }
-  }
-  if (tid < w) G[nx * CH_GS + tid] = tid == nz ? 1.0 : 0.0;
-  {
-    const int r = tid & 15, c0 = tid >> 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = c0 + 16 * q;
-      if (r < g && c < w) G[(CH_NRP + r) * CH_GS + c] = R.cv[q];
-    }
-  }
-  if (tid < g) sg[tid] = R.sv;
-}
-
-// Per-stage part after T for NS register blocks per thread: M, the symmetric sweep, the outputs. Returns the NaN flag.
-template <int NS>
-__device__ __forceinline__ bool chain_stage(const View& V, const ChainLds& S, int k, const int* d, const double* G,
-                                            const double* sg, const int (&bi)[CH_MAXT], const int (&bj)[CH_MAXT],
-                                            const ChainRegs& cur) {
+// Stage k's outputs from the LDS images to global memory (threads t of nthr): P_k, p_k from its Paug image Pb, the
+// factor columns from Fb — u rows into Lf_k, x rows into K_k (row x of the column-major nu_k x nx block), the rhs row
+// into kf_k (chain_gains turns the last two into the gains)
+__device__ __forceinline__ void chain_out(const View& V, const int* d, int k, const double* Pb, const double* Fb, int t,
+                                          int nthr) {
   const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx, np1 = nx + 1;
-  const int mk = d[0], g = d[1], nt = d[7], nz = mk + nx, n1 = nz + 1;
-  bool bad = false;
+  const int nx = L.nx, np1 = nx + 1;
+  const int mk = d[0], nz = mk + nx, n1 = nz + 1;
+  double* Pk = V.P(k);
+  double* pk = V.pv() + (long long)k * nx;
+  for (int e = t; e < nx * np1; e += nthr) {
+    const int I = e / np1, J = e - I * np1;
+    const double v = Pb[J * CH_PS + I];
+    if (J < nx) Pk[I * nx + J] = v;
+    else pk[I] = v;
+  }
+  double* Lf = V.ws + L.o_Lf + d[8];
+  double* Kx = V.ws + L.o_K + d[9];
+  double* kx = V.kf() + d[2];
+  for (int e = t; e < mk * n1; e += nthr) {
+    const int j = e / n1, x = e - j * n1;
+    if (x < j) continue;
+    const double v = Fb[j * CH_FS + x];
+    if (x < mk) Lf[j * mk + x] = v;
+    else if (x < nz) Kx[(x - mk) * mk + j] = v;
+    else kx[j] = v;
+  }
+}
+
+// (B): M = Hc + g + G' T + Gc' Sigma Gc on NS 2 x 2 lower blocks per thread, into the M image
+template <int NS>
+__device__ __forceinline__ void chain_m(const ChainLds& S, int nx, const int* d, const int (&bi)[CH_MAXT],
+                                        const int (&bj)[CH_MAXT]) {
+  const int tid = threadIdx.x, np1 = nx + 1;
+  const int mk = d[0], g = d[1], nt = d[7], nz = mk + nx;
+  const double* G = S.G0;
   double m[NS][2][2];
 #pragma unroll
-  for (int r = 0; r < NS; ++r)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) m[r][a][b] = cur.hc[r][a][b] + ((2 * bi[r] + a == nz) ? cur.gr[r][b] : 0.0);
-  // --- M = Hc + G' T + Gc' Sigma Gc ---
+  for (int r = 0; r < NS; ++r) {
+    const int tau = tid + NT * r;
+    const bool act = tau < nt;
+    const d2v* h = (const d2v*)(S.Hc + 4 * (act ? tau : 0));
+    const d2v h0 = h[0], h1 = h[1];
+    const d2v gr = *(const d2v*)(S.gb + (act ? 2 * bj[r] : 0));
+    m[r][0][0] = h0.x + (2 * bi[r] == nz ? gr.x : 0.0);
+    m[r][0][1] = h0.y + (2 * bi[r] == nz ? gr.y : 0.0);
+    m[r][1][0] = h1.x + (2 * bi[r] + 1 == nz ? gr.x : 0.0);
+    m[r][1][1] = h1.y + (2 * bi[r] + 1 == nz ? gr.y : 0.0);
+  }
 #pragma unroll 5
   for (int s = 0; s < np1; ++s) {
     const double* gr = G + s * CH_GS;
@@ -192,7 +223,7 @@ __device__ __forceinline__ bool chain_stage(const View& V, const ChainLds& S, in
     }
   }
   for (int s = 0; s < g; ++s) {
-    const double sgs = sg[s];
+    const double sgs = S.sg0[s];
     const double* gr = G + (CH_NRP + s) * CH_GS;
 #pragma unroll
     for (int r = 0; r < NS; ++r) {
@@ -205,139 +236,173 @@ __device__ __forceinline__ bool chain_stage(const View& V, const ChainLds& S, in
       m[r][1][1] = fma(gv.y, u1, m[r][1][1]);
     }
   }
-  OCP_STAMP(22);
-  // --- symmetric sweep of the nu_k input pivots, two per round ---
-  // publish(q): the pivot pair (2q, 2q + 1)'s row / column of M into the round's buffers c0 = M(., 2q),
-  // c1 = M(., 2q + 1) (lower storage: rows below from block column q, columns left from block row q)
-  auto publish = [&](int q, double* c0) {
-    double* c1 = c0 + 64;
 #pragma unroll
-    for (int r = 0; r < NS; ++r) {
-      if (tid + NT * r < nt) {
-        if (bj[r] == q) {
-#pragma unroll
-          for (int a = 0; a < 2; ++a) {
-            c0[2 * bi[r] + a] = m[r][a][0];
-            if (bi[r] > q || a == 1) c1[2 * bi[r] + a] = m[r][a][1];
-          }
-        }
-        if (bi[r] == q) {
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            if (bj[r] < q || b == 0) c0[2 * bj[r] + b] = m[r][0][b];
-            c1[2 * bj[r] + b] = m[r][1][b];
-          }
-        }
-      }
-    }
-  };
-  if (mk > 0) {
-    publish(0, S.C);
-    lds_barrier();
-    double* Lf = V.Lf(k);
-    const int npair = (mk + 1) >> 1;
-    for (int p = 0; p < npair; ++p) {
-      const int j = 2 * p, j1 = j + 1;
-      const bool two = j1 < mk;
-      const double* c0 = S.C + (p & 1) * 128;
-      const double* c1 = c0 + 64;
-      const double d0 = c0[j], a1 = c0[j1], e1 = c1[j1];
-      bad = bad || (d0 != d0);
-      const double d0i = d0 > 1e-200 ? 1.0 / d0 : 0.0;
-      const double l1 = a1 * d0i;
-      const double d1 = fma(-a1, l1, e1);
-      double d1i = 0.0;
-      if (two) {
-        bad = bad || (d1 != d1);
-        d1i = d1 > 1e-200 ? 1.0 / d1 : 0.0;
-      }
-      // the LDL' factor of M_uu: pivot column j (rows j..), column j + 1 after pivot j (rows j + 1..)
-      if (tid >= j && tid < mk) {
-        Lf[j * mk + tid] = c0[tid];
-        if (two && tid >= j1) Lf[j1 * mk + tid] = fma(-c0[tid], l1, c1[tid]);
-      }
-#pragma unroll
-      for (int r = 0; r < NS; ++r) {
-        const int i0 = 2 * bi[r], l0 = 2 * bj[r];
-        const d2v ci0 = *(const d2v*)(c0 + i0), ci1 = *(const d2v*)(c1 + i0);
-        const d2v cl0 = *(const d2v*)(c0 + l0), cl1 = *(const d2v*)(c1 + l0);
-        // per index x: at = sweep-j vector (-1 at j), c1p = M'(x, j + 1), bt = sweep-(j + 1) vector (-1 at j + 1)
-        double at[4], bt[4];
-        const int xs[4] = {i0, i0 + 1, l0, l0 + 1};
-        const double c0x[4] = {ci0.x, ci0.y, cl0.x, cl0.y}, c1x[4] = {ci1.x, ci1.y, cl1.x, cl1.y};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          at[t] = xs[t] == j ? -1.0 : c0x[t];
-          const double c1p = fma(-at[t], l1, xs[t] == j ? 0.0 : c1x[t]);
-          bt[t] = xs[t] == j1 ? -1.0 : c1p;
-        }
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int i = i0 + a, l = l0 + b;
-            const double b1 = (i == j || l == j) ? 0.0 : m[r][a][b];
-            double v = fma(-at[a] * d0i, at[2 + b], b1);
-            if (two) {
-              const double b2 = (i == j1 || l == j1) ? 0.0 : v;
-              v = fma(-bt[a] * d1i, bt[2 + b], b2);
-            }
-            m[r][a][b] = v;
-          }
-      }
-      if (p + 1 < npair) {
-        publish(p + 1, S.C + ((p + 1) & 1) * 128);
-        lds_barrier();
-      }
+  for (int r = 0; r < NS; ++r) {
+    if (tid + NT * r < nt) {
+      double* o = S.Ml + (2 * bi[r]) * CH_GS + 2 * bj[r];
+      *(d2v*)o = d2v{m[r][0][0], m[r][0][1]};
+      *(d2v*)(o + CH_GS) = d2v{m[r][1][0], m[r][1][1]};
     }
   }
-  OCP_STAMP(23);
-  // --- outputs: K_k = -(x rows of the input columns)', kff_k, P_k / p_k (global and Paug) ---
-  {
-    double* Kk = V.K(k);
-    double* kf = V.kf() + d[2];
-    double* Pk = V.P(k);
-    double* pk = V.pv() + (long long)k * nx;
+}
+
+// One pair round of (C): pivots j, j + 1 (j = 4 jb + A0). Publishes the pair's columns (rows >= 4 jb, from the
+// blocks of block column jb; the column offset A0 in the block is a template argument, so the publish needs no
+// select), stores the factor's columns, and applies the rank-2 update to every entry (entries in processed rows /
+// columns are dead: never read again). A missing second pivot (odd nu_k) has 1 / d1 = 0, which leaves the update's
+// second term exactly 0.
+template <int NB, int A0>
+__device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&bi)[NB], const int (&bj)[NB],
+                                            const bool (&on)[NB], int j, int mk, int n1, double* c0, double* c1,
+                                            double* F, bool& bad) {
+  const int lane = threadIdx.x, j1 = j + 1, jb = j >> 2;
+  const bool two = j1 < mk;
 #pragma unroll
-    for (int r = 0; r < NS; ++r) {
-      if (!(tid + NT * r < nt)) continue;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int i = 2 * bi[r] + a, l = 2 * bj[r] + b;
-          if (i < l || i >= n1 || i < mk) continue;
-          const double v = m[r][a][b];
-          const int I = i - mk;
-          if (l < mk) {
-            if (I < nx) Kk[I * mk + l] = -v;
-            else kf[l] = -v;
-          } else {
-            const int J = l - mk;
-            if (I < nx) {
-              Pk[J * nx + I] = v;
-              Pk[I * nx + J] = v;
-              S.Pa[I * CH_PS + J] = v;
-              S.Pa[J * CH_PS + I] = v;
-            } else if (J < nx) {
-              pk[J] = v;
-              S.Pa[nx * CH_PS + J] = v;
-              S.Pa[J * CH_PS + nx] = v;
-            } else {
-              S.Pa[nx * CH_PS + nx] = 0.0;
-            }
-          }
-        }
+  for (int q = 0; q < NB; ++q) {
+    if (on[q] && bj[q] == jb) {
+      double* o0 = c0 + 4 * bi[q];
+      double* o1 = c1 + 4 * bi[q];
+      *(d2v*)o0 = d2v{m[q][0][A0], m[q][1][A0]};
+      *(d2v*)(o0 + 2) = d2v{m[q][2][A0], m[q][3][A0]};
+      *(d2v*)o1 = d2v{m[q][0][A0 + 1], m[q][1][A0 + 1]};
+      *(d2v*)(o1 + 2) = d2v{m[q][2][A0 + 1], m[q][3][A0 + 1]};
     }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const double d0 = c0[j], a1 = c0[j1], e1 = c1[j1];
+  bad = bad || (d0 != d0);
+  const double d0i = d0 > 1e-200 ? 1.0 / d0 : 0.0;
+  const double l1 = a1 * d0i;
+  const double d1 = fma(-a1, l1, e1);
+  bad = bad || (two && d1 != d1);
+  const double d1i = (two && d1 > 1e-200) ? 1.0 / d1 : 0.0;
+  // the factor's columns into the F image (rows >= j; chain_out reads column j + 1 from row j + 1)
+  if (lane >= j && lane < n1) {
+    const double v0 = c0[lane];
+    F[j * CH_FS + lane] = v0;
+    if (two) F[j1 * CH_FS + lane] = fma(-v0, l1, c1[lane]);
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const d2v ri0 = *(const d2v*)(c0 + 4 * bi[q]), ri1 = *(const d2v*)(c0 + 4 * bi[q] + 2);
+    const d2v si0 = *(const d2v*)(c1 + 4 * bi[q]), si1 = *(const d2v*)(c1 + 4 * bi[q] + 2);
+    const d2v rl0 = *(const d2v*)(c0 + 4 * bj[q]), rl1 = *(const d2v*)(c0 + 4 * bj[q] + 2);
+    const d2v sl0 = *(const d2v*)(c1 + 4 * bj[q]), sl1 = *(const d2v*)(c1 + 4 * bj[q] + 2);
+    const double ci[4] = {ri0.x, ri0.y, ri1.x, ri1.y}, cl[4] = {rl0.x, rl0.y, rl1.x, rl1.y};
+    const double ei[4] = {si0.x, si0.y, si1.x, si1.y}, el[4] = {sl0.x, sl0.y, sl1.x, sl1.y};
+    double ui[4], vi[4], bl[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      ui[t] = -ci[t] * d0i;
+      vi[t] = -fma(-ci[t], l1, ei[t]) * d1i;
+      bl[t] = fma(-cl[t], l1, el[t]);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) m[q][a][b] = fma(vi[a], bl[b], fma(ui[a], cl[b], m[q][a][b]));
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// (C) on wave 0: NB 4 x 4 lower blocks of M per lane (block beta = lane + 64 q), the pair rounds, the outputs.
+// Returns the NaN flag of the pivots.
+template <int NB>
+__device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, const int* d, double* F, double* PaW) {
+  const OcpLayout& L = V.L;
+  const int lane = threadIdx.x, nx = L.nx, np1 = nx + 1;
+  const int mk = d[0], nz = mk + nx, n1 = nz + 1, nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
+  bool bad = false;
+  int bi[NB], bj[NB];
+  bool on[NB];
+  double m[NB][4][4];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int beta = lane + 64 * q;
+    on[q] = beta < nt4;
+    ch_block(on[q] ? beta : 0, bi[q], bj[q]);
+    const double* src = S.Ml + (4 * bi[q]) * CH_GS + 4 * bj[q];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const d2v v0 = *(const d2v*)(src + a * CH_GS), v1 = *(const d2v*)(src + a * CH_GS + 2);
+      m[q][a][0] = v0.x;
+      m[q][a][1] = v0.y;
+      m[q][a][2] = v1.x;
+      m[q][a][3] = v1.y;
+    }
+    if (bi[q] == bj[q]) {  // the image holds the lower triangle: the diagonal block's upper part by symmetry
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = a + 1; b < 4; ++b) m[q][a][b] = m[q][b][a];
+    }
+  }
+  double* c0 = S.C;
+  double* c1 = S.C + 64;
+  OCP_STAMP(27);
+  for (int j = 0; j < mk; j += 4) {
+    chain_round<NB, 0>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad);
+    if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad);
+  }
+  OCP_STAMP(23);
+  // --- Paug of node k: the blocks back into the image, then its live part (rows / columns >= nu_k, the lower
+  // triangle read for both halves) into PaW (global P_k, p_k: chain_out on the helper waves, a stage later) ---
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (!on[q]) continue;
+    double* o = S.Ml + (4 * bi[q]) * CH_GS + 4 * bj[q];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      *(d2v*)(o + a * CH_GS) = d2v{m[q][a][0], m[q][a][1]};
+      *(d2v*)(o + a * CH_GS + 2) = d2v{m[q][a][2], m[q][a][3]};
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  OCP_STAMP(28);
+  const int J = lane & 31;
+  double pv[14];
+#pragma unroll
+  for (int it = 0; it < 14; ++it) {
+    const int I = (lane >> 5) + 2 * it;
+    const int hi = I > J ? I : J, lo = I > J ? J : I;
+    pv[it] = (I < np1 && J < np1) ? S.Ml[(mk + hi) * CH_GS + mk + lo] : 0.0;
+  }
+#pragma unroll
+  for (int it = 0; it < 14; ++it) {
+    const int I = (lane >> 5) + 2 * it;
+    if (I < np1 && J < np1) PaW[I * CH_PS + J] = (I == nx && J == nx) ? 0.0 : pv[it];
   }
   return bad;
 }
 
-// Backward factorisation of the barrier-weighted Newton matrix, latency form. Writes P_k, pv_k (k = 0..N), K_k, kf_k,
-// and the LDL' columns Lf_k (k = 0..N-1), as factor_pass. Returns false on a NaN pivot.
+// K_k = -L_uu^-T L_xu', kff_k = -L_uu^-T l_r' for stages [k0, k1) from the LDL' factor F = L D the chain left (u rows
+// in Lf, x / rhs rows in K / kf): thread per (stage, column); a guarded pivot (d <= 1e-200) has a zero column
+__device__ __forceinline__ void chain_gains(const View& V, int k0, int k1) {
+  const OcpLayout& L = V.L;
+  const int nx = L.nx, np1 = nx + 1;
+  for (int e = threadIdx.x; e < (k1 - k0) * np1; e += NT) {
+    const int k = k0 + e / np1, c = e - (e / np1) * np1;
+    const int mk = L.nu[k];
+    if (mk == 0) continue;
+    const double* F = V.Lf(k);
+    double* x = c < nx ? V.K(k) + c * mk : V.kf() + L.cu[k];
+    for (int a = mk - 1; a >= 0; --a) {
+      const double da = F[a * mk + a];
+      const double dai = da > 1e-200 ? 1.0 / da : 0.0;
+      double s = x[a];
+      for (int b = a + 1; b < mk; ++b) s = fma(F[a * mk + b], x[b], s);
+      x[a] = -(s * dai);
+    }
+  }
+}
+
+// Backward factorisation of the barrier-weighted Newton matrix, latency form. Writes P_k, pv_k (k = 0..N), the LDL'
+// columns Lf_k and the factor's x / rhs rows (k = 0..N-1; chain_gains turns them into K_k, kf_k). Returns false on a
+// NaN pivot.
 __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, const double* hp, double reg) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, N = L.N, nx = L.nx, np1 = nx + 1;
+  const int wave = tid >> 6;
   int bi[CH_MAXT], bj[CH_MAXT];
 #pragma unroll
   for (int r = 0; r < CH_MAXT; ++r) ch_block(tid + NT * r, bi[r], bj[r]);
@@ -354,6 +419,8 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
     dk[5] = (int)L.orec[8 * k + 0];
     dk[6] = (int)L.ocon[4 * k + 0];
     dk[7] = nb * (nb + 1) / 2;
+    dk[8] = L.cM[k];
+    dk[9] = L.cK[k];
   }
   // terminal node: P_N = Q_N + reg I + C_N' Sigma C_N, p_N = g_x,N; Paug's padding rows / columns zero
   {
@@ -375,34 +442,32 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
         val = V.gx()[(long long)N * nx + c];
       }
       S.Pa[e] = val;
+      S.Pa2[e] = 0.0;
     }
   }
   __syncthreads();  // descriptors
-  ChainRegs cur;    // stage k's Hc blocks / rhs entries (its G image is in LDS)
-  chain_fetch(V, S.desc + CH_DESC * (N - 1), N - 1, bi, bj, hp, cur);
-  chain_commit(V, S.desc + CH_DESC * (N - 1), cur, S.G0, S.sg0);
+  if (wave > 0) chain_load(V, S.desc + CH_DESC * (N - 1), N - 1, hp, S, nullptr, nullptr, nullptr);
   __syncthreads();
   OCP_STAMP(20);
   for (int k = N - 1; k >= 0; --k) {
-    const int cb = (N - 1 - k) & 1;
-    const double* G = cb ? S.G1 : S.G0;
-    const double* sg = cb ? S.sg1 : S.sg0;
     const int* d = S.desc + CH_DESC * k;
     const int mk = d[0], nz = mk + nx, n1 = nz + 1, nb = (n1 + 1) >> 1, nt = d[7];
-    // --- prefetch of stage k - 1 (registers; committed to the other image at the end of this stage) ---
-    ChainRegs nxt;
-    if (k > 0) chain_fetch(V, d - CH_DESC, k - 1, bi, bj, hp, nxt);
-    // --- T = Paug [B A rb; 0 0 1]: 2 x 2 blocks over rows 0..np1 (Paug's odd pad row is zero), columns < 2 nb ---
+    const int pb = (N - 1 - k) & 1;
+    const double* PaR = pb ? S.Pa2 : S.Pa;  // Paug of node k + 1
+    double* PaW = pb ? S.Pa : S.Pa2;        // Paug of node k
+    double* Fw = (k & 1) ? S.F1 : S.F0;     // the factor image of stage k (stage k + 1's is the other)
+    // --- (A) T = Paug [B A rb; 0 0 1]: 2 x 2 blocks over rows 0..np1 (Paug's odd pad row is zero), columns < 2 nb ---
     {
+      const double* G = S.G0;
       const int nrp = (np1 + 1) >> 1, items = nrp * nb;
       const int w0 = tid, w1 = tid + NT;
       const int ws0 = w0 < items ? w0 : 0, ws1 = w1 < items ? w1 : 0;
       const int rp0 = ws0 / nb, cp0 = ws0 - rp0 * nb, rp1 = ws1 / nb, cp1 = ws1 - rp1 * nb;
-      const double* pa0 = S.Pa + 2 * rp0;
+      const double* pa0 = PaR + 2 * rp0;
       const double* gc0 = G + 2 * cp0;
       double t0[4] = {0.0, 0.0, 0.0, 0.0};
       if (items > NT) {  // uniform: two items per thread
-        const double* pa1 = S.Pa + 2 * rp1;
+        const double* pa1 = PaR + 2 * rp1;
         const double* gc1 = G + 2 * cp1;
         double t1[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 5
@@ -441,24 +506,33 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
     }
     lds_barrier();
     OCP_STAMP(21);
+    // --- (B) M into the image ---
     const int ns = (nt + NT - 1) / NT;
-    if (ns == 1) bad = chain_stage<1>(V, S, k, d, G, sg, bi, bj, cur) || bad;
-    else if (ns == 2) bad = chain_stage<2>(V, S, k, d, G, sg, bi, bj, cur) || bad;
-    else bad = chain_stage<3>(V, S, k, d, G, sg, bi, bj, cur) || bad;
-    // --- the prefetched stage k - 1 into the other image ---
-    if (k > 0) {
-      chain_commit(V, d - CH_DESC, nxt, cb ? S.G0 : S.G1, cb ? S.sg0 : S.sg1);
-#pragma unroll
-      for (int r = 0; r < CH_MAXT; ++r)
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-#pragma unroll
-          for (int b = 0; b < 2; ++b) cur.hc[r][a][b] = nxt.hc[r][a][b];
-          cur.gr[r][a] = nxt.gr[r][a];
-        }
+    if (ns == 1) chain_m<1>(S, nx, d, bi, bj);
+    else if (ns == 2) chain_m<2>(S, nx, d, bi, bj);
+    else chain_m<3>(S, nx, d, bi, bj);
+    lds_barrier();
+    OCP_STAMP(22);
+    // --- (C) wave 0: the elimination and the outputs; waves 1-3: stage k - 1's operands ---
+    if (wave == 0) {
+      const int nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
+      bool b2;
+      if (nt4 <= 64) b2 = chain_elim<1>(V, S, d, Fw, PaW);
+      else b2 = chain_elim<2>(V, S, d, Fw, PaW);  // nt4 <= 120: n1 <= 60 (OCP_CHAIN_MAX_N1, ocp_chain_lds_bytes)
+      bad = bad || b2;
+      OCP_STAMP(25);
+    } else if (k > 0) {
+      OCP_SPAN_BEGIN(t_load);
+      // stage k - 1's operands; stage k + 1's outputs (its Paug and factor images, untouched in this stage)
+      const bool out = k + 1 < N;
+      chain_load(V, d - CH_DESC, k - 1, hp, S, out ? d + CH_DESC : nullptr, PaR, (k & 1) ? S.F0 : S.F1);
+      OCP_SPAN_END(26, t_load, 64);
     }
     lds_barrier();
     OCP_STAMP(24);
   }
+  // the outputs of stages 1 (if not yet written: N == 1 has none) and 0
+  if (N > 1) chain_out(V, S.desc + CH_DESC, 1, (N & 1) ? S.Pa : S.Pa2, S.F1, tid, NT);
+  chain_out(V, S.desc, 0, (N & 1) ? S.Pa2 : S.Pa, S.F0, tid, NT);
   return __syncthreads_or(bad) == 0;
 }

@@ -315,9 +315,10 @@ int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_sett
 int cmpc_ocp_destroy(cmpc_ocp* ocp);
 int cmpc_ocp_set_settings(cmpc_ocp* ocp, const cmpc_settings* settings);
 /* Form of the Riccati factorisation for batches of up to 256 problems (one problem per CU; the MPC tick's B = 1):
- * chain = 1 (default) takes the latency form (csrc/ocp_chain.hpp: the stage's constant Hessian blocks laid out once
- * per solve, a symmetric sweep of the input pivots on the lower triangle in 2 x 2 register blocks, two pivots per
- * workgroup barrier) wherever the dimensions fit it (nx <= 27, nu_k + nx + 1 <= 64, nc_k <= 16, N <= 512);
+ * chain = 1 (default) takes the latency form (csrc/ocp_chain.hpp: the stage matrix formed by the workgroup, its input
+ * pivots eliminated two per round by one wave on 4 x 4 register blocks while the other waves load the next stage,
+ * the gains solved stage-parallel afterwards) wherever the dimensions fit it (nx <= 27, nu_k + nx + 1 <= 60,
+ * nc_k <= 16, N <= 512);
  * chain = 0 the batched form (a Gauss-Jordan sweep on the full stage matrix). Both run the same iteration; statuses and iteration counts agree, trajectories to rounding.
  * cmpc_ocp_path returns 1 when small batches take the latency form. */
 int cmpc_ocp_set_path(cmpc_ocp* ocp, int chain);

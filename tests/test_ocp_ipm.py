@@ -532,7 +532,7 @@ def test_device_grid_form_equals_one_workgroup(cm, op, projected):
 @pytest.mark.gpu
 @pytest.mark.parametrize("projected", [True, False])
 def test_device_latency_form_equals_batched_form(cm, op, projected):
-    """Small batches take the latency form of the factorisation (ocp_chain.hpp: LDL' on 2 x 2 lower blocks, gains by
+    """Small batches take the latency form of the factorisation (ocp_chain.hpp: LDL' on 4 x 4 lower blocks, gains by
     back substitution); the batched form (Gauss-Jordan sweep) is the other factorisation of the same Newton systems:
     statuses and iteration counts equal, trajectories to rounding, both against the oracle at 1e-9; a batch of 264
     (above the latency form's 256) takes the batched form and equals the small batch to rounding as well."""
