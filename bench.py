@@ -145,6 +145,9 @@ def ocp_main(args):
     iters_mean = float(it[ok].mean()) if ok.any() else 0.0
     flops = sum(ocp_flops(p0["nu"], p0.get("nc"), p0["nx"], float(it[b])) for b in range(B) if ok[b])
     ach = flops / (kernel_ms * 1e-3)
+    okey = f"ocp_{args.ocp}_B{B}"
+    traffic, traffic_src = pmc_traffic(os.path.join(ROOT, "profiles", f"traffic_{okey}.json"), "k_ocp")
+    tick = ocp_tick(gen, projected) if rank == 0 else None
     value = world * B * args.steps / elapsed
     shape = (f"nx={p0['nx']}, N={p0['N']} (67 intervals + 3 event nodes), "
              + ("nu 10/12/0 projected, no rows" if projected else "nu 24/0 with 12-14 equality rows per node"))
@@ -157,10 +160,13 @@ def ocp_main(args):
         "config": {"workload": f"{B} OCP-QPs per GPU, {shape}, stage-wise interior-point (HPIPM's method), fp64",
                    "batch_per_gpu": B, "parallelism": f"shard{world}"},
         "ms_per_solve_b1": ms_b1, "ms_per_solve_b1_host_path": ms_b1_host,
-        "roofline": {"bound": "valu", "kernel": "k_ocp_ipm", "achieved": ach / 1e12, "peak": FP64_PEAK / 1e12,
-                     "unit": "TFLOP/s", "frac": ach / FP64_PEAK, "traffic": None, "flops_per_launch": flops,
-                     "ms_per_launch": kernel_ms, "flops_counted": "ocp_flops (bench.py): Riccati factorisation, "
-                                                                  "Newton solves and residuals per IPM iteration"},
+        "roofline": {"bound": "valu", "kernel": "k_ocp_ipm / k_ocp_grid", "achieved": ach / 1e12,
+                     "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s", "frac": ach / FP64_PEAK, "traffic": traffic,
+                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                     "flops_per_launch": flops, "ms_per_launch": kernel_ms,
+                     "flops_counted": "ocp_flops (bench.py): Riccati factorisation, Newton solves and residuals per "
+                                      "IPM iteration"},
+        "tick": tick,
         "solver": {"success_frac": float(ok.mean()), "mean_iters": iters_mean},
         "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
     }
@@ -189,9 +195,57 @@ def ocp_main(args):
                                             f"-march={oracle_fast_build()[1]}, {threads} pthreads, {wall:.2f} s wall"}
         result["max_rel_du_vs_cpu_fp64"] = float(rel)
         result["statuses_equal_cpu"] = bool(np.array_equal(stc, st[:S]))
+        # the MPC tick's comparison: one problem on one CPU thread (the oracle, the reference's algorithm), ms per solve
+        reps1, t1s = 0, 0.0
+        while t1s < 1.0 or reps1 < 3:
+            t = time.perf_counter()
+            op.ocp_ipm_batch(p0["N"], p0["nx"], p0["nu"], x0[:1], recs[:1], nc=p0.get("nc"),
+                             crec=crecs[:1] if crecs is not None else None, nthreads=1)
+            t1s += time.perf_counter() - t
+            reps1 += 1
+        result["cpu_single_thread_ms_b1"] = t1s / reps1 * 1e3
+        result["cpu_single_thread_sample"] = (f"problem 0 of the batch x{reps1}, oracle_ocp_ipm_batch with 1 thread, "
+                                              f"{t1s:.2f} s wall")
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()
+
+
+def ocp_tick(gen, projected, T=60, warm=5):
+    """The MPC tick through the C++ HpipmInterface mirror (tests/cpp/bin/hpipm_tick): per tick resize + solve +
+    getRiccatiFeedback on the legged problem with the gait advancing one dt per tick (event nodes and per-stage inputs
+    shifting, t0 = 0.015 t), host times per phase and the solve's kernel time; the medians over the ticks after the
+    first `warm`. None (with the reason) when the binary is not built."""
+    import struct
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", "hpipm_tick")
+    if not os.path.exists(exe):
+        return {"error": "tests/cpp/bin/hpipm_tick not built (make -C tests/cpp)"}
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(struct.pack("<i", T))
+        for t in range(T):
+            p = gen.legged_problem(9000 + t, projected=projected, t0=0.015 * t)
+            rec, crec = gen.pack(p)
+            rows = p.get("nc") is not None
+            f.write(struct.pack("<3i", p["N"], p["nx"], 1 if rows else 0))
+            f.write(np.asarray(p["nu"], np.int32).tobytes())
+            if rows:
+                f.write(np.asarray(p["nc"], np.int32).tobytes())
+            f.write(np.asarray(p["x0"], np.float64).tobytes())
+            f.write(np.asarray(rec, np.float64).tobytes())
+            if rows:
+                f.write(np.asarray(crec, np.float64).tobytes())
+        path = f.name
+    try:
+        r = subprocess.run([exe, path, str(warm)], capture_output=True, text=True, timeout=300)
+        out = r.stdout.strip().splitlines()
+        doc = json.loads(out[-1]) if out else {"error": r.stderr[-300:]}
+        doc["what"] = ("HpipmInterface (C++ mirror): resize(extractSizesFromProblem) + solve + getRiccatiFeedback per "
+                       "tick, the gait advancing one dt per tick; host ms, kernel ms from HIP events")
+        return doc
+    finally:
+        os.unlink(path)
 
 
 def cpu_share():
@@ -427,6 +481,11 @@ def main():
     ap.add_argument("--ocp", choices=["projected", "rows"], default="",
                     help="benchmark the HpipmInterface::solve path (cmpc_ocp_solve) on ocs2_legged_robot-size OCP-QPs "
                          "instead of the centroidal headline; --batch problems per step")
+    ap.add_argument("--cadence", type=float, default=0.0, metavar="MS",
+                    help="> 0: after the timed run, one step every MS milliseconds (20 = the MPC's 50 Hz, task.info:108) "
+                         "for --cadence-calls calls, each synchronised; the per-call latency distribution is added to "
+                         "the line as 'cadence' (the clocks a 50 Hz loop runs at, not a saturated stream)")
+    ap.add_argument("--cadence-calls", type=int, default=100)
     ap.add_argument("--allow-shared", action="store_true",
                     help="let ranks share a GPU (rehearsal on a one-GPU box); the line then says shared_gpu and n_gpus "
                          "counts distinct devices")
@@ -505,6 +564,17 @@ def main():
         else:
             e.solve_device(B, x0, xref, foot, contact, uo, None, so, io, sh)
 
+    # value_short_warmup: the same timed loop right after 5 warm-up steps with no extension (the GPU near its idle
+    # clock), before the regular warm-up below; it separates clock warm-up from kernel gains in the headline
+    for i in range(5):
+        step(i)
+    H.hipDeviceSynchronize()
+    barrier()
+    t_s = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    H.hipDeviceSynchronize()
+    value_short = world * B * args.steps / max_over_ranks(time.perf_counter() - t_s)
     for i in range(args.warmup):
         step(i)
     H.hipDeviceSynchronize()
@@ -612,6 +682,24 @@ def main():
                 rg.close()
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             gather["error"] = repr(e)[:200]
+
+    cadence = None
+    if args.cadence > 0:  # one synchronised call per period, as the MPC loop issues them
+        lat = []
+        nxt = time.perf_counter()
+        for i in range(args.cadence_calls):
+            nxt += args.cadence * 1e-3
+            t = time.perf_counter()
+            direct_step(0)
+            H.hipStreamSynchronize(stream)
+            lat.append((time.perf_counter() - t) * 1e3)
+            time.sleep(max(0.0, nxt - time.perf_counter()))
+        lat = np.array(lat)
+        cadence = {"period_ms": args.cadence, "calls": args.cadence_calls,
+                   "latency_ms": {"p50": float(np.percentile(lat, 50)), "p90": float(np.percentile(lat, 90)),
+                                  "p99": float(np.percentile(lat, 99)), "max": float(lat.max()),
+                                  "first": float(lat[0])},
+                   "what": "host time of one cmpc_solve_batch call + stream sync, one call per period"}
 
     status = st.host()
     iters = it.host() if args.sqp_iters <= 0 else sqp_qi.host()
@@ -732,6 +820,8 @@ def main():
         "stage_events": args.stage_events,
         "stage_event_steps": n_prof if timed_events else None,
         "value_end_to_end": value_e2e,
+        "value_short_warmup": value_short,
+        "cadence": cadence,
         "gather_ms": gather_ms, "gather": gather,
         "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
         "solver": {"success_frac": float(ok.mean()), "mean_iters": float(iters[ok].mean()) if ok.any() else 0.0,

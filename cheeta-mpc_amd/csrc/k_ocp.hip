@@ -1519,7 +1519,8 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
     acl_pass(V, S, true);
     __syncthreads();
     OCP_STAMP(3);
-    forward_pass(V, S);
+    if constexpr (FAST) chain_affine<false>(V, CS, S.vec, S.vec + 64);
+    else forward_pass(V, S);
     OCP_STAMP(4);
     double amax = block_reduce(post_pass(V), S.red, OpMin());
     OCP_STAMP(5);
@@ -1552,12 +1553,22 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
       step_rhs(V);
       __syncthreads();
       OCP_STAMP(6);
-      backward_vec_pass(V, S);
+      if constexpr (FAST) {
+        const int N = a.L.N;
+        bwd_vec_a(V, 0, N, true);
+        __syncthreads();
+        chain_affine<true>(V, CS, S.vec, S.vec + 64);
+        __syncthreads();
+        bwd_vec_c(V, 0, N);
+      } else {
+        backward_vec_pass(V, S);
+      }
       __syncthreads();
       OCP_STAMP(7);
       acl_pass(V, S, false);
       __syncthreads();
-      forward_pass(V, S);
+      if constexpr (FAST) chain_affine<false>(V, CS, S.vec, S.vec + 64);
+      else forward_pass(V, S);
       OCP_STAMP(8);
       amax = block_reduce(post_pass(V), S.red, OpMin());
       OCP_STAMP(5);
@@ -1889,7 +1900,10 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     acl_pass(V, S, true, R.k0, R.k1, true);
     if (!sync()) break;
     OCP_STAMP(3);
-    if (lead) forward_pass(V, S);
+    if (lead) {
+      if constexpr (FAST) chain_affine<false>(V, CS, S.vec, S.vec + 64);
+      else forward_pass(V, S);
+    }
     if (!sync()) break;
     OCP_STAMP(4);
     double amax = block_reduce(post_pass(V, R.k0, R.k1, R.n1), S.red, OpMin());
@@ -1937,14 +1951,20 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       OCP_STAMP(6);
       bwd_vec_a(V, R.k0, R.k1, last);
       if (!sync()) break;
-      if (lead) bwd_vec_b(V, S);
+      if (lead) {
+        if constexpr (FAST) chain_affine<true>(V, CS, S.vec, S.vec + 64);
+        else bwd_vec_b(V, S);
+      }
       if (!sync()) break;
       bwd_vec_c(V, R.k0, R.k1);
       __syncthreads();
       OCP_STAMP(7);
       acl_pass(V, S, false, R.k0, R.k1, true);
       if (!sync()) break;
-      if (lead) forward_pass(V, S);
+      if (lead) {
+        if constexpr (FAST) chain_affine<false>(V, CS, S.vec, S.vec + 64);
+        else forward_pass(V, S);
+      }
       if (!sync()) break;
       OCP_STAMP(8);
       {
@@ -1981,8 +2001,13 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   if (!alive) status = 3;  // a barrier timed out: the grid drained, the result is not valid
   // --- the exit point's Riccati quantities (cmpc_ocp_set_keep_riccati; k_ocp_ric's outputs, same formulas) ---
   if (a.ric && alive && status != 3) {
+    // Without rows the last Newton step's factorisation is the exit point's (no Sigma): the solve keeps its P_k, K_k,
+    // Lr_k only (factor-only; the exit point's p_k, kff_k and the stage-0 rebuild come from cmpc_ocp_riccati's
+    // refactorisation when asked for, the MPC's feedback policy needs none of them). With rows the factorisation is
+    // redone at the exit point's Sigma and everything is kept.
+    const bool fonly = m == 0;
     // Sigma and the rows' step term at the exit iterate (complementarity kept), the step's right-hand side
-    {
+    if (!fonly || it == 0) {
       const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
                    *ru = V.row(R_RU);
       double *sig = V.row(R_SIG), *w = V.row(R_W);
@@ -1990,13 +2015,11 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
         sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
         w[j] = ll[j] * rl[j] / tl[j] - lu[j] * ru[j] / tu[j];
       }
+      __syncthreads();
+      step_rhs_range(V, R.k0, R.k1, R.n1);
+      sync();
     }
-    __syncthreads();
-    step_rhs_range(V, R.k0, R.k1, R.n1);
-    sync();
-    // without rows the last Newton step's factorisation is the exit point's (no Sigma): only the vector parts are
-    // redone (p_k, kff_k by the corrector's recursion on the kept K, Acl, LDL' factors); with rows (or no step taken)
-    // the factorisation itself at the exit point's Sigma
+    // the factorisation at the exit point (with rows, or when no step was taken: no factorisation to keep)
     const bool full = m > 0 || it == 0;
     if (full) {
       if (lead) {
@@ -2007,13 +2030,18 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       } else if (tid == 0) {
         mine[5] = 0.0;
       }
-    } else {
+    } else if (!fonly) {
       bwd_vec_a(V, R.k0, R.k1, last);
       sync();
-      if (lead) bwd_vec_b(V, S);
+      if (lead) {
+        if constexpr (FAST) chain_affine<true>(V, CS, S.vec, S.vec + 64);
+        else bwd_vec_b(V, S);
+      }
       sync();
       bwd_vec_c(V, R.k0, R.k1);
       if (tid == 0) mine[5] = 0.0;
+    } else if (tid == 0) {
+      mine[5] = 0.0;
     }
     sync();
     grid_collect(part + 5, G, 1, ops_max, red);
@@ -2037,7 +2065,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
           Lo[e] = (i >= j && d > 1e-200) ? F[e] / sqrt(d) : 0.0;
         }
       }
-      for (int e = (R.k0 > 1 ? L.cu[R.k0] : L.cu[1]) + tid; e < R.u1; e += NT) {
+      for (int e = (R.k0 > 1 ? L.cu[R.k0] : L.cu[1]) + tid; !fonly && e < R.u1; e += NT) {
         const int k = L.ustage[e], a2 = e - L.cu[k], mk = L.nu[k];
         const double* Kk = V.K(k);
         double s2 = u[e] + V.kf()[e];
@@ -2046,7 +2074,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       }
       const int na = R.k0 > 1 ? R.k0 : 1;
       for (int e = na * nx * nx + tid; e < R.n1 * nx * nx; e += NT) a.ricP[oP + e] = V.ws[L.o_P + e];
-      for (int e = na * nx + tid; e < R.n1 * nx; e += NT) {
+      for (int e = na * nx + tid; !fonly && e < R.n1 * nx; e += NT) {
         const int k = e / nx, i = e - k * nx;
         const double* Pk = V.P(k);
         double s2 = V.pi()[(long long)(k - 1) * nx + i] + V.pv()[e];
@@ -2055,7 +2083,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       }
     }
     sync();  // node 1's P, p and stage 0's Lr before the stage-0 reconstruction
-    if (lead && rok) ric_stage0(V, S, a.ricP + oP, a.ricp + op, a.ricK + oK, a.rick + ok2, a.ricLr + oM);
+    if (lead && rok && !fonly) ric_stage0(V, S, a.ricP + oP, a.ricp + op, a.ricK + oK, a.rick + ok2, a.ricLr + oM);
     if (lead && tid == 0) a.ricst[q] = rok ? 0 : 3;
   } else if (a.ric && lead && tid == 0) {
     a.ricst[q] = 3;

@@ -42,6 +42,7 @@ struct cmpc_ocp {
   hipEvent_t ev_done = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;  // the last solve's end; timing events
   // the last solve (for cmpc_ocp_riccati)
   int last_B = 0, ric_B = 0;  // ric_B: problems whose exit Riccati quantities the last solve left in P .. Lr
+  int ric_full = 0;            // 1: P, p, K, k, Lr all kept (rows); 0: P_k (k >= 1), K, Lr only (factor-only)
   const double *last_rec = nullptr, *last_crec = nullptr;
   int* last_status = nullptr;
 };
@@ -559,6 +560,7 @@ int cmpc_ocp_solve(cmpc_ocp* o, int B, const double* d_x0, const double* d_rec, 
   o->last_crec = d_crec;
   o->last_status = d_status;
   o->ric_B = (a.ric && a.fast && cmpc::ocp_grid_width(o->N, B, o->grid) > 0 && o->grid != 1) ? B : 0;
+  o->ric_full = o->L.m > 0 ? 1 : 0;  // without rows the kernel keeps the factorisation only (k_ocp.hip, exit block)
   return CMPC_OK;
 }
 
@@ -634,7 +636,7 @@ int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, 
     return CMPC_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (hipStreamWaitEvent(st, o->ev_done, 0) != hipSuccess) return CMPC_ERR_HIP;  // after the solve's stream
-  if (B <= o->ric_B) {  // the solve left them (the grid form with keep_riccati): copies
+  if (B <= o->ric_B && o->ric_full) {  // the solve left them (the grid form with keep_riccati): copies
     const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx, D = sizeof(double);
     int r = CMPC_OK;
     auto cp = [&](void* dst, const void* src, size_t n) {
@@ -659,8 +661,51 @@ int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, 
   a.Lr = d_Lr_out ? d_Lr_out : (double*)o->Lr.p;
   a.rstatus = d_status;
   if (cmpc::launch_ocp_ric(a, B, st) != 0) return CMPC_ERR_HIP;
-  if (o->ric_B == 0 || d_P != o->P.p) o->ric_B = 0;  // the workspace's factorisation is the refactorised one now
+  // the workspace's factorisation is the refactorised one now; refactorised into the handle's arrays, their first B
+  // problems hold everything
+  if (d_P == o->P.p && d_K == o->K.p && d_Lr_out == o->Lr.p && d_status == (int*)o->rst.p) {
+    o->ric_B = B;
+    o->ric_full = 1;
+  } else {
+    o->ric_B = 0;
+  }
   return CMPC_OK;
+}
+
+int cmpc_ocp_riccati_feedback_host(cmpc_ocp* o, int b, double* K, double* Lr, double* P1, int* status) {
+  if (!o || b < 0 || b >= o->last_B || !Lr || !P1 || !status || (o->nU > 0 && !K) || o->N < 1) return CMPC_ERR_ARG;
+  hipStream_t st = o->stream;
+  int r = CMPC_OK;
+  if (b >= o->ric_B) {  // not kept by the solve: refactorise problems 0..b into the handle's arrays
+    r = cmpc_ocp_riccati(o, b + 1, (double*)o->P.p, (double*)o->p.p, (double*)o->K.p, (double*)o->k.p,
+                         (double*)o->Lr.p, (int*)o->rst.p, st);
+    if (r != CMPC_OK) return r;
+  } else if (hipStreamWaitEvent(st, o->ev_done, 0) != hipSuccess) {
+    return CMPC_ERR_HIP;
+  }
+  const size_t NP = (size_t)o->N + 1, nx = (size_t)o->nx, D = sizeof(double);
+  const size_t nK = (size_t)o->L.nK, nM = (size_t)o->L.nM;
+  auto ck = [&r](hipError_t e) {
+    if (e != hipSuccess) r = CMPC_ERR_HIP;
+  };
+  const bool pinned = o->pin && o->max_batch <= cmpc::OCP_GRID_MAX_B;
+  unsigned char* pb = (unsigned char*)o->pin;
+  const PinMap m = pinned ? pin_map(o, o->max_batch) : PinMap{};
+  auto out = [&](void* dst, size_t off, const void* src, size_t n) {
+    if (n) ck(hipMemcpyAsync(pinned ? (void*)(pb + off) : dst, src, n, hipMemcpyDeviceToHost, st));
+  };
+  if (nK) out(K, m.K, (const double*)o->K.p + (size_t)b * nK, D * nK);
+  if (nM) out(Lr, m.Lr, (const double*)o->Lr.p + (size_t)b * nM, D * nM);
+  out(P1, m.P, (const double*)o->P.p + (size_t)b * NP * nx * nx + nx * nx, D * nx * nx);
+  out(status, m.rst, (const int*)o->rst.p + b, sizeof(int));
+  ck(hipStreamSynchronize(st));
+  if (r == CMPC_OK && pinned) {
+    if (nK) std::memcpy(K, pb + m.K, D * nK);
+    if (nM) std::memcpy(Lr, pb + m.Lr, D * nM);
+    std::memcpy(P1, pb + m.P, D * nx * nx);
+    std::memcpy(status, pb + m.rst, sizeof(int));
+  }
+  return r;
 }
 
 int cmpc_ocp_riccati_host(cmpc_ocp* o, int B, double* P, double* p, double* K, double* k, double* Lr,

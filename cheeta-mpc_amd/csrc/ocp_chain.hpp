@@ -310,7 +310,7 @@ __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&b
 template <int NB>
 __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, const int* d, double* F, double* PaW) {
   const OcpLayout& L = V.L;
-  const int lane = threadIdx.x, nx = L.nx, np1 = nx + 1;
+  const int lane = threadIdx.x, nx = L.nx;
   const int mk = d[0], nz = mk + nx, n1 = nz + 1, nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
   bool bad = false;
   int bi[NB], bj[NB];
@@ -345,33 +345,23 @@ __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, con
     if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad);
   }
   OCP_STAMP(23);
-  // --- Paug of node k: the blocks back into the image, then its live part (rows / columns >= nu_k, the lower
-  // triangle read for both halves) into PaW (global P_k, p_k: chain_out on the helper waves, a stage later) ---
+  // --- Paug of node k straight from the registers: the live entries (rows / columns >= nu_k, lower triangle of the
+  // blocks) and their mirror into PaW (global P_k, p_k: chain_out on the helper waves, a stage later); the other
+  // entries' stores go to a dummy slot, so the stores need no branch ---
+  double* dummy = S.C + 128 + lane;  // one slot per lane: a shared one would serialise the masked lanes' stores
 #pragma unroll
-  for (int q = 0; q < NB; ++q) {
-    if (!on[q]) continue;
-    double* o = S.Ml + (4 * bi[q]) * CH_GS + 4 * bj[q];
+  for (int q = 0; q < NB; ++q)
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      *(d2v*)(o + a * CH_GS) = d2v{m[q][a][0], m[q][a][1]};
-      *(d2v*)(o + a * CH_GS + 2) = d2v{m[q][a][2], m[q][a][3]};
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  OCP_STAMP(28);
-  const int J = lane & 31;
-  double pv[14];
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-  for (int it = 0; it < 14; ++it) {
-    const int I = (lane >> 5) + 2 * it;
-    const int hi = I > J ? I : J, lo = I > J ? J : I;
-    pv[it] = (I < np1 && J < np1) ? S.Ml[(mk + hi) * CH_GS + mk + lo] : 0.0;
-  }
-#pragma unroll
-  for (int it = 0; it < 14; ++it) {
-    const int I = (lane >> 5) + 2 * it;
-    if (I < np1 && J < np1) PaW[I * CH_PS + J] = (I == nx && J == nx) ? 0.0 : pv[it];
-  }
+      for (int b = 0; b < 4; ++b) {
+        const int i = 4 * bi[q] + a, l = 4 * bj[q] + b;
+        const bool live = on[q] && i >= l && l >= mk && i < n1;
+        const int I = i - mk, J = l - mk;
+        const double v = (I == nx && J == nx) ? 0.0 : m[q][a][b];
+        *(live ? PaW + I * CH_PS + J : dummy) = v;
+        *(live ? PaW + J * CH_PS + I : dummy) = v;
+      }
   return bad;
 }
 
@@ -534,5 +524,105 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
   // the outputs of stages 1 (if not yet written: N == 1 has none) and 0
   if (N > 1) chain_out(V, S.desc + CH_DESC, 1, (N & 1) ? S.Pa : S.Pa2, S.F1, tid, NT);
   chain_out(V, S.desc, 0, (N & 1) ? S.Pa2 : S.Pa, S.F0, tid, NT);
-  return __syncthreads_or(bad) == 0;
+  const bool ok = __syncthreads_or(bad) == 0;
+  __syncthreads();  // every wave's global stores (chain_out) visible to the workgroup
+  return ok;
+}
+
+// The Newton step's serial affine recursions on wave 0, their operands staged in LDS a chunk of stages ahead by waves
+// 1-3 (the factorisation's images are free then):
+//   BWD = false (forward rollout):       dx_1 = bcl_0, dx_{k+1} = Acl_k dx_k + bcl_k           (k = 1 .. N-1)
+//   BWD = true  (corrector's cost-to-go): v_N = g_x,N, p_k = Acl_k' v_{k+1} + h_k, v_k = p_k    (k = N-1 .. 1)
+// Each stage's slot holds the matrix in the order wave 0 reads it (lane r, column c at [c nx + r]: Acl_k as stored,
+// or transposed for BWD) and the vector. Wave 0 keeps the running vector in LDS (v0 / v1, read back by the same wave:
+// no barrier per stage); one workgroup barrier per chunk. The fma order per entry is the one of forward_pass /
+// bwd_vec_b.
+template <bool BWD>
+__device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, double* v0, double* v1) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx, wave = tid >> 6;
+  const int SS = (nxx + nx + 1) & ~1;
+  const int region = (int)((C.F0 + CH_MAXU * CH_FS) - C.Ml);
+  int CK = region / (2 * SS);
+  if (CK > 24 * 192 / SS) CK = 24 * 192 / SS;
+  if (CK > 16) CK = 16;
+  double* buf0 = C.Ml;
+  double* buf1 = C.Ml + CK * SS;
+  const int n = N - 1;  // stages of the recursion
+  const double* vec = BWD ? V.h() : V.bcl();
+  // waves 1-3: chunk c (stages c CK .. c CK + cnt - 1 of the sequence) into its buffer; all loads before any store
+  auto load = [&](int c) {
+    const int t = tid - 64, j0 = c * CK;
+    const int cnt = (n - j0) < CK ? (n - j0) : CK;
+    const int tot = cnt * SS;
+    double* dst = (c & 1) ? buf1 : buf0;
+    double r[24];
+    int idx[24];
+    int j = 0, w = t;
+    while (w >= SS) {
+      w -= SS;
+      ++j;
+    }
+#pragma unroll
+    for (int q = 0; q < 24; ++q) {
+      const int e = t + 192 * q;
+      const bool on = e < tot;
+      const int k = BWD ? N - 1 - (j0 + j) : 1 + j0 + j;
+      const double* src = V.ws;  // an always valid address for the entries outside the chunk
+      if (on) {
+        if (w < nxx) {
+          if (BWD) {
+            const int cc = w / nx, rr = w - cc * nx;  // slot [cc nx + rr] = Acl_k(cc, rr) = stored [rr nx + cc]
+            src = V.Acl(k) + rr * nx + cc;
+          } else {
+            src = V.Acl(k) + w;
+          }
+        } else if (w < nxx + nx) {
+          src = vec + (long long)k * nx + (w - nxx);
+        }
+      }
+      r[q] = *src;
+      idx[q] = on ? j * SS + w : -1;
+      w += 192;
+      while (w >= SS) {
+        w -= SS;
+        ++j;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 24; ++q)
+      if (idx[q] >= 0) dst[idx[q]] = r[q];
+  };
+  if (wave == 0 && tid < nx) {
+    const double d = BWD ? V.gx()[(long long)N * nx + tid] : V.bcl()[tid];
+    v0[tid] = d;
+    if (!BWD) V.dx()[nx + tid] = d;
+  }
+  if (wave > 0 && n > 0) load(0);
+  __syncthreads();
+  double* out = BWD ? V.pv() : V.dx();
+  for (int c = 0, s = 0; c * CK < n; ++c) {
+    if (wave == 0) {
+      const double* b = (c & 1) ? buf1 : buf0;
+      const int cnt = (n - c * CK) < CK ? (n - c * CK) : CK;
+      for (int j = 0; j < cnt; ++j, ++s) {
+        const double* M = b + j * SS;
+        const double* vin = (s & 1) ? v1 : v0;
+        double* vout = (s & 1) ? v0 : v1;
+        const int k = BWD ? N - 1 - s : 1 + s;
+        if (tid < nx) {
+          double acc = M[nxx + tid];
+#pragma unroll 8
+          for (int cc = 0; cc < nx; ++cc) acc = fma(M[cc * nx + tid], vin[cc], acc);
+          vout[tid] = acc;
+          out[(long long)(BWD ? k : k + 1) * nx + tid] = acc;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    } else if ((c + 1) * CK < n) {
+      load(c + 1);
+    }
+    lds_barrier();
+  }
+  __syncthreads();  // wave 0's stores of the outputs visible to the workgroup (the LDS-only barriers above do not wait)
 }

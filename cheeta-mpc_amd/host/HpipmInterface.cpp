@@ -175,20 +175,24 @@ class HpipmInterface::Impl {
     }
     if (verbose) printStatus(status, iters);
     riccatiValid_ = false;
+    ricFb_ = false;
     if (!finite) return hpipm_status::NAN_SOL;
     return (hpipm_status)status;
   }
 
   // Riccati quantities of the last solve (cmpc_ocp_riccati: factorisation at the returned point), fetched once per
-  // solve; stage 0 rebuilt from (dynamics0, cost0) as the reference does (HpipmInterface.cpp:334-347, 376-389, 416-453)
-  void riccati(const VectorFunctionLinearApproximation& dyn0, const ScalarFunctionQuadraticApproximation& cost0) {
+  // solve; stage 0 rebuilt from (dynamics0, cost0) as the reference does (HpipmInterface.cpp:334-347, 376-389, 416-453).
+  // all = false (getRiccatiFeedback, the MPC's per-tick call): K, Lr and P_1 only (cmpc_ocp_riccati_feedback_host,
+  // copies of what the solve kept); all = true: every quantity (cmpc_ocp_riccati_host).
+  void riccati(const VectorFunctionLinearApproximation& dyn0, const ScalarFunctionQuadraticApproximation& cost0,
+               bool all) {
     const Packed& p = last_;
     const int N = p.N;
     if (N == 0 || !ocp_) throw std::runtime_error("[HpipmInterface] no solved problem to take Riccati quantities from");
     if ((int)dyn0.dfdx.rows() != p.nxk[1] || (int)dyn0.dfdx.cols() != p.nxk[0] || (int)dyn0.dfdu.cols() != p.nu[0] ||
         (int)cost0.dfdxx.rows() != p.nxk[0])
       throw std::runtime_error("[HpipmInterface] dynamics0 / cost0 do not match the last solved problem");
-    if (!riccatiValid_) {
+    if (!riccatiValid_ && !(ricFb_ && !all)) {
       const int nx = p.nx;
       int nU = 0, nK = 0, nM = 0;
       for (int v : p.nu) {
@@ -202,27 +206,40 @@ class HpipmInterface::Impl {
       k_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
       Lr_.assign((size_t)(nM > 0 ? nM : 1), 0.0);
       int st = -1;
-      const int r = cmpc_ocp_riccati_host(ocp_, 1, Pm_.data(), pv_.data(), K_.data(), k_.data(), Lr_.data(), &st);
+      const int r = all ? cmpc_ocp_riccati_host(ocp_, 1, Pm_.data(), pv_.data(), K_.data(), k_.data(), Lr_.data(), &st)
+                        : cmpc_ocp_riccati_feedback_host(ocp_, 0, K_.data(), Lr_.data(), Pm_.data() + (size_t)nx * nx,
+                                                         &st);
       if (r != CMPC_OK)
         throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
       if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati factorisation: NaN pivot");
       if (minEig_ > 0.0) clampFactors(nx);
-      riccatiValid_ = true;
+      if (all) riccatiValid_ = true;
+      ricFb_ = true;
     }
-    stage0(dyn0, cost0);
+    stage0(dyn0, cost0, all || riccatiValid_);
   }
 
   int allocations() const { return ocp_ ? cmpc_ocp_alloc_count(ocp_) : -1; }
+  void enableTiming(bool on) {
+    timing_ = on;
+    if (ocp_) (void)cmpc_ocp_enable_timing(ocp_, on ? 1 : 0);
+  }
+  double lastSolveMs() const {
+    float ms = 0.f;
+    if (!ocp_ || !timing_ || cmpc_ocp_last_solve_ms(ocp_, &ms) != CMPC_OK) return NAN;
+    return ms;
+  }
 
   void setMinimumEigenvalue(double v) {
     if (!(v >= 0.0)) throw std::invalid_argument("[HpipmInterface] minimum eigenvalue must be >= 0");
     minEig_ = v;
     riccatiValid_ = false;
+    ricFb_ = false;
   }
 
   std::vector<ScalarFunctionQuadraticApproximation> costToGo(const VectorFunctionLinearApproximation& d0,
                                                               const ScalarFunctionQuadraticApproximation& c0) {
-    riccati(d0, c0);
+    riccati(d0, c0, true);
     const int N = last_.N, nx = last_.nx;
     std::vector<ScalarFunctionQuadraticApproximation> out((size_t)N + 1);
     for (int k = 0; k <= N; ++k) {  // node k's own nxk x nxk block of the padded P_k
@@ -238,7 +255,7 @@ class HpipmInterface::Impl {
     return out;
   }
   matrix_array_t feedback(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
-    riccati(d0, c0);
+    riccati(d0, c0, false);
     const int N = last_.N, nx = last_.nx;
     matrix_array_t out((size_t)N);
     size_t o = 0;
@@ -252,7 +269,7 @@ class HpipmInterface::Impl {
     return out;
   }
   vector_array_t feedforward(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
-    riccati(d0, c0);
+    riccati(d0, c0, true);
     const int N = last_.N;
     vector_array_t out((size_t)N);
     size_t o = 0;
@@ -284,6 +301,7 @@ class HpipmInterface::Impl {
       ocpNu_ = nu;
       ocpNc_ = nc;
       riccatiValid_ = false;
+      ricFb_ = false;
       return;
     }
     create(N, nx, nu, nc, defer_no_device);
@@ -315,6 +333,7 @@ class HpipmInterface::Impl {
     // the MPC reads the feedback policy of every solve (MultipleShootingSolver.cpp:337-341, useFeedbackPolicy): the
     // solve leaves its exit Riccati quantities, the getters copy them
     (void)cmpc_ocp_set_keep_riccati(ocp_, 1);
+    if (timing_) (void)cmpc_ocp_enable_timing(ocp_, 1);
     ocpN_ = N;
     ocpNx_ = nx;
     ocpNu_ = nu;
@@ -446,7 +465,9 @@ class HpipmInterface::Impl {
   // Lr_0 is the clamped factor when setRiccatiMinimumEigenvalue set a minimum (clampFactors, the reference's
   // LinearAlgebra::setTriangularMinimumEigenvalues(Lr0), :340, :379, :419); without one, the device factorisation's
   // pivot guard stands (a pivot <= 1e-200 gives a zero column, whose solves contribute 0).
-  void stage0(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0) {
+  // vectors = false (feedback only): K_0 alone (k_0, S_0, s_0 need p_1, not fetched)
+  void stage0(const VectorFunctionLinearApproximation& d0, const ScalarFunctionQuadraticApproximation& c0,
+              bool vectors) {
     const Packed& p = last_;
     const int nx = p.nx, x0n = p.nxk[0], x1n = p.nxk[1], m = p.nu[0];
     const double* P1 = Pm_.data() + (size_t)nx * nx;  // padded, column-major
@@ -503,6 +524,7 @@ class HpipmInterface::Impl {
     for (int a = 0; a < m; ++a) col[(size_t)a] = t2[(size_t)a];
     ltsolve(col.data(), 1);
     for (int a = 0; a < m; ++a) k0_[(size_t)a] = -col[(size_t)a];
+    if (!vectors) return;
     S0_.assign((size_t)x0n * x0n, 0.0);
     s0_.assign((size_t)x0n, 0.0);
     for (int i = 0; i < x0n; ++i) {
@@ -553,8 +575,10 @@ class HpipmInterface::Impl {
   int ocpN_ = 0, ocpNx_ = 0;
   std::vector<int> ocpNu_, ocpNc_;
   Packed last_;
-  bool riccatiValid_ = false;
+  bool riccatiValid_ = false;  // every Riccati quantity of the last solve fetched
+  bool ricFb_ = false;         // K, Lr, P_1 fetched
   double minEig_ = 0.0;  // setRiccatiMinimumEigenvalue (0: no clamp)
+  bool timing_ = false;  // enableDeviceTiming
   std::vector<double> xbuf_, ubuf_, recbuf_, crecbuf_, x0buf_, Pm_, pv_, K_, k_, Lr_, K0_, k0_, S0_, s0_;
 };
 
@@ -581,5 +605,7 @@ vector_array_t HpipmInterface::getRiccatiFeedforward(const VectorFunctionLinearA
 }
 void HpipmInterface::setRiccatiMinimumEigenvalue(double minEigenValue) { pImpl_->setMinimumEigenvalue(minEigenValue); }
 int HpipmInterface::deviceAllocations() const { return pImpl_->allocations(); }
+void HpipmInterface::enableDeviceTiming(bool on) { pImpl_->enableTiming(on); }
+double HpipmInterface::lastSolveDeviceMs() const { return pImpl_->lastSolveMs(); }
 
 }  // namespace ocs2

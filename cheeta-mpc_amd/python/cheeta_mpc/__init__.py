@@ -133,6 +133,7 @@ def lib():
     L.cmpc_ocp_solve_host.argtypes = [vp, C.c_int, d, d, d, d, d, i, i]
     L.cmpc_ocp_riccati.argtypes = [vp, C.c_int, d, d, d, d, d, i, vp]
     L.cmpc_ocp_riccati_host.argtypes = [vp, C.c_int, d, d, d, d, d, i]
+    L.cmpc_ocp_riccati_feedback_host.argtypes = [vp, C.c_int, d, d, d, i]
     L.cmpc_ocp_get_residuals.argtypes = [vp, C.c_int, d, vp]
     L.cmpc_ocp_stat_rows.argtypes = [vp]
     L.cmpc_ocp_get_stats.argtypes = [vp, C.c_int, d, vp]
@@ -637,6 +638,24 @@ class OcpSolver:
             ks.append(kk)
             Ms.append(mb)
         return (P.reshape(B, N + 1, nx, nx).transpose(0, 1, 3, 2).copy(), p.reshape(B, N + 1, nx), Ks, ks, Ms, st)
+
+    def riccati_feedback(self, b=0):
+        """cmpc_ocp_riccati_feedback_host of problem b: K (list of nu_k x nx), Lr (list, lower), P_1 [nx, nx], status."""
+        N, nx = self.N, self.nx
+        K = np.zeros(max(self.nK, 1))
+        M = np.zeros(max(self.nM, 1))
+        P1 = np.zeros(nx * nx)
+        st = np.zeros(1, np.int32)
+        _chk(lib().cmpc_ocp_riccati_feedback_host(self.h, b, _dp(K), _dp(M), _dp(P1), _dp(st)),
+             "cmpc_ocp_riccati_feedback_host")
+        Ks, Ms, o, om = [], [], 0, 0
+        for s in range(N):
+            m = int(self.nu[s])
+            Ks.append(K[o:o + m * nx].reshape(nx, m).T.copy())
+            Ms.append(M[om:om + m * m].reshape(m, m).T.copy())
+            o += m * nx
+            om += m * m
+        return Ks, Ms, P1.reshape(nx, nx).T.copy(), int(st[0])
 
     def residuals(self, B):
         d = DeviceArray((B, 4), np.float64)

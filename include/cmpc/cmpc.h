@@ -385,6 +385,13 @@ int cmpc_ocp_riccati(cmpc_ocp* ocp, int B, double* d_P, double* d_p, double* d_K
                      int* d_status, void* stream);
 int cmpc_ocp_riccati_host(cmpc_ocp* ocp, int B, double* P, double* p, double* K, double* k, double* Lr,
                           int* status);
+/* The MPC tick's part (HpipmInterface::getRiccatiFeedback, HpipmInterface.cpp:330-362): of problem b, K [sum nu_k*nx]
+ * and Lr [sum nu_k^2] of every stage and P_1 [nx*nx] (for the stage-0 rebuild), host buffers, synchronous. With
+ * cmpc_ocp_set_keep_riccati on a grid-form solve these are copies of what the solve kept (without rows the solve
+ * keeps only P_k, K_k, Lr_k — its last factorisation is the exit point's — and cmpc_ocp_riccati refactorises when the
+ * vectors are asked for); otherwise problems 0..b are refactorised first (as cmpc_ocp_riccati). K_0 here is the
+ * factorisation's stage-0 gain. status: 0, or 3. */
+int cmpc_ocp_riccati_feedback_host(cmpc_ocp* ocp, int b, double* K, double* Lr, double* P1, int* status);
 /* Final residuals of the last solve, d_res [B][4] = (max |r_stat|, |r_eq|, |r_ineq|, max t lam) as
  * d_ocp_qp_ipm_get_max_res_stat / _eq / _ineq / _comp (HpipmInterface.cpp:478-485); per-iteration statistics
  * d_stats [B][rows][CMPC_STAT_COLS] (rows = iter_max + 1 of the settings at create / set_settings; the columns of

@@ -103,6 +103,10 @@ class HpipmInterface {
   void setRiccatiMinimumEigenvalue(double minEigenValue);
   /* Device allocations the interface's handle has made so far (cmpc_ocp_alloc_count; -1 without a handle). */
   int deviceAllocations() const;
+  /* Extensions for timing the tick: HIP events around every solve's kernel (cmpc_ocp_enable_timing), and the last
+   * solve's kernel time in ms (cmpc_ocp_last_solve_ms; NaN without a handle or with timing off). */
+  void enableDeviceTiming(bool on);
+  double lastSolveDeviceMs() const;
 
  private:
   class Impl;

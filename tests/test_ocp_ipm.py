@@ -637,6 +637,37 @@ def test_device_keep_riccati_equals_refactorisation(cm, op, projected):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_riccati_feedback_equals_full(cm, op, projected):
+    """cmpc_ocp_riccati_feedback_host (the MPC tick's getRiccatiFeedback part: K, Lr of every stage, P_1): copies of
+    what a keep_riccati solve left — without rows the solve keeps its last factorisation only — equal to the full
+    cmpc_ocp_riccati (which refactorises without rows) to rounding, and the same from a solve that kept nothing."""
+    p = ocpgen.legged_problem(330, projected=projected)
+    rec, crec = ocpgen.pack(p)
+    res = []
+    for keep in (1, 0):
+        h = cm.OcpSolver(p["N"], p["nx"], p["nu"], p.get("nc"), max_batch=1)
+        h.set_keep_riccati(keep)
+        x, u, st, it = h.solve(p["x0"][None], rec[None], crec[None] if crec is not None else None)
+        assert st[0] == 0
+        fb = h.riccati_feedback(0)
+        full = h.riccati(1)
+        res.append((fb, full))
+        h.close()
+    tS = 1e-4 if not projected else 1e-9
+    for (K, M, P1, s), (P, pv, Kf, kf, Mf, rst) in res:
+        assert s == 0 and rst[0] == 0
+        assert _rel(P1, P[0][1]) < tS
+        for k in range(1, p["N"]):
+            assert _rel(K[k], Kf[0][k]) < tS and _rel(M[k], Mf[0][k]) < tS, k
+    (K1, M1, P11, _), _ = res[0]
+    (K0, M0, P10, _), _ = res[1]
+    assert _rel(P11, P10) < tS
+    for k in range(p["N"]):
+        assert _rel(K1[k], K0[k]) < tS and _rel(M1[k], M0[k]) < tS, k
+
+
+@pytest.mark.gpu
 def test_device_reshape_ticks_allocate_nothing(cm, op):
     """The MPC tick on one handle (HpipmInterface::resize + solve + getRiccatiFeedback, MultipleShootingSolver.cpp:276,
     :337-341): 50 ticks of the legged problem with the event nodes moving as the gait advances (N 70 / 71, the inputs
