@@ -1165,7 +1165,7 @@ __device__ __forceinline__ void ldl_solve(const double* __restrict__ F, int m, c
 // LDS of the latency form: G images (two), T, Paug, the pivot-column buffers and the rows' Sigma (two), then red and
 // vec; the other passes of the kernel see G0 / G1 as ABx / Tx (contiguous: the staged residuals' buffer)
 __device__ __forceinline__ Lds carve_fast(double* smem, const OcpLayout& L, ChainLds& C) {
-  const int ngr = CH_NRP + L.ngmax, ngp = (L.ngmax + 2) & ~1;
+  const int ngr = CH_NRP + ((L.ngmax + 3) & ~3), ngp = (L.ngmax + 4) & ~3;  // rows in groups of four (chain_m)
   const int g1 = ngr * CH_GS > CH_MAXU * CH_FS ? ngr * CH_GS : CH_MAXU * CH_FS;
   C.G0 = smem;
   C.G1 = C.G0 + ngr * CH_GS;
@@ -2276,7 +2276,7 @@ size_t ocp_chain_lds_bytes(const OcpLayout& L, int numax) {
   if (L.nzp != 64 || L.nx > OCP_CHAIN_MAX_NX || numax > OCP_CHAIN_MAX_NU || L.nx + numax + 1 > OCP_CHAIN_MAX_N1 ||
       L.ngmax > CH_MAXG || L.N > CH_MAXN)
     return 0;
-  const size_t ngr = CH_NRP + (size_t)L.ngmax, ngp = (size_t)((L.ngmax + 2) & ~1);
+  const size_t ngr = CH_NRP + (size_t)((L.ngmax + 3) & ~3), ngp = (size_t)((L.ngmax + 4) & ~3);
   const size_t g1 = std::max(ngr * CH_GS, (size_t)CH_MAXU * CH_FS);
   const size_t d = ngr * CH_GS + g1 + (size_t)CH_NRP * CH_GS + CH_PS * CH_PS + 256 + 2 * ngp + 64 + 128 +
                    (size_t)CH_MR * CH_GS + 4 * CH_MAXNT + 64 + CH_PS * CH_PS + (size_t)CH_MAXU * CH_FS;

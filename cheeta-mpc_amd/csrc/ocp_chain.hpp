@@ -147,10 +147,10 @@ __device__ __forceinline__ void chain_load(const View& V, const int* d, int k, c
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int c = c0 + 12 * q;
-      if (r < g && c < w) G[(CH_NRP + r) * CH_GS + c] = c < nz ? cv[q] : 0.0;
+      if (r < ((g + 3) & ~3) && c < w) G[(CH_NRP + r) * CH_GS + c] = (r < g && c < nz) ? cv[q] : 0.0;
     }
   }
-  if (t < g) S.sg0[t] = sv;
+  if (t < ((g + 3) & ~3)) S.sg0[t] = t < g ? sv : 0.0;
   if (t < w) S.gb[t] = t < nz ? gg : 0.0;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
@@ -208,33 +208,50 @@ __device__ __forceinline__ void chain_m(const ChainLds& S, int nx, const int* d,
     m[r][1][0] = h1.x + (2 * bi[r] + 1 == nz ? gr.x : 0.0);
     m[r][1][1] = h1.y + (2 * bi[r] + 1 == nz ? gr.y : 0.0);
   }
-#pragma unroll 5
-  for (int s = 0; s < np1; ++s) {
-    const double* gr = G + s * CH_GS;
-    const double* tr = S.T + s * CH_GS;
+  // groups of four rows, every load of a group issued before its fmas (the image's rows np1 .. np1 rounded up to 4
+  // are zero, so are the rows' block's rows g .. g rounded up to 4 and their Sigma)
+  const int np1r = (np1 + 3) & ~3, g4 = (g + 3) & ~3;
+  for (int s = 0; s < np1r; s += 4) {
+    d2v gv[4][NS], tv[4][NS];
 #pragma unroll
-    for (int r = 0; r < NS; ++r) {
-      const d2v gv = *(const d2v*)(gr + 2 * bi[r]);
-      const d2v tv = *(const d2v*)(tr + 2 * bj[r]);
-      m[r][0][0] = fma(gv.x, tv.x, m[r][0][0]);
-      m[r][0][1] = fma(gv.x, tv.y, m[r][0][1]);
-      m[r][1][0] = fma(gv.y, tv.x, m[r][1][0]);
-      m[r][1][1] = fma(gv.y, tv.y, m[r][1][1]);
-    }
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        gv[u][r] = *(const d2v*)(G + (s + u) * CH_GS + 2 * bi[r]);
+        tv[u][r] = *(const d2v*)(S.T + (s + u) * CH_GS + 2 * bj[r]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        m[r][0][0] = fma(gv[u][r].x, tv[u][r].x, m[r][0][0]);
+        m[r][0][1] = fma(gv[u][r].x, tv[u][r].y, m[r][0][1]);
+        m[r][1][0] = fma(gv[u][r].y, tv[u][r].x, m[r][1][0]);
+        m[r][1][1] = fma(gv[u][r].y, tv[u][r].y, m[r][1][1]);
+      }
   }
-  for (int s = 0; s < g; ++s) {
-    const double sgs = S.sg0[s];
-    const double* gr = G + (CH_NRP + s) * CH_GS;
+  for (int s = 0; s < g4; s += 4) {
+    d2v gv[4][NS], hv[4][NS];
+    double sgs[4];
 #pragma unroll
-    for (int r = 0; r < NS; ++r) {
-      const d2v gv = *(const d2v*)(gr + 2 * bi[r]);
-      const d2v hv = *(const d2v*)(gr + 2 * bj[r]);
-      const double u0 = sgs * hv.x, u1 = sgs * hv.y;
-      m[r][0][0] = fma(gv.x, u0, m[r][0][0]);
-      m[r][0][1] = fma(gv.x, u1, m[r][0][1]);
-      m[r][1][0] = fma(gv.y, u0, m[r][1][0]);
-      m[r][1][1] = fma(gv.y, u1, m[r][1][1]);
+    for (int u = 0; u < 4; ++u) {
+      sgs[u] = S.sg0[s + u];
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        gv[u][r] = *(const d2v*)(G + (CH_NRP + s + u) * CH_GS + 2 * bi[r]);
+        hv[u][r] = *(const d2v*)(G + (CH_NRP + s + u) * CH_GS + 2 * bj[r]);
+      }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        const double u0 = sgs[u] * hv[u][r].x, u1 = sgs[u] * hv[u][r].y;
+        m[r][0][0] = fma(gv[u][r].x, u0, m[r][0][0]);
+        m[r][0][1] = fma(gv[u][r].x, u1, m[r][0][1]);
+        m[r][1][0] = fma(gv[u][r].y, u0, m[r][1][0]);
+        m[r][1][1] = fma(gv[u][r].y, u1, m[r][1][1]);
+      }
   }
 #pragma unroll
   for (int r = 0; r < NS; ++r) {
@@ -305,6 +322,127 @@ __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&b
   __builtin_amdgcn_wave_barrier();
 }
 
+// A quad round of (C): pivots j .. j + 3 (j = 4 jb) in one publish — the whole block column jb — computing exactly
+// what the two pair rounds (j, j + 1) and (j + 2, j + 3) compute: every lane forms the second pair's columns for its
+// own rows and columns from the published pre-round values with the owners' fma sequence, and applies the two rank-2
+// updates in the same order, so the results are bit-identical with half the publish / read-back latency chains.
+template <int NB>
+__device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&bi)[NB], const int (&bj)[NB],
+                                             const bool (&on)[NB], int j, int n1, double* cb, double* F, bool& bad) {
+  const int lane = threadIdx.x, jb = j >> 2;
+  double* c0 = cb;
+  double* c1 = cb + 64;
+  double* c2 = cb + 128;
+  double* c3 = cb + 192;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (on[q] && bj[q] == jb) {
+      const int o = 4 * bi[q];
+      *(d2v*)(c0 + o) = d2v{m[q][0][0], m[q][1][0]};
+      *(d2v*)(c0 + o + 2) = d2v{m[q][2][0], m[q][3][0]};
+      *(d2v*)(c1 + o) = d2v{m[q][0][1], m[q][1][1]};
+      *(d2v*)(c1 + o + 2) = d2v{m[q][2][1], m[q][3][1]};
+      *(d2v*)(c2 + o) = d2v{m[q][0][2], m[q][1][2]};
+      *(d2v*)(c2 + o + 2) = d2v{m[q][2][2], m[q][3][2]};
+      *(d2v*)(c3 + o) = d2v{m[q][0][3], m[q][1][3]};
+      *(d2v*)(c3 + o + 2) = d2v{m[q][2][3], m[q][3][3]};
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // the pivot block (rows j .. j + 3 of the four columns)
+  const d2v q0a = *(const d2v*)(c0 + j), q0b = *(const d2v*)(c0 + j + 2);
+  const d2v q1b = *(const d2v*)(c1 + j), q1c = *(const d2v*)(c1 + j + 2);
+  const d2v q2b = *(const d2v*)(c2 + j + 2), q3b = *(const d2v*)(c3 + j + 2);
+  // first pair, as chain_round
+  const double d0 = q0a.x, a1 = q0a.y, e1 = q1b.y;
+  bad = bad || (d0 != d0);
+  const double d0i = d0 > 1e-200 ? 1.0 / d0 : 0.0;
+  const double l1 = a1 * d0i;
+  const double d1 = fma(-a1, l1, e1);
+  bad = bad || (d1 != d1);
+  const double d1i = d1 > 1e-200 ? 1.0 / d1 : 0.0;
+  // the first pair's row / column vectors at index y (published pre-round values c0_y, c1_y)
+  auto u_of = [&](double x0) { return -x0 * d0i; };
+  auto p_of = [&](double x0, double x1) { return fma(-x0, l1, x1); };
+  // pivots j + 2, j + 3 after the first pair's update (entries (j+2, j+2), (j+3, j+2), (j+3, j+3))
+  const double cl2 = q0b.x, cl3 = q0b.y;                       // c0 at j + 2, j + 3
+  const double bl2 = p_of(q0b.x, q1c.x), bl3 = p_of(q0b.y, q1c.y);  // c1~ at j + 2, j + 3
+  const double u2 = u_of(q0b.x), u3 = u_of(q0b.y);
+  const double v2 = -bl2 * d1i, v3 = -bl3 * d1i;
+  const double e2 = fma(v2, bl2, fma(u2, cl2, q2b.x));  // M'(j+2, j+2)
+  const double a3 = fma(v3, bl2, fma(u3, cl2, q2b.y));  // M'(j+3, j+2)
+  const double e3 = fma(v3, bl3, fma(u3, cl3, q3b.y));  // M'(j+3, j+3)
+  bad = bad || (e2 != e2);
+  const double d2i = e2 > 1e-200 ? 1.0 / e2 : 0.0;
+  const double l3 = a3 * d2i;
+  const double d3 = fma(-a3, l3, e3);
+  bad = bad || (d3 != d3);
+  const double d3i = d3 > 1e-200 ? 1.0 / d3 : 0.0;
+  // the factor's columns j .. j + 3 (rows >= j): c0, c1~, the updated column j + 2 and its c~ for j + 3
+  if (lane >= j && lane < n1) {
+    const double x0 = c0[lane], x1 = c1[lane], x2 = c2[lane], x3 = c3[lane];
+    const double u = u_of(x0), pp = p_of(x0, x1), v = -pp * d1i;
+    const double y2 = fma(v, bl2, fma(u, cl2, x2)), y3 = fma(v, bl3, fma(u, cl3, x3));
+    F[j * CH_FS + lane] = x0;
+    F[(j + 1) * CH_FS + lane] = pp;
+    F[(j + 2) * CH_FS + lane] = y2;
+    F[(j + 3) * CH_FS + lane] = fma(-y2, l3, y3);
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    double x0[8], x1[8], x2[8], x3[8];
+    {
+      const int oi = 4 * bi[q], ol = 4 * bj[q];
+      const d2v r0a = *(const d2v*)(c0 + oi), r0b = *(const d2v*)(c0 + oi + 2);
+      const d2v r1a = *(const d2v*)(c1 + oi), r1b = *(const d2v*)(c1 + oi + 2);
+      const d2v r2a = *(const d2v*)(c2 + oi), r2b = *(const d2v*)(c2 + oi + 2);
+      const d2v r3a = *(const d2v*)(c3 + oi), r3b = *(const d2v*)(c3 + oi + 2);
+      const d2v s0a = *(const d2v*)(c0 + ol), s0b = *(const d2v*)(c0 + ol + 2);
+      const d2v s1a = *(const d2v*)(c1 + ol), s1b = *(const d2v*)(c1 + ol + 2);
+      const d2v s2a = *(const d2v*)(c2 + ol), s2b = *(const d2v*)(c2 + ol + 2);
+      const d2v s3a = *(const d2v*)(c3 + ol), s3b = *(const d2v*)(c3 + ol + 2);
+      const double t0[8] = {r0a.x, r0a.y, r0b.x, r0b.y, s0a.x, s0a.y, s0b.x, s0b.y};
+      const double t1[8] = {r1a.x, r1a.y, r1b.x, r1b.y, s1a.x, s1a.y, s1b.x, s1b.y};
+      const double t2[8] = {r2a.x, r2a.y, r2b.x, r2b.y, s2a.x, s2a.y, s2b.x, s2b.y};
+      const double t3[8] = {r3a.x, r3a.y, r3b.x, r3b.y, s3a.x, s3a.y, s3b.x, s3b.y};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        x0[t] = t0[t];
+        x1[t] = t1[t];
+        x2[t] = t2[t];
+        x3[t] = t3[t];
+      }
+    }
+    // first pair: u (rows), c0 (columns), v (rows), c1~ (columns); second pair from the updated columns 2, 3
+    double ui[4], cl[4], vi[4], bl[4], ui2[4], cl2v[4], vi2[4], bl2v[4];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const double u = u_of(x0[t]), pp = p_of(x0[t], x1[t]), v = -pp * d1i;
+      const double y2 = fma(v, bl2, fma(u, cl2, x2[t])), y3 = fma(v, bl3, fma(u, cl3, x3[t]));
+      const double pp2 = fma(-y2, l3, y3);
+      if (t < 4) {
+        ui[t] = u;
+        vi[t] = v;
+        ui2[t] = -y2 * d2i;
+        vi2[t] = -pp2 * d3i;
+      } else {
+        cl[t - 4] = x0[t];
+        bl[t - 4] = pp;
+        cl2v[t - 4] = y2;
+        bl2v[t - 4] = pp2;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const double w = fma(vi[a], bl[b], fma(ui[a], cl[b], m[q][a][b]));
+        m[q][a][b] = fma(vi2[a], bl2v[b], fma(ui2[a], cl2v[b], w));
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // (C) on wave 0: NB 4 x 4 lower blocks of M per lane (block beta = lane + 64 q), the pair rounds, the outputs.
 // Returns the NaN flag of the pivots.
 template <int NB>
@@ -341,8 +479,12 @@ __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, con
   double* c1 = S.C + 64;
   OCP_STAMP(27);
   for (int j = 0; j < mk; j += 4) {
-    chain_round<NB, 0>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad);
-    if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad);
+    if (j + 4 <= mk) {
+      chain_round4<NB>(m, bi, bj, on, j, n1, S.C, F, bad);
+    } else {
+      chain_round<NB, 0>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad);
+      if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad);
+    }
   }
   OCP_STAMP(23);
   // --- Paug of node k straight from the registers: the live entries (rows / columns >= nu_k, lower triangle of the
@@ -435,6 +577,11 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
       S.Pa2[e] = 0.0;
     }
   }
+  // the image's rows and T's rows np1 .. CH_NRP stay zero (the T and M loops run over rows in groups of four)
+  for (int e = tid; e < (CH_NRP - np1) * CH_GS; e += NT) {
+    S.G0[np1 * CH_GS + e] = 0.0;
+    S.T[np1 * CH_GS + e] = 0.0;
+  }
   __syncthreads();  // descriptors
   if (wave > 0) chain_load(V, S.desc + CH_DESC * (N - 1), N - 1, hp, S, nullptr, nullptr, nullptr);
   __syncthreads();
@@ -456,22 +603,31 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
       const double* pa0 = PaR + 2 * rp0;
       const double* gc0 = G + 2 * cp0;
       double t0[4] = {0.0, 0.0, 0.0, 0.0};
+      const int np1r = (np1 + 3) & ~3;  // Paug's pad columns and the image's rows up to np1r are zero
       if (items > NT) {  // uniform: two items per thread
         const double* pa1 = PaR + 2 * rp1;
         const double* gc1 = G + 2 * cp1;
         double t1[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 5
-        for (int s = 0; s < np1; ++s) {
-          const d2v p0 = *(const d2v*)(pa0 + s * CH_PS), g0 = *(const d2v*)(gc0 + s * CH_GS);
-          const d2v p1 = *(const d2v*)(pa1 + s * CH_PS), g1 = *(const d2v*)(gc1 + s * CH_GS);
-          t0[0] = fma(p0.x, g0.x, t0[0]);
-          t0[1] = fma(p0.x, g0.y, t0[1]);
-          t0[2] = fma(p0.y, g0.x, t0[2]);
-          t0[3] = fma(p0.y, g0.y, t0[3]);
-          t1[0] = fma(p1.x, g1.x, t1[0]);
-          t1[1] = fma(p1.x, g1.y, t1[1]);
-          t1[2] = fma(p1.y, g1.x, t1[2]);
-          t1[3] = fma(p1.y, g1.y, t1[3]);
+        for (int s = 0; s < np1r; s += 4) {
+          d2v p0[4], g0[4], p1[4], g1[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            p0[u] = *(const d2v*)(pa0 + (s + u) * CH_PS);
+            g0[u] = *(const d2v*)(gc0 + (s + u) * CH_GS);
+            p1[u] = *(const d2v*)(pa1 + (s + u) * CH_PS);
+            g1[u] = *(const d2v*)(gc1 + (s + u) * CH_GS);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            t0[0] = fma(p0[u].x, g0[u].x, t0[0]);
+            t0[1] = fma(p0[u].x, g0[u].y, t0[1]);
+            t0[2] = fma(p0[u].y, g0[u].x, t0[2]);
+            t0[3] = fma(p0[u].y, g0[u].y, t0[3]);
+            t1[0] = fma(p1[u].x, g1[u].x, t1[0]);
+            t1[1] = fma(p1[u].x, g1[u].y, t1[1]);
+            t1[2] = fma(p1[u].y, g1[u].x, t1[2]);
+            t1[3] = fma(p1[u].y, g1[u].y, t1[3]);
+          }
         }
         if (w1 < items) {
           double* t = S.T + (2 * rp1) * CH_GS + 2 * cp1;
@@ -479,13 +635,20 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
           *(d2v*)(t + CH_GS) = d2v{t1[2], t1[3]};
         }
       } else {
-#pragma unroll 5
-        for (int s = 0; s < np1; ++s) {
-          const d2v p0 = *(const d2v*)(pa0 + s * CH_PS), g0 = *(const d2v*)(gc0 + s * CH_GS);
-          t0[0] = fma(p0.x, g0.x, t0[0]);
-          t0[1] = fma(p0.x, g0.y, t0[1]);
-          t0[2] = fma(p0.y, g0.x, t0[2]);
-          t0[3] = fma(p0.y, g0.y, t0[3]);
+        for (int s = 0; s < np1r; s += 4) {
+          d2v p0[4], g0[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            p0[u] = *(const d2v*)(pa0 + (s + u) * CH_PS);
+            g0[u] = *(const d2v*)(gc0 + (s + u) * CH_GS);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            t0[0] = fma(p0[u].x, g0[u].x, t0[0]);
+            t0[1] = fma(p0[u].x, g0[u].y, t0[1]);
+            t0[2] = fma(p0[u].y, g0[u].x, t0[2]);
+            t0[3] = fma(p0[u].y, g0[u].y, t0[3]);
+          }
         }
       }
       if (w0 < items) {
