@@ -490,6 +490,41 @@ __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, con
   // --- Paug of node k straight from the registers: the live entries (rows / columns >= nu_k, lower triangle of the
   // blocks) and their mirror into PaW (global P_k, p_k: chain_out on the helper waves, a stage later); the other
   // entries' stores go to a dummy slot, so the stores need no branch ---
+  if ((mk & 1) == 0 && ((n1 + 3) & ~3) - mk <= CH_PS) {
+    // nu_k even: every live pair of columns of a block is a 16-byte piece of a Paug row; each block writes its live
+    // rows and, mirrored, its live columns in such pieces (diagonal blocks from their lower triangle, so Paug stays
+    // exactly symmetric); the entries past n1 are written as zeros (Paug's pad rows / columns stay zero)
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (!on[q] || 4 * bj[q] + 4 <= mk) continue;
+      const int I0 = 4 * bi[q] - mk, J0 = 4 * bj[q] - mk;
+      const bool diag = bi[q] == bj[q];
+      double w[4][4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const double v = (diag && a < b) ? m[q][b][a] : m[q][a][b];
+          const int I = I0 + a, J = J0 + b;
+          w[a][b] = (I > nx || J > nx || (I == nx && J == nx)) ? 0.0 : v;
+        }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        if (I0 + a < 0) continue;
+        if (J0 >= 0) *(d2v*)(PaW + (I0 + a) * CH_PS + J0) = d2v{w[a][0], w[a][1]};
+        *(d2v*)(PaW + (I0 + a) * CH_PS + J0 + 2) = d2v{w[a][2], w[a][3]};
+      }
+      if (!diag) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (J0 + b < 0) continue;
+          if (I0 >= 0) *(d2v*)(PaW + (J0 + b) * CH_PS + I0) = d2v{w[0][b], w[1][b]};
+          *(d2v*)(PaW + (J0 + b) * CH_PS + I0 + 2) = d2v{w[2][b], w[3][b]};
+        }
+      }
+    }
+    return bad;
+  }
   double* dummy = S.C + 128 + lane;  // one slot per lane: a shared one would serialise the masked lanes' stores
 #pragma unroll
   for (int q = 0; q < NB; ++q)

@@ -589,6 +589,21 @@ class OcpSolver:
         _chk(lib().cmpc_ocp_last_solve_ms(self.h, C.byref(ms)), "cmpc_ocp_last_solve_ms")
         return float(ms.value)
 
+    def staging(self):
+        """numpy views of the handle's pinned staging (cmpc_ocp_staging): x0 [max_batch, nx], rec [max_batch,
+        rec_size], crec [max_batch, crec_size] or None; a solve whose inputs are these views copies nothing on the host
+        (the records are written in place, as the C++ mirror packs them). None when the handle has no staging."""
+        out = []
+        for which, n in ((0, self.nx), (1, self.rec_size), (2, self.crec_size if self.m else 0)):
+            if n == 0:
+                out.append(None)
+                continue
+            ptr = lib().cmpc_ocp_staging(self.h, which)
+            if not ptr:
+                return None
+            out.append(np.ctypeslib.as_array(ptr, shape=(self.max_batch * n,)).reshape(self.max_batch, n))
+        return tuple(out)
+
     def solve(self, x0, rec, crec=None, guess=None):
         """Host path (cmpc_ocp_solve_host): x0 [B,nx], rec [B,rec_size], crec [B,crec_size]; guess = (x, u), the
         initial guess read when the settings' warm_start is set. Returns x [B,N+1,nx], u [B,nU], status [B], iters."""
