@@ -162,7 +162,18 @@ def ocp_main(args):
     ach = flops / (kernel_ms * 1e-3)
     okey = f"ocp_{args.ocp}_B{B}"
     traffic, traffic_src = pmc_traffic(os.path.join(ROOT, "profiles", f"traffic_{okey}.json"), "k_ocp")
-    tick = ocp_tick(gen, projected) if rank == 0 else None
+    tick = ocp_tick(gen, projected) if rank == 0 and not args.no_tick else None
+    sq, sq_src = pmc_sq(okey, "k_ocp")
+    sq_line = {"source": sq_src}
+    if sq:
+        w = sq.get("SQ_WAVE_CYCLES", 0.0)
+        sq_line.update({
+            "valu_active_per_wave_cycle": sq.get("SQ_ACTIVE_INST_VALU", 0.0) / w if w else None,
+            "waitcnt_frac": sq.get("SQ_WAIT_ANY", 0.0) / w if w else None,
+            "issue_stall_frac": sq.get("SQ_WAIT_INST_ANY", 0.0) / w if w else None,
+            "valu_insts_per_wave": sq.get("SQ_INSTS_VALU", 0.0) / sq["SQ_WAVES"] if sq.get("SQ_WAVES") else None,
+            "lds_bank_conflict_per_lds_inst": (sq.get("SQ_LDS_BANK_CONFLICT", 0.0) / sq["SQ_INSTS_LDS"]
+                                               if sq.get("SQ_INSTS_LDS") else None)})
     value = world * B * args.steps / elapsed
     shape = (f"nx={p0['nx']}, N={p0['N']} (67 intervals + 3 event nodes), "
              + ("nu 10/12/0 projected, no rows" if projected else "nu 24/0 with 12-14 equality rows per node"))
@@ -185,6 +196,7 @@ def ocp_main(args):
                      "flops_counted": "ocp_flops (bench.py): Riccati factorisation, Newton solves and residuals per "
                                       "IPM iteration"},
         "tick": tick,
+        "sq_counters": sq_line,
         "solver": {"success_frac": float(ok.mean()), "mean_iters": iters_mean},
         "build": {"version": cm.lib().cmpc_version().decode(), "lib_md5": lib_md5()},
     }
@@ -499,6 +511,7 @@ def main():
     ap.add_argument("--ocp", choices=["projected", "rows"], default="",
                     help="benchmark the HpipmInterface::solve path (cmpc_ocp_solve) on ocs2_legged_robot-size OCP-QPs "
                          "instead of the centroidal headline; --batch problems per step")
+    ap.add_argument("--no-tick", action="store_true", help="--ocp: skip the C++ mirror tick line (counter passes)")
     ap.add_argument("--cadence", type=float, default=0.0, metavar="MS",
                     help="> 0: after the timed run, one step every MS milliseconds (20 = the MPC's 50 Hz, task.info:108) "
                          "for --cadence-calls calls, each synchronised; the per-call latency distribution is added to "

@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KEYS = ("k_solve64", "k_solve128", "k_ipm64", "k_ipm128x", "k_ipm_tiled", "k_condense64", "k_srbd_condense")
+KEYS = ("k_solve64", "k_solve128", "k_ipm64", "k_ipm128x", "k_ipm_tiled", "k_condense64", "k_srbd_condense", "k_ocp")
 
 
 def load(d):
