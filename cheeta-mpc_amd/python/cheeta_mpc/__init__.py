@@ -601,7 +601,8 @@ class OcpSolver:
             ptr = lib().cmpc_ocp_staging(self.h, which)
             if not ptr:
                 return None
-            out.append(np.ctypeslib.as_array(ptr, shape=(self.max_batch * n,)).reshape(self.max_batch, n))
+            arr = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_double)), shape=(self.max_batch * n,))
+            out.append(arr.reshape(self.max_batch, n))
         return tuple(out)
 
     def solve(self, x0, rec, crec=None, guess=None):
