@@ -59,8 +59,9 @@ def main():
     dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.split("\n")
     md5 = hashlib.md5(open(lib, "rb").read()).hexdigest()
     print(f"# llvm-readelf --notes of {os.path.basename(lib)} (md5 {md5}), gfx950 code objects: {len(rows)} kernels")
-    print("# vgpr = .vgpr_count (architected VGPRs), agpr = .agpr_count; the wave's allocation is their sum rounded")
-    print("# up to the allocation granule (512 = one wave per SIMD); spills = .vgpr_spill_count / .sgpr_spill_count")
+    print("# vgpr = .vgpr_count, agpr = .agpr_count (the notes' own fields); spills = .vgpr_spill_count /")
+    print("# .sgpr_spill_count; rocprofv3's VGPR_Count column is not this count (it reads 128 for k_solve64<double, 2>")
+    print("# at 253 here, 256 for k_ocp_grid at 436 / 180: profiles/r05_sq_*.txt 'resources')")
     print("# (SGPR spills go to VGPR lanes, not to memory); scratch = .private_segment_fixed_size bytes; lds = static")
     print(f"{'vgpr':>5} {'agpr':>5} {'sgpr':>5} {'vspill':>6} {'sspill':>6} {'scratch':>7} {'lds':>6}  kernel")
     for r, dn in sorted(zip(rows, dem), key=lambda t: t[1]):
