@@ -1219,7 +1219,7 @@ __device__ __forceinline__ GridRange grid_range(const OcpLayout& L, int g, int G
 }
 
 // Grid barrier of one problem's G workgroups (the hand-off recipe of the MI355X guide: every wave's stores drained,
-// lane-0 agent release, a relaxed agent-scope arrive on a counter zeroed before the launch, a relaxed poll with
+// lane-0 agent release, a relaxed agent-scope arrive on a counter that is zero at the launch, a relaxed poll with
 // s_sleep, one agent acquire). The spin is bounded: on a timeout (or another workgroup's) the problem's fail word is
 // set and every workgroup returns false at its next barrier, so the grid drains instead of hanging.
 __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, double* flag_lds) {
@@ -1785,6 +1785,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     }
   }
   sync();  // every node's iterate before the first residuals
+  OCP_STAMP(28);
   int status = 1, it = 0;
   double rs = 0, re = 0, ri = 0, rc = 0;
   const int ops_res[5] = {0, 0, 0, 0, 1};
@@ -1817,15 +1818,28 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       }
     }
     {
-      const double v0 = block_reduce(lrs, S.red, OpMax()), v1 = block_reduce(lre, S.red, OpMax()),
-                   v2 = block_reduce(lri, S.red, OpMax()), v3 = block_reduce(lrc, S.red, OpMax()),
-                   v4 = block_reduce(lmu, S.red, OpSum());
+      // the five reductions in one pass (one barrier; the same wave trees and wave order as block_reduce)
+      double v[5] = {lrs, lre, lri, lrc, lmu};
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const double w2 = __shfl_xor(v[c], o, 64);
+          v[c] = c < 4 ? nmax(v[c], w2) : v[c] + w2;
+        }
+      __syncthreads();  // the previous users of S.red are done
+      if ((tid & 63) == 0)
+#pragma unroll
+        for (int c = 0; c < 5; ++c) S.red[(tid >> 6) * 5 + c] = v[c];
+      __syncthreads();
       if (tid == 0) {
-        mine[0] = v0;
-        mine[1] = v1;
-        mine[2] = v2;
-        mine[3] = v3;
-        mine[4] = v4;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+          double r = S.red[c];
+#pragma unroll
+          for (int w = 1; w < NT / 64; ++w) r = c < 4 ? nmax(r, S.red[w * 5 + c]) : r + S.red[w * 5 + c];
+          mine[c] = r;
+        }
       }
     }
     if (!sync()) break;
@@ -2118,6 +2132,18 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       for (int r = it + 1; r < a.stat_rows; ++r)
         for (int c = 0; c < 10; ++c) a.stats[((long long)q * a.stat_rows + r) * 10 + c] = __builtin_nan("");
   }
+  // the barrier words back to zero for the next launch (no memset launch before it): every workgroup counts itself
+  // out after its last barrier; the last one out resets the counter, the fail word and the out-count (nobody polls
+  // them any more by then)
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned out = __hip_atomic_fetch_add(bar + 2, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (out == (unsigned)G - 1) {
+      __hip_atomic_store(bar + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 2, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Grid form: G workgroups per problem (B G <= 256, one per CU), launched as k_ocp_grid<FAST>
@@ -2293,9 +2319,9 @@ int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {
   size_t lds = ocp_lds_bytes(a.L);
   if (a.fast && lc > lds) lds = lc;
   const int G = a.fast && a.bar && a.gpart ? ocp_grid_width(a.L.N, B, a.G) : 0;
-  if (G > 0) {  // grid form: G workgroups per problem, one per CU; the barrier words zeroed before every launch
+  if (G > 0) {  // grid form: G workgroups per problem, one per CU; the barrier words zero (each launch leaves them so)
     a.G = G;
-    if (hipMemsetAsync(a.bar, 0, sizeof(unsigned) * 4 * (size_t)B, stream) != hipSuccess) return -1;
+    // the barrier words are zero at allocation and every launch leaves them zero (ipm_grid's last workgroup out)
     if (hipFuncSetAttribute((const void*)k_ocp_grid<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
       return -1;

@@ -73,7 +73,7 @@ struct OcpSolveArgs {
   double* hp;   // [B][hp_stride] Hc images of the latency form (nullptr when the handle has none)
   long long hp_stride;
   int G;           // grid form: workgroups per problem (0: one workgroup per problem)
-  unsigned* bar;   // grid form: [B][4] barrier counter, fail word (zeroed before every launch)
+  unsigned* bar;   // grid form: [B][4] barrier counter, fail word (zero at allocation; every launch leaves them zero)
   double* gpart;   // grid form: [B][G][8] per-workgroup partials of the reductions
   int ric;         // grid form: the exit Riccati quantities into ricP .. ricst (cmpc_ocp_set_keep_riccati)
   double *ricP, *ricp, *ricK, *rick, *ricLr;

@@ -12,11 +12,9 @@ objs=$(ls build/csrc/*.o | grep -v '/k_ocp.o$' | grep -v '/ocp_api.o$')
 $HC -DCMPC_OCP_STAMPS -DCMPC_OCP_CHAIN_LAB -c csrc/k_ocp.hip -o ../lab/_stamps/k_ocp_stamps.o
 $HC -DCMPC_OCP_CHAIN_LAB -c csrc/ocp_api.cpp -o ../lab/_stamps/ocp_api_lab.o
 $HC -DCMPC_OCP_CHAIN_LAB -c csrc/k_ocp.hip -o ../lab/_stamps/k_ocp_chain.o
-$HC -DCMPC_OCP_CHAIN_LAB -DCMPC_OCP_CHAIN_NOFETCH -c csrc/k_ocp.hip -o ../lab/_stamps/k_ocp_nofetch.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../lab/_stamps/libcmpc_ocpstamps.so $objs ../lab/_stamps/k_ocp_stamps.o \
   ../lab/_stamps/ocp_api_lab.o -Wl,-rpath,/opt/rocm/lib
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../lab/_stamps/libcmpc_ocpchain.so $objs ../lab/_stamps/k_ocp_chain.o \
   ../lab/_stamps/ocp_api_lab.o -Wl,-rpath,/opt/rocm/lib
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../lab/_stamps/libcmpc_ocpnofetch.so $objs ../lab/_stamps/k_ocp_nofetch.o \
   ../lab/_stamps/ocp_api_lab.o -Wl,-rpath,/opt/rocm/lib
 echo built ../lab/_stamps/libcmpc_ocpstamps.so ../lab/_stamps/libcmpc_ocpchain.so

@@ -79,7 +79,7 @@ def stamps(projected, B=1):
     L.cmpc_ocp_debug_stamps(buf, 1)
     names = {1: "residuals", 2: "rhs", 10: "fact:init", 11: "fact:T", 12: "fact:M", 13: "fact:prefetch",
              14: "fact:sweep", 15: "fact:store", 16: "fact:out", 20: "chain:init", 21: "chain:T", 22: "chain:M",
-             23: "chain:elim", 24: "chain:out", 25: "chain:outw0", 26: "[w1 load span]", 27: "chain:e-load", 28: "chain:e-wb", 17: "fact:exit", 3: "acl", 4: "forward",
+             23: "chain:elim", 24: "chain:out", 25: "chain:outw0", 26: "[w1 load span]", 27: "chain:e-load", 28: "grid prologue", 17: "fact:exit", 3: "acl", 4: "forward",
              5: "post", 6: "corr rhs", 7: "backward", 8: "acl+forward (corr)", 9: "update"}
     tot = sum(buf[i] for i in names if i != 26)  # 26: a span of wave 1, not on thread 0's timeline
     print(f"stamps {'projected' if projected else 'rows'} B={B} iters {it[0]} total {tot} cycles")
