@@ -481,6 +481,66 @@ def test_device_pointer_entry_equals_host_entry(cm, op):
     assert np.array_equal(dst.host(), st) and np.array_equal(dit.host(), it)
 
 
+@pytest.mark.gpu
+def test_device_getters_ordered_after_stream_solve(cm, op):
+    """cmpc_ocp_solve on the caller's (non-blocking) stream, then riccati / residuals / stats on the handle with no
+    synchronisation in between: the handle's getters wait on an event recorded after the solve, so they
+    read the finished workspace — equal to the same getters after a full device synchronisation."""
+    import ctypes as C
+    ps = [ocpgen.legged_problem(410 + i, projected=False) for i in range(3)]
+    recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+    B, p0 = len(ps), ps[0]
+    H = cm.hip()
+    stream = C.c_void_p()
+    assert H.hipStreamCreateWithFlags(C.byref(stream), 1) == 0  # hipStreamNonBlocking
+    dx0 = cm.DeviceArray.from_host(np.array([p["x0"] for p in ps]))
+    drec = cm.DeviceArray.from_host(np.array(recs))
+    dcrec = cm.DeviceArray.from_host(np.array(crecs))
+    out = []
+    for sync in (False, True):
+        s = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=B)
+        dx = cm.DeviceArray((B, p0["N"] + 1, p0["nx"]), np.float64)
+        du = cm.DeviceArray((B, s.nU), np.float64)
+        dst, dit = cm.DeviceArray((B,), np.int32), cm.DeviceArray((B,), np.int32)
+        s.solve_device(B, dx0, drec, dcrec, dx, du, dst, dit, stream)
+        if sync:
+            H.hipDeviceSynchronize()
+        ric = s.riccati(B)
+        res = s.residuals(B)
+        out.append((ric, res, dst.host()))
+        s.close()
+    H.hipStreamDestroy(stream)
+    (r0, e0, s0), (r1, e1, s1) = out
+    assert np.array_equal(s0, s1) and np.all(s0 == 0)
+    assert np.array_equal(e0, e1)
+    assert np.array_equal(r0[0], r1[0]) and np.array_equal(r0[1], r1[1]) and np.array_equal(r0[5], r1[5])
+    for b in range(B):
+        for k in range(p0["N"]):
+            assert np.array_equal(r0[2][b][k], r1[2][b][k]) and np.array_equal(r0[4][b][k], r1[4][b][k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("projected", [True, False])
+def test_device_staging_views_equal_copies(cm, op, projected):
+    """The host path with the problem written into the handle's pinned staging (OcpSolver.staging(): no host copy,
+    as the C++ mirror packs it) gives the same solution bit for bit as from ordinary arrays."""
+    p = ocpgen.legged_problem(420, projected=projected)
+    rec, crec = ocpgen.pack(p)
+    s = cm.OcpSolver(p["N"], p["nx"], p["nu"], p.get("nc"), max_batch=1)
+    x1, u1, st1, it1 = s.solve(p["x0"][None], rec[None], crec[None] if crec is not None else None)
+    stg = s.staging()
+    assert stg is not None
+    sx0, srec, screc = stg
+    sx0[0] = p["x0"]
+    srec[0] = rec
+    if screc is not None:
+        screc[0] = crec
+    x2, u2, st2, it2 = s.solve(sx0[:1], srec[:1], screc[:1] if screc is not None else None)
+    s.close()
+    assert st1[0] == st2[0] == 0 and it1[0] == it2[0]
+    assert np.array_equal(x1, x2) and np.array_equal(u1, u2)
+
+
 def _device_batch_path(cm, ps, chain, grid=0):
     p0 = ps[0]
     recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
