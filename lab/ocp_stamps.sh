@@ -16,5 +16,4 @@ $HC -DCMPC_OCP_CHAIN_LAB -c csrc/k_ocp.hip -o ../lab/_stamps/k_ocp_chain.o
   ../lab/_stamps/ocp_api_lab.o -Wl,-rpath,/opt/rocm/lib
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../lab/_stamps/libcmpc_ocpchain.so $objs ../lab/_stamps/k_ocp_chain.o \
   ../lab/_stamps/ocp_api_lab.o -Wl,-rpath,/opt/rocm/lib
-  ../lab/_stamps/ocp_api_lab.o -Wl,-rpath,/opt/rocm/lib
 echo built ../lab/_stamps/libcmpc_ocpstamps.so ../lab/_stamps/libcmpc_ocpchain.so
