@@ -543,8 +543,11 @@ class HpipmInterface::Impl {
 
   // The reference's verbose printout (HpipmInterface.cpp:457-503): status line, iteration count, the final max
   // residuals (d_ocp_qp_ipm_get_max_res_*) and the per-iteration statistics table (d_ocp_qp_ipm_get_stat), from the
-  // device solver's records (cmpc_ocp_get_residuals_host / cmpc_ocp_get_stats_host; the table's columns are
-  // cmpc_enable_stats', the reference's last seven (lq fact, itref, lin res) are not produced)
+  // device solver's records (cmpc_ocp_get_residuals_host / cmpc_ocp_get_stats_host). The table has the reference's
+  // 17 columns: the first ten are cmpc_enable_stats'; lq fact, itref pred and itref corr are 0 (the device solver is
+  // the Riccati recursion of the SPEED mode the reference selects, HpipmInterfaceSettings.h:45: no LQ factorisation,
+  // no iterative refinement); the four lin res columns are NaN: the device solver forms no residual of the Newton
+  // system (HPIPM is not vendored, so what HPIPM prints there in this mode is unpinned)
   void printStatus(int status, int iters) const {
     double res[4] = {NAN, NAN, NAN, NAN};
     const int rows = cmpc_ocp_stat_rows(ocp_);
@@ -562,9 +565,13 @@ class HpipmInterface::Impl {
     std::fprintf(stderr, "ipm iter = %d\n", iters);
     std::fprintf(stderr, "ipm residuals max: res_g = %e, res_b = %e, res_d = %e, res_m = %e\n", res[0], res[1], res[2],
                  res[3]);
-    std::fprintf(stderr, "\nalpha_aff\tmu_aff\t\tsigma\t\talpha_prim\talpha_dual\tmu\t\tres_stat\tres_eq\t\tres_ineq\tres_comp\n");
+    std::fprintf(stderr,
+                 "\nalpha_aff\tmu_aff\t\tsigma\t\talpha_prim\talpha_dual\tmu\t\tres_stat\tres_eq\t\tres_ineq\tres_comp\tlq fact\t\titref "
+                 "pred\titref corr\tlin res stat\tlin res eq\tlin res ineq\tlin res comp\n");
     for (int j = 0; j < iters + 1 && j < rows; ++j) {
       for (int i = 0; i < CMPC_STAT_COLS; ++i) std::fprintf(stderr, "%e\t", stats[(size_t)j * CMPC_STAT_COLS + i]);
+      for (int i = 0; i < 3; ++i) std::fprintf(stderr, "%e\t", 0.0);  // lq fact, itref pred, itref corr
+      for (int i = 0; i < 4; ++i) std::fprintf(stderr, "%e\t", (double)NAN);  // lin res stat / eq / ineq / comp
       std::fprintf(stderr, "\n");
     }
   }

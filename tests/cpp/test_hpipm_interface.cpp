@@ -6,10 +6,15 @@
 // HpipmInterface
 // mirror, whose solve runs on the MI355X engine. Random problems from a fixed-seed generator (ocs2's
 // getRandomDynamics/getRandomCost are not vendored): uniform [-1,1) matrices, costs made positive definite.
+#include <unistd.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "hpipm_catkin/HpipmInterface.h"
@@ -763,6 +768,64 @@ static void resize_ticks() {
   CHECK(ticker.deviceAllocations() == allocs_after_warm, "resize ticks allocate nothing after the first shapes");
 }
 
+// solve(..., verbose = true) prints the reference's status block and its 17-column statistics table
+// (HpipmInterface.cpp:457-503): one row per iteration 0..iter, the first ten columns the device solver's records.
+static void verbose_table() {
+  const int nx = 4, nu = 2, N = 6;
+  std::vector<VectorFunctionLinearApproximation> sys, con;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+    con.push_back(k > 0 ? randomConstraints(nx, nu, 1) : VectorFunctionLinearApproximation());
+  }
+  cost.push_back(randomCost(nx, 0));
+  con.push_back(VectorFunctionLinearApproximation());
+  HpipmInterface hpipm(hpipm_interface::extractSizesFromProblem(sys, cost, &con));
+  vector_array_t xs, us;
+  std::fflush(stderr);
+  FILE* tf = std::tmpfile();
+  const int saved = dup(2);
+  dup2(fileno(tf), 2);
+  const auto st = hpipm.solve(randv(nx), sys, cost, &con, xs, us, true);
+  std::fflush(stderr);
+  dup2(saved, 2);
+  close(saved);
+  std::rewind(tf);
+  std::string out;
+  char buf[4096];
+  size_t n;
+  while ((n = std::fread(buf, 1, sizeof buf, tf)) > 0) out.append(buf, n);
+  std::fclose(tf);
+  CHECK(st == hpipm_status::SUCCESS, "verbose solve status");
+  CHECK(out.find("HPIPM returned with flag 0. -> QP solved!") != std::string::npos, "verbose status line");
+  const size_t pi = out.find("ipm iter = ");
+  CHECK(pi != std::string::npos, "verbose iteration line");
+  const int iters = pi == std::string::npos ? -1 : std::atoi(out.c_str() + pi + 11);
+  const size_t hi = out.find("lin res comp\n");
+  CHECK(hi != std::string::npos && out.find("\tlq fact\t\titref pred\titref corr\tlin res stat") != std::string::npos,
+        "verbose table header has the 17 columns");
+  int rows = 0, bad = 0;
+  size_t at = hi == std::string::npos ? out.size() : hi + 13;
+  while (at < out.size()) {
+    const size_t e = out.find('\n', at);
+    const std::string line = out.substr(at, (e == std::string::npos ? out.size() : e) - at);
+    at = e == std::string::npos ? out.size() : e + 1;
+    if (line.empty()) continue;
+    std::vector<double> v;
+    const char* c = line.c_str();
+    char* end = nullptr;
+    for (double x = std::strtod(c, &end); end != c; x = std::strtod(c, &end)) {
+      v.push_back(x);
+      c = end;
+    }
+    ++rows;
+    if (v.size() != 17 || !std::isfinite(v[5]) || v[10] != 0.0 || v[11] != 0.0 || v[12] != 0.0 || !std::isnan(v[13])) ++bad;
+  }
+  std::printf("verbose table: %d iterations, %d rows, %d malformed\n", iters, rows, bad);
+  CHECK(rows == iters + 1 && bad == 0, "verbose table: iter + 1 rows of 17 columns");
+}
+
 int main() {
   dynamics_feasible(false);
   dynamics_feasible(true);
@@ -774,6 +837,7 @@ int main() {
   varying_state_dims();
   riccati_clamp_device();
   resize_ticks();
+  verbose_table();
   legged_size();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
   return failures ? 1 : 0;
