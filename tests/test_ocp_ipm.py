@@ -623,6 +623,31 @@ def test_device_wide_stage_class_matches_oracle(cm, op, rows):
     _check_vs_oracle(op, ps, x, u, st, it)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [
+    # (shape, latency form expected): the chain's bound nu_k + nx + 1 <= 60 (OCP_CHAIN_MAX_N1), one past it, the NZP
+    # = 64 / 128 instantiation boundary, the shortest horizon and a one-state system
+    (dict(N=6, nx=24, nu=[35] * 6), 1),
+    (dict(N=6, nx=24, nu=[35] * 6, rows=False), 1),
+    (dict(N=6, nx=24, nu=[35, 0, 12, 35, 20, 35], nc=[2, 0, 3, 1, 4, 2, 1]), 1),
+    (dict(N=6, nx=24, nu=[36] * 6), 0),
+    (dict(N=6, nx=24, nu=[36] * 6, rows=False), 0),
+    (dict(N=4, nx=20, nu=[43] * 4), 0),
+    (dict(N=4, nx=20, nu=[44, 43, 44, 10]), 0),
+    (dict(N=1, nx=3, nu=[2]), 1),
+    (dict(N=8, nx=1, nu=[1] * 8), 1),
+], ids=["n1_60", "n1_60_norows", "n1_60_mixed", "n1_61", "n1_61_norows", "n1_64", "n1_65", "N1", "nx1"])
+def test_device_dimension_boundaries_match_oracle(cm, op, case):
+    """The dimension limits of the device paths: the latency form takes nu_k + nx + 1 <= 60 and hands anything wider to
+    the batched form (cmpc_ocp_path), the batched form switches to its NZP = 128 instantiation past 64; each side of
+    each limit, the one-stage horizon and nx = 1 against the oracle (status, iterations, x / u at 1e-9)."""
+    shape, chain = case
+    ps = [_small(700 + i, **shape) for i in range(3)]
+    solver, x, u, st, it = _device_batch(cm, ps)
+    assert solver.path == chain
+    _check_vs_oracle(op, ps, x, u, st, it)
+
+
 def test_oracle_warm_start_from_solution(op):
     """HPIPM's primal warm start (warm_start = 1): from the converged x, u the IPM needs no more iterations than cold
     and lands on the same solution."""
