@@ -783,3 +783,32 @@ def test_device_reshape_ticks_allocate_nothing(cm, op):
         assert np.array_equal(ric[0], rf[0]) and np.array_equal(ric[1], rf[1]), t
         for k in range(p["N"]):
             assert np.array_equal(ric[2][0][k], rf[2][0][k]) and np.array_equal(ric[3][0][k], rf[3][0][k]), (t, k)
+
+
+@pytest.mark.gpu
+def test_device_reshape_across_path_limits(cm, op):
+    """One handle reshaped across the paths' dimension limits and back (latency form at nu_k + nx + 1 = 60, batched
+    form at 61, the NZP = 128 class at 65, a one-stage horizon, the legged problem with rows): every solve equals a
+    fresh handle's bit for bit, the path is the one the new dimensions select, and the results match the oracle."""
+    shapes = [(dict(N=6, nx=24, nu=[35] * 6), 1), (dict(N=6, nx=24, nu=[36] * 6), 0),
+              (dict(N=4, nx=20, nu=[44, 43, 44, 10]), 0), (dict(N=1, nx=3, nu=[2]), 1),
+              (dict(N=6, nx=24, nu=[35] * 6, rows=False), 1)]
+    h = None
+    for t, (shape, chain) in enumerate(shapes + shapes[::-1]):
+        ps = [_small(760 + 10 * t + i, **shape) for i in range(2)]
+        recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
+        p0 = ps[0]
+        crec = np.array(crecs) if p0.get("nc") else None
+        if h is None:
+            h = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=2)
+        else:
+            h.reshape(p0["N"], p0["nx"], p0["nu"], p0.get("nc"))
+        x, u, st, it = h.solve(np.array([p["x0"] for p in ps]), np.array(recs), crec)
+        assert h.path == chain, t
+        f, xf, uf, stf, itf = _device_batch(cm, ps)
+        f.close()
+        assert np.array_equal(st, stf) and np.array_equal(it, itf), t
+        for i in range(len(ps)):
+            assert np.array_equal(x[i], xf[i]) and np.array_equal(u[i], uf[i]), (t, i)
+        _check_vs_oracle(op, ps, x, u, st, it)
+    h.close()
