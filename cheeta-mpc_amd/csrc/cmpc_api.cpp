@@ -1197,6 +1197,7 @@ const char* cmpc_status_string(int s) {
     case CMPC_INVALID_CONTACT: return "INVALID_CONTACT";
     case CMPC_TOO_LARGE: return "TOO_LARGE";
     case CMPC_INFEASIBLE_STEP: return "INFEASIBLE_STEP";
+    case CMPC_GRID_TIMEOUT: return "GRID_TIMEOUT";
     default: return "UNKNOWN";
   }
 }

@@ -1220,9 +1220,12 @@ __device__ __forceinline__ GridRange grid_range(const OcpLayout& L, int g, int G
 
 // Grid barrier of one problem's G workgroups (the hand-off recipe of the MI355X guide: every wave's stores drained,
 // lane-0 agent release, a relaxed agent-scope arrive on a counter that is zero at the launch, a relaxed poll with
-// s_sleep, one agent acquire). The spin is bounded: on a timeout (or another workgroup's) the problem's fail word is
-// set and every workgroup returns false at its next barrier, so the grid drains instead of hanging.
-__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, double* flag_lds) {
+// s_sleep, one agent acquire). The wait is bounded in time (limit: ticks of the 100-MHz real-time counter,
+// OcpSolveArgs::grid_timeout): on a timeout (or another workgroup's) the problem's fail word is set and every workgroup
+// returns false at its next barrier, so the grid drains instead of hanging; the solve then reports
+// CMPC_GRID_TIMEOUT and the fallback launch (k_ocp_fallback) re-solves the problem on one workgroup. A negative limit
+// forces the timeout at the first barrier (cmpc_ocp_debug_force_grid_timeout).
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, double* flag_lds, long long limit) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1230,10 +1233,14 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, double
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (limit < 0) {
+      __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      good = false;
+    }
     while (good && __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) good = false;
-      if (++spins > (1u << 22)) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > limit) {
         __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         good = false;
       }
@@ -1733,7 +1740,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   unsigned nbar = 0;
   bool alive = true;
   auto sync = [&]() {
-    if (alive) alive = grid_sync(bar, (++nbar) * (unsigned)G, fl);
+    if (alive) alive = grid_sync(bar, (++nbar) * (unsigned)G, fl, a.grid_timeout);
     return alive;
   };
   double* x = V.x();
@@ -2012,7 +2019,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     if (!sync()) break;
     OCP_STAMP(9);
   }
-  if (!alive) status = 3;  // a barrier timed out: the grid drained, the result is not valid
+  if (!alive) status = OCP_GRID_TIMEOUT;  // a barrier timed out: the grid drained; k_ocp_fallback re-solves
   // --- the exit point's Riccati quantities (cmpc_ocp_set_keep_riccati; k_ocp_ric's outputs, same formulas) ---
   if (a.ric && alive && status != 3) {
     // Without rows the last Newton step's factorisation is the exit point's (no Sigma): the solve keeps its P_k, K_k,
@@ -2100,7 +2107,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     if (lead && rok && !fonly) ric_stage0(V, S, a.ricP + oP, a.ricp + op, a.ricK + oK, a.rick + ok2, a.ricLr + oM);
     if (lead && tid == 0) a.ricst[q] = rok ? 0 : 3;
   } else if (a.ric && lead && tid == 0) {
-    a.ricst[q] = 3;
+    a.ricst[q] = alive ? 3 : OCP_GRID_TIMEOUT;
   }
   // --- outputs (owned nodes / stages) ---
   bool fin = true;
@@ -2119,7 +2126,8 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   const bool ok_end = sync();
   if (ok_end) grid_collect(part + 7, G, 1, ops_max, red);
   if (lead && tid == 0) {
-    if (!ok_end || red[0] != 0.0) status = 3;
+    if (!ok_end) status = OCP_GRID_TIMEOUT;
+    else if (red[0] != 0.0) status = 3;
     a.status[q] = status;
     if (a.iters) a.iters[q] = it;
     if (a.res) {
@@ -2168,14 +2176,12 @@ __global__ __launch_bounds__(NT, MINB) void k_ocp_ipm(OcpSolveArgs a) {
   OCP_STAMP_END();
 }
 
-// Riccati quantities at the exit point (see k_ocp.hpp / cmpc.h cmpc_ocp_riccati)
+// Riccati quantities at the exit point (see k_ocp.hpp / cmpc.h cmpc_ocp_riccati) of problem q, one workgroup
 template <int NZP>
-__global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
-  extern __shared__ double smem[];
+__device__ __forceinline__ void ric_body(const OcpRicArgs& r, int q, const Lds& S) {
   const OcpSolveArgs& a = r.S;
   const OcpLayout& L = a.L;
-  const Lds S = carve(smem, L, NZP);
-  const int q = blockIdx.x, tid = threadIdx.x, nx = L.nx, N = L.N, m = L.m;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, m = L.m;
   const View V(a, q);
   if (a.status[q] == 3) {
     if (tid == 0) r.rstatus[q] = 3;
@@ -2234,6 +2240,39 @@ __global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
   if (tid == 0) r.rstatus[q] = ok ? 0 : 3;
 }
 
+template <int NZP>
+__global__ __launch_bounds__(NT) void k_ocp_ric(OcpRicArgs r) {
+  extern __shared__ double smem[];
+  ric_body<NZP>(r, blockIdx.x, carve(smem, r.S.L, NZP));
+}
+
+// Fallback of the grid form, launched after k_ocp_grid on the same stream: a problem whose grid barriers timed out
+// (status OCP_GRID_TIMEOUT: its workgroups were not all resident, e.g. another stream's kernels held the CUs) is
+// re-solved by one workgroup in the latency form (ipm_body<64, 1, true>: the same iteration) and, when the solve keeps
+// its Riccati quantities, refactorised at the exit point as k_ocp_ric does; every other problem's workgroup exits at
+// its first instruction.
+__global__ __launch_bounds__(NT, 1) void k_ocp_fallback(OcpSolveArgs a) {
+  const int q = blockIdx.x;
+  if (a.status[q] != OCP_GRID_TIMEOUT) return;
+  extern __shared__ double smem[];
+  ChainLds CS{};
+  const Lds S = carve_fast(smem, a.L, CS);
+  ipm_body<64, 1, true>(a, q, S, CS);
+  if (a.ric) {
+    __syncthreads();
+    OcpRicArgs r;
+    r.S = a;
+    r.P = a.ricP;
+    r.p = a.ricp;
+    r.K = a.ricK;
+    r.k = a.rick;
+    r.Lr = a.ricLr;
+    r.rstatus = a.ricst;
+    ric_body<64>(r, q, carve(smem, a.L, 64));
+  }
+  if (threadIdx.x == 0 && a.fallbacks) __hip_atomic_fetch_add(a.fallbacks, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 #ifdef CMPC_OCP_CHAIN_LAB
@@ -2280,16 +2319,23 @@ size_t ocp_lds_bytes(const OcpLayout& L) {
   return sizeof(double) * (pa + 2 * (size_t)nrm * L.nzp + 4 * (size_t)L.nzp + 128 + 64 + 64);
 }
 
+// CUs of the current device (cached per device: every workgroup of the grid needs a CU of its own)
+static int device_cus() {
+  static int ncu[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  const int slot = dev < 64 ? dev : 63;
+  if (ncu[slot] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 1;
+    ncu[slot] = n;
+  }
+  return ncu[slot];
+}
+
 int ocp_grid_width(int N, int B, int want) {
   if (B <= 0 || B > OCP_GRID_MAX_B) return 0;
-  static int ncu = 0;  // every workgroup of the grid needs a CU of its own (co-residency of the grid barriers)
-  if (ncu == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
-                                                hipSuccess)
-      ncu = n;
-    if (ncu <= 0) ncu = 1;
-  }
+  const int ncu = device_cus();
   const int cap = ncu < OCP_GRID_MAX_WG ? ncu : OCP_GRID_MAX_WG;
   int G = want > 0 ? want : OCP_GRID_MAX_G;
   if (G > N) G = N;
@@ -2310,6 +2356,42 @@ size_t ocp_chain_lds_bytes(const OcpLayout& L, int numax) {
   return bytes <= 160 * 1024 ? bytes : 0;  // beyond the LDS: the batched form
 }
 
+// G of the grid form for a batch of B problems of layout L (0: not the grid form): ocp_grid_width, capped by the
+// co-residency the kernel's registers and LDS admit on the current device (one workgroup per CU at most is used; the
+// occupancy query is cached per device and LDS size). Other streams' kernels can still hold CUs at the launch: the
+// barriers' time bound and the fallback launch cover that.
+int ocp_grid_for(const OcpLayout& L, int B, int want) {
+  const size_t lc = ocp_chain_lds_bytes(L, L.numax);
+  if (!lc) return 0;
+  int G = ocp_grid_width(L.N, B, want);
+  if (G == 0) return 0;
+  const size_t lds = std::max(ocp_lds_bytes(L), lc);
+  struct Occ {
+    int dev;
+    size_t lds;
+    int per_cu;
+  };
+  static Occ cache[16];
+  static int ncache = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int per_cu = -1;
+  for (int i = 0; i < ncache; ++i)
+    if (cache[i].dev == dev && cache[i].lds == lds) per_cu = cache[i].per_cu;
+  if (per_cu < 0) {
+    per_cu = 0;
+    if (hipFuncSetAttribute((const void*)k_ocp_grid<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+            hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_ocp_grid<true>, NT, lds) != hipSuccess)
+      per_cu = 0;
+    cache[ncache < 16 ? ncache++ : 15] = Occ{dev, lds, per_cu};
+  }
+  const long long resident = (long long)std::min(per_cu, 1) * device_cus();
+  if ((long long)B * G > resident) G = (int)(resident / B);
+  if (G > OCP_GRID_MAX_G) G = OCP_GRID_MAX_G;
+  return G >= 2 ? G : 0;
+}
+
 int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {
   if (B <= 0) return 0;
   OcpSolveArgs a = a0;
@@ -2318,14 +2400,19 @@ int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {
   a.fast = (a0.fast && a0.hp && lc > 0 && B <= OCP_ONE_PER_CU_MAX) ? 1 : 0;
   size_t lds = ocp_lds_bytes(a.L);
   if (a.fast && lc > lds) lds = lc;
-  const int G = a.fast && a.bar && a.gpart ? ocp_grid_width(a.L.N, B, a.G) : 0;
-  if (G > 0) {  // grid form: G workgroups per problem, one per CU; the barrier words zero (each launch leaves them so)
+  const int G = a.fast && a.bar && a.gpart ? ocp_grid_for(a.L, B, a.G) : 0;
+  if (G > 0) {  // grid form: G workgroups per problem, one per CU
     a.G = G;
     // the barrier words are zero at allocation and every launch leaves them zero (ipm_grid's last workgroup out)
     if (hipFuncSetAttribute((const void*)k_ocp_grid<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
       return -1;
     hipLaunchKernelGGL(k_ocp_grid<true>, dim3(B * G), dim3(NT), lds, stream, a);
+    // problems whose barriers timed out (status OCP_GRID_TIMEOUT) re-solved on one workgroup; the others exit at once
+    if (hipFuncSetAttribute((const void*)k_ocp_fallback, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_ocp_fallback, dim3(B), dim3(NT), lds, stream, a);
   } else if (a.fast) {  // the latency form (k_ocp_ipm<64, 1, true>): B <= OCP_ONE_PER_CU_MAX, one problem per CU
     if (hipFuncSetAttribute((const void*)k_ocp_ipm<64, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)

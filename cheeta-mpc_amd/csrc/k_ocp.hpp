@@ -46,7 +46,9 @@ struct OcpLayout {
 constexpr int OCP_GRID_MAX_B = 32;
 constexpr int OCP_GRID_MAX_G = 32;
 constexpr int OCP_GRID_MAX_WG = 256;
-int ocp_grid_width(int N, int B, int want);  // G for a batch (0: not the grid form)
+constexpr int OCP_GRID_TIMEOUT = 8;  // status of a grid-form solve whose barrier timed out (= CMPC_GRID_TIMEOUT)
+int ocp_grid_width(int N, int B, int want);  // G for a batch by the CU count (0: not the grid form)
+int ocp_grid_for(const OcpLayout& L, int B, int want);  // the same, capped by the kernel's co-residency
 
 // Limits of the latency form of the factorisation (ocp_chain.hpp, small batches)
 constexpr int OCP_CHAIN_MAX_NX = 27;
@@ -75,6 +77,9 @@ struct OcpSolveArgs {
   int G;           // grid form: workgroups per problem (0: one workgroup per problem)
   unsigned* bar;   // grid form: [B][4] barrier counter, fail word (zero at allocation; every launch leaves them zero)
   double* gpart;   // grid form: [B][G][8] per-workgroup partials of the reductions
+  long long grid_timeout;  // grid form: barrier wait bound in ticks of the 100-MHz real-time counter (< 0: time out
+                           // at the first barrier, the debug switch of the fallback test)
+  unsigned* fallbacks;     // grid form: count of problems re-solved by k_ocp_fallback (cmpc_ocp_fallback_count)
   int ric;         // grid form: the exit Riccati quantities into ricP .. ricst (cmpc_ocp_set_keep_riccati)
   double *ricP, *ricp, *ricK, *rick, *ricLr;
   int* ricst;

@@ -29,11 +29,14 @@ struct cmpc_ocp {
   cmpc_settings s{};
   OcpLayout L{};
   size_t rec_size = 0, crec_size = 0;
-  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart;
+  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart, fbk;
   long long hp_stride = 0;
   int hp_batch = 0, chain = 1;  // chain: cmpc_ocp_set_path (1 = the latency form where it applies, 0 = never)
   int grid = 0;                 // cmpc_ocp_set_grid: workgroups per problem of the grid form (0 auto, 1 off)
   int keep_ric = 0;             // cmpc_ocp_set_keep_riccati: the grid-form solve leaves the exit Riccati quantities
+  long long grid_timeout = 5000000;  // cmpc_ocp_set_grid_timeout: barrier wait bound, 100-MHz ticks (50 ms)
+  int force_timeout = 0;        // cmpc_ocp_debug_force_grid_timeout
+  int broken = 0;               // a failed (re-)layout left the buffers inconsistent: solves are refused
   void* pin = nullptr;          // pinned host staging of cmpc_ocp_solve_host / _riccati_host (small batches)
   size_t pin_cap = 0;
   int allocs = 0;               // device / pinned allocations made (cmpc_ocp_alloc_count)
@@ -186,7 +189,7 @@ size_t vbytes(const std::vector<T>& v) {
 
 void free_all(cmpc_ocp* o) {
   for (DBuf* b : {&o->dims, &o->ws, &o->x0, &o->rec, &o->crec, &o->x, &o->u, &o->res, &o->stats, &o->status,
-                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart})
+                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart, &o->fbk})
     if (b->p) (void)hipFree(b->p);
   if (o->pin) (void)hipHostFree(o->pin);
   if (o->ev_done) (void)hipEventDestroy(o->ev_done);
@@ -254,8 +257,10 @@ int alloc_stats(cmpc_ocp* o) {
   return grow(o, o->stats, sizeof(double) * (size_t)o->max_batch * o->stat_rows * CMPC_STAT_COLS);
 }
 
-// (Re-)lay out the handle for dimensions (N, nx, nu, nc): the layout arrays are uploaded into the dims block, every
-// device buffer grows to the new size if it exceeds its capacity, nothing else is allocated
+// (Re-)lay out the handle for dimensions (N, nx, nu, nc): every device buffer grows to the new size if it exceeds its
+// capacity (nothing else is allocated), then the layout arrays are uploaded into the dims block and the new layout is
+// committed. A failed growth leaves the handle marked broken (grow frees before it allocates), so later solves are
+// refused instead of reading freed memory; the next successful layout repairs it.
 int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
   int nzp = 0, ngmax = 0;
   if (!dims_ok(N, nx, nu, nc, nzp, ngmax)) return CMPC_ERR_ARG;
@@ -265,38 +270,19 @@ int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
   size_t rec_size = 0, crec_size = 0;
   Dims d = build_dims(N, nx, nu, nc, L, rec_size, crec_size);
   if (cmpc::ocp_lds_bytes(L) > 160 * 1024) return CMPC_ERR_ARG;
-  // work of an earlier layout may still be in flight on the device (its dims block is about to be overwritten)
+  // work of an earlier layout may still be in flight on the device (its buffers and dims block are about to change)
   if (o->ev_done && hipEventSynchronize(o->ev_done) != hipSuccess) return CMPC_ERR_HIP;
   const size_t b_int = vbytes(d.nu) + vbytes(d.ng) + vbytes(d.cu) + vbytes(d.cr) + vbytes(d.cK) + vbytes(d.cM) +
                        vbytes(d.ustage) + vbytes(d.rstage) + vbytes(d.cHp) + 10 * 8;
   const size_t b_ll = vbytes(d.orec) + vbytes(d.ocon);
-  int r = grow(o, o->dims, b_ll + b_int + 64);
-  if (r != CMPC_OK) return r;
-  std::vector<unsigned char> img(b_ll + b_int + 64, 0);
-  size_t off = 0;
-  auto put = [&](const void* src, size_t n) {
-    std::memcpy(img.data() + off, src, n);
-    const size_t at = off;
-    off += (n + 7) & ~(size_t)7;
-    return (const void*)((unsigned char*)o->dims.p + at);
-  };
-  L.orec = (const long long*)put(d.orec.data(), vbytes(d.orec));
-  L.ocon = (const long long*)put(d.ocon.data(), vbytes(d.ocon));
-  L.nu = (const int*)put(d.nu.data(), vbytes(d.nu));
-  L.ng = (const int*)put(d.ng.data(), vbytes(d.ng));
-  L.cu = (const int*)put(d.cu.data(), vbytes(d.cu));
-  L.cr = (const int*)put(d.cr.data(), vbytes(d.cr));
-  L.cK = (const int*)put(d.cK.data(), vbytes(d.cK));
-  L.cM = (const int*)put(d.cM.data(), vbytes(d.cM));
-  L.ustage = (const int*)put(d.ustage.data(), vbytes(d.ustage));
-  L.rstage = (const int*)put(d.rstage.data(), vbytes(d.rstage));
-  L.cHp = (const int*)put(d.cHp.data(), vbytes(d.cHp));
-  if (hipMemcpy(o->dims.p, img.data(), off, hipMemcpyHostToDevice) != hipSuccess) return CMPC_ERR_HIP;
   const size_t B = (size_t)o->max_batch, NP = (size_t)N + 1, D = sizeof(double);
   const int nU = L.nU;
+  int r = CMPC_OK;
   auto ck = [&r](int e) {
     if (r == CMPC_OK) r = e;
   };
+  o->broken = 1;  // until the layout below is committed
+  ck(grow(o, o->dims, b_ll + b_int + 64));
   ck(grow(o, o->ws, D * B * (size_t)L.ws_stride));
   ck(grow(o, o->x0, D * B * nx));
   ck(grow(o, o->rec, D * B * rec_size));
@@ -320,12 +306,38 @@ int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
     hp_batch = std::min(o->max_batch, cmpc::OCP_ONE_PER_CU_MAX);
     hp_stride = ((long long)d.cHp[(size_t)N] + 1) & ~1LL;
     ck(grow(o, o->hp, D * (size_t)hp_batch * (size_t)hp_stride));
-    if (!o->bar.p) {
+    if (!o->bar.p && r == CMPC_OK) {
+      // the grid barriers' words and the fallback counter start at zero (every launch leaves the words zero); a handle
+      // created outside the latency form's limits gets them at its first layout inside them
       ck(grow(o, o->bar, sizeof(unsigned) * 4 * (size_t)cmpc::OCP_GRID_MAX_B));
       ck(grow(o, o->gpart, D * 8 * (size_t)cmpc::OCP_GRID_MAX_WG));
+      ck(grow(o, o->fbk, sizeof(unsigned) * 4));
+      if (r == CMPC_OK && (hipMemset(o->bar.p, 0, o->bar.cap) != hipSuccess ||
+                           hipMemset(o->fbk.p, 0, o->fbk.cap) != hipSuccess))
+        r = CMPC_ERR_HIP;
     }
   }
   if (r != CMPC_OK) return r;
+  std::vector<unsigned char> img(b_ll + b_int + 64, 0);
+  size_t off = 0;
+  auto put = [&](const void* src, size_t n) {
+    std::memcpy(img.data() + off, src, n);
+    const size_t at = off;
+    off += (n + 7) & ~(size_t)7;
+    return (const void*)((unsigned char*)o->dims.p + at);
+  };
+  L.orec = (const long long*)put(d.orec.data(), vbytes(d.orec));
+  L.ocon = (const long long*)put(d.ocon.data(), vbytes(d.ocon));
+  L.nu = (const int*)put(d.nu.data(), vbytes(d.nu));
+  L.ng = (const int*)put(d.ng.data(), vbytes(d.ng));
+  L.cu = (const int*)put(d.cu.data(), vbytes(d.cu));
+  L.cr = (const int*)put(d.cr.data(), vbytes(d.cr));
+  L.cK = (const int*)put(d.cK.data(), vbytes(d.cK));
+  L.cM = (const int*)put(d.cM.data(), vbytes(d.cM));
+  L.ustage = (const int*)put(d.ustage.data(), vbytes(d.ustage));
+  L.rstage = (const int*)put(d.rstage.data(), vbytes(d.rstage));
+  L.cHp = (const int*)put(d.cHp.data(), vbytes(d.cHp));
+  if (hipMemcpy(o->dims.p, img.data(), off, hipMemcpyHostToDevice) != hipSuccess) return CMPC_ERR_HIP;
   o->N = N;
   o->nx = nx;
   o->L = L;
@@ -341,6 +353,7 @@ int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
   o->ric_B = 0;
   o->last_rec = o->last_crec = nullptr;
   o->last_status = nullptr;
+  o->broken = 0;
   return CMPC_OK;
 }
 
@@ -370,6 +383,8 @@ cmpc::OcpSolveArgs solve_args(cmpc_ocp* o, const double* x0, const double* rec, 
   a.G = o->grid;  // 0 auto; 1 disables the grid form (ocp_grid_width returns 0 below 2)
   a.bar = o->grid == 1 ? nullptr : (unsigned*)o->bar.p;
   a.gpart = (double*)o->gpart.p;
+  a.grid_timeout = o->force_timeout ? -1 : o->grid_timeout;
+  a.fallbacks = (unsigned*)o->fbk.p;
   // the exit Riccati quantities of the grid form (cmpc_ocp_set_keep_riccati) into the handle's arrays
   a.ric = o->keep_ric;
   a.ricP = (double*)o->P.p;
@@ -456,7 +471,6 @@ int cmpc_ocp_create(int N, int nx, const int* nu, const int* nc, const cmpc_sett
     r = CMPC_ERR_HIP;
   if (r == CMPC_OK) r = layout(o, N, nx, nu, nc);
   if (r == CMPC_OK) r = alloc_stats(o);
-  if (r == CMPC_OK && o->bar.p && hipMemset(o->bar.p, 0, o->bar.cap) != hipSuccess) r = CMPC_ERR_HIP;
   if (r == CMPC_OK && max_batch <= cmpc::OCP_GRID_MAX_B) r = grow_pin(o, pin_map(o, max_batch).total);
   if (r != CMPC_OK) {
     free_all(o);
@@ -508,8 +522,29 @@ int cmpc_ocp_set_grid(cmpc_ocp* o, int G) {
 
 int cmpc_ocp_grid(const cmpc_ocp* o, int B) {
   if (!o || B <= 0) return CMPC_ERR_ARG;
-  if (!has_chain(o) || !o->bar.p || o->grid == 1) return 0;
-  return cmpc::ocp_grid_width(o->N, B, o->grid);
+  if (!has_chain(o) || !o->bar.p || o->grid == 1 || B > o->hp_batch) return 0;
+  return cmpc::ocp_grid_for(o->L, B, o->grid);
+}
+
+int cmpc_ocp_set_grid_timeout(cmpc_ocp* o, double us) {
+  if (!o || !(us >= 0.0) || us > 60e6) return CMPC_ERR_ARG;
+  o->grid_timeout = us == 0.0 ? 5000000 : (long long)(us * 100.0);  // 100-MHz ticks; 0: the default 50 ms
+  return CMPC_OK;
+}
+
+int cmpc_ocp_debug_force_grid_timeout(cmpc_ocp* o, int on) {
+  if (!o || on < 0 || on > 1) return CMPC_ERR_ARG;
+  o->force_timeout = on;
+  return CMPC_OK;
+}
+
+int cmpc_ocp_fallback_count(cmpc_ocp* o) {
+  if (!o) return CMPC_ERR_ARG;
+  if (!o->fbk.p) return 0;
+  unsigned n = 0;
+  if (o->ev_done && hipEventSynchronize(o->ev_done) != hipSuccess) return CMPC_ERR_HIP;
+  if (hipMemcpy(&n, o->fbk.p, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return CMPC_ERR_HIP;
+  return (int)n;
 }
 
 int cmpc_ocp_set_keep_riccati(cmpc_ocp* o, int on) {
@@ -532,7 +567,7 @@ int cmpc_ocp_last_solve_ms(cmpc_ocp* o, float* ms) {
 }
 
 double* cmpc_ocp_staging(cmpc_ocp* o, int which) {
-  if (!o || !o->pin || o->max_batch > cmpc::OCP_GRID_MAX_B) return nullptr;
+  if (!o || !o->pin || o->broken || o->max_batch > cmpc::OCP_GRID_MAX_B) return nullptr;
   const PinMap m = pin_map(o, o->max_batch);
   unsigned char* b = (unsigned char*)o->pin;
   switch (which) {
@@ -545,7 +580,7 @@ double* cmpc_ocp_staging(cmpc_ocp* o, int which) {
 
 int cmpc_ocp_solve(cmpc_ocp* o, int B, const double* d_x0, const double* d_rec, const double* d_crec, double* d_x,
                    double* d_u, int* d_status, int* d_iters, void* stream) {
-  if (!o || B < 0 || B > o->max_batch || !d_x0 || !d_rec || !d_x || !d_u || !d_status) return CMPC_ERR_ARG;
+  if (!o || B < 0 || B > o->max_batch || !d_x0 || !d_rec || !d_x || !d_u || !d_status || o->broken) return CMPC_ERR_ARG;
   if (o->m > 0 && !d_crec) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
   const cmpc::OcpSolveArgs a = solve_args(o, d_x0, d_rec, d_crec, d_x, d_u, d_status, d_iters);
@@ -559,14 +594,15 @@ int cmpc_ocp_solve(cmpc_ocp* o, int B, const double* d_x0, const double* d_rec, 
   o->last_rec = d_rec;
   o->last_crec = d_crec;
   o->last_status = d_status;
-  o->ric_B = (a.ric && a.fast && cmpc::ocp_grid_width(o->N, B, o->grid) > 0 && o->grid != 1) ? B : 0;
+  o->ric_B = (a.ric && cmpc_ocp_grid(o, B) > 0) ? B : 0;
   o->ric_full = o->L.m > 0 ? 1 : 0;  // without rows the kernel keeps the factorisation only (k_ocp.hip, exit block)
   return CMPC_OK;
 }
 
 int cmpc_ocp_solve_host(cmpc_ocp* o, int B, const double* x0, const double* rec, const double* crec, double* x,
                         double* u, int* status, int* iters) {
-  if (!o || B < 0 || B > o->max_batch || !x0 || !rec || !x || (!u && o->nU > 0) || !status) return CMPC_ERR_ARG;
+  if (!o || B < 0 || B > o->max_batch || !x0 || !rec || !x || (!u && o->nU > 0) || !status || o->broken)
+    return CMPC_ERR_ARG;
   if (o->m > 0 && !crec) return CMPC_ERR_ARG;
   if (B == 0) return CMPC_OK;
   const size_t NP = (size_t)o->N + 1, D = sizeof(double);
@@ -631,7 +667,7 @@ int cmpc_ocp_solve_host(cmpc_ocp* o, int B, const double* x0, const double* rec,
 
 int cmpc_ocp_riccati(cmpc_ocp* o, int B, double* d_P, double* d_p, double* d_K, double* d_k, double* d_Lr_out,
                      int* d_status, void* stream) {
-  if (!o || B <= 0 || B > o->last_B || !d_P || !d_p || !d_status || (o->nU > 0 && (!d_K || !d_k)) ||
+  if (!o || o->broken || B <= 0 || B > o->last_B || !d_P || !d_p || !d_status || (o->nU > 0 && (!d_K || !d_k)) ||
       !o->last_rec || !o->last_status)
     return CMPC_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;

@@ -10,6 +10,10 @@
 // ocs2_core; the device is reached only through the C ABI (cmpc/cmpc.h).
 #include "hpipm_catkin/HpipmInterface.h"
 
+#ifdef CMPC_HAVE_OCS2_CORE
+#include <ocs2_core/misc/LinearAlgebra.h>  // the reference's clamp (HpipmInterface.cpp:32), with ocs2_core's default
+#endif
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -212,7 +216,7 @@ class HpipmInterface::Impl {
       if (r != CMPC_OK)
         throw std::runtime_error(std::string("[HpipmInterface] device Riccati failed: ") + cmpc_error_string(r));
       if (st != CMPC_SUCCESS) throw std::runtime_error("[HpipmInterface] Riccati factorisation: NaN pivot");
-      if (minEig_ > 0.0) clampFactors(nx);
+      if (clampActive()) clampFactors(nx);
       if (all) riccatiValid_ = true;
       ricFb_ = true;
     }
@@ -233,6 +237,7 @@ class HpipmInterface::Impl {
   void setMinimumEigenvalue(double v) {
     if (!(v >= 0.0)) throw std::invalid_argument("[HpipmInterface] minimum eigenvalue must be >= 0");
     minEig_ = v;
+    minEigSet_ = true;
     riccatiValid_ = false;
     ricFb_ = false;
   }
@@ -440,6 +445,31 @@ class HpipmInterface::Impl {
   // minimum in magnitude (hpipm_interface::setTriangularMinimumEigenvalues); K_k (k >= 1) is re-derived from the
   // clamped factor as the reference's getRiccatiFeedback does, K_k = -Lr_c^-T Ls', with Ls' = -Lr' K_k of the
   // device's factor; stage 0 uses the clamped Lr_0. The feedforward of k >= 1 is read as the reference reads ric_k.
+  // With ocs2_core on the include path and no minimum set, every getter clamps as the reference does, by ocs2's own
+  // LinearAlgebra::setTriangularMinimumEigenvalues with its default minimum; setRiccatiMinimumEigenvalue(v) replaces
+  // that by v (0: no clamp). With the stand-in types there is no ocs2 default to take: the clamp runs when a minimum
+  // is set.
+  bool clampActive() const {
+#ifdef CMPC_HAVE_OCS2_CORE
+    if (!minEigSet_) return true;
+#endif
+    return minEig_ > 0.0;
+  }
+  // the clamp of one stage's m x m lower factor (column-major) in place; returns whether a diagonal entry changed
+  bool clampStage(double* Lc, int m) const {
+#ifdef CMPC_HAVE_OCS2_CORE
+    if (!minEigSet_) {
+      matrix_t L(m, m);
+      std::copy(Lc, Lc + (size_t)m * m, L.data());
+      LinearAlgebra::setTriangularMinimumEigenvalues(L);
+      bool changed = false;
+      for (int i = 0; i < m; ++i) changed = changed || L.data()[(size_t)i * m + i] != Lc[(size_t)i * m + i];
+      std::copy(L.data(), L.data() + (size_t)m * m, Lc);
+      return changed;
+    }
+#endif
+    return hpipm_interface::setTriangularMinimumEigenvalues(Lc, m, minEig_);
+  }
   void clampFactors(int nx) {
     const Packed& p = last_;
     size_t oK = 0, oM = 0;
@@ -448,7 +478,7 @@ class HpipmInterface::Impl {
       const int m = p.nu[(size_t)k];
       double* Lr = Lr_.data() + oM;
       Lc.assign(Lr, Lr + (size_t)m * m);
-      if (hpipm_interface::setTriangularMinimumEigenvalues(Lc.data(), m, minEig_) && k >= 1) {
+      if (m > 0 && clampStage(Lc.data(), m) && k >= 1) {
         Ls.resize((size_t)m);
         hpipm_interface::rederiveFeedback(Lr, Lc.data(), K_.data() + oK, m, nx, Ls.data());
       }
@@ -584,7 +614,8 @@ class HpipmInterface::Impl {
   Packed last_;
   bool riccatiValid_ = false;  // every Riccati quantity of the last solve fetched
   bool ricFb_ = false;         // K, Lr, P_1 fetched
-  double minEig_ = 0.0;  // setRiccatiMinimumEigenvalue (0: no clamp)
+  double minEig_ = 0.0;     // setRiccatiMinimumEigenvalue (0: no clamp)
+  bool minEigSet_ = false;  // a minimum was set (otherwise, with ocs2_core, ocs2's own default clamps)
   bool timing_ = false;  // enableDeviceTiming
   std::vector<double> xbuf_, ubuf_, recbuf_, crecbuf_, x0buf_, Pm_, pv_, K_, k_, Lr_, K0_, k0_, S0_, s0_;
 };

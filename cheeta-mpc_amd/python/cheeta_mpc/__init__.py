@@ -127,6 +127,9 @@ def lib():
     L.cmpc_ocp_set_keep_riccati.argtypes = [vp, C.c_int]
     L.cmpc_ocp_enable_timing.argtypes = [vp, C.c_int]
     L.cmpc_ocp_last_solve_ms.argtypes = [vp, P(C.c_float)]
+    L.cmpc_ocp_set_grid_timeout.argtypes = [vp, C.c_double]
+    L.cmpc_ocp_fallback_count.argtypes = [vp]
+    L.cmpc_ocp_debug_force_grid_timeout.argtypes = [vp, C.c_int]
     L.cmpc_ocp_staging.argtypes = [vp, C.c_int]
     L.cmpc_ocp_staging.restype = d
     L.cmpc_ocp_solve.argtypes = [vp, C.c_int, d, d, d, d, d, i, i, vp]
@@ -527,9 +530,33 @@ class OcpSolver:
         self.crec_size = (int(lib().cmpc_ocp_constraint_record_size(self.N, self.nx, _dp(self.nu), _dp(self.nc)))
                           if self.nc is not None else 0)
         self.stat_rows = lib().cmpc_ocp_stat_rows(self.h)
+        self._views = []  # staging views handed out since the last reshape (cmpc.h: valid until reshape / destroy)
+        self._stale = []  # (address, bytes) of staging blocks a reshape or close invalidated
+
+    def _invalidate_staging(self):
+        # cmpc_ocp_staging's pointers die with a reshape (the pin block may be reallocated, the record offsets move) or
+        # the handle: the views handed out become read-only, and solve() refuses arrays inside the old blocks
+        for v in self._views:
+            self._stale.append((v.ctypes.data, v.nbytes))
+            try:
+                v.flags.writeable = False
+            except ValueError:
+                pass
+        self._views = []
+
+    def _check_not_stale(self, *arrays):
+        for a in arrays:
+            if a is None or not self._stale:
+                continue
+            lo, hi = a.ctypes.data, a.ctypes.data + a.nbytes
+            for addr, n in self._stale:
+                if lo < addr + n and addr < hi:
+                    raise RuntimeError("OcpSolver: an input lies in staging invalidated by reshape()/close(); "
+                                       "call staging() again")
 
     def close(self):
         if self.h:
+            self._invalidate_staging()
             lib().cmpc_ocp_destroy(self.h)
             self.h = C.c_void_p()
 
@@ -560,10 +587,27 @@ class OcpSolver:
     def grid(self, B):
         return int(lib().cmpc_ocp_grid(self.h, int(B)))
 
+    def set_grid_timeout(self, us):
+        """cmpc_ocp_set_grid_timeout: the grid barriers' wait bound in microseconds (0: the default 50 ms)."""
+        _chk(lib().cmpc_ocp_set_grid_timeout(self.h, float(us)), "cmpc_ocp_set_grid_timeout")
+
+    def force_grid_timeout(self, on):
+        """cmpc_ocp_debug_force_grid_timeout: every grid barrier times out at once (the fallback's test switch)."""
+        _chk(lib().cmpc_ocp_debug_force_grid_timeout(self.h, int(on)), "cmpc_ocp_debug_force_grid_timeout")
+
+    @property
+    def fallback_count(self):
+        """Problems re-solved on one workgroup after a grid-barrier timeout since the handle was created."""
+        n = int(lib().cmpc_ocp_fallback_count(self.h))
+        if n < 0:
+            _chk(n, "cmpc_ocp_fallback_count")
+        return n
+
     def reshape(self, N, nx, nu, nc=None):
         """cmpc_ocp_reshape: new dimensions on the same handle (grow-only buffers, HpipmInterface::resize)."""
         nu_a = np.ascontiguousarray(list(nu)[:N], dtype=np.int32)
         nc_a = None if nc is None else np.ascontiguousarray(list(nc), dtype=np.int32)
+        self._invalidate_staging()
         _chk(lib().cmpc_ocp_reshape(self.h, int(N), int(nx), _dp(nu_a), _dp(nc_a)), "cmpc_ocp_reshape")
         self.N, self.nx, self.nu, self.nc = int(N), int(nx), nu_a, nc_a
         self.nU = int(nu_a.sum())
@@ -592,7 +636,9 @@ class OcpSolver:
     def staging(self):
         """numpy views of the handle's pinned staging (cmpc_ocp_staging): x0 [max_batch, nx], rec [max_batch,
         rec_size], crec [max_batch, crec_size] or None; a solve whose inputs are these views copies nothing on the host
-        (the records are written in place, as the C++ mirror packs them). None when the handle has no staging."""
+        (the records are written in place, as the C++ mirror packs them). None when the handle has no staging.
+        The views are valid until the next reshape() or close() (cmpc.h): those make them read-only, and solve() refuses
+        inputs inside invalidated staging — fetch them again."""
         out = []
         for which, n in ((0, self.nx), (1, self.rec_size), (2, self.crec_size if self.m else 0)):
             if n == 0:
@@ -602,12 +648,17 @@ class OcpSolver:
             if not ptr:
                 return None
             arr = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_double)), shape=(self.max_batch * n,))
-            out.append(arr.reshape(self.max_batch, n))
+            view = arr.reshape(self.max_batch, n)
+            self._views.append(view)
+            lo, hi = view.ctypes.data, view.ctypes.data + view.nbytes  # the live staging is not stale (a reshape
+            self._stale = [(ad, m) for ad, m in self._stale if not (lo < ad + m and ad < hi)]  # may keep the block)
+            out.append(view)
         return tuple(out)
 
     def solve(self, x0, rec, crec=None, guess=None):
         """Host path (cmpc_ocp_solve_host): x0 [B,nx], rec [B,rec_size], crec [B,crec_size]; guess = (x, u), the
         initial guess read when the settings' warm_start is set. Returns x [B,N+1,nx], u [B,nU], status [B], iters."""
+        self._check_not_stale(*(a for a in (x0, rec, crec) if isinstance(a, np.ndarray)))
         x0 = np.ascontiguousarray(np.atleast_2d(x0), np.float64)
         B = x0.shape[0]
         rec = np.ascontiguousarray(rec, np.float64).reshape(B, self.rec_size)

@@ -57,6 +57,7 @@ enum cmpc_error {
   CMPC_ERR_HIP = -2,      /* HIP runtime error */
   CMPC_ERR_SIZE = -3,     /* batch larger than the context's max_batch, or horizon mismatch */
   CMPC_ERR_NO_DEVICE = -4 /* no usable gfx950 device */
+  /* cmpc_ocp: a solve on a handle whose last cmpc_ocp_reshape failed returns CMPC_ERR_ARG until a reshape succeeds */
 };
 
 /* Per-QP solver status. 0..4 keep HPIPM's hpipm_status order (HpipmInterface.h:79-85). */
@@ -70,10 +71,13 @@ enum cmpc_qp_status {
   CMPC_INVALID_CONTACT = 5,  /* a horizon step has no stance leg: reference throws "mpc table invalid"
                                 (CentroidalMPC.cpp:328-330) */
   CMPC_TOO_LARGE = 6,        /* condensed size exceeds what this build's kernels support */
-  CMPC_INFEASIBLE_STEP = 7   /* cmpc_nlp_solve_batch: the step box of CentroidalMPC.cpp:196-198 cannot be met: a
+  CMPC_INFEASIBLE_STEP = 7,  /* cmpc_nlp_solve_batch: the step box of CentroidalMPC.cpp:196-198 cannot be met: a
                                 later stance run's foothold box is empty (des_foot_pos varies over the run by more
                                 than the box), or a run from step 0 keeps the current foot (:165-167) outside the box
                                 around des_foot_pos at one of its nodes */
+  CMPC_GRID_TIMEOUT = 8      /* cmpc_ocp grid form only, internal: a grid barrier timed out (the problem's workgroups
+                                were not all resident). The same cmpc_ocp_solve call re-solves such a problem on one
+                                workgroup (cmpc_ocp_fallback_count), so no solve returns this code */
 };
 
 /* Foothold step box of the NLP (CentroidalMPC.cpp:30-31): step_lb <= foot_pos - des_foot_pos <= step_ub at every node
@@ -332,6 +336,17 @@ int cmpc_ocp_path(const cmpc_ocp* ocp);
  * (0: one workgroup per problem). */
 int cmpc_ocp_set_grid(cmpc_ocp* ocp, int G);
 int cmpc_ocp_grid(const cmpc_ocp* ocp, int B);
+/* Co-residency of the grid form. cmpc_ocp_grid caps G by the occupancy the kernel admits on the current device (one
+ * workgroup per CU). Kernels of other streams can still hold CUs when a solve starts: each grid barrier waits at most
+ * us microseconds (cmpc_ocp_set_grid_timeout; 0 = the default 50 ms), then the problem's grid drains and the same
+ * cmpc_ocp_solve re-solves it on one workgroup (a second launch on the stream, which returns at once for problems
+ * whose grid finished; the result is the one-workgroup form's: same statuses and iterations, trajectories to
+ * rounding). cmpc_ocp_fallback_count returns how many problems took that fallback since the handle was created
+ * (synchronises on the last solve). cmpc_ocp_debug_force_grid_timeout(ocp, 1) makes every grid barrier time out at
+ * once (tests of the fallback). */
+int cmpc_ocp_set_grid_timeout(cmpc_ocp* ocp, double us);
+int cmpc_ocp_fallback_count(cmpc_ocp* ocp);
+int cmpc_ocp_debug_force_grid_timeout(cmpc_ocp* ocp, int on);
 /* New dimensions for an existing handle (HpipmInterface::resize, HpipmInterface.cpp:92-129): the layout arrays are
  * re-uploaded and a device (or pinned host) buffer is reallocated only when the new size exceeds its capacity, as
  * HPIPM's MemoryBlock::reserve grows only (:46-67); handles for up to 32 problems keep 25 % headroom from the first
@@ -350,7 +365,9 @@ int cmpc_ocp_set_keep_riccati(cmpc_ocp* ocp, int keep);
 int cmpc_ocp_enable_timing(cmpc_ocp* ocp, int on);
 int cmpc_ocp_last_solve_ms(cmpc_ocp* ocp, float* ms);
 /* Pinned host staging of cmpc_ocp_solve_host for handles of up to 32 problems (NULL otherwise): a caller that packs
- * its records straight into these (sized for max_batch problems) saves the host copy into the staging. */
+ * its records straight into these (sized for max_batch problems) saves the host copy into the staging. The pointers
+ * are valid until the next cmpc_ocp_reshape or cmpc_ocp_destroy of the handle: a reshape may reallocate the staging
+ * and moves the record offsets with the record size, so fetch them again after it. */
 #define CMPC_OCP_STAGE_X0 0
 #define CMPC_OCP_STAGE_REC 1
 #define CMPC_OCP_STAGE_CREC 2

@@ -96,10 +96,13 @@ class HpipmInterface {
   vector_array_t getRiccatiFeedforward(const VectorFunctionLinearApproximation& dynamics0,
                                        const ScalarFunctionQuadraticApproximation& cost0);
 
-  /* The minimum eigenvalue the getters clamp Lr_k to (hpipm_interface::setTriangularMinimumEigenvalues; the reference
-   * always clamps, to ocs2_core's default numeric_traits::weakEpsilon). 0 (the default here) leaves the device factor
-   * as it is: its pivot guard already zeroes a column whose pivot is <= 1e-200. With a minimum set, a clamped stage's
-   * K_k is re-derived from the clamped factor as getRiccatiFeedback derives it (:361), and stage 0 uses clamped Lr_0. */
+  /* The minimum eigenvalue the getters clamp Lr_k to. The reference always clamps, by ocs2_core's
+   * LinearAlgebra::setTriangularMinimumEigenvalues with its default minimum (HpipmInterface.cpp:340, :357, :379, :419):
+   * so does this mirror when ocs2_core is on the include path and no minimum is set. Setting a minimum replaces that
+   * (0: no clamp, the device factor as it is: its pivot guard already zeroes a column whose pivot is <= 1e-200). With
+   * the stand-in types (no ocs2_core) there is no ocs2 default: the clamp runs once a minimum is set
+   * (hpipm_interface::setTriangularMinimumEigenvalues). A clamped stage's K_k is re-derived from the clamped factor as
+   * getRiccatiFeedback derives it (:361), and stage 0 uses the clamped Lr_0. */
   void setRiccatiMinimumEigenvalue(double minEigenValue);
   /* Device allocations the interface's handle has made so far (cmpc_ocp_alloc_count; -1 without a handle). */
   int deviceAllocations() const;

@@ -18,6 +18,9 @@
 #include <vector>
 
 #include "hpipm_catkin/HpipmInterface.h"
+#ifdef CMPC_HAVE_OCS2_CORE
+#include <ocs2_core/misc/LinearAlgebra.h>
+#endif
 
 using namespace ocs2;
 
@@ -727,6 +730,58 @@ static void riccati_clamp_device() {
   CHECK(std::fabs(rmin - want) < 1e-6 * want && std::fabs(rmax - want) < 1e-6 * want, "riccati clamp row factor");
 }
 
+#ifdef CMPC_HAVE_OCS2_CORE
+// The getters' default clamp with ocs2_core on the include path (here the mock's ocs2_core/misc/LinearAlgebra.h): no
+// minimum set, every getter clamps Lr through ocs2's LinearAlgebra::setTriangularMinimumEigenvalues with its own
+// default (the reference's HpipmInterface.cpp:340, :357, :379, :419). Stage 2 gets R = diag(1e-24, R11), B_2's first
+// column 0 and reg_prim = 0, so Lr_2(0,0) = 1e-12 lies below the default (1e-9 in the mock): K_2's first row scales by
+// 1e-12 / 1e-9 against the unclamped getter (setRiccatiMinimumEigenvalue(0)), everything else is unchanged.
+static void riccati_clamp_ocs2_default() {
+  const int nx = 3, nu = 2, N = 5;
+  const vector_t x0 = randv(nx);
+  std::vector<VectorFunctionLinearApproximation> sys;
+  std::vector<ScalarFunctionQuadraticApproximation> cost;
+  for (int k = 0; k < N; ++k) {
+    sys.push_back(randomDynamics(nx, nu));
+    cost.push_back(randomCost(nx, nu));
+  }
+  cost.push_back(randomCost(nx, 0));
+  for (int i = 0; i < nx; ++i) sys[2].dfdu(i, 0) = 0.0;
+  cost[2].dfduu(0, 0) = 1e-24;
+  cost[2].dfduu(0, 1) = cost[2].dfduu(1, 0) = 0.0;
+  for (int j = 0; j < nx; ++j) cost[2].dfdux(0, j) *= 1e-12;
+  cost[2].dfdu[0] *= 1e-12;
+  HpipmInterface::Settings st;
+  st.reg_prim = 0.0;
+  HpipmInterface hpipm(HpipmInterface::OcpSize(N, nx, nu), st);
+  vector_array_t xs, us;
+  CHECK(hpipm.solve(x0, sys, cost, nullptr, xs, us, false) == SUCCESS, "ocs2 default clamp status");
+  const int calls0 = LinearAlgebra::mockTriangularClampCalls();
+  const auto Kd = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  const int calls = LinearAlgebra::mockTriangularClampCalls() - calls0;
+  hpipm.setRiccatiMinimumEigenvalue(0.0);
+  const auto Ku = hpipm.getRiccatiFeedback(sys[0], cost[0]);
+  double e_same = 0.0, rmin = 1e300, rmax = -1e300;
+  for (int k = 0; k < N; ++k)
+    for (int j = 0; j < nx; ++j)
+      for (int a = 0; a < nu; ++a) {
+        if (k == 2 && a == 0) {
+          const double r = Kd[2](0, j) / Ku[2](0, j);
+          rmin = std::fmin(rmin, r);
+          rmax = std::fmax(rmax, r);
+        } else {
+          e_same = std::fmax(e_same, std::fabs(Kd[(size_t)k](a, j) - Ku[(size_t)k](a, j)) /
+                                         std::fmax(1.0, std::fabs(Ku[(size_t)k](a, j))));
+        }
+      }
+  std::printf("riccati clamp (ocs2 default): %d LinearAlgebra calls, other rows %.3e, clamped row factor [%.6e, %.6e]\n",
+              calls, e_same, rmin, rmax);
+  CHECK(calls == N, "the default getter clamps every stage through ocs2's LinearAlgebra");
+  CHECK(e_same < 1e-12, "ocs2 default clamp leaves the other rows");
+  CHECK(std::fabs(rmin - 1e-3) < 1e-6 && std::fabs(rmax - 1e-3) < 1e-6, "ocs2 default clamp row factor 1e-12 / 1e-9");
+}
+#endif
+
 // An MPC loop's ticks through resize (MultipleShootingSolver.cpp:275-277 resizes every iteration): the sizes shift
 // between the legged shapes (rows at some nodes, then none, nu changing), each tick's solution against a fresh
 // interface; after the first round of shapes no device buffer is allocated again (cmpc_ocp_alloc_count).
@@ -836,6 +891,9 @@ int main() {
   constrained_riccati();
   varying_state_dims();
   riccati_clamp_device();
+#ifdef CMPC_HAVE_OCS2_CORE
+  riccati_clamp_ocs2_default();
+#endif
   resize_ticks();
   verbose_table();
   legged_size();
