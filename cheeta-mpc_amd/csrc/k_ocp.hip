@@ -52,6 +52,13 @@ __shared__ unsigned long long ocp_stamp_lds[33];
   do {                                                                                    \
     if (blockIdx.x == 0 && threadIdx.x == (t)) ocp_stamp_lds[id] += __builtin_amdgcn_s_memtime() - (var); \
   } while (0)
+// a span of thread 0 of workgroup blk, added straight to the device array (another workgroup's timeline)
+#define OCP_SPANG_END(id, var, blk)                                                                          \
+  do {                                                                                                       \
+    if (blockIdx.x == (blk) && threadIdx.x == 0)                                                             \
+      __hip_atomic_fetch_add(&ocp_stamp_acc[id], __builtin_amdgcn_s_memtime() - (var), __ATOMIC_RELAXED,     \
+                             __HIP_MEMORY_SCOPE_AGENT);                                                      \
+  } while (0)
 #define OCP_STAMP_BEGIN()                                                     \
   do {                                                                        \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
@@ -76,6 +83,9 @@ __shared__ unsigned long long ocp_stamp_lds[33];
   } while (0)
 #define OCP_SPAN_END(id, var, t) \
   do {                           \
+  } while (0)
+#define OCP_SPANG_END(id, var, blk) \
+  do {                              \
   } while (0)
 #define OCP_STAMP_END() \
   do {                  \
@@ -1161,6 +1171,7 @@ __device__ __forceinline__ void ldl_solve(const double* __restrict__ F, int m, c
 }
 
 #include "ocp_chain.hpp"
+#include "ocp_part.hpp"
 
 // LDS of the latency form: G images (two), T, Paug, the pivot-column buffers and the rows' Sigma (two), then red and
 // vec; the other passes of the kernel see G0 / G1 as ABx / Tx (contiguous: the staged residuals' buffer)
@@ -1743,9 +1754,74 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     if (alive) alive = grid_sync(bar, (++nbar) * (unsigned)G, fl, a.grid_timeout);
     return alive;
   };
+  const int ops_res[5] = {0, 0, 0, 0, 1};
+  const int ops_min[1] = {2};
+  const int ops_sum[1] = {1};
+  const int ops_max[1] = {0};
   double* x = V.x();
   double* u = V.u();
   double* hp = FAST ? a.hp + (long long)q * a.hp_stride : nullptr;
+  // The factorisation (ocp_part.hpp): nseg segments of the horizon on workgroups 0 .. nseg-1 — P1 (the last segment
+  // from the terminal node, the middle ones from a zero value function, then their elements), P2 (the combine on
+  // workgroup 0), P3 (segments 0 .. nseg-2 from their end node's exact value) — or, with one segment, the serial
+  // chain on workgroup 0. Leaves mine[5] = the NaN flag for the caller's barrier + collect. Partials: the first
+  // pass's flags in slot 4, the combine's in slot 6 (both collected well before their next writers, see above).
+  double* segq = a.seg ? a.seg + (long long)q * a.seg_stride : nullptr;
+  const int nseg = (FAST && segq) ? part_segments(a.nseg, G, N) : 1;
+  auto factor_grid = [&]() __attribute__((always_inline)) -> bool {
+    // phase 0: P1; 1: P3; 2: the serial chain on workgroup 0 (one segment, or the fallback). One chain_factor call
+    // site for all of them (each inlined copy of the chain costs registers).
+    const int cb = seg_begin(N, nseg, g), ce = seg_begin(N, nseg, g + 1);
+    const bool mid = g >= 1 && g < nseg - 1;
+    int fl = 0;
+    int ph = nseg > 1 ? 0 : 2;
+    while (true) {
+      bool run;
+      int k0 = 0, k1 = N, term = CH_TERM_NODE;
+      const double* Pt = nullptr;
+      if (ph == 0) {
+        run = g >= 1 && g < nseg;
+        k0 = cb;
+        k1 = g == nseg - 1 ? N : ce;
+        term = g == nseg - 1 ? CH_TERM_NODE : CH_TERM_ZERO;
+      } else if (ph == 1) {
+        run = g < nseg - 1;
+        k0 = cb;
+        k1 = ce;
+        term = CH_TERM_GIVEN;
+        Pt = segq + OCP_GRID_MAX_G * seg_esz(nx) + (g + 1) * seg_bsz(nx);
+      } else {
+        run = lead;
+      }
+      OCP_SPAN_BEGIN(t_ch);
+      const int f = run ? chain_factor(V, CS, hp, a.reg, k0, k1, term, Pt, Pt ? Pt + nx * nx : nullptr) : 0;
+      OCP_SPANG_END(30, t_ch, 1);
+      if (ph != 0) {
+        OCP_STAMP(29);
+        fl = f;
+        break;
+      }
+      OCP_SPAN_BEGIN(t_el);
+      if (f == 0 && mid) seg_element(V, S, CS.Ml, cb, ce, segq + g * seg_esz(nx));
+      OCP_SPANG_END(31, t_el, 1);
+      if (tid == 0) mine[4] = (double)f;
+      if (!sync()) return false;
+      grid_collect(part + 4, G, 1, ops_max, red);
+      OCP_STAMP(18);
+      bool pok = red[0] == 0.0;
+      if (pok) {
+        const bool cok = lead ? seg_combine(V, CS.Ml, segq, nseg, N) : true;
+        if (tid == 0) mine[6] = cok ? 0.0 : 1.0;
+        if (!sync()) return false;
+        grid_collect(part + 6, G, 1, ops_max, red);
+        pok = red[0] == 0.0;
+      }
+      OCP_STAMP(19);
+      ph = pok ? 1 : 2;  // a dropped pivot in the first pass, a NaN or a failed combine: the serial chain
+    }
+    if (tid == 0) mine[5] = (fl & CH_NAN) ? 1.0 : 0.0;
+    return true;
+  };
   if (FAST) {  // this workgroup's stages' constant Hessian blocks (read by workgroup 0's chain after a barrier)
     const int e0 = L.cHp[R.k0], e1 = L.cHp[R.k1];
     int k = R.k0;
@@ -1795,10 +1871,6 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   OCP_STAMP(28);
   int status = 1, it = 0;
   double rs = 0, re = 0, ri = 0, rc = 0;
-  const int ops_res[5] = {0, 0, 0, 0, 1};
-  const int ops_min[1] = {2};
-  const int ops_sum[1] = {1};
-  const int ops_max[1] = {0};
   for (it = 0; alive; ++it) {
     // --- residuals (owned nodes / rows), reduced over the grid ---
     rows_value(V, x, u, V.row(R_C), R.r0, R.r1);
@@ -1898,11 +1970,11 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     step_rhs_range(V, R.k0, R.k1, R.n1);
     if (!sync()) break;
     OCP_STAMP(2);
-    // --- factorisation on workgroup 0 ---
-    if (lead) {
-      bool fok;
-      if constexpr (FAST) fok = chain_factor(V, CS, hp, a.reg);
-      else fok = factor_pass<64>(V, S, a.reg);
+    // --- factorisation: the partitioned chain over the grid (FAST; nseg = 1: the serial chain on workgroup 0) ---
+    if constexpr (FAST) {
+      if (!factor_grid()) break;
+    } else if (lead) {
+      const bool fok = factor_pass<64>(V, S, a.reg);
       if (tid == 0) mine[5] = fok ? 0.0 : 1.0;
     } else if (tid == 0) {
       mine[5] = 0.0;
@@ -2043,10 +2115,10 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     // the factorisation at the exit point (with rows, or when no step was taken: no factorisation to keep)
     const bool full = m > 0 || it == 0;
     if (full) {
-      if (lead) {
-        bool fok;
-        if constexpr (FAST) fok = chain_factor(V, CS, hp, a.reg);
-        else fok = factor_pass<64>(V, S, a.reg);
+      if constexpr (FAST) {
+        (void)factor_grid();
+      } else if (lead) {
+        const bool fok = factor_pass<64>(V, S, a.reg);
         if (tid == 0) mine[5] = fok ? 0.0 : 1.0;
       } else if (tid == 0) {
         mine[5] = 0.0;

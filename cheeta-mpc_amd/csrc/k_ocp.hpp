@@ -50,6 +50,10 @@ constexpr int OCP_GRID_TIMEOUT = 8;  // status of a grid-form solve whose barrie
 int ocp_grid_width(int N, int B, int want);  // G for a batch by the CU count (0: not the grid form)
 int ocp_grid_for(const OcpLayout& L, int B, int want);  // the same, capped by the kernel's co-residency
 
+// Segment buffer of the grid form's partitioned factorisation (ocp_part.hpp: seg_esz / seg_bsz), doubles
+__host__ __device__ inline int seg_esz(int nx) { return (2 * nx * nx + nx + 1) & ~1; }
+__host__ __device__ inline int seg_bsz(int nx) { return (nx * nx + nx + 1) & ~1; }
+
 // Limits of the latency form of the factorisation (ocp_chain.hpp, small batches)
 constexpr int OCP_CHAIN_MAX_NX = 27;
 constexpr int OCP_CHAIN_MAX_NU = 36;
@@ -80,6 +84,9 @@ struct OcpSolveArgs {
   long long grid_timeout;  // grid form: barrier wait bound in ticks of the 100-MHz real-time counter (< 0: time out
                            // at the first barrier, the debug switch of the fallback test)
   unsigned* fallbacks;     // grid form: count of problems re-solved by k_ocp_fallback (cmpc_ocp_fallback_count)
+  double* seg;             // grid form: [B][seg_stride] segment elements and boundary values (ocp_part.hpp), or null
+  long long seg_stride;
+  int nseg;                // grid form: segments of the partitioned factorisation (0 auto, 1 the serial chain)
   int ric;         // grid form: the exit Riccati quantities into ricP .. ricst (cmpc_ocp_set_keep_riccati)
   double *ricP, *ricp, *ricK, *rick, *ricLr;
   int* ricst;

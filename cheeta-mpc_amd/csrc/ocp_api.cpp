@@ -29,7 +29,7 @@ struct cmpc_ocp {
   cmpc_settings s{};
   OcpLayout L{};
   size_t rec_size = 0, crec_size = 0;
-  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart, fbk;
+  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart, fbk, seg;
   long long hp_stride = 0;
   int hp_batch = 0, chain = 1;  // chain: cmpc_ocp_set_path (1 = the latency form where it applies, 0 = never)
   int grid = 0;                 // cmpc_ocp_set_grid: workgroups per problem of the grid form (0 auto, 1 off)
@@ -37,6 +37,8 @@ struct cmpc_ocp {
   long long grid_timeout = 5000000;  // cmpc_ocp_set_grid_timeout: barrier wait bound, 100-MHz ticks (50 ms)
   int force_timeout = 0;        // cmpc_ocp_debug_force_grid_timeout
   int broken = 0;               // a failed (re-)layout left the buffers inconsistent: solves are refused
+  int nseg = 0;                 // cmpc_ocp_set_segments: segments of the grid form's factorisation (0 auto)
+  long long seg_stride = 0;     // doubles per problem of the segment buffer
   void* pin = nullptr;          // pinned host staging of cmpc_ocp_solve_host / _riccati_host (small batches)
   size_t pin_cap = 0;
   int allocs = 0;               // device / pinned allocations made (cmpc_ocp_alloc_count)
@@ -189,7 +191,7 @@ size_t vbytes(const std::vector<T>& v) {
 
 void free_all(cmpc_ocp* o) {
   for (DBuf* b : {&o->dims, &o->ws, &o->x0, &o->rec, &o->crec, &o->x, &o->u, &o->res, &o->stats, &o->status,
-                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart, &o->fbk})
+                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart, &o->fbk, &o->seg})
     if (b->p) (void)hipFree(b->p);
   if (o->pin) (void)hipHostFree(o->pin);
   if (o->ev_done) (void)hipEventDestroy(o->ev_done);
@@ -299,13 +301,16 @@ int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
   ck(grow(o, o->k, D * B * (size_t)std::max(nU, 1)));
   ck(grow(o, o->Lr, D * B * (size_t)std::max(L.nM, 1)));
   // the latency form (small batches: one problem per CU, or G per problem) where the dimensions fit it
-  long long hp_stride = 0;
+  long long hp_stride = 0, seg_stride = 0;
   int hp_batch = 0;
   const size_t lc = cmpc::ocp_chain_lds_bytes(L, L.numax);
   if (lc > 0 && lc <= 160 * 1024) {
     hp_batch = std::min(o->max_batch, cmpc::OCP_ONE_PER_CU_MAX);
     hp_stride = ((long long)d.cHp[(size_t)N] + 1) & ~1LL;
     ck(grow(o, o->hp, D * (size_t)hp_batch * (size_t)hp_stride));
+    // the grid form's segment elements and boundary values (ocp_part.hpp), per problem of a grid-sized batch
+    seg_stride = (long long)cmpc::OCP_GRID_MAX_G * (cmpc::seg_esz(nx) + cmpc::seg_bsz(nx));
+    if (o->max_batch <= cmpc::OCP_GRID_MAX_B) ck(grow(o, o->seg, D * (size_t)o->max_batch * (size_t)seg_stride));
     if (!o->bar.p && r == CMPC_OK) {
       // the grid barriers' words and the fallback counter start at zero (every launch leaves the words zero); a handle
       // created outside the latency form's limits gets them at its first layout inside them
@@ -349,6 +354,7 @@ int layout(cmpc_ocp* o, int N, int nx, const int* nu, const int* nc) {
   o->crec_size = crec_size;
   o->hp_stride = hp_stride;
   o->hp_batch = hp_batch;
+  o->seg_stride = seg_stride;
   o->last_B = 0;  // the Riccati quantities of a solve of another layout are gone
   o->ric_B = 0;
   o->last_rec = o->last_crec = nullptr;
@@ -384,6 +390,9 @@ cmpc::OcpSolveArgs solve_args(cmpc_ocp* o, const double* x0, const double* rec, 
   a.bar = o->grid == 1 ? nullptr : (unsigned*)o->bar.p;
   a.gpart = (double*)o->gpart.p;
   a.grid_timeout = o->force_timeout ? -1 : o->grid_timeout;
+  a.seg = (o->seg.p && o->seg_stride > 0) ? (double*)o->seg.p : nullptr;
+  a.seg_stride = o->seg_stride;
+  a.nseg = o->nseg;
   a.fallbacks = (unsigned*)o->fbk.p;
   // the exit Riccati quantities of the grid form (cmpc_ocp_set_keep_riccati) into the handle's arrays
   a.ric = o->keep_ric;
@@ -524,6 +533,21 @@ int cmpc_ocp_grid(const cmpc_ocp* o, int B) {
   if (!o || B <= 0) return CMPC_ERR_ARG;
   if (!has_chain(o) || !o->bar.p || o->grid == 1 || B > o->hp_batch) return 0;
   return cmpc::ocp_grid_for(o->L, B, o->grid);
+}
+
+int cmpc_ocp_set_segments(cmpc_ocp* o, int S) {
+  if (!o || S < 0 || S > cmpc::OCP_GRID_MAX_G) return CMPC_ERR_ARG;
+  o->nseg = S;
+  return CMPC_OK;
+}
+
+int cmpc_ocp_segments(const cmpc_ocp* o, int B) {
+  const int G = cmpc_ocp_grid(o, B);
+  if (G < 0) return G;
+  if (G == 0 || !o->seg.p) return 1;
+  int S = o->nseg > 0 ? o->nseg : (int)(std::sqrt(2.0f * (float)o->N) + 0.5f);  // part_segments (ocp_part.hpp)
+  S = std::min(S, std::min(G, o->N));
+  return S < 1 ? 1 : S;
 }
 
 int cmpc_ocp_set_grid_timeout(cmpc_ocp* o, double us) {

@@ -35,6 +35,9 @@ constexpr int CH_DESC = 10;   // ints per stage descriptor
 constexpr int CH_MR = 60;     // rows of the M image (n1 <= OCP_CHAIN_MAX_N1)
 constexpr int CH_FS = 60;     // column stride of the factor image F (rows x of the pivot column j at F[j CH_FS + x])
 constexpr int CH_MAXU = 36;   // pivot columns of the factor image (nu_k <= OCP_CHAIN_MAX_NU)
+// LDS from ChainLds::Ml to the descriptor table (M image, Hc image, g, the second Paug, F0): scratch of the
+// partitioned factorisation's element and combine steps (ocp_part.hpp) between chains
+constexpr int CH_SCRATCH = CH_MR * CH_GS + 4 * CH_MAXNT + 64 + CH_PS * CH_PS + CH_MAXU * CH_FS;
 typedef double d2v __attribute__((ext_vector_type(2)));
 
 // 2 x 2 block tau of the lower triangle in row order: tau = bi (bi + 1) / 2 + bj, bj <= bi
@@ -271,7 +274,7 @@ __device__ __forceinline__ void chain_m(const ChainLds& S, int nx, const int* d,
 template <int NB, int A0>
 __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&bi)[NB], const int (&bj)[NB],
                                             const bool (&on)[NB], int j, int mk, int n1, double* c0, double* c1,
-                                            double* F, bool& bad) {
+                                            double* F, bool& bad, bool& weak) {
   const int lane = threadIdx.x, j1 = j + 1, jb = j >> 2;
   const bool two = j1 < mk;
 #pragma unroll
@@ -293,6 +296,7 @@ __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&b
   const double d1 = fma(-a1, l1, e1);
   bad = bad || (two && d1 != d1);
   const double d1i = (two && d1 > 1e-200) ? 1.0 / d1 : 0.0;
+  weak = weak || !(d0 > 1e-200) || (two && !(d1 > 1e-200));
   // the factor's columns into the F image (rows >= j; chain_out reads column j + 1 from row j + 1)
   if (lane >= j && lane < n1) {
     const double v0 = c0[lane];
@@ -328,7 +332,8 @@ __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&b
 // updates in the same order, so the results are bit-identical with half the publish / read-back latency chains.
 template <int NB>
 __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&bi)[NB], const int (&bj)[NB],
-                                             const bool (&on)[NB], int j, int n1, double* cb, double* F, bool& bad) {
+                                             const bool (&on)[NB], int j, int n1, double* cb, double* F, bool& bad,
+                                             bool& weak) {
   const int lane = threadIdx.x, jb = j >> 2;
   double* c0 = cb;
   double* c1 = cb + 64;
@@ -378,6 +383,7 @@ __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&
   const double d3 = fma(-a3, l3, e3);
   bad = bad || (d3 != d3);
   const double d3i = d3 > 1e-200 ? 1.0 / d3 : 0.0;
+  weak = weak || !(d0 > 1e-200) || !(d1 > 1e-200) || !(e2 > 1e-200) || !(d3 > 1e-200);
   // the factor's columns j .. j + 3 (rows >= j): c0, c1~, the updated column j + 2 and its c~ for j + 3
   if (lane >= j && lane < n1) {
     const double x0 = c0[lane], x1 = c1[lane], x2 = c2[lane], x3 = c3[lane];
@@ -444,13 +450,14 @@ __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&
 }
 
 // (C) on wave 0: NB 4 x 4 lower blocks of M per lane (block beta = lane + 64 q), the pair rounds, the outputs.
-// Returns the NaN flag of the pivots.
+// Returns the pivots' flags: CH_NAN (a NaN pivot), CH_WEAK (a pivot the guard dropped, d <= 1e-200).
+constexpr int CH_NAN = 1, CH_WEAK = 2;
 template <int NB>
-__device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, const int* d, double* F, double* PaW) {
+__device__ __forceinline__ int chain_elim(const View& V, const ChainLds& S, const int* d, double* F, double* PaW) {
   const OcpLayout& L = V.L;
   const int lane = threadIdx.x, nx = L.nx;
   const int mk = d[0], nz = mk + nx, n1 = nz + 1, nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
-  bool bad = false;
+  bool bad = false, weak = false;
   int bi[NB], bj[NB];
   bool on[NB];
   double m[NB][4][4];
@@ -480,10 +487,10 @@ __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, con
   OCP_STAMP(27);
   for (int j = 0; j < mk; j += 4) {
     if (j + 4 <= mk) {
-      chain_round4<NB>(m, bi, bj, on, j, n1, S.C, F, bad);
+      chain_round4<NB>(m, bi, bj, on, j, n1, S.C, F, bad, weak);
     } else {
-      chain_round<NB, 0>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad);
-      if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad);
+      chain_round<NB, 0>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad, weak);
+      if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad, weak);
     }
   }
   OCP_STAMP(23);
@@ -523,7 +530,7 @@ __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, con
         }
       }
     }
-    return bad;
+    return (bad ? CH_NAN : 0) | (weak ? CH_WEAK : 0);
   }
   double* dummy = S.C + 128 + lane;  // one slot per lane: a shared one would serialise the masked lanes' stores
 #pragma unroll
@@ -539,7 +546,7 @@ __device__ __forceinline__ bool chain_elim(const View& V, const ChainLds& S, con
         *(live ? PaW + I * CH_PS + J : dummy) = v;
         *(live ? PaW + J * CH_PS + I : dummy) = v;
       }
-  return bad;
+  return (bad ? CH_NAN : 0) | (weak ? CH_WEAK : 0);
 }
 
 // K_k = -L_uu^-T L_xu', kff_k = -L_uu^-T l_r' for stages [k0, k1) from the LDL' factor F = L D the chain left (u rows
@@ -563,19 +570,25 @@ __device__ __forceinline__ void chain_gains(const View& V, int k0, int k1) {
   }
 }
 
-// Backward factorisation of the barrier-weighted Newton matrix, latency form. Writes P_k, pv_k (k = 0..N), the LDL'
-// columns Lf_k and the factor's x / rhs rows (k = 0..N-1; chain_gains turns them into K_k, kf_k). Returns false on a
-// NaN pivot.
-__device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, const double* hp, double reg) {
+// Backward factorisation of the barrier-weighted Newton matrix, latency form, over the stages [k0, k1) from the value
+// function of node k1 given by term:
+//   CH_TERM_NODE  node k1 = N: P_N = Q_N + reg I + C_N' Sigma C_N, p_N = g_x,N (written to P(N), pv(N));
+//   CH_TERM_ZERO  V_k1 = 0 (a segment of the partitioned factorisation, ocp_part.hpp: its first pass);
+//   CH_TERM_GIVEN V_k1(x) = x'Pt x / 2 + pt'x (Pt column-major nx x nx, pt [nx]; the partitioned form's second pass).
+// Writes P_k, pv_k (k = k0..k1-1), the LDL' columns Lf_k and the factor's x / rhs rows (chain_gains turns them into
+// K_k, kf_k). Returns the pivots' flags of all four waves (CH_NAN, CH_WEAK), workgroup-uniform.
+constexpr int CH_TERM_NODE = 0, CH_TERM_ZERO = 1, CH_TERM_GIVEN = 2;
+__device__ __forceinline__ int chain_factor(const View& V, const ChainLds& S, const double* hp, double reg, int k0,
+                                            int k1, int term, const double* Pt, const double* pt) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, N = L.N, nx = L.nx, np1 = nx + 1;
   const int wave = tid >> 6;
   int bi[CH_MAXT], bj[CH_MAXT];
 #pragma unroll
   for (int r = 0; r < CH_MAXT; ++r) ch_block(tid + NT * r, bi[r], bj[r]);
-  bool bad = false;
+  int flags = 0;
   // stage descriptors into LDS
-  for (int k = tid; k < N; k += NT) {
+  for (int k = k0 + tid; k < k1; k += NT) {
     int* dk = S.desc + CH_DESC * k;
     const int mk = L.nu[k], n1 = mk + nx + 1, nb = (n1 + 1) >> 1;
     dk[0] = mk;
@@ -589,8 +602,8 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
     dk[8] = L.cM[k];
     dk[9] = L.cK[k];
   }
-  // terminal node: P_N = Q_N + reg I + C_N' Sigma C_N, p_N = g_x,N; Paug's padding rows / columns zero
-  {
+  // the value function of node k1 into Paug; Paug's padding rows / columns zero
+  if (term == CH_TERM_NODE) {  // terminal node: P_N = Q_N + reg I + C_N' Sigma C_N, p_N = g_x,N
     const int g = L.ng[N];
     const double* Q = V.Q(N);
     const double* sig = V.row(R_SIG) + L.cr[N];
@@ -611,6 +624,18 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
       S.Pa[e] = val;
       S.Pa2[e] = 0.0;
     }
+  } else {
+    for (int e = tid; e < CH_PS * CH_PS; e += NT) {
+      const int r = e / CH_PS, c = e - r * CH_PS;
+      double val = 0.0;
+      if (term == CH_TERM_GIVEN) {
+        if (r < nx && c < nx) val = Pt[c * nx + r];
+        else if (r < nx && c == nx) val = pt[r];
+        else if (r == nx && c < nx) val = pt[c];
+      }
+      S.Pa[e] = val;
+      S.Pa2[e] = 0.0;
+    }
   }
   // the image's rows and T's rows np1 .. CH_NRP stay zero (the T and M loops run over rows in groups of four)
   for (int e = tid; e < (CH_NRP - np1) * CH_GS; e += NT) {
@@ -618,13 +643,13 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
     S.T[np1 * CH_GS + e] = 0.0;
   }
   __syncthreads();  // descriptors
-  if (wave > 0) chain_load(V, S.desc + CH_DESC * (N - 1), N - 1, hp, S, nullptr, nullptr, nullptr);
+  if (wave > 0) chain_load(V, S.desc + CH_DESC * (k1 - 1), k1 - 1, hp, S, nullptr, nullptr, nullptr);
   __syncthreads();
   OCP_STAMP(20);
-  for (int k = N - 1; k >= 0; --k) {
+  for (int k = k1 - 1; k >= k0; --k) {
     const int* d = S.desc + CH_DESC * k;
     const int mk = d[0], nz = mk + nx, n1 = nz + 1, nb = (n1 + 1) >> 1, nt = d[7];
-    const int pb = (N - 1 - k) & 1;
+    const int pb = (k1 - 1 - k) & 1;
     const double* PaR = pb ? S.Pa2 : S.Pa;  // Paug of node k + 1
     double* PaW = pb ? S.Pa : S.Pa2;        // Paug of node k
     double* Fw = (k & 1) ? S.F1 : S.F0;     // the factor image of stage k (stage k + 1's is the other)
@@ -704,27 +729,32 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
     // --- (C) wave 0: the elimination and the outputs; waves 1-3: stage k - 1's operands ---
     if (wave == 0) {
       const int nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
-      bool b2;
-      if (nt4 <= 64) b2 = chain_elim<1>(V, S, d, Fw, PaW);
-      else b2 = chain_elim<2>(V, S, d, Fw, PaW);  // nt4 <= 120: n1 <= 60 (OCP_CHAIN_MAX_N1, ocp_chain_lds_bytes)
-      bad = bad || b2;
+      if (nt4 <= 64) flags |= chain_elim<1>(V, S, d, Fw, PaW);
+      else flags |= chain_elim<2>(V, S, d, Fw, PaW);  // nt4 <= 120: n1 <= 60 (OCP_CHAIN_MAX_N1, ocp_chain_lds_bytes)
       OCP_STAMP(25);
-    } else if (k > 0) {
+    } else if (k > k0) {
       OCP_SPAN_BEGIN(t_load);
       // stage k - 1's operands; stage k + 1's outputs (its Paug and factor images, untouched in this stage)
-      const bool out = k + 1 < N;
+      const bool out = k + 1 < k1;
       chain_load(V, d - CH_DESC, k - 1, hp, S, out ? d + CH_DESC : nullptr, PaR, (k & 1) ? S.F0 : S.F1);
       OCP_SPAN_END(26, t_load, 64);
     }
     lds_barrier();
     OCP_STAMP(24);
   }
-  // the outputs of stages 1 (if not yet written: N == 1 has none) and 0
-  if (N > 1) chain_out(V, S.desc + CH_DESC, 1, (N & 1) ? S.Pa : S.Pa2, S.F1, tid, NT);
-  chain_out(V, S.desc, 0, (N & 1) ? S.Pa2 : S.Pa, S.F0, tid, NT);
-  const bool ok = __syncthreads_or(bad) == 0;
+  // the outputs of stages k0 + 1 (if not yet written: a one-stage range has none) and k0
+  if (k1 - k0 > 1)
+    chain_out(V, S.desc + CH_DESC * (k0 + 1), k0 + 1, ((k1 - k0) & 1) ? S.Pa : S.Pa2, ((k0 + 1) & 1) ? S.F1 : S.F0,
+              tid, NT);
+  chain_out(V, S.desc + CH_DESC * k0, k0, ((k1 - k0) & 1) ? S.Pa2 : S.Pa, (k0 & 1) ? S.F1 : S.F0, tid, NT);
+  const int fl = (__syncthreads_or(flags & CH_NAN) ? CH_NAN : 0) | (__syncthreads_or(flags & CH_WEAK) ? CH_WEAK : 0);
   __syncthreads();  // every wave's global stores (chain_out) visible to the workgroup
-  return ok;
+  return fl;
+}
+
+// The whole horizon from the terminal node (the serial chain); returns false on a NaN pivot
+__device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, const double* hp, double reg) {
+  return (chain_factor(V, S, hp, reg, 0, V.L.N, CH_TERM_NODE, nullptr, nullptr) & CH_NAN) == 0;
 }
 
 // The Newton step's serial affine recursions on wave 0, their operands staged in LDS a chunk of stages ahead by waves

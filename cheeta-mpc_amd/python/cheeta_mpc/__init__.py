@@ -127,6 +127,8 @@ def lib():
     L.cmpc_ocp_set_keep_riccati.argtypes = [vp, C.c_int]
     L.cmpc_ocp_enable_timing.argtypes = [vp, C.c_int]
     L.cmpc_ocp_last_solve_ms.argtypes = [vp, P(C.c_float)]
+    L.cmpc_ocp_set_segments.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_segments.argtypes = [vp, C.c_int]
     L.cmpc_ocp_set_grid_timeout.argtypes = [vp, C.c_double]
     L.cmpc_ocp_fallback_count.argtypes = [vp]
     L.cmpc_ocp_debug_force_grid_timeout.argtypes = [vp, C.c_int]
@@ -586,6 +588,13 @@ class OcpSolver:
 
     def grid(self, B):
         return int(lib().cmpc_ocp_grid(self.h, int(B)))
+
+    def set_segments(self, S):
+        """cmpc_ocp_set_segments: segments of the grid form's partitioned factorisation (0 auto, 1 the serial chain)."""
+        _chk(lib().cmpc_ocp_set_segments(self.h, int(S)), "cmpc_ocp_set_segments")
+
+    def segments(self, B):
+        return int(lib().cmpc_ocp_segments(self.h, int(B)))
 
     def set_grid_timeout(self, us):
         """cmpc_ocp_set_grid_timeout: the grid barriers' wait bound in microseconds (0: the default 50 ms)."""

@@ -22,6 +22,7 @@ def run(projected, B, reps=int(os.environ.get("OCP_REPS", "5"))):
     s = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=B)
     s.set_path(int(os.environ.get("OCP_CHAIN", "1")))
     s.set_grid(int(os.environ.get("OCP_GRID", "0")))
+    s.set_segments(int(os.environ.get("OCP_SEGS", "0")))
     dx0 = cm.DeviceArray.from_host(np.array([p["x0"] for p in ps]))
     drec = cm.DeviceArray.from_host(np.array(recs))
     dcrec = cm.DeviceArray.from_host(np.array(crecs)) if not projected else None
@@ -51,7 +52,8 @@ def run(projected, B, reps=int(os.environ.get("OCP_REPS", "5"))):
     per = ms.value / reps
     print(f"{'projected' if projected else 'rows     '} B={B:5d} N={p0['N']} nx=24 nu={sorted(set(p0['nu']))} "
           f"kernel {per:8.3f} ms/solve ({B / per * 1e3:9.0f} solves/s), iters {it.mean():.2f}, "
-          f"status ok {np.mean(st == 0):.2f}; host path {th:.2f} ms; path {s.path} grid {s.grid(B)}", flush=True)
+          f"status ok {np.mean(st == 0):.2f}; host path {th:.2f} ms; path {s.path} grid {s.grid(B)} segments "
+          f"{s.segments(B)} fallbacks {s.fallback_count}", flush=True)
 
 
 if __name__ == "__main__" and "--stamps" not in sys.argv and "--chain" not in sys.argv:
@@ -72,6 +74,7 @@ def stamps(projected, B=1):
     s = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=B)
     s.set_path(int(os.environ.get("OCP_CHAIN", "1")))
     s.set_grid(int(os.environ.get("OCP_GRID", "0")))
+    s.set_segments(int(os.environ.get("OCP_SEGS", "0")))
     x0 = np.array([p["x0"] for p in ps])
     s.solve(x0, np.array(recs), np.array(crecs) if not projected else None)
     L.cmpc_ocp_debug_stamps(buf, 1)
@@ -80,8 +83,9 @@ def stamps(projected, B=1):
     names = {1: "residuals", 2: "rhs", 10: "fact:init", 11: "fact:T", 12: "fact:M", 13: "fact:prefetch",
              14: "fact:sweep", 15: "fact:store", 16: "fact:out", 20: "chain:init", 21: "chain:T", 22: "chain:M",
              23: "chain:elim", 24: "chain:out", 25: "chain:outw0", 26: "[w1 load span]", 27: "chain:e-load", 28: "grid prologue", 17: "fact:exit", 3: "acl", 4: "forward",
-             5: "post", 6: "corr rhs", 7: "backward", 8: "acl+forward (corr)", 9: "update"}
-    tot = sum(buf[i] for i in names if i != 26)  # 26: a span of wave 1, not on thread 0's timeline
+             5: "post", 6: "corr rhs", 7: "backward", 8: "acl+forward (corr)", 9: "update", 18: "part:P1+wait",
+             19: "part:combine+wait", 29: "part:P3", 30: "[wg1 chain spans]", 31: "[wg1 element spans]"}
+    tot = sum(buf[i] for i in names if i not in (26, 30, 31))  # spans of other waves / workgroups
     print(f"stamps {'projected' if projected else 'rows'} B={B} iters {it[0]} total {tot} cycles")
     for i, n in names.items():
         print(f"  {n:22s} {buf[i]:12d}  {100.0 * buf[i] / max(tot, 1):5.1f} %")
