@@ -1171,7 +1171,6 @@ __device__ __forceinline__ void ldl_solve(const double* __restrict__ F, int m, c
 }
 
 #include "ocp_chain.hpp"
-#include "ocp_part.hpp"
 
 // LDS of the latency form: G images (two), T, Paug, the pivot-column buffers and the rows' Sigma (two), then red and
 // vec; the other passes of the kernel see G0 / G1 as ABx / Tx (contiguous: the staged residuals' buffer)
@@ -1285,6 +1284,8 @@ __device__ __forceinline__ void grid_collect(const double* part, int G, int nv, 
   }
   __syncthreads();
 }
+
+#include "ocp_part.hpp"
 
 // Corrector's backward vector pass split for the grid form: (a) y_k = P_{k+1} rb_k and h_k on the owned stages
 // (p_N = g_x,N on the last workgroup), (b) the serial recursion p_k = Acl_k' p_{k+1} + h_k on workgroup 0, (c) the
@@ -1404,6 +1405,79 @@ __device__ __forceinline__ void backward_vec_pass(const View& V, const Lds& S) {
   bwd_vec_c(V, 0, N);
 }
 
+// Residuals of the Newton system an iteration solved, at its final direction (dz = (dx, du), dpi, the rows' dt, dl),
+// HPIPM's "lin res" statistics (HpipmInterface.cpp:492-501, d_ocp_qp_ipm_get_stat columns 13-16): the inf-norms of
+//   stat  H~ dz + G'dpi - Gc'(dl_l - dl_u) + r_g   (H~ the factorised Hessian: reg_prim on its diagonal),
+//   eq    A_k dx_k + B_k du_k - dx_{k+1} + r_b,
+//   ineq  Gc dz - dt_l + r_l,  -Gc dz - dt_u + r_u,
+//   comp  t_l dl_l + l_l dt_l + r_ml,  t_u dl_u + l_u dt_u + r_mu
+// over the nodes [n0, n1) and their rows [r0, r1) (local maxima; the caller reduces). r_g, r_b are the iteration's
+// residuals (rgu / rgx / rb), r_m the final direction's complementarity right-hand side; c = Gc dz goes through R_W
+// (free after the step's right-hand side).
+__device__ __forceinline__ void lin_res(const View& V, double reg, int n0, int n1, double* o) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N;
+  const double *dx = V.dx(), *du = V.du(), *dpi = V.dpi();
+  const double *dll = V.row(R_DLL), *dlu = V.row(R_DLU);
+  const int P = L.nzp + nx;
+  for (int w = n0 * P + tid; w < n1 * P; w += NT) {
+    const int k = w / P, e = w - k * P;
+    const int mk = L.nu[k], g = L.ng[k];
+    const int m1 = mk, m2 = k >= 1 ? nx : 0, m3 = k < N ? nx : 0;
+    if (e >= m1 + m2 + m3) continue;
+    const double* A = V.A(k);
+    const double* Bm = V.Bm(k);
+    const double* dxk = dx + (long long)k * nx;
+    const double* duk = du + L.cu[k];
+    const double* dpk = dpi + (long long)k * nx;
+    const int rk = L.cr[k];
+    if (e < m1) {
+      const int a = e;
+      const double *R = V.R(k), *Sm = V.S(k);
+      double s = fma(reg, duk[a], V.rgu()[L.cu[k] + a]);
+      for (int c = 0; c < mk; ++c) s = fma(R[c * mk + a], duk[c], s);
+      for (int j = 0; j < nx; ++j) s = fma(Sm[j * mk + a], dxk[j], s);
+      for (int t = 0; t < m3; ++t) s = fma(Bm[a * nx + t], dpk[t], s);
+      if (g) {
+        const double* D = V.D(k);
+        for (int j = 0; j < g; ++j) s = fma(-D[a * g + j], dll[rk + j] - dlu[rk + j], s);
+      }
+      o[0] = nmax(o[0], fabs(s));
+    } else if (e < m1 + m2) {
+      const int i = e - m1;
+      const double *Q = V.Q(k), *Sm = V.S(k);
+      double s = fma(reg, dxk[i], V.rgx()[(long long)k * nx + i] - dpi[(long long)(k - 1) * nx + i]);
+      for (int j = 0; j < nx; ++j) s = fma(Q[j * nx + i], dxk[j], s);
+      for (int a = 0; a < mk; ++a) s = fma(Sm[i * mk + a], duk[a], s);
+      for (int t = 0; t < m3; ++t) s = fma(A[i * nx + t], dpk[t], s);
+      if (g) {
+        const double* C = V.C(k);
+        for (int j = 0; j < g; ++j) s = fma(-C[i * g + j], dll[rk + j] - dlu[rk + j], s);
+      }
+      o[0] = nmax(o[0], fabs(s));
+    } else {
+      const int i = e - m1 - m2;
+      double s = V.rb()[(long long)k * nx + i] - dx[(long long)(k + 1) * nx + i];
+      for (int j = 0; j < nx; ++j) s = fma(A[j * nx + i], dxk[j], s);
+      for (int a = 0; a < mk; ++a) s = fma(Bm[a * nx + i], duk[a], s);
+      o[1] = nmax(o[1], fabs(s));
+    }
+  }
+  const int r0 = L.cr[n0], r1 = L.cr[n1 < N + 1 ? n1 : N + 1];
+  if (r1 > r0) {
+    double* c = V.row(R_W);
+    rows_value(V, dx, du, c, r0, r1);  // each thread reads back only its own rows
+    const double *rl = V.row(R_RL), *ru = V.row(R_RU), *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL),
+                 *lu = V.row(R_LU), *rml = V.row(R_RML), *rmu = V.row(R_RMU), *dtl = V.row(R_DTL),
+                 *dtu = V.row(R_DTU);
+    for (int j = r0 + tid; j < r1; j += NT) {
+      o[2] = nmax(o[2], nmax(fabs(c[j] + rl[j] - dtl[j]), fabs(ru[j] - c[j] - dtu[j])));
+      o[3] = nmax(o[3], nmax(fabs(fma(tl[j], dll[j], fma(ll[j], dtl[j], rml[j]))),
+                             fabs(fma(tu[j], dlu[j], fma(lu[j], dtu[j], rmu[j])))));
+    }
+  }
+}
+
 // (l_l - l_u) into R_W
 __device__ __forceinline__ void load_lamdiff(const View& V) {
   double* w = V.row(R_W);
@@ -1411,7 +1485,7 @@ __device__ __forceinline__ void load_lamdiff(const View& V) {
   for (int j = threadIdx.x; j < V.L.m; j += NT) w[j] = ll[j] - lu[j];
 }
 
-template <int NZP, int MINB, bool FAST>
+template <int NZP, int MINB, bool FAST, bool LINRES = false>
 __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds& S, const ChainLds& CS) {
   const View V(a, q);
   const OcpLayout& L = a.L;
@@ -1481,6 +1555,8 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
     const double mu = m > 0 ? musum / (2.0 * m) : 0.0;
     OCP_STAMP(1);
     double* sr = (a.stats && it < a.stat_rows) ? a.stats + ((long long)q * a.stat_rows + it) * 10 : nullptr;
+    if (sr && tid == 0 && a.linres)
+      for (int c = 0; c < 4; ++c) a.linres[((long long)q * a.stat_rows + it) * 4 + c] = __builtin_nan("");
     if (sr && tid == 0) {
       for (int c = 0; c < 5; ++c) sr[c] = __builtin_nan("");
       sr[5] = mu;
@@ -1593,6 +1669,17 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
       alpha = fmin(1.0, TAU_OCP * amax);
     }
     if (sr && tid == 0) sr[3] = sr[4] = alpha;
+    if (LINRES && a.linres && it < a.stat_rows) {  // the Newton system's residuals at the final direction (cmpc_ocp_set_linres)
+      double lr[4] = {0.0, 0.0, 0.0, 0.0};
+      __syncthreads();
+      lin_res(V, a.reg, 0, N + 1, lr);
+      double* lo = a.linres + ((long long)q * a.stat_rows + it) * 4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double v = block_reduce(lr[c], S.red, OpMax());
+        if (tid == 0) lo[c] = v;
+      }
+    }
     if (alpha < a.alpha_min) {
       status = 2;
       break;
@@ -1641,6 +1728,9 @@ __device__ __forceinline__ void ipm_body(const OcpSolveArgs& a, int q, const Lds
   if (a.stats)  // rows after the last iteration: NaN (cmpc.h)
     for (int e = tid; e < (a.stat_rows - it - 1) * 10; e += NT)
       a.stats[((long long)q * a.stat_rows + it + 1) * 10 + e] = __builtin_nan("");
+  if (a.linres)  // rows after the last iteration: NaN (the last one's is NaN unless it computed a direction)
+    for (int e = tid; e < (a.stat_rows - it - 1) * 4; e += NT)
+      a.linres[((long long)q * a.stat_rows + it + 1) * 4 + e] = __builtin_nan("");
 }
 
 // MINB workgroups per CU: 1 (the whole register file for one problem's chain: the lowest latency, B <= #CUs) or 2
@@ -1769,57 +1859,66 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   double* segq = a.seg ? a.seg + (long long)q * a.seg_stride : nullptr;
   const int nseg = (FAST && segq) ? part_segments(a.nseg, G, N) : 1;
   auto factor_grid = [&]() __attribute__((always_inline)) -> bool {
-    // phase 0: P1; 1: P3; 2: the serial chain on workgroup 0 (one segment, or the fallback). One chain_factor call
-    // site for all of them (each inlined copy of the chain costs registers).
-    const int cb = seg_begin(N, nseg, g), ce = seg_begin(N, nseg, g + 1);
+    if (nseg <= 1) {  // the serial chain on workgroup 0
+      if (lead) {
+        const bool fok = chain_factor(V, CS, hp, a.reg);
+        if (tid == 0) mine[5] = fok ? 0.0 : 1.0;
+      } else if (tid == 0) {
+        mine[5] = 0.0;
+      }
+      return true;
+    }
+    // phase 0 = P1: the last segment from the terminal node, the middle ones from a zero end value (then their
+    // elements); phase 1 = P3: segments 0 .. nseg-2 from their end node's exact value, or (a dropped pivot in the
+    // first pass, a NaN or a failed combine) the serial chain on workgroup 0. One chain_factor call site (each inlined
+    // copy of the chain costs registers); workgroups g >= nseg only take part in the barriers.
+    const int cb = seg_begin(N, nseg, g < nseg ? g : nseg), ce = seg_begin(N, nseg, g < nseg ? g + 1 : nseg);
     const bool mid = g >= 1 && g < nseg - 1;
-    int fl = 0;
-    int ph = nseg > 1 ? 0 : 2;
-    while (true) {
+    int f = 0;
+    bool pok = true;
+    for (int ph = 0; ph < 2; ++ph) {
       bool run;
-      int k0 = 0, k1 = N, term = CH_TERM_NODE;
+      int k0 = cb, k1 = ce, term = CH_TERM_ZERO;
       const double* Pt = nullptr;
       if (ph == 0) {
         run = g >= 1 && g < nseg;
-        k0 = cb;
-        k1 = g == nseg - 1 ? N : ce;
-        term = g == nseg - 1 ? CH_TERM_NODE : CH_TERM_ZERO;
-      } else if (ph == 1) {
+        if (g == nseg - 1) {
+          k1 = N;
+          term = CH_TERM_NODE;
+        }
+      } else if (pok) {
         run = g < nseg - 1;
-        k0 = cb;
-        k1 = ce;
         term = CH_TERM_GIVEN;
         Pt = segq + OCP_GRID_MAX_G * seg_esz(nx) + (g + 1) * seg_bsz(nx);
       } else {
         run = lead;
+        k0 = 0;
+        k1 = N;
+        term = CH_TERM_NODE;
       }
       OCP_SPAN_BEGIN(t_ch);
-      const int f = run ? chain_factor(V, CS, hp, a.reg, k0, k1, term, Pt, Pt ? Pt + nx * nx : nullptr) : 0;
+      f = run ? chain_factor<true>(V, CS, hp, a.reg, k0, k1, term, Pt, Pt ? Pt + nx * nx : nullptr) : 0;
       OCP_SPANG_END(30, t_ch, 1);
-      if (ph != 0) {
-        OCP_STAMP(29);
-        fl = f;
-        break;
-      }
+      if (ph == 1) break;
       OCP_SPAN_BEGIN(t_el);
-      if (f == 0 && mid) seg_element(V, S, CS.Ml, cb, ce, segq + g * seg_esz(nx));
+      if (f == 0 && mid) f |= seg_element(V, CS, cb, ce, segq + g * seg_esz(nx));
       OCP_SPANG_END(31, t_el, 1);
       if (tid == 0) mine[4] = (double)f;
       if (!sync()) return false;
       grid_collect(part + 4, G, 1, ops_max, red);
       OCP_STAMP(18);
-      bool pok = red[0] == 0.0;
-      if (pok) {
-        const bool cok = lead ? seg_combine(V, CS.Ml, segq, nseg, N) : true;
+      pok = red[0] == 0.0;
+      if (pok) {  // P2: the boundary values on workgroup 0
+        const bool cok = lead ? seg_combine(V, CS, segq, nseg, N) : true;
         if (tid == 0) mine[6] = cok ? 0.0 : 1.0;
         if (!sync()) return false;
         grid_collect(part + 6, G, 1, ops_max, red);
         pok = red[0] == 0.0;
       }
       OCP_STAMP(19);
-      ph = pok ? 1 : 2;  // a dropped pivot in the first pass, a NaN or a failed combine: the serial chain
     }
-    if (tid == 0) mine[5] = (fl & CH_NAN) ? 1.0 : 0.0;
+    OCP_STAMP(29);
+    if (tid == 0) mine[5] = (f & CH_NAN) ? 1.0 : 0.0;
     return true;
   };
   if (FAST) {  // this workgroup's stages' constant Hessian blocks (read by workgroup 0's chain after a barrier)
@@ -1871,7 +1970,13 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   OCP_STAMP(28);
   int status = 1, it = 0;
   double rs = 0, re = 0, ri = 0, rc = 0;
+  // keep_riccati: the factorisation at the exit point (with rows; or without a step taken) runs through this loop's
+  // factor phase once more (ric_pass), so the kernel carries one copy of the factorisation code
+  bool ric_pass = false, rok = false;
   for (it = 0; alive; ++it) {
+   double mu = 0.0;
+   double* sr = nullptr;
+   if (!ric_pass) {
     // --- residuals (owned nodes / rows), reduced over the grid ---
     rows_value(V, x, u, V.row(R_C), R.r0, R.r1);
     {
@@ -1928,8 +2033,10 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     re = red[1];
     ri = red[2];
     rc = red[3];
-    const double mu = m > 0 ? red[4] / (2.0 * m) : 0.0;
-    double* sr = (lead && a.stats && it < a.stat_rows) ? a.stats + ((long long)q * a.stat_rows + it) * 10 : nullptr;
+    mu = m > 0 ? red[4] / (2.0 * m) : 0.0;
+    sr = (lead && a.stats && it < a.stat_rows) ? a.stats + ((long long)q * a.stat_rows + it) * 10 : nullptr;
+    if (sr && tid == 0 && a.linres)
+      for (int c = 0; c < 4; ++c) a.linres[((long long)q * a.stat_rows + it) * 4 + c] = __builtin_nan("");
     if (sr && tid == 0) {
       for (int c = 0; c < 5; ++c) sr[c] = __builtin_nan("");
       sr[5] = mu;
@@ -1938,22 +2045,30 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       sr[8] = ri;
       sr[9] = rc;
     }
-    if (!(isfinite(rs) && isfinite(re) && isfinite(ri) && isfinite(rc))) {
-      status = 3;
-      break;
-    }
-    if (rs <= a.tol_stat && re <= a.tol_eq && ri <= a.tol_ineq && rc <= a.tol_comp) {
-      status = 0;
-      break;
-    }
-    if (it >= a.iter_max) {
-      status = 1;
-      break;
-    }
-    if (m > 0 && !(mu > 1e-300)) {
-      status = 2;
-      break;
-    }
+    int ex = -1;
+    if (!(isfinite(rs) && isfinite(re) && isfinite(ri) && isfinite(rc))) ex = 3;
+    else if (rs <= a.tol_stat && re <= a.tol_eq && ri <= a.tol_ineq && rc <= a.tol_comp) ex = 0;
+    else if (it >= a.iter_max) ex = 1;
+    else if (m > 0 && !(mu > 1e-300)) ex = 2;
+    if (ex >= 0) {
+      status = ex;
+      // the exit point's factorisation for keep_riccati: with rows at the exit point's Sigma; without rows the last
+      // Newton step's factorisation is the exit point's (kept as it is), unless no step was taken
+      if (!(a.ric && status != 3 && (m > 0 || it == 0))) break;
+      ric_pass = true;
+      {  // Sigma and the rows' step term at the exit iterate (complementarity kept), the step's right-hand side
+        const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
+                     *ru = V.row(R_RU);
+        double *sig = V.row(R_SIG), *w = V.row(R_W);
+        for (int j = R.r0 + tid; j < R.r1; j += NT) {
+          sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
+          w[j] = ll[j] * rl[j] / tl[j] - lu[j] * ru[j] / tu[j];
+        }
+      }
+      __syncthreads();
+      step_rhs_range(V, R.k0, R.k1, R.n1);
+      if (!sync()) break;
+    } else {
     // --- predictor right-hand side (owned rows / nodes) ---
     {
       const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
@@ -1969,6 +2084,8 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     __syncthreads();
     step_rhs_range(V, R.k0, R.k1, R.n1);
     if (!sync()) break;
+    }
+   }
     OCP_STAMP(2);
     // --- factorisation: the partitioned chain over the grid (FAST; nseg = 1: the serial chain on workgroup 0) ---
     if constexpr (FAST) {
@@ -1982,6 +2099,10 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     if (!sync()) break;
     grid_collect(part + 5, G, 1, ops_max, red);
     OCP_STAMP(17);
+    if (ric_pass) {
+      rok = red[0] == 0.0;
+      break;
+    }
     if (red[0] != 0.0) {
       status = 3;
       break;
@@ -2096,49 +2217,11 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   if (a.ric && alive && status != 3) {
     // Without rows the last Newton step's factorisation is the exit point's (no Sigma): the solve keeps its P_k, K_k,
     // Lr_k only (factor-only; the exit point's p_k, kff_k and the stage-0 rebuild come from cmpc_ocp_riccati's
-    // refactorisation when asked for, the MPC's feedback policy needs none of them). With rows the factorisation is
-    // redone at the exit point's Sigma and everything is kept.
+    // refactorisation when asked for, the MPC's feedback policy needs none of them). With rows (or when no step was
+    // taken) the loop's last pass refactorised at the exit point (ric_pass) and everything is kept.
     const bool fonly = m == 0;
-    // Sigma and the rows' step term at the exit iterate (complementarity kept), the step's right-hand side
-    if (!fonly || it == 0) {
-      const double *tl = V.row(R_TL), *tu = V.row(R_TU), *ll = V.row(R_LL), *lu = V.row(R_LU), *rl = V.row(R_RL),
-                   *ru = V.row(R_RU);
-      double *sig = V.row(R_SIG), *w = V.row(R_W);
-      for (int j = R.r0 + tid; j < R.r1; j += NT) {
-        sig[j] = ll[j] / tl[j] + lu[j] / tu[j];
-        w[j] = ll[j] * rl[j] / tl[j] - lu[j] * ru[j] / tu[j];
-      }
-      __syncthreads();
-      step_rhs_range(V, R.k0, R.k1, R.n1);
-      sync();
-    }
-    // the factorisation at the exit point (with rows, or when no step was taken: no factorisation to keep)
-    const bool full = m > 0 || it == 0;
-    if (full) {
-      if constexpr (FAST) {
-        (void)factor_grid();
-      } else if (lead) {
-        const bool fok = factor_pass<64>(V, S, a.reg);
-        if (tid == 0) mine[5] = fok ? 0.0 : 1.0;
-      } else if (tid == 0) {
-        mine[5] = 0.0;
-      }
-    } else if (!fonly) {
-      bwd_vec_a(V, R.k0, R.k1, last);
-      sync();
-      if (lead) {
-        if constexpr (FAST) chain_affine<true>(V, CS, S.vec, S.vec + 64);
-        else bwd_vec_b(V, S);
-      }
-      sync();
-      bwd_vec_c(V, R.k0, R.k1);
-      if (tid == 0) mine[5] = 0.0;
-    } else if (tid == 0) {
-      mine[5] = 0.0;
-    }
-    sync();
-    grid_collect(part + 5, G, 1, ops_max, red);
-    const bool rok = alive && red[0] == 0.0;
+    const bool full = ric_pass;
+    if (!full) rok = true;
     if (FAST && full) {
       chain_gains(V, R.k0, R.k1);
       __syncthreads();
@@ -2211,6 +2294,9 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     if (a.stats)  // rows after the last iteration: NaN (cmpc.h)
       for (int r = it + 1; r < a.stat_rows; ++r)
         for (int c = 0; c < 10; ++c) a.stats[((long long)q * a.stat_rows + r) * 10 + c] = __builtin_nan("");
+    if (a.linres)  // rows after the last iteration: NaN (the last one's is NaN unless it computed a direction)
+      for (int r = it + 1; r < a.stat_rows; ++r)
+        for (int c = 0; c < 4; ++c) a.linres[((long long)q * a.stat_rows + r) * 4 + c] = __builtin_nan("");
   }
   // the barrier words back to zero for the next launch (no memset launch before it): every workgroup counts itself
   // out after its last barrier; the last one out resets the counter, the fail word and the out-count (nobody polls
@@ -2246,6 +2332,17 @@ __global__ __launch_bounds__(NT, MINB) void k_ocp_ipm(OcpSolveArgs a) {
   OCP_STAMP_BEGIN();
   ipm_body<NZP, MINB, FAST>(a, blockIdx.x, S, CS);
   OCP_STAMP_END();
+}
+
+// The statistics solve (cmpc_ocp_set_linres: HPIPM's lin res columns of the verbose table): one workgroup per problem,
+// the batched form's factorisation, the Newton systems' residuals recorded per iteration. A separate instantiation, so
+// the solves' kernels carry none of it (the same iteration; trajectories equal the other forms' to rounding).
+template <int NZP>
+__global__ __launch_bounds__(NT, 1) void k_ocp_ipm_linres(OcpSolveArgs a) {
+  extern __shared__ double smem[];
+  ChainLds CS{};
+  const Lds S = carve(smem, a.L, NZP);
+  ipm_body<NZP, 1, false, true>(a, blockIdx.x, S, CS);
 }
 
 // Riccati quantities at the exit point (see k_ocp.hpp / cmpc.h cmpc_ocp_riccati) of problem q, one workgroup
@@ -2469,6 +2566,15 @@ int launch_ocp_ipm(const OcpSolveArgs& a0, int B, hipStream_t stream) {
   OcpSolveArgs a = a0;
   a.par_res = B <= OCP_PAR_RES_MAX ? 1 : 0;
   const size_t lc = ocp_chain_lds_bytes(a.L, a.L.numax);
+  if (a.linres) {  // the statistics solve (k_ocp_ipm_linres)
+    a.fast = 0;
+    const size_t l0 = ocp_lds_bytes(a.L);
+    const void* kf = a.L.nzp == 64 ? (const void*)k_ocp_ipm_linres<64> : (const void*)k_ocp_ipm_linres<128>;
+    if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l0) != hipSuccess) return -1;
+    if (a.L.nzp == 64) hipLaunchKernelGGL(k_ocp_ipm_linres<64>, dim3(B), dim3(NT), l0, stream, a);
+    else hipLaunchKernelGGL(k_ocp_ipm_linres<128>, dim3(B), dim3(NT), l0, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   a.fast = (a0.fast && a0.hp && lc > 0 && B <= OCP_ONE_PER_CU_MAX) ? 1 : 0;
   size_t lds = ocp_lds_bytes(a.L);
   if (a.fast && lc > lds) lds = lc;

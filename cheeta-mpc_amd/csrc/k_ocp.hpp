@@ -71,6 +71,7 @@ struct OcpSolveArgs {
   int* iters;          // [B]
   double* res;         // [B][4]
   double* stats;       // [B][stat_rows][10] or nullptr
+  double* linres;      // [B][stat_rows][4] or nullptr: HPIPM's lin res stat / eq / ineq / comp (cmpc_ocp_set_linres)
   int stat_rows;
   int iter_max;
   int warm;  // Settings.warm_start: x (nodes >= 1), u start from x / u (HPIPM's primal warm start)

@@ -29,7 +29,7 @@ struct cmpc_ocp {
   cmpc_settings s{};
   OcpLayout L{};
   size_t rec_size = 0, crec_size = 0;
-  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart, fbk, seg;
+  DBuf dims, ws, x0, rec, crec, x, u, res, stats, status, iters, rst, P, p, K, k, Lr, hp, bar, gpart, fbk, seg, linres;
   long long hp_stride = 0;
   int hp_batch = 0, chain = 1;  // chain: cmpc_ocp_set_path (1 = the latency form where it applies, 0 = never)
   int grid = 0;                 // cmpc_ocp_set_grid: workgroups per problem of the grid form (0 auto, 1 off)
@@ -38,6 +38,7 @@ struct cmpc_ocp {
   int force_timeout = 0;        // cmpc_ocp_debug_force_grid_timeout
   int broken = 0;               // a failed (re-)layout left the buffers inconsistent: solves are refused
   int nseg = 0;                 // cmpc_ocp_set_segments: segments of the grid form's factorisation (0 auto)
+  int linres_on = 0;            // cmpc_ocp_set_linres: the solves record the Newton systems' residuals
   long long seg_stride = 0;     // doubles per problem of the segment buffer
   void* pin = nullptr;          // pinned host staging of cmpc_ocp_solve_host / _riccati_host (small batches)
   size_t pin_cap = 0;
@@ -191,7 +192,8 @@ size_t vbytes(const std::vector<T>& v) {
 
 void free_all(cmpc_ocp* o) {
   for (DBuf* b : {&o->dims, &o->ws, &o->x0, &o->rec, &o->crec, &o->x, &o->u, &o->res, &o->stats, &o->status,
-                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart, &o->fbk, &o->seg})
+                  &o->iters, &o->rst, &o->P, &o->p, &o->K, &o->k, &o->Lr, &o->hp, &o->bar, &o->gpart, &o->fbk, &o->seg,
+                  &o->linres})
     if (b->p) (void)hipFree(b->p);
   if (o->pin) (void)hipHostFree(o->pin);
   if (o->ev_done) (void)hipEventDestroy(o->ev_done);
@@ -256,7 +258,9 @@ int grow_pin(cmpc_ocp* o, size_t need) {
 
 int alloc_stats(cmpc_ocp* o) {
   o->stat_rows = o->s.iter_max + 1;
-  return grow(o, o->stats, sizeof(double) * (size_t)o->max_batch * o->stat_rows * CMPC_STAT_COLS);
+  int r = grow(o, o->stats, sizeof(double) * (size_t)o->max_batch * o->stat_rows * CMPC_STAT_COLS);
+  if (r == CMPC_OK && o->linres_on) r = grow(o, o->linres, sizeof(double) * (size_t)o->max_batch * o->stat_rows * 4);
+  return r;
 }
 
 // (Re-)lay out the handle for dimensions (N, nx, nu, nc): every device buffer grows to the new size if it exceeds its
@@ -380,6 +384,7 @@ cmpc::OcpSolveArgs solve_args(cmpc_ocp* o, const double* x0, const double* rec, 
   a.iters = iters;
   a.res = (double*)o->res.p;
   a.stats = (double*)o->stats.p;
+  a.linres = o->linres_on ? (double*)o->linres.p : nullptr;
   a.stat_rows = o->stat_rows;
   a.iter_max = o->s.iter_max;
   a.warm = (o->s.warm_start != 0 && x && u) ? 1 : 0;
@@ -618,7 +623,7 @@ int cmpc_ocp_solve(cmpc_ocp* o, int B, const double* d_x0, const double* d_rec, 
   o->last_rec = d_rec;
   o->last_crec = d_crec;
   o->last_status = d_status;
-  o->ric_B = (a.ric && cmpc_ocp_grid(o, B) > 0) ? B : 0;
+  o->ric_B = (a.ric && !o->linres_on && cmpc_ocp_grid(o, B) > 0) ? B : 0;  // the statistics solve keeps none
   o->ric_full = o->L.m > 0 ? 1 : 0;  // without rows the kernel keeps the factorisation only (k_ocp.hip, exit block)
   return CMPC_OK;
 }
@@ -820,6 +825,34 @@ int cmpc_ocp_get_residuals(cmpc_ocp* o, int B, double* d_res, void* stream) {
 }
 
 int cmpc_ocp_stat_rows(const cmpc_ocp* o) { return o ? o->stat_rows : CMPC_ERR_ARG; }
+
+int cmpc_ocp_set_linres(cmpc_ocp* o, int on) {
+  if (!o || on < 0 || on > 1) return CMPC_ERR_ARG;
+  if (o->ev_done) (void)hipEventSynchronize(o->ev_done);
+  o->linres_on = on;
+  return on ? alloc_stats(o) : CMPC_OK;
+}
+
+int cmpc_ocp_get_linres(cmpc_ocp* o, int B, double* d_linres, void* stream) {
+  if (!o || B < 0 || B > o->max_batch || !d_linres || !o->linres_on) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  if (hipStreamWaitEvent((hipStream_t)stream, o->ev_done, 0) != hipSuccess) return CMPC_ERR_HIP;
+  return hipMemcpyAsync(d_linres, o->linres.p, sizeof(double) * B * o->stat_rows * 4, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream) == hipSuccess
+             ? CMPC_OK
+             : CMPC_ERR_HIP;
+}
+
+int cmpc_ocp_get_linres_host(cmpc_ocp* o, int B, double* linres) {
+  if (!o || B < 0 || B > o->max_batch || !linres || !o->linres_on) return CMPC_ERR_ARG;
+  if (B == 0) return CMPC_OK;
+  if (hipStreamWaitEvent(o->stream, o->ev_done, 0) != hipSuccess ||
+      hipMemcpyAsync(linres, o->linres.p, sizeof(double) * B * o->stat_rows * 4, hipMemcpyDeviceToHost, o->stream) !=
+          hipSuccess ||
+      hipStreamSynchronize(o->stream) != hipSuccess)
+    return CMPC_ERR_HIP;
+  return CMPC_OK;
+}
 
 int cmpc_ocp_get_stats(cmpc_ocp* o, int B, double* d_stats, void* stream) {
   if (!o || B < 0 || B > o->max_batch || !d_stats) return CMPC_ERR_ARG;

@@ -271,7 +271,7 @@ __device__ __forceinline__ void chain_m(const ChainLds& S, int nx, const int* d,
 // select), stores the factor's columns, and applies the rank-2 update to every entry (entries in processed rows /
 // columns are dead: never read again). A missing second pivot (odd nu_k) has 1 / d1 = 0, which leaves the update's
 // second term exactly 0.
-template <int NB, int A0>
+template <int NB, int A0, bool WEAK>
 __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&bi)[NB], const int (&bj)[NB],
                                             const bool (&on)[NB], int j, int mk, int n1, double* c0, double* c1,
                                             double* F, bool& bad, bool& weak) {
@@ -296,7 +296,7 @@ __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&b
   const double d1 = fma(-a1, l1, e1);
   bad = bad || (two && d1 != d1);
   const double d1i = (two && d1 > 1e-200) ? 1.0 / d1 : 0.0;
-  weak = weak || !(d0 > 1e-200) || (two && !(d1 > 1e-200));
+  if (WEAK) weak = weak || !(d0 > 1e-200) || (two && !(d1 > 1e-200));
   // the factor's columns into the F image (rows >= j; chain_out reads column j + 1 from row j + 1)
   if (lane >= j && lane < n1) {
     const double v0 = c0[lane];
@@ -330,7 +330,7 @@ __device__ __forceinline__ void chain_round(double (&m)[NB][4][4], const int (&b
 // what the two pair rounds (j, j + 1) and (j + 2, j + 3) compute: every lane forms the second pair's columns for its
 // own rows and columns from the published pre-round values with the owners' fma sequence, and applies the two rank-2
 // updates in the same order, so the results are bit-identical with half the publish / read-back latency chains.
-template <int NB>
+template <int NB, bool WEAK>
 __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&bi)[NB], const int (&bj)[NB],
                                              const bool (&on)[NB], int j, int n1, double* cb, double* F, bool& bad,
                                              bool& weak) {
@@ -383,7 +383,7 @@ __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&
   const double d3 = fma(-a3, l3, e3);
   bad = bad || (d3 != d3);
   const double d3i = d3 > 1e-200 ? 1.0 / d3 : 0.0;
-  weak = weak || !(d0 > 1e-200) || !(d1 > 1e-200) || !(e2 > 1e-200) || !(d3 > 1e-200);
+  if (WEAK) weak = weak || !(d0 > 1e-200) || !(d1 > 1e-200) || !(e2 > 1e-200) || !(d3 > 1e-200);
   // the factor's columns j .. j + 3 (rows >= j): c0, c1~, the updated column j + 2 and its c~ for j + 3
   if (lane >= j && lane < n1) {
     const double x0 = c0[lane], x1 = c1[lane], x2 = c2[lane], x3 = c3[lane];
@@ -452,11 +452,11 @@ __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&
 // (C) on wave 0: NB 4 x 4 lower blocks of M per lane (block beta = lane + 64 q), the pair rounds, the outputs.
 // Returns the pivots' flags: CH_NAN (a NaN pivot), CH_WEAK (a pivot the guard dropped, d <= 1e-200).
 constexpr int CH_NAN = 1, CH_WEAK = 2;
-template <int NB>
-__device__ __forceinline__ int chain_elim(const View& V, const ChainLds& S, const int* d, double* F, double* PaW) {
+template <int NB, bool WEAK>
+__device__ __forceinline__ int chain_elim(const View& V, const ChainLds& S, int mk, double* F, double* PaW) {
   const OcpLayout& L = V.L;
   const int lane = threadIdx.x, nx = L.nx;
-  const int mk = d[0], nz = mk + nx, n1 = nz + 1, nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
+  const int nz = mk + nx, n1 = nz + 1, nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
   bool bad = false, weak = false;
   int bi[NB], bj[NB];
   bool on[NB];
@@ -487,10 +487,10 @@ __device__ __forceinline__ int chain_elim(const View& V, const ChainLds& S, cons
   OCP_STAMP(27);
   for (int j = 0; j < mk; j += 4) {
     if (j + 4 <= mk) {
-      chain_round4<NB>(m, bi, bj, on, j, n1, S.C, F, bad, weak);
+      chain_round4<NB, WEAK>(m, bi, bj, on, j, n1, S.C, F, bad, weak);
     } else {
-      chain_round<NB, 0>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad, weak);
-      if (j + 2 < mk) chain_round<NB, 2>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad, weak);
+      chain_round<NB, 0, WEAK>(m, bi, bj, on, j, mk, n1, c0, c1, F, bad, weak);
+      if (j + 2 < mk) chain_round<NB, 2, WEAK>(m, bi, bj, on, j + 2, mk, n1, c0, c1, F, bad, weak);
     }
   }
   OCP_STAMP(23);
@@ -577,7 +577,10 @@ __device__ __forceinline__ void chain_gains(const View& V, int k0, int k1) {
 //   CH_TERM_GIVEN V_k1(x) = x'Pt x / 2 + pt'x (Pt column-major nx x nx, pt [nx]; the partitioned form's second pass).
 // Writes P_k, pv_k (k = k0..k1-1), the LDL' columns Lf_k and the factor's x / rhs rows (chain_gains turns them into
 // K_k, kf_k). Returns the pivots' flags of all four waves (CH_NAN, CH_WEAK), workgroup-uniform.
+// PART = false: the serial chain (k0 = 0, k1 = N, CH_TERM_NODE; no guarded-pivot flag), the form the solve's own loop
+// inlines; PART = true: any range and end value (ocp_part.hpp, compiled in its own function).
 constexpr int CH_TERM_NODE = 0, CH_TERM_ZERO = 1, CH_TERM_GIVEN = 2;
+template <bool PART>
 __device__ __forceinline__ int chain_factor(const View& V, const ChainLds& S, const double* hp, double reg, int k0,
                                             int k1, int term, const double* Pt, const double* pt) {
   const OcpLayout& L = V.L;
@@ -729,8 +732,8 @@ __device__ __forceinline__ int chain_factor(const View& V, const ChainLds& S, co
     // --- (C) wave 0: the elimination and the outputs; waves 1-3: stage k - 1's operands ---
     if (wave == 0) {
       const int nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
-      if (nt4 <= 64) flags |= chain_elim<1>(V, S, d, Fw, PaW);
-      else flags |= chain_elim<2>(V, S, d, Fw, PaW);  // nt4 <= 120: n1 <= 60 (OCP_CHAIN_MAX_N1, ocp_chain_lds_bytes)
+      if (nt4 <= 64) flags |= chain_elim<1, PART>(V, S, d[0], Fw, PaW);
+      else flags |= chain_elim<2, PART>(V, S, d[0], Fw, PaW);  // nt4 <= 120: n1 <= 60 (OCP_CHAIN_MAX_N1, ocp_chain_lds_bytes)
       OCP_STAMP(25);
     } else if (k > k0) {
       OCP_SPAN_BEGIN(t_load);
@@ -754,7 +757,7 @@ __device__ __forceinline__ int chain_factor(const View& V, const ChainLds& S, co
 
 // The whole horizon from the terminal node (the serial chain); returns false on a NaN pivot
 __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, const double* hp, double reg) {
-  return (chain_factor(V, S, hp, reg, 0, V.L.N, CH_TERM_NODE, nullptr, nullptr) & CH_NAN) == 0;
+  return (chain_factor<false>(V, S, hp, reg, 0, V.L.N, CH_TERM_NODE, nullptr, nullptr) & CH_NAN) == 0;
 }
 
 // The Newton step's serial affine recursions on wave 0, their operands staged in LDS a chunk of stages ahead by waves

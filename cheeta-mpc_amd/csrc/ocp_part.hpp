@@ -14,8 +14,14 @@
 //      x_b = Phi x_a + f + sum Phi(b, k+1) B_k v_k, so for the true value function V_b(x) = x'P_b x / 2 + p_b'x the
 //      minimum over v gives V_a exactly:
 //        P_a = P^0_a + Phi' P_b X_Phi,   p_a = p^0_a + Phi' P_b X_f + X_Phi' p_b,   [X_Phi X_f] = (I + W P_b)^-1 [Phi f].
-//   P2 (workgroup 0): that combine, backward from the last segment's value at c_{S-1} down to c_1 (S - 2 steps, each a
-//      Gauss-Jordan solve of the nx x nx system with partial pivoting): the exact value function at every boundary.
+//      With W = Gw Gw' (its Cholesky factor, formed by the segment's workgroup) and Woodbury, the same combine reads
+//        P_a = D - C' N^-1 C,  p_a = e - C' N^-1 g,  N = I + Gw' P_b Gw,  C = Gw' P_b Phi,  D = P^0_a + Phi' P_b Phi,
+//        g = Gw' h,  e = p^0_a + Phi' h,  h = P_b f + p_b,
+//      i.e. the Schur complement of the symmetric positive definite pivot block N (eigenvalues >= 1) in
+//        M = U' P_b U + [I 0 Gw'p_b; 0 P^0_a p^0_a + Phi'p_b; . . 0],  U = [Gw Phi f]:
+//      exactly the elimination a chain stage performs (chain_elim on wave 0, nx pivots, no pivoting needed).
+//   P2 (workgroup 0): that combine, backward from the last segment's value at c_{S-1} down to c_1 (S - 2 steps: two
+//      products and one chain_elim each): the exact value function at every boundary.
 //   P3 (segments 0 .. S-2 at once): the chain again over the segment from its end node's exact value: every stage's
 //      P_k, p_k, LDL' factor and gains are the factorisation of the serial chain, up to rounding.
 // The serial depth is ~2 N / S chain stages plus S - 2 combines instead of N stages. A pivot the first pass's guard
@@ -25,7 +31,7 @@
 
 __device__ __forceinline__ int seg_begin(int N, int S, int s) { return (int)((long long)N * s / S); }
 
-// Per-problem segment buffer (OcpSolveArgs::seg, doubles): element s (Phi, W column-major nx x nx, f [nx]) at
+// Per-problem segment buffer (OcpSolveArgs::seg, doubles): element s (U = [Gw Phi f], column-major nx x (2 nx + 1)) at
 // s * seg_esz(nx); the boundary value of node c_j (P column-major, p) at OCP_GRID_MAX_G * seg_esz(nx) + j * seg_bsz(nx)
 // (seg_esz / seg_bsz: k_ocp.hpp)
 
@@ -38,149 +44,283 @@ __device__ __forceinline__ int part_segments(int want, int G, int N) {
   return S < 1 ? 1 : S;
 }
 
-// P1 of a middle segment [a, b) after its chain from V_b = 0 (workgroup-wide; scr: LDS scratch of ChainLds::Ml):
-// the gains and closed loop of the pass (chain_gains, acl_pass into the workspace, overwritten by P3), Yt_k =
-// B_k L_k^-T D_k^-1/2 into K_k's storage (M^0_uu,k = L D L' from the LDL' columns F = L D, guarded pivots 0), then
-// Phi, f, W by the backward accumulation, into el
-__device__ __forceinline__ void seg_element(const View& V, const Lds& S, double* scr, int a, int b, double* el) {
-  const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx;
-  chain_gains(V, a, b);
-  __syncthreads();
-  acl_pass(V, S, true, a, b, true);
-  {
-    // one (stage, row) item per thread, its y in an LDS slot (the items in chunks that fit the scratch)
-    const int slot = L.numax > 0 ? L.numax : 1, items = (b - a) * nx;
-    const int chunk = CH_SCRATCH / slot < NT ? CH_SCRATCH / slot : NT;
-    for (int base = 0; base < items; base += chunk) {
-      const int e = base + tid;
-      if (tid < chunk && e < items) {
-        const int k = a + e / nx, r = e - (e / nx) * nx, mk = L.nu[k];
-        const double* __restrict__ F = V.Lf(k);
-        const double* __restrict__ Bk = V.Bm(k);
-        double* __restrict__ Yt = V.K(k);
-        double* yd = scr + tid * slot;  // y_c / d_c
-        for (int qq = 0; qq < mk; ++qq) {  // y L' = b (L(q, c) = F(q, c) / d_c): y_q = b_q - sum_{c<q} F(q, c) y_c / d_c
-          double s = Bk[qq * nx + r];
-          for (int c = 0; c < qq; ++c) s = fma(-F[c * mk + qq], yd[c], s);
-          const double d = F[qq * mk + qq];
-          const double di = d > 1e-200 ? 1.0 / d : 0.0;
-          yd[qq] = s * di;
-          Yt[r * mk + qq] = s * sqrt(di);
-        }
+// 2 x 2 output block (i0, j0) of sum_{t<K} A(i, t) B(t, j), A(i, t) = A[i ai + t at], B(t, j) = B[t bt + j bj] (LDS
+// operands), added to c. The loads of 8 consecutive t are issued before their fmas (one LDS round trip per 8 t: these
+// small products are latency-bound with one wave per SIMD). A row / column past m / n reads row / column m-1 / n-1
+// (the caller does not store it); the fma order over t is fixed, so the (i, j) entry of one block and the (j, i) entry
+// of the transposed product's block are the same fma chain.
+__device__ __forceinline__ void blk2(const double* A, int ai, int at, const double* B, int bt, int bj, int i0, int j0,
+                                     int m, int n, int K, double (&c)[2][2]) {
+  const int i1 = i0 + 1 < m ? i0 + 1 : i0, j1 = j0 + 1 < n ? j0 + 1 : j0;
+  for (int t0 = 0; t0 < K; t0 += 8) {
+    double a0[8], a1[8], b0[8], b1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u < K ? t0 + u : K - 1;
+      a0[u] = A[i0 * ai + t * at];
+      a1[u] = A[i1 * ai + t * at];
+      b0[u] = B[t * bt + j0 * bj];
+      b1[u] = B[t * bt + j1 * bj];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (t0 + u < K) {
+        c[0][0] = fma(a0[u], b0[u], c[0][0]);
+        c[0][1] = fma(a0[u], b1[u], c[0][1]);
+        c[1][0] = fma(a1[u], b0[u], c[1][0]);
+        c[1][1] = fma(a1[u], b1[u], c[1][1]);
       }
-      __syncthreads();
     }
   }
-  // backward accumulation over the segment's stages; each stage's operands [Acl_k | Yt_k | bcl_k] staged in LDS, the
-  // next stage's loaded into registers meanwhile (no global latency inside the products)
-  const int osz = nxx + nx * (L.numax > 0 ? L.numax : 1) + nx;  // <= 1728 doubles (nx <= 27, numax <= 36)
-  double* Ph0 = scr;
+}
+// store a 2 x 2 block into a column-major m x n array (leading dimension ld) where it lies inside
+__device__ __forceinline__ void st2(double* C, int ld, int i0, int j0, int m, int n, const double (&c)[2][2]) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+      if (i0 + x < m && j0 + y < n) C[(j0 + y) * ld + i0 + x] = c[x][y];
+}
+
+// P1 of a middle segment [a, b) after its chain from V_b = 0 (workgroup-wide), from the factor the chain left (LDL'
+// columns F = L D of M^0_uu,k in Lf_k, its x rows F_x and rhs row F_r in K_k / kf_k): with Yd_k = B_k L_k^-T D_k^-1
+// (nx x nu_k, row-wise forward substitution; a guarded pivot's column 0),
+//   Acl_k = A_k + B_k K^0_k = A_k - Yd_k F_x',  bcl_k = rb_k + B_k kff^0_k = rb_k - Yd_k F_r',
+//   B_k (M^0_uu,k)^-1 B_k' = Ys_k Ys_k',  Ys_k = Yd_k D_k^1/2,
+// and backward over the stages Phi <- Phi Acl_k, f += Phi bcl_k, W += Gs Gs' (Gs = Phi Ys_k). The stages go in chunks of
+// up to SEG_CHUNK: a chunk's operands [A | B | rb | F | F_x | F_r] come into LDS (region B, ChainLds::Ml) in one pass of
+// loads, then its Yd (one thread per (stage, row)), Acl and bcl are formed for all its stages at once (in place of A,
+// B, rb), and the accumulation takes one phase per stage (Phi Acl, Phi Ys, Phi bcl and the previous stage's W update
+// side by side, 2 x 2 register blocks). Phi, W, f and the Gs double buffer in region A (from ChainLds::G0). Finally
+// W = Gw Gw' by chain_elim on wave 0 (nx pivots of [W 0; 0 0]; a dropped pivot leaves a zero column). Writes U = [Gw
+// Phi f] to el. Returns chain_elim's NaN flag.
+constexpr int SEG_CHUNK = 9;  // stages per chunk: Yd takes one thread per (stage, row), 9 * 27 <= NT
+__device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, int a, int b, double* el) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx, hb = (nx + 1) >> 1;
+  const int numax = L.numax > 0 ? L.numax : 1;
+  const int ssz = (nxx + 2 * nx * numax + nx + numax * numax + numax + 1) & ~1;  // one stage's slot (<= 4032 doubles)
+  int cmax = CH_SCRATCH / ssz;
+  if (cmax > SEG_CHUNK) cmax = SEG_CHUNK;
+  double* Ph0 = CS.G0;  // region A
   double* Ph1 = Ph0 + nxx;
   double* Wm = Ph1 + nxx;
   double* fv = Wm + nxx;
-  double* Gm = fv + 32;  // [CH_MAXU][nx]
-  double* Op0 = Gm + CH_MAXU * 27;
-  double* Op1 = Op0 + osz;
-  constexpr int PRE = 7;  // ceil(1728 / NT)
-  auto fetch = [&](int k, double (&r)[PRE]) {
-    const int mk = L.nu[k], nA = nxx, nY = nx * mk;
-    const double* Ac = V.Acl(k);
-    const double* Yt = V.K(k);
-    const double* bc = V.bcl() + (long long)k * nx;
-#pragma unroll
-    for (int i = 0; i < PRE; ++i) {
-      const int e = tid + NT * i;
-      const double* src = e < nA ? Ac + e : (e < nA + nY ? Yt + (e - nA) : (e < nA + nY + nx ? bc + (e - nA - nY) : Ac));
-      r[i] = *src;
-    }
-  };
-  auto stash = [&](int k, const double (&r)[PRE], double* Op) {
-    const int tot = nxx + nx * L.nu[k] + nx;
-#pragma unroll
-    for (int i = 0; i < PRE; ++i) {
-      const int e = tid + NT * i;
-      if (e < tot) Op[e] = r[i];
-    }
-  };
-  double pre[PRE];
-  fetch(b - 1, pre);
+  double* Gs0 = fv + 32;
+  double* Gs1 = Gs0 + nx * numax;
+  double* Op = CS.Ml;  // region B: the chunk's stage slots
   for (int e = tid; e < nxx; e += NT) {
     const int i = e % nx, j = e / nx;
     Ph0[e] = i == j ? 1.0 : 0.0;
     Wm[e] = 0.0;
   }
   if (tid < nx) fv[tid] = 0.0;
-  stash(b - 1, pre, Op0);
-  __syncthreads();
-  int cur = 0;
-  for (int k = b - 1; k >= a; --k) {
-    const int mk = L.nu[k];
-    const double* Ph = cur ? Ph1 : Ph0;  // Phi(b, k + 1), column-major
-    double* Pn = cur ? Ph0 : Ph1;
-    const double* Op = cur ? Op1 : Op0;
-    double* On = cur ? Op0 : Op1;
-    const double* Ac = Op;
-    const double* Yt = Op + nxx;
-    const double* bc = Yt + nx * mk;
-    if (k > a) fetch(k - 1, pre);
-    const int nG = nx * mk;
-    for (int e = tid; e < nxx + nG + nx; e += NT) {
-      if (e < nxx) {  // Phi(b, k) = Phi(b, k + 1) Acl_k
-        const int i = e % nx, j = e / nx;
-        double s = 0.0;
-#pragma unroll 8
-        for (int t = 0; t < nx; ++t) s = fma(Ph[t * nx + i], Ac[j * nx + t], s);
-        Pn[e] = s;
-      } else if (e < nxx + nG) {  // G = Phi(b, k + 1) Yt_k
-        const int e2 = e - nxx, i = e2 % nx, qq = e2 / nx;
-        double s = 0.0;
-#pragma unroll 8
-        for (int t = 0; t < nx; ++t) s = fma(Ph[t * nx + i], Yt[t * mk + qq], s);
-        Gm[qq * nx + i] = s;
-      } else {  // f += Phi(b, k + 1) bcl_k
-        const int i = e - nxx - nG;
-        double s = fv[i];
-#pragma unroll 8
-        for (int t = 0; t < nx; ++t) s = fma(Ph[t * nx + i], bc[t], s);
-        fv[i] = s;
+  int cur = 0, mprev = 0;  // Phi buffer; nu of the stage whose Gs waits for its W update
+  for (int ce = b; ce > a; ce -= cmax) {
+    const int cb = ce - cmax > a ? ce - cmax : a, nc = ce - cb;
+    OCP_SPAN_BEGIN(t_f);
+    // (1) the chunk's operands: flat over the stage slots, 16 loads per thread in flight per round
+    {
+      int s0 = tid / ssz, o0 = tid - s0 * ssz;
+      const int tot = nc * ssz;
+      for (int base = 0; base < tot; base += 16 * NT) {
+        double r[16];
+        int sl[16], ol[16];
+        int sx = s0, ox = o0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sl[i] = sx;
+          ol[i] = ox;
+          const int k = cb + (sx < nc ? sx : nc - 1), mk = L.nu[k];
+          const int oB = nxx, oR = oB + nx * mk, oF = oR + nx, oX = oF + mk * mk, oL = oX + nx * mk, oe = oL + mk;
+          const double* src = ox < oB ? V.A(k) + ox
+                              : ox < oR ? V.Bm(k) + (ox - oB)
+                              : ox < oF ? V.rb() + (long long)k * nx + (ox - oR)
+                              : ox < oX ? V.Lf(k) + (ox - oF)
+                              : ox < oL ? V.K(k) + (ox - oX)
+                              : ox < oe ? V.kf() + L.cu[k] + (ox - oL)
+                                        : nullptr;
+          r[i] = (sx < nc && src) ? *src : 0.0;
+          ox += NT;
+          while (ox >= ssz) {
+            ox -= ssz;
+            ++sx;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (sl[i] < nc) Op[sl[i] * ssz + ol[i]] = r[i];
+        s0 = sx;
+        o0 = ox;
       }
     }
     __syncthreads();
-    for (int e = tid; e < nxx; e += NT) {  // W += G G' (the same fma order for (i, j) and (j, i): exactly symmetric)
-      const int i = e % nx, j = e / nx;
-      double s = Wm[e];
-      for (int qq = 0; qq < mk; ++qq) s = fma(Gm[qq * nx + i], Gm[qq * nx + j], s);
-      Wm[e] = s;
+    OCP_SPANG_END(10, t_f, 1);
+    OCP_SPAN_BEGIN(t_1);
+    // (2) Yd of every stage of the chunk: thread (stage, row r), in place of B (8 terms per LDS round trip)
+    if (tid < nc * nx) {
+      const int sl = tid / nx, r = tid - sl * nx, mk = L.nu[cb + sl];
+      double* O = Op + sl * ssz;
+      double* Yd = O + nxx;
+      const double* F = Yd + nx * mk + nx;
+      for (int q = 0; q < mk; ++q) {
+        double s2 = Yd[q * nx + r];
+        for (int c0 = 0; c0 < q; c0 += 8) {
+          double fq[8], yc[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int c = c0 + u < q ? c0 + u : q - 1;
+            fq[u] = F[c * mk + q];
+            yc[u] = Yd[c * nx + r];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (c0 + u < q) s2 = fma(-fq[u], yc[u], s2);
+        }
+        const double d = F[q * mk + q];
+        Yd[q * nx + r] = d > 1e-200 ? s2 / d : 0.0;
+      }
     }
-    if (k > a) stash(k - 1, pre, On);
-    cur ^= 1;
     __syncthreads();
+    OCP_SPANG_END(11, t_1, 1);
+    OCP_SPAN_BEGIN(t_2);
+    // (3) Acl = A - Yd F_x' in place of A, bcl = rb - Yd F_r' in place of rb (2 x 2 blocks of every stage)
+    for (int w = tid; w < nc * (hb * hb + hb); w += NT) {
+      const int sl = w / (hb * hb + hb), v = w - sl * (hb * hb + hb), mk = L.nu[cb + sl];
+      double* O = Op + sl * ssz;
+      const double* Yd = O + nxx;
+      double* rb = O + nxx + nx * mk;
+      const double* Fx = rb + nx + mk * mk;
+      const double* Fr = Fx + nx * mk;
+      const bool isA = v < hb * hb;
+      const int i0 = isA ? 2 * (v % hb) : 2 * (v - hb * hb), j0 = isA ? 2 * (v / hb) : 0, n = isA ? nx : 1;
+      double* C = isA ? O : rb;
+      double c[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+      blk2(Yd, 1, nx, isA ? Fx : Fr, 1, isA ? mk : 0, i0, j0, nx, n, mk, c);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const int i = i0 + x < nx ? i0 + x : nx - 1, j = j0 + y < n ? j0 + y : n - 1;
+          c[x][y] = C[j * nx + i] - c[x][y];
+        }
+      st2(C, nx, i0, j0, nx, n, c);
+    }
+    __syncthreads();
+    OCP_SPANG_END(12, t_2, 1);
+    OCP_SPAN_BEGIN(t_3);
+    // (4) backward over the chunk's stages, one phase each: Phi Acl_k, Gs = Phi Ys_k, f += Phi bcl_k, and the W update
+    // of the stage before (its Gs from the last phase)
+    for (int k = ce - 1; k >= cb; --k) {
+      const int mk = L.nu[k], hq = (mk + 1) >> 1;
+      const double* O = Op + (k - cb) * ssz;
+      const double* Acl = O;
+      const double* Yd = O + nxx;
+      const double* bcl = Yd + nx * mk;
+      const double* F = bcl + nx;
+      const double* Ph = cur ? Ph1 : Ph0;
+      double* Pn = cur ? Ph0 : Ph1;
+      double* Gn = cur ? Gs1 : Gs0;
+      const double* Gp = cur ? Gs0 : Gs1;
+      const int n0 = hb * hb, n1 = n0 + hb * hq, n2 = n1 + hb, n3 = n2 + (mprev > 0 ? hb * hb : 0);
+      for (int w = tid; w < n3; w += NT) {
+        double c[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+        if (w < n0) {
+          const int i0 = 2 * (w % hb), j0 = 2 * (w / hb);
+          blk2(Ph, 1, nx, Acl, 1, nx, i0, j0, nx, nx, nx, c);
+          st2(Pn, nx, i0, j0, nx, nx, c);
+        } else if (w < n1) {
+          const int v = w - n0, i0 = 2 * (v % hb), q0 = 2 * (v / hb);
+          blk2(Ph, 1, nx, Yd, 1, nx, i0, q0, nx, mk, nx, c);
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const int qq = q0 + y < mk ? q0 + y : mk - 1;
+            const double d = F[qq * mk + qq], sd = d > 1e-200 ? sqrt(d) : 0.0;
+            c[0][y] *= sd;
+            c[1][y] *= sd;
+          }
+          st2(Gn, nx, i0, q0, nx, mk, c);
+        } else if (w < n2) {
+          const int i0 = 2 * (w - n1);
+#pragma unroll
+          for (int x = 0; x < 2; ++x) c[x][0] = fv[i0 + x < nx ? i0 + x : nx - 1];
+          blk2(Ph, 1, nx, bcl, 1, 0, i0, 0, nx, 1, nx, c);
+          st2(fv, nx, i0, 0, nx, 1, c);
+        } else {
+          const int v = w - n2, i0 = 2 * (v % hb), j0 = 2 * (v / hb);
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+              c[x][y] = Wm[(j0 + y < nx ? j0 + y : nx - 1) * nx + (i0 + x < nx ? i0 + x : nx - 1)];
+          blk2(Gp, 1, nx, Gp, nx, 1, i0, j0, nx, nx, mprev, c);
+          st2(Wm, nx, i0, j0, nx, nx, c);
+        }
+      }
+      mprev = mk;
+      cur ^= 1;
+      __syncthreads();
+    }
+    OCP_SPANG_END(13, t_3, 1);
   }
-  const double* Ph = cur ? Ph1 : Ph0;
-  for (int e = tid; e < 2 * nxx + nx; e += NT) el[e] = e < nxx ? Ph[e] : (e < 2 * nxx ? Wm[e - nxx] : fv[e - 2 * nxx]);
+  // the last stage's W update, then M = [W 0; 0 0] (lower triangle, rows / columns up to the 4 x 4 blocks' pad)
+  const double* Gp = cur ? Gs0 : Gs1;
+  const int n1 = 2 * nx + 1, np = (n1 + 3) & ~3;
+  if (mprev > 0)
+    for (int w = tid; w < hb * hb; w += NT) {
+      const int i0 = 2 * (w % hb), j0 = 2 * (w / hb);
+      double c[2][2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) c[x][y] = Wm[(j0 + y < nx ? j0 + y : nx - 1) * nx + (i0 + x < nx ? i0 + x : nx - 1)];
+      blk2(Gp, 1, nx, Gp, nx, 1, i0, j0, nx, nx, mprev, c);
+      st2(Wm, nx, i0, j0, nx, nx, c);
+    }
   __syncthreads();
+  for (int e = tid; e < np * np; e += NT) {
+    const int i = e / np, j = e - i * np;
+    CS.Ml[i * CH_GS + j] = (i < nx && j < nx) ? Wm[j * nx + i] : 0.0;
+  }
+  __syncthreads();
+  OCP_SPAN_BEGIN(t_c);
+  int fl = 0;
+  if (tid < 64) fl = chain_elim<2, false>(V, CS, nx, CS.F0, CS.Pa2);
+  fl = __syncthreads_or(fl & CH_NAN) ? CH_NAN : 0;
+  OCP_SPANG_END(13, t_c, 1);
+  // U = [Gw Phi f]: Gw(x, j) = F(x, j) / sqrt(d_j) below the diagonal (0 for a dropped pivot)
+  const double* Ph = cur ? Ph1 : Ph0;
+  for (int e = tid; e < 2 * nxx + nx; e += NT) {
+    double v;
+    if (e < nxx) {
+      const int x = e % nx, j = e / nx;
+      const double d = CS.F0[j * CH_FS + j];
+      v = (x >= j && d > 1e-200) ? CS.F0[j * CH_FS + x] / sqrt(d) : 0.0;
+    } else {
+      v = e < 2 * nxx ? Ph[e - nxx] : fv[e - 2 * nxx];
+    }
+    el[e] = v;
+  }
+  __syncthreads();
+  return fl;
 }
 
 // P2 on one workgroup: the exact value function at the boundaries c_{S-1} .. c_1 into the segment buffer (the last
-// segment's own P, p at c_{S-1}; then the combine per middle segment). scr: LDS scratch of ChainLds::Ml (9080
-// doubles: the layout below needs 11 nx^2 + 7 nx + 64 <= 8272 for nx <= 27). Returns false on a zero or non-finite
-// pivot of a combine's solve.
-__device__ __forceinline__ bool seg_combine(const View& V, double* scr, double* sq, int S, int N) {
+// segment's own P, p at c_{S-1}; then the combine per middle segment, see the header): T = P_b U (+ p_b on the f
+// column: h), the M image's lower triangle T' U + [I; P^0_a; p^0_a] (2 x 2 blocks), chain_elim of its nx pivots on wave
+// 0; its Paug image is [P_a p_a]. Region A holds U, T, P_b, p_b; region B the chain's M image, factor and Paug images.
+// Returns false on a NaN or dropped pivot (then the serial chain runs).
+__device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, double* sq, int S, int N) {
   const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx, LW = 2 * nx + 2;
+  const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx, hb = (nx + 1) >> 1;
+  const int LU = 2 * nx + 1, hu = (LU + 1) >> 1, np = (LU + 3) & ~3;
   const int esz = seg_esz(nx), bsz = seg_bsz(nx);
   double* bnd = sq + OCP_GRID_MAX_G * esz;
-  double* A0 = scr;             // [nx][LW] row-major: I + W P_b | Phi | f
-  double* A1 = A0 + nx * LW;    // Gauss-Jordan double buffer
-  double* Pb = A1 + nx * LW;    // P_b (column-major), p_b
+  double* U = CS.G0;        // [Gw Phi f], column-major nx x LU
+  double* T = U + nx * LU;  // P_b U, then + p_b on column 2 nx
+  double* Pb = T + nx * LU;
   double* pb = Pb + nxx;
-  double* Pa = pb + 32;         // P_a, p_a
-  double* pa = Pa + nxx;
-  double* Ph = pa + 32;         // Phi
-  double* Wm = Ph + nxx;        // W
-  double* Y = Wm + nxx;         // P_b X (column-major nx x (nx + 1))
-  double* Z = Y + nxx + nx;     // Phi' P_b X_Phi
+  double* Ml = CS.Ml;
   {
     const int cl = seg_begin(N, S, S - 1);
     const double* P = V.P(cl);
@@ -192,114 +332,73 @@ __device__ __forceinline__ bool seg_combine(const View& V, double* scr, double* 
       else pb[e - nxx] = v;
       bo[e] = v;
     }
+    for (int e = tid; e < np * np; e += NT) {  // the image's pad rows / columns stay zero
+      const int i = e / np, j = e - i * np;
+      if (i >= LU || j >= LU) Ml[i * CH_GS + j] = 0.0;
+    }
   }
   bool ok = true;
   for (int s = S - 2; s >= 1; --s) {
     const int cs = seg_begin(N, S, s);
     const double* el = sq + s * esz;
-    for (int e = tid; e < 2 * nxx; e += NT) {
-      if (e < nxx) Ph[e] = el[e];
-      else Wm[e - nxx] = el[e];
+    for (int e = tid; e < nx * LU; e += NT) U[e] = el[e];
+    __syncthreads();
+    OCP_SPAN_BEGIN(t_a);
+    for (int w = tid; w < hb * hu; w += NT) {
+      const int i0 = 2 * (w % hb), j0 = 2 * (w / hb);
+      double c[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+      blk2(Pb, 1, nx, U, 1, nx, i0, j0, nx, LU, nx, c);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          if (j0 + y == 2 * nx) c[x][y] += pb[i0 + x < nx ? i0 + x : nx - 1];
+      st2(T, nx, i0, j0, nx, LU, c);
     }
     __syncthreads();
-    // A = [I + W P_b | Phi | f]
-    for (int e = tid; e < nx * (2 * nx + 1); e += NT) {
-      const int i = e / (2 * nx + 1), j = e - i * (2 * nx + 1);
-      double v;
-      if (j < nx) {
-        v = i == j ? 1.0 : 0.0;
-#pragma unroll 8
-        for (int t = 0; t < nx; ++t) v = fma(Wm[t * nx + i], Pb[j * nx + t], v);
-      } else if (j < 2 * nx) {
-        v = Ph[(j - nx) * nx + i];
-      } else {
-        v = el[2 * nxx + i];
-      }
-      A0[i * LW + j] = v;
-    }
-    __syncthreads();
-    // Gauss-Jordan with partial pivoting (the pivot row found by every thread from the same LDS column: no extra
-    // barrier); row k takes the pivot row scaled, the pivot row the old row k eliminated, columns < k are never read
-    double* Ac = A0;
-    double* An = A1;
-    for (int k = 0; k < nx; ++k) {
-      int p = k;
-      double best = fabs(Ac[k * LW + k]);
-      for (int i = k + 1; i < nx; ++i) {
-        const double v = fabs(Ac[i * LW + k]);
-        if (v > best) {
-          best = v;
-          p = i;
-        }
-      }
-      const double piv = Ac[p * LW + k];
-      ok = ok && piv != 0.0 && isfinite(piv);
-      const double pinv = 1.0 / piv;
-      const int wc = 2 * nx + 1 - k;
-      for (int e = tid; e < nx * wc; e += NT) {
-        const int i = e / wc, j = k + (e - i * wc);
-        const double rk = Ac[p * LW + j] * pinv;
-        double v = rk;
-        if (i != k) {
-          const int src = i == p ? k : i;
-          v = fma(-Ac[src * LW + k], rk, Ac[src * LW + j]);
-        }
-        An[i * LW + j] = v;
-      }
-      __syncthreads();
-      double* t = Ac;
-      Ac = An;
-      An = t;
-    }
-    // Y = P_b [X_Phi X_f]
-    for (int e = tid; e < nxx + nx; e += NT) {
-      const int i = e % nx, j = e / nx;
-      double v = 0.0;
-#pragma unroll 8
-      for (int t = 0; t < nx; ++t) v = fma(Pb[t * nx + i], Ac[t * LW + nx + j], v);
-      Y[j * nx + i] = v;
-    }
-    __syncthreads();
-    // Z = Phi' Y_Phi; p_a = p^0_a + Phi' Y_f + X_Phi' p_b
+    // M(i, j), i >= j: T(:, i)' U(:, j) + (i == j < nx) + P^0_a / p^0_a in the x rows
     const double* P0 = V.P(cs);
     const double* p0 = V.pv() + (long long)cs * nx;
-    for (int e = tid; e < nxx + nx; e += NT) {
-      if (e < nxx) {
-        const int i = e % nx, j = e / nx;
-        double v = 0.0;
-#pragma unroll 8
-        for (int t = 0; t < nx; ++t) v = fma(Ph[i * nx + t], Y[j * nx + t], v);
-        Z[e] = v;
-      } else {
-        const int i = e - nxx;
-        double v = 0.0, w = 0.0;
-#pragma unroll 8
-        for (int t = 0; t < nx; ++t) {
-          v = fma(Ph[i * nx + t], Y[nxx + t], v);
-          w = fma(Ac[t * LW + nx + i], pb[t], w);
+    for (int w = tid; w < hu * (hu + 1) / 2; w += NT) {
+      int bi, bj;
+      ch_block(w, bi, bj);
+      const int i0 = 2 * bi, j0 = 2 * bj;
+      double c[2][2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const int i = i0 + x, j = j0 + y;
+          double v = (i == j && i < nx) ? 1.0 : 0.0;
+          if (i >= nx && i < 2 * nx && j >= nx && j < 2 * nx) v = P0[(j - nx) * nx + (i - nx)];
+          else if (i == 2 * nx && j >= nx && j < 2 * nx) v = p0[j - nx];
+          c[x][y] = v;
         }
-        pa[i] = p0[i] + (v + w);
-      }
+      blk2(T, nx, 1, U, 1, nx, i0, j0, LU, LU, nx, c);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          if (i0 + x < LU && j0 + y <= i0 + x) Ml[(i0 + x) * CH_GS + j0 + y] = c[x][y];
     }
     __syncthreads();
+    OCP_SPANG_END(14, t_a, 0);
+    OCP_SPAN_BEGIN(t_g);
+    int fl = 0;
+    if (tid < 64) fl = chain_elim<2, true>(V, CS, nx, CS.F0, CS.Pa2);
+    ok = ok && !__syncthreads_or(fl);
+    OCP_SPANG_END(15, t_g, 0);
+    OCP_SPAN_BEGIN(t_p);
     double* bo = bnd + s * bsz;
     for (int e = tid; e < nxx + nx; e += NT) {
-      if (e < nxx) {
-        const int i = e % nx, j = e / nx;
-        const double v = P0[e] + 0.5 * (Z[e] + Z[i * nx + j]);  // symmetric by construction
-        Pa[e] = v;
-        bo[e] = v;
-      } else {
-        bo[e] = pa[e - nxx];
-      }
+      const int I = e < nxx ? e % nx : e - nxx, J = e < nxx ? e / nx : nx;
+      const double v = CS.Pa2[I * CH_PS + J];
+      if (e < nxx) Pb[e] = v;
+      else pb[e - nxx] = v;
+      bo[e] = v;
     }
     __syncthreads();
-    for (int e = tid; e < nxx + nx; e += NT) {
-      if (e < nxx) Pb[e] = Pa[e];
-      else pb[e - nxx] = pa[e - nxx];
-    }
-    __syncthreads();
+    OCP_SPANG_END(16, t_p, 0);
   }
-  __syncthreads();  // the boundary stores (global) ordered before the grid barrier's release
-  return __syncthreads_and(ok) != 0;
+  return ok;
 }

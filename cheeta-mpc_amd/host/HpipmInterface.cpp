@@ -154,6 +154,9 @@ class HpipmInterface::Impl {
     if (!settings_.warm_start || xbuf_.size() != (size_t)(N + 1) * nx) xbuf_.assign((size_t)(N + 1) * nx, 0.0);
     if (!settings_.warm_start || ubuf_.size() != (size_t)(nU > 0 ? nU : 1)) ubuf_.assign((size_t)(nU > 0 ? nU : 1), 0.0);
     int status = -1, iters = 0;
+    // the verbose table's lin res columns: the device records the Newton systems' residuals for this solve only
+    if (cmpc_ocp_set_linres(ocp_, verbose ? 1 : 0) != CMPC_OK)
+      throw std::runtime_error("[HpipmInterface] cannot record the statistics");
     const int r = cmpc_ocp_solve_host(ocp_, 1, x0p, rec, crec, xbuf_.data(), ubuf_.data(), &status, &iters);
     if (r != CMPC_OK) throw std::runtime_error(std::string("[HpipmInterface] device solve failed: ") + cmpc_error_string(r));
     // getStateSolution / getInputSolution (:303-328): x[0] = x0, each node in its own dimension; non-finite -> NAN_SOL
@@ -576,14 +579,16 @@ class HpipmInterface::Impl {
   // device solver's records (cmpc_ocp_get_residuals_host / cmpc_ocp_get_stats_host). The table has the reference's
   // 17 columns: the first ten are cmpc_enable_stats'; lq fact, itref pred and itref corr are 0 (the device solver is
   // the Riccati recursion of the SPEED mode the reference selects, HpipmInterfaceSettings.h:45: no LQ factorisation,
-  // no iterative refinement); the four lin res columns are NaN: the device solver forms no residual of the Newton
-  // system (HPIPM is not vendored, so what HPIPM prints there in this mode is unpinned)
+  // no iterative refinement); the four lin res columns are the device's residuals of each iteration's Newton system
+  // at its final direction (cmpc_ocp_set_linres; what HPIPM prints there is unpinned: it is not vendored)
   void printStatus(int status, int iters) const {
     double res[4] = {NAN, NAN, NAN, NAN};
     const int rows = cmpc_ocp_stat_rows(ocp_);
     std::vector<double> stats((size_t)(rows > 0 ? rows : 1) * CMPC_STAT_COLS, NAN);
+    std::vector<double> lin((size_t)(rows > 0 ? rows : 1) * 4, NAN);
     cmpc_ocp_get_residuals_host(ocp_, 1, res);
     if (rows > 0) cmpc_ocp_get_stats_host(ocp_, 1, stats.data());
+    if (rows > 0) cmpc_ocp_get_linres_host(ocp_, 1, lin.data());
     std::fprintf(stderr, "\n=== HPIPM (MI355X engine) ===\n");
     std::fprintf(stderr, "HPIPM returned with flag %i. -> ", status);
     if (status == CMPC_SUCCESS) std::fprintf(stderr, "QP solved!\n");
@@ -601,7 +606,7 @@ class HpipmInterface::Impl {
     for (int j = 0; j < iters + 1 && j < rows; ++j) {
       for (int i = 0; i < CMPC_STAT_COLS; ++i) std::fprintf(stderr, "%e\t", stats[(size_t)j * CMPC_STAT_COLS + i]);
       for (int i = 0; i < 3; ++i) std::fprintf(stderr, "%e\t", 0.0);  // lq fact, itref pred, itref corr
-      for (int i = 0; i < 4; ++i) std::fprintf(stderr, "%e\t", (double)NAN);  // lin res stat / eq / ineq / comp
+      for (int i = 0; i < 4; ++i) std::fprintf(stderr, "%e\t", lin[(size_t)j * 4 + i]);  // lin res stat/eq/ineq/comp
       std::fprintf(stderr, "\n");
     }
   }

@@ -127,6 +127,8 @@ def lib():
     L.cmpc_ocp_set_keep_riccati.argtypes = [vp, C.c_int]
     L.cmpc_ocp_enable_timing.argtypes = [vp, C.c_int]
     L.cmpc_ocp_last_solve_ms.argtypes = [vp, P(C.c_float)]
+    L.cmpc_ocp_set_linres.argtypes = [vp, C.c_int]
+    L.cmpc_ocp_get_linres_host.argtypes = [vp, C.c_int, d]
     L.cmpc_ocp_set_segments.argtypes = [vp, C.c_int]
     L.cmpc_ocp_segments.argtypes = [vp, C.c_int]
     L.cmpc_ocp_set_grid_timeout.argtypes = [vp, C.c_double]
@@ -737,6 +739,15 @@ class OcpSolver:
         d = DeviceArray((B, 4), np.float64)
         _chk(lib().cmpc_ocp_get_residuals(self.h, B, d.ptr, None), "cmpc_ocp_get_residuals")
         return d.host()
+
+    def set_linres(self, on):
+        """cmpc_ocp_set_linres: record each iteration's Newton-system residuals (HPIPM's lin res statistics)."""
+        _chk(lib().cmpc_ocp_set_linres(self.h, int(on)), "cmpc_ocp_set_linres")
+
+    def linres(self, B):
+        out = np.zeros((B, self.stat_rows, 4))
+        _chk(lib().cmpc_ocp_get_linres_host(self.h, B, _dp(out)), "cmpc_ocp_get_linres_host")
+        return out
 
     def stats(self, B):
         d = DeviceArray((B, self.stat_rows, 10), np.float64)

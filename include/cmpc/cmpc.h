@@ -429,6 +429,16 @@ int cmpc_ocp_get_stats(cmpc_ocp* ocp, int B, double* d_stats, void* stream);
 /* Same, host pointers, synchronous (the HpipmInterface mirror's verbose printout). */
 int cmpc_ocp_get_residuals_host(cmpc_ocp* ocp, int B, double* res);
 int cmpc_ocp_get_stats_host(cmpc_ocp* ocp, int B, double* stats);
+/* on = 1: every solve also records, per problem and iteration, the residuals of the Newton system it solved at its
+ * final direction (predictor, or corrector with rows): HPIPM's "lin res stat / eq / ineq / comp" statistics columns
+ * (HpipmInterface.cpp:492-501), the inf-norms of H~dz + G'dpi - Gc'dlam + r_stat (H~ the factorised Hessian, reg_prim
+ * on its diagonal), A dx + B du - dx+ + r_eq, Gc dz - dt + r_ineq and t dlam + lam dt + r_comp.
+ * d_linres [B][rows][4] (rows as cmpc_ocp_stat_rows; a row without a direction — the exit iteration's and those after
+ * it — is NaN). Off by default (it costs one more pass and, in the grid form, one grid barrier per iteration);
+ * cmpc_ocp_get_linres* return CMPC_ERR_ARG while it is off. */
+int cmpc_ocp_set_linres(cmpc_ocp* ocp, int on);
+int cmpc_ocp_get_linres(cmpc_ocp* ocp, int B, double* d_linres, void* stream);
+int cmpc_ocp_get_linres_host(cmpc_ocp* ocp, int B, double* linres);
 
 /* One-shot host entry points (create, solve, destroy; kept from the 0.3 ABI): the equality-free problem
  * (cmpc_ocp_solve_batch_host), with rows (cmpc_ocp_solve_batch_eq_host; nc == NULL is CMPC_ERR_ARG), and its Riccati

@@ -861,6 +861,7 @@ static void verbose_table() {
   CHECK(hi != std::string::npos && out.find("\tlq fact\t\titref pred\titref corr\tlin res stat") != std::string::npos,
         "verbose table header has the 17 columns");
   int rows = 0, bad = 0;
+  double linmax = 0.0;
   size_t at = hi == std::string::npos ? out.size() : hi + 13;
   while (at < out.size()) {
     const size_t e = out.find('\n', at);
@@ -874,10 +875,21 @@ static void verbose_table() {
       v.push_back(x);
       c = end;
     }
+    // lin res stat / eq / ineq / comp (columns 13-16): the device's Newton-system residuals, finite and at rounding
+    // level for every iteration that computed a direction, NaN for the exit row (no direction)
+    bool lin_ok = v.size() == 17;
+    for (int c = 13; lin_ok && c < 17; ++c) {
+      if (rows < iters) {
+        lin_ok = std::isfinite(v[(size_t)c]) && v[(size_t)c] <= 1e-6 * std::fmax(1.0, v[6]);
+        linmax = std::fmax(linmax, v[(size_t)c]);
+      } else {
+        lin_ok = std::isnan(v[(size_t)c]);
+      }
+    }
     ++rows;
-    if (v.size() != 17 || !std::isfinite(v[5]) || v[10] != 0.0 || v[11] != 0.0 || v[12] != 0.0 || !std::isnan(v[13])) ++bad;
+    if (v.size() != 17 || !std::isfinite(v[5]) || v[10] != 0.0 || v[11] != 0.0 || v[12] != 0.0 || !lin_ok) ++bad;
   }
-  std::printf("verbose table: %d iterations, %d rows, %d malformed\n", iters, rows, bad);
+  std::printf("verbose table: %d iterations, %d rows, %d malformed, largest lin res %.3e\n", iters, rows, bad, linmax);
   CHECK(rows == iters + 1 && bad == 0, "verbose table: iter + 1 rows of 17 columns");
 }
 

@@ -90,3 +90,30 @@ def test_device_partitioned_dropped_pivot_falls_back_to_the_serial_chain(cm, op)
     assert np.array_equal(st1, st8) and np.array_equal(it1, it8)
     assert np.array_equal(x1, x8) and np.array_equal(u1, u8)
     _check_vs_oracle(op, [p], x8, u8, st8, it8, settings=op.default_settings(reg_prim=0.0))
+
+
+@pytest.mark.parametrize("grid", [0, 1])
+def test_device_linres_statistics(cm, op, grid):
+    """cmpc_ocp_set_linres: per iteration the residuals of the Newton system at the final direction (HPIPM's lin res
+    stat / eq / ineq / comp columns, HpipmInterface.cpp:492-501), in the grid form and the one-workgroup form: finite
+    and at rounding level (relative to the iteration's own residuals) for every iteration that computed a direction,
+    NaN for the exit row and after it; the solve's result the same to rounding (the recording solve runs the batched
+    form's factorisation: same iterations and statuses, x and u at 1e-10)."""
+    ps = [ocpgen.legged_problem(595 + i, projected=False) for i in range(2)]
+    p0 = ps[0]
+    h = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=2)
+    h.set_grid(grid)
+    x0, u0, st0, it0 = _solve(h, ps)
+    h.set_linres(1)
+    x, u, st, it = _solve(h, ps)
+    assert np.array_equal(it, it0) and np.array_equal(st, st0)
+    assert _rel(x, x0) < 1e-10 and _rel(u, u0) < 1e-10
+    lr = h.linres(2)
+    stats = h.stats(2)
+    for i in range(2):
+        n = it[i]
+        assert np.all(np.isfinite(lr[i][:n])), lr[i][:n]
+        assert np.all(np.isnan(lr[i][n:]))
+        scale = np.maximum(1.0, np.nanmax(stats[i][:n, 6:10], axis=1))
+        assert np.all(lr[i][:n].max(axis=1) <= 1e-6 * scale), (lr[i][:n], scale)
+    h.close()

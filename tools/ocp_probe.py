@@ -80,12 +80,12 @@ def stamps(projected, B=1):
     L.cmpc_ocp_debug_stamps(buf, 1)
     x, u, st, it = s.solve(x0, np.array(recs), np.array(crecs) if not projected else None)
     L.cmpc_ocp_debug_stamps(buf, 1)
-    names = {1: "residuals", 2: "rhs", 10: "fact:init", 11: "fact:T", 12: "fact:M", 13: "fact:prefetch",
-             14: "fact:sweep", 15: "fact:store", 16: "fact:out", 20: "chain:init", 21: "chain:T", 22: "chain:M",
+    names = {1: "residuals", 2: "rhs", 10: "[wg1 el:fetch]", 11: "[wg1 el:Yd]", 12: "[wg1 el:Acl,bcl]",
+             13: "[wg1 el:accum+Gw]", 14: "[wg0 comb:products]", 15: "[wg0 comb:elim]", 16: "[wg0 comb:out]", 20: "chain:init", 21: "chain:T", 22: "chain:M",
              23: "chain:elim", 24: "chain:out", 25: "chain:outw0", 26: "[w1 load span]", 27: "chain:e-load", 28: "grid prologue", 17: "fact:exit", 3: "acl", 4: "forward",
              5: "post", 6: "corr rhs", 7: "backward", 8: "acl+forward (corr)", 9: "update", 18: "part:P1+wait",
              19: "part:combine+wait", 29: "part:P3", 30: "[wg1 chain spans]", 31: "[wg1 element spans]"}
-    tot = sum(buf[i] for i in names if i not in (26, 30, 31))  # spans of other waves / workgroups
+    tot = sum(buf[i] for i in names if i not in (10, 11, 12, 13, 14, 15, 16, 26, 30, 31))  # spans (other timelines)
     print(f"stamps {'projected' if projected else 'rows'} B={B} iters {it[0]} total {tot} cycles")
     for i, n in names.items():
         print(f"  {n:22s} {buf[i]:12d}  {100.0 * buf[i] / max(tot, 1):5.1f} %")
