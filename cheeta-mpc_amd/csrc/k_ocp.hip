@@ -1858,6 +1858,34 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   // pass's flags in slot 4, the combine's in slot 6 (both collected well before their next writers, see above).
   double* segq = a.seg ? a.seg + (long long)q * a.seg_stride : nullptr;
   const int nseg = (FAST && segq) ? part_segments(a.nseg, G, N) : 1;
+  // segments of the partitioned affine scans (ocp_part.hpp): at most the steps N - 1 and what affine_bound stages
+  const int naff = [&] {
+    int Sa = nseg < N - 1 ? nseg : N - 1;
+    const int cap = 1 + CH_SCRATCH / (nx * (nx + 1));
+    return Sa > cap ? cap : Sa;
+  }();
+  // a serial vector recursion of the chain (the rollout, BWD = false, or the corrector's cost-to-go): on workgroup 0,
+  // or as the partitioned scan (A: compositions, B: boundary values, C: the segments' own steps); false when a grid
+  // barrier failed. The caller's barrier follows.
+  auto affine_scan = [&](auto bwd) __attribute__((always_inline)) -> bool {
+    constexpr bool BWD = decltype(bwd)::value;
+    if constexpr (FAST) {
+      if (naff <= 1) {
+        if (lead) chain_affine<BWD>(V, CS, S.vec, S.vec + 64);
+        return true;
+      }
+      const int n = N - 1, s0 = aff_begin(n, naff, g < naff ? g : naff), s1 = aff_begin(n, naff, g < naff ? g + 1 : naff);
+      if (g < naff - 1) affine_comp<BWD>(V, CS, s0, s1, segq + g * seg_esz(nx));
+      if (!sync()) return false;
+      if (lead) affine_bound<BWD>(V, CS, segq, naff, S.vec);
+      if (!sync()) return false;
+      if (g < naff) chain_affine<BWD>(V, CS, S.vec, S.vec + 64, s0, s1, g < naff - 1);
+    } else if (lead) {
+      if constexpr (BWD) bwd_vec_b(V, S);
+      else forward_pass(V, S);
+    }
+    return true;
+  };
   auto factor_grid = [&]() __attribute__((always_inline)) -> bool {
     if (nseg <= 1) {  // the serial chain on workgroup 0
       if (lead) {
@@ -1895,6 +1923,8 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
         k0 = 0;
         k1 = N;
         term = CH_TERM_NODE;
+        if (lead && tid == 0 && a.fallbacks)
+          __hip_atomic_fetch_add(a.fallbacks + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       OCP_SPAN_BEGIN(t_ch);
       f = run ? chain_factor<true>(V, CS, hp, a.reg, k0, k1, term, Pt, Pt ? Pt + nx * nx : nullptr) : 0;
@@ -2114,10 +2144,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     acl_pass(V, S, true, R.k0, R.k1, true);
     if (!sync()) break;
     OCP_STAMP(3);
-    if (lead) {
-      if constexpr (FAST) chain_affine<false>(V, CS, S.vec, S.vec + 64);
-      else forward_pass(V, S);
-    }
+    if (!affine_scan(std::integral_constant<bool, false>{})) break;
     if (!sync()) break;
     OCP_STAMP(4);
     double amax = block_reduce(post_pass(V, R.k0, R.k1, R.n1), S.red, OpMin());
@@ -2165,20 +2192,14 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       OCP_STAMP(6);
       bwd_vec_a(V, R.k0, R.k1, last);
       if (!sync()) break;
-      if (lead) {
-        if constexpr (FAST) chain_affine<true>(V, CS, S.vec, S.vec + 64);
-        else bwd_vec_b(V, S);
-      }
+      if (!affine_scan(std::integral_constant<bool, true>{})) break;
       if (!sync()) break;
       bwd_vec_c(V, R.k0, R.k1);
       __syncthreads();
       OCP_STAMP(7);
       acl_pass(V, S, false, R.k0, R.k1, true);
       if (!sync()) break;
-      if (lead) {
-        if constexpr (FAST) chain_affine<false>(V, CS, S.vec, S.vec + 64);
-        else forward_pass(V, S);
-      }
+      if (!affine_scan(std::integral_constant<bool, false>{})) break;
       if (!sync()) break;
       OCP_STAMP(8);
       {

@@ -576,6 +576,15 @@ int cmpc_ocp_fallback_count(cmpc_ocp* o) {
   return (int)n;
 }
 
+int cmpc_ocp_partition_fallback_count(cmpc_ocp* o) {
+  if (!o) return CMPC_ERR_ARG;
+  if (!o->fbk.p) return 0;
+  unsigned n[2] = {0, 0};
+  if (o->ev_done && hipEventSynchronize(o->ev_done) != hipSuccess) return CMPC_ERR_HIP;
+  if (hipMemcpy(n, o->fbk.p, sizeof(n), hipMemcpyDeviceToHost) != hipSuccess) return CMPC_ERR_HIP;
+  return (int)n[1];
+}
+
 int cmpc_ocp_set_keep_riccati(cmpc_ocp* o, int on) {
   if (!o || on < 0 || on > 1) return CMPC_ERR_ARG;
   o->keep_ric = on;

@@ -768,8 +768,13 @@ __device__ __forceinline__ bool chain_factor(const View& V, const ChainLds& S, c
 // or transposed for BWD) and the vector. Wave 0 keeps the running vector in LDS (v0 / v1, read back by the same wave:
 // no barrier per stage); one workgroup barrier per chunk. The fma order per entry is the one of forward_pass /
 // bwd_vec_b.
+// The steps s = s0 .. s1 - 1 of the sequence (k = 1 + s forward, N - 1 - s backward; s1 < 0: to the end): s0 = 0 starts
+// from the recursion's own initial value, s0 > 0 from the output row before step s0 (dx_{1 + s0} / p_{N - s0}, written
+// by the caller); keep_last leaves the last step's output row alone (the partitioned scan's boundary value, owned by the
+// caller: affine_grid).
 template <bool BWD>
-__device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, double* v0, double* v1) {
+__device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, double* v0, double* v1, int s0 = 0,
+                                             int s1 = -1, bool keep_last = false) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx, wave = tid >> 6;
   const int SS = (nxx + nx + 1) & ~1;
@@ -779,9 +784,10 @@ __device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, d
   if (CK > 16) CK = 16;
   double* buf0 = C.Ml;
   double* buf1 = C.Ml + CK * SS;
-  const int n = N - 1;  // stages of the recursion
+  const int n = (s1 < 0 ? N - 1 : s1) - s0;  // steps of this range
   const double* vec = BWD ? V.h() : V.bcl();
-  // waves 1-3: chunk c (stages c CK .. c CK + cnt - 1 of the sequence) into its buffer; all loads before any store
+  // waves 1-3: chunk c (steps s0 + c CK .. s0 + c CK + cnt - 1 of the sequence) into its buffer; all loads before any
+  // store
   auto load = [&](int c) {
     const int t = tid - 64, j0 = c * CK;
     const int cnt = (n - j0) < CK ? (n - j0) : CK;
@@ -798,7 +804,7 @@ __device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, d
     for (int q = 0; q < 24; ++q) {
       const int e = t + 192 * q;
       const bool on = e < tot;
-      const int k = BWD ? N - 1 - (j0 + j) : 1 + j0 + j;
+      const int k = BWD ? N - 1 - (s0 + j0 + j) : 1 + s0 + j0 + j;
       const double* src = V.ws;  // an always valid address for the entries outside the chunk
       if (on) {
         if (w < nxx) {
@@ -825,9 +831,14 @@ __device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, d
       if (idx[q] >= 0) dst[idx[q]] = r[q];
   };
   if (wave == 0 && tid < nx) {
-    const double d = BWD ? V.gx()[(long long)N * nx + tid] : V.bcl()[tid];
+    double d;
+    if (s0 == 0) {
+      d = BWD ? V.gx()[(long long)N * nx + tid] : V.bcl()[tid];
+      if (!BWD) V.dx()[nx + tid] = d;
+    } else {
+      d = BWD ? V.pv()[(long long)(N - s0) * nx + tid] : V.dx()[(long long)(1 + s0) * nx + tid];
+    }
     v0[tid] = d;
-    if (!BWD) V.dx()[nx + tid] = d;
   }
   if (wave > 0 && n > 0) load(0);
   __syncthreads();
@@ -840,13 +851,13 @@ __device__ __forceinline__ void chain_affine(const View& V, const ChainLds& C, d
         const double* M = b + j * SS;
         const double* vin = (s & 1) ? v1 : v0;
         double* vout = (s & 1) ? v0 : v1;
-        const int k = BWD ? N - 1 - s : 1 + s;
+        const int k = BWD ? N - 1 - (s0 + s) : 1 + s0 + s;
         if (tid < nx) {
           double acc = M[nxx + tid];
 #pragma unroll 8
           for (int cc = 0; cc < nx; ++cc) acc = fma(M[cc * nx + tid], vin[cc], acc);
           vout[tid] = acc;
-          out[(long long)(BWD ? k : k + 1) * nx + tid] = acc;
+          if (!(keep_last && s == n - 1)) out[(long long)(BWD ? k : k + 1) * nx + tid] = acc;
         }
         __builtin_amdgcn_wave_barrier();
       }

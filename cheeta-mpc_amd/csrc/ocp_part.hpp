@@ -82,6 +82,30 @@ __device__ __forceinline__ void st2(double* C, int ld, int i0, int j0, int m, in
       if (i0 + x < m && j0 + y < n) C[(j0 + y) * ld + i0 + x] = c[x][y];
 }
 
+// One 16 x 16 tile (rows r0 .., columns c0 ..) of sum_{t<K} A(i, t) B(t, j) added to acc on v_mfma_f64_16x16x4f64 (one
+// wave): A(i, t) = A[i ai + t at], B(t, j) = B[t bt + j bj] (LDS), rows >= m / columns >= n / t >= K read as zero; the
+// loads of up to 7 k-steps (t < 28) issued before their mfmas. acc[q] is the entry (r0 + (lane >> 4) + 4 q,
+// c0 + (lane & 15)).
+__device__ __forceinline__ v4d mtile(const double* A, int ai, int at, const double* B, int bt, int bj, int r0, int c0,
+                                     int m, int n, int K, v4d acc) {
+  const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+  const int i = r0 + lr, j = c0 + lr, nks = (K + 3) >> 2;
+  for (int k0 = 0; k0 < nks; k0 += 7) {
+    double av[7], bv[7];
+#pragma unroll
+    for (int kk = 0; kk < 7; ++kk) {
+      const int t = 4 * (k0 + kk) + lk;
+      const bool tv = k0 + kk < nks && t < K;
+      av[kk] = (tv && i < m) ? A[i * ai + t * at] : 0.0;
+      bv[kk] = (tv && j < n) ? B[t * bt + j * bj] : 0.0;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 7; ++kk)
+      if (k0 + kk < nks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], bv[kk], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
 // P1 of a middle segment [a, b) after its chain from V_b = 0 (workgroup-wide), from the factor the chain left (LDL'
 // columns F = L D of M^0_uu,k in Lf_k, its x rows F_x and rhs row F_r in K_k / kf_k): with Yd_k = B_k L_k^-T D_k^-1
 // (nx x nu_k, row-wise forward substitution; a guarded pivot's column 0),
@@ -209,52 +233,48 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
     __syncthreads();
     OCP_SPANG_END(12, t_2, 1);
     OCP_SPAN_BEGIN(t_3);
-    // (4) backward over the chunk's stages, one phase each: Phi Acl_k, Gs = Phi Ys_k, f += Phi bcl_k, and the W update
-    // of the stage before (its Gs from the last phase)
+    // (4) backward over the chunk's stages, one phase each: Phi [Acl_k Yd_k bcl_k] (one nx x (nx + nu_k + 1) product:
+    // Phi Acl_k, Gs = Phi Yd_k D^1/2, f += Phi bcl_k) and the W update of the stage before (its Gs from the last phase),
+    // 16 x 16 tiles on the matrix cores, tile w + 4 v on wave w
     for (int k = ce - 1; k >= cb; --k) {
-      const int mk = L.nu[k], hq = (mk + 1) >> 1;
-      const double* O = Op + (k - cb) * ssz;
-      const double* Acl = O;
-      const double* Yd = O + nxx;
-      const double* bcl = Yd + nx * mk;
-      const double* F = bcl + nx;
+      const int mk = L.nu[k], LX = nx + mk + 1;
+      const double* X = Op + (k - cb) * ssz;  // [Acl | Yd | bcl], column-major, ld nx
+      const double* F = X + nx * LX;
       const double* Ph = cur ? Ph1 : Ph0;
       double* Pn = cur ? Ph0 : Ph1;
       double* Gn = cur ? Gs1 : Gs0;
       const double* Gp = cur ? Gs0 : Gs1;
-      const int n0 = hb * hb, n1 = n0 + hb * hq, n2 = n1 + hb, n3 = n2 + (mprev > 0 ? hb * hb : 0);
-      for (int w = tid; w < n3; w += NT) {
-        double c[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-        if (w < n0) {
-          const int i0 = 2 * (w % hb), j0 = 2 * (w / hb);
-          blk2(Ph, 1, nx, Acl, 1, nx, i0, j0, nx, nx, nx, c);
-          st2(Pn, nx, i0, j0, nx, nx, c);
-        } else if (w < n1) {
-          const int v = w - n0, i0 = 2 * (v % hb), q0 = 2 * (v / hb);
-          blk2(Ph, 1, nx, Yd, 1, nx, i0, q0, nx, mk, nx, c);
+      const int nt = (nx + 15) >> 4, nP = nt * ((LX + 15) >> 4), nW = mprev > 0 ? nt * nt : 0;
+      const int lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+      for (int w = tid >> 6; w < nP + nW; w += 4) {
+        if (w < nP) {
+          const int r0 = 16 * (w % nt), c0 = 16 * (w / nt), j = c0 + lr;
+          const v4d acc = mtile(Ph, 1, nx, X, 1, nx, r0, c0, nx, LX, nx, v4d{0.0, 0.0, 0.0, 0.0});
+          const int qd = (j >= nx && j < nx + mk) ? j - nx : 0;
+          const double d = F[qd * mk + qd], sd = d > 1e-200 ? sqrt(d) : 0.0;
 #pragma unroll
-          for (int y = 0; y < 2; ++y) {
-            const int qq = q0 + y < mk ? q0 + y : mk - 1;
-            const double d = F[qq * mk + qq], sd = d > 1e-200 ? sqrt(d) : 0.0;
-            c[0][y] *= sd;
-            c[1][y] *= sd;
+          for (int q = 0; q < 4; ++q) {
+            const int i = r0 + lk + 4 * q;
+            if (i < nx) {
+              if (j < nx) Pn[j * nx + i] = acc[q];
+              else if (j < nx + mk) Gn[(j - nx) * nx + i] = acc[q] * sd;
+              else if (j == nx + mk) fv[i] += acc[q];
+            }
           }
-          st2(Gn, nx, i0, q0, nx, mk, c);
-        } else if (w < n2) {
-          const int i0 = 2 * (w - n1);
-#pragma unroll
-          for (int x = 0; x < 2; ++x) c[x][0] = fv[i0 + x < nx ? i0 + x : nx - 1];
-          blk2(Ph, 1, nx, bcl, 1, 0, i0, 0, nx, 1, nx, c);
-          st2(fv, nx, i0, 0, nx, 1, c);
         } else {
-          const int v = w - n2, i0 = 2 * (v % hb), j0 = 2 * (v / hb);
+          const int v = w - nP, r0 = 16 * (v % nt), c0 = 16 * (v / nt), j = c0 + lr;
+          v4d acc;
 #pragma unroll
-          for (int x = 0; x < 2; ++x)
+          for (int q = 0; q < 4; ++q) {
+            const int i = r0 + lk + 4 * q;
+            acc[q] = (i < nx && j < nx) ? Wm[j * nx + i] : 0.0;
+          }
+          acc = mtile(Gp, 1, nx, Gp, nx, 1, r0, c0, nx, nx, mprev, acc);
 #pragma unroll
-            for (int y = 0; y < 2; ++y)
-              c[x][y] = Wm[(j0 + y < nx ? j0 + y : nx - 1) * nx + (i0 + x < nx ? i0 + x : nx - 1)];
-          blk2(Gp, 1, nx, Gp, nx, 1, i0, j0, nx, nx, mprev, c);
-          st2(Wm, nx, i0, j0, nx, nx, c);
+          for (int q = 0; q < 4; ++q) {
+            const int i = r0 + lk + 4 * q;
+            if (i < nx && j < nx) Wm[j * nx + i] = acc[q];
+          }
         }
       }
       mprev = mk;
@@ -266,17 +286,24 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
   // the last stage's W update, then M = [W 0; 0 0] (lower triangle, rows / columns up to the 4 x 4 blocks' pad)
   const double* Gp = cur ? Gs0 : Gs1;
   const int n1 = 2 * nx + 1, np = (n1 + 3) & ~3;
-  if (mprev > 0)
-    for (int w = tid; w < hb * hb; w += NT) {
-      const int i0 = 2 * (w % hb), j0 = 2 * (w / hb);
-      double c[2][2];
+  if (mprev > 0) {
+    const int nt = (nx + 15) >> 4, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+    for (int v = tid >> 6; v < nt * nt; v += 4) {
+      const int r0 = 16 * (v % nt), c0 = 16 * (v / nt), j = c0 + lr;
+      v4d acc;
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int q = 0; q < 4; ++q) {
+        const int i = r0 + lk + 4 * q;
+        acc[q] = (i < nx && j < nx) ? Wm[j * nx + i] : 0.0;
+      }
+      acc = mtile(Gp, 1, nx, Gp, nx, 1, r0, c0, nx, nx, mprev, acc);
 #pragma unroll
-        for (int y = 0; y < 2; ++y) c[x][y] = Wm[(j0 + y < nx ? j0 + y : nx - 1) * nx + (i0 + x < nx ? i0 + x : nx - 1)];
-      blk2(Gp, 1, nx, Gp, nx, 1, i0, j0, nx, nx, mprev, c);
-      st2(Wm, nx, i0, j0, nx, nx, c);
+      for (int q = 0; q < 4; ++q) {
+        const int i = r0 + lk + 4 * q;
+        if (i < nx && j < nx) Wm[j * nx + i] = acc[q];
+      }
     }
+  }
   __syncthreads();
   for (int e = tid; e < np * np; e += NT) {
     const int i = e / np, j = e - i * np;
@@ -307,18 +334,21 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
 
 // P2 on one workgroup: the exact value function at the boundaries c_{S-1} .. c_1 into the segment buffer (the last
 // segment's own P, p at c_{S-1}; then the combine per middle segment, see the header): T = P_b U (+ p_b on the f
-// column: h), the M image's lower triangle T' U + [I; P^0_a; p^0_a] (2 x 2 blocks), chain_elim of its nx pivots on wave
-// 0; its Paug image is [P_a p_a]. Region A holds U, T, P_b, p_b; region B the chain's M image, factor and Paug images.
+// column: h), the M image's lower triangle T' U + [I; P^0_a; p^0_a], both as 16 x 16 tiles on the matrix cores (U and T
+// kept row-major, so that each tile's loads are unit-stride across its lanes); chain_elim of its nx pivots on wave 0;
+// its Paug image is [P_a p_a]. Region A holds U, T, P_b, p_b; region B the chain's M image, factor and Paug images.
 // Returns false on a NaN or dropped pivot (then the serial chain runs).
+constexpr double SEG_CANCEL = 1e5;  // largest max D_ii / max P_a,ii a combine may leave (about 1e-11 relative error)
 __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, double* sq, int S, int N) {
   const OcpLayout& L = V.L;
-  const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx, hb = (nx + 1) >> 1;
-  const int LU = 2 * nx + 1, hu = (LU + 1) >> 1, np = (LU + 3) & ~3;
+  const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx;
+  const int LU = 2 * nx + 1, np = (LU + 3) & ~3, nt = (nx + 15) >> 4, nu4 = (LU + 15) >> 4;
+  const int lane = tid & 63, lr = lane & 15, lk = lane >> 4;
   const int esz = seg_esz(nx), bsz = seg_bsz(nx);
   double* bnd = sq + OCP_GRID_MAX_G * esz;
-  double* U = CS.G0;        // [Gw Phi f], column-major nx x LU
-  double* T = U + nx * LU;  // P_b U, then + p_b on column 2 nx
-  double* Pb = T + nx * LU;
+  double* Ut = CS.G0;        // U = [Gw Phi f] row-major: U(t, j) at t LU + j
+  double* Tt = Ut + nx * LU; // T = P_b U (+ p_b on column 2 nx), row-major
+  double* Pb = Tt + nx * LU;
   double* pb = Pb + nxx;
   double* Ml = CS.Ml;
   {
@@ -340,52 +370,65 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
   bool ok = true;
   for (int s = S - 2; s >= 1; --s) {
     const int cs = seg_begin(N, S, s);
-    const double* el = sq + s * esz;
-    for (int e = tid; e < nx * LU; e += NT) U[e] = el[e];
-    __syncthreads();
-    OCP_SPAN_BEGIN(t_a);
-    for (int w = tid; w < hb * hu; w += NT) {
-      const int i0 = 2 * (w % hb), j0 = 2 * (w / hb);
-      double c[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-      blk2(Pb, 1, nx, U, 1, nx, i0, j0, nx, LU, nx, c);
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-          if (j0 + y == 2 * nx) c[x][y] += pb[i0 + x < nx ? i0 + x : nx - 1];
-      st2(T, nx, i0, j0, nx, LU, c);
+    const double* el = sq + s * esz;  // U column-major
+    for (int e = tid; e < nx * LU; e += NT) {
+      const int j = e / nx, t = e - j * nx;
+      Ut[t * LU + j] = el[e];
     }
     __syncthreads();
-    // M(i, j), i >= j: T(:, i)' U(:, j) + (i == j < nx) + P^0_a / p^0_a in the x rows
+    OCP_SPAN_BEGIN(t_a);
+    for (int w = tid >> 6; w < nt * nu4; w += 4) {
+      const int r0 = 16 * (w % nt), c0 = 16 * (w / nt), j = c0 + lr;
+      v4d acc = mtile(Pb, 1, nx, Ut, LU, 1, r0, c0, nx, LU, nx, v4d{0.0, 0.0, 0.0, 0.0});
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = r0 + lk + 4 * q;
+        if (i < nx && j < LU) Tt[i * LU + j] = acc[q] + (j == 2 * nx ? pb[i] : 0.0);
+      }
+    }
+    __syncthreads();
+    // M(i, j), i >= j: T(:, i)' U(:, j) + (i == j < nx) + P^0_a / p^0_a in the x rows (lower 16 x 16 tiles)
     const double* P0 = V.P(cs);
     const double* p0 = V.pv() + (long long)cs * nx;
-    for (int w = tid; w < hu * (hu + 1) / 2; w += NT) {
-      int bi, bj;
-      ch_block(w, bi, bj);
-      const int i0 = 2 * bi, j0 = 2 * bj;
-      double c[2][2];
+    for (int w = tid >> 6; w < nu4 * (nu4 + 1) / 2; w += 4) {
+      int rb = 0;
+      while ((rb + 1) * (rb + 2) / 2 <= w) ++rb;
+      const int cb = w - rb * (rb + 1) / 2, r0 = 16 * rb, c0 = 16 * cb, j = c0 + lr;
+      v4d acc;
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int q = 0; q < 4; ++q) {
+        const int i = r0 + lk + 4 * q;
+        double v = (i == j && i < nx) ? 1.0 : 0.0;
+        if (i >= nx && i < 2 * nx && j >= nx && j < 2 * nx) v = P0[(j - nx) * nx + (i - nx)];
+        else if (i == 2 * nx && j >= nx && j < 2 * nx) v = p0[j - nx];
+        acc[q] = v;
+      }
+      acc = mtile(Tt, 1, LU, Ut, LU, 1, r0, c0, LU, LU, nx, acc);
 #pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          const int i = i0 + x, j = j0 + y;
-          double v = (i == j && i < nx) ? 1.0 : 0.0;
-          if (i >= nx && i < 2 * nx && j >= nx && j < 2 * nx) v = P0[(j - nx) * nx + (i - nx)];
-          else if (i == 2 * nx && j >= nx && j < 2 * nx) v = p0[j - nx];
-          c[x][y] = v;
-        }
-      blk2(T, nx, 1, U, 1, nx, i0, j0, LU, LU, nx, c);
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-          if (i0 + x < LU && j0 + y <= i0 + x) Ml[(i0 + x) * CH_GS + j0 + y] = c[x][y];
+      for (int q = 0; q < 4; ++q) {
+        const int i = r0 + lk + 4 * q;
+        if (i < LU && j <= i) Ml[i * CH_GS + j] = acc[q];
+      }
     }
     __syncthreads();
     OCP_SPANG_END(14, t_a, 0);
     OCP_SPAN_BEGIN(t_g);
     int fl = 0;
-    if (tid < 64) fl = chain_elim<2, true>(V, CS, nx, CS.F0, CS.Pa2);
+    if (tid < 64) {
+      fl = chain_elim<2, true>(V, CS, nx, CS.F0, CS.Pa2);
+      // cancellation guard: P_a = D - C'N^-1 C loses log10(max D_ii / max P_a,ii) digits; past SEG_CANCEL the combine
+      // is refused and the serial chain runs
+      double dm = 0.0, am = 0.0;
+      if (tid < nx) {
+        dm = Ml[(nx + tid) * CH_GS + nx + tid];
+        am = CS.Pa2[tid * CH_PS + tid];
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        dm = fmax(dm, __shfl_xor(dm, o));
+        am = fmax(am, __shfl_xor(am, o));
+      }
+      if (!(dm <= SEG_CANCEL * am)) fl |= CH_WEAK;
+    }
     ok = ok && !__syncthreads_or(fl);
     OCP_SPANG_END(15, t_g, 0);
     OCP_SPAN_BEGIN(t_p);
@@ -401,4 +444,133 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
     OCP_SPANG_END(16, t_p, 0);
   }
   return ok;
+}
+
+// ---- the partitioned affine scan (the grid form's serial vector recursions: chain_affine's forward rollout
+// dx_{k+1} = Acl_k dx_k + bcl_k and the corrector's p_k = Acl_k' p_{k+1} + h_k) ----
+// Step s of the sequence maps y_s to y_{s+1} = M_s y_s + c_s (forward: M_s = Acl_{1+s}, c_s = bcl_{1+s}; backward:
+// M_s = Acl_{N-1-s}', c_s = h_{N-1-s}); segment g owns the steps [a_g, a_{g+1}), a_g = floor(n g / S), n = N - 1.
+//   A: every segment composes its steps' affine maps, [Psi_g psi_g] = M_{a_{g+1}-1} .. M_{a_g} [I 0] + ..., into the
+//      segment buffer (affine_comp, on the matrix cores);
+//   B: one workgroup carries the boundary values y_{a_g} = Psi_{g-1} y_{a_{g-1}} + psi_{g-1} (g = 1 .. S-1, from the
+//      recursion's initial value) into the output rows (affine_bound);
+//   C: every segment runs its steps from its boundary value (chain_affine over the range; the last output row, the
+//      next segment's boundary value, stays as B wrote it).
+// The serial depth is ~2 n / S steps plus S - 1 matrix-vector products instead of n steps.
+__device__ __forceinline__ int aff_begin(int n, int S, int g) { return (int)((long long)n * g / S); }
+
+// A for one segment (workgroup-wide): the steps' matrices and offsets staged in LDS in chunks (region B), the
+// composition on the matrix cores ([Psi psi] double-buffered in region A, one 16 x 16 tile per wave per step), the
+// result [Psi psi] (column-major nx x (nx + 1)) to dst
+template <bool BWD>
+__device__ __forceinline__ void affine_comp(const View& V, const ChainLds& CS, int s0, int s1, double* dst) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, nxx = nx * nx, LX = nx + 1;
+  const int SS = (nxx + nx + 1) & ~1, cmax = CH_SCRATCH / SS;
+  const int nt = (nx + 15) >> 4, nc = (LX + 15) >> 4, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+  const double* vec = BWD ? V.h() : V.bcl();
+  double* X0 = CS.G0;
+  double* X1 = X0 + nx * LX;
+  for (int e = tid; e < nx * LX; e += NT) {
+    const int i = e % nx, j = e / nx;
+    X0[e] = i == j ? 1.0 : 0.0;
+  }
+  int cur = 0;
+  for (int cb = s0; cb < s1; cb += cmax) {
+    const int ce = cb + cmax < s1 ? cb + cmax : s1, cnt = ce - cb;
+    {  // the chunk's [M_s (as stored: Acl_k column-major) | c_s], 16 loads per thread before their stores
+      int sx = tid / SS, ox = tid - sx * SS;
+      for (int base = 0; base < cnt * SS; base += 16 * NT) {
+        double r[16];
+        int sl[16], ol[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sl[i] = sx;
+          ol[i] = ox;
+          const int k = BWD ? N - 1 - (cb + sx) : 1 + cb + sx;
+          const double* src = ox < nxx ? V.Acl(k) + ox : (ox < nxx + nx ? vec + (long long)k * nx + (ox - nxx) : nullptr);
+          r[i] = (sx < cnt && src) ? *src : 0.0;
+          ox += NT;
+          while (ox >= SS) {
+            ox -= SS;
+            ++sx;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (sl[i] < cnt) CS.Ml[sl[i] * SS + ol[i]] = r[i];
+      }
+    }
+    __syncthreads();
+    for (int s = 0; s < cnt; ++s) {
+      const double* M = CS.Ml + s * SS;
+      const double* Xc = cur ? X1 : X0;
+      double* Xn = cur ? X0 : X1;
+      for (int w = tid >> 6; w < nt * nc; w += 4) {
+        const int r0 = 16 * (w % nt), c0 = 16 * (w / nt), j = c0 + lr;
+        v4d acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = r0 + lk + 4 * q;
+          acc[q] = (j == nx && i < nx) ? M[nxx + i] : 0.0;
+        }
+        // forward M(i, t) = Acl(i, t) at [t nx + i]; backward M(i, t) = Acl(t, i) at [i nx + t]
+        acc = mtile(M, BWD ? nx : 1, BWD ? 1 : nx, Xc, 1, nx, r0, c0, nx, LX, nx, acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = r0 + lk + 4 * q;
+          if (i < nx && j < LX) Xn[j * nx + i] = acc[q];
+        }
+      }
+      cur ^= 1;
+      __syncthreads();
+    }
+  }
+  const double* Xc = cur ? X1 : X0;
+  for (int e = tid; e < nx * LX; e += NT) dst[e] = Xc[e];
+  __syncthreads();
+}
+
+// B on one workgroup: y at the start of segments 1 .. S-1 from the recursion's initial value through the compositions
+// (staged in LDS region B: (S - 1) nx (nx + 1) doubles; wave 0, y in LDS), into the output rows
+template <bool BWD>
+__device__ __forceinline__ void affine_bound(const View& V, const ChainLds& CS, const double* sq, int S, double* y) {
+  const OcpLayout& L = V.L;
+  const int tid = threadIdx.x, nx = L.nx, N = L.N, n = N - 1, esz = seg_esz(nx), LX = nx + 1;
+  double* out = BWD ? V.pv() : V.dx();
+  double* Ps = CS.Ml;  // [S - 1][nx (nx + 1)]
+  const int tot = (S - 1) * nx * LX;
+  for (int e = tid; e < tot; e += NT) {
+    const int g = e / (nx * LX), o = e - g * (nx * LX);
+    Ps[e] = sq[(long long)g * esz + o];
+  }
+  if (tid < nx) y[tid] = BWD ? V.gx()[(long long)N * nx + tid] : V.bcl()[tid];
+  __syncthreads();
+  if (tid < 64) {
+    for (int g = 1; g < S; ++g) {
+      const double* P = Ps + (g - 1) * nx * LX;
+      const int a = aff_begin(n, S, g);
+      const long long rw = BWD ? N - a : 1 + a;
+      if (tid < nx) {
+        double acc = P[nx * nx + tid];
+        for (int c0 = 0; c0 < nx; c0 += 8) {
+          double pv[8], yv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int c = c0 + u < nx ? c0 + u : nx - 1;
+            pv[u] = P[c * nx + tid];
+            yv[u] = y[c];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (c0 + u < nx) acc = fma(pv[u], yv[u], acc);
+        }
+        __builtin_amdgcn_wave_barrier();
+        y[tid] = acc;
+        out[rw * nx + tid] = acc;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  __syncthreads();
 }

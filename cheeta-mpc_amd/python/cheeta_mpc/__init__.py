@@ -133,6 +133,7 @@ def lib():
     L.cmpc_ocp_segments.argtypes = [vp, C.c_int]
     L.cmpc_ocp_set_grid_timeout.argtypes = [vp, C.c_double]
     L.cmpc_ocp_fallback_count.argtypes = [vp]
+    L.cmpc_ocp_partition_fallback_count.argtypes = [vp]
     L.cmpc_ocp_debug_force_grid_timeout.argtypes = [vp, C.c_int]
     L.cmpc_ocp_staging.argtypes = [vp, C.c_int]
     L.cmpc_ocp_staging.restype = d
@@ -612,6 +613,14 @@ class OcpSolver:
         n = int(lib().cmpc_ocp_fallback_count(self.h))
         if n < 0:
             _chk(n, "cmpc_ocp_fallback_count")
+        return n
+
+    @property
+    def partition_fallbacks(self):
+        """Factorisations of the partitioned form that fell back to the serial chain since the handle was created."""
+        n = int(lib().cmpc_ocp_partition_fallback_count(self.h))
+        if n < 0:
+            _chk(n, "cmpc_ocp_partition_fallback_count")
         return n
 
     def reshape(self, N, nx, nu, nc=None):

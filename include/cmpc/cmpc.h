@@ -348,11 +348,15 @@ int cmpc_ocp_grid(const cmpc_ocp* ocp, int B);
  * segments on the problem's first S workgroups — each middle segment factorised from a zero end value and summarised
  * by its closed-loop transition, offset and controllability Gramian, the exact boundary values combined backward on
  * one workgroup, then every segment refactorised from its exact end value — so the serial depth is ~2 N / S stages
- * plus S - 2 combines instead of N stages. The result is the serial chain's factorisation up to rounding (a pivot the
- * first pass drops, or a failed combine, falls back to the serial chain). S = 0 (default): ~sqrt(2 N), at most G and
- * N; S = 1: the serial chain. cmpc_ocp_segments returns the S a batch of B problems runs with. */
+ * plus S - 2 combines instead of N stages. The result is the serial chain's factorisation up to rounding: a pivot the
+ * first pass drops, a NaN, or a combine that would cancel more than 5 digits (an unstable segment: its free-evolution
+ * cost-to-go exceeds the optimal one by > 1e5) falls back to the serial chain for that factorisation, counted by
+ * cmpc_ocp_partition_fallback_count (since the handle was created; synchronises on the last solve). S = 0 (default):
+ * ~sqrt(2 N), at most G and N; S = 1: the serial chain. cmpc_ocp_segments returns the S a batch of B problems runs
+ * with. */
 int cmpc_ocp_set_segments(cmpc_ocp* ocp, int S);
 int cmpc_ocp_segments(const cmpc_ocp* ocp, int B);
+int cmpc_ocp_partition_fallback_count(cmpc_ocp* ocp);
 int cmpc_ocp_set_grid_timeout(cmpc_ocp* ocp, double us);
 int cmpc_ocp_fallback_count(cmpc_ocp* ocp);
 int cmpc_ocp_debug_force_grid_timeout(cmpc_ocp* ocp, int on);

@@ -53,7 +53,7 @@ def run(projected, B, reps=int(os.environ.get("OCP_REPS", "5"))):
     print(f"{'projected' if projected else 'rows     '} B={B:5d} N={p0['N']} nx=24 nu={sorted(set(p0['nu']))} "
           f"kernel {per:8.3f} ms/solve ({B / per * 1e3:9.0f} solves/s), iters {it.mean():.2f}, "
           f"status ok {np.mean(st == 0):.2f}; host path {th:.2f} ms; path {s.path} grid {s.grid(B)} segments "
-          f"{s.segments(B)} fallbacks {s.fallback_count}", flush=True)
+          f"{s.segments(B)} fallbacks {s.fallback_count} serial fallbacks {s.partition_fallbacks}", flush=True)
 
 
 if __name__ == "__main__" and "--stamps" not in sys.argv and "--chain" not in sys.argv:
