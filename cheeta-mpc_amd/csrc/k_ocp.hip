@@ -1857,7 +1857,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   // chain on workgroup 0. Leaves mine[5] = the NaN flag for the caller's barrier + collect. Partials: the first
   // pass's flags in slot 4, the combine's in slot 6 (both collected well before their next writers, see above).
   double* segq = a.seg ? a.seg + (long long)q * a.seg_stride : nullptr;
-  const int nseg = (FAST && segq) ? part_segments(a.nseg, G, N) : 1;
+  const int nseg = (FAST && segq) ? part_segments(a.nseg, G, N, L.m) : 1;
   // segments of the partitioned affine scans (ocp_part.hpp): at most the steps N - 1 and what affine_bound stages
   const int naff = [&] {
     int Sa = nseg < N - 1 ? nseg : N - 1;

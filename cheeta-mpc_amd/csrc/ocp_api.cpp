@@ -550,7 +550,7 @@ int cmpc_ocp_segments(const cmpc_ocp* o, int B) {
   const int G = cmpc_ocp_grid(o, B);
   if (G < 0) return G;
   if (G == 0 || !o->seg.p) return 1;
-  int S = o->nseg > 0 ? o->nseg : (int)(std::sqrt(2.0f * (float)o->N) + 0.5f);  // part_segments (ocp_part.hpp)
+  int S = o->nseg > 0 ? o->nseg : (int)(std::sqrt((o->m > 0 ? 2.0f : 1.0f) * (float)o->N) + 0.5f);  // part_segments
   S = std::min(S, std::min(G, o->N));
   return S < 1 ? 1 : S;
 }

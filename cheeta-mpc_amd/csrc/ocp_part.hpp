@@ -36,9 +36,11 @@ __device__ __forceinline__ int seg_begin(int N, int S, int s) { return (int)((lo
 // (seg_esz / seg_bsz: k_ocp.hpp)
 
 // Segments of the partitioned factorisation for a grid of G workgroups (want: cmpc_ocp_set_segments, 0 = auto): at
-// most G and N; auto ~ sqrt(2 N) (two chain passes of N / S stages plus S - 2 combines of about a stage each)
-__device__ __forceinline__ int part_segments(int want, int G, int N) {
-  int S = want > 0 ? want : (int)(sqrtf(2.0f * (float)N) + 0.5f);
+// most G and N; auto ~ sqrt(N) without rows, sqrt(2 N) with them (two chain passes of N / S stages and the segment
+// elements against S - 2 combines; with rows the three affine scans per iteration also shorten with S; measured
+// optimum at the legged size: 7-8 / 12-14)
+__device__ __forceinline__ int part_segments(int want, int G, int N, int m) {
+  int S = want > 0 ? want : (int)(sqrtf((m > 0 ? 2.0f : 1.0f) * (float)N) + 0.5f);
   if (S > G) S = G;
   if (S > N) S = N;
   return S < 1 ? 1 : S;
@@ -350,7 +352,28 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
   double* Tt = Ut + nx * LU; // T = P_b U (+ p_b on column 2 nx), row-major
   double* Pb = Tt + nx * LU;
   double* pb = Pb + nxx;
+  double* P0s = pb + 32;  // P^0_a, p^0_a of the boundary (column-major, then the vector)
   double* Ml = CS.Ml;
+  // the next combine's element and P^0 / p^0 in registers: their global loads (written by other workgroups) overlap
+  // the current combine
+  double rel[6], rp0[3];
+  auto prefetch = [&](int s) {
+    const double* el = sq + s * esz;
+    const int cs = seg_begin(N, S, s);
+    const double* P0 = V.P(cs);
+    const double* p0 = V.pv() + (long long)cs * nx;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int e = tid + NT * i;
+      rel[i] = e < nx * LU ? el[e] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = tid + NT * i;
+      rp0[i] = e < nxx ? P0[e] : (e < nxx + nx ? p0[e - nxx] : 0.0);
+    }
+  };
+  if (S > 2) prefetch(S - 2);
   {
     const int cl = seg_begin(N, S, S - 1);
     const double* P = V.P(cl);
@@ -369,12 +392,17 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
   }
   bool ok = true;
   for (int s = S - 2; s >= 1; --s) {
-    const int cs = seg_begin(N, S, s);
-    const double* el = sq + s * esz;  // U column-major
-    for (int e = tid; e < nx * LU; e += NT) {
-      const int j = e / nx, t = e - j * nx;
-      Ut[t * LU + j] = el[e];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {  // U (column-major in the segment buffer) transposed into Ut
+      const int e = tid + NT * i, j = e / nx, t = e - j * nx;
+      if (e < nx * LU) Ut[t * LU + j] = rel[i];
     }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = tid + NT * i;
+      if (e < nxx + nx) P0s[e] = rp0[i];
+    }
+    if (s > 1) prefetch(s - 1);
     __syncthreads();
     OCP_SPAN_BEGIN(t_a);
     for (int w = tid >> 6; w < nt * nu4; w += 4) {
@@ -388,8 +416,8 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
     }
     __syncthreads();
     // M(i, j), i >= j: T(:, i)' U(:, j) + (i == j < nx) + P^0_a / p^0_a in the x rows (lower 16 x 16 tiles)
-    const double* P0 = V.P(cs);
-    const double* p0 = V.pv() + (long long)cs * nx;
+    const double* P0 = P0s;
+    const double* p0 = P0s + nxx;
     for (int w = tid >> 6; w < nu4 * (nu4 + 1) / 2; w += 4) {
       int rb = 0;
       while ((rb + 1) * (rb + 2) / 2 <= w) ++rb;

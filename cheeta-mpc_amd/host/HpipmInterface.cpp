@@ -227,6 +227,10 @@ class HpipmInterface::Impl {
   }
 
   int allocations() const { return ocp_ ? cmpc_ocp_alloc_count(ocp_) : -1; }
+  void setKeep(bool on) {
+    keep_ = on;
+    if (ocp_) (void)cmpc_ocp_set_keep_riccati(ocp_, on ? 1 : 0);
+  }
   void enableTiming(bool on) {
     timing_ = on;
     if (ocp_) (void)cmpc_ocp_enable_timing(ocp_, on ? 1 : 0);
@@ -340,7 +344,7 @@ class HpipmInterface::Impl {
     }
     // the MPC reads the feedback policy of every solve (MultipleShootingSolver.cpp:337-341, useFeedbackPolicy): the
     // solve leaves its exit Riccati quantities, the getters copy them
-    (void)cmpc_ocp_set_keep_riccati(ocp_, 1);
+    (void)cmpc_ocp_set_keep_riccati(ocp_, keep_ ? 1 : 0);
     if (timing_) (void)cmpc_ocp_enable_timing(ocp_, 1);
     ocpN_ = N;
     ocpNx_ = nx;
@@ -622,6 +626,7 @@ class HpipmInterface::Impl {
   double minEig_ = 0.0;     // setRiccatiMinimumEigenvalue (0: no clamp)
   bool minEigSet_ = false;  // a minimum was set (otherwise, with ocs2_core, ocs2's own default clamps)
   bool timing_ = false;  // enableDeviceTiming
+  bool keep_ = true;     // keepRiccati
   std::vector<double> xbuf_, ubuf_, recbuf_, crecbuf_, x0buf_, Pm_, pv_, K_, k_, Lr_, K0_, k0_, S0_, s0_;
 };
 
@@ -650,5 +655,6 @@ void HpipmInterface::setRiccatiMinimumEigenvalue(double minEigenValue) { pImpl_-
 int HpipmInterface::deviceAllocations() const { return pImpl_->allocations(); }
 void HpipmInterface::enableDeviceTiming(bool on) { pImpl_->enableTiming(on); }
 double HpipmInterface::lastSolveDeviceMs() const { return pImpl_->lastSolveMs(); }
+void HpipmInterface::keepRiccati(bool on) { pImpl_->setKeep(on); }
 
 }  // namespace ocs2

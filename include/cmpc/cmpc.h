@@ -351,9 +351,10 @@ int cmpc_ocp_grid(const cmpc_ocp* ocp, int B);
  * plus S - 2 combines instead of N stages. The result is the serial chain's factorisation up to rounding: a pivot the
  * first pass drops, a NaN, or a combine that would cancel more than 5 digits (an unstable segment: its free-evolution
  * cost-to-go exceeds the optimal one by > 1e5) falls back to the serial chain for that factorisation, counted by
- * cmpc_ocp_partition_fallback_count (since the handle was created; synchronises on the last solve). S = 0 (default):
- * ~sqrt(2 N), at most G and N; S = 1: the serial chain. cmpc_ocp_segments returns the S a batch of B problems runs
- * with. */
+ * cmpc_ocp_partition_fallback_count (since the handle was created; synchronises on the last solve). The serial vector
+ * recursions (the rollout, the corrector's cost-to-go) run as a partitioned affine scan over the same segments.
+ * S = 0 (default): ~sqrt(N) without rows, ~sqrt(2 N) with rows, at most G and N; S = 1: the serial chain.
+ * cmpc_ocp_segments returns the S a batch of B problems runs with. */
 int cmpc_ocp_set_segments(cmpc_ocp* ocp, int S);
 int cmpc_ocp_segments(const cmpc_ocp* ocp, int B);
 int cmpc_ocp_partition_fallback_count(cmpc_ocp* ocp);

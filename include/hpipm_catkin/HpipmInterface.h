@@ -110,6 +110,9 @@ class HpipmInterface {
    * solve's kernel time in ms (cmpc_ocp_last_solve_ms; NaN without a handle or with timing off). */
   void enableDeviceTiming(bool on);
   double lastSolveDeviceMs() const;
+  /* Extension for measuring what keeping the exit factorisation costs: on (default) every solve leaves its exit Riccati
+   * quantities for the getters (cmpc_ocp_set_keep_riccati); off, the getters refactorise on demand. */
+  void keepRiccati(bool on);
 
  private:
   class Impl;

@@ -159,13 +159,31 @@ int main(int argc, char** argv) {
     t_tick.push_back(ms(t0, t3));
     t_kernel.push_back(kern);
   }
+  // the same ticks again without keeping the exit factorisation: the keep's kernel cost, tick by tick
+  std::vector<double> t_kernel_nokeep, t_keep_cost;
+  {
+    HpipmInterface h2;
+    h2.enableDeviceTiming(true);
+    h2.keepRiccati(false);
+    for (int t = 0; t < T; ++t) {
+      Tick& k = ticks[(size_t)t];
+      vector_array_t xs, us;
+      h2.resize(hpipm_interface::extractSizesFromProblem(k.dyn, k.cost, k.rows ? &k.con : nullptr));
+      (void)h2.solve(k.x0, k.dyn, k.cost, k.rows ? &k.con : nullptr, xs, us, false);
+      const double kern = h2.lastSolveDeviceMs();
+      if (t < warm) continue;
+      t_kernel_nokeep.push_back(kern);
+      t_keep_cost.push_back(t_kernel[(size_t)(t - warm)] - kern);
+    }
+  }
   std::printf("{\"ticks\": %d, \"timed\": %zu, \"success\": %d, \"rows\": %s, "
               "\"tick_ms_median\": %.4f, \"tick_ms_p90\": %.4f, \"resize_ms_median\": %.4f, \"solve_ms_median\": %.4f, "
               "\"solve_ms_p90\": %.4f, \"feedback_ms_median\": %.4f, \"feedback_ms_p90\": %.4f, "
-              "\"kernel_ms_median\": %.4f, \"host_over_kernel_ms_median\": %.4f, \"allocations_after_warmup\": %d}\n",
+              "\"kernel_ms_median\": %.4f, \"host_over_kernel_ms_median\": %.4f, \"allocations_after_warmup\": %d, "
+              "\"kernel_ms_median_nokeep\": %.4f, \"keep_cost_ms_median\": %.4f}\n",
               T, t_tick.size(), ok, ticks[0].rows ? "true" : "false", pct(t_tick, 0.5), pct(t_tick, 0.9),
               pct(t_resize, 0.5), pct(t_solve, 0.5), pct(t_solve, 0.9), pct(t_fb, 0.5), pct(t_fb, 0.9),
               pct(t_kernel, 0.5), pct(t_solve, 0.5) - pct(t_kernel, 0.5),
-              hpipm.deviceAllocations() - allocs_warm);
+              hpipm.deviceAllocations() - allocs_warm, pct(t_kernel_nokeep, 0.5), pct(t_keep_cost, 0.5));
   return ok == T ? 0 : 1;
 }

@@ -35,7 +35,7 @@ def test_device_partitioned_factorisation_matches_oracle(cm, op, projected):
         h = cm.OcpSolver(p0["N"], p0["nx"], p0["nu"], p0.get("nc"), max_batch=2)
         h.set_segments(S)
         h.set_keep_riccati(1)
-        want = S if S else int(np.sqrt(2.0 * p0["N"]) + 0.5)
+        want = S if S else int(np.sqrt((2.0 if rows else 1.0) * p0["N"]) + 0.5)
         assert h.segments(2) == min(want, h.grid(2)), S
         x, u, st, it = _solve(h, ps)
         assert np.array_equal(st, st1) and np.array_equal(it, it1), S
