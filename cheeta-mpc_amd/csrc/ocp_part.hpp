@@ -3,7 +3,8 @@
 // Riccati factorisation; restated serially by oracle/ocp_ipm.c:ocp_factor) split over S horizon segments, so that the
 // chain is S times shorter. Included inside k_ocp.hip's anonymous namespace after ocp_chain.hpp.
 //
-// Segment s holds the stages [c_s, c_{s+1}), c_s = floor(N s / S), and runs on workgroup s of the problem's grid.
+// Segment s holds the stages [c_s, c_{s+1}) (seg_begin: the last segment 5/2 times the others) and runs on workgroup s
+// of the problem's grid.
 //   P1 (all segments at once): the last segment runs the chain from the terminal node: its values are exact. Every
 //      middle segment (1 <= s <= S-2) runs the chain from a zero value function at its end node b = c_{s+1} (V^0) and
 //      then forms its element: with the closed loop of that pass, Acl_k = A_k + B_k K^0_k, bcl_k = rb_k + B_k kff^0_k,
@@ -29,7 +30,17 @@
 // guarded-pivot behaviour is always the serial one's.
 #pragma once
 
-__device__ __forceinline__ int seg_begin(int N, int S, int s) { return (int)((long long)N * s / S); }
+// Segment boundaries c_s, s = 0 .. S (c_0 = 0, c_S = N): segments 0 .. S-2 weigh one, the last one 5/2 — in P1 it
+// runs only its chain (about 13 k cycles per stage at the legged size) while the middle ones run the chain and their
+// element (about 33 k), and P3 spans the others; at least one stage per segment
+__device__ __forceinline__ int seg_begin(int N, int S, int s) {
+  if (s <= 0) return 0;
+  if (s >= S) return N;
+  int c = (int)((long long)2 * N * s / (2 * S + 3));
+  if (c < s) c = s;
+  if (c > N - (S - s)) c = N - (S - s);
+  return c;
+}
 
 // Per-problem segment buffer (OcpSolveArgs::seg, doubles): element s (U = [Gw Phi f], column-major nx x (2 nx + 1)) at
 // s * seg_esz(nx); the boundary value of node c_j (P column-major, p) at OCP_GRID_MAX_G * seg_esz(nx) + j * seg_bsz(nx)

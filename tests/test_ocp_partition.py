@@ -18,6 +18,15 @@ from test_ocp_ipm import _check_vs_oracle, _device_batch_path, _rel, _small
 pytestmark = pytest.mark.gpu
 
 
+def _seg_begin(N, S, s):
+    """Segment boundary c_s of csrc/ocp_part.hpp:seg_begin (the last segment weighs 5/2)."""
+    if s <= 0:
+        return 0
+    if s >= S:
+        return N
+    return min(max(2 * N * s // (2 * S + 3), s), N - (S - s))
+
+
 def _solve(h, ps):
     recs, crecs = zip(*[ocpgen.pack(p) for p in ps])
     return h.solve(np.array([p["x0"] for p in ps]), np.array(recs), np.array(crecs) if ps[0].get("nc") else None)
@@ -77,7 +86,7 @@ def test_device_partitioned_dropped_pivot_falls_back_to_the_serial_chain(cm, op)
     p = ocpgen.legged_problem(590, projected=True)
     N = p["N"]
     # the last stage of a middle segment (S = 8): its first-pass end value is 0, so M^0_uu = R_k = 0 there
-    k = next(N * s // 8 - 1 for s in (4, 3, 5, 2, 6) if p["nu"][N * s // 8 - 1] > 0)
+    k = next(_seg_begin(N, 8, s + 1) - 1 for s in (4, 3, 5, 2, 1) if p["nu"][_seg_begin(N, 8, s + 1) - 1] > 0)
     p["R"][k] = np.zeros_like(p["R"][k])
     p["S"][k] = np.zeros_like(p["S"][k])
     p["r"][k] = np.zeros_like(p["r"][k])
