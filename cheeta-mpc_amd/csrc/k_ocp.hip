@@ -1858,6 +1858,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
   // pass's flags in slot 4, the combine's in slot 6 (both collected well before their next writers, see above).
   double* segq = a.seg ? a.seg + (long long)q * a.seg_stride : nullptr;
   const int nseg = (FAST && segq) ? part_segments(a.nseg, G, N, L.m) : 1;
+  unsigned fgen = 0;  // partitioned factorisations so far (the generation of the level word's values)
   // segments of the partitioned affine scans (ocp_part.hpp): at most the steps N - 1 and what affine_bound stages
   const int naff = [&] {
     int Sa = nseg < N - 1 ? nseg : N - 1;
@@ -1897,14 +1898,18 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       return true;
     }
     // phase 0 = P1: the last segment from the terminal node, the middle ones from a zero end value (then their
-    // elements); phase 1 = P3: segments 0 .. nseg-2 from their end node's exact value, or (a dropped pivot in the
-    // first pass, a NaN or a failed combine) the serial chain on workgroup 0. One chain_factor call site (each inlined
-    // copy of the chain costs registers); workgroups g >= nseg only take part in the barriers.
+    // elements); phase 1 = P2 on workgroup 0 with P3 behind it: segment g < nseg-1 refactorises from boundary g + 1's
+    // exact value as soon as workgroup 0 has published it (segment 0, on workgroup 0, after the last combine);
+    // phase 2 (a dropped pivot in the first pass, a NaN or a failed combine): the serial chain on workgroup 0. One
+    // chain_factor call site (each inlined copy of the chain costs registers); workgroups g >= nseg only take part in
+    // the barriers.
     const int cb = seg_begin(N, nseg, g < nseg ? g : nseg), ce = seg_begin(N, nseg, g < nseg ? g + 1 : nseg);
     const bool mid = g >= 1 && g < nseg - 1;
+    unsigned* lvl = bar + 3;
+    const unsigned gen = ++fgen;
     int f = 0;
     bool pok = true;
-    for (int ph = 0; ph < 2; ++ph) {
+    for (int ph = 0; ph < 3; ++ph) {
       bool run;
       int k0 = cb, k1 = ce, term = CH_TERM_ZERO;
       const double* Pt = nullptr;
@@ -1914,11 +1919,27 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
           k1 = N;
           term = CH_TERM_NODE;
         }
-      } else if (pok) {
+      } else if (ph == 1) {
+        if (!pok) continue;
         run = g < nseg - 1;
         term = CH_TERM_GIVEN;
         Pt = segq + OCP_GRID_MAX_G * seg_esz(nx) + (g + 1) * seg_bsz(nx);
+        bool cok = true;
+        if (lead) {
+          cok = seg_combine(V, CS, segq, nseg, N, lvl, gen);
+          run = run && cok;
+        } else if (run) {
+          const int w = seg_wait(bar, lvl, gen * 64u + (unsigned)(nseg - g - 1), gen * 64u + SEG_FAIL, red,
+                                 a.grid_timeout);
+          if (w < 0) {
+            alive = false;
+            return false;
+          }
+          run = w > 0;
+        }
+        if (tid == 0) mine[6] = cok ? 0.0 : 1.0;
       } else {
+        if (pok) break;
         run = lead;
         k0 = 0;
         k1 = N;
@@ -1929,23 +1950,22 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       OCP_SPAN_BEGIN(t_ch);
       f = run ? chain_factor<true>(V, CS, hp, a.reg, k0, k1, term, Pt, Pt ? Pt + nx * nx : nullptr) : 0;
       OCP_SPANG_END(30, t_ch, 1);
-      if (ph == 1) break;
-      OCP_SPAN_BEGIN(t_el);
-      if (f == 0 && mid) f |= seg_element(V, CS, cb, ce, segq + g * seg_esz(nx));
-      OCP_SPANG_END(31, t_el, 1);
-      if (tid == 0) mine[4] = (double)f;
-      if (!sync()) return false;
-      grid_collect(part + 4, G, 1, ops_max, red);
-      OCP_STAMP(18);
-      pok = red[0] == 0.0;
-      if (pok) {  // P2: the boundary values on workgroup 0
-        const bool cok = lead ? seg_combine(V, CS, segq, nseg, N) : true;
-        if (tid == 0) mine[6] = cok ? 0.0 : 1.0;
+      if (ph == 2) break;
+      if (ph == 0) {
+        OCP_SPAN_BEGIN(t_el);
+        if (f == 0 && mid) f |= seg_element(V, CS, cb, ce, segq + g * seg_esz(nx));
+        OCP_SPANG_END(31, t_el, 1);
+        if (tid == 0) mine[4] = (double)f;
+        if (!sync()) return false;
+        grid_collect(part + 4, G, 1, ops_max, red);
+        OCP_STAMP(18);
+        pok = red[0] == 0.0;
+      } else {
         if (!sync()) return false;
         grid_collect(part + 6, G, 1, ops_max, red);
+        OCP_STAMP(19);
         pok = red[0] == 0.0;
       }
-      OCP_STAMP(19);
     }
     OCP_STAMP(29);
     if (tid == 0) mine[5] = (f & CH_NAN) ? 1.0 : 0.0;
@@ -2328,6 +2348,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     if (out == (unsigned)G - 1) {
       __hip_atomic_store(bar + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(bar + 2, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

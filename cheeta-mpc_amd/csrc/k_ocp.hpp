@@ -51,7 +51,7 @@ int ocp_grid_width(int N, int B, int want);  // G for a batch by the CU count (0
 int ocp_grid_for(const OcpLayout& L, int B, int want);  // the same, capped by the kernel's co-residency
 
 // Segment buffer of the grid form's partitioned factorisation (ocp_part.hpp: seg_esz / seg_bsz), doubles
-__host__ __device__ inline int seg_esz(int nx) { return (2 * nx * nx + nx + 1) & ~1; }
+__host__ __device__ inline int seg_esz(int nx) { return (3 * nx * nx + 2 * nx + 1) & ~1; }
 __host__ __device__ inline int seg_bsz(int nx) { return (nx * nx + nx + 1) & ~1; }
 
 // Limits of the latency form of the factorisation (ocp_chain.hpp, small batches)

@@ -30,19 +30,21 @@
 // guarded-pivot behaviour is always the serial one's.
 #pragma once
 
-// Segment boundaries c_s, s = 0 .. S (c_0 = 0, c_S = N): segments 0 .. S-2 weigh one, the last one 5/2 — in P1 it
+// Segment boundaries c_s, s = 0 .. S (c_0 = 0, c_S = N): the middle segments weigh one, the last one 5/2 — in P1 it
 // runs only its chain (about 13 k cycles per stage at the legged size) while the middle ones run the chain and their
-// element (about 33 k), and P3 spans the others; at least one stage per segment
+// element (about 33 k) — and segment 0 one half: its second pass is the only one that waits for the last combine (the
+// others run behind the combines); at least one stage per segment
 __device__ __forceinline__ int seg_begin(int N, int S, int s) {
   if (s <= 0) return 0;
   if (s >= S) return N;
-  int c = (int)((long long)2 * N * s / (2 * S + 3));
+  int c = (int)((long long)N * (10 * s - 5) / (10 * S + 10));
   if (c < s) c = s;
   if (c > N - (S - s)) c = N - (S - s);
   return c;
 }
 
-// Per-problem segment buffer (OcpSolveArgs::seg, doubles): element s (U = [Gw Phi f], column-major nx x (2 nx + 1)) at
+// Per-problem segment buffer (OcpSolveArgs::seg, doubles): element s (U = [Gw Phi f], column-major nx x (2 nx + 1),
+// then P^0, p^0 of its start node) at
 // s * seg_esz(nx); the boundary value of node c_j (P column-major, p) at OCP_GRID_MAX_G * seg_esz(nx) + j * seg_bsz(nx)
 // (seg_esz / seg_bsz: k_ocp.hpp)
 
@@ -328,16 +330,22 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
   if (tid < 64) fl = chain_elim<2, false>(V, CS, nx, CS.F0, CS.Pa2);
   fl = __syncthreads_or(fl & CH_NAN) ? CH_NAN : 0;
   OCP_SPANG_END(13, t_c, 1);
-  // U = [Gw Phi f]: Gw(x, j) = F(x, j) / sqrt(d_j) below the diagonal (0 for a dropped pivot)
+  // U = [Gw Phi f]: Gw(x, j) = F(x, j) / sqrt(d_j) below the diagonal (0 for a dropped pivot); then this pass's
+  // P^0_a, p^0_a (the combine reads them here: the segment's second pass overwrites the workspace's while P2 runs)
   const double* Ph = cur ? Ph1 : Ph0;
-  for (int e = tid; e < 2 * nxx + nx; e += NT) {
+  const double* P0 = V.P(a);
+  const double* p0 = V.pv() + (long long)a * nx;
+  for (int e = tid; e < 3 * nxx + 2 * nx; e += NT) {
     double v;
     if (e < nxx) {
       const int x = e % nx, j = e / nx;
       const double d = CS.F0[j * CH_FS + j];
       v = (x >= j && d > 1e-200) ? CS.F0[j * CH_FS + x] / sqrt(d) : 0.0;
-    } else {
+    } else if (e < 2 * nxx + nx) {
       v = e < 2 * nxx ? Ph[e - nxx] : fv[e - 2 * nxx];
+    } else {
+      const int o = e - (2 * nxx + nx);
+      v = o < nxx ? P0[o] : p0[o - nxx];
     }
     el[e] = v;
   }
@@ -351,8 +359,47 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
 // kept row-major, so that each tile's loads are unit-stride across its lanes); chain_elim of its nx pivots on wave 0;
 // its Paug image is [P_a p_a]. Region A holds U, T, P_b, p_b; region B the chain's M image, factor and Paug images.
 // Returns false on a NaN or dropped pivot (then the serial chain runs).
+// Boundary values published by P2 while P3 runs behind it (the pipelined form): workgroup 0 stores, per
+// factorisation gen, gen * 64 + (S - s) into the problem's level word once boundary s is in the segment buffer
+// (SEG_FAIL: a combine failed), with the grid barrier's hand-off (every thread's stores drained, one agent release);
+// segment g's workgroup waits for boundary g + 1 (time-bounded like grid_sync: a timeout fails the grid).
+constexpr unsigned SEG_FAIL = 63;
+__device__ __forceinline__ void seg_publish(unsigned* lvl, unsigned val) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(lvl, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// 1: the boundary is there; 0: a combine failed; -1: the grid failed or the wait timed out (the grid fail word set)
+__device__ __forceinline__ int seg_wait(unsigned* bar, unsigned* lvl, unsigned target, unsigned failv, double* flag_lds,
+                                        long long limit) {
+  if (threadIdx.x == 0) {
+    int r = 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned v;
+    while ((v = __hip_atomic_load(lvl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
+      if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+          (long long)(__builtin_amdgcn_s_memrealtime() - t0) > limit) {
+        __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r = -1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (r == 1 && v == failv) r = 0;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    flag_lds[0] = (double)r;
+  }
+  __syncthreads();
+  return (int)flag_lds[0];
+}
+
 constexpr double SEG_CANCEL = 1e5;  // largest max D_ii / max P_a,ii a combine may leave (about 1e-11 relative error)
-__device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, double* sq, int S, int N) {
+__device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, double* sq, int S, int N, unsigned* lvl,
+                                            unsigned gen) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, nxx = nx * nx;
   const int LU = 2 * nx + 1, np = (LU + 3) & ~3, nt = (nx + 15) >> 4, nu4 = (LU + 15) >> 4;
@@ -370,9 +417,8 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
   double rel[6], rp0[3];
   auto prefetch = [&](int s) {
     const double* el = sq + s * esz;
-    const int cs = seg_begin(N, S, s);
-    const double* P0 = V.P(cs);
-    const double* p0 = V.pv() + (long long)cs * nx;
+    const double* P0 = el + nx * LU;  // the segment's first-pass P^0, p^0 at its start node (seg_element)
+    const double* p0 = P0 + nxx;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int e = tid + NT * i;
@@ -401,6 +447,7 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
       if (i >= LU || j >= LU) Ml[i * CH_GS + j] = 0.0;
     }
   }
+  if (lvl) seg_publish(lvl, gen * 64u + 1u);
   bool ok = true;
   for (int s = S - 2; s >= 1; --s) {
 #pragma unroll
@@ -470,6 +517,10 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
     }
     ok = ok && !__syncthreads_or(fl);
     OCP_SPANG_END(15, t_g, 0);
+    if (!ok) {
+      if (lvl) seg_publish(lvl, gen * 64u + SEG_FAIL);
+      break;
+    }
     OCP_SPAN_BEGIN(t_p);
     double* bo = bnd + s * bsz;
     for (int e = tid; e < nxx + nx; e += NT) {
@@ -479,6 +530,7 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
       else pb[e - nxx] = v;
       bo[e] = v;
     }
+    if (lvl) seg_publish(lvl, gen * 64u + (unsigned)(S - s));
     __syncthreads();
     OCP_SPANG_END(16, t_p, 0);
   }

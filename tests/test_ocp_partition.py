@@ -19,12 +19,12 @@ pytestmark = pytest.mark.gpu
 
 
 def _seg_begin(N, S, s):
-    """Segment boundary c_s of csrc/ocp_part.hpp:seg_begin (the last segment weighs 5/2)."""
+    """Segment boundary c_s of csrc/ocp_part.hpp:seg_begin (segment 0 weighs 1/2, the last one 5/2)."""
     if s <= 0:
         return 0
     if s >= S:
         return N
-    return min(max(2 * N * s // (2 * S + 3), s), N - (S - s))
+    return min(max(N * (10 * s - 5) // (10 * S + 10), s), N - (S - s))
 
 
 def _solve(h, ps):
