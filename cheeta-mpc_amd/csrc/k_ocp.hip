@@ -1878,8 +1878,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       const int n = N - 1, s0 = aff_begin(n, naff, g < naff ? g : naff), s1 = aff_begin(n, naff, g < naff ? g + 1 : naff);
       if (g < naff - 1) affine_comp<BWD>(V, CS, s0, s1, segq + g * seg_esz(nx));
       if (!sync()) return false;
-      if (lead) affine_bound<BWD>(V, CS, segq, naff, S.vec);
-      if (!sync()) return false;
+      if (g >= 1 && g < naff) affine_bound<BWD>(V, CS, segq, naff, g, S.vec);
       if (g < naff) chain_affine<BWD>(V, CS, S.vec, S.vec + 64, s0, s1, g < naff - 1);
     } else if (lead) {
       if constexpr (BWD) bwd_vec_b(V, S);

@@ -543,10 +543,10 @@ __device__ __forceinline__ bool seg_combine(const View& V, const ChainLds& CS, d
 // M_s = Acl_{N-1-s}', c_s = h_{N-1-s}); segment g owns the steps [a_g, a_{g+1}), a_g = floor(n g / S), n = N - 1.
 //   A: every segment composes its steps' affine maps, [Psi_g psi_g] = M_{a_{g+1}-1} .. M_{a_g} [I 0] + ..., into the
 //      segment buffer (affine_comp, on the matrix cores);
-//   B: one workgroup carries the boundary values y_{a_g} = Psi_{g-1} y_{a_{g-1}} + psi_{g-1} (g = 1 .. S-1, from the
-//      recursion's initial value) into the output rows (affine_bound);
+//   B: every segment g >= 1 carries the boundary values y_{a_h} = Psi_{h-1} y_{a_{h-1}} + psi_{h-1} (h = 1 .. g, from
+//      the recursion's initial value) up to its own, into its first output row (affine_bound);
 //   C: every segment runs its steps from its boundary value (chain_affine over the range; the last output row, the
-//      next segment's boundary value, stays as B wrote it).
+//      next segment's boundary value, stays as that segment's B wrote it). One grid barrier between A and B.
 // The serial depth is ~2 n / S steps plus S - 1 matrix-vector products instead of n steps.
 __device__ __forceinline__ int aff_begin(int n, int S, int g) { return (int)((long long)n * g / S); }
 
@@ -622,26 +622,26 @@ __device__ __forceinline__ void affine_comp(const View& V, const ChainLds& CS, i
   __syncthreads();
 }
 
-// B on one workgroup: y at the start of segments 1 .. S-1 from the recursion's initial value through the compositions
-// (staged in LDS region B: (S - 1) nx (nx + 1) doubles; wave 0, y in LDS), into the output rows
+// B on every segment's workgroup g >= 1: y at the start of segments 1 .. g from the recursion's initial value through
+// the compositions (staged in LDS region B: g nx (nx + 1) doubles; wave 0, y in LDS), its own one into its output
+// row (the one its steps start from; the segment before leaves that row alone), so C follows without a grid barrier
 template <bool BWD>
-__device__ __forceinline__ void affine_bound(const View& V, const ChainLds& CS, const double* sq, int S, double* y) {
+__device__ __forceinline__ void affine_bound(const View& V, const ChainLds& CS, const double* sq, int S, int g,
+                                             double* y) {
   const OcpLayout& L = V.L;
   const int tid = threadIdx.x, nx = L.nx, N = L.N, n = N - 1, esz = seg_esz(nx), LX = nx + 1;
   double* out = BWD ? V.pv() : V.dx();
-  double* Ps = CS.Ml;  // [S - 1][nx (nx + 1)]
-  const int tot = (S - 1) * nx * LX;
+  double* Ps = CS.Ml;  // [g][nx (nx + 1)]
+  const int tot = g * nx * LX;
   for (int e = tid; e < tot; e += NT) {
-    const int g = e / (nx * LX), o = e - g * (nx * LX);
-    Ps[e] = sq[(long long)g * esz + o];
+    const int h = e / (nx * LX), o = e - h * (nx * LX);
+    Ps[e] = sq[(long long)h * esz + o];
   }
   if (tid < nx) y[tid] = BWD ? V.gx()[(long long)N * nx + tid] : V.bcl()[tid];
   __syncthreads();
   if (tid < 64) {
-    for (int g = 1; g < S; ++g) {
-      const double* P = Ps + (g - 1) * nx * LX;
-      const int a = aff_begin(n, S, g);
-      const long long rw = BWD ? N - a : 1 + a;
+    for (int h = 1; h <= g; ++h) {
+      const double* P = Ps + (h - 1) * nx * LX;
       if (tid < nx) {
         double acc = P[nx * nx + tid];
         for (int c0 = 0; c0 < nx; c0 += 8) {
@@ -658,7 +658,10 @@ __device__ __forceinline__ void affine_bound(const View& V, const ChainLds& CS, 
         }
         __builtin_amdgcn_wave_barrier();
         y[tid] = acc;
-        out[rw * nx + tid] = acc;
+        if (h == g) {
+          const int a = aff_begin(n, S, g);
+          out[(long long)(BWD ? N - a : 1 + a) * nx + tid] = acc;
+        }
       }
       __builtin_amdgcn_wave_barrier();
     }
