@@ -453,9 +453,9 @@ __device__ __forceinline__ void chain_round4(double (&m)[NB][4][4], const int (&
 // Returns the pivots' flags: CH_NAN (a NaN pivot), CH_WEAK (a pivot the guard dropped, d <= 1e-200).
 constexpr int CH_NAN = 1, CH_WEAK = 2;
 template <int NB, bool WEAK>
-__device__ __forceinline__ int chain_elim(const View& V, const ChainLds& S, int mk, double* F, double* PaW) {
+__device__ __forceinline__ int chain_elim(const View& V, const ChainLds& S, int mk, double* F, double* PaW, int nxo = -1) {
   const OcpLayout& L = V.L;
-  const int lane = threadIdx.x, nx = L.nx;
+  const int lane = threadIdx.x, nx = nxo >= 0 ? nxo : L.nx;  // nxo: the trailing block's size when not nx
   const int nz = mk + nx, n1 = nz + 1, nb4 = (n1 + 3) >> 2, nt4 = nb4 * (nb4 + 1) / 2;
   bool bad = false, weak = false;
   int bi[NB], bj[NB];

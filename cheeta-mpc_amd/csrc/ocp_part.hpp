@@ -131,7 +131,8 @@ __device__ __forceinline__ v4d mtile(const double* A, int ai, int at, const doub
 // loads, then its Yd (one thread per (stage, row)), Acl and bcl are formed for all its stages at once (in place of A,
 // B, rb), and the accumulation takes one phase per stage (Phi Acl, Phi Ys, Phi bcl and the previous stage's W update
 // side by side, 2 x 2 register blocks). Phi, W, f and the Gs double buffer in region A (from ChainLds::G0). Finally
-// W = Gw Gw' by chain_elim on wave 0 (nx pivots of [W 0; 0 0]; a dropped pivot leaves a zero column). Writes U = [Gw
+// W = Gw Gw' by chain_elim on wave 0 (nx pivots of [W 0; 0 0] with a 4-wide zero trailing block, so one 4 x 4 block
+// per lane; a dropped pivot leaves a zero column). Writes U = [Gw
 // Phi f] to el. Returns chain_elim's NaN flag.
 constexpr int SEG_CHUNK = 9;  // stages per chunk: Yd takes one thread per (stage, row), 9 * 27 <= NT
 __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, int a, int b, double* el) {
@@ -327,7 +328,7 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
   __syncthreads();
   OCP_SPAN_BEGIN(t_c);
   int fl = 0;
-  if (tid < 64) fl = chain_elim<2, false>(V, CS, nx, CS.F0, CS.Pa2);
+  if (tid < 64) fl = chain_elim<1, false>(V, CS, nx, CS.F0, CS.Pa2, 3);  // trailing block of 3 + 1 zeros: NB = 1
   fl = __syncthreads_or(fl & CH_NAN) ? CH_NAN : 0;
   OCP_SPANG_END(13, t_c, 1);
   // U = [Gw Phi f]: Gw(x, j) = F(x, j) / sqrt(d_j) below the diagonal (0 for a dropped pivot); then this pass's
