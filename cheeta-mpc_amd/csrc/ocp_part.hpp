@@ -159,7 +159,22 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
   for (int ce = b; ce > a; ce -= cmax) {
     const int cb = ce - cmax > a ? ce - cmax : a, nc = ce - cb;
     OCP_SPAN_BEGIN(t_f);
-    // (1) the chunk's operands: flat over the stage slots, 16 loads per thread in flight per round
+    // (1) the chunk's operands: flat over the stage slots, 16 loads per thread in flight per round; each stage's six
+    // source pointers and nu_k first into an LDS table (ChainLds::C, free until the Cholesky at the end), so an
+    // element's address costs LDS reads instead of dependent global reads of the layout arrays
+    long long* ptab = (long long*)CS.C;  // [slot][8]: A, B, rb, F (Lf), F_x (K), F_r (kf), nu_k
+    if (tid < nc) {
+      const int k = cb + tid;
+      long long* pt = ptab + tid * 8;
+      pt[0] = (long long)V.A(k);
+      pt[1] = (long long)V.Bm(k);
+      pt[2] = (long long)(V.rb() + (long long)k * nx);
+      pt[3] = (long long)V.Lf(k);
+      pt[4] = (long long)V.K(k);
+      pt[5] = (long long)(V.kf() + L.cu[k]);
+      pt[6] = L.nu[k];
+    }
+    __syncthreads();
     {
       int s0 = tid / ssz, o0 = tid - s0 * ssz;
       const int tot = nc * ssz;
@@ -171,16 +186,13 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
         for (int i = 0; i < 16; ++i) {
           sl[i] = sx;
           ol[i] = ox;
-          const int k = cb + (sx < nc ? sx : nc - 1), mk = L.nu[k];
+          const long long* pt = ptab + (sx < nc ? sx : nc - 1) * 8;
+          const int mk = (int)pt[6];
           const int oB = nxx, oR = oB + nx * mk, oF = oR + nx, oX = oF + mk * mk, oL = oX + nx * mk, oe = oL + mk;
-          const double* src = ox < oB ? V.A(k) + ox
-                              : ox < oR ? V.Bm(k) + (ox - oB)
-                              : ox < oF ? V.rb() + (long long)k * nx + (ox - oR)
-                              : ox < oX ? V.Lf(k) + (ox - oF)
-                              : ox < oL ? V.K(k) + (ox - oX)
-                              : ox < oe ? V.kf() + L.cu[k] + (ox - oL)
-                                        : nullptr;
-          r[i] = (sx < nc && src) ? *src : 0.0;
+          const int seg = ox < oB ? 0 : ox < oR ? 1 : ox < oF ? 2 : ox < oX ? 3 : ox < oL ? 4 : 5;
+          const int o = ox - (seg == 0 ? 0 : seg == 1 ? oB : seg == 2 ? oR : seg == 3 ? oF : seg == 4 ? oX : oL);
+          const double* src = (const double*)pt[seg] + o;
+          r[i] = (sx < nc && ox < oe) ? *src : 0.0;
           ox += NT;
           while (ox >= ssz) {
             ox -= ssz;
