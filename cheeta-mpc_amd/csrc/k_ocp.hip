@@ -36,14 +36,14 @@ constexpr double TAU_OCP = 0.995;  // fraction-to-boundary, as oracle/ocp_ipm.c
 #ifdef CMPC_OCP_STAMPS
 // thread 0 of problem 0 accumulates in LDS (no global round trip on the timed path) and adds to the device array at
 // the kernel's end
-__device__ unsigned long long ocp_stamp_acc[32];
-__shared__ unsigned long long ocp_stamp_lds[33];
+__device__ unsigned long long ocp_stamp_acc[48];
+__shared__ unsigned long long ocp_stamp_lds[49];
 #define OCP_STAMP(id)                                                         \
   do {                                                                        \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
       const unsigned long long now_ = __builtin_amdgcn_s_memtime();           \
-      ocp_stamp_lds[id] += now_ - ocp_stamp_lds[32];                          \
-      ocp_stamp_lds[32] = now_;                                               \
+      ocp_stamp_lds[id] += now_ - ocp_stamp_lds[48];                          \
+      ocp_stamp_lds[48] = now_;                                               \
     }                                                                         \
   } while (0)
 // a span of one thread other than 0 (t, e.g. a helper wave's work): cycles between OCP_SPAN_BEGIN and OCP_SPAN_END
@@ -62,14 +62,14 @@ __shared__ unsigned long long ocp_stamp_lds[33];
 #define OCP_STAMP_BEGIN()                                                     \
   do {                                                                        \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                \
-      for (int i_ = 0; i_ < 32; ++i_) ocp_stamp_lds[i_] = 0;                  \
-      ocp_stamp_lds[32] = __builtin_amdgcn_s_memtime();                       \
+      for (int i_ = 0; i_ < 48; ++i_) ocp_stamp_lds[i_] = 0;                  \
+      ocp_stamp_lds[48] = __builtin_amdgcn_s_memtime();                       \
     }                                                                         \
   } while (0)
 #define OCP_STAMP_END()                                                       \
   do {                                                                        \
     if (blockIdx.x == 0 && threadIdx.x == 0)                                  \
-      for (int i_ = 0; i_ < 32; ++i_) ocp_stamp_acc[i_] += ocp_stamp_lds[i_]; \
+      for (int i_ = 0; i_ < 48; ++i_) ocp_stamp_acc[i_] += ocp_stamp_lds[i_]; \
   } while (0)
 #else
 #define OCP_STAMP(id) \
@@ -1877,7 +1877,9 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       }
       const int n = N - 1, s0 = aff_begin(n, naff, g < naff ? g : naff), s1 = aff_begin(n, naff, g < naff ? g + 1 : naff);
       if (g < naff - 1) affine_comp<BWD>(V, CS, s0, s1, segq + g * seg_esz(nx));
+      OCP_STAMP(34);
       if (!sync()) return false;
+      OCP_STAMP(35);
       if (g >= 1 && g < naff) affine_bound<BWD>(V, CS, segq, naff, g, S.vec);
       if (g < naff) chain_affine<BWD>(V, CS, S.vec, S.vec + 64, s0, s1, g < naff - 1);
     } else if (lead) {
@@ -2036,6 +2038,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
     __syncthreads();
     double lrs = 0.0, lre = 0.0, lri = 0.0, lrc = 0.0, lmu = 0.0;
     residuals_par(V, lrs, lre, R.k0, R.n1);
+    OCP_STAMP(32);
     {
       const double *c = V.row(R_C), *lg = V.row(R_LG), *ug = V.row(R_UG), *tl = V.row(R_TL), *tu = V.row(R_TU),
                    *ll = V.row(R_LL), *lu = V.row(R_LU);
@@ -2160,6 +2163,7 @@ __device__ __forceinline__ void ipm_grid(const OcpSolveArgs& a, int q, int g, co
       chain_gains(V, R.k0, R.k1);
       __syncthreads();
     }
+    OCP_STAMP(33);
     acl_pass(V, S, true, R.k0, R.k1, true);
     if (!sync()) break;
     OCP_STAMP(3);
@@ -2514,7 +2518,7 @@ int launch_ocp_chain_lab(const OcpSolveArgs& a, int B, hipStream_t stream) {
 
 #ifdef CMPC_OCP_STAMPS
 extern "C" int cmpc_ocp_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ocp_stamp_acc), sizeof(unsigned long long) * 32) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ocp_stamp_acc), sizeof(unsigned long long) * 48) != hipSuccess) return -2;
   if (reset) {
     unsigned long long z[32] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(ocp_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;

@@ -211,7 +211,7 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
     OCP_SPAN_BEGIN(t_1);
     // (2) Yd of every stage of the chunk: thread (stage, row r), in place of B (8 terms per LDS round trip)
     if (tid < nc * nx) {
-      const int sl = tid / nx, r = tid - sl * nx, mk = L.nu[cb + sl];
+      const int sl = tid / nx, r = tid - sl * nx, mk = (int)ptab[sl * 8 + 6];
       double* O = Op + sl * ssz;
       double* Yd = O + nxx;
       const double* F = Yd + nx * mk + nx;
@@ -238,7 +238,7 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
     OCP_SPAN_BEGIN(t_2);
     // (3) Acl = A - Yd F_x' in place of A, bcl = rb - Yd F_r' in place of rb (2 x 2 blocks of every stage)
     for (int w = tid; w < nc * (hb * hb + hb); w += NT) {
-      const int sl = w / (hb * hb + hb), v = w - sl * (hb * hb + hb), mk = L.nu[cb + sl];
+      const int sl = w / (hb * hb + hb), v = w - sl * (hb * hb + hb), mk = (int)ptab[sl * 8 + 6];
       double* O = Op + sl * ssz;
       const double* Yd = O + nxx;
       double* rb = O + nxx + nx * mk;
@@ -265,7 +265,7 @@ __device__ __forceinline__ int seg_element(const View& V, const ChainLds& CS, in
     // Phi Acl_k, Gs = Phi Yd_k D^1/2, f += Phi bcl_k) and the W update of the stage before (its Gs from the last phase),
     // 16 x 16 tiles on the matrix cores, tile w + 4 v on wave w
     for (int k = ce - 1; k >= cb; --k) {
-      const int mk = L.nu[k], LX = nx + mk + 1;
+      const int mk = (int)ptab[(k - cb) * 8 + 6], LX = nx + mk + 1;
       const double* X = Op + (k - cb) * ssz;  // [Acl | Yd | bcl], column-major, ld nx
       const double* F = X + nx * LX;
       const double* Ph = cur ? Ph1 : Ph0;

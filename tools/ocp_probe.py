@@ -67,7 +67,7 @@ def stamps(projected, B=1):
     """Per-phase cycles of problem 0 (lab build: CMPC_LIB=lab/_stamps/libcmpc_ocpstamps.so)."""
     L = cm.lib()
     L.cmpc_ocp_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 32)()
+    buf = (C.c_ulonglong * 48)()
     ps = [gen.legged_problem(1000 + i, projected=projected) for i in range(B)]
     p0 = ps[0]
     recs, crecs = zip(*[gen.pack(p) for p in ps])
@@ -84,7 +84,8 @@ def stamps(projected, B=1):
              13: "[wg1 el:accum+Gw]", 14: "[wg0 comb:products]", 15: "[wg0 comb:elim]", 16: "[wg0 comb:out]", 20: "chain:init", 21: "chain:T", 22: "chain:M",
              23: "chain:elim", 24: "chain:out", 25: "chain:outw0", 26: "[w1 load span]", 27: "chain:e-load", 28: "grid prologue", 17: "fact:exit", 3: "acl", 4: "forward",
              5: "post", 6: "corr rhs", 7: "backward", 8: "acl+forward (corr)", 9: "update", 18: "part:P1+wait",
-             19: "part:combine+wait", 29: "part:P3", 30: "[wg1 chain spans]", 31: "[wg1 element spans]"}
+             19: "part:combine+wait", 29: "part:P3", 30: "[wg1 chain spans]", 31: "[wg1 element spans]",
+             32: "residuals: compute", 33: "acl: gains", 34: "scan: compose", 35: "scan: barrier"}
     tot = sum(buf[i] for i in names if i not in (10, 11, 12, 13, 14, 15, 16, 26, 30, 31))  # spans (other timelines)
     print(f"stamps {'projected' if projected else 'rows'} B={B} iters {it[0]} total {tot} cycles")
     for i, n in names.items():
